@@ -1,0 +1,133 @@
+"""Headline benchmark: images/sec (whole node), ResNet-50 224x224 bf16, DDP over N MI355X.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it
+is launched by ``torch.distributed.run`` with one rank per GPU (RCCL over xGMI).
+W untimed warmup steps, then exactly K timed steps bracketed by a barrier and
+``torch.cuda.synchronize()``; the max time over ranks is reported; rank 0
+prints ONE JSON line.
+
+Workload per step = the reference training step (reference train.py:44-73):
+forward (ResNet-50 + reference MLP head, 7 classes, class-weighted CE), loss
+all-reduce / world, backward with bucketed gradient all-reduce overlapped, Adam
+step.  Synthetic data (fp32 NCHW normalised images generated on device,
+converted to bf16 NHWC inside the step), random-init weights, per-GPU batch
+fixed (weak scaling).  SyncBN follows the reference semantics (on when N>1).
+
+``--compute torch`` runs the *reference stack* (torch DDP + nn.SyncBatchNorm +
+bf16 autocast over ATen/MIOpen) on the identical workload for the baseline.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+from pytorch_imageclassification_distributed_amd.data import DeviceSyntheticLoader
+from pytorch_imageclassification_distributed_amd.engine import Trainer, build_parser
+from pytorch_imageclassification_distributed_amd.parallel import barrier, destroy, init_distributed
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+METRIC = "images/sec (whole node) ResNet-50 224x224 bf16 at 1/2/4/8 MI355X"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=30)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    p.add_argument("--model", default="resnet50")
+    p.add_argument("--image-size", type=int, default=224)
+    p.add_argument("--num-classes", type=int, default=7)
+    p.add_argument("--compute", default="hip", choices=["hip", "torch"])
+    p.add_argument("--sync-bn", default="auto", choices=["auto", "on", "off"])
+    p.add_argument("--bucket-mb", type=float, default=32.0)
+    p.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
+    p.add_argument("--graph", action="store_true", help="capture the step in a HIP graph")
+    p.add_argument("--profile-steps", type=int, default=0)
+    return p.parse_args()
+
+
+def load_baseline(n_gpus: int):
+    path = os.path.join(HERE, "benchmarks", "reference_stack.json")
+    try:
+        with open(path) as f:
+            ref = json.load(f)
+        v = ref.get("images_per_sec", {}).get(str(n_gpus))
+        return float(v) if v else None
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    a = parse()
+    if "LOCAL_RANK" in os.environ and "WORLD_SIZE" in os.environ:
+        n = int(os.environ["WORLD_SIZE"])
+    else:
+        n = 1
+    ctx = init_distributed(device="cuda")
+    sync_bn = (a.sync_bn == "on") or (a.sync_bn == "auto" and ctx.world_size > 1)
+    targs = build_parser().parse_args([
+        "--synthetic", "--model", a.model, "--image-size", str(a.image_size),
+        "--batchsize", str(a.batch), "--num-classes", str(a.num_classes),
+        "--num-workers", "0", "--synthetic-train-size", "8", "--synthetic-val-size", "8",
+        "--compute", a.compute, "--bucket-mb", str(a.bucket_mb), "--comm-dtype", a.comm_dtype,
+        "--lr", "1e-4",
+    ] + ([] if sync_bn else ["--no-sync-bn"]))
+    tr = Trainer(targs, ctx)
+    tr.net.train()
+    data = DeviceSyntheticLoader(a.batch, a.num_classes, a.image_size, ctx.device,
+                                 steps=a.warmup + a.steps, ring=2, seed=1234 + ctx.rank)
+    batches = list(iter(data))
+
+    def step(i):
+        b = batches[i]
+        loss = tr.train_step(b["image"], b["label"])
+        return tr.reduce_loss(loss)
+
+    for i in range(a.warmup):
+        last = step(i)
+    torch.cuda.synchronize()
+    if not torch.isfinite(last).item():
+        raise FloatingPointError(f"non-finite loss in warmup: {last.item()}")
+    barrier(ctx)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        last = step(a.warmup + i)
+    torch.cuda.synchronize()
+    barrier(ctx)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=ctx.device)
+    if ctx.world_size > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    loss_val = float(last.item())
+    if ctx.rank == 0:
+        imgs = a.batch * ctx.world_size * a.steps
+        value = imgs / dt
+        base = load_baseline(ctx.world_size)
+        print(json.dumps({
+            "metric": METRIC, "value": round(value, 2), "unit": "images/sec",
+            "n_gpus": ctx.world_size, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": round(value / base, 4) if base else None,
+            "dtype": "bf16", "data": "synthetic (on-device random images, random-init weights)",
+            "config": {"model": a.model, "global_batch": a.batch * ctx.world_size,
+                       "per_gpu_batch": a.batch, "seq_len": None, "image_size": a.image_size,
+                       "num_classes": a.num_classes, "parallelism": f"dp{ctx.world_size}",
+                       "sync_bn": sync_bn, "compute": a.compute, "optimizer": "adam",
+                       "final_loss": round(loss_val, 5)},
+        }), flush=True)
+    destroy()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

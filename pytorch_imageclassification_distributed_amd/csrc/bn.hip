@@ -1,0 +1,347 @@
+// BatchNorm (training + eval) for NHWC bf16 activations, fp32 statistics.
+//
+// Forward (K5, K8, K9):
+//   conv epilogue -> per-channel (sum, sumsq) fp32 partials in G rotating rows
+//   bn_partials   -> fp64 per-channel sums, partial rows re-zeroed for the next layer
+//   [SyncBN: RCCL all-reduce of the fp64 sums + count]
+//   bn_finalize   -> scale = gamma*invstd, shift = beta - mean*scale (+ mean, invstd),
+//                    running-stat update (momentum, unbiased var), num_batches_tracked++
+//   bn_apply      -> out = act(y*scale + shift [+ residual]), 8 channels per lane,
+//                    optional write into a channel slice of a wider (concat) tensor
+// Backward (K6):
+//   bn_bwd_reduce -> dz = act'(z) * g (z recomputed from y, coefficients, residual),
+//                    partial (sum dz, sum dz*xhat) per channel; dz materialised only
+//                    when it is also the residual branch's gradient
+//   bn_partials   -> fp64 sums (+ local dgamma / dbeta written to the param grads)
+//   [SyncBN: all-reduce of the two sums]
+//   bn_bwd_elemt  -> dy = scale * (dz - sum_dz/n - xhat * sum_dzxhat/n)
+// Eval (K7): bn_eval_coef -> scale/shift from running stats, then bn_apply.
+#include "common.h"
+
+namespace {
+
+// ---- partial rows [G][2][C] -> fp64 sums [2][C]; zero the rows -------------
+__global__ void bn_partials_kernel(float* __restrict__ part, int G, int C, double* __restrict__ sums,
+                                   float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int g = 0; g < G; ++g) {
+    float* r = part + (size_t)g * 2 * C;
+    s += (double)r[c];
+    q += (double)r[C + c];
+    r[c] = 0.f;
+    r[C + c] = 0.f;
+  }
+  sums[c] = s;
+  sums[C + c] = q;
+  if (dbeta) dbeta[c] = (float)s;       // backward: sum dz
+  if (dgamma) dgamma[c] = (float)q;     // backward: sum dz * xhat
+}
+
+// ---- fp64 sums -> coefficients, running stats -----------------------------
+// coef layout [4][C]: scale, shift, mean, invstd
+__global__ void bn_finalize_kernel(const double* __restrict__ sums, const double* __restrict__ count_p,
+                                   double count_host, const float* __restrict__ gamma,
+                                   const float* __restrict__ beta, float* __restrict__ rmean,
+                                   float* __restrict__ rvar, long long* __restrict__ nbt, float momentum,
+                                   float eps, int C, float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const double n = count_p ? *count_p : count_host;
+  if (c == 0 && nbt) *nbt += 1;
+  if (c >= C) return;
+  const double mean = sums[c] / n;
+  double var = sums[C + c] / n - mean * mean;
+  var = var < 0.0 ? 0.0 : var;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+  const float scale = g * invstd;
+  coef[c] = scale;
+  coef[C + c] = b - (float)mean * scale;
+  coef[2 * C + c] = (float)mean;
+  coef[3 * C + c] = invstd;
+  if (rmean) {
+    const double unb = n > 1.0 ? var * n / (n - 1.0) : var;
+    rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mean;
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
+  }
+}
+
+__global__ void bn_eval_coef_kernel(const float* __restrict__ gamma, const float* __restrict__ beta,
+                                    const float* __restrict__ rmean, const float* __restrict__ rvar,
+                                    float eps, int C, float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float invstd = rsqrtf(rvar[c] + eps);
+  const float scale = (gamma ? gamma[c] : 1.f) * invstd;
+  coef[c] = scale;
+  coef[C + c] = (beta ? beta[c] : 0.f) - rmean[c] * scale;
+  coef[2 * C + c] = rmean[c];
+  coef[3 * C + c] = invstd;
+}
+
+// ---- apply: out = act(y*scale + shift [+ res]) -----------------------------
+__global__ void bn_apply_kernel(const bf16_t* __restrict__ y, const float* __restrict__ coef,
+                                const bf16_t* __restrict__ res, bf16_t* __restrict__ out, long rows,
+                                int C, int ldo, int c_off, int act) {
+  const int cch = C >> 3;
+  const long total = rows * cch;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long row = i / cch;
+    const int c0 = (int)(i - row * cch) * 8;
+    float v[8], sc[8], sh[8];
+    unpack8(*(const uint4*)(y + row * C + c0), v);
+    *(float4*)sc = *(const float4*)(coef + c0);
+    *(float4*)(sc + 4) = *(const float4*)(coef + c0 + 4);
+    *(float4*)sh = *(const float4*)(coef + C + c0);
+    *(float4*)(sh + 4) = *(const float4*)(coef + C + c0 + 4);
+    float r[8];
+    if (res) unpack8(*(const uint4*)(res + row * C + c0), r);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float z = v[k] * sc[k] + sh[k];
+      if (res) z += r[k];
+      v[k] = apply_act(z, act);
+    }
+    *(uint4*)(out + row * ldo + c_off + c0) = pack8(v);
+  }
+}
+
+// ---- backward reduce -------------------------------------------------------
+// grid: (row blocks, channel-chunk slices); block 256 = CHB chunk lanes x RP row lanes
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
+    const bf16_t* __restrict__ g, const bf16_t* __restrict__ y, const float* __restrict__ coef,
+    const bf16_t* __restrict__ res, bf16_t* __restrict__ dz_out, long rows, int C, int act,
+    long rows_per_block, float* __restrict__ part, int G) {
+  __shared__ float red[2][256][9];
+  const int cch = C >> 3;
+  const int CHB = cch < 256 ? cch : 256;
+  const int RP = 256 / CHB;
+  const int tid = threadIdx.x;
+  const int lc = tid % CHB, lr = tid / CHB;
+  const int chunk = blockIdx.y * CHB + lc;
+  const bool active = lr < RP && chunk < cch;
+  float s[8], q[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { s[k] = 0.f; q[k] = 0.f; }
+  if (active) {
+    const int c0 = chunk * 8;
+    float sc[8], sh[8], mu[8], is[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      sc[k] = coef[c0 + k]; sh[k] = coef[C + c0 + k];
+      mu[k] = coef[2 * C + c0 + k]; is[k] = coef[3 * C + c0 + k];
+    }
+    const long rbeg = blockIdx.x * rows_per_block;
+    const long rend = rbeg + rows_per_block < rows ? rbeg + rows_per_block : rows;
+    for (long row = rbeg + lr; row < rend; row += RP) {
+      float gv[8], yv[8], rv[8];
+      unpack8(*(const uint4*)(g + row * C + c0), gv);
+      unpack8(*(const uint4*)(y + row * C + c0), yv);
+      if (res) unpack8(*(const uint4*)(res + row * C + c0), rv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float dz = gv[k];
+        if (act != ACT_NONE) {
+          float z = yv[k] * sc[k] + sh[k];
+          if (res) z += rv[k];
+          dz = act_grad(z, gv[k], act);
+        }
+        gv[k] = dz;
+        s[k] += dz;
+        q[k] += dz * (yv[k] - mu[k]) * is[k];
+      }
+      if (dz_out) *(uint4*)(dz_out + row * C + c0) = pack8(gv);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { red[0][tid][k] = s[k]; red[1][tid][k] = q[k]; }
+  __syncthreads();
+  if (lr == 0 && chunk < cch) {
+    for (int r = 1; r < RP; ++r) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s[k] += red[0][tid + r * CHB][k];
+        q[k] += red[1][tid + r * CHB][k];
+      }
+    }
+    float* dst = part + (size_t)(blockIdx.x % G) * 2 * C + chunk * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      atomicAdd(dst + k, s[k]);
+      atomicAdd(dst + C + k, q[k]);
+    }
+  }
+}
+
+
+// ---- standalone statistics pass (outputs not produced by the GEMM epilogue) --
+__global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict__ y, long rows, int C,
+                                                       long rows_per_block, float* __restrict__ part, int G) {
+  __shared__ float red[2][256][9];
+  const int cch = C >> 3;
+  const int CHB = cch < 256 ? cch : 256;
+  const int RP = 256 / CHB;
+  const int tid = threadIdx.x;
+  const int lc = tid % CHB, lr = tid / CHB;
+  const int chunk = blockIdx.y * CHB + lc;
+  float s[8], q[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { s[k] = 0.f; q[k] = 0.f; }
+  if (lr < RP && chunk < cch) {
+    const long rbeg = blockIdx.x * rows_per_block;
+    const long rend = rbeg + rows_per_block < rows ? rbeg + rows_per_block : rows;
+    for (long row = rbeg + lr; row < rend; row += RP) {
+      float v[8];
+      unpack8(*(const uint4*)(y + row * C + chunk * 8), v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { s[k] += v[k]; q[k] += v[k] * v[k]; }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { red[0][tid][k] = s[k]; red[1][tid][k] = q[k]; }
+  __syncthreads();
+  if (lr == 0 && chunk < cch) {
+    for (int r = 1; r < RP; ++r)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { s[k] += red[0][tid + r * CHB][k]; q[k] += red[1][tid + r * CHB][k]; }
+    float* dst = part + (size_t)(blockIdx.x % G) * 2 * C + chunk * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { atomicAdd(dst + k, s[k]); atomicAdd(dst + C + k, q[k]); }
+  }
+}
+
+// sums (fp64, possibly all-reduced) -> k[2][C] = (sum_dz/n, sum_dzxhat/n)
+__global__ void bn_bwd_k_kernel(const double* __restrict__ sums, const double* __restrict__ count_p, double n_host,
+                                int C, float* __restrict__ kout) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double n = count_p ? *count_p : n_host;
+  kout[c] = (float)(sums[c] / n);
+  kout[C + c] = (float)(sums[C + c] / n);
+}
+
+__global__ void bn_bwd_elemt_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ y,
+                                    const float* __restrict__ coef, const float* __restrict__ kk,
+                                    const bf16_t* __restrict__ res, const bf16_t* __restrict__ dz_in,
+                                    bf16_t* __restrict__ dy, long rows, int C, int act) {
+  const int cch = C >> 3;
+  const long total = rows * cch;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long row = i / cch;
+    const int c0 = (int)(i - row * cch) * 8;
+    float gv[8], yv[8];
+    unpack8(*(const uint4*)(y + row * C + c0), yv);
+    if (dz_in) {
+      unpack8(*(const uint4*)(dz_in + row * C + c0), gv);
+    } else {
+      unpack8(*(const uint4*)(g + row * C + c0), gv);
+      if (act != ACT_NONE) {
+        float rv[8];
+        if (res) unpack8(*(const uint4*)(res + row * C + c0), rv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float z = yv[k] * coef[c0 + k] + coef[C + c0 + k];
+          if (res) z += rv[k];
+          gv[k] = act_grad(z, gv[k], act);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = c0 + k;
+      const float xhat = (yv[k] - coef[2 * C + c]) * coef[3 * C + c];
+      gv[k] = coef[c] * (gv[k] - kk[c] - xhat * kk[C + c]);
+    }
+    *(uint4*)(dy + row * C + c0) = pack8(gv);
+  }
+}
+
+int grid_for(long work, int per_block = 256, int cap = 4096) {
+  long b = (work + per_block - 1) / per_block;
+  return (int)(b < 1 ? 1 : (b > cap ? cap : b));
+}
+
+}  // namespace
+
+int bn_partials_launch(float* part, int G, int C, double* sums, float* dgamma, float* dbeta,
+                       hipStream_t s) {
+  hipLaunchKernelGGL(bn_partials_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, part, G, C, sums, dgamma, dbeta);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int bn_finalize_launch(const double* sums, const double* count_p, double count, const float* gamma,
+                       const float* beta, float* rmean, float* rvar, long long* nbt, float momentum,
+                       float eps, int C, float* coef, hipStream_t s) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, sums, count_p, count, gamma,
+                     beta, rmean, rvar, nbt, momentum, eps, C, coef);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int bn_eval_coef_launch(const float* gamma, const float* beta, const float* rmean, const float* rvar,
+                        float eps, int C, float* coef, hipStream_t s) {
+  hipLaunchKernelGGL(bn_eval_coef_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, gamma, beta, rmean, rvar, eps,
+                     C, coef);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int bn_apply_launch(const bf16_t* y, const float* coef, const bf16_t* res, bf16_t* out, long rows, int C,
+                    int ldo, int c_off, int act, hipStream_t s) {
+  const long work = rows * (C / 8);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(work, 256, 8192)), dim3(256), 0, s, y, coef, res, out,
+                     rows, C, ldo, c_off, act);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int bn_bwd_reduce_launch(const bf16_t* g, const bf16_t* y, const float* coef, const bf16_t* res,
+                         bf16_t* dz_out, long rows, int C, int act, float* part, int G, hipStream_t s) {
+  const int cch = C / 8;
+  const int CHB = cch < 256 ? cch : 256;
+  const int slices = cdiv(cch, CHB);
+  const int RP = 256 / CHB;
+  // aim for ~1024 blocks in total, at least 4 row passes per block
+  long rblocks = 1024 / slices;
+  if (rblocks < 1) rblocks = 1;
+  long rpb = (rows + rblocks - 1) / rblocks;
+  if (rpb < 4L * RP) rpb = 4L * RP;
+  rblocks = (rows + rpb - 1) / rpb;
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3((unsigned)rblocks, slices), dim3(256), 0, s, g, y, coef, res,
+                     dz_out, rows, C, act, rpb, part, G);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int bn_bwd_k_launch(const double* sums, const double* count_p, double n, int C, float* k, hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_k_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, sums, count_p, n, C, k);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int bn_bwd_elemt_launch(const bf16_t* g, const bf16_t* y, const float* coef, const float* k,
+                        const bf16_t* res, const bf16_t* dz_in, bf16_t* dy, long rows, int C, int act,
+                        hipStream_t s) {
+  const long work = rows * (C / 8);
+  hipLaunchKernelGGL(bn_bwd_elemt_kernel, dim3(grid_for(work, 256, 8192)), dim3(256), 0, s, g, y, coef, k,
+                     res, dz_in, dy, rows, C, act);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int bn_stats_launch(const bf16_t* y, long rows, int C, float* part, int G, hipStream_t s) {
+  const int cch = C / 8;
+  const int CHB = cch < 256 ? cch : 256;
+  const int slices = cdiv(cch, CHB);
+  const int RP = 256 / CHB;
+  long rblocks = 1024 / slices;
+  if (rblocks < 1) rblocks = 1;
+  long rpb = (rows + rblocks - 1) / rblocks;
+  if (rpb < 4L * RP) rpb = 4L * RP;
+  rblocks = (rows + rpb - 1) / rpb;
+  hipLaunchKernelGGL(bn_stats_kernel, dim3((unsigned)rblocks, slices), dim3(256), 0, s, y, rows, C, rpb, part, G);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}

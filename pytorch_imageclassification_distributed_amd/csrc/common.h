@@ -1,0 +1,87 @@
+// Shared device helpers for the gfx950 (MI355X, CDNA4) kernels.
+//
+// Conventions used by every kernel in csrc/:
+//   * activations are NHWC ("channels-last") bf16, stored as raw uint16;
+//   * statistics, master weights, optimizer state and gradients are fp32;
+//   * 64-lane wavefronts, 256-thread workgroups unless a kernel says otherwise;
+//   * global loads/stores of bf16 data are 16 B per lane (8 elements).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define DEVI __device__ __forceinline__
+
+DEVI float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+// round-to-nearest-even; lowers to v_cvt_pk_bf16_f32 on gfx950 (NaN-preserving)
+DEVI bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+
+DEVI uint32_t pack2(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+// unpack 8 bf16 held in a uint4 into floats
+DEVI void unpack8(const uint4& v, float* f) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+
+DEVI uint4 pack8(const float* f) {
+  uint4 v;
+  v.x = pack2(f[0], f[1]); v.y = pack2(f[2], f[3]);
+  v.z = pack2(f[4], f[5]); v.w = pack2(f[6], f[7]);
+  return v;
+}
+
+// component-wise select: a ternary on the uint4 *struct* makes LLVM route both
+// operands through private memory (scratch); per-component selects stay in VGPRs
+DEVI uint4 sel4(bool ok, const uint4& v) {
+  uint4 r;
+  r.x = ok ? v.x : 0u; r.y = ok ? v.y : 0u; r.z = ok ? v.z : 0u; r.w = ok ? v.w : 0u;
+  return r;
+}
+
+DEVI float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+DEVI float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+DEVI float silu_f(float x) { return x / (1.f + __expf(-x)); }
+DEVI float sigmoid_f(float x) { return 1.f / (1.f + __expf(-x)); }
+
+// activation codes shared by host and device
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_SILU = 2 };
+
+DEVI float apply_act(float x, int act) {
+  if (act == ACT_RELU) return fmaxf(x, 0.f);
+  if (act == ACT_SILU) return silu_f(x);
+  return x;
+}
+
+// d act(z)/dz * g, given the pre-activation z
+DEVI float act_grad(float z, float g, int act) {
+  if (act == ACT_RELU) return z > 0.f ? g : 0.f;
+  if (act == ACT_SILU) {
+    float s = sigmoid_f(z);
+    return g * s * (1.f + z * (1.f - s));
+  }
+  return g;
+}
+
+#define HIP_CHECK_LAUNCH() do { hipError_t e__ = hipGetLastError(); if (e__ != hipSuccess) return (int)e__; } while (0)
+
+static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

@@ -1,0 +1,50 @@
+// Implicit-GEMM convolution on MFMA (gfx950) - shared parameter block.
+//
+// One kernel serves conv forward (K1) and conv data-gradient (K2):
+//   C[m][n] = sum_k A[m][k] * B[n][k]
+// where row m enumerates a pixel grid (n_img, gh, gw) of size N x GH x GW and
+// k = tap * CA + ci walks a list of kernel taps, each contributing CA channels.
+//   A[m][k] = Src[n_img, gh*sA + tap_dh[tap], gw*sA + tap_dw[tap], ci]   (0 outside)
+//   B[n][k] = Wmat[n * ldb + tap_b[tap] * CA + ci]
+//   output pixel = (n_img, gh*so + oh0, gw*so + ow0) in an OH x OW map, row
+//   stride ldc channels, channel offset c_off (concat-free writes).
+// Forward: taps = every (r, c) of the filter, dh = r*dil - pad_t, sA = stride,
+//   so = 1; Wmat = weight [Cout][KH][KW][Cin] (KRSC, = channels_last fp32
+//   master cast to bf16).
+// Dgrad, stride s: the input pixels split into s*s phases (ph, pw); phase
+//   (ph, pw) only receives taps with (ph + pad - r) % s == 0, at
+//   dh = (ph + pad - r) / s; Wmat = transposed weight [Cin][KH][KW][Cout].
+//   One launch per phase; a phase with no taps writes zeros (K = 0).
+#pragma once
+#include "common.h"
+
+#define CONV_MAX_TAPS 49
+
+struct ConvParams {
+  const bf16_t* A;
+  const bf16_t* B;
+  bf16_t* C;
+  float* stats;        // optional BN partials [G][2][Ncols] fp32 (sum, sum of squares)
+  const float* bias;   // optional [Ncols]
+  int M, Ncols, K, CA;
+  int GH, GW, IH, IW, sA;
+  int ldb;
+  int OH, OW, so, oh0, ow0, ldc, c_off;
+  int ntaps, stats_groups;
+  int tap_dh[CONV_MAX_TAPS];
+  int tap_dw[CONV_MAX_TAPS];
+  int tap_b[CONV_MAX_TAPS];
+};
+
+// Weight-gradient (K3): dW[co][tap][ci] = sum_m dY[m][co] * X[pix(m) + tap][ci]
+struct WgradParams {
+  const bf16_t* dY;    // [M][Cout] NHWC
+  const bf16_t* X;     // [N][IH][IW][Cin] NHWC
+  float* dW;           // [Cout][KH*KW][Cin] fp32, accumulated with atomics (pre-zeroed)
+  int M, Cout, Cin, Ntot;  // Ntot = KH*KW*Cin
+  int OH, OW, IH, IW, stride_h, stride_w, pad_t, pad_l, dil_h, dil_w, KW;
+  int k_per_split;     // pixels (GEMM K) per split, multiple of 32
+};
+
+int conv_gemm_launch(const ConvParams& p, hipStream_t stream);
+int conv_wgrad_launch(const WgradParams& p, int splits, hipStream_t stream);

@@ -1,0 +1,402 @@
+// MFMA implicit-GEMM convolution kernels for gfx950 (MI355X).
+//
+// conv_gemm_kernel<BN>  : forward (K1) and data-gradient (K2), see conv_gemm.h.
+// conv_wgrad_kernel<BM> : weight-gradient (K3), split over the pixel (GEMM-K) axis.
+//
+// Design (CDNA4-first, not a translation of a CUDA tiling):
+//  * 256-thread workgroups = 4 wave64s in a 2x2 arrangement; each wave owns a
+//    (BM/2)x(BN/2) output tile computed with v_mfma_f32_16x16x32_bf16
+//    (fp32 accumulators, 4 per fragment);
+//  * BK = 64 (guide: BK 32 loses on every variant); A and B tiles are staged
+//    through registers into double-buffered LDS - register staging (not
+//    global_load_lds) because the A operand is an *implicit im2col gather*
+//    with zero padding that is resolved per 16-byte chunk, and because the
+//    wgrad tiles need a transposing image;
+//  * forward/dgrad LDS images are [row][64 k] with 128-B rows and an XOR
+//    swizzle chunk ^ ((row >> 1) & 7): the ds_read_b128 fragment reads of a
+//    16-lane group then hit 16 distinct 16-B bank slots (conflict-free);
+//  * wgrad images are [k=pixel][m or n] read with ds_read_b64_tr_b16 (the
+//    gfx950 hardware transpose read) so both operands, which are contiguous
+//    along M/N and strided along K, feed MFMA without a register transpose;
+//    the k order inside a 32-slice is permuted identically for both operands
+//    (sum-invariant) so each 32-lane half reads 8 distinct rows of a 288-B
+//    stride image -> conflict-free;
+//  * one __syncthreads per k-step: load(k+1) is issued before the MFMAs of
+//    step k and written to the other LDS buffer after them;
+//  * blockIdx -> tile is remapped so blocks sharing an A row panel are
+//    consecutive *within one XCD* (bijective form of the guide's T1 remap);
+//  * the epilogue stages the bf16 tile through LDS for 16-B coalesced stores
+//    into NHWC (optionally a channel slice of a wider concat buffer) and,
+//    optionally, emits per-channel BatchNorm partial sums (sum, sum of squares
+//    of the bf16-rounded outputs) with one fp32 atomic per channel per block
+//    into G rotating partial rows (low contention) - so the BN statistics pass
+//    never re-reads the conv output.
+#include "conv_gemm.h"
+
+namespace {
+
+constexpr int BM = 128;
+constexpr int BK = 64;
+constexpr int NT = 256;
+
+DEVI int swz(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+
+DEVI int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, local = bid >> 3;
+  const int q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
+}
+
+template <int BN>
+__global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(const ConvParams p) {
+  constexpr int A_BYTES = BM * BK * 2;
+  constexpr int B_BYTES = BN * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int WTM = BM / 2, WTN = BN / 2;
+  constexpr int RM = WTM / 16, RN = WTN / 16;
+  constexpr int AR = BM / 32, BR = BN / 32;
+  constexpr int TAP_BYTES = 3 * CONV_MAX_TAPS * 4;
+  constexpr int CST = BN + 8;  // C tile row stride (elements)
+  static_assert(BM * CST * 2 + 4 * BN * 4 <= 2 * STAGE, "epilogue LDS reuse");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + TAP_BYTES];
+  int* s_dh = (int*)(smem + 2 * STAGE);
+  int* s_dw = s_dh + CONV_MAX_TAPS;
+  int* s_tb = s_dw + CONV_MAX_TAPS;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int gm = (p.M + BM - 1) / BM, gn = (p.Ncols + BN - 1) / BN;
+  const int lin = xcd_remap(blockIdx.x, gm * gn);
+  const int bm = lin / gn, bn = lin - bm * gn;
+  const int m0 = bm * BM, n0 = bn * BN;
+
+  if (tid < p.ntaps) {
+    s_dh[tid] = p.tap_dh[tid];
+    s_dw[tid] = p.tap_dw[tid];
+    s_tb[tid] = p.tap_b[tid];
+  }
+
+  const int ld_row = tid >> 3, ld_chunk = tid & 7;
+  const int ghw = p.GH * p.GW;
+  int a_base[AR], a_ih[AR], a_iw[AR];
+#pragma unroll
+  for (int i = 0; i < AR; ++i) {
+    const int m = m0 + ld_row + 32 * i;
+    if (m < p.M) {
+      const int n = m / ghw, r = m - n * ghw;
+      const int gh = r / p.GW, gw = r - gh * p.GW;
+      a_base[i] = n * p.IH * p.IW * p.CA;
+      a_ih[i] = gh * p.sA;
+      a_iw[i] = gw * p.sA;
+    } else {
+      a_base[i] = 0;
+      a_ih[i] = -(1 << 28);
+      a_iw[i] = 0;
+    }
+  }
+  int b_off[BR];
+  bool b_ok[BR];
+#pragma unroll
+  for (int i = 0; i < BR; ++i) {
+    const int n = n0 + ld_row + 32 * i;
+    b_ok[i] = n < p.Ncols;
+    b_off[i] = b_ok[i] ? n * p.ldb : 0;
+  }
+  __syncthreads();
+
+  uint4 ra[AR], rb[BR];
+#define CONV_LOAD(kt_)                                                                          \
+  do {                                                                                          \
+    const int k_ = (kt_) * BK + ld_chunk * 8;                                                   \
+    const bool kok_ = k_ < p.K;                                                                 \
+    const int tap_ = kok_ ? k_ / p.CA : 0;                                                      \
+    const int ci_ = k_ - tap_ * p.CA;                                                           \
+    const int dh_ = s_dh[tap_], dw_ = s_dw[tap_];                                               \
+    const int boff_ = s_tb[tap_] * p.CA + ci_;                                                  \
+    _Pragma("unroll") for (int i = 0; i < AR; ++i) {                                            \
+      const int ih_ = a_ih[i] + dh_, iw_ = a_iw[i] + dw_;                                       \
+      const bool ok_ = kok_ && (unsigned)ih_ < (unsigned)p.IH && (unsigned)iw_ < (unsigned)p.IW; \
+      const bf16_t* src_ = p.A + (ok_ ? a_base[i] + (ih_ * p.IW + iw_) * p.CA + ci_ : 0);       \
+      const uint4 v_ = *(const uint4*)src_;                                                     \
+      ra[i] = sel4(ok_, v_);                                                                    \
+    }                                                                                           \
+    _Pragma("unroll") for (int i = 0; i < BR; ++i) {                                            \
+      const bool ok_ = kok_ && b_ok[i];                                                         \
+      const uint4 v_ = *(const uint4*)(p.B + (ok_ ? b_off[i] + boff_ : 0));                     \
+      rb[i] = sel4(ok_, v_);                                                                    \
+    }                                                                                           \
+  } while (0)
+#define CONV_STORE(buf_)                                                                        \
+  do {                                                                                          \
+    char* sa_ = smem + (buf_) * STAGE;                                                          \
+    char* sb_ = sa_ + A_BYTES;                                                                  \
+    _Pragma("unroll") for (int i = 0; i < AR; ++i) *(uint4*)(sa_ + swz(ld_row + 32 * i, ld_chunk)) = ra[i]; \
+    _Pragma("unroll") for (int i = 0; i < BR; ++i) *(uint4*)(sb_ + swz(ld_row + 32 * i, ld_chunk)) = rb[i]; \
+  } while (0)
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (p.K + BK - 1) / BK;
+  if (nk > 0) {
+    CONV_LOAD(0);
+    CONV_STORE(0);
+  }
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) CONV_LOAD(kt + 1);
+    const char* sa = smem + (kt & 1) * STAGE;
+    const char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[RM], bfg[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i) af[i] = *(const bf16x8*)(sa + swz(wm * WTM + i * 16 + fr, kk * 4 + fq));
+#pragma unroll
+      for (int j = 0; j < RN; ++j) bfg[j] = *(const bf16x8*)(sb + swz(wn * WTN + j * 16 + fr, kk * 4 + fq));
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) CONV_STORE((kt + 1) & 1);
+    __syncthreads();
+  }
+#undef CONV_LOAD
+#undef CONV_STORE
+
+  // ---------------- epilogue ----------------
+  bf16_t* ct = (bf16_t*)smem;
+  float* red = (float*)(smem + BM * CST * 2);  // [2 (s,q)][2 (wm)][BN]
+  const bool do_stats = p.stats != nullptr;
+#pragma unroll
+  for (int j = 0; j < RN; ++j) {
+    const int col = wn * WTN + j * 16 + fr;
+    const float bv = (p.bias != nullptr && n0 + col < p.Ncols) ? p.bias[n0 + col] : 0.f;
+    float s = 0.f, q = 0.f;
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * WTM + i * 16 + fq * 4 + r;
+        const bf16_t h = f2bf(acc[i][j][r] + bv);
+        ct[row * CST + col] = h;
+        if (do_stats && m0 + row < p.M) {
+          const float v = bf2f(h);
+          s += v;
+          q += v * v;
+        }
+      }
+    }
+    if (do_stats) {
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (fq == 0) {
+        red[(0 * 2 + wm) * BN + col] = s;
+        red[(1 * 2 + wm) * BN + col] = q;
+      }
+    }
+  }
+  __syncthreads();
+  if (do_stats && tid < BN && n0 + tid < p.Ncols) {
+    const float s = red[(0 * 2 + 0) * BN + tid] + red[(0 * 2 + 1) * BN + tid];
+    const float q = red[(1 * 2 + 0) * BN + tid] + red[(1 * 2 + 1) * BN + tid];
+    float* dst = p.stats + (size_t)(bm % p.stats_groups) * 2 * p.Ncols + n0 + tid;
+    atomicAdd(dst, s);
+    atomicAdd(dst + p.Ncols, q);
+  }
+  constexpr int CPR = BN / 8;
+  const bool direct = (p.so == 1 && p.oh0 == 0 && p.ow0 == 0 && p.GH == p.OH && p.GW == p.OW);
+#pragma unroll 4
+  for (int idx = tid; idx < BM * CPR; idx += NT) {
+    const int row = idx / CPR, ch = idx - row * CPR;
+    const int m = m0 + row, col = n0 + ch * 8;
+    if (m < p.M && col < p.Ncols) {
+      long pix;
+      if (direct) {
+        pix = m;
+      } else {
+        const int n = m / ghw, r = m - n * ghw;
+        const int gh = r / p.GW, gw = r - gh * p.GW;
+        pix = ((long)n * p.OH + gh * p.so + p.oh0) * p.OW + gw * p.so + p.ow0;
+      }
+      *(uint4*)(p.C + pix * p.ldc + p.c_off + col) = *(const uint4*)(ct + row * CST + ch * 8);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// weight gradient
+// ---------------------------------------------------------------------------
+constexpr int WBN = 128;      // columns (tap*Cin) per tile
+constexpr int WBK = 64;       // pixels per k-step
+constexpr int WROW = 288;     // LDS image row stride in bytes (256 + 32 pad)
+
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+DEVI bf16x4 tr_read(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(p));
+}
+
+template <int WBM>
+__global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(const WgradParams p) {
+  constexpr int A_BYTES = WBK * WROW;  // image [64 k][<=128 co] (row stride fixed 288 B)
+  constexpr int B_BYTES = WBK * WROW;  // image [64 k][128 cols]
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int WTM = WBM / 2, WTN = WBN / 2;
+  constexpr int RM = WTM / 16, RN = WTN / 16;
+  constexpr int ACH = WBM / 8;             // 16-B chunks per A image row
+  constexpr int AROWS = NT / ACH;          // rows covered by one pass of the block
+  constexpr int AR = WBK / AROWS;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int gm = (p.Cout + WBM - 1) / WBM;
+  const int tile = blockIdx.x;
+  const int bm = tile % gm, bn = tile / gm;
+  const int co0 = bm * WBM, j0 = bn * WBN;
+  const int kbeg = blockIdx.y * p.k_per_split;
+  const int kend = min(p.M, kbeg + p.k_per_split);
+
+  // B (X gather) loader: chunk column fixed per thread -> tap / ci fixed
+  const int b_cc = tid & 15, b_r0 = tid >> 4;  // 16 chunks x 16 rows per pass, 4 passes
+  const int jb = j0 + b_cc * 8;
+  const bool b_colok = jb < p.Ntot;
+  const int b_tap = b_colok ? jb / p.Cin : 0;
+  const int b_ci = jb - b_tap * p.Cin;
+  const int b_r = b_tap / p.KW, b_c = b_tap - (b_tap / p.KW) * p.KW;
+  const int b_dh = b_r * p.dil_h - p.pad_t, b_dw = b_c * p.dil_w - p.pad_l;
+  // A (dY) loader
+  const int a_cc = tid % ACH, a_r0 = tid / ACH;
+  const int coa = co0 + a_cc * 8;
+  const bool a_colok = coa < p.Cout;
+  const int ohw = p.OH * p.OW;
+
+  uint4 ra[AR], rb[4];
+#define WG_LOAD(k0_)                                                                            \
+  do {                                                                                          \
+    _Pragma("unroll") for (int i = 0; i < AR; ++i) {                                            \
+      const int m_ = (k0_) + a_r0 + AROWS * i;                                                  \
+      const bool ok_ = a_colok && m_ < kend;                                                    \
+      const uint4 v_ = *(const uint4*)(p.dY + (ok_ ? (long)m_ * p.Cout + coa : 0));             \
+      ra[i] = sel4(ok_, v_);                                                                    \
+    }                                                                                           \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                             \
+      const int m_ = (k0_) + b_r0 + 16 * i;                                                     \
+      const int n_ = m_ / ohw, r_ = m_ - n_ * ohw;                                              \
+      const int oh_ = r_ / p.OW, ow_ = r_ - oh_ * p.OW;                                         \
+      const int ih_ = oh_ * p.stride_h + b_dh, iw_ = ow_ * p.stride_w + b_dw;                   \
+      const bool ok_ = b_colok && m_ < kend && (unsigned)ih_ < (unsigned)p.IH &&                \
+                       (unsigned)iw_ < (unsigned)p.IW;                                          \
+      const uint4 v_ = *(const uint4*)(p.X + (ok_ ? (((long)n_ * p.IH + ih_) * p.IW + iw_) * p.Cin + b_ci : 0)); \
+      rb[i] = sel4(ok_, v_);                                                                    \
+    }                                                                                           \
+  } while (0)
+#define WG_STORE(buf_)                                                                          \
+  do {                                                                                          \
+    char* sa_ = smem + (buf_) * STAGE;                                                          \
+    char* sb_ = sa_ + A_BYTES;                                                                  \
+    _Pragma("unroll") for (int i = 0; i < AR; ++i) *(uint4*)(sa_ + (a_r0 + AROWS * i) * WROW + a_cc * 16) = ra[i]; \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) *(uint4*)(sb_ + (b_r0 + 16 * i) * WROW + b_cc * 16) = rb[i];     \
+  } while (0)
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (kend - kbeg + WBK - 1) / WBK;
+  if (nk > 0) {
+    WG_LOAD(kbeg);
+    WG_STORE(0);
+  }
+  __syncthreads();
+  // transposed-read addressing: lane i of 16-lane group g supplies row q=i>>2, cols 4*(i&3)
+  const int g = lane >> 4, li = lane & 15;
+  const int tq = li >> 2, tp = li & 3;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) WG_LOAD(kbeg + (kt + 1) * WBK);
+    const char* sa = smem + (kt & 1) * STAGE;
+    const char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      // permuted k order: elements 0-3 <- rows 4g+q, elements 4-7 <- rows 16+4g+q
+      const int r0 = kk * 32 + 4 * g + tq, r1 = r0 + 16;
+      bf16x8 af[RM], bfg[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+        const int c = (wm * WTM + i * 16 + 4 * tp) * 2;
+        const bf16x4 lo = tr_read(sa + r0 * WROW + c), hi = tr_read(sa + r1 * WROW + c);
+        af[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const int c = (wn * WTN + j * 16 + 4 * tp) * 2;
+        const bf16x4 lo = tr_read(sb + r0 * WROW + c), hi = tr_read(sb + r1 * WROW + c);
+        bfg[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) WG_STORE((kt + 1) & 1);
+    __syncthreads();
+  }
+#undef WG_LOAD
+#undef WG_STORE
+  if (nk == 0) return;
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = co0 + wm * WTM + i * 16 + fq * 4 + r;
+      if (co >= p.Cout) continue;
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const int col = j0 + wn * WTN + j * 16 + fr;
+        if (col < p.Ntot) atomicAdd(p.dW + (long)co * p.Ntot + col, acc[i][j][r]);
+      }
+    }
+}
+
+}  // namespace
+
+int conv_gemm_launch(const ConvParams& p, hipStream_t stream) {
+  if (p.M <= 0 || p.Ncols <= 0) return 0;
+  const int gm = cdiv(p.M, BM);
+  if (p.Ncols <= 64) {
+    const int gn = cdiv(p.Ncols, 64);
+    hipLaunchKernelGGL(conv_gemm_kernel<64>, dim3(gm * gn), dim3(NT), 0, stream, p);
+  } else {
+    const int gn = cdiv(p.Ncols, 128);
+    hipLaunchKernelGGL(conv_gemm_kernel<128>, dim3(gm * gn), dim3(NT), 0, stream, p);
+  }
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int conv_wgrad_launch(const WgradParams& p, int splits, hipStream_t stream) {
+  if (p.M <= 0) return 0;
+  const int gn = cdiv(p.Ntot, WBN);
+  if (p.Cout <= 64) {
+    const int gm = cdiv(p.Cout, 64);
+    hipLaunchKernelGGL(conv_wgrad_kernel<64>, dim3(gm * gn, splits), dim3(NT), 0, stream, p);
+  } else {
+    const int gm = cdiv(p.Cout, 128);
+    hipLaunchKernelGGL(conv_wgrad_kernel<128>, dim3(gm * gn, splits), dim3(NT), 0, stream, p);
+  }
+  HIP_CHECK_LAUNCH();
+  return 0;
+}

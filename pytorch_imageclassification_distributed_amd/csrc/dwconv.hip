@@ -1,0 +1,274 @@
+// Depthwise convolution (K4) and squeeze-excitation helpers (K13/K19) for
+// EfficientNet, NHWC bf16.  Depthwise conv has no reduction over channels, so
+// it is a bandwidth-bound VALU/LDS kernel, not an MFMA GEMM: every lane owns 8
+// consecutive channels of one output pixel and walks the kh x kw taps with
+// 16-B loads; the filter is pre-transposed to [taps][C] so a tap's 8 weights
+// are one 16-B load too.  Backward-data is written in gather form (per input
+// pixel), backward-weight reduces over pixels per (tap, channel chunk) with one
+// fp32 atomic per block and element.
+#include "common.h"
+
+namespace {
+
+struct DwGeom {
+  int N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl;
+};
+
+int grid_for(long work, int cap = 8192) {
+  long b = (work + 255) / 256;
+  return (int)(b < 1 ? 1 : (b > cap ? cap : b));
+}
+
+__global__ void dw_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w, bf16_t* __restrict__ y,
+                              DwGeom g) {
+  const int cch = g.C >> 3;
+  const long total = (long)g.N * g.OH * g.OW * cch;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cch) * 8;
+    long t = i / cch;
+    const int ow = (int)(t % g.OW); t /= g.OW;
+    const int oh = (int)(t % g.OH);
+    const int n = (int)(t / g.OH);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int r = 0; r < g.kh; ++r) {
+      const int ih = oh * g.sh - g.pt + r;
+      if ((unsigned)ih >= (unsigned)g.H) continue;
+      for (int c = 0; c < g.kw; ++c) {
+        const int iw = ow * g.sw - g.pl + c;
+        if ((unsigned)iw >= (unsigned)g.W) continue;
+        float xv[8], wv[8];
+        unpack8(*(const uint4*)(x + (((long)n * g.H + ih) * g.W + iw) * g.C + c0), xv);
+        unpack8(*(const uint4*)(w + (long)(r * g.kw + c) * g.C + c0), wv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += xv[k] * wv[k];
+      }
+    }
+    *(uint4*)(y + (((long)n * g.OH + oh) * g.OW + ow) * g.C + c0) = pack8(acc);
+  }
+}
+
+__global__ void dw_dgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ w,
+                                bf16_t* __restrict__ dx, DwGeom g) {
+  const int cch = g.C >> 3;
+  const long total = (long)g.N * g.H * g.W * cch;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cch) * 8;
+    long t = i / cch;
+    const int wi = (int)(t % g.W); t /= g.W;
+    const int h = (int)(t % g.H);
+    const int n = (int)(t / g.H);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int r = 0; r < g.kh; ++r) {
+      const int a = h + g.pt - r;
+      if (a < 0 || a % g.sh) continue;
+      const int oh = a / g.sh;
+      if (oh >= g.OH) continue;
+      for (int c = 0; c < g.kw; ++c) {
+        const int b = wi + g.pl - c;
+        if (b < 0 || b % g.sw) continue;
+        const int ow = b / g.sw;
+        if (ow >= g.OW) continue;
+        float dv[8], wv[8];
+        unpack8(*(const uint4*)(dy + (((long)n * g.OH + oh) * g.OW + ow) * g.C + c0), dv);
+        unpack8(*(const uint4*)(w + (long)(r * g.kw + c) * g.C + c0), wv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += dv[k] * wv[k];
+      }
+    }
+    *(uint4*)(dx + (((long)n * g.H + h) * g.W + wi) * g.C + c0) = pack8(acc);
+  }
+}
+
+// grid: (pixel blocks, taps); block = CHB chunk lanes x RP pixel lanes; dw layout [C][taps] fp32
+__global__ __launch_bounds__(256) void dw_wgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                        float* __restrict__ dw, DwGeom g, long pix_per_block) {
+  __shared__ float red[256][9];
+  const int cch = g.C >> 3;
+  const int CHB = cch < 256 ? cch : 256;
+  const int RP = 256 / CHB;
+  const int tid = threadIdx.x;
+  const int lc = tid % CHB, lr = tid / CHB;
+  const int tap = blockIdx.y;
+  const int r = tap / g.kw, q = tap - r * g.kw;
+  const long npix = (long)g.N * g.OH * g.OW;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int cb = 0; cb < cch; cb += CHB) {
+    const int chunk = cb + lc;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+    if (lr < RP && chunk < cch) {
+      const int c0 = chunk * 8;
+      const long pbeg = blockIdx.x * pix_per_block;
+      const long pend = pbeg + pix_per_block < npix ? pbeg + pix_per_block : npix;
+      for (long pix = pbeg + lr; pix < pend; pix += RP) {
+        long t = pix;
+        const int ow = (int)(t % g.OW); t /= g.OW;
+        const int oh = (int)(t % g.OH);
+        const int n = (int)(t / g.OH);
+        const int ih = oh * g.sh - g.pt + r, iw = ow * g.sw - g.pl + q;
+        if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) continue;
+        float dv[8], xv[8];
+        unpack8(*(const uint4*)(dy + pix * g.C + c0), dv);
+        unpack8(*(const uint4*)(x + (((long)n * g.H + ih) * g.W + iw) * g.C + c0), xv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += dv[k] * xv[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[tid][k] = acc[k];
+    __syncthreads();
+    if (lr == 0 && chunk < cch) {
+      for (int rr = 1; rr < RP; ++rr)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += red[tid + rr * CHB][k];
+      const int T = g.kh * g.kw;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) atomicAdd(dw + (long)(chunk * 8 + k) * T + tap, acc[k]);
+    }
+    __syncthreads();
+  }
+}
+
+// y[n,p,c] = x[n,p,c] * s[n,c]
+__global__ void se_scale_kernel(const bf16_t* __restrict__ x, const float* __restrict__ s, bf16_t* __restrict__ y,
+                                int N, int HW, int C) {
+  const int cch = C >> 3;
+  const long total = (long)N * HW * cch;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cch) * 8;
+    const long pix = i / cch;
+    const int n = (int)(pix / HW);
+    float v[8];
+    unpack8(*(const uint4*)(x + pix * C + c0), v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] *= s[(long)n * C + c0 + k];
+    *(uint4*)(y + pix * C + c0) = pack8(v);
+  }
+}
+
+// ds[n,c] = sum_p dy[n,p,c] * x[n,p,c]   (one thread per (n, chunk))
+__global__ void se_ds_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, float* __restrict__ ds,
+                             int N, int HW, int C) {
+  const int cch = C >> 3;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * cch) return;
+  const int n = i / cch, c0 = (i - n * cch) * 8;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int p = 0; p < HW; ++p) {
+    float a[8], b[8];
+    const long o = ((long)n * HW + p) * C + c0;
+    unpack8(*(const uint4*)(dy + o), a);
+    unpack8(*(const uint4*)(x + o), b);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] += a[k] * b[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) ds[(long)n * C + c0 + k] = acc[k];
+}
+
+// dx = dy * s[n,c] + dp[n,c] / HW
+__global__ void se_dx_kernel(const bf16_t* __restrict__ dy, const float* __restrict__ s, const float* __restrict__ dp,
+                             bf16_t* __restrict__ dx, int N, int HW, int C) {
+  const int cch = C >> 3;
+  const long total = (long)N * HW * cch;
+  const float inv = 1.f / HW;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cch) * 8;
+    const long pix = i / cch;
+    const int n = (int)(pix / HW);
+    float v[8];
+    unpack8(*(const uint4*)(dy + pix * C + c0), v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = v[k] * s[(long)n * C + c0 + k] + dp[(long)n * C + c0 + k] * inv;
+    *(uint4*)(dx + pix * C + c0) = pack8(v);
+  }
+}
+
+// fp32 activations for the SE MLP: 0 = silu, 1 = sigmoid
+__global__ void act32_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, long n, int kind) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    y[i] = kind == 0 ? silu_f(x[i]) : sigmoid_f(x[i]);
+}
+
+// dx = dy * act'(x) ; for sigmoid the caller passes y = sigmoid(x) in x with kind 2
+__global__ void act32_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ dx,
+                                 long n, int kind) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float v = x[i];
+    float d;
+    if (kind == 0) {
+      const float s = sigmoid_f(v);
+      d = s * (1.f + v * (1.f - s));
+    } else if (kind == 1) {
+      const float s = sigmoid_f(v);
+      d = s * (1.f - s);
+    } else {
+      d = v * (1.f - v);
+    }
+    dx[i] = dy[i] * d;
+  }
+}
+
+}  // namespace
+
+int dw_fwd_launch(const bf16_t* x, const bf16_t* w, bf16_t* y, float* /*stats*/, int N, int H, int W, int C, int OH,
+                  int OW, int kh, int kw, int sh, int sw, int pt, int pl, hipStream_t s) {
+  DwGeom g{N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl};
+  hipLaunchKernelGGL(dw_fwd_kernel, dim3(grid_for((long)N * OH * OW * (C / 8))), dim3(256), 0, s, x, w, y, g);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int dw_dgrad_launch(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int W, int C, int OH, int OW,
+                    int kh, int kw, int sh, int sw, int pt, int pl, hipStream_t s) {
+  DwGeom g{N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl};
+  hipLaunchKernelGGL(dw_dgrad_kernel, dim3(grid_for((long)N * H * W * (C / 8))), dim3(256), 0, s, dy, w, dx, g);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int dw_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, int N, int H, int W, int C, int OH, int OW,
+                    int kh, int kw, int sh, int sw, int pt, int pl, hipStream_t s) {
+  DwGeom g{N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl};
+  const long npix = (long)N * OH * OW;
+  const int T = kh * kw;
+  long pblocks = 2048 / T;
+  if (pblocks < 8) pblocks = 8;
+  long ppb = (npix + pblocks - 1) / pblocks;
+  if (ppb < 64) ppb = 64;
+  pblocks = (npix + ppb - 1) / ppb;
+  hipLaunchKernelGGL(dw_wgrad_kernel, dim3((unsigned)pblocks, T), dim3(256), 0, s, dy, x, dw, g, ppb);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int se_scale_launch(const bf16_t* x, const float* sc, bf16_t* y, int N, int HW, int C, hipStream_t s) {
+  hipLaunchKernelGGL(se_scale_kernel, dim3(grid_for((long)N * HW * (C / 8))), dim3(256), 0, s, x, sc, y, N, HW, C);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int se_ds_launch(const bf16_t* dy, const bf16_t* x, float* ds, int N, int HW, int C, hipStream_t s) {
+  hipLaunchKernelGGL(se_ds_kernel, dim3(cdiv((long)N * (C / 8), 256)), dim3(256), 0, s, dy, x, ds, N, HW, C);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int se_dx_launch(const bf16_t* dy, const float* sc, const float* dp, bf16_t* dx, int N, int HW, int C,
+                 hipStream_t s) {
+  hipLaunchKernelGGL(se_dx_kernel, dim3(grid_for((long)N * HW * (C / 8))), dim3(256), 0, s, dy, sc, dp, dx, N, HW, C);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int act32_fwd_launch(const float* x, float* y, long n, int kind, hipStream_t s) {
+  hipLaunchKernelGGL(act32_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, y, n, kind);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int act32_bwd_launch(const float* x, const float* dy, float* dx, long n, int kind, hipStream_t s) {
+  hipLaunchKernelGGL(act32_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, dy, dx, n, kind);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,209 @@
+// Layout / cast / elementwise helpers (K17, K20, K22, K24-K26 and weight prep).
+//
+//  prepare_input   fp32 NCHW (loader output) -> bf16 NHWC padded to Cp channels,
+//                  optional per-channel affine (Inception transform_input) - one pass
+//  cast_bf16       fp32 -> bf16 (weight shadow initialisation)
+//  weight_pad      [Co][T][Ci] -> [Co][T][Cp] zero-padded (stem conv, Cin 3 -> 8)
+//  weight_t        [Co][T][Ci] -> [Ci][T'][Co] with optional tap flip, for dgrad
+//  grad_unpad      fp32 [Co][T][Cp] -> [Co][T][Ci]
+//  copy_channels   strided channel-slice copy (concat forward / split backward)
+//  add             bf16 out = a + b
+//  dropout         fp32 features, counter-based hash RNG (seed, offset from device memory)
+//  drop_connect    per-sample scale on bf16 NHWC (efficientnet stochastic depth)
+#include "common.h"
+
+namespace {
+
+int grid_for(long work, int cap = 8192) {
+  long b = (work + 255) / 256;
+  return (int)(b < 1 ? 1 : (b > cap ? cap : b));
+}
+
+__global__ void prepare_input_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int N, int C, int HW,
+                                     int Cp, const float* __restrict__ sc, const float* __restrict__ sh) {
+  const long total = (long)N * HW;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long n = i / HW, s = i - n * HW;
+    for (int c0 = 0; c0 < Cp; c0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int c = c0 + k;
+        float t = 0.f;
+        if (c < C) {
+          t = x[(n * C + c) * HW + s];
+          if (sc) t = t * sc[c] + sh[c];
+        }
+        v[k] = t;
+      }
+      *(uint4*)(y + i * Cp + c0) = pack8(v);
+    }
+  }
+}
+
+__global__ void cast_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    y[i] = f2bf(x[i]);
+}
+
+__global__ void weight_pad_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ o, long rows, int Ci, int Cp) {
+  const long total = rows * Cp;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / Cp;
+    const int c = (int)(i - r * Cp);
+    o[i] = c < Ci ? w[r * Ci + c] : (bf16_t)0;
+  }
+}
+
+// out[ci][t][co] = w[co][flip ? T-1-t : t][ci]
+__global__ void weight_t_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ o, int Co, int T, int Ci) {
+  const long total = (long)Co * T * Ci;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int co = (int)(i % Co);
+    long r = i / Co;
+    const int t = (int)(r % T);
+    const int ci = (int)(r / T);
+    o[i] = w[((long)co * T + t) * Ci + ci];
+  }
+}
+
+__global__ void grad_unpad_kernel(const float* __restrict__ g, float* __restrict__ o, long rows, int Cp, int Ci) {
+  const long total = rows * Ci;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / Ci;
+    const int c = (int)(i - r * Ci);
+    o[i] = g[r * Cp + c];
+  }
+}
+
+// dst[row*ldd + doff + c] = src[row*lds + soff + c], c < C (C, offsets multiples of 8)
+__global__ void copy_channels_kernel(const bf16_t* __restrict__ src, int lds, int soff, bf16_t* __restrict__ dst,
+                                     int ldd, int doff, long rows, int C) {
+  const int cch = C >> 3;
+  const long total = rows * cch;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / cch;
+    const int c0 = (int)(i - r * cch) * 8;
+    *(uint4*)(dst + r * ldd + doff + c0) = *(const uint4*)(src + r * lds + soff + c0);
+  }
+}
+
+__global__ void add_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ b, bf16_t* __restrict__ o,
+                           long n8) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    float x[8], y[8];
+    unpack8(*(const uint4*)(a + i * 8), x);
+    unpack8(*(const uint4*)(b + i * 8), y);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] += y[k];
+    *(uint4*)(o + i * 8) = pack8(x);
+  }
+}
+
+DEVI uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
+  // murmur3-style finalizer over a 3-word counter
+  uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u ^ c * 0xC2B2AE3Du;
+  h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+  return h;
+}
+
+// y = x * keep/(1-p); mask byte saved for backward.  seed[0] = seed, seed[1] = offset
+__global__ void dropout_kernel(const float* __restrict__ x, float* __restrict__ y, uint8_t* __restrict__ mask,
+                               long n, float p, const long long* __restrict__ seed) {
+  const uint32_t s0 = (uint32_t)seed[0], s1 = (uint32_t)seed[1];
+  const float scale = 1.f / (1.f - p);
+  const uint32_t thr = (uint32_t)(p * 4294967296.0);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const bool keep = hash3(s0, s1, (uint32_t)i) >= thr;
+    mask[i] = keep;
+    y[i] = keep ? x[i] * scale : 0.f;
+  }
+}
+
+__global__ void dropout_bwd_kernel(const float* __restrict__ dy, const uint8_t* __restrict__ mask,
+                                   float* __restrict__ dx, long n, float p) {
+  const float scale = 1.f / (1.f - p);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    dx[i] = mask[i] ? dy[i] * scale : 0.f;
+}
+
+// per-sample scale: y[n,...] = x[n,...] * scale[n]
+__global__ void scale_rows_kernel(const bf16_t* __restrict__ x, const float* __restrict__ scale,
+                                  bf16_t* __restrict__ y, long per_sample8, long n8) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    const float s = scale[i / per_sample8];
+    float v[8];
+    unpack8(*(const uint4*)(x + i * 8), v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] *= s;
+    *(uint4*)(y + i * 8) = pack8(v);
+  }
+}
+
+}  // namespace
+
+int prepare_input_launch(const float* x, bf16_t* y, int N, int C, int HW, int Cp, const float* sc,
+                         const float* sh, hipStream_t s) {
+  hipLaunchKernelGGL(prepare_input_kernel, dim3(grid_for((long)N * HW)), dim3(256), 0, s, x, y, N, C, HW, Cp, sc,
+                     sh);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int cast_bf16_launch(const float* x, bf16_t* y, long n, hipStream_t s) {
+  hipLaunchKernelGGL(cast_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, y, n);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int weight_pad_launch(const bf16_t* w, bf16_t* o, long rows, int Ci, int Cp, hipStream_t s) {
+  hipLaunchKernelGGL(weight_pad_kernel, dim3(grid_for(rows * Cp)), dim3(256), 0, s, w, o, rows, Ci, Cp);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int weight_t_launch(const bf16_t* w, bf16_t* o, int Co, int T, int Ci, hipStream_t s) {
+  hipLaunchKernelGGL(weight_t_kernel, dim3(grid_for((long)Co * T * Ci)), dim3(256), 0, s, w, o, Co, T, Ci);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int grad_unpad_launch(const float* g, float* o, long rows, int Cp, int Ci, hipStream_t s) {
+  hipLaunchKernelGGL(grad_unpad_kernel, dim3(grid_for(rows * Ci)), dim3(256), 0, s, g, o, rows, Cp, Ci);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int copy_channels_launch(const bf16_t* src, int lds, int soff, bf16_t* dst, int ldd, int doff, long rows, int C,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(copy_channels_kernel, dim3(grid_for(rows * (C / 8))), dim3(256), 0, s, src, lds, soff, dst,
+                     ldd, doff, rows, C);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int add_launch(const bf16_t* a, const bf16_t* b, bf16_t* o, long n, hipStream_t s) {
+  hipLaunchKernelGGL(add_kernel, dim3(grid_for(n / 8)), dim3(256), 0, s, a, b, o, n / 8);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int dropout_launch(const float* x, float* y, uint8_t* mask, long n, float p, const long long* seed,
+                   hipStream_t s) {
+  hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, y, mask, n, p, seed);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int dropout_bwd_launch(const float* dy, const uint8_t* mask, float* dx, long n, float p, hipStream_t s) {
+  hipLaunchKernelGGL(dropout_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, dy, mask, dx, n, p);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int scale_rows_launch(const bf16_t* x, const float* scale, bf16_t* y, long per_sample, long n, hipStream_t s) {
+  hipLaunchKernelGGL(scale_rows_kernel, dim3(grid_for(n / 8)), dim3(256), 0, s, x, scale, y, per_sample / 8,
+                     n / 8);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,241 @@
+// Pooling for NHWC bf16 (K10-K13).  Every kernel moves 8 channels (16 B) per
+// lane; backward passes are written in *gather* form (each input pixel sums
+// the outputs whose window covers it), so no atomics are needed.
+//
+//   max_pool  fwd: window max + uint8 argmax (window index) per element
+//             bwd: dx = sum over covering outputs whose argmax points here
+//   avg_pool  fwd/bwd: count_include_pad=True (divisor kh*kw), torch default
+//   global avg fwd: [N,HW,C] bf16 -> [N,C] fp32;  bwd: dx = dy / HW (bf16)
+#include "common.h"
+
+namespace {
+
+struct PoolGeom {
+  int N, H, W, C, OH, OW, kh, kw, sh, sw, ph, pw;
+};
+
+__global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                   uint8_t* __restrict__ idx, PoolGeom g) {
+  const int cch = g.C >> 3;
+  const long total = (long)g.N * g.OH * g.OW * cch;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cch) * 8;
+    long t = i / cch;
+    const int ow = (int)(t % g.OW); t /= g.OW;
+    const int oh = (int)(t % g.OH);
+    const int n = (int)(t / g.OH);
+    float best[8];
+    int bi[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; bi[k] = 0; }
+    for (int r = 0; r < g.kh; ++r) {
+      const int ih = oh * g.sh - g.ph + r;
+      if ((unsigned)ih >= (unsigned)g.H) continue;
+      for (int c = 0; c < g.kw; ++c) {
+        const int iw = ow * g.sw - g.pw + c;
+        if ((unsigned)iw >= (unsigned)g.W) continue;
+        float v[8];
+        unpack8(*(const uint4*)(x + (((long)n * g.H + ih) * g.W + iw) * g.C + c0), v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (v[k] > best[k] || (v[k] != v[k])) { best[k] = v[k]; bi[k] = r * g.kw + c; }
+      }
+    }
+    const long o = (((long)n * g.OH + oh) * g.OW + ow) * g.C + c0;
+    *(uint4*)(y + o) = pack8(best);
+    if (idx) {
+      uint2 pk;
+      pk.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
+      pk.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
+      *(uint2*)(idx + o) = pk;
+    }
+  }
+}
+
+__global__ void maxpool_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                   bf16_t* __restrict__ dx, PoolGeom g) {
+  const int cch = g.C >> 3;
+  const long total = (long)g.N * g.H * g.W * cch;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cch) * 8;
+    long t = i / cch;
+    const int w = (int)(t % g.W); t /= g.W;
+    const int h = (int)(t % g.H);
+    const int n = (int)(t / g.H);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // outputs oh with oh*sh - ph <= h <= oh*sh - ph + kh - 1
+    const int oh_lo = max(0, (h + g.ph - g.kh + g.sh) / g.sh);
+    const int oh_hi = min(g.OH - 1, (h + g.ph) / g.sh);
+    const int ow_lo = max(0, (w + g.pw - g.kw + g.sw) / g.sw);
+    const int ow_hi = min(g.OW - 1, (w + g.pw) / g.sw);
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      const int r = h - (oh * g.sh - g.ph);
+      if (r < 0 || r >= g.kh) continue;
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const int c = w - (ow * g.sw - g.pw);
+        if (c < 0 || c >= g.kw) continue;
+        const int me = r * g.kw + c;
+        const long o = (((long)n * g.OH + oh) * g.OW + ow) * g.C + c0;
+        const uint2 pk = *(const uint2*)(idx + o);
+        float v[8];
+        unpack8(*(const uint4*)(dy + o), v);
+        const uint32_t w0 = pk.x, w1 = pk.y;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if ((int)((w0 >> (8 * k)) & 0xff) == me) acc[k] += v[k];
+          if ((int)((w1 >> (8 * k)) & 0xff) == me) acc[4 + k] += v[4 + k];
+        }
+      }
+    }
+    *(uint4*)(dx + (((long)n * g.H + h) * g.W + w) * g.C + c0) = pack8(acc);
+  }
+}
+
+__global__ void avgpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, PoolGeom g) {
+  const int cch = g.C >> 3;
+  const long total = (long)g.N * g.OH * g.OW * cch;
+  const float inv = 1.f / (g.kh * g.kw);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cch) * 8;
+    long t = i / cch;
+    const int ow = (int)(t % g.OW); t /= g.OW;
+    const int oh = (int)(t % g.OH);
+    const int n = (int)(t / g.OH);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int r = 0; r < g.kh; ++r) {
+      const int ih = oh * g.sh - g.ph + r;
+      if ((unsigned)ih >= (unsigned)g.H) continue;
+      for (int c = 0; c < g.kw; ++c) {
+        const int iw = ow * g.sw - g.pw + c;
+        if ((unsigned)iw >= (unsigned)g.W) continue;
+        float v[8];
+        unpack8(*(const uint4*)(x + (((long)n * g.H + ih) * g.W + iw) * g.C + c0), v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += v[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] *= inv;
+    *(uint4*)(y + (((long)n * g.OH + oh) * g.OW + ow) * g.C + c0) = pack8(acc);
+  }
+}
+
+__global__ void avgpool_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx, PoolGeom g) {
+  const int cch = g.C >> 3;
+  const long total = (long)g.N * g.H * g.W * cch;
+  const float inv = 1.f / (g.kh * g.kw);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cch) * 8;
+    long t = i / cch;
+    const int w = (int)(t % g.W); t /= g.W;
+    const int h = (int)(t % g.H);
+    const int n = (int)(t / g.H);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int oh_lo = max(0, (h + g.ph - g.kh + g.sh) / g.sh);
+    const int oh_hi = min(g.OH - 1, (h + g.ph) / g.sh);
+    const int ow_lo = max(0, (w + g.pw - g.kw + g.sw) / g.sw);
+    const int ow_hi = min(g.OW - 1, (w + g.pw) / g.sw);
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      const int r = h - (oh * g.sh - g.ph);
+      if (r < 0 || r >= g.kh) continue;
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const int c = w - (ow * g.sw - g.pw);
+        if (c < 0 || c >= g.kw) continue;
+        float v[8];
+        unpack8(*(const uint4*)(dy + (((long)n * g.OH + oh) * g.OW + ow) * g.C + c0), v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += v[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] *= inv;
+    *(uint4*)(dx + (((long)n * g.H + h) * g.W + w) * g.C + c0) = pack8(acc);
+  }
+}
+
+// one thread per (n, 8-channel chunk); loops over HW
+__global__ void gap_fwd_kernel(const bf16_t* __restrict__ x, float* __restrict__ y, int N, int HW, int C) {
+  const int cch = C >> 3;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * cch) return;
+  const int n = i / cch, c0 = (i - n * cch) * 8;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const bf16_t* p = x + (long)n * HW * C + c0;
+  for (int s = 0; s < HW; ++s) {
+    float v[8];
+    unpack8(*(const uint4*)(p + (long)s * C), v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] += v[k];
+  }
+  const float inv = 1.f / HW;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) y[(long)n * C + c0 + k] = acc[k] * inv;
+}
+
+__global__ void gap_bwd_kernel(const float* __restrict__ dy, bf16_t* __restrict__ dx, int N, int HW, int C) {
+  const int cch = C >> 3;
+  const long total = (long)N * HW * cch;
+  const float inv = 1.f / HW;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cch) * 8;
+    const long pix = i / cch;
+    const int n = (int)(pix / HW);
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = dy[(long)n * C + c0 + k] * inv;
+    *(uint4*)(dx + pix * C + c0) = pack8(v);
+  }
+}
+
+int grid_for(long work, int cap = 8192) {
+  long b = (work + 255) / 256;
+  return (int)(b < 1 ? 1 : (b > cap ? cap : b));
+}
+
+}  // namespace
+
+int maxpool_fwd_launch(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH, int OW,
+                       int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t s) {
+  PoolGeom g{N, H, W, C, OH, OW, kh, kw, sh, sw, ph, pw};
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((long)N * OH * OW * (C / 8))), dim3(256), 0, s, x, y,
+                     idx, g);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int maxpool_bwd_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W, int C, int OH,
+                       int OW, int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t s) {
+  PoolGeom g{N, H, W, C, OH, OW, kh, kw, sh, sw, ph, pw};
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for((long)N * H * W * (C / 8))), dim3(256), 0, s, dy, idx,
+                     dx, g);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int avgpool_fwd_launch(const bf16_t* x, bf16_t* y, int N, int H, int W, int C, int OH, int OW, int kh, int kw,
+                       int sh, int sw, int ph, int pw, hipStream_t s) {
+  PoolGeom g{N, H, W, C, OH, OW, kh, kw, sh, sw, ph, pw};
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(grid_for((long)N * OH * OW * (C / 8))), dim3(256), 0, s, x, y, g);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int avgpool_bwd_launch(const bf16_t* dy, bf16_t* dx, int N, int H, int W, int C, int OH, int OW, int kh,
+                       int kw, int sh, int sw, int ph, int pw, hipStream_t s) {
+  PoolGeom g{N, H, W, C, OH, OW, kh, kw, sh, sw, ph, pw};
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_for((long)N * H * W * (C / 8))), dim3(256), 0, s, dy, dx, g);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int gap_fwd_launch(const bf16_t* x, float* y, int N, int HW, int C, hipStream_t s) {
+  hipLaunchKernelGGL(gap_fwd_kernel, dim3(cdiv((long)N * (C / 8), 256)), dim3(256), 0, s, x, y, N, HW, C);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int gap_bwd_launch(const float* dy, bf16_t* dx, int N, int HW, int C, hipStream_t s) {
+  hipLaunchKernelGGL(gap_bwd_kernel, dim3(grid_for((long)N * HW * (C / 8))), dim3(256), 0, s, dy, dx, N, HW, C);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,77 @@
+"""CLI / config for ``train.py``.
+
+The reference has exactly three flags (train.py:27-31): ``--local_rank`` (int,
+default 0), ``--datadir`` (required), ``--batchsize`` (int, default 4).  They are
+kept with the same names and defaults (``--local-rank`` is accepted too, A7).
+Everything the reference hard-codes becomes a flag whose default equals the
+reference constant: model ``inceptionv3`` (train.py:122), image
+size 299 (:110), lr 5e-6 (:127), milestones 50/80 and gamma 0.5 (:156), class
+weights 3,3,10,1,4,4,5 (:157), 100 epochs (:161), 6 workers (:114), val batch 1
+(:118), aux weight 0.4 (:52), ``dtmodel/cp`` (:136), latest every 5 epochs (:183).
+"""
+from __future__ import annotations
+
+import argparse
+
+REF_CLASS_WEIGHTS = (3.0, 3.0, 10.0, 1.0, 4.0, 4.0, 5.0)
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(description="MI355X-native distributed image classification trainer")
+    # --- reference flags (train.py:27-31)
+    p.add_argument("--local_rank", "--local-rank", dest="local_rank", default=0, type=int)
+    p.add_argument("--datadir", default="", help="ImageFolder root with train/ and valid/ (required unless --synthetic)")
+    p.add_argument("--batchsize", default=4, type=int, help="per-process batch size")
+    # --- reference constants as flags
+    p.add_argument("--model", default="inceptionv3")
+    p.add_argument("--image-size", type=int, default=None, help="default: 299 for inceptionv3, 224 resnets, native for efficientnet")
+    p.add_argument("--lr", type=float, default=0.5e-5)
+    p.add_argument("--epochs", type=int, default=100)
+    p.add_argument("--milestones", type=int, nargs="*", default=[50, 80])
+    p.add_argument("--gamma", type=float, default=0.5)
+    p.add_argument("--class-weights", default="auto",
+                   help="comma list, 'auto' (reference weights if 7 classes else uniform) or 'none'")
+    p.add_argument("--num-workers", type=int, default=6)
+    p.add_argument("--val-batchsize", type=int, default=1)
+    p.add_argument("--aux-weight", type=float, default=0.4)
+    p.add_argument("--ckpt-dir", default="dtmodel/cp")
+    p.add_argument("--latest-every", type=int, default=5)
+    # --- new
+    p.add_argument("--synthetic", action="store_true", help="synthetic data instead of --datadir")
+    p.add_argument("--synthetic-train-size", type=int, default=512)
+    p.add_argument("--synthetic-val-size", type=int, default=128)
+    p.add_argument("--num-classes", type=int, default=None, help="default: from dataset (synthetic: 7)")
+    p.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
+    p.add_argument("--backend", default="auto", help="process group backend: auto|rccl|nccl|gloo")
+    p.add_argument("--compute", default="auto", choices=["auto", "hip", "torch"],
+                   help="hip = native kernels (GPU default); torch = ATen reference stack")
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
+                   help="GPU activation dtype (hip path computes in bf16 with fp32 master weights)")
+    p.add_argument("--sync-bn", dest="sync_bn", action="store_true", default=True)
+    p.add_argument("--no-sync-bn", dest="sync_bn", action="store_false")
+    p.add_argument("--bucket-mb", type=float, default=32.0)
+    p.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
+    p.add_argument("--steps-per-epoch", type=int, default=None, help="cap on train steps per epoch")
+    p.add_argument("--val-steps", type=int, default=None, help="cap on validation steps")
+    p.add_argument("--resume", default="best",
+                   help="best (reference behaviour) | latest | auto | none | <path>")
+    p.add_argument("--log-interval", type=int, default=1,
+                   help="host-side loss readback every N steps (1 = reference per-step semantics)")
+    p.add_argument("--no-progress", action="store_true", help="disable tqdm progress bar")
+    p.add_argument("--metrics-file", default=None, help="rank-0 JSONL metrics output")
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--exact-val", action="store_true", help="mask DistributedSampler padding in validation (A15)")
+    p.add_argument("--pretrained", default=None, help="local torchvision-layout state_dict to initialise the backbone")
+    p.add_argument("--timeout-min", type=float, default=10.0, help="process-group timeout (minutes)")
+    return p
+
+
+def parse_class_weights(spec: str, num_classes: int):
+    if spec == "none":
+        return None
+    if spec == "auto":
+        return list(REF_CLASS_WEIGHTS) if num_classes == len(REF_CLASS_WEIGHTS) else None
+    w = [float(x) for x in spec.split(",")]
+    if len(w) != num_classes:
+        raise ValueError(f"--class-weights has {len(w)} entries, dataset has {num_classes} classes")
+    return w

@@ -1,0 +1,263 @@
+"""Training engine with the reference's semantics (reference train.py:36-188).
+
+Per training step (reference train.py:44-73):
+  H2D copy -> forward (Inception: ``CE(logits) + 0.4*CE(aux)``) -> loss
+  all-reduce SUM / world -> meter update -> rank-0 progress text
+  ``Epoch: {e}; Loss {val:.4f}|({avg:.4f})`` -> zero_grad -> backward -> step.
+Per epoch (train.py:161-188): ``sampler.set_epoch`` -> train -> scheduler.step
+-> validate (top-1 %, all ranks combined) -> rank 0 saves ``best_model`` on
+improvement and ``latest_model`` every 5 epochs.
+
+Execution paths:
+* ``compute='hip'`` (GPU default): our kernels, our bucketed RCCL reducer
+  (``parallel.GradReducer``), our SyncBN, fused Adam.
+* ``compute='torch'`` on GPU: the *reference stack* - torch DDP +
+  nn.SyncBatchNorm + bf16 autocast over ATen/MIOpen - used to measure the
+  baseline on the same box.
+* CPU: ATen reference ops, gloo, our reducer/SyncBN (torch SyncBN is GPU-only).
+
+Host syncs: the loss readback happens every ``log_interval`` steps (1 =
+reference behaviour, A21); validation accumulates correct/total on device and
+all-reduces two integers (A14) instead of per-sample ``.cpu()`` + pickle.
+"""
+from __future__ import annotations
+
+import math
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+from torch.utils.data import DataLoader
+from torch.utils.data.distributed import DistributedSampler
+
+from ..data import CudaPrefetcher, ImageDataset, SyntheticImageDataset
+from ..models import DEFAULT_IMAGE_SIZE, Classifier
+from ..ops import functional as Fx
+from ..parallel import GradReducer, convert_sync_batchnorm
+from ..utils import (BEST, LATEST, AccuracyCounter, DeviceMeter, JsonlLogger, load_checkpoint,
+                     load_model_state, resolve_resume, save_checkpoint)
+from .config import parse_class_weights
+from .optim import FusedAdam, MultiStepLR
+
+
+def _is_inception(name: str) -> bool:
+    return "inception" in name
+
+
+class Trainer:
+    def __init__(self, args, ctx):
+        self.args, self.ctx = args, ctx
+        self.dev = ctx.device
+        torch.manual_seed(args.seed)
+        if args.compute != "auto":
+            Fx.set_backend(args.compute)
+        self.hip = self.dev.type == "cuda" and Fx.get_backend() != "torch"
+        self.name = args.model
+        self.image_size = args.image_size or DEFAULT_IMAGE_SIZE.get(args.model, 224)
+        self._build_data()
+        self._build_model()
+
+    # ------------------------------------------------------------------ data
+    def _build_data(self):
+        a = self.args
+        if a.synthetic:
+            nc = a.num_classes or 7
+            self.train_ds = SyntheticImageDataset(a.synthetic_train_size, nc, self.image_size, seed=a.seed)
+            self.val_ds = SyntheticImageDataset(a.synthetic_val_size, nc, self.image_size, seed=a.seed + 1)
+        else:
+            if not a.datadir:
+                raise SystemExit("--datadir is required unless --synthetic is given")
+            self.train_ds = ImageDataset(a.datadir, "train", self.image_size)
+            self.val_ds = ImageDataset(a.datadir, "valid", self.image_size)
+        self.num_classes = a.num_classes or (self.train_ds.num_classes if not a.synthetic else 7)
+        pin = self.dev.type == "cuda"
+        self.train_sampler = DistributedSampler(self.train_ds, num_replicas=self.ctx.world_size,
+                                                rank=self.ctx.rank, seed=a.seed)
+        self.train_loader = DataLoader(self.train_ds, batch_size=a.batchsize, shuffle=False,
+                                       num_workers=a.num_workers, pin_memory=pin,
+                                       sampler=self.train_sampler, drop_last=False,
+                                       persistent_workers=a.num_workers > 0)
+        self.val_sampler = DistributedSampler(self.val_ds, num_replicas=self.ctx.world_size,
+                                              rank=self.ctx.rank, seed=a.seed)
+        self.val_loader = DataLoader(self.val_ds, batch_size=a.val_batchsize, shuffle=False,
+                                     num_workers=a.num_workers, pin_memory=pin, sampler=self.val_sampler)
+
+    # ------------------------------------------------------------------ model
+    def _build_model(self):
+        a, ctx = self.args, self.ctx
+        model = Classifier(self.name, self.num_classes, pretrained=a.pretrained).to(self.dev)
+        self.ddp = None
+        self.reducer = None
+        self.autocast = False
+        if self.dev.type == "cuda" and not self.hip:
+            # reference stack: torch DDP + SyncBatchNorm (+ bf16 autocast)
+            model = model.to(memory_format=torch.channels_last)
+            if a.sync_bn and ctx.world_size > 1:
+                model = nn.SyncBatchNorm.convert_sync_batchnorm(model)
+            self.autocast = a.dtype == "bf16"
+            net = model
+            if ctx.world_size > 1:
+                net = nn.parallel.DistributedDataParallel(model, device_ids=[ctx.local_rank],
+                                                          output_device=ctx.local_rank,
+                                                          bucket_cap_mb=a.bucket_mb)
+            self.net = net
+        else:
+            if self.hip:
+                model = model.to(memory_format=torch.channels_last)
+            if a.sync_bn:
+                convert_sync_batchnorm(model)
+            if ctx.world_size > 1:
+                comm = torch.bfloat16 if a.comm_dtype == "bf16" else None
+                self.reducer = GradReducer(model, bucket_cap_mb=a.bucket_mb, comm_dtype=comm)
+            self.net = model
+        self.model = model
+        self.optimizer = FusedAdam(model.parameters(), lr=a.lr)
+        self.scheduler = MultiStepLR(self.optimizer, milestones=a.milestones, gamma=a.gamma)
+        w = parse_class_weights(a.class_weights, self.num_classes)
+        self.class_weight = torch.tensor(w, dtype=torch.float32, device=self.dev) if w else None
+        self.best_score = 0.0
+        self.start_epoch = 0
+
+    # ------------------------------------------------------------------ step
+    def compute_loss(self, images, labels):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.autocast):
+            out = self.net(images)
+        if _is_inception(self.name) and isinstance(out, tuple):
+            return (Fx.cross_entropy(out[0], labels, self.class_weight)
+                    + self.args.aux_weight * Fx.cross_entropy(out[1], labels, self.class_weight))
+        return Fx.cross_entropy(out, labels, self.class_weight)
+
+    def train_step(self, images, labels):
+        """forward + loss + backward + (overlapped) all-reduce + Adam.  Returns the local loss."""
+        loss = self.compute_loss(images, labels)
+        self.optimizer.zero_grad(set_to_none=True)
+        loss.backward()
+        scale = self.reducer.finish() if self.reducer is not None else 1.0
+        self.optimizer.step(grad_scale=scale)
+        return loss.detach()
+
+    def reduce_loss(self, loss):
+        """Reference train.py:59-63: all-reduce SUM / world (enqueued, no host sync)."""
+        red = loss.clone().float()
+        if self.ctx.world_size > 1:
+            dist.all_reduce(red, op=dist.ReduceOp.SUM)
+            red /= self.ctx.world_size
+        return red
+
+    # ------------------------------------------------------------------ epochs
+    def _loader(self, loader):
+        return CudaPrefetcher(loader, self.dev) if self.dev.type == "cuda" else loader
+
+    def train_epoch(self, epoch: int):
+        a = self.args
+        self.net.train()
+        meter = DeviceMeter(self.dev)
+        show = self.ctx.is_main and not a.no_progress
+        it = self._loader(self.train_loader)
+        bar = None
+        if show:
+            from tqdm import tqdm
+            bar = tqdm(total=len(self.train_loader) if a.steps_per_epoch is None
+                       else min(len(self.train_loader), a.steps_per_epoch), file=sys.stdout)
+        for index, data in enumerate(it):
+            if a.steps_per_epoch is not None and index >= a.steps_per_epoch:
+                break
+            images, labels = data["image"], data["label"]
+            if images.device != self.dev:
+                images = images.to(self.dev, non_blocking=True)
+                labels = labels.to(self.dev, non_blocking=True)
+            loss = self.train_step(images, labels)
+            meter.update(self.reduce_loss(loss), images.size(0))
+            if bar is not None:
+                bar.update(1)
+                if (index + 1) % max(a.log_interval, 1) == 0:
+                    bar.set_description(f"Epoch: {epoch}; Loss {meter.val:.4f}|({meter.avg:.4f})")
+        if bar is not None:
+            bar.set_description(f"Epoch: {epoch}; Loss {meter.val:.4f}|({meter.avg:.4f})")
+            bar.close()
+        return meter.avg if meter.count else float("nan")
+
+    @torch.no_grad()
+    def val_epoch(self, epoch: int) -> float:
+        a = self.args
+        self.net.eval()
+        acc = AccuracyCounter(self.dev)
+        n_real = len(self.val_ds)
+        rank, world = self.ctx.rank, self.ctx.world_size
+        for index, data in enumerate(self._loader(self.val_loader)):
+            if a.val_steps is not None and index >= a.val_steps:
+                break
+            images, labels = data["image"], data["label"]
+            if images.device != self.dev:
+                images = images.to(self.dev, non_blocking=True)
+                labels = labels.to(self.dev, non_blocking=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.autocast):
+                out = self.net(images)
+            valid = None
+            if a.exact_val:
+                # sampler index i*world+rank >= len(dataset) is DistributedSampler padding
+                pos = index * a.val_batchsize + torch.arange(labels.numel(), device=self.dev)
+                valid = (pos * world + rank) < n_real
+            acc.update(out.float(), labels, valid)
+        counts = torch.stack([acc.correct, acc.total]).to(torch.float64)
+        if world > 1:
+            dist.all_reduce(counts)
+        comb = float(counts[0] / counts[1].clamp(min=1) * 100.0)
+        if self.ctx.is_main:
+            print(f"Validation Accuracy {comb}", flush=True)
+        return comb
+
+    # ------------------------------------------------------------------ ckpt
+    def ckpt_path(self, which: str) -> str:
+        return os.path.join(self.args.ckpt_dir, self.name, which)
+
+    def maybe_resume(self):
+        path = resolve_resume(self.args.ckpt_dir, self.name, self.args.resume)
+        if path is None:
+            return
+        which = os.path.basename(path)
+        if self.ctx.is_main:
+            print(f"Loading Checkpoint from {which}", flush=True)
+        ck = load_checkpoint(path)
+        load_model_state(self.model, ck["state_dict"])
+        self.start_epoch = int(ck["epoch"]) + 1
+        self.best_score = float(ck["best_score"])
+        if "optimizer" in ck:
+            self.optimizer.load_state_dict(ck["optimizer"])
+        if "scheduler" in ck:
+            self.scheduler.load_state_dict(ck["scheduler"])
+        if self.ctx.is_main:
+            print(f"Loaded Checkpoint: {which}, with epoch {ck['epoch']} and best score {self.best_score}",
+                  flush=True)
+
+    def fit(self):
+        a = self.args
+        self.maybe_resume()
+        log = JsonlLogger(a.metrics_file, self.ctx.is_main)
+        history = []
+        for epoch in range(self.start_epoch, a.epochs):
+            self.train_sampler.set_epoch(epoch)
+            train_loss = self.train_epoch(epoch)
+            self.scheduler.step()
+            if self.dev.type == "cuda":
+                torch.cuda.empty_cache()
+            val_acc = self.val_epoch(epoch)
+            improved = val_acc > self.best_score
+            if improved:
+                self.best_score = val_acc
+            if self.ctx.is_main:
+                if improved:
+                    print(f"Model improved to {val_acc} so storing checkpoint", flush=True)
+                    save_checkpoint(self.ckpt_path(BEST), self.model, epoch, val_acc)
+                if a.latest_every and epoch % a.latest_every == 0:
+                    save_checkpoint(self.ckpt_path(LATEST), self.model, epoch, self.best_score,
+                                    self.optimizer, self.scheduler)
+            rec = dict(epoch=epoch, train_loss=train_loss, val_acc=val_acc, best=self.best_score,
+                       lr=self.optimizer.param_groups[0]["lr"])
+            history.append(rec)
+            log.log(**rec)
+            if not math.isfinite(train_loss):
+                raise FloatingPointError(f"non-finite training loss at epoch {epoch}")
+        return history

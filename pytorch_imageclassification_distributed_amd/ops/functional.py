@@ -1,0 +1,216 @@
+"""Functional op layer the model zoo is written against.
+
+Every model in ``models/`` expresses its forward pass with the handful of
+primitives below (``conv_bn_act``, pooling, ``linear``, ``mlp``, ``se_gate``,
+``drop_connect`` ...).  Each primitive has exactly two implementations:
+
+* the **HIP path** (``ops/hip.py``): hand-written gfx950 kernels from
+  ``csrc/*.hip`` operating on channels-last (NHWC) bf16 activations with fp32
+  statistics/master weights.  Used for every CUDA (=HIP) tensor.
+* the **reference path**: plain ATen ops in the module's own dtype.  Used on
+  CPU (BASELINE config 1, the unit-test oracle) and, when explicitly requested
+  with ``set_backend('torch')``, on the GPU to measure the reference stack
+  (PyTorch DDP + SyncBatchNorm + MIOpen) on the same box.
+
+This mirrors what the reference computes implicitly through torchvision /
+efficientnet_pytorch modules (reference nn/classifier.py:11-37) but lets the
+GPU path fuse conv -> BN -> (+residual) -> activation.
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import torch
+import torch.nn.functional as F
+
+_BACKEND = os.environ.get("IMGCLS_BACKEND", "auto")  # auto | hip | torch
+
+
+def set_backend(name: str) -> None:
+    global _BACKEND
+    if name not in ("auto", "hip", "torch"):
+        raise ValueError(f"unknown backend {name!r}")
+    _BACKEND = name
+
+
+def get_backend() -> str:
+    return _BACKEND
+
+
+def use_hip(x: torch.Tensor) -> bool:
+    """HIP kernels run for every GPU tensor unless the torch backend is forced."""
+    if not x.is_cuda:
+        if _BACKEND == "hip":
+            raise RuntimeError("backend 'hip' requested for a CPU tensor")
+        return False
+    return _BACKEND != "torch"
+
+
+def _hip():
+    from . import hip  # noqa: WPS433  (lazy: loads the native extension)
+    return hip
+
+
+# ---------------------------------------------------------------------------
+# padding helpers
+# ---------------------------------------------------------------------------
+def conv_padding(conv, h: int, w: int):
+    """Return (pad_top, pad_bottom, pad_left, pad_right) for ``conv``.
+
+    ``conv.tf_same`` (set by the EfficientNet builder) selects TensorFlow
+    "SAME" padding computed from the actual input size, as efficientnet_pytorch's
+    Conv2dStaticSamePadding does for its configured image size.
+    """
+    kh, kw = conv.kernel_size
+    sh, sw = conv.stride
+    dh, dw = conv.dilation
+    if getattr(conv, "tf_same", False):
+        oh, ow = math.ceil(h / sh), math.ceil(w / sw)
+        ph = max((oh - 1) * sh + (kh - 1) * dh + 1 - h, 0)
+        pw = max((ow - 1) * sw + (kw - 1) * dw + 1 - w, 0)
+        return ph // 2, ph - ph // 2, pw // 2, pw - pw // 2
+    ph, pw = conv.padding
+    return ph, ph, pw, pw
+
+
+def _torch_conv(x, conv):
+    pt, pb, pl, pr = conv_padding(conv, x.shape[-2], x.shape[-1])
+    if (pt, pl) != (pb, pr):
+        x = F.pad(x, (pl, pr, pt, pb))
+        return F.conv2d(x, conv.weight, conv.bias, conv.stride, 0, conv.dilation, conv.groups)
+    return F.conv2d(x, conv.weight, conv.bias, conv.stride, (pt, pl), conv.dilation, conv.groups)
+
+
+def _act(x, act):
+    if act is None:
+        return x
+    if act == "relu":
+        return F.relu(x)
+    if act == "silu":
+        return F.silu(x)
+    raise ValueError(act)
+
+
+def _torch_bn(x, bn):
+    sync = getattr(bn, "sync_group", None)
+    if sync is not None and bn.training:
+        from ..parallel.syncbn import sync_batch_norm
+        return sync_batch_norm(x, bn, sync)
+    return bn(x)
+
+
+# ---------------------------------------------------------------------------
+# primitives
+# ---------------------------------------------------------------------------
+def conv_bn_act(x, conv, bn, act="relu", residual=None):
+    """act(bn(conv(x)) [+ residual]).
+
+    Reference equivalents: torchvision ``BasicConv2d`` (conv -> BN -> ReLU),
+    ResNet ``Bottleneck``/``BasicBlock`` tails (BN -> +identity -> ReLU) and
+    efficientnet_pytorch ``MBConvBlock`` (conv -> BN -> swish).
+    """
+    if use_hip(x):
+        return _hip().conv_bn_act(x, conv, bn, act, residual)
+    y = _torch_bn(_torch_conv(x, conv), bn)
+    if residual is not None:
+        y = y + residual
+    return _act(y, act)
+
+
+def conv(x, conv_mod):
+    """Plain convolution (with optional bias), no normalisation."""
+    if use_hip(x):
+        return _hip().conv(x, conv_mod)
+    return _torch_conv(x, conv_mod)
+
+
+def max_pool2d(x, kernel_size, stride, padding=0):
+    if use_hip(x):
+        return _hip().max_pool2d(x, kernel_size, stride, padding)
+    return F.max_pool2d(x, kernel_size, stride, padding)
+
+
+def avg_pool2d(x, kernel_size, stride, padding=0):
+    """count_include_pad=True semantics (torch default, used by torchvision Inception)."""
+    if use_hip(x):
+        return _hip().avg_pool2d(x, kernel_size, stride, padding)
+    return F.avg_pool2d(x, kernel_size, stride, padding)
+
+
+def global_avg_pool(x):
+    """adaptive_avg_pool2d(x, 1) + flatten -> [N, C]."""
+    if use_hip(x):
+        return _hip().global_avg_pool(x)
+    return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+
+
+def linear(x, lin, act=None):
+    if use_hip(x):
+        return _hip().linear(x, lin, act)
+    return _act(F.linear(x, lin.weight, lin.bias), act)
+
+
+def mlp(x, seq):
+    """The reference classifier head: Linear/ReLU stack (nn/classifier.py:26-34)."""
+    if use_hip(x):
+        return _hip().mlp(x, seq)
+    return seq(x)
+
+
+def dropout(x, p, training):
+    if p == 0.0 or not training:
+        return x
+    if use_hip(x):
+        return _hip().dropout(x, p)
+    return F.dropout(x, p, True)
+
+
+def cat_channels(xs):
+    if use_hip(xs[0]):
+        return _hip().cat_channels(xs)
+    return torch.cat(xs, 1)
+
+
+def add(x, y):
+    if use_hip(x):
+        return _hip().add(x, y)
+    return x + y
+
+
+def se_gate(x, se_reduce, se_expand):
+    """Squeeze-and-excitation: x * sigmoid(expand(swish(reduce(avgpool(x)))))."""
+    if use_hip(x):
+        return _hip().se_gate(x, se_reduce, se_expand)
+    s = F.adaptive_avg_pool2d(x, 1)
+    s = se_expand(F.silu(se_reduce(s)))
+    return torch.sigmoid(s) * x
+
+
+def drop_connect(x, p, training):
+    """efficientnet_pytorch utils.drop_connect: per-sample stochastic depth."""
+    if not training or p == 0.0:
+        return x
+    if use_hip(x):
+        return _hip().drop_connect(x, p)
+    keep = 1.0 - p
+    mask = torch.floor(keep + torch.rand([x.shape[0], 1, 1, 1], dtype=x.dtype, device=x.device))
+    return x / keep * mask
+
+
+def cross_entropy(logits, labels, weight=None):
+    """CrossEntropyLoss(weight) with mean reduction: sum_i w_yi*nll_i / sum_i w_yi
+    (reference train.py:157-158)."""
+    if use_hip(logits):
+        return _hip().cross_entropy(logits, labels, weight)
+    return F.cross_entropy(logits.float(), labels, weight=weight)
+
+
+def prepare_input(x):
+    """Move/convert a batch to the layout the active path expects.
+
+    HIP path: channels-last bf16 (NHWC in memory).  Reference path: unchanged.
+    """
+    if use_hip(x):
+        return _hip().prepare_input(x)
+    return x

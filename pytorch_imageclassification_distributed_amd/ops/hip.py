@@ -1,0 +1,854 @@
+"""HIP path of the functional op layer: autograd Functions over the gfx950 kernels.
+
+Tensor conventions on this path:
+* activations: logical NCHW tensors in ``torch.channels_last`` memory format,
+  bf16 - i.e. NHWC in memory, which is what every kernel in ``csrc/`` reads;
+* conv weights: fp32 master parameters in channels_last (KRSC in memory); the
+  kernels read a bf16 *shadow* of each weight that the fused Adam kernel
+  rewrites after every step (see ``weight_bf16`` / ``engine.optim``);
+* classifier features / logits: fp32 ``[N, C]``;
+* BatchNorm statistics: fp32 partial sums produced by the conv epilogue,
+  reduced in fp64; SyncBN exchanges the fp64 sums with one RCCL all-reduce.
+
+Nothing here falls back to ATen math: a missing extension raises.
+"""
+from __future__ import annotations
+
+import math
+import weakref
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .. import _ext
+
+C = _ext.load()
+
+CL = torch.channels_last
+BF16 = torch.bfloat16
+ACT = {None: 0, "relu": 1, "silu": 2}
+G_STATS = 64  # rotating partial rows for BN statistics atomics
+
+
+# ---------------------------------------------------------------------------
+# per-device workspaces
+# ---------------------------------------------------------------------------
+class _Workspace:
+    def __init__(self, dev):
+        self.dev = dev
+        self.stats = torch.zeros(0, dtype=torch.float32, device=dev)
+
+    def stats_buf(self, c: int) -> torch.Tensor:
+        need = G_STATS * 2 * c
+        if self.stats.numel() < need:
+            # consumers re-zero what they read, so a fresh buffer only needs one memset
+            self.stats = torch.zeros(max(need, G_STATS * 2 * 2048), dtype=torch.float32, device=self.dev)
+        return self.stats
+
+
+_WS: dict = {}
+
+
+def ws(dev) -> _Workspace:
+    key = (dev.type, dev.index)
+    w = _WS.get(key)
+    if w is None:
+        w = _WS[key] = _Workspace(dev)
+    return w
+
+
+# ---------------------------------------------------------------------------
+# bf16 weight shadows
+# ---------------------------------------------------------------------------
+class _Shadow:
+    __slots__ = ("t", "ptr", "version", "fused", "ref")
+
+
+_SHADOWS: dict = {}
+_SHADOW_GEN = [0]
+
+
+def _krsc_compatible(p: torch.Tensor) -> bool:
+    if p.dim() != 4:
+        return p.is_contiguous()
+    return p.is_contiguous(memory_format=CL)
+
+
+def weight_bf16(p: torch.Tensor) -> torch.Tensor:
+    """bf16 copy of ``p`` in KRSC order ([Co][kh][kw][Ci] for conv weights).
+
+    Refreshed when ``p`` changed outside the fused optimizer (version counter or
+    storage moved); the fused Adam kernel keeps registered shadows current.
+    """
+    key = id(p)
+    e = _SHADOWS.get(key)
+    if e is not None and e.ref() is p and e.ptr == p.data_ptr() and (e.fused or e.version == p._version):
+        return e.t
+    if e is None or e.ref() is not p or e.t.numel() != p.numel():
+        e = _Shadow()
+        e.t = torch.empty(p.numel(), dtype=BF16, device=p.device)
+        e.fused = False
+        e.ref = weakref.ref(p)
+        _SHADOWS[key] = e
+        _SHADOW_GEN[0] += 1
+    src = p.detach()
+    if not _krsc_compatible(src):
+        src = src.permute(0, 2, 3, 1).contiguous() if src.dim() == 4 else src.contiguous()
+    C.cast_bf16(src.reshape(-1) if src.is_contiguous() else src.contiguous().reshape(-1), e.t)
+    e.ptr = p.data_ptr()
+    e.version = p._version
+    return e.t
+
+
+def shadow_for_optimizer(p: torch.Tensor):
+    """Shadow tensor the Adam kernel should rewrite for ``p`` (or None)."""
+    e = _SHADOWS.get(id(p))
+    if e is None or e.ref() is not p or not _krsc_compatible(p):
+        return None
+    e.fused = True
+    return e.t
+
+
+def shadow_generation() -> int:
+    return _SHADOW_GEN[0]
+
+
+def ensure_channels_last_weight(conv) -> None:
+    w = conv.weight
+    if w.dim() == 4 and not w.is_contiguous(memory_format=CL):
+        w.data = w.data.contiguous(memory_format=CL)
+
+
+# ---------------------------------------------------------------------------
+# helpers
+# ---------------------------------------------------------------------------
+def _cl(x: torch.Tensor) -> torch.Tensor:
+    return x if x.is_contiguous(memory_format=CL) else x.contiguous(memory_format=CL)
+
+
+def _empty_cl(n, c, h, w, dev, dtype=BF16):
+    return torch.empty((n, c, h, w), dtype=dtype, device=dev, memory_format=CL)
+
+
+def _pad_tuple(conv, h, w):
+    from .functional import conv_padding
+    return conv_padding(conv, h, w)
+
+
+def _sync_group(bn):
+    g = getattr(bn, "sync_group", None)
+    if g is None or not dist.is_initialized() or dist.get_world_size(g) == 1:
+        return None
+    return g
+
+
+# ---------------------------------------------------------------------------
+# convolution (implicit GEMM on MFMA)
+# ---------------------------------------------------------------------------
+class ConvGeom:
+    __slots__ = ("N", "Ci", "Cx", "H", "W", "Co", "kh", "kw", "sh", "sw", "dil", "pt", "pb", "pl", "pr",
+                 "OH", "OW", "T")
+
+    def __init__(self, x, conv):
+        self.N, self.Cx, self.H, self.W = x.shape
+        self.Co, self.Ci, self.kh, self.kw = conv.weight.shape
+        self.sh, self.sw = conv.stride
+        self.dil = conv.dilation[0]
+        if conv.dilation[0] != conv.dilation[1]:
+            raise NotImplementedError("anisotropic dilation")
+        self.pt, self.pb, self.pl, self.pr = _pad_tuple(conv, self.H, self.W)
+        self.OH = (self.H + self.pt + self.pb - self.dil * (self.kh - 1) - 1) // self.sh + 1
+        self.OW = (self.W + self.pl + self.pr - self.dil * (self.kw - 1) - 1) // self.sw + 1
+        self.T = self.kh * self.kw
+
+
+def _fwd_taps(g: ConvGeom):
+    dh, dw, tb = [], [], []
+    for r in range(g.kh):
+        for c in range(g.kw):
+            dh.append(r * g.dil - g.pt)
+            dw.append(c * g.dil - g.pl)
+            tb.append(r * g.kw + c)
+    return dh, dw, tb
+
+
+def _dgrad_phases(g: ConvGeom):
+    """Sub-pixel decomposition of the transposed convolution (one GEMM per phase)."""
+    out = []
+    for ph in range(g.sh):
+        for pw in range(g.sw):
+            dh, dw, tb = [], [], []
+            for r in range(g.kh):
+                a = ph + g.pt - r * g.dil
+                if a % g.sh:
+                    continue
+                for c in range(g.kw):
+                    b = pw + g.pl - c * g.dil
+                    if b % g.sw:
+                        continue
+                    dh.append(a // g.sh)
+                    dw.append(b // g.sw)
+                    tb.append(r * g.kw + c)
+            gh = (g.H - ph + g.sh - 1) // g.sh
+            gw = (g.W - pw + g.sw - 1) // g.sw
+            out.append((ph, pw, gh, gw, dh, dw, tb))
+    return out
+
+
+def _weight_for_input(w_param, cx):
+    """bf16 KRSC weight, zero-padded along Ci when the input carries padded channels (stem)."""
+    wb = weight_bf16(w_param)
+    co, ci, kh, kw = w_param.shape
+    if cx == ci:
+        return wb
+    out = torch.empty(co * kh * kw * cx, dtype=BF16, device=w_param.device)
+    C.weight_pad(wb, out, co * kh * kw, ci, cx)
+    return out
+
+
+def conv_forward_raw(x, w_param, g: ConvGeom, stats=None, bias=None, out=None, c_off=0):
+    dev = x.device
+    wb = _weight_for_input(w_param, g.Cx)
+    y = out if out is not None else _empty_cl(g.N, g.Co, g.OH, g.OW, dev)
+    ldc = y.shape[1]
+    dh, dw, tb = _fwd_taps(g)
+    if g.sh != g.sw:
+        raise NotImplementedError("anisotropic stride")
+    C.conv_gemm(x, wb, y, stats, bias, g.N * g.OH * g.OW, g.Co, g.T * g.Cx, g.Cx, g.OH, g.OW, g.H, g.W,
+                g.sh, g.T * g.Cx, g.OH, g.OW, 1, 0, 0, ldc, c_off, dh, dw, tb, G_STATS)
+    return y
+
+
+def conv_dgrad_raw(dy, w_param, g: ConvGeom):
+    dev = dy.device
+    wb = weight_bf16(w_param)
+    wt = torch.empty(g.Ci * g.T * g.Co, dtype=BF16, device=dev)
+    C.weight_t(wb, wt, g.Co, g.T, g.Ci)
+    dx = _empty_cl(g.N, g.Ci, g.H, g.W, dev)
+    for ph, pw, gh, gw, dh, dw, tb in _dgrad_phases(g):
+        if gh <= 0 or gw <= 0:
+            continue
+        C.conv_gemm(dy, wt, dx, None, None, g.N * gh * gw, g.Ci, len(tb) * g.Co, g.Co, gh, gw, g.OH, g.OW,
+                    1, g.T * g.Co, g.H, g.W, g.sh, ph, pw, g.Ci, 0, dh, dw, tb, 1)
+    return dx
+
+
+def _wgrad_split(m, tiles):
+    splits = max(1, min(-(-1024 // max(tiles, 1)), -(-m // 512)))
+    kps = -(-m // splits)
+    kps = -(-kps // 64) * 64
+    splits = -(-m // kps)
+    return kps, splits
+
+
+def conv_wgrad_raw(dy, x, w_param, g: ConvGeom):
+    dev = dy.device
+    m = g.N * g.OH * g.OW
+    ntot = g.T * g.Cx
+    tiles = (-(-g.Co // (64 if g.Co <= 64 else 128))) * (-(-ntot // 128))
+    kps, splits = _wgrad_split(m, tiles)
+    if g.Cx == g.Ci:
+        dw = torch.zeros_like(w_param, memory_format=CL)
+        C.conv_wgrad(dy, x, dw, m, g.Co, g.Cx, ntot, g.OH, g.OW, g.H, g.W, g.sh, g.sw, g.pt, g.pl,
+                     g.dil, g.dil, g.kw, kps, splits)
+        return dw
+    full = torch.zeros(g.Co * ntot, dtype=torch.float32, device=dev)
+    C.conv_wgrad(dy, x, full, m, g.Co, g.Cx, ntot, g.OH, g.OW, g.H, g.W, g.sh, g.sw, g.pt, g.pl,
+                 g.dil, g.dil, g.kw, kps, splits)
+    dw = torch.empty_like(w_param, memory_format=CL)
+    C.grad_unpad(full, dw, g.Co * g.T, g.Cx, g.Ci)
+    return dw
+
+
+class ConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, conv, want_stats):
+        g = ConvGeom(x, conv)
+        stats = ws(x.device).stats_buf(g.Co) if want_stats else None
+        y = conv_forward_raw(x, w, g, stats=stats)
+        ctx.g = g
+        ctx.save_for_backward(x, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        g = ctx.g
+        dy = _cl(dy)
+        dx = conv_dgrad_raw(dy, w, g) if ctx.needs_input_grad[0] else None
+        dw = conv_wgrad_raw(dy, x, w, g) if ctx.needs_input_grad[1] else None
+        return dx, dw, None, None
+
+
+# ---------------------------------------------------------------------------
+# depthwise convolution (EfficientNet)
+# ---------------------------------------------------------------------------
+class DwConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, conv):
+        g = ConvGeom(x, conv)
+        wt = torch.empty(g.T * g.Co, dtype=BF16, device=x.device)
+        C.weight_t(weight_bf16(w), wt, g.Co, g.T, 1)
+        y = _empty_cl(g.N, g.Co, g.OH, g.OW, x.device)
+        C.dw_fwd(x, wt, y, None, g.N, g.H, g.W, g.Co, g.OH, g.OW, g.kh, g.kw, g.sh, g.sw, g.pt, g.pl)
+        ctx.g = g
+        ctx.save_for_backward(x, w, wt)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, wt = ctx.saved_tensors
+        g = ctx.g
+        dy = _cl(dy)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = _empty_cl(g.N, g.Co, g.H, g.W, x.device)
+            C.dw_dgrad(dy, wt, dx, g.N, g.H, g.W, g.Co, g.OH, g.OW, g.kh, g.kw, g.sh, g.sw, g.pt, g.pl)
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = torch.zeros_like(w)
+            C.dw_wgrad(dy, x, dw, g.N, g.H, g.W, g.Co, g.OH, g.OW, g.kh, g.kw, g.sh, g.sw, g.pt, g.pl)
+        return dx, dw, None
+
+
+# ---------------------------------------------------------------------------
+# BatchNorm (+ residual) (+ activation)
+# ---------------------------------------------------------------------------
+class BNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, gamma, beta, res, bn, act, stats_ready):
+        dev = y.device
+        n, c, h, w = y.shape
+        rows = n * h * w
+        a = ACT[act]
+        coef = torch.empty(4 * c, dtype=torch.float32, device=dev)
+        group = None
+        count_t = None
+        if bn.training:
+            part = ws(dev).stats_buf(c)
+            if not stats_ready:
+                C.bn_stats(y, rows, c, part, G_STATS)
+            group = _sync_group(bn)
+            sums = torch.empty(2 * c + 1, dtype=torch.float64, device=dev)
+            C.bn_partials(part, G_STATS, c, sums, None, None)
+            if group is not None:
+                sums[2 * c:].fill_(float(rows))
+                dist.all_reduce(sums, group=group)
+                count_t = sums[2 * c:]
+            mom = bn.momentum if bn.momentum is not None else 0.1
+            track = bn.track_running_stats and bn.running_mean is not None
+            C.bn_finalize(sums, count_t, float(rows), gamma, beta,
+                          bn.running_mean if track else None, bn.running_var if track else None,
+                          bn.num_batches_tracked if track else None, mom, bn.eps, c, coef)
+        else:
+            if stats_ready:
+                raise RuntimeError("eval-mode BN received fused statistics")
+            C.bn_eval_coef(gamma, beta, bn.running_mean, bn.running_var, bn.eps, c, coef)
+        out = _empty_cl(n, c, h, w, dev)
+        C.bn_apply(y, coef, res, out, rows, c, c, 0, a)
+        ctx.act, ctx.group, ctx.rows, ctx.c = a, group, rows, c
+        ctx.count_t = count_t
+        ctx.has_res = res is not None
+        ctx.save_for_backward(y, coef, res if res is not None else y)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        y, coef, res = ctx.saved_tensors
+        res = res if ctx.has_res else None
+        dev = y.device
+        c, rows = ctx.c, ctx.rows
+        g = _cl(gout)
+        part = ws(dev).stats_buf(c)
+        dz = torch.empty_like(y, memory_format=CL) if ctx.has_res else None
+        C.bn_bwd_reduce(g, y, coef, res, dz, rows, c, ctx.act, part, G_STATS)
+        sums = torch.empty(2 * c, dtype=torch.float64, device=dev)
+        dgamma = torch.empty(c, dtype=torch.float32, device=dev)
+        dbeta = torch.empty(c, dtype=torch.float32, device=dev)
+        C.bn_partials(part, G_STATS, c, sums, dgamma, dbeta)
+        if ctx.group is not None:
+            dist.all_reduce(sums, group=ctx.group)
+        k = torch.empty(2 * c, dtype=torch.float32, device=dev)
+        C.bn_bwd_k(sums, ctx.count_t, float(rows), c, k)
+        dy = torch.empty_like(y, memory_format=CL)
+        C.bn_bwd_elemt(None if dz is not None else g, y, coef, k, res, dz, dy, rows, c, ctx.act)
+        return dy, dgamma, dbeta, dz, None, None, None
+
+
+def conv_bn_act(x, conv, bn, act, residual):
+    x = _cl(x)
+    if residual is not None:
+        residual = _cl(residual)
+    ensure_channels_last_weight(conv)
+    depthwise = conv.groups > 1
+    if depthwise:
+        if not (conv.groups == conv.in_channels == conv.out_channels):
+            raise NotImplementedError("grouped (non-depthwise) convolution")
+        y = DwConvFn.apply(x, conv.weight, conv)
+        ready = False
+    else:
+        if conv.groups != 1:
+            raise NotImplementedError("grouped convolution")
+        y = ConvFn.apply(x, conv.weight, conv, bn.training)
+        ready = bn.training
+    if conv.bias is not None:
+        raise NotImplementedError("conv bias before BatchNorm")
+    return BNActFn.apply(y, bn.weight, bn.bias, residual, bn, act, ready)
+
+
+class ConvBiasFn(torch.autograd.Function):
+    """Plain convolution with optional bias (no BN)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, conv):
+        g = ConvGeom(x, conv)
+        y = conv_forward_raw(x, w, g, bias=b)
+        ctx.g = g
+        ctx.has_b = b is not None
+        ctx.save_for_backward(x, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        g = ctx.g
+        dy = _cl(dy)
+        dx = conv_dgrad_raw(dy, w, g) if ctx.needs_input_grad[0] else None
+        dw = conv_wgrad_raw(dy, x, w, g) if ctx.needs_input_grad[1] else None
+        db = None
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            part = ws(dy.device).stats_buf(g.Co)
+            C.bn_stats(dy, g.N * g.OH * g.OW, g.Co, part, G_STATS)
+            sums = torch.empty(2 * g.Co, dtype=torch.float64, device=dy.device)
+            db = torch.empty(g.Co, dtype=torch.float32, device=dy.device)
+            C.bn_partials(part, G_STATS, g.Co, sums, None, db)
+        return dx, dw, db, None
+
+
+def conv(x, conv_mod):
+    ensure_channels_last_weight(conv_mod)
+    if conv_mod.groups != 1:
+        raise NotImplementedError("grouped convolution without BN")
+    return ConvBiasFn.apply(_cl(x), conv_mod.weight, conv_mod.bias, conv_mod)
+
+
+# ---------------------------------------------------------------------------
+# pooling
+# ---------------------------------------------------------------------------
+def _pool_args(k, s, p):
+    k = (k, k) if isinstance(k, int) else tuple(k)
+    s = (s, s) if isinstance(s, int) else tuple(s)
+    p = (p, p) if isinstance(p, int) else tuple(p)
+    return k, s, p
+
+
+class MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        n, c, h, w = x.shape
+        oh = (h + 2 * p[0] - k[0]) // s[0] + 1
+        ow = (w + 2 * p[1] - k[1]) // s[1] + 1
+        y = _empty_cl(n, c, oh, ow, x.device)
+        idx = torch.empty((n, oh, ow, c), dtype=torch.uint8, device=x.device)
+        C.maxpool_fwd(x, y, idx, n, h, w, c, oh, ow, k[0], k[1], s[0], s[1], p[0], p[1])
+        ctx.geo = (n, h, w, c, oh, ow, k, s, p)
+        ctx.save_for_backward(idx)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        n, h, w, c, oh, ow, k, s, p = ctx.geo
+        dx = _empty_cl(n, c, h, w, dy.device)
+        C.maxpool_bwd(_cl(dy), idx, dx, n, h, w, c, oh, ow, k[0], k[1], s[0], s[1], p[0], p[1])
+        return dx, None, None, None
+
+
+def max_pool2d(x, kernel_size, stride, padding=0):
+    k, s, p = _pool_args(kernel_size, stride, padding)
+    return MaxPoolFn.apply(_cl(x), k, s, p)
+
+
+class AvgPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        n, c, h, w = x.shape
+        oh = (h + 2 * p[0] - k[0]) // s[0] + 1
+        ow = (w + 2 * p[1] - k[1]) // s[1] + 1
+        y = _empty_cl(n, c, oh, ow, x.device)
+        C.avgpool_fwd(x, y, n, h, w, c, oh, ow, k[0], k[1], s[0], s[1], p[0], p[1])
+        ctx.geo = (n, h, w, c, oh, ow, k, s, p)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        n, h, w, c, oh, ow, k, s, p = ctx.geo
+        dx = _empty_cl(n, c, h, w, dy.device)
+        C.avgpool_bwd(_cl(dy), dx, n, h, w, c, oh, ow, k[0], k[1], s[0], s[1], p[0], p[1])
+        return dx, None, None, None
+
+
+def avg_pool2d(x, kernel_size, stride, padding=0):
+    k, s, p = _pool_args(kernel_size, stride, padding)
+    return AvgPoolFn.apply(_cl(x), k, s, p)
+
+
+class GapFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        n, c, h, w = x.shape
+        y = torch.empty((n, c), dtype=torch.float32, device=x.device)
+        C.gap_fwd(x, y, n, h * w, c)
+        ctx.geo = (n, c, h, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        n, c, h, w = ctx.geo
+        dx = _empty_cl(n, c, h, w, dy.device)
+        C.gap_bwd(dy.contiguous().float(), dx, n, h * w, c)
+        return dx
+
+
+def global_avg_pool(x):
+    return GapFn.apply(_cl(x))
+
+
+# ---------------------------------------------------------------------------
+# classifier head (fp32)
+# ---------------------------------------------------------------------------
+def _mm(a, b, out, m, n, k, sam, sak, sbk, sbn, bias=None, mask=None, smm=0, smk=0, relu=False, acc=False):
+    C.sgemm(a, b, out, bias, mask, m, n, k, sam, sak, sbk, sbn, n if out.dim() == 2 else out.stride(0),
+            smm, smk, relu, acc)
+
+
+class MlpFn(torch.autograd.Function):
+    """Stack of Linear layers, ReLU after every layer whose flag is set."""
+
+    @staticmethod
+    def forward(ctx, x, relus, *wb):
+        x = x.contiguous().float()
+        acts = [x]
+        h = x
+        for i, r in enumerate(relus):
+            w, b = wb[2 * i], wb[2 * i + 1]
+            nout, nin = w.shape
+            y = torch.empty((h.shape[0], nout), dtype=torch.float32, device=h.device)
+            _mm(h, w.contiguous(), y, h.shape[0], nout, nin, nin, 1, 1, nin, bias=b, relu=r)
+            acts.append(y)
+            h = y
+        ctx.relus = relus
+        ctx.nb = [b is not None for b in wb[1::2]]
+        ctx.save_for_backward(*acts, *[w for w in wb[0::2]])
+        return h
+
+    @staticmethod
+    def backward(ctx, gout):
+        saved = ctx.saved_tensors
+        nl = len(ctx.relus)
+        acts, ws_ = saved[:nl + 1], saved[nl + 1:]
+        g = gout.contiguous().float()
+        grads = [None] * (2 * nl)
+        mb = g.shape[0]
+        for i in reversed(range(nl)):
+            w = ws_[i].contiguous()
+            nout, nin = w.shape
+            xin, yout = acts[i], acts[i + 1]
+            mask = yout if ctx.relus[i] else None
+            dw = torch.empty((nout, nin), dtype=torch.float32, device=g.device)
+            # dW[o][f] = sum_b g[b][o] * x[b][f]   (A(m=o,k=b) = g[b][o])
+            _mm(g, xin, dw, nout, nin, mb, 1, nout, nin, 1, mask=mask, smm=1, smk=nout)
+            grads[2 * i] = dw
+            if ctx.nb[i]:
+                db = torch.empty(nout, dtype=torch.float32, device=g.device)
+                C.colsum(g, mask, db, mb, nout, nout, False)
+                grads[2 * i + 1] = db
+            if i > 0 or ctx.needs_input_grad[0]:
+                dx = torch.empty((mb, nin), dtype=torch.float32, device=g.device)
+                # dX[b][f] = sum_o g[b][o] * W[o][f]
+                _mm(g, w, dx, mb, nin, nout, nout, 1, nin, 1, mask=mask, smm=nout, smk=1)
+                g = dx
+        return (g if ctx.needs_input_grad[0] else None, None, *grads)
+
+
+def mlp(x, seq):
+    import torch.nn as nn
+    layers = list(seq) if isinstance(seq, nn.Sequential) else [seq]
+    lins, relus = [], []
+    for m in layers:
+        if isinstance(m, nn.Linear):
+            lins.append(m)
+            relus.append(False)
+        elif isinstance(m, nn.ReLU):
+            relus[-1] = True
+        else:
+            raise NotImplementedError(f"head layer {type(m).__name__}")
+    wb = []
+    for m in lins:
+        wb += [m.weight, m.bias]
+    return MlpFn.apply(x, tuple(relus), *wb)
+
+
+def linear(x, lin, act=None):
+    if act not in (None, "relu"):
+        raise NotImplementedError(act)
+    return MlpFn.apply(x, (act == "relu",), lin.weight, lin.bias)
+
+
+class CrossEntropyFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, weight):
+        x = logits.contiguous().float()
+        b, c = x.shape
+        prob = torch.empty_like(x)
+        out = torch.empty(2, dtype=torch.float32, device=x.device)
+        lab = labels.contiguous().long()
+        C.ce_fwd(x, lab, weight, prob, out, b, c)
+        ctx.save_for_backward(prob, lab, out, weight if weight is not None else out)
+        ctx.has_w = weight is not None
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, gout):
+        prob, lab, out, w = ctx.saved_tensors
+        b, c = prob.shape
+        dx = torch.empty_like(prob)
+        C.ce_bwd(prob, lab, w if ctx.has_w else None, out, gout.reshape(1).float().contiguous(), dx, b, c)
+        return dx, None, None
+
+
+def cross_entropy(logits, labels, weight=None):
+    return CrossEntropyFn.apply(logits, labels, weight)
+
+
+# ---------------------------------------------------------------------------
+# misc
+# ---------------------------------------------------------------------------
+_AFFINE_CACHE: dict = {}
+
+
+def prepare_input(x, scale=None, shift=None):
+    """fp32 NCHW batch -> bf16 NHWC padded to a multiple of 8 channels (one kernel)."""
+    if x.dtype == BF16 and x.is_contiguous(memory_format=CL) and x.shape[1] % 8 == 0:
+        return x
+    x = x.contiguous().float()
+    n, c, h, w = x.shape
+    cp = (c + 7) // 8 * 8
+    y = _empty_cl(n, cp, h, w, x.device)
+    sc = sh = None
+    if scale is not None:
+        key = (x.device, tuple(scale), tuple(shift))
+        if key not in _AFFINE_CACHE:
+            _AFFINE_CACHE[key] = (torch.tensor(scale, dtype=torch.float32, device=x.device),
+                                  torch.tensor(shift, dtype=torch.float32, device=x.device))
+        sc, sh = _AFFINE_CACHE[key]
+    C.prepare_input(x, y, n, c, h * w, cp, sc, sh)
+    return y
+
+
+class CatFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, *xs):
+        n, _, h, w = xs[0].shape
+        cs = [t.shape[1] for t in xs]
+        tot = sum(cs)
+        y = _empty_cl(n, tot, h, w, xs[0].device)
+        off = 0
+        rows = n * h * w
+        for t, c in zip(xs, cs):
+            C.copy_channels(t, c, 0, y, tot, off, rows, c)
+            off += c
+        ctx.cs = cs
+        ctx.geo = (n, h, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        gy = _cl(gy)
+        n, h, w = ctx.geo
+        tot = sum(ctx.cs)
+        outs, off = [], 0
+        for c in ctx.cs:
+            g = _empty_cl(n, c, h, w, gy.device)
+            C.copy_channels(gy, tot, off, g, c, 0, n * h * w, c)
+            outs.append(g)
+            off += c
+        return tuple(outs)
+
+
+def cat_channels(xs):
+    return CatFn.apply(*[_cl(t) for t in xs])
+
+
+class AddFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        y = torch.empty_like(a, memory_format=CL)
+        C.add(a, b, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, g
+
+
+def add(x, y):
+    return AddFn.apply(_cl(x), _cl(y))
+
+
+class DropoutFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p):
+        x = x.contiguous().float()
+        seed = torch.randint(0, 2**31 - 1, (2,), device=x.device, dtype=torch.int64)
+        y = torch.empty_like(x)
+        mask = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+        C.dropout(x, y, mask, p, seed)
+        ctx.p = p
+        ctx.save_for_backward(mask)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (mask,) = ctx.saved_tensors
+        dx = torch.empty_like(mask, dtype=torch.float32)
+        C.dropout_bwd(g.contiguous().float(), mask, dx, ctx.p)
+        return dx, None
+
+
+def dropout(x, p):
+    return DropoutFn.apply(x, float(p))
+
+
+class ScaleRowsFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, scale):
+        y = torch.empty_like(x, memory_format=CL)
+        per = x.numel() // x.shape[0]
+        C.scale_rows(x, scale, y, per)
+        ctx.save_for_backward(scale)
+        ctx.per = per
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (scale,) = ctx.saved_tensors
+        g = _cl(g)
+        dx = torch.empty_like(g, memory_format=CL)
+        C.scale_rows(g, scale, dx, ctx.per)
+        return dx, None
+
+
+def drop_connect(x, p):
+    keep = 1.0 - p
+    r = torch.rand(x.shape[0], dtype=torch.float32, device=x.device)
+    scale = torch.floor(r + keep) / keep
+    return ScaleRowsFn.apply(_cl(x), scale)
+
+
+class SEFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, wr, br, we, be):
+        n, c, h, w = x.shape
+        hw = h * w
+        nsq = wr.shape[0]
+        wr2, we2 = wr.reshape(nsq, c).contiguous(), we.reshape(c, nsq).contiguous()
+        p = torch.empty((n, c), dtype=torch.float32, device=x.device)
+        C.gap_fwd(x, p, n, hw, c)
+        hpre = torch.empty((n, nsq), dtype=torch.float32, device=x.device)
+        _mm(p, wr2, hpre, n, nsq, c, c, 1, 1, c, bias=br)
+        a = torch.empty_like(hpre)
+        C.act32_fwd(hpre, a, 0)
+        e = torch.empty((n, c), dtype=torch.float32, device=x.device)
+        _mm(a, we2, e, n, c, nsq, nsq, 1, 1, nsq, bias=be)
+        s = torch.empty_like(e)
+        C.act32_fwd(e, s, 1)
+        y = torch.empty_like(x, memory_format=CL)
+        C.se_scale(x, s, y, n, hw, c)
+        ctx.save_for_backward(x, p, hpre, a, s, wr2, we2)
+        ctx.geo = (n, c, hw, nsq)
+        ctx.shapes = (wr.shape, we.shape)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, p, hpre, a, s, wr2, we2 = ctx.saved_tensors
+        n, c, hw, nsq = ctx.geo
+        dy = _cl(dy)
+        dev = dy.device
+        ds = torch.empty((n, c), dtype=torch.float32, device=dev)
+        C.se_ds(dy, x, ds, n, hw, c)
+        de = torch.empty_like(ds)
+        C.act32_bwd(s, ds, de, 2)
+        dwe = torch.empty((c, nsq), dtype=torch.float32, device=dev)
+        _mm(de, a, dwe, c, nsq, n, 1, c, nsq, 1)
+        dbe = torch.empty(c, dtype=torch.float32, device=dev)
+        C.colsum(de, None, dbe, n, c, c, False)
+        da = torch.empty((n, nsq), dtype=torch.float32, device=dev)
+        _mm(de, we2, da, n, nsq, c, c, 1, nsq, 1)
+        dh = torch.empty_like(da)
+        C.act32_bwd(hpre, da, dh, 0)
+        dwr = torch.empty((nsq, c), dtype=torch.float32, device=dev)
+        _mm(dh, p, dwr, nsq, c, n, 1, nsq, c, 1)
+        dbr = torch.empty(nsq, dtype=torch.float32, device=dev)
+        C.colsum(dh, None, dbr, n, nsq, nsq, False)
+        dp = torch.empty((n, c), dtype=torch.float32, device=dev)
+        _mm(dh, wr2, dp, n, c, nsq, nsq, 1, c, 1)
+        dx = torch.empty_like(dy, memory_format=CL)
+        C.se_dx(dy, s, dp, dx, n, hw, c)
+        wrs, wes = ctx.shapes
+        return dx, dwr.reshape(wrs), dbr, dwe.reshape(wes), dbe
+
+
+def se_gate(x, se_reduce, se_expand):
+    return SEFn.apply(_cl(x), se_reduce.weight, se_reduce.bias, se_expand.weight, se_expand.bias)
+
+
+# ---------------------------------------------------------------------------
+# fused Adam
+# ---------------------------------------------------------------------------
+_ADAM_CHUNK = 65536
+_TENSOR_DT = np.dtype([("p", "<u8"), ("g", "<u8"), ("m", "<u8"), ("v", "<u8"), ("s", "<u8"), ("n", "<i8")])
+
+
+def adam_build_table(opt, items):
+    groups = {}
+    for gi, group, p in items:
+        groups.setdefault(gi, (group, []))[1].append(p)
+    tables = []
+    for gi, (group, ps) in sorted(groups.items()):
+        recs = np.zeros(len(ps), dtype=_TENSOR_DT)
+        chunks = []
+        for t, p in enumerate(ps):
+            st = opt.state[p]
+            sh = shadow_for_optimizer(p)
+            recs[t] = (p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
+                       sh.data_ptr() if sh is not None else 0, p.numel())
+            for ck in range(-(-p.numel() // _ADAM_CHUNK)):
+                chunks.append((t, ck))
+            if not (p.grad.is_contiguous(memory_format=CL) if p.dim() == 4 and p.is_contiguous(memory_format=CL)
+                    else p.grad.is_contiguous()) or p.grad.stride() != p.stride():
+                raise RuntimeError("fused Adam: gradient layout differs from parameter layout")
+        dev = ps[0].device
+        tab = torch.from_numpy(recs.view(np.uint8).copy()).to(dev)
+        ck = torch.tensor(chunks, dtype=torch.int32).reshape(-1).to(dev)
+        lr_step = getattr(opt, "_lr_step", {}).get(gi)
+        if lr_step is None:
+            step0 = float(opt.state[ps[0]]["step"]) if "step" in opt.state[ps[0]] else 0.0
+            lr_step = torch.tensor([group["lr"], step0], dtype=torch.float32, device=dev)
+            opt.__dict__.setdefault("_lr_step", {})[gi] = lr_step
+        tables.append((gi, tab, ck, len(chunks), lr_step, [p for p in ps]))
+    return (tables, shadow_generation())
+
+
+def adam_step(opt, items, table, grad_scale):
+    tables, gen = table
+    if gen != shadow_generation():
+        opt._table_key = None  # rebuild next step so new shadows are kept fresh
+    for gi, tab, ck, nck, lr_step, ps in tables:
+        group = opt.param_groups[gi]
+        b1, b2 = group["betas"]
+        C.adam_tick(lr_step, float(group["lr"]))
+        C.adam(tab, ck, nck, lr_step, b1, b2, group["eps"], group["weight_decay"], float(grad_scale), _ADAM_CHUNK)
+    opt._host_steps = getattr(opt, "_host_steps", 0) + 1

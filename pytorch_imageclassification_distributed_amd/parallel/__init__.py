@@ -1,0 +1,11 @@
+from .comm import all_gather, all_gather_tensor, all_reduce_sum_, reduce_tensor
+from .dist import DistContext, barrier, destroy, get_rank, get_world_size, init_distributed
+from .reducer import GradReducer, broadcast_module_state
+from .syncbn import combine_stats, convert_sync_batchnorm, sync_batch_norm
+
+__all__ = [
+    "DistContext", "init_distributed", "barrier", "destroy", "get_rank", "get_world_size",
+    "GradReducer", "broadcast_module_state",
+    "convert_sync_batchnorm", "sync_batch_norm", "combine_stats",
+    "all_gather", "all_gather_tensor", "all_reduce_sum_", "reduce_tensor",
+]

@@ -1,0 +1,198 @@
+"""Bucketed gradient all-reduce overlapped with backward (our DDP).
+
+Reference: ``DistributedDataParallel(model, device_ids=[local_rank], ...)``
+(train.py:128) - the C++ Reducer all-reduces 25 MiB gradient buckets (1 MiB
+first bucket) as they become ready during backward, after broadcasting rank 0's
+parameters and buffers at construction (torch/nn/parallel/distributed.py:
+659-666, 828-871, 1197-1248).
+
+MI355X design:
+* every gradient lives in ONE flat fp32 buffer laid out in bucket order, so a
+  bucket is a contiguous slice (one RCCL call, no pack/unpack) and the fused
+  Adam kernel reads gradients in place;
+* a ``post_accumulate_grad`` hook per parameter copies the freshly produced
+  gradient into its slot and, when the bucket's last gradient lands, launches an
+  *asynchronous* RCCL all-reduce.  ProcessGroupNCCL runs it on its own HIP
+  stream after an event wait on the compute stream, so the reduction of early
+  buckets overlaps the rest of backward; ``finish()`` makes the compute stream
+  wait for the comm stream (no host sync);
+* buckets are re-laid-out once, after the first backward, in the order the
+  gradients actually became ready (DDP's bucket rebuild);
+* the 1/world mean is *not* applied as a separate pass: ``grad_scale`` is handed
+  to the fused optimizer (Adam is scale-invariant only up to eps, so the scale
+  is applied exactly, not skipped);
+* bucket size defaults to 32 MiB: on MI355X each GPU has 7 xGMI links of
+  ~153 GB/s; RCCL's ring/tree algorithms saturate them from a few MiB, and
+  fewer, larger buckets mean fewer ~10-20 us collective launches.  The first
+  bucket is kept small (1 MiB) so communication starts early in backward.
+* optional bf16 gradient transport (``comm_dtype=torch.bfloat16``) halves the
+  xGMI bytes.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+_ALIGN = 64  # elements (256 B) so every slot starts on a cache-line boundary
+
+
+def broadcast_module_state(module: nn.Module, src: int = 0, group=None) -> None:
+    """Coalesced broadcast of parameters and buffers from ``src`` (DDP ctor, X2)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return
+    tensors = [t for t in module.state_dict().values() if isinstance(t, torch.Tensor)]
+    by_dtype: dict = {}
+    for t in tensors:
+        by_dtype.setdefault((t.dtype, t.device), []).append(t)
+    for (_dt, _dev), ts in by_dtype.items():
+        flat = torch.cat([t.detach().reshape(-1) for t in ts])
+        dist.broadcast(flat, src, group=group)
+        off = 0
+        with torch.no_grad():
+            for t in ts:
+                n = t.numel()
+                t.copy_(flat[off:off + n].view_as(t))
+                off += n
+
+
+class GradReducer:
+    def __init__(self, module: nn.Module, group=None, bucket_cap_mb: float = 32.0,
+                 first_bucket_mb: float = 1.0, broadcast: bool = True,
+                 rebuild_buckets: bool = True, comm_dtype: torch.dtype | None = None):
+        self.module = module
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.params = [p for p in module.parameters() if p.requires_grad]
+        self.index = {id(p): i for i, p in enumerate(self.params)}
+        self.bucket_cap = int(bucket_cap_mb * 2**20) // 4
+        self.first_cap = int(first_bucket_mb * 2**20) // 4
+        self.comm_dtype = comm_dtype
+        self._rebuild_pending = rebuild_buckets and self.world > 1
+        self._ready_order: list[int] = []
+        self.works: list = []
+        self.flat: torch.Tensor | None = None
+        if broadcast:
+            broadcast_module_state(module, 0, group)
+        self._build(list(reversed(range(len(self.params)))))
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+
+    # ------------------------------------------------------------------ layout
+    def _build(self, order: list[int]) -> None:
+        old_flat, old_views = self.flat, getattr(self, "views", None)
+        dev = self.params[0].device
+        offsets = [0] * len(self.params)
+        buckets, cur, cur_start, off = [], [], 0, 0
+        cap = self.first_cap
+        for i in order:
+            p = self.params[i]
+            n = p.numel()
+            if cur and (off - cur_start) + n > cap:
+                buckets.append((cur_start, off, cur))
+                cur, cur_start, cap = [], off, self.bucket_cap
+            offsets[i] = off
+            cur.append(i)
+            off += (n + _ALIGN - 1) // _ALIGN * _ALIGN
+        if cur:
+            buckets.append((cur_start, off, cur))
+        self.flat = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.views = [torch.as_strided(self.flat, p.size(), p.stride(), offsets[i])
+                      for i, p in enumerate(self.params)]
+        self.buckets = buckets
+        self.bucket_of = [0] * len(self.params)
+        for b, (_s, _e, idx) in enumerate(buckets):
+            for i in idx:
+                self.bucket_of[i] = b
+        self._reset_counts()
+        if old_flat is not None:
+            with torch.no_grad():
+                for i, p in enumerate(self.params):
+                    self.views[i].copy_(old_views[i])
+                    if p.grad is not None:
+                        p.grad = self.views[i]
+
+    def _reset_counts(self) -> None:
+        self.pending = [len(idx) for (_s, _e, idx) in self.buckets]
+        self.launched = [False] * len(self.buckets)
+        self.got = [False] * len(self.params)
+
+    def bucket_sizes_mb(self) -> list[float]:
+        return [(e - s) * 4 / 2**20 for (s, e, _i) in self.buckets]
+
+    # ------------------------------------------------------------------ hooks
+    @torch.no_grad()
+    def _on_grad(self, p: torch.Tensor) -> None:
+        i = self.index[id(p)]
+        v = self.views[i]
+        if p.grad is not v:
+            v.copy_(p.grad)
+            p.grad = v
+        if self._rebuild_pending:
+            self._ready_order.append(i)
+        if not self.got[i]:
+            self.got[i] = True
+            b = self.bucket_of[i]
+            self.pending[b] -= 1
+            if self.pending[b] == 0:
+                self._launch(b)
+
+    def _launch(self, b: int) -> None:
+        self.launched[b] = True
+        if self.world == 1:
+            return
+        s, e, _ = self.buckets[b]
+        t = self.flat[s:e]
+        if self.comm_dtype is not None and self.comm_dtype != torch.float32:
+            c = t.to(self.comm_dtype)
+            self.works.append((dist.all_reduce(c, group=self.group, async_op=True), t, c))
+        else:
+            self.works.append((dist.all_reduce(t, group=self.group, async_op=True), None, None))
+
+    # ------------------------------------------------------------------ step
+    @torch.no_grad()
+    def finish(self) -> float:
+        """Flush the remaining buckets, make the compute stream wait for RCCL.
+
+        Returns the factor that turns the summed gradients into the world mean
+        (consumed by the fused optimizer).
+        """
+        for i, p in enumerate(self.params):  # parameters that got no gradient
+            if not self.got[i]:
+                self.views[i].zero_()
+                p.grad = self.views[i]
+                self.got[i] = True
+                b = self.bucket_of[i]
+                self.pending[b] -= 1
+        for b in range(len(self.buckets)):
+            if not self.launched[b]:
+                self._launch(b)
+        for work, dst, comp in self.works:
+            work.wait()
+            if dst is not None:
+                dst.copy_(comp)
+        self.works.clear()
+        self._reset_counts()
+        if self._rebuild_pending:
+            self._rebuild_pending = False
+            seen = set(self._ready_order)
+            order = self._ready_order + [i for i in reversed(range(len(self.params))) if i not in seen]
+            self._build(order)
+            self._ready_order = []
+        return 1.0 / self.world
+
+    def average_(self) -> None:
+        """Turn the summed flat gradients into means in place (for stock optimizers)."""
+        if self.world > 1:
+            self.flat.mul_(1.0 / self.world)
+
+    def sync_buffers(self, src: int = 0) -> None:
+        """DDP ``broadcast_buffers`` (X3): redundant with SyncBN, kept for parity."""
+        if self.world == 1:
+            return
+        for b in self.module.buffers():
+            dist.broadcast(b, src, group=self.group)
+
+    def remove_hooks(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []

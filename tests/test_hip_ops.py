@@ -1,0 +1,278 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op.
+
+Inputs are rounded to bf16 first (the HIP path stores activations/weights in
+bf16), the reference then runs in fp32 on those exact values, so the remaining
+error is the kernels' fp32-accumulation order plus the bf16 rounding of outputs.
+"""
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+CL = torch.channels_last
+
+
+def _hip():
+    from pytorch_imageclassification_distributed_amd.ops import hip
+    return hip
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).abs().max() / b.abs().max().clamp(min=1e-6)).item()
+
+
+def bf(x):
+    return x.to(torch.bfloat16).float()
+
+
+CONV_CASES = [
+    # N, Cin, H, W, Cout, k, stride, pad
+    (2, 64, 56, 56, 64, (1, 1), 1, (0, 0)),
+    (2, 64, 56, 56, 64, (3, 3), 1, (1, 1)),
+    (2, 64, 56, 56, 256, (1, 1), 1, (0, 0)),
+    (2, 128, 56, 56, 128, (3, 3), 2, (1, 1)),
+    (2, 256, 56, 56, 512, (1, 1), 2, (0, 0)),
+    (2, 512, 7, 7, 2048, (1, 1), 1, (0, 0)),
+    (3, 512, 7, 7, 512, (3, 3), 1, (1, 1)),
+    (2, 8, 64, 64, 64, (7, 7), 2, (3, 3)),
+    (2, 64, 17, 17, 64, (1, 7), 1, (0, 3)),
+    (2, 64, 17, 17, 96, (7, 1), 1, (3, 0)),
+    (2, 48, 35, 35, 64, (5, 5), 1, (2, 2)),
+    (2, 96, 35, 35, 96, (3, 3), 2, (0, 0)),
+    (1, 32, 15, 13, 40, (3, 3), 1, (0, 0)),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_bwd(case):
+    hip = _hip()
+    n, cin, h, w, cout, k, s, p = case
+    torch.manual_seed(0)
+    conv = nn.Conv2d(cin, cout, k, s, p, bias=False).to(DEV).to(memory_format=CL)
+    with torch.no_grad():
+        conv.weight.copy_(bf(conv.weight))
+    x = bf(torch.randn(n, cin, h, w, device=DEV)).contiguous(memory_format=CL)
+    xb = x.to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
+    y = hip.ConvFn.apply(xb, conv.weight, conv, False)
+    xr = x.clone().requires_grad_(True)
+    wr = conv.weight.detach().clone().requires_grad_(True)
+    yr = F.conv2d(xr, wr, None, s, p)
+    assert y.shape == yr.shape
+    assert rel_err(y, yr) < 1e-2
+    gy = bf(torch.randn_like(yr))
+    y.backward(gy.to(torch.bfloat16).contiguous(memory_format=CL))
+    yr.backward(gy)
+    assert rel_err(xb.grad, xr.grad) < 2e-2
+    assert rel_err(conv.weight.grad, wr.grad) < 2e-2
+
+
+def test_stem_padded_input():
+    """Cin=3 image -> prepare_input pads to 8 channels; weight padded inside the op."""
+    hip = _hip()
+    torch.manual_seed(1)
+    conv = nn.Conv2d(3, 64, 7, 2, 3, bias=False).to(DEV).to(memory_format=CL)
+    with torch.no_grad():
+        conv.weight.copy_(bf(conv.weight))
+    x = bf(torch.randn(2, 3, 32, 32, device=DEV))
+    xp = hip.prepare_input(x)
+    assert xp.shape[1] == 8
+    y = hip.ConvFn.apply(xp, conv.weight, conv, False)
+    yr = F.conv2d(x, conv.weight, None, 2, 3)
+    assert rel_err(y, yr) < 1e-2
+    g = bf(torch.randn_like(yr))
+    y.backward(g.to(torch.bfloat16).contiguous(memory_format=CL))
+    wr = torch.autograd.grad(F.conv2d(x, conv.weight, None, 2, 3), conv.weight, g)[0]
+    assert rel_err(conv.weight.grad, wr) < 2e-2
+
+
+@pytest.mark.parametrize("act,use_res", [("relu", False), ("relu", True), (None, False), ("silu", False)])
+def test_conv_bn_act(act, use_res):
+    hip = _hip()
+    torch.manual_seed(2)
+    n, c, h, w, co = 4, 64, 14, 14, 128
+    conv = nn.Conv2d(c, co, 3, 1, 1, bias=False).to(DEV).to(memory_format=CL)
+    bn = nn.BatchNorm2d(co).to(DEV)
+    with torch.no_grad():
+        conv.weight.copy_(bf(conv.weight))
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    conv_r = nn.Conv2d(c, co, 3, 1, 1, bias=False).to(DEV)
+    bn_r = nn.BatchNorm2d(co).to(DEV)
+    conv_r.load_state_dict(conv.state_dict())
+    bn_r.load_state_dict(bn.state_dict())
+    x = bf(torch.randn(n, c, h, w, device=DEV))
+    res = bf(torch.randn(n, co, h, w, device=DEV)) if use_res else None
+    xb = x.to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
+    rb = res.to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True) if use_res else None
+    out = hip.conv_bn_act(xb, conv, bn, act, rb)
+    xr = x.clone().requires_grad_(True)
+    rr = res.clone().requires_grad_(True) if use_res else None
+    z = bn_r(conv_r(xr))
+    if use_res:
+        z = z + rr
+    ref = {None: z, "relu": F.relu(z) if act == "relu" else z, "silu": F.silu(z)}[act]
+    assert rel_err(out, ref) < 2e-2
+    assert torch.allclose(bn.running_mean, bn_r.running_mean, rtol=1e-2, atol=1e-3)
+    assert torch.allclose(bn.running_var, bn_r.running_var, rtol=1e-2, atol=1e-3)
+    assert int(bn.num_batches_tracked) == 1
+    g = bf(torch.randn_like(ref))
+    out.backward(g.to(torch.bfloat16).contiguous(memory_format=CL))
+    ref.backward(g)
+    assert rel_err(xb.grad, xr.grad) < 3e-2
+    assert rel_err(bn.weight.grad, bn_r.weight.grad) < 3e-2
+    assert rel_err(bn.bias.grad, bn_r.bias.grad) < 3e-2
+    assert rel_err(conv.weight.grad, conv_r.weight.grad) < 3e-2
+    if use_res:
+        assert rel_err(rb.grad, rr.grad) < 3e-2
+    # eval mode uses running statistics
+    bn.eval()
+    bn_r.eval()
+    with torch.no_grad():
+        oe = hip.conv_bn_act(xb.detach(), conv, bn, act, rb.detach() if use_res else None)
+        ze = bn_r(conv_r(x)) + (res if use_res else 0)
+        re = {None: ze, "relu": F.relu(ze) if act == "relu" else ze, "silu": F.silu(ze)}[act]
+    assert rel_err(oe, re) < 2e-2
+
+
+def test_depthwise_bn_silu():
+    hip = _hip()
+    torch.manual_seed(3)
+    for (c, k, s, hw) in [(96, 3, 2, 28), (144, 5, 1, 14), (32, 3, 1, 16)]:
+        conv = nn.Conv2d(c, c, k, s, 0, groups=c, bias=False).to(DEV).to(memory_format=CL)
+        conv.tf_same = True
+        bn = nn.BatchNorm2d(c, eps=1e-3, momentum=0.01).to(DEV)
+        with torch.no_grad():
+            conv.weight.copy_(bf(conv.weight))
+        x = bf(torch.randn(2, c, hw, hw, device=DEV))
+        xb = x.to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
+        out = hip.conv_bn_act(xb, conv, bn, "silu", None)
+        from pytorch_imageclassification_distributed_amd.ops.functional import conv_padding
+        pt, pb, pl, pr = conv_padding(conv, hw, hw)
+        xr = x.clone().requires_grad_(True)
+        wr = conv.weight.detach().clone().requires_grad_(True)
+        z = F.conv2d(F.pad(xr, (pl, pr, pt, pb)), wr, None, s, 0, 1, c)
+        ref = F.silu(F.batch_norm(z, None, None, training=True, eps=1e-3))
+        assert rel_err(out, ref) < 2e-2
+        g = bf(torch.randn_like(ref))
+        out.backward(g.to(torch.bfloat16).contiguous(memory_format=CL))
+        ref.backward(g)
+        assert rel_err(xb.grad, xr.grad) < 3e-2
+        assert rel_err(conv.weight.grad, wr.grad) < 3e-2
+
+
+@pytest.mark.parametrize("kind", ["max311", "max320", "avg311", "avg530"])
+def test_pools(kind):
+    hip = _hip()
+    torch.manual_seed(4)
+    x = bf(torch.randn(2, 64, 17, 17, device=DEV))
+    xb = x.to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
+    xr = x.clone().requires_grad_(True)
+    k, s, p = int(kind[3]), int(kind[4]), int(kind[5])
+    if kind.startswith("max"):
+        y, yr = hip.max_pool2d(xb, k, s, p), F.max_pool2d(xr, k, s, p)
+    else:
+        y, yr = hip.avg_pool2d(xb, k, s, p), F.avg_pool2d(xr, k, s, p)
+    assert rel_err(y, yr) < 1e-2
+    g = bf(torch.randn_like(yr))
+    y.backward(g.to(torch.bfloat16).contiguous(memory_format=CL))
+    yr.backward(g)
+    assert rel_err(xb.grad, xr.grad) < 2e-2
+
+
+def test_gap_head_ce():
+    hip = _hip()
+    from pytorch_imageclassification_distributed_amd.models import mlp_head
+    torch.manual_seed(5)
+    x = bf(torch.randn(8, 256, 7, 7, device=DEV))
+    xb = x.to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
+    head = mlp_head(256, 7).to(DEV)
+    w = torch.tensor([3, 3, 10, 1, 4, 4, 5], dtype=torch.float32, device=DEV)
+    lab = torch.randint(0, 7, (8,), device=DEV)
+    loss = hip.cross_entropy(hip.mlp(hip.global_avg_pool(xb), head), lab, w)
+    head_r = mlp_head(256, 7).to(DEV)
+    head_r.load_state_dict(head.state_dict())
+    xr = x.clone().requires_grad_(True)
+    loss_r = F.cross_entropy(head_r(F.adaptive_avg_pool2d(xr, 1).flatten(1)), lab, weight=w)
+    assert abs(loss.item() - loss_r.item()) < 1e-4 * max(1.0, abs(loss_r.item()))
+    (0.7 * loss).backward()
+    (0.7 * loss_r).backward()
+    assert rel_err(xb.grad, xr.grad) < 1e-2
+    for (n1, p1), (_n2, p2) in zip(head.named_parameters(), head_r.named_parameters()):
+        assert rel_err(p1.grad, p2.grad) < 1e-4, n1
+
+
+def test_se_gate_and_misc():
+    hip = _hip()
+    torch.manual_seed(6)
+    c, nsq = 96, 4
+    red = nn.Conv2d(c, nsq, 1).to(DEV)
+    exp = nn.Conv2d(nsq, c, 1).to(DEV)
+    x = bf(torch.randn(2, c, 9, 9, device=DEV))
+    xb = x.to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
+    y = hip.se_gate(xb, red, exp)
+    xr = x.clone().requires_grad_(True)
+    s = torch.sigmoid(exp(F.silu(red(F.adaptive_avg_pool2d(xr, 1)))))
+    yr = s * xr
+    assert rel_err(y, yr) < 1e-2
+    g = bf(torch.randn_like(yr))
+    y.backward(g.to(torch.bfloat16).contiguous(memory_format=CL))
+    gr = torch.autograd.grad(yr, [xr, red.weight, exp.weight], g)
+    assert rel_err(xb.grad, gr[0]) < 2e-2
+    # cat / add
+    a = torch.randn(2, 16, 5, 5, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=CL)
+    b = torch.randn(2, 24, 5, 5, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=CL)
+    assert torch.equal(hip.cat_channels([a, b]), torch.cat([a, b], 1))
+    assert rel_err(hip.add(a, a), a.float() * 2) < 1e-2
+
+
+def test_fused_adam_matches_torch():
+    from pytorch_imageclassification_distributed_amd.engine.optim import FusedAdam
+    torch.manual_seed(7)
+    p1 = torch.randn(4097, device=DEV, requires_grad=True)
+    p2 = torch.randn(64, 3, 3, 3, device=DEV).contiguous(memory_format=CL).requires_grad_(True)
+    q1, q2 = p1.detach().clone().requires_grad_(True), p2.detach().clone().requires_grad_(True)
+    opt = FusedAdam([p1, p2], lr=1e-2)
+    ref = torch.optim.Adam([q1, q2], lr=1e-2)
+    for _ in range(5):
+        g1, g2 = torch.randn_like(p1), torch.randn_like(p2)
+        p1.grad, p2.grad = g1.clone(), g2.clone().contiguous(memory_format=CL)
+        q1.grad, q2.grad = g1.clone(), g2.clone()
+        opt.step()
+        ref.step()
+    assert torch.allclose(p1, q1, atol=1e-5, rtol=1e-5)
+    assert torch.allclose(p2, q2, atol=1e-5, rtol=1e-5)
+    sd = opt.state_dict()
+    assert float(sd["state"][0]["step"]) == 5.0
+
+
+def test_resnet18_matches_reference_path():
+    """Whole-model forward/backward: HIP bf16 path vs ATen fp32 path on identical weights."""
+    from pytorch_imageclassification_distributed_amd.models import Classifier
+    from pytorch_imageclassification_distributed_amd.ops import functional as Fx
+    torch.manual_seed(8)
+    m = Classifier("resnet18", 7).to(DEV)
+    m_ref = Classifier("resnet18", 7).to(DEV)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_(bf(p))
+    m_ref.load_state_dict(m.state_dict())
+    m = m.to(memory_format=CL)
+    x = bf(torch.randn(8, 3, 64, 64, device=DEV))
+    lab = torch.randint(0, 7, (8,), device=DEV)
+    loss = Fx.cross_entropy(m(x), lab)
+    loss.backward()
+    Fx.set_backend("torch")
+    try:
+        loss_r = Fx.cross_entropy(m_ref(x), lab)
+        loss_r.backward()
+    finally:
+        Fx.set_backend("auto")
+    assert abs(loss.item() - loss_r.item()) < 0.05 * abs(loss_r.item()) + 1e-3
+    g1 = m.encoder.layer1[0].conv1.weight.grad
+    g2 = m_ref.encoder.layer1[0].conv1.weight.grad
+    cos = F.cosine_similarity(g1.flatten(), g2.flatten(), dim=0).item()
+    assert cos > 0.95, cos
