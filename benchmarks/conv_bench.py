@@ -1,0 +1,100 @@
+"""Per-shape conv kernel benchmark: our MFMA implicit-GEMM (fwd / dgrad / wgrad) vs MIOpen.
+
+Shapes: the 23 unique ResNet-50 @224 convolutions at a given batch.
+Prints one line per shape and a JSON summary (TFLOP/s = 2*MACs / time).
+
+    python benchmarks/conv_bench.py --batch 256 [--torch]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+# Cin, Cout, k, s, p, H_in, count   (ResNet-50 @224)
+R50 = [
+    (256, 256, 3, 1, 1, 14, 5), (64, 64, 3, 1, 1, 56, 3), (128, 128, 3, 1, 1, 28, 3),
+    (256, 1024, 1, 1, 0, 14, 6), (1024, 256, 1, 1, 0, 14, 5), (512, 512, 3, 1, 1, 7, 2),
+    (64, 256, 1, 1, 0, 56, 4), (128, 512, 1, 1, 0, 28, 4), (512, 128, 1, 1, 0, 28, 3),
+    (512, 2048, 1, 1, 0, 7, 3), (8, 64, 7, 2, 3, 224, 1), (128, 128, 3, 2, 1, 56, 1),
+    (256, 256, 3, 2, 1, 28, 1), (512, 512, 3, 2, 1, 14, 1), (256, 64, 1, 1, 0, 56, 2),
+    (256, 128, 1, 1, 0, 56, 1), (256, 512, 1, 2, 0, 56, 1), (512, 256, 1, 1, 0, 28, 1),
+    (512, 1024, 1, 2, 0, 28, 1), (1024, 512, 1, 1, 0, 14, 1), (1024, 2048, 1, 2, 0, 14, 1),
+    (2048, 512, 1, 1, 0, 7, 2), (64, 64, 1, 1, 0, 56, 1),
+]
+
+
+def timeit(fn, iters=10, warm=2):
+    for _ in range(warm):
+        fn()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    b.synchronize()
+    return a.elapsed_time(b) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--torch", action="store_true", help="also time MIOpen (torch) for each shape")
+    ap.add_argument("--iters", type=int, default=10)
+    a = ap.parse_args()
+    from pytorch_imageclassification_distributed_amd.ops import hip
+    dev = "cuda"
+    n = a.batch
+    rows = []
+    tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0, "t_fwd": 0.0, "t_bwd": 0.0}
+    for (ci, co, k, s, p, h, cnt) in R50:
+        conv = nn.Conv2d(ci, co, k, s, p, bias=False).to(dev).to(memory_format=torch.channels_last)
+        x = torch.randn(n, ci, h, h, device=dev, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        g = hip.ConvGeom(x, conv)
+        stats = hip.ws(x.device).stats_buf(co)
+        part_sums = torch.empty(2 * co, dtype=torch.float64, device=dev)
+        y = hip.conv_forward_raw(x, conv.weight, g, stats=stats)
+        hip.C.bn_partials(stats, hip.G_STATS, co, part_sums, None, None)
+        dy = torch.randn_like(y)
+        macs = n * g.OH * g.OW * co * ci * k * k
+        tf = lambda ms: 2 * macs / (ms * 1e-3) / 1e12  # noqa: E731
+
+        def fwd():
+            hip.conv_forward_raw(x, conv.weight, g, stats=stats)
+            hip.C.bn_partials(stats, hip.G_STATS, co, part_sums, None, None)
+
+        t_f = timeit(fwd, a.iters)
+        t_d = timeit(lambda: hip.conv_dgrad_raw(dy, conv.weight, g), a.iters) if ci != 8 else 0.0
+        t_w = timeit(lambda: hip.conv_wgrad_raw(dy, x, conv.weight, g), a.iters)
+        r = dict(shape=f"{ci}->{co} k{k}s{s} {h}x{h}", count=cnt, fwd_ms=t_f, dgrad_ms=t_d, wgrad_ms=t_w,
+                 fwd_tf=tf(t_f), dgrad_tf=tf(t_d) if t_d else None, wgrad_tf=tf(t_w))
+        tot["fwd"] += t_f * cnt
+        tot["dgrad"] += t_d * cnt
+        tot["wgrad"] += t_w * cnt
+        if a.torch:
+            xt = x.detach().requires_grad_(True)
+            wt = conv.weight.detach().to(torch.bfloat16).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+            tt_f = timeit(lambda: F.conv2d(xt, wt, None, s, p), a.iters)
+            yt = F.conv2d(xt, wt, None, s, p)
+            tt_b = timeit(lambda: torch.autograd.grad(yt, [xt, wt], dy, retain_graph=True), a.iters)
+            r.update(torch_fwd_ms=tt_f, torch_bwd_ms=tt_b, torch_fwd_tf=tf(tt_f))
+            tot["t_fwd"] += tt_f * cnt
+            tot["t_bwd"] += tt_b * cnt
+        rows.append(r)
+        msg = (f"{r['shape']:>26} x{cnt}: fwd {t_f:7.3f}ms {r['fwd_tf']:6.0f}TF | dgrad {t_d:7.3f}ms "
+               f"{(r['dgrad_tf'] or 0):6.0f}TF | wgrad {t_w:7.3f}ms {r['wgrad_tf']:6.0f}TF")
+        if a.torch:
+            msg += f" || miopen fwd {r['torch_fwd_ms']:7.3f}ms bwd {r['torch_bwd_ms']:7.3f}ms"
+        print(msg, flush=True)
+    print(json.dumps({"batch": n, "total_ms": tot, "rows": rows}))
+
+
+if __name__ == "__main__":
+    main()

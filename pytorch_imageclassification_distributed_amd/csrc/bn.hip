@@ -21,22 +21,36 @@
 namespace {
 
 // ---- partial rows [G][2][C] -> fp64 sums [2][C]; zero the rows -------------
-__global__ void bn_partials_kernel(float* __restrict__ part, int G, int C, double* __restrict__ sums,
-                                   float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// block = 64 channels x 4 row-groups; each row-group sums G/4 partial rows
+__global__ __launch_bounds__(256) void bn_partials_kernel(float* __restrict__ part, int G, int C,
+                                                          double* __restrict__ sums, float* __restrict__ dgamma,
+                                                          float* __restrict__ dbeta) {
+  __shared__ double red[2][4][64];
+  const int lc = threadIdx.x & 63, lg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lc;
   double s = 0.0, q = 0.0;
-  for (int g = 0; g < G; ++g) {
-    float* r = part + (size_t)g * 2 * C;
-    s += (double)r[c];
-    q += (double)r[C + c];
-    r[c] = 0.f;
-    r[C + c] = 0.f;
+  if (c < C) {
+#pragma unroll 4
+    for (int g = lg; g < G; g += 4) {
+      float* r = part + (size_t)g * 2 * C;
+      const float a = r[c], b = r[C + c];
+      r[c] = 0.f;
+      r[C + c] = 0.f;
+      s += (double)a;
+      q += (double)b;
+    }
   }
-  sums[c] = s;
-  sums[C + c] = q;
-  if (dbeta) dbeta[c] = (float)s;       // backward: sum dz
-  if (dgamma) dgamma[c] = (float)q;     // backward: sum dz * xhat
+  red[0][lg][lc] = s;
+  red[1][lg][lc] = q;
+  __syncthreads();
+  if (lg == 0 && c < C) {
+    s = red[0][0][lc] + red[0][1][lc] + red[0][2][lc] + red[0][3][lc];
+    q = red[1][0][lc] + red[1][1][lc] + red[1][2][lc] + red[1][3][lc];
+    sums[c] = s;
+    sums[C + c] = q;
+    if (dbeta) dbeta[c] = (float)s;    // backward: sum dz
+    if (dgamma) dgamma[c] = (float)q;  // backward: sum dz * xhat
+  }
 }
 
 // ---- fp64 sums -> coefficients, running stats -----------------------------
@@ -221,6 +235,11 @@ __global__ void bn_bwd_k_kernel(const double* __restrict__ sums, const double* _
   kout[C + c] = (float)(sums[C + c] / n);
 }
 
+DEVI void load8f(const float* p, float* v) {
+  *(float4*)v = *(const float4*)p;
+  *(float4*)(v + 4) = *(const float4*)(p + 4);
+}
+
 __global__ void bn_bwd_elemt_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ y,
                                     const float* __restrict__ coef, const float* __restrict__ kk,
                                     const bf16_t* __restrict__ res, const bf16_t* __restrict__ dz_in,
@@ -230,18 +249,24 @@ __global__ void bn_bwd_elemt_kernel(const bf16_t* __restrict__ g, const bf16_t* 
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const long row = i / cch;
     const int c0 = (int)(i - row * cch) * 8;
-    float gv[8], yv[8];
+    float gv[8], yv[8], sc[8], mu[8], is[8], k1[8], k2[8];
     unpack8(*(const uint4*)(y + row * C + c0), yv);
+    load8f(coef + c0, sc);
+    load8f(coef + 2 * C + c0, mu);
+    load8f(coef + 3 * C + c0, is);
+    load8f(kk + c0, k1);
+    load8f(kk + C + c0, k2);
     if (dz_in) {
       unpack8(*(const uint4*)(dz_in + row * C + c0), gv);
     } else {
       unpack8(*(const uint4*)(g + row * C + c0), gv);
       if (act != ACT_NONE) {
-        float rv[8];
+        float sh[8], rv[8];
+        load8f(coef + C + c0, sh);
         if (res) unpack8(*(const uint4*)(res + row * C + c0), rv);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          float z = yv[k] * coef[c0 + k] + coef[C + c0 + k];
+          float z = yv[k] * sc[k] + sh[k];
           if (res) z += rv[k];
           gv[k] = act_grad(z, gv[k], act);
         }
@@ -249,9 +274,8 @@ __global__ void bn_bwd_elemt_kernel(const bf16_t* __restrict__ g, const bf16_t* 
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int c = c0 + k;
-      const float xhat = (yv[k] - coef[2 * C + c]) * coef[3 * C + c];
-      gv[k] = coef[c] * (gv[k] - kk[c] - xhat * kk[C + c]);
+      const float xhat = (yv[k] - mu[k]) * is[k];
+      gv[k] = sc[k] * (gv[k] - k1[k] - xhat * k2[k]);
     }
     *(uint4*)(dy + row * C + c0) = pack8(gv);
   }
@@ -266,7 +290,7 @@ int grid_for(long work, int per_block = 256, int cap = 4096) {
 
 int bn_partials_launch(float* part, int G, int C, double* sums, float* dgamma, float* dbeta,
                        hipStream_t s) {
-  hipLaunchKernelGGL(bn_partials_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, part, G, C, sums, dgamma, dbeta);
+  hipLaunchKernelGGL(bn_partials_kernel, dim3(cdiv(C, 64)), dim3(256), 0, s, part, G, C, sums, dgamma, dbeta);
   HIP_CHECK_LAUNCH();
   return 0;
 }

@@ -57,7 +57,7 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(const ConvParams p) {
   constexpr int AR = BM / 32, BR = BN / 32;
   constexpr int TAP_BYTES = 3 * CONV_MAX_TAPS * 4;
   constexpr int CST = BN + 8;  // C tile row stride (elements)
-  static_assert(BM * CST * 2 + 4 * BN * 4 <= 2 * STAGE, "epilogue LDS reuse");
+  static_assert(BM * CST * 2 <= 2 * STAGE, "epilogue LDS reuse");
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + TAP_BYTES];
   int* s_dh = (int*)(smem + 2 * STAGE);
   int* s_dw = s_dh + CONV_MAX_TAPS;
@@ -162,7 +162,7 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(const ConvParams p) {
       for (int i = 0; i < RM; ++i)
 #pragma unroll
         for (int j = 0; j < RN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[j], af[i], acc[i][j], 0, 0, 0);
     }
     if (kt + 1 < nk) CONV_STORE((kt + 1) & 1);
     __syncthreads();
@@ -171,54 +171,46 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(const ConvParams p) {
 #undef CONV_STORE
 
   // ---------------- epilogue ----------------
+  // acc[i][j][r] = C[pixel m0 + wm*WTM + i*16 + fr][channel n0 + wn*WTN + j*16 + fq*4 + r]
+  // 1) 4 consecutive channels -> one 8-B ds_write into the bf16 tile [BM][CST]
   bf16_t* ct = (bf16_t*)smem;
-  float* red = (float*)(smem + BM * CST * 2);  // [2 (s,q)][2 (wm)][BN]
-  const bool do_stats = p.stats != nullptr;
 #pragma unroll
-  for (int j = 0; j < RN; ++j) {
-    const int col = wn * WTN + j * 16 + fr;
-    const float bv = (p.bias != nullptr && n0 + col < p.Ncols) ? p.bias[n0 + col] : 0.f;
-    float s = 0.f, q = 0.f;
+  for (int i = 0; i < RM; ++i) {
+    const int row = wm * WTM + i * 16 + fr;
 #pragma unroll
-    for (int i = 0; i < RM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wm * WTM + i * 16 + fq * 4 + r;
-        const bf16_t h = f2bf(acc[i][j][r] + bv);
-        ct[row * CST + col] = h;
-        if (do_stats && m0 + row < p.M) {
-          const float v = bf2f(h);
-          s += v;
-          q += v * v;
-        }
+    for (int j = 0; j < RN; ++j) {
+      const int col = wn * WTN + j * 16 + fq * 4;
+      float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
+      if (p.bias != nullptr) {
+        const int c = n0 + col;
+        v0 += c + 0 < p.Ncols ? p.bias[c + 0] : 0.f;
+        v1 += c + 1 < p.Ncols ? p.bias[c + 1] : 0.f;
+        v2 += c + 2 < p.Ncols ? p.bias[c + 2] : 0.f;
+        v3 += c + 3 < p.Ncols ? p.bias[c + 3] : 0.f;
       }
-    }
-    if (do_stats) {
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
-      if (fq == 0) {
-        red[(0 * 2 + wm) * BN + col] = s;
-        red[(1 * 2 + wm) * BN + col] = q;
-      }
+      uint2 pk;
+      pk.x = pack2(v0, v1);
+      pk.y = pack2(v2, v3);
+      *(uint2*)(ct + row * CST + col) = pk;
     }
   }
   __syncthreads();
-  if (do_stats && tid < BN && n0 + tid < p.Ncols) {
-    const float s = red[(0 * 2 + 0) * BN + tid] + red[(0 * 2 + 1) * BN + tid];
-    const float q = red[(1 * 2 + 0) * BN + tid] + red[(1 * 2 + 1) * BN + tid];
-    float* dst = p.stats + (size_t)(bm % p.stats_groups) * 2 * p.Ncols + n0 + tid;
-    atomicAdd(dst, s);
-    atomicAdd(dst + p.Ncols, q);
-  }
-  constexpr int CPR = BN / 8;
+  // 2) stream the tile out: 16 B (8 channels of one pixel) per lane, coalesced rows;
+  //    BN partial statistics accumulate on the way out (from the bf16-rounded values)
+  constexpr int CPR = BN / 8;        // chunks per row
+  constexpr int RPP = NT / CPR;      // rows per pass
+  const int sch = tid % CPR, srow = tid / CPR;
+  const int col = n0 + sch * 8;
+  const bool col_ok = col < p.Ncols;
   const bool direct = (p.so == 1 && p.oh0 == 0 && p.ow0 == 0 && p.GH == p.OH && p.GW == p.OW);
+  float s8[8], q8[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { s8[k] = 0.f; q8[k] = 0.f; }
 #pragma unroll 4
-  for (int idx = tid; idx < BM * CPR; idx += NT) {
-    const int row = idx / CPR, ch = idx - row * CPR;
-    const int m = m0 + row, col = n0 + ch * 8;
-    if (m < p.M && col < p.Ncols) {
+  for (int row = srow; row < BM; row += RPP) {
+    const int m = m0 + row;
+    if (m < p.M && col_ok) {
+      const uint4 v = *(const uint4*)(ct + row * CST + sch * 8);
       long pix;
       if (direct) {
         pix = m;
@@ -227,7 +219,45 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(const ConvParams p) {
         const int gh = r / p.GW, gw = r - gh * p.GW;
         pix = ((long)n * p.OH + gh * p.so + p.oh0) * p.OW + gw * p.so + p.ow0;
       }
-      *(uint4*)(p.C + pix * p.ldc + p.c_off + col) = *(const uint4*)(ct + row * CST + ch * 8);
+      *(uint4*)(p.C + pix * p.ldc + p.c_off + col) = v;
+      if (p.stats != nullptr) {
+        float f[8];
+        unpack8(v, f);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { s8[k] += f[k]; q8[k] += f[k] * f[k]; }
+      }
+    }
+  }
+  if (p.stats != nullptr) {
+    // lanes with equal sch inside a wave: tid, tid+CPR, ... (stride CPR); reduce over the wave
+#pragma unroll
+    for (int o = CPR; o < 64; o <<= 1) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s8[k] += __shfl_xor(s8[k], o, 64);
+        q8[k] += __shfl_xor(q8[k], o, 64);
+      }
+    }
+    __syncthreads();  // tile reads done; reuse LDS for the cross-wave reduction
+    float* red = (float*)smem;  // [4 waves][2][BN]
+    if (lane < CPR) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        red[(wid * 2 + 0) * BN + sch * 8 + k] = s8[k];
+        red[(wid * 2 + 1) * BN + sch * 8 + k] = q8[k];
+      }
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < p.Ncols) {
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        s += red[(w * 2 + 0) * BN + tid];
+        q += red[(w * 2 + 1) * BN + tid];
+      }
+      float* dst = p.stats + (size_t)(bm % p.stats_groups) * 2 * p.Ncols + n0 + tid;
+      atomicAdd(dst, s);
+      atomicAdd(dst + p.Ncols, q);
     }
   }
 }

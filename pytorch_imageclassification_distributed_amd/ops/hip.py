@@ -93,9 +93,9 @@ def weight_bf16(p: torch.Tensor) -> torch.Tensor:
         _SHADOWS[key] = e
         _SHADOW_GEN[0] += 1
     src = p.detach()
-    if not _krsc_compatible(src):
-        src = src.permute(0, 2, 3, 1).contiguous() if src.dim() == 4 else src.contiguous()
-    C.cast_bf16(src.reshape(-1) if src.is_contiguous() else src.contiguous().reshape(-1), e.t)
+    # flatten in KRSC order: a free view for channels_last weights, a copy otherwise
+    flat = src.permute(0, 2, 3, 1).reshape(-1) if src.dim() == 4 else src.reshape(-1)
+    C.cast_bf16(flat, e.t)
     e.ptr = p.data_ptr()
     e.version = p._version
     return e.t

@@ -48,9 +48,9 @@ def all_gather_tensor(tensor: torch.Tensor, group=None) -> torch.Tensor:
     w = dist.get_world_size(group) if dist.is_initialized() else 1
     if w == 1:
         return tensor.unsqueeze(0)
-    out = torch.empty((w,) + tuple(tensor.shape), dtype=tensor.dtype, device=tensor.device)
-    dist.all_gather_into_tensor(out, tensor.contiguous(), group=group)
-    return out
+    out = torch.empty(w * tensor.numel(), dtype=tensor.dtype, device=tensor.device)
+    dist.all_gather_into_tensor(out, tensor.contiguous().reshape(-1), group=group)
+    return out.view((w,) + tuple(tensor.shape))
 
 
 def all_gather(data):

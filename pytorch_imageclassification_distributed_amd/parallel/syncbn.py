@@ -55,9 +55,8 @@ class _SyncBN(torch.autograd.Function):
         mean = xf.mean(dims)
         m2 = ((xf - mean.view(1, -1, 1, 1)) ** 2).sum(dims)
         packed = torch.cat([mean, m2, torch.tensor([float(cnt)], device=x.device)])
-        w = dist.get_world_size(group)
-        allp = torch.empty(w, packed.numel(), device=x.device, dtype=packed.dtype)
-        dist.all_gather_into_tensor(allp, packed, group=group)
+        from .comm import all_gather_tensor
+        allp = all_gather_tensor(packed, group=group)
         c = mean.numel()
         gmean, gvar, n = combine_stats(allp[:, :c], allp[:, c:2 * c], allp[:, 2 * c])
         invstd = torch.rsqrt(gvar + eps)
