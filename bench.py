@@ -48,7 +48,7 @@ def parse():
     p.add_argument("--sync-bn", default="auto", choices=["auto", "on", "off"])
     p.add_argument("--bucket-mb", type=float, default=32.0)
     p.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
-    p.add_argument("--graph", action="store_true", help="capture the step in a HIP graph")
+    p.add_argument("--dist-backend", default="auto", help="auto (RCCL) | gloo (functional multi-rank runs on one GPU)")
     p.add_argument("--profile-steps", type=int, default=0)
     return p.parse_args()
 
@@ -66,11 +66,7 @@ def load_baseline(n_gpus: int):
 
 def main():
     a = parse()
-    if "LOCAL_RANK" in os.environ and "WORLD_SIZE" in os.environ:
-        n = int(os.environ["WORLD_SIZE"])
-    else:
-        n = 1
-    ctx = init_distributed(device="cuda")
+    ctx = init_distributed(device="cuda", backend=a.dist_backend)
     sync_bn = (a.sync_bn == "on") or (a.sync_bn == "auto" and ctx.world_size > 1)
     targs = build_parser().parse_args([
         "--synthetic", "--model", a.model, "--image-size", str(a.image_size),

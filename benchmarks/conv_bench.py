@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--torch", action="store_true", help="also time MIOpen (torch) for each shape")
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--variants", default="", help="comma list of conv fwd/dgrad kernel variants to A/B (1,2,3)")
     a = ap.parse_args()
     from pytorch_imageclassification_distributed_amd.ops import hip
     dev = "cuda"
@@ -70,6 +71,14 @@ def main():
             hip.conv_forward_raw(x, conv.weight, g, stats=stats)
             hip.C.bn_partials(stats, hip.G_STATS, co, part_sums, None, None)
 
+        if a.variants:
+            alt = []
+            for v in [int(t) for t in a.variants.split(",")]:
+                hip.C.conv_set_variant(v)
+                alt.append((v, timeit(fwd, a.iters), timeit(lambda: hip.conv_dgrad_raw(dy, conv.weight, g), a.iters)
+                            if ci != 8 else 0.0))
+            hip.C.conv_set_variant(0)
+            print("   variants " + "  ".join(f"v{v}: fwd {tf_:.3f} dgrad {td_:.3f}" for v, tf_, td_ in alt), flush=True)
         t_f = timeit(fwd, a.iters)
         t_d = timeit(lambda: hip.conv_dgrad_raw(dy, conv.weight, g), a.iters) if ci != 8 else 0.0
         t_w = timeit(lambda: hip.conv_wgrad_raw(dy, x, conv.weight, g), a.iters)

@@ -90,8 +90,9 @@ constexpr auto F32 = at::kFloat;
 
 void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols, int K, int CA, int GH, int GW,
                int IH, int IW, int sA, int ldb, int OH, int OW, int so, int oh0, int ow0, int ldc, int c_off,
-               std::vector<int> dh, std::vector<int> dw, std::vector<int> tb, int stats_groups) {
+               std::vector<int> dh, std::vector<int> dw, std::vector<int> tb, int stats_groups, Tensor zero) {
   req(A, BF, "A"); req(B, BF, "B"); req(C, BF, "C");
+  TORCH_CHECK(zero.is_cuda() && zero.nbytes() >= 16, "conv_gemm: zero page must be >= 16 device bytes");
   TORCH_CHECK(CA % 8 == 0 && Ncols % 8 == 0 && ldc % 8 == 0 && c_off % 8 == 0, "conv_gemm: channel counts must be multiples of 8");
   TORCH_CHECK((int)dh.size() <= CONV_MAX_TAPS && dh.size() == dw.size() && dh.size() == tb.size(), "bad taps");
   TORCH_CHECK(A.numel() < (1LL << 31) && B.numel() < (1LL << 31), "conv_gemm: operand too large for 32-bit indexing");
@@ -102,6 +103,7 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
   p.M = M; p.Ncols = Ncols; p.K = K; p.CA = CA; p.GH = GH; p.GW = GW; p.IH = IH; p.IW = IW; p.sA = sA;
   p.ldb = ldb; p.OH = OH; p.OW = OW; p.so = so; p.oh0 = oh0; p.ow0 = ow0; p.ldc = ldc; p.c_off = c_off;
   p.ntaps = (int)dh.size(); p.stats_groups = stats_groups > 0 ? stats_groups : 1;
+  p.zero = ptr<bf16_t>(zero);
   for (size_t i = 0; i < dh.size(); ++i) { p.tap_dh[i] = dh[i]; p.tap_dw[i] = dw[i]; p.tap_b[i] = tb[i]; }
   check(conv_gemm_launch(p, cur()), "conv_gemm");
 }
@@ -347,6 +349,7 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "gfx950 (MI355X) HIP kernels for pytorch_imageclassification_distributed_amd";
   m.def("conv_gemm", &conv_gemm);
   m.def("conv_wgrad", &conv_wgrad);
+  m.def("conv_set_variant", &conv_set_variant);
   m.def("bn_partials", &bn_partials);
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_eval_coef", &bn_eval_coef);

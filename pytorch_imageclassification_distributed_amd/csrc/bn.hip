@@ -148,6 +148,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     }
     const long rbeg = blockIdx.x * rows_per_block;
     const long rend = rbeg + rows_per_block < rows ? rbeg + rows_per_block : rows;
+#pragma unroll 4
     for (long row = rbeg + lr; row < rend; row += RP) {
       float gv[8], yv[8], rv[8];
       unpack8(*(const uint4*)(g + row * C + c0), gv);
@@ -205,6 +206,7 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict_
   if (lr < RP && chunk < cch) {
     const long rbeg = blockIdx.x * rows_per_block;
     const long rend = rbeg + rows_per_block < rows ? rbeg + rows_per_block : rows;
+#pragma unroll 4
     for (long row = rbeg + lr; row < rend; row += RP) {
       float v[8];
       unpack8(*(const uint4*)(y + row * C + chunk * 8), v);

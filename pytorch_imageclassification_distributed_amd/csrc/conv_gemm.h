@@ -31,6 +31,7 @@ struct ConvParams {
   int ldb;
   int OH, OW, so, oh0, ow0, ldc, c_off;
   int ntaps, stats_groups;
+  const bf16_t* zero;  // >= 16 zero bytes: source of padded / out-of-range LDS-DMA chunks
   int tap_dh[CONV_MAX_TAPS];
   int tap_dw[CONV_MAX_TAPS];
   int tap_b[CONV_MAX_TAPS];
@@ -47,4 +48,5 @@ struct WgradParams {
 };
 
 int conv_gemm_launch(const ConvParams& p, hipStream_t stream);
+void conv_set_variant(int v);  // 0 = auto, 1 = register-staged, 2 = LDS-DMA 2-stage, 3 = LDS-DMA 3-stage
 int conv_wgrad_launch(const WgradParams& p, int splits, hipStream_t stream);

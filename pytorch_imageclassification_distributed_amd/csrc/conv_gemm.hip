@@ -48,6 +48,104 @@ DEVI int xcd_remap(int bid, int nwg) {
 }
 
 template <int BN>
+DEVI void conv_epilogue(const ConvParams& p, f32x4 (&acc)[BM / 32][BN / 32], char* smem, int tid, int lane,
+                        int wid, int wm, int wn, int m0, int n0, int bm, int ghw) {
+  constexpr int WTM = BM / 2, WTN = BN / 2;
+  constexpr int RM = WTM / 16, RN = WTN / 16;
+  constexpr int CST = BN + 8;
+  const int fr = lane & 15, fq = lane >> 4;
+  // acc[i][j][r] = C[pixel m0 + wm*WTM + i*16 + fr][channel n0 + wn*WTN + j*16 + fq*4 + r]
+  // 1) 4 consecutive channels -> one 8-B ds_write into the bf16 tile [BM][CST]
+  bf16_t* ct = (bf16_t*)smem;
+#pragma unroll
+  for (int i = 0; i < RM; ++i) {
+    const int row = wm * WTM + i * 16 + fr;
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      const int col = wn * WTN + j * 16 + fq * 4;
+      float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
+      if (p.bias != nullptr) {
+        const int c = n0 + col;
+        v0 += c + 0 < p.Ncols ? p.bias[c + 0] : 0.f;
+        v1 += c + 1 < p.Ncols ? p.bias[c + 1] : 0.f;
+        v2 += c + 2 < p.Ncols ? p.bias[c + 2] : 0.f;
+        v3 += c + 3 < p.Ncols ? p.bias[c + 3] : 0.f;
+      }
+      uint2 pk;
+      pk.x = pack2(v0, v1);
+      pk.y = pack2(v2, v3);
+      *(uint2*)(ct + row * CST + col) = pk;
+    }
+  }
+  __syncthreads();
+  // 2) stream the tile out: 16 B (8 channels of one pixel) per lane, coalesced rows;
+  //    BN partial statistics accumulate on the way out (from the bf16-rounded values)
+  constexpr int CPR = BN / 8;        // chunks per row
+  constexpr int RPP = NT / CPR;      // rows per pass
+  const int sch = tid % CPR, srow = tid / CPR;
+  const int col = n0 + sch * 8;
+  const bool col_ok = col < p.Ncols;
+  const bool direct = (p.so == 1 && p.oh0 == 0 && p.ow0 == 0 && p.GH == p.OH && p.GW == p.OW);
+  float s8[8], q8[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { s8[k] = 0.f; q8[k] = 0.f; }
+#pragma unroll 4
+  for (int row = srow; row < BM; row += RPP) {
+    const int m = m0 + row;
+    if (m < p.M && col_ok) {
+      const uint4 v = *(const uint4*)(ct + row * CST + sch * 8);
+      long pix;
+      if (direct) {
+        pix = m;
+      } else {
+        const int n = m / ghw, r = m - n * ghw;
+        const int gh = r / p.GW, gw = r - gh * p.GW;
+        pix = ((long)n * p.OH + gh * p.so + p.oh0) * p.OW + gw * p.so + p.ow0;
+      }
+      *(uint4*)(p.C + pix * p.ldc + p.c_off + col) = v;
+      if (p.stats != nullptr) {
+        float f[8];
+        unpack8(v, f);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { s8[k] += f[k]; q8[k] += f[k] * f[k]; }
+      }
+    }
+  }
+  if (p.stats != nullptr) {
+    // lanes with equal sch inside a wave: tid, tid+CPR, ... (stride CPR); reduce over the wave
+#pragma unroll
+    for (int o = CPR; o < 64; o <<= 1) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s8[k] += __shfl_xor(s8[k], o, 64);
+        q8[k] += __shfl_xor(q8[k], o, 64);
+      }
+    }
+    __syncthreads();  // tile reads done; reuse LDS for the cross-wave reduction
+    float* red = (float*)smem;  // [4 waves][2][BN]
+    if (lane < CPR) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        red[(wid * 2 + 0) * BN + sch * 8 + k] = s8[k];
+        red[(wid * 2 + 1) * BN + sch * 8 + k] = q8[k];
+      }
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < p.Ncols) {
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        s += red[(w * 2 + 0) * BN + tid];
+        q += red[(w * 2 + 1) * BN + tid];
+      }
+      float* dst = p.stats + (size_t)(bm % p.stats_groups) * 2 * p.Ncols + n0 + tid;
+      atomicAdd(dst, s);
+      atomicAdd(dst + p.Ncols, q);
+    }
+  }
+}
+
+template <int BN>
 __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(const ConvParams p) {
   constexpr int A_BYTES = BM * BK * 2;
   constexpr int B_BYTES = BN * BK * 2;
@@ -170,96 +268,168 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(const ConvParams p) {
 #undef CONV_LOAD
 #undef CONV_STORE
 
-  // ---------------- epilogue ----------------
-  // acc[i][j][r] = C[pixel m0 + wm*WTM + i*16 + fr][channel n0 + wn*WTN + j*16 + fq*4 + r]
-  // 1) 4 consecutive channels -> one 8-B ds_write into the bf16 tile [BM][CST]
-  bf16_t* ct = (bf16_t*)smem;
+  conv_epilogue<BN>(p, acc, smem, tid, lane, wid, wm, wn, m0, n0, bm, ghw);
+}
+
+
+// ---------------------------------------------------------------------------
+// forward / dgrad, LDS-DMA variant: global_load_lds (16 B per lane, per-lane
+// gather source, lane-linear LDS destination) into a STAGES-deep ring; counted
+// vmcnt + raw s_barrier keep STAGES-2 tiles in flight across the barrier, and no
+// staging VGPRs are spent.  The XOR swizzle moves to the *source* address: the
+// lane that fills physical chunk pc of row r fetches logical chunk pc ^ ((r>>1)&7)
+// (guide rule 21), and fragment reads use the same swz().
+// ---------------------------------------------------------------------------
+template <int N>
+DEVI void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | (((N >> 4) & 3) << 14));
+}
+
+DEVI void glds16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+template <int BN, int STAGES, bool TAP_UNIFORM>
+__global__ __launch_bounds__(NT, 1) void conv_gemm_glds_kernel(const ConvParams p) {
+  constexpr int A_BYTES = BM * BK * 2;
+  constexpr int B_BYTES = BN * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int WTM = BM / 2, WTN = BN / 2;
+  constexpr int RM = WTM / 16, RN = WTN / 16;
+  constexpr int AL = BM / 32;        // LDS-DMA instructions per wave per stage (A): 8 rows each
+  constexpr int BL = BN / 32;        // (B)
+  constexpr int LPS = AL + BL;
+  constexpr int TAP_BYTES = 3 * CONV_MAX_TAPS * 4;
+  constexpr int CST = BN + 8;
+  static_assert(BM * CST * 2 <= STAGES * STAGE, "epilogue LDS reuse");
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE + TAP_BYTES];
+  int* s_dh = (int*)(smem + STAGES * STAGE);
+  int* s_dw = s_dh + CONV_MAX_TAPS;
+  int* s_tb = s_dw + CONV_MAX_TAPS;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform (M0 base)
+  const int wm = wid >> 1, wn = wid & 1;
+  const int gm = (p.M + BM - 1) / BM, gn = (p.Ncols + BN - 1) / BN;
+  const int lin = xcd_remap(blockIdx.x, gm * gn);
+  const int bm = lin / gn, bn = lin - bm * gn;
+  const int m0 = bm * BM, n0 = bn * BN;
+  if (tid < p.ntaps) {
+    s_dh[tid] = p.tap_dh[tid];
+    s_dw[tid] = p.tap_dw[tid];
+    s_tb[tid] = p.tap_b[tid];
+  }
+  // lane -> (row within an 8-row group, physical chunk); logical chunk per instruction
+  const int lrow = lane >> 3, pch = lane & 7;
+  const int ghw = p.GH * p.GW;
+  int a_base[AL], a_ih[AL], a_iw[AL], a_ch[AL];
 #pragma unroll
-  for (int i = 0; i < RM; ++i) {
-    const int row = wm * WTM + i * 16 + fr;
+  for (int i = 0; i < AL; ++i) {
+    const int row = wid * (BM / 4) + i * 8 + lrow;
+    a_ch[i] = pch ^ ((row >> 1) & 7);
+    const int m = m0 + row;
+    if (m < p.M) {
+      const int n = m / ghw, r = m - n * ghw;
+      const int gh = r / p.GW, gw = r - gh * p.GW;
+      a_base[i] = n * p.IH * p.IW * p.CA;
+      a_ih[i] = gh * p.sA;
+      a_iw[i] = gw * p.sA;
+    } else {
+      a_base[i] = 0;
+      a_ih[i] = -(1 << 28);
+      a_iw[i] = 0;
+    }
+  }
+  int b_off[BL], b_ch[BL];
 #pragma unroll
-    for (int j = 0; j < RN; ++j) {
-      const int col = wn * WTN + j * 16 + fq * 4;
-      float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
-      if (p.bias != nullptr) {
-        const int c = n0 + col;
-        v0 += c + 0 < p.Ncols ? p.bias[c + 0] : 0.f;
-        v1 += c + 1 < p.Ncols ? p.bias[c + 1] : 0.f;
-        v2 += c + 2 < p.Ncols ? p.bias[c + 2] : 0.f;
-        v3 += c + 3 < p.Ncols ? p.bias[c + 3] : 0.f;
+  for (int i = 0; i < BL; ++i) {
+    const int row = wid * (BN / 4) + i * 8 + lrow;
+    b_ch[i] = pch ^ ((row >> 1) & 7);
+    const int n = n0 + row;
+    b_off[i] = n < p.Ncols ? n * p.ldb : -1;
+  }
+  __syncthreads();
+
+  // all addresses (incl. the LDS tap-table reads) are formed before the first LDS-DMA of
+  // the stage: a DMA into the same __shared__ array would otherwise force the compiler
+  // to re-read the tables behind an lgkmcnt wait between every two DMAs
+  auto issue = [&](int kt, int buf) {
+    char* sa = smem + buf * STAGE;
+    char* sb = sa + A_BYTES;
+    const bf16_t* srca[AL];
+    const bf16_t* srcb[BL];
+    if (TAP_UNIFORM) {
+      const int k0 = kt * BK;
+      const int tap = k0 / p.CA, ci0 = k0 - tap * p.CA;
+      const int dh = s_dh[tap], dw = s_dw[tap], tb = s_tb[tap];
+#pragma unroll
+      for (int i = 0; i < AL; ++i) {
+        const int ih = a_ih[i] + dh, iw = a_iw[i] + dw;
+        const bool ok = (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+        srca[i] = ok ? p.A + a_base[i] + (ih * p.IW + iw) * p.CA + ci0 + a_ch[i] * 8 : p.zero;
       }
-      uint2 pk;
-      pk.x = pack2(v0, v1);
-      pk.y = pack2(v2, v3);
-      *(uint2*)(ct + row * CST + col) = pk;
+#pragma unroll
+      for (int i = 0; i < BL; ++i)
+        srcb[i] = b_off[i] >= 0 ? p.B + b_off[i] + tb * p.CA + ci0 + b_ch[i] * 8 : p.zero;
+    } else {
+#pragma unroll
+      for (int i = 0; i < AL; ++i) {
+        const int k = kt * BK + a_ch[i] * 8;
+        const int tap = k < p.K ? k / p.CA : 0;
+        const int ci = k - tap * p.CA;
+        const int ih = a_ih[i] + s_dh[tap], iw = a_iw[i] + s_dw[tap];
+        const bool ok = k < p.K && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+        srca[i] = ok ? p.A + a_base[i] + (ih * p.IW + iw) * p.CA + ci : p.zero;
+      }
+#pragma unroll
+      for (int i = 0; i < BL; ++i) {
+        const int k = kt * BK + b_ch[i] * 8;
+        const int tap = k < p.K ? k / p.CA : 0;
+        const int ci = k - tap * p.CA;
+        srcb[i] = (k < p.K && b_off[i] >= 0) ? p.B + b_off[i] + s_tb[tap] * p.CA + ci : p.zero;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < AL; ++i) glds16(srca[i], sa + (wid * (BM / 4) + i * 8) * 128);
+#pragma unroll
+    for (int i = 0; i < BL; ++i) glds16(srcb[i], sb + (wid * (BN / 4) + i * 8) * 128);
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (p.K + BK - 1) / BK;
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) issue(s, s);
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + STAGES - 2 < nk) wait_vmcnt<(STAGES - 2) * LPS>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+    const char* sa = smem + (kt % STAGES) * STAGE;
+    const char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[RM], bfg[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i) af[i] = *(const bf16x8*)(sa + swz(wm * WTM + i * 16 + fr, kk * 4 + fq));
+#pragma unroll
+      for (int j = 0; j < RN; ++j) bfg[j] = *(const bf16x8*)(sb + swz(wn * WTN + j * 16 + fr, kk * 4 + fq));
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[j], af[i], acc[i][j], 0, 0, 0);
     }
   }
   __syncthreads();
-  // 2) stream the tile out: 16 B (8 channels of one pixel) per lane, coalesced rows;
-  //    BN partial statistics accumulate on the way out (from the bf16-rounded values)
-  constexpr int CPR = BN / 8;        // chunks per row
-  constexpr int RPP = NT / CPR;      // rows per pass
-  const int sch = tid % CPR, srow = tid / CPR;
-  const int col = n0 + sch * 8;
-  const bool col_ok = col < p.Ncols;
-  const bool direct = (p.so == 1 && p.oh0 == 0 && p.ow0 == 0 && p.GH == p.OH && p.GW == p.OW);
-  float s8[8], q8[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) { s8[k] = 0.f; q8[k] = 0.f; }
-#pragma unroll 4
-  for (int row = srow; row < BM; row += RPP) {
-    const int m = m0 + row;
-    if (m < p.M && col_ok) {
-      const uint4 v = *(const uint4*)(ct + row * CST + sch * 8);
-      long pix;
-      if (direct) {
-        pix = m;
-      } else {
-        const int n = m / ghw, r = m - n * ghw;
-        const int gh = r / p.GW, gw = r - gh * p.GW;
-        pix = ((long)n * p.OH + gh * p.so + p.oh0) * p.OW + gw * p.so + p.ow0;
-      }
-      *(uint4*)(p.C + pix * p.ldc + p.c_off + col) = v;
-      if (p.stats != nullptr) {
-        float f[8];
-        unpack8(v, f);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) { s8[k] += f[k]; q8[k] += f[k] * f[k]; }
-      }
-    }
-  }
-  if (p.stats != nullptr) {
-    // lanes with equal sch inside a wave: tid, tid+CPR, ... (stride CPR); reduce over the wave
-#pragma unroll
-    for (int o = CPR; o < 64; o <<= 1) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        s8[k] += __shfl_xor(s8[k], o, 64);
-        q8[k] += __shfl_xor(q8[k], o, 64);
-      }
-    }
-    __syncthreads();  // tile reads done; reuse LDS for the cross-wave reduction
-    float* red = (float*)smem;  // [4 waves][2][BN]
-    if (lane < CPR) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        red[(wid * 2 + 0) * BN + sch * 8 + k] = s8[k];
-        red[(wid * 2 + 1) * BN + sch * 8 + k] = q8[k];
-      }
-    }
-    __syncthreads();
-    if (tid < BN && n0 + tid < p.Ncols) {
-      float s = 0.f, q = 0.f;
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        s += red[(w * 2 + 0) * BN + tid];
-        q += red[(w * 2 + 1) * BN + tid];
-      }
-      float* dst = p.stats + (size_t)(bm % p.stats_groups) * 2 * p.Ncols + n0 + tid;
-      atomicAdd(dst, s);
-      atomicAdd(dst + p.Ncols, q);
-    }
-  }
+  conv_epilogue<BN>(p, acc, smem, tid, lane, wid, wm, wn, m0, n0, bm, ghw);
 }
 
 // ---------------------------------------------------------------------------
@@ -403,16 +573,30 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(const WgradParams p) 
 
 }  // namespace
 
+static int g_variant = 0;
+void conv_set_variant(int v) { g_variant = v; }
+
+template <int BN>
+static void launch_bn(const ConvParams& p, int gm, hipStream_t stream) {
+  const int gn = cdiv(p.Ncols, BN);
+  const bool uni = (p.CA % BK) == 0;
+  const int v = g_variant == 0 ? 2 : g_variant;  // measured: 2-stage LDS-DMA wins (benchmarks/conv_bench.py --variants)
+  if (v == 1) {
+    hipLaunchKernelGGL(conv_gemm_kernel<BN>, dim3(gm * gn), dim3(NT), 0, stream, p);
+  } else if (v == 2) {
+    if (uni) hipLaunchKernelGGL((conv_gemm_glds_kernel<BN, 2, true>), dim3(gm * gn), dim3(NT), 0, stream, p);
+    else hipLaunchKernelGGL((conv_gemm_glds_kernel<BN, 2, false>), dim3(gm * gn), dim3(NT), 0, stream, p);
+  } else {
+    if (uni) hipLaunchKernelGGL((conv_gemm_glds_kernel<BN, 3, true>), dim3(gm * gn), dim3(NT), 0, stream, p);
+    else hipLaunchKernelGGL((conv_gemm_glds_kernel<BN, 3, false>), dim3(gm * gn), dim3(NT), 0, stream, p);
+  }
+}
+
 int conv_gemm_launch(const ConvParams& p, hipStream_t stream) {
   if (p.M <= 0 || p.Ncols <= 0) return 0;
   const int gm = cdiv(p.M, BM);
-  if (p.Ncols <= 64) {
-    const int gn = cdiv(p.Ncols, 64);
-    hipLaunchKernelGGL(conv_gemm_kernel<64>, dim3(gm * gn), dim3(NT), 0, stream, p);
-  } else {
-    const int gn = cdiv(p.Ncols, 128);
-    hipLaunchKernelGGL(conv_gemm_kernel<128>, dim3(gm * gn), dim3(NT), 0, stream, p);
-  }
+  if (p.Ncols <= 64) launch_bn<64>(p, gm, stream);
+  else launch_bn<128>(p, gm, stream);
   HIP_CHECK_LAUNCH();
   return 0;
 }

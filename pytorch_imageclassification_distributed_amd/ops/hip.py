@@ -38,6 +38,7 @@ class _Workspace:
     def __init__(self, dev):
         self.dev = dev
         self.stats = torch.zeros(0, dtype=torch.float32, device=dev)
+        self.zero = torch.zeros(64, dtype=BF16, device=dev)  # zero page for padded LDS-DMA chunks
 
     def stats_buf(self, c: int) -> torch.Tensor:
         need = G_STATS * 2 * c
@@ -216,7 +217,7 @@ def conv_forward_raw(x, w_param, g: ConvGeom, stats=None, bias=None, out=None, c
     if g.sh != g.sw:
         raise NotImplementedError("anisotropic stride")
     C.conv_gemm(x, wb, y, stats, bias, g.N * g.OH * g.OW, g.Co, g.T * g.Cx, g.Cx, g.OH, g.OW, g.H, g.W,
-                g.sh, g.T * g.Cx, g.OH, g.OW, 1, 0, 0, ldc, c_off, dh, dw, tb, G_STATS)
+                g.sh, g.T * g.Cx, g.OH, g.OW, 1, 0, 0, ldc, c_off, dh, dw, tb, G_STATS, ws(dev).zero)
     return y
 
 
@@ -230,7 +231,7 @@ def conv_dgrad_raw(dy, w_param, g: ConvGeom):
         if gh <= 0 or gw <= 0:
             continue
         C.conv_gemm(dy, wt, dx, None, None, g.N * gh * gw, g.Ci, len(tb) * g.Co, g.Co, gh, gw, g.OH, g.OW,
-                    1, g.T * g.Co, g.H, g.W, g.sh, ph, pw, g.Ci, 0, dh, dw, tb, 1)
+                    1, g.T * g.Co, g.H, g.W, g.sh, ph, pw, g.Ci, 0, dh, dw, tb, 1, ws(dev).zero)
     return dx
 
 
@@ -812,6 +813,16 @@ _ADAM_CHUNK = 65536
 _TENSOR_DT = np.dtype([("p", "<u8"), ("g", "<u8"), ("m", "<u8"), ("v", "<u8"), ("s", "<u8"), ("n", "<i8")])
 
 
+def _same_memory_order(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Dense tensors whose elements sit in the same order in memory (size-1 dims ignored)."""
+    if a.shape != b.shape:
+        return False
+    dense = lambda t: t.is_contiguous() or t.is_contiguous(memory_format=CL)  # noqa: E731
+    if not (dense(a) and dense(b)):
+        return False
+    return all(sa == sb for n, sa, sb in zip(a.shape, a.stride(), b.stride()) if n > 1)
+
+
 def adam_build_table(opt, items):
     groups = {}
     for gi, group, p in items:
@@ -827,8 +838,7 @@ def adam_build_table(opt, items):
                        sh.data_ptr() if sh is not None else 0, p.numel())
             for ck in range(-(-p.numel() // _ADAM_CHUNK)):
                 chunks.append((t, ck))
-            if not (p.grad.is_contiguous(memory_format=CL) if p.dim() == 4 and p.is_contiguous(memory_format=CL)
-                    else p.grad.is_contiguous()) or p.grad.stride() != p.stride():
+            if not _same_memory_order(p, p.grad):
                 raise RuntimeError("fused Adam: gradient layout differs from parameter layout")
         dev = ps[0].device
         tab = torch.from_numpy(recs.view(np.uint8).copy()).to(dev)

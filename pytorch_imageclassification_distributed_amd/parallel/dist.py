@@ -55,8 +55,10 @@ def init_distributed(device: str = "auto", backend: str | None = None,
     if device == "auto":
         device = "cuda" if torch.cuda.is_available() else "cpu"
     if device == "cuda":
-        torch.cuda.set_device(lr)
-        dev = torch.device("cuda", lr)
+        # one process per GPU; ranks beyond the visible devices share them (functional tests only)
+        idx = lr % max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(idx)
+        dev = torch.device("cuda", idx)
     else:
         dev = torch.device("cpu")
     if backend is None or backend == "auto":

@@ -1,0 +1,13 @@
+#!/bin/bash
+set -o pipefail
+ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+cd "$ROOT"; mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+fatal() { case "$1" in 124|134|137|139) echo "fatal rc=$1 at $2"; exit "$1";; esac; }
+AMD_SERIALIZE_KERNEL=3 timeout -k 10 600 python -m pytest tests/test_hip_ops.py -x -q -s -m gpu > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+echo "pytest rc=$rc"; tail -4 gpurun_out/pytest_gpu.log; fatal $rc pytest
+[ $rc -eq 0 ] || exit 1
+timeout -k 10 600 python benchmarks/conv_bench.py --batch 256 --variants 1,2,3 > gpurun_out/conv_variants.log 2>&1; rc=$?
+echo "conv_bench rc=$rc"; grep -v '^{' gpurun_out/conv_variants.log | tail -48; fatal $rc conv_bench
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_hip.log 2>&1; rc=$?
+echo "bench rc=$rc"; tail -1 gpurun_out/bench_hip.log; fatal $rc bench

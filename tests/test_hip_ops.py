@@ -116,7 +116,9 @@ def test_conv_bn_act(act, use_res):
     out = hip.conv_bn_act(xb, conv, bn, act, rb)
     xr = x.clone().requires_grad_(True)
     rr = res.clone().requires_grad_(True) if use_res else None
-    z = bn_r(conv_r(xr))
+    yc = conv_r(xr)
+    yc = yc + (bf(yc) - yc).detach()  # the HIP path stores the conv output in bf16: same values here
+    z = bn_r(yc)
     if use_res:
         z = z + rr
     ref = {None: z, "relu": F.relu(z) if act == "relu" else z, "silu": F.silu(z)}[act]
@@ -127,9 +129,7 @@ def test_conv_bn_act(act, use_res):
     g = bf(torch.randn_like(ref))
     out.backward(g.to(torch.bfloat16).contiguous(memory_format=CL))
     ref.backward(g)
-    # bf16 storage of the pre-activation can flip a few ReLU masks near z=0: loose max-norm,
-    # tight mean-norm
-    assert rel_err(xb.grad, xr.grad) < 8e-2
+    assert rel_err(xb.grad, xr.grad) < 3e-2
     assert mean_err(xb.grad, xr.grad) < 1e-2
     assert rel_err(bn.weight.grad, bn_r.weight.grad) < 3e-2
     assert rel_err(bn.bias.grad, bn_r.bias.grad) < 3e-2
@@ -223,7 +223,9 @@ def test_se_gate_and_misc():
     xb = x.to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
     y = hip.se_gate(xb, red, exp)
     xr = x.clone().requires_grad_(True)
-    s = torch.sigmoid(exp(F.silu(red(F.adaptive_avg_pool2d(xr, 1)))))
+    pool = xr.mean((2, 3))
+    hid = F.silu(F.linear(pool, red.weight.flatten(1), red.bias))
+    s = torch.sigmoid(F.linear(hid, exp.weight.flatten(1), exp.bias))[:, :, None, None]
     yr = s * xr
     assert rel_err(y, yr) < 1e-2
     g = bf(torch.randn_like(yr))
@@ -258,29 +260,47 @@ def test_fused_adam_matches_torch():
 
 
 def test_resnet18_matches_reference_path():
-    """Whole-model forward/backward: HIP bf16 path vs ATen fp32 path on identical weights."""
+    """Whole-model forward/backward: HIP bf16 path vs ATen fp32 path on identical weights.
+
+    Gradient agreement is measured by cosine similarity per layer and compared with what
+    the reference stack itself achieves in bf16 autocast (same weights, same data): the
+    HIP path must be at least as close to fp32 as torch's own bf16 path, minus a margin.
+    """
     from pytorch_imageclassification_distributed_amd.models import Classifier
     from pytorch_imageclassification_distributed_amd.ops import functional as Fx
     torch.manual_seed(8)
-    m = Classifier("resnet18", 7).to(DEV)
-    m_ref = Classifier("resnet18", 7).to(DEV)
+    base = Classifier("resnet18", 7)
     with torch.no_grad():
-        for p in m.parameters():
+        for p in base.parameters():
             p.copy_(bf(p))
-    m_ref.load_state_dict(m.state_dict())
-    m = m.to(memory_format=CL)
-    x = bf(torch.randn(8, 3, 64, 64, device=DEV))
-    lab = torch.randint(0, 7, (8,), device=DEV)
-    loss = Fx.cross_entropy(m(x), lab)
-    loss.backward()
-    Fx.set_backend("torch")
-    try:
-        loss_r = Fx.cross_entropy(m_ref(x), lab)
-        loss_r.backward()
-    finally:
-        Fx.set_backend("auto")
-    assert abs(loss.item() - loss_r.item()) < 0.05 * abs(loss_r.item()) + 1e-3
-    g1 = m.encoder.layer1[0].conv1.weight.grad
-    g2 = m_ref.encoder.layer1[0].conv1.weight.grad
-    cos = F.cosine_similarity(g1.flatten(), g2.flatten(), dim=0).item()
-    assert cos > 0.95, cos
+    sd = base.state_dict()
+    x = bf(torch.randn(16, 3, 64, 64, device=DEV))
+    lab = torch.randint(0, 7, (16,), device=DEV)
+    layers = ["encoder.fc.6.weight", "encoder.layer4.1.conv2.weight", "encoder.layer3.0.conv1.weight",
+              "encoder.layer2.0.conv1.weight", "encoder.layer1.0.conv1.weight", "encoder.conv1.weight"]
+
+    def run(backend, autocast):
+        m = Classifier("resnet18", 7).to(DEV)
+        m.load_state_dict(sd)
+        if backend == "hip":
+            m = m.to(memory_format=CL)
+        Fx.set_backend(backend)
+        try:
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+                out = m(x)
+            loss = Fx.cross_entropy(out.float(), lab)
+            loss.backward()
+        finally:
+            Fx.set_backend("auto")
+        g = dict(m.named_parameters())
+        return loss.item(), {k: g[k].grad.float().flatten() for k in layers}
+
+    l32, g32 = run("torch", False)
+    lbf, gbf = run("torch", True)
+    lh, gh = run("hip", False)
+    assert abs(lh - l32) < 0.02 * abs(l32) + 1e-3
+    for k in layers:
+        c_h = F.cosine_similarity(gh[k], g32[k], dim=0).item()
+        c_t = F.cosine_similarity(gbf[k], g32[k], dim=0).item()
+        print(f"{k}: cos(hip, fp32)={c_h:.4f} cos(torch-bf16, fp32)={c_t:.4f}")
+        assert c_h > min(0.98, c_t - 0.05), (k, c_h, c_t)

@@ -45,8 +45,9 @@ def test_lr_schedule_multistep(tmp_path):
 
 
 def test_inception_aux_loss_path(tmp_path):
-    hist = train.main(["--synthetic", "--model", "inceptionv3", "--image-size", "160", "--device", "cpu",
-                       "--batchsize", "4", "--num-workers", "0", "--synthetic-train-size", "8",
-                       "--synthetic-val-size", "4", "--no-progress", "--epochs", "1", "--ckpt-dir", str(tmp_path),
+    # the aux head (avgpool 5x5/3 -> 5x5 conv) needs the full 299 resolution (Mixed_6e at 17x17)
+    hist = train.main(["--synthetic", "--model", "inceptionv3", "--image-size", "299", "--device", "cpu",
+                       "--batchsize", "2", "--num-workers", "0", "--synthetic-train-size", "4",
+                       "--synthetic-val-size", "2", "--no-progress", "--epochs", "1", "--ckpt-dir", str(tmp_path),
                        "--resume", "none", "--val-batchsize", "2"])
     assert torch.isfinite(torch.tensor(hist[0]["train_loss"]))
