@@ -53,14 +53,15 @@ def parse():
     return p.parse_args()
 
 
-def load_baseline(n_gpus: int):
+def load_baseline(n_gpus: int, batch: int):
+    """Reference-stack images/sec measured on MI355X at the same per-GPU batch and GPU count."""
     path = os.path.join(HERE, "benchmarks", "reference_stack.json")
     try:
         with open(path) as f:
             ref = json.load(f)
-        v = ref.get("images_per_sec", {}).get(str(n_gpus))
+        v = ref.get("images_per_sec", {}).get(str(batch), {}).get(str(n_gpus))
         return float(v) if v else None
-    except (OSError, ValueError):
+    except (OSError, ValueError, AttributeError):
         return None
 
 
@@ -108,7 +109,7 @@ def main():
     if ctx.rank == 0:
         imgs = a.batch * ctx.world_size * a.steps
         value = imgs / dt
-        base = load_baseline(ctx.world_size)
+        base = load_baseline(ctx.world_size, a.batch)
         print(json.dumps({
             "metric": METRIC, "value": round(value, 2), "unit": "images/sec",
             "n_gpus": ctx.world_size, "steps": a.steps, "warmup": a.warmup,

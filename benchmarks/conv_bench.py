@@ -49,6 +49,8 @@ def main():
     ap.add_argument("--torch", action="store_true", help="also time MIOpen (torch) for each shape")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--variants", default="", help="comma list of conv fwd/dgrad kernel variants to A/B (1,2,3)")
+    ap.add_argument("--wvariants", default="", help="comma list of wgrad kernel variants to A/B (1,2)")
+    ap.add_argument("--wblocks", default="", help="comma list of wgrad split-K target block counts to sweep")
     a = ap.parse_args()
     from pytorch_imageclassification_distributed_amd.ops import hip
     dev = "cuda"
@@ -79,6 +81,20 @@ def main():
                             if ci != 8 else 0.0))
             hip.C.conv_set_variant(0)
             print("   variants " + "  ".join(f"v{v}: fwd {tf_:.3f} dgrad {td_:.3f}" for v, tf_, td_ in alt), flush=True)
+        if a.wvariants:
+            alt = []
+            for v in [int(t) for t in a.wvariants.split(",")]:
+                hip.C.conv_set_wgrad_variant(v)
+                alt.append((v, timeit(lambda: hip.conv_wgrad_raw(dy, x, conv.weight, g), a.iters)))
+            hip.C.conv_set_wgrad_variant(0)
+            print("   wgrad variants " + "  ".join(f"w{v}: {t:.3f}" for v, t in alt), flush=True)
+        if a.wblocks:
+            alt, keep = [], hip.WGRAD_TARGET_BLOCKS
+            for nb in [int(t) for t in a.wblocks.split(",")]:
+                hip.WGRAD_TARGET_BLOCKS = nb
+                alt.append((nb, timeit(lambda: hip.conv_wgrad_raw(dy, x, conv.weight, g), a.iters)))
+            hip.WGRAD_TARGET_BLOCKS = keep
+            print("   wgrad blocks " + "  ".join(f"{nb}: {t:.3f}" for nb, t in alt), flush=True)
         t_f = timeit(fwd, a.iters)
         t_d = timeit(lambda: hip.conv_dgrad_raw(dy, conv.weight, g), a.iters) if ci != 8 else 0.0
         t_w = timeit(lambda: hip.conv_wgrad_raw(dy, x, conv.weight, g), a.iters)

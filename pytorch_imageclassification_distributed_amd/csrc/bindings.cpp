@@ -109,7 +109,7 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
 }
 
 void conv_wgrad(Tensor dY, Tensor X, Tensor dW, int M, int Cout, int Cin, int Ntot, int OH, int OW, int IH, int IW,
-                int sh, int sw, int pt, int pl, int dh, int dwd, int KW, int k_per_split, int splits) {
+                int sh, int sw, int pt, int pl, int dh, int dwd, int KW, int k_per_split, int splits, Tensor zero) {
   req(dY, BF, "dY"); req(X, BF, "X"); req(dW, F32, "dW");
   TORCH_CHECK(Cin % 8 == 0 && Cout % 8 == 0, "conv_wgrad: channels must be multiples of 8");
   TORCH_CHECK(k_per_split % 64 == 0, "conv_wgrad: k_per_split must be a multiple of 64");
@@ -118,6 +118,7 @@ void conv_wgrad(Tensor dY, Tensor X, Tensor dW, int M, int Cout, int Cin, int Nt
   p.M = M; p.Cout = Cout; p.Cin = Cin; p.Ntot = Ntot; p.OH = OH; p.OW = OW; p.IH = IH; p.IW = IW;
   p.stride_h = sh; p.stride_w = sw; p.pad_t = pt; p.pad_l = pl; p.dil_h = dh; p.dil_w = dwd; p.KW = KW;
   p.k_per_split = k_per_split;
+  p.zero = ptr<bf16_t>(zero);
   check(conv_wgrad_launch(p, splits, cur()), "conv_wgrad");
 }
 
@@ -350,6 +351,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_gemm", &conv_gemm);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_set_variant", &conv_set_variant);
+  m.def("conv_set_wgrad_variant", &conv_set_wgrad_variant);
   m.def("bn_partials", &bn_partials);
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_eval_coef", &bn_eval_coef);

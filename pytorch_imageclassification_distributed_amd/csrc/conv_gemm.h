@@ -44,9 +44,11 @@ struct WgradParams {
   float* dW;           // [Cout][KH*KW][Cin] fp32, accumulated with atomics (pre-zeroed)
   int M, Cout, Cin, Ntot;  // Ntot = KH*KW*Cin
   int OH, OW, IH, IW, stride_h, stride_w, pad_t, pad_l, dil_h, dil_w, KW;
-  int k_per_split;     // pixels (GEMM K) per split, multiple of 32
+  int k_per_split;     // pixels (GEMM K) per split, multiple of 64
+  const bf16_t* zero;  // >= 16 zero bytes (LDS-DMA source of padded chunks)
 };
 
 int conv_gemm_launch(const ConvParams& p, hipStream_t stream);
 void conv_set_variant(int v);  // 0 = auto, 1 = register-staged, 2 = LDS-DMA 2-stage, 3 = LDS-DMA 3-stage
 int conv_wgrad_launch(const WgradParams& p, int splits, hipStream_t stream);
+void conv_set_wgrad_variant(int v);  // 0 = auto, 1 = register-staged, 2 = LDS-DMA

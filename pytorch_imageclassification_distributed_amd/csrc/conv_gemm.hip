@@ -571,6 +571,177 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(const WgradParams p) 
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// weight gradient, LDS-DMA variant.  Images [64 pixels][cols] with 32-B blocks
+// XOR-swizzled per row (phys = blk ^ f(row)) so the ds_read_b64_tr_b16 fragment
+// reads of a 32-lane half (8 consecutive pixel rows) hit 8 distinct bank slots;
+// the swizzle is applied on the LDS-DMA *source* address (lane-linear dest).
+// ---------------------------------------------------------------------------
+DEVI int fdiv(int n, int d, float inv, int& rem) {
+  int q = (int)((float)n * inv);
+  int r = n - q * d;
+  if (r < 0) { --q; r += d; } else if (r >= d) { ++q; r -= d; }
+  rem = r;
+  return q;
+}
+
+template <int ROWB>
+DEVI int wswz(int row) {  // XOR mask on the 32-B block index
+  return ROWB == 256 ? (row & 7) : ((row >> 1) & 3);
+}
+
+template <int WBM>
+__global__ __launch_bounds__(NT, 2) void conv_wgrad_glds_kernel(const WgradParams p) {
+  constexpr int AROWB = WBM * 2;            // A image row bytes (128 / 256)
+  constexpr int BROWB = WBN * 2;            // 256
+  constexpr int A_BYTES = WBK * AROWB;
+  constexpr int B_BYTES = WBK * BROWB;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int WTM = WBM / 2, WTN = WBN / 2;
+  constexpr int RM = WTM / 16, RN = WTN / 16;
+  constexpr int ARPI = 1024 / AROWB;        // rows per LDS-DMA instruction (8 / 4)
+  constexpr int AL = WBK / ARPI / 4;        // instructions per wave per stage (2 / 4)
+  constexpr int BRPI = 1024 / BROWB;        // 4
+  constexpr int BL = WBK / BRPI / 4;        // 4
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int gm = (p.Cout + WBM - 1) / WBM;
+  const int tile = blockIdx.x;
+  const int bm = tile % gm, bn = tile / gm;
+  const int co0 = bm * WBM, j0 = bn * WBN;
+  const int kbeg = blockIdx.y * p.k_per_split;
+  const int kend = min(p.M, kbeg + p.k_per_split);
+  const int ohw = p.OH * p.OW;
+  const float inv_ohw = 1.f / (float)ohw, inv_ow = 1.f / (float)p.OW;
+
+  // A (dY): lane -> (row in instruction, 16-B chunk) ; logical column chunk after unswizzle
+  const int a_lr = lane / (AROWB / 16), a_pc = lane % (AROWB / 16);
+  int a_col[AL];
+  bool a_cok[AL];
+#pragma unroll
+  for (int i = 0; i < AL; ++i) {
+    const int row = (wid * AL + i) * ARPI + a_lr;
+    const int lchunk = (((a_pc >> 1) ^ wswz<AROWB>(row)) << 1) | (a_pc & 1);
+    a_col[i] = co0 + lchunk * 8;
+    a_cok[i] = a_col[i] < p.Cout;
+  }
+  // B (X gather): per instruction the logical column -> (tap, ci) is fixed over k-steps
+  const int b_lr = lane >> 4, b_pc = lane & 15;
+  int b_ci[BL], b_dh[BL], b_dw[BL];
+  bool b_cok[BL];
+#pragma unroll
+  for (int i = 0; i < BL; ++i) {
+    const int row = (wid * BL + i) * BRPI + b_lr;
+    const int lchunk = (((b_pc >> 1) ^ wswz<BROWB>(row)) << 1) | (b_pc & 1);
+    const int j = j0 + lchunk * 8;
+    b_cok[i] = j < p.Ntot;
+    const int tap = b_cok[i] ? j / p.Cin : 0;
+    b_ci[i] = j - tap * p.Cin;
+    const int r = tap / p.KW, c = tap - r * p.KW;
+    b_dh[i] = r * p.dil_h - p.pad_t;
+    b_dw[i] = c * p.dil_w - p.pad_l;
+  }
+
+  auto issue = [&](int k0, int buf) {
+    char* sa = smem + buf * STAGE;
+    char* sb = sa + A_BYTES;
+    const bf16_t* srca[AL];
+    const bf16_t* srcb[BL];
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      const int m = k0 + (wid * AL + i) * ARPI + a_lr;
+      srca[i] = (a_cok[i] && m < kend) ? p.dY + (long)m * p.Cout + a_col[i] : p.zero;
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      const int m = k0 + (wid * BL + i) * BRPI + b_lr;
+      int rem, ow;
+      const int n = fdiv(m, ohw, inv_ohw, rem);
+      const int oh = fdiv(rem, p.OW, inv_ow, ow);
+      const int ih = oh * p.stride_h + b_dh[i], iw = ow * p.stride_w + b_dw[i];
+      const bool ok = b_cok[i] && m < kend && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+      srcb[i] = ok ? p.X + (((long)n * p.IH + ih) * p.IW + iw) * p.Cin + b_ci[i] : p.zero;
+    }
+#pragma unroll
+    for (int i = 0; i < AL; ++i) glds16(srca[i], sa + (wid * AL + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < BL; ++i) glds16(srcb[i], sb + (wid * BL + i) * 1024);
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (kend - kbeg + WBK - 1) / WBK;
+  if (nk <= 0) return;
+  issue(kbeg, 0);
+  const int g = lane >> 4, li = lane & 15;
+  const int tq = li >> 2, tp = li & 3;
+  for (int kt = 0; kt < nk; ++kt) {
+    wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    if (kt + 1 < nk) issue(kbeg + (kt + 1) * WBK, (kt + 1) & 1);
+    const char* sa = smem + (kt & 1) * STAGE;
+    const char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      // permuted k order (identical for A and B): elements 0-3 <- rows 4g+q, 4-7 <- rows 16+4g+q
+      const int r0 = kk * 32 + 4 * g + tq, r1 = r0 + 16;
+      bf16x8 af[RM], bfg[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+        const int blk = (wm * WTM + i * 16) >> 4;
+        const bf16x4 lo = tr_read(sa + r0 * AROWB + ((blk ^ wswz<AROWB>(r0)) << 5) + tp * 8);
+        const bf16x4 hi = tr_read(sa + r1 * AROWB + ((blk ^ wswz<AROWB>(r1)) << 5) + tp * 8);
+        af[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const int blk = (wn * WTN + j * 16) >> 4;
+        const bf16x4 lo = tr_read(sb + r0 * BROWB + ((blk ^ wswz<BROWB>(r0)) << 5) + tp * 8);
+        const bf16x4 hi = tr_read(sb + r1 * BROWB + ((blk ^ wswz<BROWB>(r1)) << 5) + tp * 8);
+        bfg[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[j], af[i], acc[i][j], 0, 0, 0);
+    }
+  }
+  const int fr = lane & 15, fq = lane >> 4;
+  // acc[i][j][r] = dW[co0 + wm*WTM + i*16 + fr][j0 + wn*WTN + j*16 + fq*4 + r]: 4 consecutive columns
+  // per lane -> one 16-B LDS write; the fp32 tile is staged through LDS in row halves of WTM rows and
+  // added to global memory with atomics whose wave-instructions each cover 256 contiguous bytes.
+  constexpr int LDT = WBN + 4;  // floats per staged row
+  static_assert(WTM * LDT * 4 <= 2 * STAGE, "wgrad epilogue staging");
+  float* st = (float*)smem;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    __syncthreads();
+    if (wm == half) {
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          *(f32x4*)(st + (i * 16 + fr) * LDT + wn * WTN + j * 16 + fq * 4) = acc[i][j];
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int e = tid; e < WTM * WBN; e += NT) {  // consecutive lanes -> consecutive floats
+      const int row = e / WBN, c = e - row * WBN;
+      const int co = co0 + half * WTM + row, col = j0 + c;
+      if (co < p.Cout && col < p.Ntot) atomicAdd(p.dW + (long)co * p.Ntot + col, st[row * LDT + c]);
+    }
+  }
+}
+
 }  // namespace
 
 static int g_variant = 0;
@@ -601,15 +772,21 @@ int conv_gemm_launch(const ConvParams& p, hipStream_t stream) {
   return 0;
 }
 
+static int g_wvariant = 0;
+void conv_set_wgrad_variant(int v) { g_wvariant = v; }
+
 int conv_wgrad_launch(const WgradParams& p, int splits, hipStream_t stream) {
   if (p.M <= 0) return 0;
   const int gn = cdiv(p.Ntot, WBN);
+  const bool dma = g_wvariant != 1;
   if (p.Cout <= 64) {
     const int gm = cdiv(p.Cout, 64);
-    hipLaunchKernelGGL(conv_wgrad_kernel<64>, dim3(gm * gn, splits), dim3(NT), 0, stream, p);
+    if (dma) hipLaunchKernelGGL(conv_wgrad_glds_kernel<64>, dim3(gm * gn, splits), dim3(NT), 0, stream, p);
+    else hipLaunchKernelGGL(conv_wgrad_kernel<64>, dim3(gm * gn, splits), dim3(NT), 0, stream, p);
   } else {
     const int gm = cdiv(p.Cout, 128);
-    hipLaunchKernelGGL(conv_wgrad_kernel<128>, dim3(gm * gn, splits), dim3(NT), 0, stream, p);
+    if (dma) hipLaunchKernelGGL(conv_wgrad_glds_kernel<128>, dim3(gm * gn, splits), dim3(NT), 0, stream, p);
+    else hipLaunchKernelGGL(conv_wgrad_kernel<128>, dim3(gm * gn, splits), dim3(NT), 0, stream, p);
   }
   HIP_CHECK_LAUNCH();
   return 0;

@@ -15,6 +15,7 @@ Nothing here falls back to ATen math: a missing extension raises.
 from __future__ import annotations
 
 import math
+import os
 import weakref
 
 import numpy as np
@@ -235,12 +236,53 @@ def conv_dgrad_raw(dy, w_param, g: ConvGeom):
     return dx
 
 
-def _wgrad_split(m, tiles):
-    splits = max(1, min(-(-1024 // max(tiles, 1)), -(-m // 512)))
+WGRAD_TARGET_BLOCKS = int(os.environ.get("IMGCLS_WGRAD_BLOCKS", "0"))  # 0 = autotune per shape
+WGRAD_MIN_K = int(os.environ.get("IMGCLS_WGRAD_MIN_K", "512"))
+WGRAD_CANDIDATES = (256, 512, 1024, 2048)
+_WGRAD_TUNED: dict = {}
+
+
+def _wgrad_split(m, tiles, target):
+    splits = max(1, min(-(-target // max(tiles, 1)), -(-m // WGRAD_MIN_K)))
     kps = -(-m // splits)
     kps = -(-kps // 64) * 64
     splits = -(-m // kps)
     return kps, splits
+
+
+def _wgrad_launch(dy, x, out, g: ConvGeom, m, ntot, kps, splits):
+    C.conv_wgrad(dy, x, out, m, g.Co, g.Cx, ntot, g.OH, g.OW, g.H, g.W, g.sh, g.sw, g.pt, g.pl,
+                 g.dil, g.dil, g.kw, kps, splits, ws(dy.device).zero)
+
+
+def _wgrad_target(dy, x, g: ConvGeom, m, ntot, tiles):
+    """Split-K block target: fixed by IMGCLS_WGRAD_BLOCKS, else timed once per shape (cached).
+
+    Tuning runs on a scratch gradient buffer, outside any graph capture, the first time a shape
+    is seen (warmup), like a conv-algorithm "find" step."""
+    if WGRAD_TARGET_BLOCKS > 0:
+        return WGRAD_TARGET_BLOCKS
+    key = (g.N, g.Cx, g.H, g.W, g.Co, g.kh, g.kw, g.sh, g.pt, g.pl, g.dil)
+    best = _WGRAD_TUNED.get(key)
+    if best is not None:
+        return best
+    if torch.cuda.is_current_stream_capturing():
+        return 512
+    scratch = torch.zeros(g.Co * ntot, dtype=torch.float32, device=dy.device)
+    times = {}
+    for cand in WGRAD_CANDIDATES:
+        kps, splits = _wgrad_split(m, tiles, cand)
+        _wgrad_launch(dy, x, scratch, g, m, ntot, kps, splits)  # warm
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(3):
+            _wgrad_launch(dy, x, scratch, g, m, ntot, kps, splits)
+        b.record()
+        b.synchronize()
+        times[cand] = a.elapsed_time(b)
+    best = min(times, key=times.get)
+    _WGRAD_TUNED[key] = best
+    return best
 
 
 def conv_wgrad_raw(dy, x, w_param, g: ConvGeom):
@@ -248,15 +290,13 @@ def conv_wgrad_raw(dy, x, w_param, g: ConvGeom):
     m = g.N * g.OH * g.OW
     ntot = g.T * g.Cx
     tiles = (-(-g.Co // (64 if g.Co <= 64 else 128))) * (-(-ntot // 128))
-    kps, splits = _wgrad_split(m, tiles)
+    kps, splits = _wgrad_split(m, tiles, _wgrad_target(dy, x, g, m, ntot, tiles))
     if g.Cx == g.Ci:
         dw = torch.zeros_like(w_param, memory_format=CL)
-        C.conv_wgrad(dy, x, dw, m, g.Co, g.Cx, ntot, g.OH, g.OW, g.H, g.W, g.sh, g.sw, g.pt, g.pl,
-                     g.dil, g.dil, g.kw, kps, splits)
+        _wgrad_launch(dy, x, dw, g, m, ntot, kps, splits)
         return dw
     full = torch.zeros(g.Co * ntot, dtype=torch.float32, device=dev)
-    C.conv_wgrad(dy, x, full, m, g.Co, g.Cx, ntot, g.OH, g.OW, g.H, g.W, g.sh, g.sw, g.pt, g.pl,
-                 g.dil, g.dil, g.kw, kps, splits)
+    _wgrad_launch(dy, x, full, g, m, ntot, kps, splits)
     dw = torch.empty_like(w_param, memory_format=CL)
     C.grad_unpad(full, dw, g.Co * g.T, g.Cx, g.Ci)
     return dw

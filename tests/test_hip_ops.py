@@ -75,6 +75,21 @@ def test_conv_fwd_bwd(case):
     assert rel_err(conv.weight.grad, wr.grad) < 2e-2
 
 
+@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("case", [CONV_CASES[1], CONV_CASES[3], CONV_CASES[7], CONV_CASES[10], CONV_CASES[12]])
+def test_conv_kernel_variants(case, variant):
+    """Every fwd/dgrad kernel variant (register-staged, LDS-DMA 2/3-stage) and both wgrad
+    variants produce the same numbers as the fp32 reference."""
+    hip = _hip()
+    hip.C.conv_set_variant(variant)
+    hip.C.conv_set_wgrad_variant(1 if variant == 1 else 2)
+    try:
+        test_conv_fwd_bwd(case)
+    finally:
+        hip.C.conv_set_variant(0)
+        hip.C.conv_set_wgrad_variant(0)
+
+
 def test_stem_padded_input():
     """Cin=3 image -> prepare_input pads to 8 channels; weight padded inside the op."""
     hip = _hip()
