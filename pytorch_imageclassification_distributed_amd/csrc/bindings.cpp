@@ -90,7 +90,8 @@ constexpr auto F32 = at::kFloat;
 
 void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols, int K, int CA, int GH, int GW,
                int IH, int IW, int sA, int ldb, int OH, int OW, int so, int oh0, int ow0, int ldc, int c_off,
-               std::vector<int> dh, std::vector<int> dw, std::vector<int> tb, int stats_groups, Tensor zero) {
+               std::vector<int> dh, std::vector<int> dw, std::vector<int> tb, int stats_groups, Tensor zero,
+               OT addend, OT bwd_y, OT bwd_res, OT bwd_coef, OT bwd_part, int bwd_act, int bwd_groups) {
   req(A, BF, "A"); req(B, BF, "B"); req(C, BF, "C");
   TORCH_CHECK(zero.is_cuda() && zero.nbytes() >= 16, "conv_gemm: zero page must be >= 16 device bytes");
   TORCH_CHECK(CA % 8 == 0 && Ncols % 8 == 0 && ldc % 8 == 0 && c_off % 8 == 0, "conv_gemm: channel counts must be multiples of 8");
@@ -105,6 +106,19 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
   p.ntaps = (int)dh.size(); p.stats_groups = stats_groups > 0 ? stats_groups : 1;
   p.zero = ptr<bf16_t>(zero);
   for (size_t i = 0; i < dh.size(); ++i) { p.tap_dh[i] = dh[i]; p.tap_dw[i] = dw[i]; p.tap_b[i] = tb[i]; }
+  p.addend = optr<bf16_t>(addend);
+  p.bwd_y = optr<bf16_t>(bwd_y);
+  p.bwd_res = optr<bf16_t>(bwd_res);
+  p.bwd_coef = optr<float>(bwd_coef);
+  p.bwd_part = optr<float>(bwd_part);
+  p.bwd_act = bwd_act;
+  p.bwd_groups = bwd_groups > 0 ? bwd_groups : 1;
+  if (p.bwd_y) {
+    TORCH_CHECK(bwd_y->numel() == C.numel() && p.bwd_coef && p.bwd_part && c_off == 0,
+                "conv_gemm: fused BN-backward needs y matching C, coefficients and a partial buffer");
+    TORCH_CHECK(!p.bwd_res || bwd_res->numel() == C.numel(), "conv_gemm: bwd_res must match C");
+  }
+  if (p.addend) TORCH_CHECK(addend->numel() == C.numel() && addend->scalar_type() == BF, "conv_gemm: addend must match C");
   check(conv_gemm_launch(p, cur()), "conv_gemm");
 }
 

@@ -32,6 +32,15 @@ struct ConvParams {
   int OH, OW, so, oh0, ow0, ldc, c_off;
   int ntaps, stats_groups;
   const bf16_t* zero;  // >= 16 zero bytes: source of padded / out-of-range LDS-DMA chunks
+  const bf16_t* addend;  // optional: C += addend (same indexing as C) - fused gradient accumulation
+  // optional fused BatchNorm-backward reduce (dgrad of a conv whose input is act(bn(y) [+res])):
+  // the epilogue turns the gradient g into dz = act'(y*scale+shift[+res]) * g, writes dz and
+  // accumulates per-channel (sum dz, sum dz*xhat) into bwd_part rows.  bwd_coef = [scale|shift|mean|invstd].
+  const bf16_t* bwd_y;
+  const bf16_t* bwd_res;
+  const float* bwd_coef;
+  float* bwd_part;
+  int bwd_act, bwd_groups;
   int tap_dh[CONV_MAX_TAPS];
   int tap_dw[CONV_MAX_TAPS];
   int tap_b[CONV_MAX_TAPS];

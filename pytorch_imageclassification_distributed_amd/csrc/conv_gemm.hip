@@ -89,11 +89,23 @@ DEVI void conv_epilogue(const ConvParams& p, f32x4 (&acc)[BM / 32][BN / 32], cha
   float s8[8], q8[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { s8[k] = 0.f; q8[k] = 0.f; }
+  const bool bwd = p.bwd_y != nullptr;
+  float bsc[8], bsh[8], bmu[8], bis[8];
+  if (bwd && col_ok) {
+    const int C = p.Ncols;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      bsc[k] = p.bwd_coef[col + k];
+      bsh[k] = p.bwd_coef[C + col + k];
+      bmu[k] = p.bwd_coef[2 * C + col + k];
+      bis[k] = p.bwd_coef[3 * C + col + k];
+    }
+  }
 #pragma unroll 4
   for (int row = srow; row < BM; row += RPP) {
     const int m = m0 + row;
     if (m < p.M && col_ok) {
-      const uint4 v = *(const uint4*)(ct + row * CST + sch * 8);
+      uint4 v = *(const uint4*)(ct + row * CST + sch * 8);
       long pix;
       if (direct) {
         pix = m;
@@ -101,6 +113,33 @@ DEVI void conv_epilogue(const ConvParams& p, f32x4 (&acc)[BM / 32][BN / 32], cha
         const int n = m / ghw, r = m - n * ghw;
         const int gh = r / p.GW, gw = r - gh * p.GW;
         pix = ((long)n * p.OH + gh * p.so + p.oh0) * p.OW + gw * p.so + p.ow0;
+      }
+      if (p.addend != nullptr) {
+        float f[8], a[8];
+        unpack8(v, f);
+        unpack8(*(const uint4*)(p.addend + pix * p.ldc + p.c_off + col), a);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) f[k] += a[k];
+        v = pack8(f);
+      }
+      if (bwd) {
+        float gv[8], yv[8], rv[8];
+        unpack8(v, gv);
+        unpack8(*(const uint4*)(p.bwd_y + pix * p.ldc + col), yv);
+        if (p.bwd_res) unpack8(*(const uint4*)(p.bwd_res + pix * p.ldc + col), rv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float dz = gv[k];
+          if (p.bwd_act != ACT_NONE) {
+            float z = yv[k] * bsc[k] + bsh[k];
+            if (p.bwd_res) z += rv[k];
+            dz = act_grad(z, gv[k], p.bwd_act);
+          }
+          gv[k] = dz;
+          s8[k] += dz;
+          q8[k] += dz * (yv[k] - bmu[k]) * bis[k];
+        }
+        v = pack8(gv);
       }
       *(uint4*)(p.C + pix * p.ldc + p.c_off + col) = v;
       if (p.stats != nullptr) {
@@ -111,7 +150,9 @@ DEVI void conv_epilogue(const ConvParams& p, f32x4 (&acc)[BM / 32][BN / 32], cha
       }
     }
   }
-  if (p.stats != nullptr) {
+  float* const stat_dst = p.stats != nullptr ? p.stats : (bwd ? p.bwd_part : nullptr);
+  const int stat_groups = p.stats != nullptr ? p.stats_groups : p.bwd_groups;
+  if (stat_dst != nullptr) {
     // lanes with equal sch inside a wave: tid, tid+CPR, ... (stride CPR); reduce over the wave
 #pragma unroll
     for (int o = CPR; o < 64; o <<= 1) {
@@ -138,7 +179,7 @@ DEVI void conv_epilogue(const ConvParams& p, f32x4 (&acc)[BM / 32][BN / 32], cha
         s += red[(w * 2 + 0) * BN + tid];
         q += red[(w * 2 + 1) * BN + tid];
       }
-      float* dst = p.stats + (size_t)(bm % p.stats_groups) * 2 * p.Ncols + n0 + tid;
+      float* dst = stat_dst + (size_t)(bm % stat_groups) * 2 * p.Ncols + n0 + tid;
       atomicAdd(dst, s);
       atomicAdd(dst + p.Ncols, q);
     }

@@ -38,12 +38,14 @@ class BasicBlock(nn.Module):
         self.stride = stride
 
     def forward(self, x):
+        slot = Fx.grad_slot(x)  # x feeds conv1 and the identity/downsample branch
         if self.downsample is not None:
-            identity = Fx.conv_bn_act(x, self.downsample[0], self.downsample[1], None)
+            identity = Fx.conv_bn_act(x, self.downsample[0], self.downsample[1], None, x_slot=slot)
         else:
             identity = x
-        out = Fx.conv_bn_act(x, self.conv1, self.bn1, "relu")
-        return Fx.conv_bn_act(out, self.conv2, self.bn2, "relu", residual=identity)
+        out = Fx.conv_bn_act(x, self.conv1, self.bn1, "relu", x_slot=slot)
+        return Fx.conv_bn_act(out, self.conv2, self.bn2, "relu", residual=identity,
+                              res_slot=None if self.downsample is not None else slot, exclusive_input=True)
 
 
 class Bottleneck(nn.Module):
@@ -63,13 +65,15 @@ class Bottleneck(nn.Module):
         self.stride = stride
 
     def forward(self, x):
+        slot = Fx.grad_slot(x)  # x feeds conv1 and the identity/downsample branch
         if self.downsample is not None:
-            identity = Fx.conv_bn_act(x, self.downsample[0], self.downsample[1], None)
+            identity = Fx.conv_bn_act(x, self.downsample[0], self.downsample[1], None, x_slot=slot)
         else:
             identity = x
-        out = Fx.conv_bn_act(x, self.conv1, self.bn1, "relu")
-        out = Fx.conv_bn_act(out, self.conv2, self.bn2, "relu")
-        return Fx.conv_bn_act(out, self.conv3, self.bn3, "relu", residual=identity)
+        out = Fx.conv_bn_act(x, self.conv1, self.bn1, "relu", x_slot=slot)
+        out = Fx.conv_bn_act(out, self.conv2, self.bn2, "relu", exclusive_input=True)
+        return Fx.conv_bn_act(out, self.conv3, self.bn3, "relu", residual=identity,
+                              res_slot=None if self.downsample is not None else slot, exclusive_input=True)
 
 
 class ResNet(nn.Module):

@@ -103,7 +103,14 @@ def _torch_bn(x, bn):
 # ---------------------------------------------------------------------------
 # primitives
 # ---------------------------------------------------------------------------
-def conv_bn_act(x, conv, bn, act="relu", residual=None):
+def grad_slot(x):
+    """A paired-gradient slot for a tensor with exactly two consumers (HIP path; None otherwise)."""
+    if use_hip(x) and x.requires_grad and torch.is_grad_enabled():
+        return _hip().GradSlot()
+    return None
+
+
+def conv_bn_act(x, conv, bn, act="relu", residual=None, x_slot=None, res_slot=None, exclusive_input=False):
     """act(bn(conv(x)) [+ residual]).
 
     Reference equivalents: torchvision ``BasicConv2d`` (conv -> BN -> ReLU),
@@ -111,7 +118,7 @@ def conv_bn_act(x, conv, bn, act="relu", residual=None):
     efficientnet_pytorch ``MBConvBlock`` (conv -> BN -> swish).
     """
     if use_hip(x):
-        return _hip().conv_bn_act(x, conv, bn, act, residual)
+        return _hip().conv_bn_act(x, conv, bn, act, residual, x_slot, res_slot, exclusive_input)
     y = _torch_bn(_torch_conv(x, conv), bn)
     if residual is not None:
         y = y + residual

@@ -30,6 +30,8 @@ CL = torch.channels_last
 BF16 = torch.bfloat16
 ACT = {None: 0, "relu": 1, "silu": 2}
 G_STATS = 64  # rotating partial rows for BN statistics atomics
+FUSE_BN_BWD = os.environ.get("IMGCLS_FUSE_BN_BWD", "1") == "1"  # BN-backward reduce in the consumer's dgrad
+FUSED_BWD_COUNT = [0]  # number of BN-backward reduces served by a conv epilogue (tests / diagnostics)
 
 
 # ---------------------------------------------------------------------------
@@ -218,12 +220,21 @@ def conv_forward_raw(x, w_param, g: ConvGeom, stats=None, bias=None, out=None, c
     if g.sh != g.sw:
         raise NotImplementedError("anisotropic stride")
     C.conv_gemm(x, wb, y, stats, bias, g.N * g.OH * g.OW, g.Co, g.T * g.Cx, g.Cx, g.OH, g.OW, g.H, g.W,
-                g.sh, g.T * g.Cx, g.OH, g.OW, 1, 0, 0, ldc, c_off, dh, dw, tb, G_STATS, ws(dev).zero)
+                g.sh, g.T * g.Cx, g.OH, g.OW, 1, 0, 0, ldc, c_off, dh, dw, tb, G_STATS, ws(dev).zero, None,
+                None, None, None, None, 0, 1)
     return y
 
 
-def conv_dgrad_raw(dy, w_param, g: ConvGeom):
+def conv_dgrad_raw(dy, w_param, g: ConvGeom, addend=None, link=None):
+    """dX = conv_transpose(dY, W) [+ addend], one MFMA GEMM per sub-pixel phase.
+
+    With ``link`` (the producer BN of the conv input) the epilogue instead emits
+    dz = act'(z) * dX and the producer's BN-backward partial sums (fused reduce)."""
     dev = dy.device
+    bwd = (None, None, None, None, 0, 1)
+    if link is not None:
+        link.part = torch.zeros(G_STATS * 2 * g.Ci, dtype=torch.float32, device=dev)
+        bwd = (link.y, link.res, link.coef, link.part, link.act, G_STATS)
     wb = weight_bf16(w_param)
     wt = torch.empty(g.Ci * g.T * g.Co, dtype=BF16, device=dev)
     C.weight_t(wb, wt, g.Co, g.T, g.Ci)
@@ -232,7 +243,7 @@ def conv_dgrad_raw(dy, w_param, g: ConvGeom):
         if gh <= 0 or gw <= 0:
             continue
         C.conv_gemm(dy, wt, dx, None, None, g.N * gh * gw, g.Ci, len(tb) * g.Co, g.Co, gh, gw, g.OH, g.OW,
-                    1, g.T * g.Co, g.H, g.W, g.sh, ph, pw, g.Ci, 0, dh, dw, tb, 1, ws(dev).zero)
+                    1, g.T * g.Co, g.H, g.W, g.sh, ph, pw, g.Ci, 0, dh, dw, tb, 1, ws(dev).zero, addend, *bwd)
     return dx
 
 
@@ -302,13 +313,54 @@ def conv_wgrad_raw(dy, x, w_param, g: ConvGeom):
     return dw
 
 
+class GradSlot:
+    """Pairs the two backward contributions to one tensor's gradient (e.g. a ResNet block input
+    feeding conv1 and the identity / downsample branch).  The first consumer to run backward parks
+    its gradient here and reports none to autograd; the second adds the parked one - inside its
+    dgrad epilogue when it is a convolution - so autograd's separate accumulation pass disappears.
+    Order-independent; only valid when exactly two consumers share the slot."""
+
+    __slots__ = ("t",)
+
+    def __init__(self):
+        self.t = None
+
+    def deliver(self, grad, fused=False):
+        """Return what the consumer should hand to autograd."""
+        if self.t is None:
+            self.t = grad
+            return None
+        if fused:  # `grad` already contains the parked contribution
+            self.t = None
+            return grad
+        out = torch.empty_like(grad, memory_format=CL)
+        C.add(_cl(grad), _cl(self.t), out)
+        self.t = None
+        return out
+
+
+class BwdLink:
+    """Ties a BN(+act) output to the conv that consumes it, so the consumer's dgrad epilogue can run
+    the producer's BN-backward reduce (``done`` tells the producer its gradient arrives as dz)."""
+
+    __slots__ = ("y", "coef", "res", "act", "part", "done")
+
+    def __init__(self):
+        self.y = self.coef = self.res = self.part = None
+        self.act = 0
+        self.done = False
+
+
 class ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, conv, want_stats):
+    def forward(ctx, x, w, conv, want_stats, slot=None, fuse_bwd=False):
         g = ConvGeom(x, conv)
         stats = ws(x.device).stats_buf(g.Co) if want_stats else None
         y = conv_forward_raw(x, w, g, stats=stats)
         ctx.g = g
+        ctx.slot = slot
+        link = getattr(x, "_imgcls_link", None) if (fuse_bwd or slot is not None) else None
+        ctx.link = link if (link is not None and link.y is not None and g.Cx == g.Ci) else None
         ctx.save_for_backward(x, w)
         return y
 
@@ -317,9 +369,25 @@ class ConvFn(torch.autograd.Function):
         x, w = ctx.saved_tensors
         g = ctx.g
         dy = _cl(dy)
-        dx = conv_dgrad_raw(dy, w, g) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            slot, link = ctx.slot, ctx.link
+            if link is not None and link.done:
+                link = None
+            if slot is not None and slot.t is None:  # first of a pair: park the partial gradient
+                dx = slot.deliver(conv_dgrad_raw(dy, w, g))
+            elif slot is not None and g.Cx == g.Ci:  # second of a pair: fused accumulation (+ BN reduce)
+                dx = slot.deliver(conv_dgrad_raw(dy, w, g, addend=slot.t, link=link), fused=True)
+                if link is not None:
+                    link.done = True
+            else:
+                dx = conv_dgrad_raw(dy, w, g, link=link)
+                if link is not None:
+                    link.done = True
+                if slot is not None:
+                    dx = slot.deliver(dx)
         dw = conv_wgrad_raw(dy, x, w, g) if ctx.needs_input_grad[1] else None
-        return dx, dw, None, None
+        return dx, dw, None, None, None, None
 
 
 # ---------------------------------------------------------------------------
@@ -358,7 +426,7 @@ class DwConvFn(torch.autograd.Function):
 # ---------------------------------------------------------------------------
 class BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, y, gamma, beta, res, bn, act, stats_ready):
+    def forward(ctx, y, gamma, beta, res, bn, act, stats_ready, res_slot=None, link=None):
         dev = y.device
         n, c, h, w = y.shape
         rows = n * h * w
@@ -390,6 +458,11 @@ class BNActFn(torch.autograd.Function):
         C.bn_apply(y, coef, res, out, rows, c, c, 0, a)
         ctx.act, ctx.group, ctx.rows, ctx.c = a, group, rows, c
         ctx.count_t = count_t
+        ctx.res_slot = res_slot
+        ctx.link = None
+        if link is not None and bn.training:  # (grad mode is always off inside forward)
+            link.y, link.coef, link.res, link.act = y, coef, res, a
+            ctx.link = link
         ctx.has_res = res is not None
         ctx.save_for_backward(y, coef, res if res is not None else y)
         return out
@@ -401,9 +474,16 @@ class BNActFn(torch.autograd.Function):
         dev = y.device
         c, rows = ctx.c, ctx.rows
         g = _cl(gout)
-        part = ws(dev).stats_buf(c)
-        dz = torch.empty_like(y, memory_format=CL) if ctx.has_res else None
-        C.bn_bwd_reduce(g, y, coef, res, dz, rows, c, ctx.act, part, G_STATS)
+        link = ctx.link
+        if link is not None and link.done:
+            # the consuming conv's dgrad epilogue already produced dz and the partial sums
+            part, dz = link.part, g
+            FUSED_BWD_COUNT[0] += 1
+            link.y = link.coef = link.res = link.part = None
+        else:
+            part = ws(dev).stats_buf(c)
+            dz = torch.empty_like(y, memory_format=CL) if ctx.has_res else None
+            C.bn_bwd_reduce(g, y, coef, res, dz, rows, c, ctx.act, part, G_STATS)
         sums = torch.empty(2 * c, dtype=torch.float64, device=dev)
         dgamma = torch.empty(c, dtype=torch.float32, device=dev)
         dbeta = torch.empty(c, dtype=torch.float32, device=dev)
@@ -414,10 +494,15 @@ class BNActFn(torch.autograd.Function):
         C.bn_bwd_k(sums, ctx.count_t, float(rows), c, k)
         dy = torch.empty_like(y, memory_format=CL)
         C.bn_bwd_elemt(None if dz is not None else g, y, coef, k, res, dz, dy, rows, c, ctx.act)
-        return dy, dgamma, dbeta, dz, None, None, None
+        dres = dz if ctx.has_res else None
+        if dres is not None and ctx.res_slot is not None:
+            dres = ctx.res_slot.deliver(dres)
+        return dy, dgamma, dbeta, dres, None, None, None, None, None
 
 
-def conv_bn_act(x, conv, bn, act, residual):
+def conv_bn_act(x, conv, bn, act, residual, x_slot=None, res_slot=None, exclusive_input=False):
+    """``exclusive_input``: this conv is the only consumer of ``x`` (lets its dgrad fuse the BN-backward
+    reduce of x's producer); a slot-paired consumer qualifies automatically."""
     x = _cl(x)
     if residual is not None:
         residual = _cl(residual)
@@ -431,11 +516,15 @@ def conv_bn_act(x, conv, bn, act, residual):
     else:
         if conv.groups != 1:
             raise NotImplementedError("grouped convolution")
-        y = ConvFn.apply(x, conv.weight, conv, bn.training)
+        y = ConvFn.apply(x, conv.weight, conv, bn.training, x_slot, exclusive_input and FUSE_BN_BWD)
         ready = bn.training
     if conv.bias is not None:
         raise NotImplementedError("conv bias before BatchNorm")
-    return BNActFn.apply(y, bn.weight, bn.bias, residual, bn, act, ready)
+    link = BwdLink() if (FUSE_BN_BWD and bn.training and torch.is_grad_enabled()) else None
+    out = BNActFn.apply(y, bn.weight, bn.bias, residual, bn, act, ready, res_slot, link)
+    if link is not None:
+        out._imgcls_link = link
+    return out
 
 
 class ConvBiasFn(torch.autograd.Function):

@@ -12,5 +12,6 @@ timeout -k 10 300 python bench.py --steps 30 --warmup 10 $BENCH_ARGS > gpurun_ou
 echo "bench rc=$rc"; tail -1 gpurun_out/bench_hip.log; fatal $rc bench
 timeout -k 10 300 python bench.py --steps 20 --warmup 10 --batch 512 > gpurun_out/bench_hip512.log 2>&1; rc=$?
 echo "bench512 rc=$rc"; tail -1 gpurun_out/bench_hip512.log; fatal $rc bench512
-timeout -k 10 400 python bench.py --compute torch --steps 20 --warmup 10 --batch 512 > gpurun_out/bench_torch512.log 2>&1; rc=$?
-echo "bench torch512 rc=$rc"; tail -1 gpurun_out/bench_torch512.log; fatal $rc bench_torch512
+export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/prof_q" -o hip -- python3 "$ROOT/bench.py" --steps 5 --warmup 3 > gpurun_out/prof_q.log 2>&1; rc=$?
+echo "prof rc=$rc"; fatal $rc prof

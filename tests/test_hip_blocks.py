@@ -1,0 +1,60 @@
+"""Residual blocks on the HIP path: gradients with the fused paired-gradient slots must equal the
+gradients autograd produces when the two contributions are summed separately."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _grads(block, x, use_slots):
+    """use_slots=False: no paired slots and no BN-backward fusion (plain autograd accumulation +
+    standalone BN reduce kernel) - the reference the fused path must match."""
+    from pytorch_imageclassification_distributed_amd.ops import functional as Fx
+    from pytorch_imageclassification_distributed_amd.ops import hip
+    orig, orig_fuse = Fx.grad_slot, hip.FUSE_BN_BWD
+    if not use_slots:
+        Fx.grad_slot = lambda t: None
+        hip.FUSE_BN_BWD = False
+    try:
+        for p in block.parameters():
+            p.grad = None
+        xx = x.clone().requires_grad_(True)
+        out = block(xx)
+        (out.float() * torch.linspace(-1, 1, out.numel(), device=DEV).view_as(out)).sum().backward()
+    finally:
+        Fx.grad_slot = orig
+        hip.FUSE_BN_BWD = orig_fuse
+    return xx.grad.float(), {n: p.grad.float().clone() for n, p in block.named_parameters()}
+
+
+@pytest.mark.parametrize("kind", ["basic_id", "basic_ds", "bottle_id", "bottle_ds", "chain"])
+def test_block_slots(kind):
+    import torch.nn as nn
+    from pytorch_imageclassification_distributed_amd.models.resnet import BasicBlock, Bottleneck, _conv1x1
+    torch.manual_seed(0)
+    if kind == "basic_id":
+        blk, cin = BasicBlock(64, 64), 64
+    elif kind == "basic_ds":
+        blk, cin = BasicBlock(64, 128, 2, nn.Sequential(_conv1x1(64, 128, 2), nn.BatchNorm2d(128))), 64
+    elif kind == "bottle_id":
+        blk, cin = Bottleneck(256, 64), 256
+    elif kind == "bottle_ds":
+        blk, cin = Bottleneck(256, 128, 2, nn.Sequential(_conv1x1(256, 512, 2), nn.BatchNorm2d(512))), 256
+    else:  # two blocks: the second block's fused dgrad runs the first block's BN3 backward reduce
+        blk = nn.Sequential(Bottleneck(256, 128, 2, nn.Sequential(_conv1x1(256, 512, 2), nn.BatchNorm2d(512))),
+                            Bottleneck(512, 128))
+        cin = 256
+    blk = blk.to(DEV).to(memory_format=torch.channels_last)
+    x = torch.randn(4, cin, 16, 16, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    from pytorch_imageclassification_distributed_amd.ops import hip
+    gx0, gp0 = _grads(blk, x, False)
+    before = hip.FUSED_BWD_COUNT[0]
+    gx1, gp1 = _grads(blk, x, True)
+    fused = hip.FUSED_BWD_COUNT[0] - before
+    expect = {"basic_id": 1, "basic_ds": 1, "bottle_id": 2, "bottle_ds": 2, "chain": 5}[kind]
+    assert fused == expect, (kind, fused)
+    err = lambda a, b: ((a - b).abs().max() / b.abs().max().clamp(min=1e-6)).item()  # noqa: E731
+    assert err(gx1, gx0) < 2e-2, err(gx1, gx0)
+    for n in gp0:
+        assert err(gp1[n], gp0[n]) < 2e-2, (n, err(gp1[n], gp0[n]))

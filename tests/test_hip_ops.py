@@ -319,3 +319,23 @@ def test_resnet18_matches_reference_path():
         c_t = F.cosine_similarity(gbf[k], g32[k], dim=0).item()
         print(f"{k}: cos(hip, fp32)={c_h:.4f} cos(torch-bf16, fp32)={c_t:.4f}")
         assert c_h > min(0.98, c_t - 0.05), (k, c_h, c_t)
+
+
+def test_grad_slot_fused_accumulation():
+    """Block input feeding two convs: the slot-fused dgrad (epilogue addend) equals autograd's sum."""
+    hip = _hip()
+    torch.manual_seed(9)
+    c1 = nn.Conv2d(64, 32, 1, bias=False).to(DEV).to(memory_format=CL)
+    c2 = nn.Conv2d(64, 128, 1, 2, bias=False).to(DEV).to(memory_format=CL)
+    x = torch.randn(2, 64, 14, 14, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=CL)
+    xa = x.clone().requires_grad_(True)
+    slot = hip.GradSlot()
+    ya = hip.ConvFn.apply(xa, c1.weight, c1, False, slot)
+    za = hip.ConvFn.apply(xa, c2.weight, c2, False, slot)
+    (ya.float().square().sum() + za.float().sum()).backward()
+    xb = x.clone().requires_grad_(True)
+    yb = hip.ConvFn.apply(xb, c1.weight, c1, False)
+    zb = hip.ConvFn.apply(xb, c2.weight, c2, False)
+    (yb.float().square().sum() + zb.float().sum()).backward()
+    assert slot.t is None
+    assert rel_err(xa.grad, xb.grad) < 1e-2
