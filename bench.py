@@ -90,6 +90,12 @@ def main():
     for i in range(a.warmup):
         last = step(i)
     torch.cuda.synchronize()
+    # host enqueue cost of one step (diagnostic, stderr): > ms_per_step would mean CPU-bound
+    t_host = time.perf_counter()
+    last = step(0)
+    t_host = time.perf_counter() - t_host
+    torch.cuda.synchronize()
+    print(f"[bench] rank {ctx.rank}: host enqueue {t_host * 1e3:.1f} ms/step", file=sys.stderr, flush=True)
     if not torch.isfinite(last).item():
         raise FloatingPointError(f"non-finite loss in warmup: {last.item()}")
     barrier(ctx)

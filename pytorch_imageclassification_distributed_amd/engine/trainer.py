@@ -35,6 +35,7 @@ from torch.utils.data.distributed import DistributedSampler
 from ..data import CudaPrefetcher, ImageDataset, SyntheticImageDataset
 from ..models import DEFAULT_IMAGE_SIZE, Classifier
 from ..ops import functional as Fx
+from ..ops.grad_arena import GradArena
 from ..parallel import GradReducer, convert_sync_batchnorm
 from ..utils import (BEST, LATEST, AccuracyCounter, DeviceMeter, JsonlLogger, load_checkpoint,
                      load_model_state, resolve_resume, save_checkpoint)
@@ -90,6 +91,7 @@ class Trainer:
         model = Classifier(self.name, self.num_classes, pretrained=a.pretrained).to(self.dev)
         self.ddp = None
         self.reducer = None
+        self.arena = None
         self.autocast = False
         if self.dev.type == "cuda" and not self.hip:
             # reference stack: torch DDP + SyncBatchNorm (+ bf16 autocast)
@@ -111,6 +113,10 @@ class Trainer:
             if ctx.world_size > 1:
                 comm = torch.bfloat16 if a.comm_dtype == "bf16" else None
                 self.reducer = GradReducer(model, bucket_cap_mb=a.bucket_mb, comm_dtype=comm)
+                self.arena = self.reducer.arena
+            elif self.hip:
+                params = [p for p in model.parameters() if p.requires_grad]
+                self.arena = GradArena(params, list(reversed(range(len(params)))))
             self.net = model
         self.model = model
         self.optimizer = FusedAdam(model.parameters(), lr=a.lr)
@@ -133,6 +139,8 @@ class Trainer:
         """forward + loss + backward + (overlapped) all-reduce + Adam.  Returns the local loss."""
         loss = self.compute_loss(images, labels)
         self.optimizer.zero_grad(set_to_none=True)
+        if self.arena is not None:
+            self.arena.begin()  # one memset; backward kernels write into persistent slots
         loss.backward()
         scale = self.reducer.finish() if self.reducer is not None else 1.0
         self.optimizer.step(grad_scale=scale)

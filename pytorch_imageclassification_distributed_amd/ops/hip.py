@@ -23,6 +23,7 @@ import torch
 import torch.distributed as dist
 
 from .. import _ext
+from .grad_arena import grad_buffer
 
 C = _ext.load()
 
@@ -42,6 +43,19 @@ class _Workspace:
         self.dev = dev
         self.stats = torch.zeros(0, dtype=torch.float32, device=dev)
         self.zero = torch.zeros(64, dtype=BF16, device=dev)  # zero page for padded LDS-DMA chunks
+        self.parts: list = []  # zeroed partial-stat buffers for fused BN-backward reduces
+
+    def take_part(self, c: int) -> torch.Tensor:
+        """A zeroed partial-sum buffer for a fused BN-backward reduce; handed back by ``give_part``
+        after ``bn_partials`` has read (and re-zeroed) it, so the pool never needs a memset."""
+        need = G_STATS * 2 * c
+        for i, b in enumerate(self.parts):
+            if b.numel() >= need:
+                return self.parts.pop(i)
+        return torch.zeros(max(need, G_STATS * 2 * 2048), dtype=torch.float32, device=self.dev)
+
+    def give_part(self, b: torch.Tensor) -> None:
+        self.parts.append(b)
 
     def stats_buf(self, c: int) -> torch.Tensor:
         need = G_STATS * 2 * c
@@ -233,7 +247,7 @@ def conv_dgrad_raw(dy, w_param, g: ConvGeom, addend=None, link=None):
     dev = dy.device
     bwd = (None, None, None, None, 0, 1)
     if link is not None:
-        link.part = torch.zeros(G_STATS * 2 * g.Ci, dtype=torch.float32, device=dev)
+        link.part = ws(dev).take_part(g.Ci)
         bwd = (link.y, link.res, link.coef, link.part, link.act, G_STATS)
     wb = weight_bf16(w_param)
     wt = torch.empty(g.Ci * g.T * g.Co, dtype=BF16, device=dev)
@@ -303,12 +317,12 @@ def conv_wgrad_raw(dy, x, w_param, g: ConvGeom):
     tiles = (-(-g.Co // (64 if g.Co <= 64 else 128))) * (-(-ntot // 128))
     kps, splits = _wgrad_split(m, tiles, _wgrad_target(dy, x, g, m, ntot, tiles))
     if g.Cx == g.Ci:
-        dw = torch.zeros_like(w_param, memory_format=CL)
+        dw = grad_buffer(w_param)
         _wgrad_launch(dy, x, dw, g, m, ntot, kps, splits)
         return dw
     full = torch.zeros(g.Co * ntot, dtype=torch.float32, device=dev)
     _wgrad_launch(dy, x, full, g, m, ntot, kps, splits)
-    dw = torch.empty_like(w_param, memory_format=CL)
+    dw = grad_buffer(w_param, zero=False)
     C.grad_unpad(full, dw, g.Co * g.T, g.Cx, g.Ci)
     return dw
 
@@ -416,7 +430,7 @@ class DwConvFn(torch.autograd.Function):
             C.dw_dgrad(dy, wt, dx, g.N, g.H, g.W, g.Co, g.OH, g.OW, g.kh, g.kw, g.sh, g.sw, g.pt, g.pl)
         dw = None
         if ctx.needs_input_grad[1]:
-            dw = torch.zeros_like(w)
+            dw = grad_buffer(w)
             C.dw_wgrad(dy, x, dw, g.N, g.H, g.W, g.Co, g.OH, g.OW, g.kh, g.kw, g.sh, g.sw, g.pt, g.pl)
         return dx, dw, None
 
@@ -464,6 +478,7 @@ class BNActFn(torch.autograd.Function):
             link.y, link.coef, link.res, link.act = y, coef, res, a
             ctx.link = link
         ctx.has_res = res is not None
+        ctx.params = (gamma, beta)
         ctx.save_for_backward(y, coef, res if res is not None else y)
         return out
 
@@ -485,9 +500,11 @@ class BNActFn(torch.autograd.Function):
             dz = torch.empty_like(y, memory_format=CL) if ctx.has_res else None
             C.bn_bwd_reduce(g, y, coef, res, dz, rows, c, ctx.act, part, G_STATS)
         sums = torch.empty(2 * c, dtype=torch.float64, device=dev)
-        dgamma = torch.empty(c, dtype=torch.float32, device=dev)
-        dbeta = torch.empty(c, dtype=torch.float32, device=dev)
+        dgamma = grad_buffer(ctx.params[0], zero=False)
+        dbeta = grad_buffer(ctx.params[1], zero=False)
         C.bn_partials(part, G_STATS, c, sums, dgamma, dbeta)
+        if link is not None and link.done:
+            ws(dev).give_part(part)
         if ctx.group is not None:
             dist.all_reduce(sums, group=ctx.group)
         k = torch.empty(2 * c, dtype=torch.float32, device=dev)
@@ -536,6 +553,7 @@ class ConvBiasFn(torch.autograd.Function):
         y = conv_forward_raw(x, w, g, bias=b)
         ctx.g = g
         ctx.has_b = b is not None
+        ctx.bias = b
         ctx.save_for_backward(x, w)
         return y
 
@@ -551,7 +569,7 @@ class ConvBiasFn(torch.autograd.Function):
             part = ws(dy.device).stats_buf(g.Co)
             C.bn_stats(dy, g.N * g.OH * g.OW, g.Co, part, G_STATS)
             sums = torch.empty(2 * g.Co, dtype=torch.float64, device=dy.device)
-            db = torch.empty(g.Co, dtype=torch.float32, device=dy.device)
+            db = grad_buffer(ctx.bias, zero=False)
             C.bn_partials(part, G_STATS, g.Co, sums, None, db)
         return dx, dw, db, None
 
@@ -669,6 +687,7 @@ class MlpFn(torch.autograd.Function):
             acts.append(y)
             h = y
         ctx.relus = relus
+        ctx.params = wb
         ctx.nb = [b is not None for b in wb[1::2]]
         ctx.save_for_backward(*acts, *[w for w in wb[0::2]])
         return h
@@ -686,12 +705,12 @@ class MlpFn(torch.autograd.Function):
             nout, nin = w.shape
             xin, yout = acts[i], acts[i + 1]
             mask = yout if ctx.relus[i] else None
-            dw = torch.empty((nout, nin), dtype=torch.float32, device=g.device)
+            dw = grad_buffer(ctx.params[2 * i], zero=False)
             # dW[o][f] = sum_b g[b][o] * x[b][f]   (A(m=o,k=b) = g[b][o])
             _mm(g, xin, dw, nout, nin, mb, 1, nout, nin, 1, mask=mask, smm=1, smk=nout)
             grads[2 * i] = dw
             if ctx.nb[i]:
-                db = torch.empty(nout, dtype=torch.float32, device=g.device)
+                db = grad_buffer(ctx.params[2 * i + 1], zero=False)
                 C.colsum(g, mask, db, mb, nout, nout, False)
                 grads[2 * i + 1] = db
             if i > 0 or ctx.needs_input_grad[0]:
@@ -898,7 +917,7 @@ class SEFn(torch.autograd.Function):
         C.se_scale(x, s, y, n, hw, c)
         ctx.save_for_backward(x, p, hpre, a, s, wr2, we2)
         ctx.geo = (n, c, hw, nsq)
-        ctx.shapes = (wr.shape, we.shape)
+        ctx.params = (wr, br, we, be)
         return y
 
     @staticmethod
@@ -911,24 +930,24 @@ class SEFn(torch.autograd.Function):
         C.se_ds(dy, x, ds, n, hw, c)
         de = torch.empty_like(ds)
         C.act32_bwd(s, ds, de, 2)
-        dwe = torch.empty((c, nsq), dtype=torch.float32, device=dev)
+        wr, br, we, be = ctx.params
+        dwe = grad_buffer(we, zero=False)  # [c][nsq](1x1) in memory for either weight layout
         _mm(de, a, dwe, c, nsq, n, 1, c, nsq, 1)
-        dbe = torch.empty(c, dtype=torch.float32, device=dev)
+        dbe = grad_buffer(be, zero=False)
         C.colsum(de, None, dbe, n, c, c, False)
         da = torch.empty((n, nsq), dtype=torch.float32, device=dev)
         _mm(de, we2, da, n, nsq, c, c, 1, nsq, 1)
         dh = torch.empty_like(da)
         C.act32_bwd(hpre, da, dh, 0)
-        dwr = torch.empty((nsq, c), dtype=torch.float32, device=dev)
+        dwr = grad_buffer(wr, zero=False)
         _mm(dh, p, dwr, nsq, c, n, 1, nsq, c, 1)
-        dbr = torch.empty(nsq, dtype=torch.float32, device=dev)
+        dbr = grad_buffer(br, zero=False)
         C.colsum(dh, None, dbr, n, nsq, nsq, False)
         dp = torch.empty((n, c), dtype=torch.float32, device=dev)
         _mm(dh, wr2, dp, n, c, nsq, nsq, 1, c, 1)
         dx = torch.empty_like(dy, memory_format=CL)
         C.se_dx(dy, s, dp, dx, n, hw, c)
-        wrs, wes = ctx.shapes
-        return dx, dwr.reshape(wrs), dbr, dwe.reshape(wes), dbe
+        return dx, dwr, dbr, dwe, dbe
 
 
 def se_gate(x, se_reduce, se_expand):
@@ -970,8 +989,9 @@ def adam_build_table(opt, items):
             if not _same_memory_order(p, p.grad):
                 raise RuntimeError("fused Adam: gradient layout differs from parameter layout")
         dev = ps[0].device
-        tab = torch.from_numpy(recs.view(np.uint8).copy()).to(dev)
-        ck = torch.tensor(chunks, dtype=torch.int32).reshape(-1).to(dev)
+        # pinned + non_blocking: a pageable H2D copy would stall the host until the GPU drains
+        tab = torch.from_numpy(recs.view(np.uint8).copy()).pin_memory().to(dev, non_blocking=True)
+        ck = torch.tensor(chunks, dtype=torch.int32).reshape(-1).pin_memory().to(dev, non_blocking=True)
         lr_step = getattr(opt, "_lr_step", {}).get(gi)
         if lr_step is None:
             step0 = float(opt.state[ps[0]]["step"]) if "step" in opt.state[ps[0]] else 0.0

@@ -10,8 +10,9 @@ MI355X design:
 * every gradient lives in ONE flat fp32 buffer laid out in bucket order, so a
   bucket is a contiguous slice (one RCCL call, no pack/unpack) and the fused
   Adam kernel reads gradients in place;
-* a ``post_accumulate_grad`` hook per parameter copies the freshly produced
-  gradient into its slot and, when the bucket's last gradient lands, launches an
+* the flat buffer is a ``GradArena``: our backward kernels write each gradient
+  straight into its slot (``ops.grad_arena``), so the ``post_accumulate_grad``
+  hook only copies gradients produced elsewhere (ATen ops), and, when the bucket's last gradient lands, launches an
   *asynchronous* RCCL all-reduce.  ProcessGroupNCCL runs it on its own HIP
   stream after an event wait on the compute stream, so the reduction of early
   buckets overlaps the rest of backward; ``finish()`` makes the compute stream
@@ -34,7 +35,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-_ALIGN = 64  # elements (256 B) so every slot starts on a cache-line boundary
+from ..ops.grad_arena import GradArena
 
 
 def broadcast_module_state(module: nn.Module, src: int = 0, group=None) -> None:
@@ -71,7 +72,7 @@ class GradReducer:
         self._rebuild_pending = rebuild_buckets and self.world > 1
         self._ready_order: list[int] = []
         self.works: list = []
-        self.flat: torch.Tensor | None = None
+        self.arena: GradArena | None = None
         if broadcast:
             broadcast_module_state(module, 0, group)
         self._build(list(reversed(range(len(self.params)))))
@@ -79,37 +80,35 @@ class GradReducer:
 
     # ------------------------------------------------------------------ layout
     def _build(self, order: list[int]) -> None:
-        old_flat, old_views = self.flat, getattr(self, "views", None)
-        dev = self.params[0].device
-        offsets = [0] * len(self.params)
-        buckets, cur, cur_start, off = [], [], 0, 0
+        if self.arena is None:
+            self.arena = GradArena(self.params, order)
+        else:
+            self.arena.layout(order)
+        offsets = self.arena.offsets
+        buckets, cur, cur_start = [], [], 0
         cap = self.first_cap
         for i in order:
-            p = self.params[i]
-            n = p.numel()
-            if cur and (off - cur_start) + n > cap:
+            off = offsets[i]
+            if cur and off - cur_start + self.params[i].numel() > cap:
                 buckets.append((cur_start, off, cur))
                 cur, cur_start, cap = [], off, self.bucket_cap
-            offsets[i] = off
             cur.append(i)
-            off += (n + _ALIGN - 1) // _ALIGN * _ALIGN
         if cur:
-            buckets.append((cur_start, off, cur))
-        self.flat = torch.zeros(off, dtype=torch.float32, device=dev)
-        self.views = [torch.as_strided(self.flat, p.size(), p.stride(), offsets[i])
-                      for i, p in enumerate(self.params)]
+            buckets.append((cur_start, self.arena.flat.numel(), cur))
         self.buckets = buckets
         self.bucket_of = [0] * len(self.params)
         for b, (_s, _e, idx) in enumerate(buckets):
             for i in idx:
                 self.bucket_of[i] = b
         self._reset_counts()
-        if old_flat is not None:
-            with torch.no_grad():
-                for i, p in enumerate(self.params):
-                    self.views[i].copy_(old_views[i])
-                    if p.grad is not None:
-                        p.grad = self.views[i]
+
+    @property
+    def flat(self) -> torch.Tensor:
+        return self.arena.flat
+
+    def begin(self) -> None:
+        """Zero and arm the gradient slots before a backward (one memset)."""
+        self.arena.begin()
 
     def _reset_counts(self) -> None:
         self.pending = [len(idx) for (_s, _e, idx) in self.buckets]
@@ -123,8 +122,8 @@ class GradReducer:
     @torch.no_grad()
     def _on_grad(self, p: torch.Tensor) -> None:
         i = self.index[id(p)]
-        v = self.views[i]
-        if p.grad is not v:
+        if not self.arena.owns(p):
+            v = self.arena.view(i)
             v.copy_(p.grad)
             p.grad = v
         if self._rebuild_pending:
@@ -158,8 +157,9 @@ class GradReducer:
         """
         for i, p in enumerate(self.params):  # parameters that got no gradient
             if not self.got[i]:
-                self.views[i].zero_()
-                p.grad = self.views[i]
+                v = self.arena.view(i)
+                v.zero_()
+                p.grad = v
                 self.got[i] = True
                 b = self.bucket_of[i]
                 self.pending[b] -= 1
@@ -196,3 +196,4 @@ class GradReducer:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        self.arena.detach_params()

@@ -9,7 +9,7 @@ timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.lo
 echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log; fatal $rc pytest
 [ $rc -eq 0 ] || exit 1
 timeout -k 10 300 python bench.py --steps 30 --warmup 10 $BENCH_ARGS > gpurun_out/bench_hip.log 2>&1; rc=$?
-echo "bench rc=$rc"; tail -1 gpurun_out/bench_hip.log; fatal $rc bench
+echo "bench rc=$rc"; grep -h "host enqueue" gpurun_out/bench_hip.log; tail -1 gpurun_out/bench_hip.log; fatal $rc bench
 timeout -k 10 300 python bench.py --steps 20 --warmup 10 --batch 512 > gpurun_out/bench_hip512.log 2>&1; rc=$?
 echo "bench512 rc=$rc"; tail -1 gpurun_out/bench_hip512.log; fatal $rc bench512
 export TMPDIR=/tmp

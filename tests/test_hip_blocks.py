@@ -58,3 +58,47 @@ def test_block_slots(kind):
     assert err(gx1, gx0) < 2e-2, err(gx1, gx0)
     for n in gp0:
         assert err(gp1[n], gp0[n]) < 2e-2, (n, err(gp1[n], gp0[n]))
+
+
+@pytest.mark.parametrize("model_name", ["resnet18", "efficientnet-b0"])
+def test_grad_arena(model_name):
+    """Backward kernels write gradients straight into the persistent arena slots: same values as
+    freshly allocated gradients, every .grad aliases its slot, a second backward without begin()
+    accumulates, and the fused Adam pointer table is built once across steps."""
+    from pytorch_imageclassification_distributed_amd.engine.optim import FusedAdam
+    from pytorch_imageclassification_distributed_amd.models import Classifier
+    from pytorch_imageclassification_distributed_amd.ops.grad_arena import GradArena
+    torch.manual_seed(0)
+    m = Classifier(model_name, 5).to(DEV).to(memory_format=torch.channels_last).train()
+    x = torch.randn(4, 3, 64, 64, device=DEV)
+    params = [p for p in m.parameters() if p.requires_grad]
+
+    def loss_fn():
+        torch.manual_seed(1)  # same dropout / drop-connect masks every call
+        return m(x).float().square().mean()
+
+    loss_fn().backward()  # no arena: fresh tensors
+    ref = [p.grad.clone() for p in params]
+    arena = GradArena(params, list(reversed(range(len(params)))))
+    for p in params:
+        p.grad = None
+    arena.begin()
+    loss_fn().backward()
+    assert all(arena.owns(p) for p in params), [n for n, p in m.named_parameters() if not arena.owns(p)]
+    for p, r in zip(params, ref):
+        torch.testing.assert_close(p.grad, r, rtol=2e-2, atol=1e-5 + 2e-2 * r.abs().max().item())
+    one = [p.grad.clone() for p in params]
+    loss_fn().backward()  # accumulation without re-arming: slot += new gradient
+    for p, o in zip(params, one):
+        assert arena.owns(p)
+        torch.testing.assert_close(p.grad, 2 * o, rtol=3e-2, atol=1e-5 + 3e-2 * o.abs().max().item())
+    opt = FusedAdam(params, lr=1e-4)
+    keys = set()
+    for _ in range(3):
+        opt.zero_grad(set_to_none=True)
+        arena.begin()
+        loss_fn().backward()
+        opt.step()
+        keys.add(opt._table_key)
+    assert len(keys) == 1
+    torch.cuda.synchronize()
