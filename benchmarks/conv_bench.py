@@ -49,6 +49,7 @@ def main():
     ap.add_argument("--torch", action="store_true", help="also time MIOpen (torch) for each shape")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--variants", default="", help="comma list of conv fwd/dgrad kernel variants to A/B (1,2,3)")
+    ap.add_argument("--single", default="", help="comma list of 1-stage-ring k-step thresholds to A/B (0 = never)")
     ap.add_argument("--wvariants", default="", help="comma list of wgrad kernel variants to A/B (1,2)")
     ap.add_argument("--wblocks", default="", help="comma list of wgrad split-K target block counts to sweep")
     a = ap.parse_args()
@@ -81,6 +82,17 @@ def main():
                             if ci != 8 else 0.0))
             hip.C.conv_set_variant(0)
             print("   variants " + "  ".join(f"v{v}: fwd {tf_:.3f} dgrad {td_:.3f}" for v, tf_, td_ in alt), flush=True)
+        if a.single:
+            alt, keep = [], hip.CONV_STAGES
+            hip.CONV_STAGES = "0"
+            for nk in [int(t) for t in a.single.split(",")]:
+                hip.C.conv_set_single_stage(nk)
+                alt.append((nk, timeit(fwd, a.iters), timeit(lambda: hip.conv_dgrad_raw(dy, conv.weight, g), a.iters)
+                            if ci != 8 else 0.0))
+            hip.C.conv_set_single_stage(4)
+            hip.CONV_STAGES = keep
+            print("   single-stage " + "  ".join(f"nk<={v}: fwd {tf_:.3f} dgrad {td_:.3f}" for v, tf_, td_ in alt),
+                  flush=True)
         if a.wvariants:
             alt = []
             for v in [int(t) for t in a.wvariants.split(",")]:

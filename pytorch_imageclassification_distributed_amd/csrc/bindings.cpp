@@ -91,7 +91,8 @@ constexpr auto F32 = at::kFloat;
 void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols, int K, int CA, int GH, int GW,
                int IH, int IW, int sA, int ldb, int OH, int OW, int so, int oh0, int ow0, int ldc, int c_off,
                std::vector<int> dh, std::vector<int> dw, std::vector<int> tb, int stats_groups, Tensor zero,
-               OT addend, OT bwd_y, OT bwd_res, OT bwd_coef, OT bwd_part, int bwd_act, int bwd_groups) {
+               OT addend, OT bwd_y, OT bwd_res, OT bwd_coef, OT bwd_part, int bwd_act, int bwd_groups,
+               int stages) {
   req(A, BF, "A"); req(B, BF, "B"); req(C, BF, "C");
   TORCH_CHECK(zero.is_cuda() && zero.nbytes() >= 16, "conv_gemm: zero page must be >= 16 device bytes");
   TORCH_CHECK(CA % 8 == 0 && Ncols % 8 == 0 && ldc % 8 == 0 && c_off % 8 == 0, "conv_gemm: channel counts must be multiples of 8");
@@ -113,6 +114,8 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
   p.bwd_part = optr<float>(bwd_part);
   p.bwd_act = bwd_act;
   p.bwd_groups = bwd_groups > 0 ? bwd_groups : 1;
+  TORCH_CHECK(stages >= 0 && stages <= 2, "conv_gemm: stages must be 0 (auto), 1 or 2");
+  p.stages = stages;
   if (p.bwd_y) {
     TORCH_CHECK(bwd_y->numel() == C.numel() && p.bwd_coef && p.bwd_part && c_off == 0,
                 "conv_gemm: fused BN-backward needs y matching C, coefficients and a partial buffer");
@@ -365,6 +368,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_gemm", &conv_gemm);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_set_variant", &conv_set_variant);
+  m.def("conv_set_single_stage", &conv_set_single_stage);
   m.def("conv_set_wgrad_variant", &conv_set_wgrad_variant);
   m.def("bn_partials", &bn_partials);
   m.def("bn_finalize", &bn_finalize);

@@ -41,6 +41,7 @@ struct ConvParams {
   const float* bwd_coef;
   float* bwd_part;
   int bwd_act, bwd_groups;
+  int stages;  // LDS-DMA ring depth: 1 (high occupancy) or 2; 0 = k-step heuristic
   int tap_dh[CONV_MAX_TAPS];
   int tap_dw[CONV_MAX_TAPS];
   int tap_b[CONV_MAX_TAPS];
@@ -59,5 +60,6 @@ struct WgradParams {
 
 int conv_gemm_launch(const ConvParams& p, hipStream_t stream);
 void conv_set_variant(int v);  // 0 = auto, 1 = register-staged, 2 = LDS-DMA 2-stage, 3 = LDS-DMA 3-stage
+void conv_set_single_stage(int nk);  // GEMMs with K <= nk*64 use the 1-stage (high-occupancy) ring
 int conv_wgrad_launch(const WgradParams& p, int splits, hipStream_t stream);
 void conv_set_wgrad_variant(int v);  // 0 = auto, 1 = register-staged, 2 = LDS-DMA

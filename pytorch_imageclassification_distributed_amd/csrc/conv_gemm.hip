@@ -332,7 +332,7 @@ DEVI void glds16(const void* src, char* lds_wave_base) {
 }
 
 template <int BN, int STAGES, bool TAP_UNIFORM>
-__global__ __launch_bounds__(NT, 1) void conv_gemm_glds_kernel(const ConvParams p) {
+__global__ __launch_bounds__(NT, STAGES == 1 ? (BN == 128 ? 3 : 4) : 1) void conv_gemm_glds_kernel(const ConvParams p) {
   constexpr int A_BYTES = BM * BK * 2;
   constexpr int B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
@@ -343,9 +343,10 @@ __global__ __launch_bounds__(NT, 1) void conv_gemm_glds_kernel(const ConvParams 
   constexpr int LPS = AL + BL;
   constexpr int TAP_BYTES = 3 * CONV_MAX_TAPS * 4;
   constexpr int CST = BN + 8;
-  static_assert(BM * CST * 2 <= STAGES * STAGE, "epilogue LDS reuse");
-  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE + TAP_BYTES];
-  int* s_dh = (int*)(smem + STAGES * STAGE);
+  // the epilogue tile reuses the ring; a 1-stage ring (short K) is sized by the epilogue instead
+  constexpr int MAIN = STAGES * STAGE > BM * CST * 2 ? STAGES * STAGE : BM * CST * 2;
+  __shared__ __attribute__((aligned(16))) char smem[MAIN + TAP_BYTES];
+  int* s_dh = (int*)(smem + MAIN);
   int* s_dw = s_dh + CONV_MAX_TAPS;
   int* s_tb = s_dw + CONV_MAX_TAPS;
 
@@ -449,10 +450,18 @@ __global__ __launch_bounds__(NT, 1) void conv_gemm_glds_kernel(const ConvParams 
     if (s < nk) issue(s, s);
   const int fr = lane & 15, fq = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + STAGES - 2 < nk) wait_vmcnt<(STAGES - 2) * LPS>();
-    else wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-    if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+    if constexpr (STAGES == 1) {
+      // no in-block overlap: latency is hidden by the 4 co-resident blocks this LDS size allows
+      if (kt > 0) __builtin_amdgcn_s_barrier();
+      issue(kt, 0);
+      wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+    } else {
+      if (kt + STAGES - 2 < nk) wait_vmcnt<(STAGES - 2) * LPS>();
+      else wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+    }
     const char* sa = smem + (kt % STAGES) * STAGE;
     const char* sb = sa + A_BYTES;
 #pragma unroll
@@ -787,6 +796,8 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_glds_kernel(const WgradParam
 
 static int g_variant = 0;
 void conv_set_variant(int v) { g_variant = v; }
+static int g_single_nk = 4;  // GEMMs with at most this many 64-wide k-steps use the 1-stage ring
+void conv_set_single_stage(int nk) { g_single_nk = nk; }
 
 template <int BN>
 static void launch_bn(const ConvParams& p, int gm, hipStream_t stream) {
@@ -795,6 +806,9 @@ static void launch_bn(const ConvParams& p, int gm, hipStream_t stream) {
   const int v = g_variant == 0 ? 2 : g_variant;  // measured: 2-stage LDS-DMA wins (benchmarks/conv_bench.py --variants)
   if (v == 1) {
     hipLaunchKernelGGL(conv_gemm_kernel<BN>, dim3(gm * gn), dim3(NT), 0, stream, p);
+  } else if (v == 2 && (p.stages == 1 || (p.stages == 0 && cdiv(p.K, BK) <= g_single_nk))) {
+    if (uni) hipLaunchKernelGGL((conv_gemm_glds_kernel<BN, 1, true>), dim3(gm * gn), dim3(NT), 0, stream, p);
+    else hipLaunchKernelGGL((conv_gemm_glds_kernel<BN, 1, false>), dim3(gm * gn), dim3(NT), 0, stream, p);
   } else if (v == 2) {
     if (uni) hipLaunchKernelGGL((conv_gemm_glds_kernel<BN, 2, true>), dim3(gm * gn), dim3(NT), 0, stream, p);
     else hipLaunchKernelGGL((conv_gemm_glds_kernel<BN, 2, false>), dim3(gm * gn), dim3(NT), 0, stream, p);

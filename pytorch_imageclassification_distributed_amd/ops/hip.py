@@ -225,6 +225,48 @@ def _weight_for_input(w_param, cx):
     return out
 
 
+CONV_STAGES = os.environ.get("IMGCLS_CONV_STAGES", "auto")  # auto (timed per shape) | 0 (heuristic) | 1 | 2
+_STAGES_TUNED: dict = {}
+
+
+def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(None, None, None, None, 0, 1)):
+    """One implicit-GEMM launch; the LDS-DMA ring depth (1 = high occupancy, 2 = pipelined) is
+    chosen once per GEMM geometry by timing both on scratch outputs (a conv-algorithm "find")."""
+    if CONV_STAGES != "auto":
+        st = int(CONV_STAGES)
+    else:
+        key = (tuple(geo), out.shape[1], tuple(dh), tuple(dw), stats is not None, bias is not None,
+               addend is not None, bwd[0] is not None, bwd[1] is not None, bwd[4])
+        st = _STAGES_TUNED.get(key)
+        if st is None:
+            st = 0 if torch.cuda.is_current_stream_capturing() else _tune_stages(
+                A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd)
+            if st:
+                _STAGES_TUNED[key] = st
+    C.conv_gemm(A, B, out, stats, bias, *geo, dh, dw, tb, G_STATS, zero, addend, *bwd, st)
+
+
+def _tune_stages(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd):
+    scratch = torch.empty_like(out)
+    sst = torch.zeros_like(stats) if stats is not None else None
+    bwd = tuple(bwd)
+    if bwd[3] is not None:
+        bwd = bwd[:3] + (torch.zeros_like(bwd[3]),) + bwd[4:]
+    times = {}
+    for st in (1, 2):
+        run = lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, G_STATS, zero,  # noqa: E731
+                                  addend, *bwd, st)
+        run()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(3):
+            run()
+        b.record()
+        b.synchronize()
+        times[st] = a.elapsed_time(b)
+    return min(times, key=times.get)
+
+
 def conv_forward_raw(x, w_param, g: ConvGeom, stats=None, bias=None, out=None, c_off=0):
     dev = x.device
     wb = _weight_for_input(w_param, g.Cx)
@@ -233,9 +275,9 @@ def conv_forward_raw(x, w_param, g: ConvGeom, stats=None, bias=None, out=None, c
     dh, dw, tb = _fwd_taps(g)
     if g.sh != g.sw:
         raise NotImplementedError("anisotropic stride")
-    C.conv_gemm(x, wb, y, stats, bias, g.N * g.OH * g.OW, g.Co, g.T * g.Cx, g.Cx, g.OH, g.OW, g.H, g.W,
-                g.sh, g.T * g.Cx, g.OH, g.OW, 1, 0, 0, ldc, c_off, dh, dw, tb, G_STATS, ws(dev).zero, None,
-                None, None, None, None, 0, 1)
+    geo = (g.N * g.OH * g.OW, g.Co, g.T * g.Cx, g.Cx, g.OH, g.OW, g.H, g.W, g.sh, g.T * g.Cx, g.OH, g.OW,
+           1, 0, 0, ldc, c_off)
+    _conv_gemm(x, wb, y, stats, bias, geo, dh, dw, tb, ws(dev).zero)
     return y
 
 
@@ -256,8 +298,9 @@ def conv_dgrad_raw(dy, w_param, g: ConvGeom, addend=None, link=None):
     for ph, pw, gh, gw, dh, dw, tb in _dgrad_phases(g):
         if gh <= 0 or gw <= 0:
             continue
-        C.conv_gemm(dy, wt, dx, None, None, g.N * gh * gw, g.Ci, len(tb) * g.Co, g.Co, gh, gw, g.OH, g.OW,
-                    1, g.T * g.Co, g.H, g.W, g.sh, ph, pw, g.Ci, 0, dh, dw, tb, 1, ws(dev).zero, addend, *bwd)
+        geo = (g.N * gh * gw, g.Ci, len(tb) * g.Co, g.Co, gh, gw, g.OH, g.OW, 1, g.T * g.Co, g.H, g.W, g.sh,
+               ph, pw, g.Ci, 0)
+        _conv_gemm(dy, wt, dx, None, None, geo, dh, dw, tb, ws(dev).zero, addend, bwd)
     return dx
 
 

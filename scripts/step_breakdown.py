@@ -1,0 +1,27 @@
+"""Per-kernel breakdown of ONE steady-state training step from a rocprofv3 kernel trace.
+
+usage: python scripts/step_breakdown.py gpurun_out/prof_q/hip_kernel_trace.csv [marker=adam_kernel]
+The step is the span between the last two launches of the marker kernel (one per optimizer step)."""
+import collections
+import csv
+import re
+import sys
+
+path = sys.argv[1]
+marker = sys.argv[2] if len(sys.argv) > 2 else "adam_kernel"
+rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+idx = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
+a, b = idx[-2], idx[-1]
+step = rows[a + 1:b + 1]
+busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in step)
+span = int(step[-1]["End_Timestamp"]) - int(rows[a]["End_Timestamp"])
+agg = collections.defaultdict(lambda: [0, 0])
+for r in step:
+    name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
+    name = re.sub(r"\((?!\)).*", "", name) or r["Kernel_Name"]
+    name = name[:70]
+    agg[name][0] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    agg[name][1] += 1
+print(f"step span {span / 1e6:.3f} ms, kernel busy {busy / 1e6:.3f} ms, launches {len(step)}")
+for k, (t, n) in sorted(agg.items(), key=lambda kv: -kv[1][0]):
+    print(f"{t / 1e6:8.3f} ms {n:5d}x  {k}")

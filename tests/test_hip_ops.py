@@ -75,18 +75,23 @@ def test_conv_fwd_bwd(case):
     assert rel_err(conv.weight.grad, wr.grad) < 2e-2
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("variant,single", [(1, 1), (2, 0), (2, 1000), (3, 1)])
 @pytest.mark.parametrize("case", [CONV_CASES[1], CONV_CASES[3], CONV_CASES[7], CONV_CASES[10], CONV_CASES[12]])
-def test_conv_kernel_variants(case, variant):
-    """Every fwd/dgrad kernel variant (register-staged, LDS-DMA 2/3-stage) and both wgrad
-    variants produce the same numbers as the fp32 reference."""
+def test_conv_kernel_variants(case, variant, single):
+    """Every fwd/dgrad kernel variant (register-staged, LDS-DMA 1/2/3-stage ring) and both wgrad
+    variants produce the same numbers as the fp32 reference.  ``single`` = largest k-step count
+    that takes the 1-stage ring (0: never, 1000: always)."""
     hip = _hip()
     hip.C.conv_set_variant(variant)
+    hip.C.conv_set_single_stage(single)
     hip.C.conv_set_wgrad_variant(1 if variant == 1 else 2)
+    keep, hip.CONV_STAGES = hip.CONV_STAGES, "0"  # the k-step heuristic, not the per-shape tuner
     try:
         test_conv_fwd_bwd(case)
     finally:
+        hip.CONV_STAGES = keep
         hip.C.conv_set_variant(0)
+        hip.C.conv_set_single_stage(4)
         hip.C.conv_set_wgrad_variant(0)
 
 
