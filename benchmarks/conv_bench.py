@@ -8,6 +8,7 @@ Prints one line per shape and a JSON summary (TFLOP/s = 2*MACs / time).
 from __future__ import annotations
 
 import argparse
+import collections
 import json
 import os
 import sys
@@ -130,6 +131,9 @@ def main():
         if a.torch:
             msg += f" || miopen fwd {r['torch_fwd_ms']:7.3f}ms bwd {r['torch_bwd_ms']:7.3f}ms"
         print(msg, flush=True)
+    print("tuned wgrad (blocks, stages):", {f"{k[4]}<-{k[1]} k{k[5]}s{k[7]} {k[2]}x{k[3]}": v
+                                             for k, v in hip._WGRAD_TUNED.items()})
+    print("tuned fwd/dgrad ring depth:", sorted(collections.Counter(hip._STAGES_TUNED.values()).items()))
     print(json.dumps({"batch": n, "total_ms": tot, "rows": rows}))
 
 

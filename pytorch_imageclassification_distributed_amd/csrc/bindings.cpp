@@ -126,7 +126,8 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
 }
 
 void conv_wgrad(Tensor dY, Tensor X, Tensor dW, int M, int Cout, int Cin, int Ntot, int OH, int OW, int IH, int IW,
-                int sh, int sw, int pt, int pl, int dh, int dwd, int KW, int k_per_split, int splits, Tensor zero) {
+                int sh, int sw, int pt, int pl, int dh, int dwd, int KW, int k_per_split, int splits, Tensor zero,
+                int stages) {
   req(dY, BF, "dY"); req(X, BF, "X"); req(dW, F32, "dW");
   TORCH_CHECK(Cin % 8 == 0 && Cout % 8 == 0, "conv_wgrad: channels must be multiples of 8");
   TORCH_CHECK(k_per_split % 64 == 0, "conv_wgrad: k_per_split must be a multiple of 64");
@@ -136,6 +137,8 @@ void conv_wgrad(Tensor dY, Tensor X, Tensor dW, int M, int Cout, int Cin, int Nt
   p.stride_h = sh; p.stride_w = sw; p.pad_t = pt; p.pad_l = pl; p.dil_h = dh; p.dil_w = dwd; p.KW = KW;
   p.k_per_split = k_per_split;
   p.zero = ptr<bf16_t>(zero);
+  TORCH_CHECK(stages >= 0 && stages <= 2, "conv_wgrad: stages must be 0, 1 or 2");
+  p.stages = stages;
   check(conv_wgrad_launch(p, splits, cur()), "conv_wgrad");
 }
 

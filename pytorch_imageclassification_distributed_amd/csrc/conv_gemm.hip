@@ -641,8 +641,8 @@ DEVI int wswz(int row) {  // XOR mask on the 32-B block index
   return ROWB == 256 ? (row & 7) : ((row >> 1) & 3);
 }
 
-template <int WBM>
-__global__ __launch_bounds__(NT, 2) void conv_wgrad_glds_kernel(const WgradParams p) {
+template <int WBM, int STAGES>
+__global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_wgrad_glds_kernel(const WgradParams p) {
   constexpr int AROWB = WBM * 2;            // A image row bytes (128 / 256)
   constexpr int BROWB = WBN * 2;            // 256
   constexpr int A_BYTES = WBK * AROWB;
@@ -654,7 +654,10 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_glds_kernel(const WgradParam
   constexpr int AL = WBK / ARPI / 4;        // instructions per wave per stage (2 / 4)
   constexpr int BRPI = 1024 / BROWB;        // 4
   constexpr int BL = WBK / BRPI / 4;        // 4
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  constexpr int LDT = WBN + 4;              // floats per staged epilogue row
+  constexpr int EPI = (WBM / 2) * LDT * 4;
+  constexpr int MAIN = STAGES * STAGE > EPI ? STAGES * STAGE : EPI;
+  __shared__ __attribute__((aligned(16))) char smem[MAIN];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -730,14 +733,21 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_glds_kernel(const WgradParam
 
   const int nk = (kend - kbeg + WBK - 1) / WBK;
   if (nk <= 0) return;
-  issue(kbeg, 0);
+  if (STAGES == 2) issue(kbeg, 0);
   const int g = lane >> 4, li = lane & 15;
   const int tq = li >> 2, tp = li & 3;
   for (int kt = 0; kt < nk; ++kt) {
-    wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-    if (kt + 1 < nk) issue(kbeg + (kt + 1) * WBK, (kt + 1) & 1);
-    const char* sa = smem + (kt & 1) * STAGE;
+    if constexpr (STAGES == 1) {  // latency hidden by co-resident blocks instead of the ring
+      if (kt > 0) __builtin_amdgcn_s_barrier();
+      issue(kbeg + kt * WBK, 0);
+      wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+    } else {
+      wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      if (kt + 1 < nk) issue(kbeg + (kt + 1) * WBK, (kt + 1) & 1);
+    }
+    const char* sa = smem + (STAGES == 1 ? 0 : (kt & 1) * STAGE);
     const char* sb = sa + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -769,8 +779,6 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_glds_kernel(const WgradParam
   // acc[i][j][r] = dW[co0 + wm*WTM + i*16 + fr][j0 + wn*WTN + j*16 + fq*4 + r]: 4 consecutive columns
   // per lane -> one 16-B LDS write; the fp32 tile is staged through LDS in row halves of WTM rows and
   // added to global memory with atomics whose wave-instructions each cover 256 contiguous bytes.
-  constexpr int LDT = WBN + 4;  // floats per staged row
-  static_assert(WTM * LDT * 4 <= 2 * STAGE, "wgrad epilogue staging");
   float* st = (float*)smem;
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
@@ -836,11 +844,13 @@ int conv_wgrad_launch(const WgradParams& p, int splits, hipStream_t stream) {
   const bool dma = g_wvariant != 1;
   if (p.Cout <= 64) {
     const int gm = cdiv(p.Cout, 64);
-    if (dma) hipLaunchKernelGGL(conv_wgrad_glds_kernel<64>, dim3(gm * gn, splits), dim3(NT), 0, stream, p);
+    if (dma && p.stages == 1) hipLaunchKernelGGL((conv_wgrad_glds_kernel<64, 1>), dim3(gm * gn, splits), dim3(NT), 0, stream, p);
+    else if (dma) hipLaunchKernelGGL((conv_wgrad_glds_kernel<64, 2>), dim3(gm * gn, splits), dim3(NT), 0, stream, p);
     else hipLaunchKernelGGL(conv_wgrad_kernel<64>, dim3(gm * gn, splits), dim3(NT), 0, stream, p);
   } else {
     const int gm = cdiv(p.Cout, 128);
-    if (dma) hipLaunchKernelGGL(conv_wgrad_glds_kernel<128>, dim3(gm * gn, splits), dim3(NT), 0, stream, p);
+    if (dma && p.stages == 1) hipLaunchKernelGGL((conv_wgrad_glds_kernel<128, 1>), dim3(gm * gn, splits), dim3(NT), 0, stream, p);
+    else if (dma) hipLaunchKernelGGL((conv_wgrad_glds_kernel<128, 2>), dim3(gm * gn, splits), dim3(NT), 0, stream, p);
     else hipLaunchKernelGGL(conv_wgrad_kernel<128>, dim3(gm * gn, splits), dim3(NT), 0, stream, p);
   }
   HIP_CHECK_LAUNCH();

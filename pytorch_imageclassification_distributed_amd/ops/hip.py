@@ -318,36 +318,43 @@ def _wgrad_split(m, tiles, target):
     return kps, splits
 
 
-def _wgrad_launch(dy, x, out, g: ConvGeom, m, ntot, kps, splits):
+WGRAD_STAGES = int(os.environ.get("IMGCLS_WGRAD_STAGES", "0"))  # 0 = tuned with the split count; 1 | 2
+
+
+def _wgrad_launch(dy, x, out, g: ConvGeom, m, ntot, kps, splits, stages=2):
     C.conv_wgrad(dy, x, out, m, g.Co, g.Cx, ntot, g.OH, g.OW, g.H, g.W, g.sh, g.sw, g.pt, g.pl,
-                 g.dil, g.dil, g.kw, kps, splits, ws(dy.device).zero)
+                 g.dil, g.dil, g.kw, kps, splits, ws(dy.device).zero, stages)
 
 
-def _wgrad_target(dy, x, g: ConvGeom, m, ntot, tiles):
-    """Split-K block target: fixed by IMGCLS_WGRAD_BLOCKS, else timed once per shape (cached).
+def _wgrad_config(dy, x, g: ConvGeom, m, ntot, tiles):
+    """(split-K block target, LDS ring depth): fixed by IMGCLS_WGRAD_BLOCKS / IMGCLS_WGRAD_STAGES,
+    else timed jointly once per shape (cached).
 
     Tuning runs on a scratch gradient buffer, outside any graph capture, the first time a shape
     is seen (warmup), like a conv-algorithm "find" step."""
-    if WGRAD_TARGET_BLOCKS > 0:
-        return WGRAD_TARGET_BLOCKS
-    key = (g.N, g.Cx, g.H, g.W, g.Co, g.kh, g.kw, g.sh, g.pt, g.pl, g.dil)
+    blocks = (WGRAD_TARGET_BLOCKS,) if WGRAD_TARGET_BLOCKS > 0 else WGRAD_CANDIDATES
+    stages = (WGRAD_STAGES,) if WGRAD_STAGES > 0 else (1, 2)
+    if len(blocks) == 1 and len(stages) == 1:
+        return blocks[0], stages[0]
+    key = (g.N, g.Cx, g.H, g.W, g.Co, g.kh, g.kw, g.sh, g.pt, g.pl, g.dil, blocks, stages)
     best = _WGRAD_TUNED.get(key)
     if best is not None:
         return best
     if torch.cuda.is_current_stream_capturing():
-        return 512
+        return blocks[len(blocks) // 2], stages[-1]
     scratch = torch.zeros(g.Co * ntot, dtype=torch.float32, device=dy.device)
     times = {}
-    for cand in WGRAD_CANDIDATES:
-        kps, splits = _wgrad_split(m, tiles, cand)
-        _wgrad_launch(dy, x, scratch, g, m, ntot, kps, splits)  # warm
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
-        for _ in range(3):
-            _wgrad_launch(dy, x, scratch, g, m, ntot, kps, splits)
-        b.record()
-        b.synchronize()
-        times[cand] = a.elapsed_time(b)
+    for st in stages:
+        for cand in blocks:
+            kps, splits = _wgrad_split(m, tiles, cand)
+            _wgrad_launch(dy, x, scratch, g, m, ntot, kps, splits, st)  # warm
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(3):
+                _wgrad_launch(dy, x, scratch, g, m, ntot, kps, splits, st)
+            b.record()
+            b.synchronize()
+            times[(cand, st)] = a.elapsed_time(b)
     best = min(times, key=times.get)
     _WGRAD_TUNED[key] = best
     return best
@@ -358,13 +365,14 @@ def conv_wgrad_raw(dy, x, w_param, g: ConvGeom):
     m = g.N * g.OH * g.OW
     ntot = g.T * g.Cx
     tiles = (-(-g.Co // (64 if g.Co <= 64 else 128))) * (-(-ntot // 128))
-    kps, splits = _wgrad_split(m, tiles, _wgrad_target(dy, x, g, m, ntot, tiles))
+    target, stages = _wgrad_config(dy, x, g, m, ntot, tiles)
+    kps, splits = _wgrad_split(m, tiles, target)
     if g.Cx == g.Ci:
         dw = grad_buffer(w_param)
-        _wgrad_launch(dy, x, dw, g, m, ntot, kps, splits)
+        _wgrad_launch(dy, x, dw, g, m, ntot, kps, splits, stages)
         return dw
     full = torch.zeros(g.Co * ntot, dtype=torch.float32, device=dev)
-    _wgrad_launch(dy, x, full, g, m, ntot, kps, splits)
+    _wgrad_launch(dy, x, full, g, m, ntot, kps, splits, stages)
     dw = grad_buffer(w_param, zero=False)
     C.grad_unpad(full, dw, g.Co * g.T, g.Cx, g.Ci)
     return dw

@@ -86,10 +86,12 @@ def test_conv_kernel_variants(case, variant, single):
     hip.C.conv_set_single_stage(single)
     hip.C.conv_set_wgrad_variant(1 if variant == 1 else 2)
     keep, hip.CONV_STAGES = hip.CONV_STAGES, "0"  # the k-step heuristic, not the per-shape tuner
+    keep_w, hip.WGRAD_STAGES = hip.WGRAD_STAGES, (1 if single == 1000 else 2)
     try:
         test_conv_fwd_bwd(case)
     finally:
         hip.CONV_STAGES = keep
+        hip.WGRAD_STAGES = keep_w
         hip.C.conv_set_variant(0)
         hip.C.conv_set_single_stage(4)
         hip.C.conv_set_wgrad_variant(0)
