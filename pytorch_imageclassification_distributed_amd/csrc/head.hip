@@ -17,6 +17,7 @@ struct SgemmArgs {
   int M, N, K;
   long sam, sak, sbk, sbn, ldc, smm, smk;
   int relu, accumulate;
+  int kchunk, atomic;  // split-K: blockIdx.z covers [z*kchunk, (z+1)*kchunk); atomic adds raw partial sums
 };
 
 constexpr int TS = 64, TK = 16;
@@ -27,19 +28,20 @@ __global__ __launch_bounds__(256) void sgemm_kernel(SgemmArgs a) {
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   const int m0 = blockIdx.y * TS, n0 = blockIdx.x * TS;
   float acc[4][4] = {};
-  for (int k0 = 0; k0 < a.K; k0 += TK) {
+  const int kb = blockIdx.z * a.kchunk, ke = min(a.K, kb + a.kchunk);
+  for (int k0 = kb; k0 < ke; k0 += TK) {
     for (int e = threadIdx.x; e < TS * TK; e += 256) {
       const int mm = e / TK, kk = e % TK;  // A tile: k fastest
       const int m = m0 + mm, k = k0 + kk;
       float v = 0.f;
-      if (m < a.M && k < a.K) {
+      if (m < a.M && k < ke) {
         v = a.A[m * a.sam + k * a.sak];
         if (a.mask && !(a.mask[m * a.smm + k * a.smk] > 0.f)) v = 0.f;
       }
       As[kk][mm] = v;
       const int nn = e / TK;
       const int n = n0 + nn;
-      Bs[kk][nn] = (n < a.N && k < a.K) ? a.B[k * a.sbk + n * a.sbn] : 0.f;
+      Bs[kk][nn] = (n < a.N && k < ke) ? a.B[k * a.sbk + n * a.sbn] : 0.f;
     }
     __syncthreads();
 #pragma unroll
@@ -65,6 +67,10 @@ __global__ __launch_bounds__(256) void sgemm_kernel(SgemmArgs a) {
       const int n = n0 + tx * 4 + j;
       if (n >= a.N) continue;
       float v = acc[i][j];
+      if (a.atomic) {
+        atomicAdd(a.C + m * a.ldc + n, v);
+        continue;
+      }
       if (a.bias) v += a.bias[n];
       if (a.accumulate) v += a.C[m * a.ldc + n];
       if (a.relu) v = fmaxf(v, 0.f);
@@ -73,18 +79,34 @@ __global__ __launch_bounds__(256) void sgemm_kernel(SgemmArgs a) {
   }
 }
 
-// column sums: out[n] (+)= sum_m X[m*ld + n] * (mask ? mask[m*ld+n] > 0 : 1)
-__global__ void colsum_kernel(const float* __restrict__ X, const float* __restrict__ mask, float* out,
-                              int M, int N, long ld, int accumulate) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
+// split-K finishing pass: C = act(C + bias)
+__global__ void bias_act_kernel(float* C, const float* __restrict__ bias, int M, int N, long ldc, int relu) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)M * N) return;
+  const int m = (int)(i / N), n = (int)(i - (long)m * N);
+  float v = C[m * ldc + n] + (bias ? bias[n] : 0.f);
+  C[m * ldc + n] = relu ? fmaxf(v, 0.f) : v;
+}
+
+// column sums: out[n] += sum_m X[m*ld + n] * (mask ? mask[m*ld+n] > 0 : 1)
+// block = 64 columns x 4 row lanes over a CS_ROWS-row chunk; one atomic per column per block
+constexpr int CS_ROWS = 32;
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ X, const float* __restrict__ mask,
+                                                     float* out, int M, int N, long ld) {
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, r = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + c;
+  const int m0 = blockIdx.y * CS_ROWS, m1 = min(M, m0 + CS_ROWS);
   float s = 0.f;
-  for (int m = 0; m < M; ++m) {
-    float v = X[m * ld + n];
-    if (mask && !(mask[m * ld + n] > 0.f)) v = 0.f;
-    s += v;
-  }
-  out[n] = accumulate ? out[n] + s : s;
+  if (n < N)
+    for (int m = m0 + r; m < m1; m += 4) {
+      float v = X[m * ld + n];
+      if (mask && !(mask[m * ld + n] > 0.f)) v = 0.f;
+      s += v;
+    }
+  red[r][c] = s;
+  __syncthreads();
+  if (r == 0 && n < N) atomicAdd(out + n, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
 }
 
 // weighted CE forward: loss = sum_i w[y_i] * (lse_i - x_i[y_i]) / sum_i w[y_i]
@@ -141,15 +163,33 @@ __global__ void ce_bwd_kernel(const float* __restrict__ prob, const long long* _
 int sgemm_launch(const float* A, const float* B, float* C, const float* bias, const float* mask, int M, int N,
                  int K, long sam, long sak, long sbk, long sbn, long ldc, long smm, long smk, int relu,
                  int accumulate, hipStream_t s) {
-  SgemmArgs a{A, B, C, bias, mask, M, N, K, sam, sak, sbk, sbn, ldc, smm, smk, relu, accumulate};
-  hipLaunchKernelGGL(sgemm_kernel, dim3(cdiv(N, TS), cdiv(M, TS)), dim3(256), 0, s, a);
+  // split K until the grid covers the chip (these GEMMs are skinny: M = batch, N <= 2048)
+  const int tiles = cdiv(N, TS) * cdiv(M, TS);
+  int splits = 1;
+  while (tiles * splits < 256 && K / (splits * 2) >= 4 * TK) splits *= 2;
+  const int kchunk = cdiv(cdiv(K, splits), TK) * TK;
+  splits = cdiv(K, kchunk);
+  SgemmArgs a{A, B, C, bias, mask, M, N, K, sam, sak, sbk, sbn, ldc, smm, smk, relu, accumulate, kchunk, splits > 1};
+  if (splits > 1 && !accumulate) {
+    if (ldc == N) {
+      if (hipMemsetAsync(C, 0, sizeof(float) * (size_t)M * N, s) != hipSuccess) return 1;
+    } else {
+      return 2;  // strided split-K output without accumulate: not needed by the callers
+    }
+  }
+  hipLaunchKernelGGL(sgemm_kernel, dim3(cdiv(N, TS), cdiv(M, TS), splits), dim3(256), 0, s, a);
   HIP_CHECK_LAUNCH();
+  if (splits > 1 && (bias || relu)) {
+    hipLaunchKernelGGL(bias_act_kernel, dim3(cdiv(M * N, 256)), dim3(256), 0, s, C, bias, M, N, ldc, relu);
+    HIP_CHECK_LAUNCH();
+  }
   return 0;
 }
 
 int colsum_launch(const float* X, const float* mask, float* out, int M, int N, long ld, int accumulate,
                   hipStream_t s) {
-  hipLaunchKernelGGL(colsum_kernel, dim3(cdiv(N, 256)), dim3(256), 0, s, X, mask, out, M, N, ld, accumulate);
+  if (!accumulate && hipMemsetAsync(out, 0, sizeof(float) * (size_t)N, s) != hipSuccess) return 1;
+  hipLaunchKernelGGL(colsum_kernel, dim3(cdiv(N, 64), cdiv(M, CS_ROWS)), dim3(256), 0, s, X, mask, out, M, N, ld);
   HIP_CHECK_LAUNCH();
   return 0;
 }
