@@ -133,7 +133,7 @@ def main():
         print(msg, flush=True)
     print("tuned wgrad (blocks, stages):", {f"{k[4]}<-{k[1]} k{k[5]}s{k[7]} {k[2]}x{k[3]}": v
                                              for k, v in hip._WGRAD_TUNED.items()})
-    print("tuned fwd/dgrad ring depth:", sorted(collections.Counter(hip._STAGES_TUNED.values()).items()))
+    print("tuned fwd/dgrad (ring depth, tile_n):", sorted(collections.Counter(hip._STAGES_TUNED.values()).items()))
     print(json.dumps({"batch": n, "total_ms": tot, "rows": rows}))
 
 

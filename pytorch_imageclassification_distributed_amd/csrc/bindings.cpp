@@ -92,7 +92,7 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
                int IH, int IW, int sA, int ldb, int OH, int OW, int so, int oh0, int ow0, int ldc, int c_off,
                std::vector<int> dh, std::vector<int> dw, std::vector<int> tb, int stats_groups, Tensor zero,
                OT addend, OT bwd_y, OT bwd_res, OT bwd_coef, OT bwd_part, int bwd_act, int bwd_groups,
-               int stages) {
+               int stages, int tile_n) {
   req(A, BF, "A"); req(B, BF, "B"); req(C, BF, "C");
   TORCH_CHECK(zero.is_cuda() && zero.nbytes() >= 16, "conv_gemm: zero page must be >= 16 device bytes");
   TORCH_CHECK(CA % 8 == 0 && Ncols % 8 == 0 && ldc % 8 == 0 && c_off % 8 == 0, "conv_gemm: channel counts must be multiples of 8");
@@ -116,6 +116,8 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
   p.bwd_groups = bwd_groups > 0 ? bwd_groups : 1;
   TORCH_CHECK(stages >= 0 && stages <= 2, "conv_gemm: stages must be 0 (auto), 1 or 2");
   p.stages = stages;
+  TORCH_CHECK(tile_n == 0 || tile_n == 64 || tile_n == 128, "conv_gemm: tile_n must be 0, 64 or 128");
+  p.tile_n = tile_n;
   if (p.bwd_y) {
     TORCH_CHECK(bwd_y->numel() == C.numel() && p.bwd_coef && p.bwd_part && c_off == 0,
                 "conv_gemm: fused BN-backward needs y matching C, coefficients and a partial buffer");

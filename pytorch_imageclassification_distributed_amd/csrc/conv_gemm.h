@@ -42,6 +42,7 @@ struct ConvParams {
   float* bwd_part;
   int bwd_act, bwd_groups;
   int stages;  // LDS-DMA ring depth: 1 (high occupancy) or 2; 0 = k-step heuristic
+  int tile_n;  // output-channel tile: 64 or 128; 0 = 64 iff Ncols <= 64
   int tap_dh[CONV_MAX_TAPS];
   int tap_dw[CONV_MAX_TAPS];
   int tap_b[CONV_MAX_TAPS];

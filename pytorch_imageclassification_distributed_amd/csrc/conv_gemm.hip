@@ -829,7 +829,7 @@ static void launch_bn(const ConvParams& p, int gm, hipStream_t stream) {
 int conv_gemm_launch(const ConvParams& p, hipStream_t stream) {
   if (p.M <= 0 || p.Ncols <= 0) return 0;
   const int gm = cdiv(p.M, BM);
-  if (p.Ncols <= 64) launch_bn<64>(p, gm, stream);
+  if (p.Ncols <= 64 || p.tile_n == 64) launch_bn<64>(p, gm, stream);
   else launch_bn<128>(p, gm, stream);
   HIP_CHECK_LAUNCH();
   return 0;

@@ -230,32 +230,36 @@ _STAGES_TUNED: dict = {}
 
 
 def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(None, None, None, None, 0, 1)):
-    """One implicit-GEMM launch; the LDS-DMA ring depth (1 = high occupancy, 2 = pipelined) is
-    chosen once per GEMM geometry by timing both on scratch outputs (a conv-algorithm "find")."""
+    """One implicit-GEMM launch.  The kernel configuration - LDS-DMA ring depth (1 = high occupancy,
+    2 = pipelined) x output-channel tile (64 / 128: more tiles balance 256 CUs better on small
+    layers) - is chosen once per GEMM geometry by timing the candidates on scratch outputs (a
+    conv-algorithm "find" step)."""
     if CONV_STAGES != "auto":
-        st = int(CONV_STAGES)
+        cfg = (int(CONV_STAGES), 0)
     else:
         key = (tuple(geo), out.shape[1], tuple(dh), tuple(dw), stats is not None, bias is not None,
                addend is not None, bwd[0] is not None, bwd[1] is not None, bwd[4])
-        st = _STAGES_TUNED.get(key)
-        if st is None:
-            st = 0 if torch.cuda.is_current_stream_capturing() else _tune_stages(
+        cfg = _STAGES_TUNED.get(key)
+        if cfg is None:
+            cfg = (0, 0) if torch.cuda.is_current_stream_capturing() else _tune_conv(
                 A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd)
-            if st:
-                _STAGES_TUNED[key] = st
-    C.conv_gemm(A, B, out, stats, bias, *geo, dh, dw, tb, G_STATS, zero, addend, *bwd, st)
+            if cfg[0]:
+                _STAGES_TUNED[key] = cfg
+    C.conv_gemm(A, B, out, stats, bias, *geo, dh, dw, tb, G_STATS, zero, addend, *bwd, *cfg)
 
 
-def _tune_stages(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd):
+def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd):
     scratch = torch.empty_like(out)
     sst = torch.zeros_like(stats) if stats is not None else None
     bwd = tuple(bwd)
     if bwd[3] is not None:
         bwd = bwd[:3] + (torch.zeros_like(bwd[3]),) + bwd[4:]
+    ncols = geo[1]
+    cands = [(st, tn) for st in (1, 2) for tn in ((64,) if ncols <= 64 else (64, 128))]
     times = {}
-    for st in (1, 2):
+    for cfg in cands:
         run = lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, G_STATS, zero,  # noqa: E731
-                                  addend, *bwd, st)
+                                  addend, *bwd, *cfg)
         run()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
@@ -263,7 +267,7 @@ def _tune_stages(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd):
             run()
         b.record()
         b.synchronize()
-        times[st] = a.elapsed_time(b)
+        times[cfg] = a.elapsed_time(b)
     return min(times, key=times.get)
 
 
@@ -522,6 +526,7 @@ class BNActFn(torch.autograd.Function):
         out = _empty_cl(n, c, h, w, dev)
         C.bn_apply(y, coef, res, out, rows, c, c, 0, a)
         ctx.act, ctx.group, ctx.rows, ctx.c = a, group, rows, c
+        ctx.training = bn.training
         ctx.count_t = count_t
         ctx.res_slot = res_slot
         ctx.link = None
@@ -558,8 +563,11 @@ class BNActFn(torch.autograd.Function):
             ws(dev).give_part(part)
         if ctx.group is not None:
             dist.all_reduce(sums, group=ctx.group)
-        k = torch.empty(2 * c, dtype=torch.float32, device=dev)
-        C.bn_bwd_k(sums, ctx.count_t, float(rows), c, k)
+        if ctx.training:
+            k = torch.empty(2 * c, dtype=torch.float32, device=dev)
+            C.bn_bwd_k(sums, ctx.count_t, float(rows), c, k)
+        else:  # running statistics are constants: dy = scale * dz
+            k = torch.zeros(2 * c, dtype=torch.float32, device=dev)
         dy = torch.empty_like(y, memory_format=CL)
         C.bn_bwd_elemt(None if dz is not None else g, y, coef, k, res, dz, dy, rows, c, ctx.act)
         dres = dz if ctx.has_res else None

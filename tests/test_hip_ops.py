@@ -166,6 +166,22 @@ def test_conv_bn_act(act, use_res):
         ze = bn_r(conv_r(x)) + (res if use_res else 0)
         re = {None: ze, "relu": F.relu(ze) if act == "relu" else ze, "silu": F.silu(ze)}[act]
     assert rel_err(oe, re) < 2e-2
+    # eval-mode backward (frozen statistics: dy = scale * dz, no batch-statistics terms)
+    for p_ in list(conv.parameters()) + list(bn.parameters()) + list(conv_r.parameters()) + list(bn_r.parameters()):
+        p_.grad = None
+    xe = xb.detach().clone().requires_grad_(True)
+    oe = hip.conv_bn_act(xe, conv, bn, act, rb.detach() if use_res else None)
+    xer = x.clone().requires_grad_(True)
+    yce = conv_r(xer)
+    ze = bn_r(yce + (bf(yce) - yce).detach()) + (res if use_res else 0)
+    re = {None: ze, "relu": F.relu(ze) if act == "relu" else ze, "silu": F.silu(ze)}[act]
+    ge = bf(torch.randn_like(re))
+    oe.backward(ge.to(torch.bfloat16).contiguous(memory_format=CL))
+    re.backward(ge)
+    assert rel_err(xe.grad, xer.grad) < 3e-2
+    assert rel_err(bn.weight.grad, bn_r.weight.grad) < 3e-2
+    assert rel_err(bn.bias.grad, bn_r.bias.grad) < 3e-2
+    assert rel_err(conv.weight.grad, conv_r.weight.grad) < 3e-2
 
 
 def test_depthwise_bn_silu():
