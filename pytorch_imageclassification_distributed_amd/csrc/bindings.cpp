@@ -16,6 +16,9 @@ using OT = std::optional<Tensor>;
 
 // ---- launcher prototypes (defined in *.hip) ----
 int bn_partials_launch(float*, int, int, double*, float*, float*, hipStream_t);
+int bn_reduce_finalize_launch(float*, int, int, double, const float*, const float*, float*, float*, long long*, float,
+                              float, float*, hipStream_t);
+int bn_reduce_bwd_launch(float*, int, int, double, float*, float*, float*, hipStream_t);
 int bn_finalize_launch(const double*, const double*, double, const float*, const float*, float*, float*,
                        long long*, float, float, int, float*, hipStream_t);
 int bn_eval_coef_launch(const float*, const float*, const float*, const float*, float, int, float*, hipStream_t);
@@ -157,6 +160,24 @@ void bn_finalize(Tensor sums, OT count_t, double count, OT gamma, OT beta, OT rm
                            optr<float>(rmean), optr<float>(rvar), optr<long long>(nbt), (float)momentum, (float)eps,
                            C, ptr<float>(coef), cur()),
         "bn_finalize");
+}
+
+void bn_reduce_finalize(Tensor part, int G, int C, double count, OT gamma, OT beta, OT rmean, OT rvar, OT nbt,
+                        double momentum, double eps, Tensor coef) {
+  req(part, F32, "part"); req(coef, F32, "coef");
+  TORCH_CHECK(part.numel() >= (int64_t)G * 2 * C && coef.numel() >= 4 * C, "bn_reduce_finalize: buffer sizes");
+  check(bn_reduce_finalize_launch(ptr<float>(part), G, C, count, optr<float>(gamma), optr<float>(beta),
+                                  optr<float>(rmean), optr<float>(rvar), optr<long long>(nbt), (float)momentum,
+                                  (float)eps, ptr<float>(coef), cur()),
+        "bn_reduce_finalize");
+}
+
+void bn_reduce_bwd(Tensor part, int G, int C, double count, OT dgamma, OT dbeta, Tensor k) {
+  req(part, F32, "part"); req(k, F32, "k");
+  TORCH_CHECK(part.numel() >= (int64_t)G * 2 * C && k.numel() >= 2 * C, "bn_reduce_bwd: buffer sizes");
+  check(bn_reduce_bwd_launch(ptr<float>(part), G, C, count, optr<float>(dgamma), optr<float>(dbeta), ptr<float>(k),
+                             cur()),
+        "bn_reduce_bwd");
 }
 
 void bn_eval_coef(OT gamma, OT beta, Tensor rmean, Tensor rvar, double eps, int C, Tensor coef) {
@@ -377,6 +398,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_set_wgrad_variant", &conv_set_wgrad_variant);
   m.def("bn_partials", &bn_partials);
   m.def("bn_finalize", &bn_finalize);
+  m.def("bn_reduce_finalize", &bn_reduce_finalize);
+  m.def("bn_reduce_bwd", &bn_reduce_bwd);
   m.def("bn_eval_coef", &bn_eval_coef);
   m.def("bn_apply", &bn_apply);
   m.def("bn_bwd_reduce", &bn_bwd_reduce);

@@ -53,6 +53,78 @@ __global__ __launch_bounds__(256) void bn_partials_kernel(float* __restrict__ pa
   }
 }
 
+// ---- single-GPU fast paths: partial-row reduce fused with what follows ------
+// (no SyncBN all-reduce in between, so one launch replaces bn_partials + bn_finalize / bn_bwd_k)
+struct BnFinalizeArgs {
+  float* part; int G, C; double count;
+  const float* gamma; const float* beta; float* rmean; float* rvar; long long* nbt;
+  float momentum, eps; float* coef;
+};
+
+DEVI void reduce_partials_64(float* part, int G, int C, int c, int lc, int lg, double (*red)[4][64],
+                             double& s, double& q) {
+  s = 0.0; q = 0.0;
+  if (c < C) {
+#pragma unroll 4
+    for (int g = lg; g < G; g += 4) {
+      float* r = part + (size_t)g * 2 * C;
+      const float a = r[c], b = r[C + c];
+      r[c] = 0.f;
+      r[C + c] = 0.f;
+      s += (double)a;
+      q += (double)b;
+    }
+  }
+  red[0][lg][lc] = s;
+  red[1][lg][lc] = q;
+  __syncthreads();
+  s = red[0][0][lc] + red[0][1][lc] + red[0][2][lc] + red[0][3][lc];
+  q = red[1][0][lc] + red[1][1][lc] + red[1][2][lc] + red[1][3][lc];
+}
+
+__global__ __launch_bounds__(256) void bn_reduce_finalize_kernel(BnFinalizeArgs a) {
+  __shared__ double red[2][4][64];
+  const int lc = threadIdx.x & 63, lg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lc;
+  double s, q;
+  reduce_partials_64(a.part, a.G, a.C, c, lc, lg, red, s, q);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && a.nbt) *a.nbt += 1;
+  if (lg != 0 || c >= a.C) return;
+  const double n = a.count;
+  const double mean = s / n;
+  double var = q / n - mean * mean;
+  var = var < 0.0 ? 0.0 : var;
+  const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
+  const float g = a.gamma ? a.gamma[c] : 1.f, b = a.beta ? a.beta[c] : 0.f;
+  const float scale = g * invstd;
+  const int C = a.C;
+  a.coef[c] = scale;
+  a.coef[C + c] = b - (float)mean * scale;
+  a.coef[2 * C + c] = (float)mean;
+  a.coef[3 * C + c] = invstd;
+  if (a.rmean) {
+    const double unb = n > 1.0 ? var * n / (n - 1.0) : var;
+    a.rmean[c] = (1.f - a.momentum) * a.rmean[c] + a.momentum * (float)mean;
+    a.rvar[c] = (1.f - a.momentum) * a.rvar[c] + a.momentum * (float)unb;
+  }
+}
+
+// backward: (sum dz, sum dz*xhat) -> dbeta, dgamma and k = sums / n for bn_bwd_elemt
+__global__ __launch_bounds__(256) void bn_reduce_bwd_kernel(float* part, int G, int C, double count,
+                                                            float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                            float* __restrict__ kout) {
+  __shared__ double red[2][4][64];
+  const int lc = threadIdx.x & 63, lg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lc;
+  double s, q;
+  reduce_partials_64(part, G, C, c, lc, lg, red, s, q);
+  if (lg != 0 || c >= C) return;
+  if (dbeta) dbeta[c] = (float)s;
+  if (dgamma) dgamma[c] = (float)q;
+  kout[c] = (float)(s / count);
+  kout[C + c] = (float)(q / count);
+}
+
 // ---- fp64 sums -> coefficients, running stats -----------------------------
 // coef layout [4][C]: scale, shift, mean, invstd
 __global__ void bn_finalize_kernel(const double* __restrict__ sums, const double* __restrict__ count_p,
@@ -293,6 +365,22 @@ int grid_for(long work, int per_block = 256, int cap = 4096) {
 int bn_partials_launch(float* part, int G, int C, double* sums, float* dgamma, float* dbeta,
                        hipStream_t s) {
   hipLaunchKernelGGL(bn_partials_kernel, dim3(cdiv(C, 64)), dim3(256), 0, s, part, G, C, sums, dgamma, dbeta);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int bn_reduce_finalize_launch(float* part, int G, int C, double count, const float* gamma, const float* beta,
+                              float* rmean, float* rvar, long long* nbt, float momentum, float eps, float* coef,
+                              hipStream_t s) {
+  BnFinalizeArgs a{part, G, C, count, gamma, beta, rmean, rvar, nbt, momentum, eps, coef};
+  hipLaunchKernelGGL(bn_reduce_finalize_kernel, dim3(cdiv(C, 64)), dim3(256), 0, s, a);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int bn_reduce_bwd_launch(float* part, int G, int C, double count, float* dgamma, float* dbeta, float* k,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(bn_reduce_bwd_kernel, dim3(cdiv(C, 64)), dim3(256), 0, s, part, G, C, count, dgamma, dbeta, k);
   HIP_CHECK_LAUNCH();
   return 0;
 }

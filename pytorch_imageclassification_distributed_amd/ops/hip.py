@@ -508,17 +508,18 @@ class BNActFn(torch.autograd.Function):
             if not stats_ready:
                 C.bn_stats(y, rows, c, part, G_STATS)
             group = _sync_group(bn)
-            sums = torch.empty(2 * c + 1, dtype=torch.float64, device=dev)
-            C.bn_partials(part, G_STATS, c, sums, None, None)
-            if group is not None:
+            mom = bn.momentum if bn.momentum is not None else 0.1
+            track = bn.track_running_stats and bn.running_mean is not None
+            rs = (bn.running_mean, bn.running_var, bn.num_batches_tracked) if track else (None, None, None)
+            if group is None:  # one launch: partial rows -> coefficients + running stats
+                C.bn_reduce_finalize(part, G_STATS, c, float(rows), gamma, beta, *rs, mom, bn.eps, coef)
+            else:
+                sums = torch.empty(2 * c + 1, dtype=torch.float64, device=dev)
+                C.bn_partials(part, G_STATS, c, sums, None, None)
                 sums[2 * c:].fill_(float(rows))
                 dist.all_reduce(sums, group=group)
                 count_t = sums[2 * c:]
-            mom = bn.momentum if bn.momentum is not None else 0.1
-            track = bn.track_running_stats and bn.running_mean is not None
-            C.bn_finalize(sums, count_t, float(rows), gamma, beta,
-                          bn.running_mean if track else None, bn.running_var if track else None,
-                          bn.num_batches_tracked if track else None, mom, bn.eps, c, coef)
+                C.bn_finalize(sums, count_t, float(rows), gamma, beta, *rs, mom, bn.eps, c, coef)
         else:
             if stats_ready:
                 raise RuntimeError("eval-mode BN received fused statistics")
@@ -555,19 +556,22 @@ class BNActFn(torch.autograd.Function):
             part = ws(dev).stats_buf(c)
             dz = torch.empty_like(y, memory_format=CL) if ctx.has_res else None
             C.bn_bwd_reduce(g, y, coef, res, dz, rows, c, ctx.act, part, G_STATS)
-        sums = torch.empty(2 * c, dtype=torch.float64, device=dev)
         dgamma = grad_buffer(ctx.params[0], zero=False)
         dbeta = grad_buffer(ctx.params[1], zero=False)
-        C.bn_partials(part, G_STATS, c, sums, dgamma, dbeta)
+        k = torch.empty(2 * c, dtype=torch.float32, device=dev)
+        if ctx.training and ctx.group is None:  # one launch: partial rows -> dgamma, dbeta, k
+            C.bn_reduce_bwd(part, G_STATS, c, float(rows), dgamma, dbeta, k)
+        else:
+            sums = torch.empty(2 * c, dtype=torch.float64, device=dev)
+            C.bn_partials(part, G_STATS, c, sums, dgamma, dbeta)
+            if ctx.group is not None:
+                dist.all_reduce(sums, group=ctx.group)
+            if ctx.training:
+                C.bn_bwd_k(sums, ctx.count_t, float(rows), c, k)
+            else:  # running statistics are constants: dy = scale * dz
+                k.zero_()
         if link is not None and link.done:
             ws(dev).give_part(part)
-        if ctx.group is not None:
-            dist.all_reduce(sums, group=ctx.group)
-        if ctx.training:
-            k = torch.empty(2 * c, dtype=torch.float32, device=dev)
-            C.bn_bwd_k(sums, ctx.count_t, float(rows), c, k)
-        else:  # running statistics are constants: dy = scale * dz
-            k = torch.zeros(2 * c, dtype=torch.float32, device=dev)
         dy = torch.empty_like(y, memory_format=CL)
         C.bn_bwd_elemt(None if dz is not None else g, y, coef, k, res, dz, dy, rows, c, ctx.act)
         dres = dz if ctx.has_res else None
