@@ -72,6 +72,16 @@ def _compile(src: str, flags: list[str], verbose: bool) -> str:
     return obj
 
 
+def _check_loadable(path: str) -> None:
+    """dlopen the freshly linked module with every symbol bound now: a shared-library link
+    tolerates undefined symbols (a binding left pointing at a removed kernel), import does not."""
+    code = ("import ctypes, os, torch; ctypes.CDLL(os.path.abspath(%r), mode=os.RTLD_NOW | os.RTLD_GLOBAL)" % path)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True)
+    if r.returncode != 0:
+        os.remove(path)
+        raise RuntimeError(f"linked module does not load:\n{r.stderr[-2000:]}")
+
+
 def build(verbose: bool = False, jobs: int | None = None) -> str:
     os.makedirs(BUILD, exist_ok=True)
     cflags, ldflags = _torch_flags()
@@ -92,6 +102,7 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed\n{r.stdout}\n{r.stderr}")
+    _check_loadable(OUT + ".tmp")
     os.replace(OUT + ".tmp", OUT)
     with open(stamp, "w") as f:
         f.write(key)

@@ -50,6 +50,8 @@ int prepare_input_launch(const float*, bf16_t*, int, int, int, int, const float*
 int cast_bf16_launch(const float*, bf16_t*, long, hipStream_t);
 int weight_pad_launch(const bf16_t*, bf16_t*, long, int, int, hipStream_t);
 int weight_t_launch(const bf16_t*, bf16_t*, int, int, int, hipStream_t);
+int weight_t_tiles_launch(const void*, const void*, int, hipStream_t);
+int weight_t_job_bytes();
 int grad_unpad_launch(const float*, float*, long, int, int, hipStream_t);
 int copy_channels_launch(const bf16_t*, int, int, bf16_t*, int, int, long, int, hipStream_t);
 int add_launch(const bf16_t*, const bf16_t*, bf16_t*, long, hipStream_t);
@@ -301,6 +303,11 @@ void weight_pad(Tensor w, Tensor o, long rows, int Ci, int Cp) {
   check(weight_pad_launch(ptr<bf16_t>(w), ptr<bf16_t>(o), rows, Ci, Cp, cur()), "weight_pad");
 }
 
+void weight_t_tiles(Tensor jobs, Tensor tiles, int ntiles) {
+  TORCH_CHECK(jobs.is_cuda() && tiles.is_cuda() && tiles.numel() >= (int64_t)ntiles * 4, "weight_t_tiles: bad tables");
+  check(weight_t_tiles_launch(jobs.data_ptr(), tiles.data_ptr(), ntiles, cur()), "weight_t_tiles");
+}
+
 void weight_t(Tensor w, Tensor o, int Co, int T, int Ci) {
   check(weight_t_launch(ptr<bf16_t>(w), ptr<bf16_t>(o), Co, T, Ci, cur()), "weight_t");
 }
@@ -417,6 +424,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("ce_bwd", &ce_bwd);
   m.def("adam", &adam);
   m.def("adam_tick", &adam_tick);
+  m.def("weight_t_tiles", &weight_t_tiles);
+  m.def("weight_t_job_bytes", &weight_t_job_bytes);
   m.def("prepare_input", &prepare_input);
   m.def("cast_bf16", &cast_bf16);
   m.def("weight_pad", &weight_pad);

@@ -67,6 +67,35 @@ __global__ void weight_t_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict
   }
 }
 
+// Batched, LDS-tiled form of weight_t for every conv weight the optimizer just updated (one launch
+// after the fused Adam instead of one gathered transpose per layer).  tile = (job, tap, co0, ci0).
+struct WtJob {
+  const bf16_t* w;
+  bf16_t* o;
+  int Co, T, Ci, pad_;
+};
+
+__global__ __launch_bounds__(256) void weight_t_tiles_kernel(const WtJob* __restrict__ jobs,
+                                                             const int4* __restrict__ tiles) {
+  __shared__ unsigned short tile[64][65];
+  const int4 td = tiles[blockIdx.x];
+  const WtJob j = jobs[td.x];
+  const int tap = td.y, co0 = td.z, ci0 = td.w;
+  const unsigned short* w = (const unsigned short*)j.w;
+  unsigned short* o = (unsigned short*)j.o;
+  for (int e = threadIdx.x; e < 64 * 64; e += 256) {  // read rows of ci (contiguous)
+    const int r = e >> 6, c = e & 63;
+    const int co = co0 + r, ci = ci0 + c;
+    tile[r][c] = (co < j.Co && ci < j.Ci) ? w[((long)co * j.T + tap) * j.Ci + ci] : (unsigned short)0;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 64 * 64; e += 256) {  // write rows of co (contiguous)
+    const int r = e >> 6, c = e & 63;
+    const int ci = ci0 + r, co = co0 + c;
+    if (ci < j.Ci && co < j.Co) o[((long)ci * j.T + tap) * j.Co + co] = tile[c][r];
+  }
+}
+
 __global__ void grad_unpad_kernel(const float* __restrict__ g, float* __restrict__ o, long rows, int Cp, int Ci) {
   const long total = rows * Ci;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
@@ -167,6 +196,15 @@ int weight_t_launch(const bf16_t* w, bf16_t* o, int Co, int T, int Ci, hipStream
   HIP_CHECK_LAUNCH();
   return 0;
 }
+
+int weight_t_tiles_launch(const void* jobs, const void* tiles, int ntiles, hipStream_t s) {
+  if (ntiles <= 0) return 0;
+  hipLaunchKernelGGL(weight_t_tiles_kernel, dim3(ntiles), dim3(256), 0, s, (const WtJob*)jobs, (const int4*)tiles);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int weight_t_job_bytes() { return (int)sizeof(WtJob); }
 
 int grad_unpad_launch(const float* g, float* o, long rows, int Cp, int Ci, hipStream_t s) {
   hipLaunchKernelGGL(grad_unpad_kernel, dim3(grid_for(rows * Ci)), dim3(256), 0, s, g, o, rows, Cp, Ci);

@@ -80,7 +80,9 @@ def ws(dev) -> _Workspace:
 # bf16 weight shadows
 # ---------------------------------------------------------------------------
 class _Shadow:
-    __slots__ = ("t", "ptr", "version", "fused", "ref")
+    # t: bf16 KRSC copy; tt: bf16 [Ci][T][Co] copy for dgrad (lazily, conv weights only).
+    # stamp counts re-casts of t; tt is current when tt_stamp == stamp or the optimizer maintains it.
+    __slots__ = ("t", "ptr", "version", "fused", "ref", "stamp", "tt", "tgeom", "tt_stamp", "tfused")
 
 
 _SHADOWS: dict = {}
@@ -108,6 +110,7 @@ def weight_bf16(p: torch.Tensor) -> torch.Tensor:
         e.t = torch.empty(p.numel(), dtype=BF16, device=p.device)
         e.fused = False
         e.ref = weakref.ref(p)
+        e.stamp, e.tt, e.tgeom, e.tt_stamp, e.tfused = 0, None, None, -1, False
         _SHADOWS[key] = e
         _SHADOW_GEN[0] += 1
     src = p.detach()
@@ -116,7 +119,27 @@ def weight_bf16(p: torch.Tensor) -> torch.Tensor:
     C.cast_bf16(flat, e.t)
     e.ptr = p.data_ptr()
     e.version = p._version
+    e.stamp += 1
     return e.t
+
+
+def weight_bf16_t(p: torch.Tensor, co: int, taps: int, ci: int) -> torch.Tensor:
+    """bf16 copy of a KRSC conv weight transposed to [Ci][T][Co] (the dgrad B operand).
+
+    Cached with the KRSC shadow; once registered with the fused Adam (``shadow_t_for_optimizer``)
+    the optimizer rewrites it in its update pass, so steady-state training never transposes."""
+    wb = weight_bf16(p)
+    e = _SHADOWS[id(p)]
+    if e.tt is not None and e.tgeom == (co, taps, ci) and (e.tfused or e.tt_stamp == e.stamp):
+        return e.tt
+    if e.tt is None or e.tgeom != (co, taps, ci):
+        e.tt = torch.empty(co * taps * ci, dtype=BF16, device=p.device)
+        e.tgeom = (co, taps, ci)
+        e.tfused = False
+        _SHADOW_GEN[0] += 1  # the optimizer table picks the new copy up on its next step
+    C.weight_t(wb, e.tt, co, taps, ci)
+    e.tt_stamp = e.stamp
+    return e.tt
 
 
 def shadow_for_optimizer(p: torch.Tensor):
@@ -126,6 +149,15 @@ def shadow_for_optimizer(p: torch.Tensor):
         return None
     e.fused = True
     return e.t
+
+
+def shadow_t_for_optimizer(p: torch.Tensor):
+    """(transposed shadow, co, taps, ci) the Adam kernel should rewrite for ``p`` (or None)."""
+    e = _SHADOWS.get(id(p))
+    if e is None or e.ref() is not p or e.tt is None or not _krsc_compatible(p) or p.dim() != 4:
+        return None
+    e.tfused = True
+    return (e.tt,) + e.tgeom
 
 
 def shadow_generation() -> int:
@@ -295,9 +327,7 @@ def conv_dgrad_raw(dy, w_param, g: ConvGeom, addend=None, link=None):
     if link is not None:
         link.part = ws(dev).take_part(g.Ci)
         bwd = (link.y, link.res, link.coef, link.part, link.act, G_STATS)
-    wb = weight_bf16(w_param)
-    wt = torch.empty(g.Ci * g.T * g.Co, dtype=BF16, device=dev)
-    C.weight_t(wb, wt, g.Co, g.T, g.Ci)
+    wt = weight_bf16_t(w_param, g.Co, g.T, g.Ci)
     dx = _empty_cl(g.N, g.Ci, g.H, g.W, dev)
     for ph, pw, gh, gw, dh, dw, tb in _dgrad_phases(g):
         if gh <= 0 or gw <= 0:
@@ -466,8 +496,7 @@ class DwConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, conv):
         g = ConvGeom(x, conv)
-        wt = torch.empty(g.T * g.Co, dtype=BF16, device=x.device)
-        C.weight_t(weight_bf16(w), wt, g.Co, g.T, 1)
+        wt = weight_bf16_t(w, g.Co, g.T, 1)
         y = _empty_cl(g.N, g.Co, g.OH, g.OW, x.device)
         C.dw_fwd(x, wt, y, None, g.N, g.H, g.W, g.Co, g.OH, g.OW, g.kh, g.kw, g.sh, g.sw, g.pt, g.pl)
         ctx.g = g
@@ -1022,6 +1051,12 @@ def se_gate(x, se_reduce, se_expand):
 # ---------------------------------------------------------------------------
 _ADAM_CHUNK = 65536
 _TENSOR_DT = np.dtype([("p", "<u8"), ("g", "<u8"), ("m", "<u8"), ("v", "<u8"), ("s", "<u8"), ("n", "<i8")])
+_WTJOB_DT = np.dtype([("w", "<u8"), ("o", "<u8"), ("co", "<i4"), ("t", "<i4"), ("ci", "<i4"), ("pad", "<i4")])
+
+
+def _upload(arr: np.ndarray, dev) -> torch.Tensor:
+    # pinned + non_blocking: a pageable H2D copy would stall the host until the GPU drains
+    return torch.from_numpy(arr).pin_memory().to(dev, non_blocking=True)
 
 
 def _same_memory_order(a: torch.Tensor, b: torch.Tensor) -> bool:
@@ -1035,7 +1070,10 @@ def _same_memory_order(a: torch.Tensor, b: torch.Tensor) -> bool:
 
 
 def adam_build_table(opt, items):
+    if C.weight_t_job_bytes() != _WTJOB_DT.itemsize:
+        raise RuntimeError("weight_t_tiles: job record layout mismatch between Python and the kernel")
     groups = {}
+    wt_jobs = []
     for gi, group, p in items:
         groups.setdefault(gi, (group, []))[1].append(p)
     tables = []
@@ -1047,25 +1085,34 @@ def adam_build_table(opt, items):
             sh = shadow_for_optimizer(p)
             recs[t] = (p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
                        sh.data_ptr() if sh is not None else 0, p.numel())
+            stt = shadow_t_for_optimizer(p) if sh is not None else None
+            if stt is not None:
+                wt_jobs.append((sh.data_ptr(), stt[0].data_ptr()) + tuple(stt[1:]) + (0,))
             for ck in range(-(-p.numel() // _ADAM_CHUNK)):
                 chunks.append((t, ck))
             if not _same_memory_order(p, p.grad):
                 raise RuntimeError("fused Adam: gradient layout differs from parameter layout")
         dev = ps[0].device
-        # pinned + non_blocking: a pageable H2D copy would stall the host until the GPU drains
-        tab = torch.from_numpy(recs.view(np.uint8).copy()).pin_memory().to(dev, non_blocking=True)
-        ck = torch.tensor(chunks, dtype=torch.int32).reshape(-1).pin_memory().to(dev, non_blocking=True)
+        tab = _upload(recs.view(np.uint8).copy(), dev)
+        ck = _upload(np.asarray(chunks, dtype=np.int32).reshape(-1), dev)
         lr_step = getattr(opt, "_lr_step", {}).get(gi)
         if lr_step is None:
             step0 = float(opt.state[ps[0]]["step"]) if "step" in opt.state[ps[0]] else 0.0
             lr_step = torch.tensor([group["lr"], step0], dtype=torch.float32, device=dev)
             opt.__dict__.setdefault("_lr_step", {})[gi] = lr_step
         tables.append((gi, tab, ck, len(chunks), lr_step, [p for p in ps]))
-    return (tables, shadow_generation())
+    wt = None
+    if wt_jobs:
+        jobs = np.array(wt_jobs, dtype=_WTJOB_DT)
+        tiles = [(j, t, co0, ci0) for j, (_w, _o, co, taps, ci, _p) in enumerate(wt_jobs)
+                 for t in range(taps) for co0 in range(0, co, 64) for ci0 in range(0, ci, 64)]
+        wt = (_upload(jobs.view(np.uint8).copy(), tables[0][1].device),
+              _upload(np.asarray(tiles, dtype=np.int32).reshape(-1), tables[0][1].device), len(tiles))
+    return (tables, shadow_generation(), wt)
 
 
 def adam_step(opt, items, table, grad_scale):
-    tables, gen = table
+    tables, gen, wt = table
     if gen != shadow_generation():
         opt._table_key = None  # rebuild next step so new shadows are kept fresh
     for gi, tab, ck, nck, lr_step, ps in tables:
@@ -1073,4 +1120,6 @@ def adam_step(opt, items, table, grad_scale):
         b1, b2 = group["betas"]
         C.adam_tick(lr_step, float(group["lr"]))
         C.adam(tab, ck, nck, lr_step, b1, b2, group["eps"], group["weight_decay"], float(grad_scale), _ADAM_CHUNK)
+    if wt is not None:  # refresh every transposed dgrad shadow from the updated KRSC shadows: one launch
+        C.weight_t_tiles(*wt)
     opt._host_steps = getattr(opt, "_host_steps", 0) + 1

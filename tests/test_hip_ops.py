@@ -297,6 +297,33 @@ def test_fused_adam_matches_torch():
     assert float(sd["state"][0]["step"]) == 5.0
 
 
+def test_adam_maintains_weight_shadows():
+    """After fused-Adam steps the bf16 KRSC shadow and the transposed [Ci][T][Co] dgrad shadow
+    (rewritten inside the Adam kernel, never re-transposed) equal a fresh cast of the weights."""
+    from pytorch_imageclassification_distributed_amd.engine.optim import FusedAdam
+    hip = _hip()
+    torch.manual_seed(9)
+    conv = nn.Conv2d(32, 48, 3, 1, 1, bias=False).to(DEV).to(memory_format=CL)
+    dw = nn.Conv2d(48, 48, 5, 1, 2, groups=48, bias=False).to(DEV).to(memory_format=CL)
+    opt = FusedAdam(list(conv.parameters()) + list(dw.parameters()), lr=1e-2)
+    x = torch.randn(2, 32, 12, 12, device=DEV).to(torch.bfloat16).contiguous(memory_format=CL)
+    for _ in range(3):
+        opt.zero_grad(set_to_none=True)
+        xx = x.clone().requires_grad_(True)
+        y = hip.ConvFn.apply(xx, conv.weight, conv, False)
+        z = hip.DwConvFn.apply(y, dw.weight, dw)
+        z.float().square().mean().backward()
+        opt.step()
+    torch.cuda.synchronize()
+    for w, ci in ((conv.weight, 32), (dw.weight, 1)):
+        co, t = w.shape[0], w.shape[2] * w.shape[3]
+        e = hip._SHADOWS[id(w)]
+        assert e.fused and e.tfused
+        krsc = w.detach().permute(0, 2, 3, 1).reshape(co, t, ci).to(torch.bfloat16)
+        assert torch.equal(hip.weight_bf16(w).view(co, t, ci), krsc)
+        assert torch.equal(hip.weight_bf16_t(w, co, t, ci).view(ci, t, co), krsc.permute(2, 1, 0))
+
+
 def test_resnet18_matches_reference_path():
     """Whole-model forward/backward: HIP bf16 path vs ATen fp32 path on identical weights.
 
