@@ -257,6 +257,22 @@ def _weight_for_input(w_param, cx):
     return out
 
 
+def _time_ms(run, reps: int = 3, trials: int = 3) -> float:
+    """Best-of-``trials`` mean time of ``reps`` back-to-back launches (after one warm launch):
+    the minimum is robust to the occasional preempted trial that made single-shot choices noisy."""
+    run()
+    best = float("inf")
+    for _ in range(trials):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            run()
+        b.record()
+        b.synchronize()
+        best = min(best, a.elapsed_time(b) / reps)
+    return best
+
+
 CONV_STAGES = os.environ.get("IMGCLS_CONV_STAGES", "auto")  # auto (timed per shape) | 0 (heuristic) | 1 | 2
 _STAGES_TUNED: dict = {}
 
@@ -290,16 +306,8 @@ def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd):
     cands = [(st, tn) for st in (1, 2) for tn in ((64,) if ncols <= 64 else (64, 128))]
     times = {}
     for cfg in cands:
-        run = lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, G_STATS, zero,  # noqa: E731
-                                  addend, *bwd, *cfg)
-        run()
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
-        for _ in range(3):
-            run()
-        b.record()
-        b.synchronize()
-        times[cfg] = a.elapsed_time(b)
+        times[cfg] = _time_ms(lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, G_STATS, zero,
+                                                  addend, *bwd, *cfg))
     return min(times, key=times.get)
 
 
@@ -381,14 +389,7 @@ def _wgrad_config(dy, x, g: ConvGeom, m, ntot, tiles):
     for st in stages:
         for cand in blocks:
             kps, splits = _wgrad_split(m, tiles, cand)
-            _wgrad_launch(dy, x, scratch, g, m, ntot, kps, splits, st)  # warm
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record()
-            for _ in range(3):
-                _wgrad_launch(dy, x, scratch, g, m, ntot, kps, splits, st)
-            b.record()
-            b.synchronize()
-            times[(cand, st)] = a.elapsed_time(b)
+            times[(cand, st)] = _time_ms(lambda: _wgrad_launch(dy, x, scratch, g, m, ntot, kps, splits, st))
     best = min(times, key=times.get)
     _WGRAD_TUNED[key] = best
     return best
