@@ -11,6 +11,8 @@
 
 #include "conv_gemm.h"
 
+extern int g_imgcls_det;  // misc.hip: deterministic mode
+
 using at::Tensor;
 using OT = std::optional<Tensor>;
 
@@ -63,7 +65,9 @@ int dw_fwd_launch(const bf16_t*, const bf16_t*, bf16_t*, float*, int, int, int, 
 int dw_dgrad_launch(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int, int,
                     int, hipStream_t);
 int dw_wgrad_launch(const bf16_t*, const bf16_t*, float*, int, int, int, int, int, int, int, int, int, int, int,
-                    int, hipStream_t);
+                    int, float*, hipStream_t);
+long dw_wgrad_partial_rows(int, int, int, int, int);
+void set_deterministic(int);
 int se_scale_launch(const bf16_t*, const float*, bf16_t*, int, int, int, hipStream_t);
 int se_ds_launch(const bf16_t*, const bf16_t*, float*, int, int, int, hipStream_t);
 int se_dx_launch(const bf16_t*, const float*, const float*, bf16_t*, int, int, int, hipStream_t);
@@ -362,8 +366,18 @@ void dw_dgrad(Tensor dy, Tensor w, Tensor dx, int N, int H, int W, int C, int OH
 void dw_wgrad(Tensor dy, Tensor x, Tensor dw, int N, int H, int W, int C, int OH, int OW, int kh, int kw, int sh,
               int sw, int pt, int pl) {
   req(dw, F32, "dw");
+  if (g_imgcls_det) {  // per-block partial rows, then an ordered column sum (no cross-block atomics)
+    const long rows = dw_wgrad_partial_rows(N, OH, OW, kh, kw);
+    const int cols = C * kh * kw;
+    Tensor part = at::zeros({rows, (long)cols}, dw.options());
+    check(dw_wgrad_launch(ptr<bf16_t>(dy), ptr<bf16_t>(x), ptr<float>(dw), N, H, W, C, OH, OW, kh, kw, sh, sw, pt,
+                          pl, ptr<float>(part), cur()),
+          "dw_wgrad");
+    check(colsum_launch(ptr<float>(part), nullptr, ptr<float>(dw), (int)rows, cols, cols, 1, cur()), "dw_wgrad");
+    return;
+  }
   check(dw_wgrad_launch(ptr<bf16_t>(dy), ptr<bf16_t>(x), ptr<float>(dw), N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl,
-                        cur()),
+                        nullptr, cur()),
         "dw_wgrad");
 }
 
@@ -401,6 +415,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_gemm", &conv_gemm);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_set_variant", &conv_set_variant);
+  m.def("set_deterministic", [](bool v) { set_deterministic(v ? 1 : 0); });
   m.def("conv_set_single_stage", &conv_set_single_stage);
   m.def("conv_set_wgrad_variant", &conv_set_wgrad_variant);
   m.def("bn_partials", &bn_partials);

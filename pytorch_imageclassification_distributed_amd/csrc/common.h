@@ -9,6 +9,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Deterministic mode (set from Python): every fp32 atomic accumulation site is reorganised so each
+// address receives exactly one contribution (split-K off, per-block partial rows reduced in order).
+extern int g_imgcls_det;
+
 typedef uint16_t bf16_t;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));

@@ -81,7 +81,8 @@ __global__ void dw_dgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __r
 
 // grid: (pixel blocks, taps); block = CHB chunk lanes x RP pixel lanes; dw layout [C][taps] fp32
 __global__ __launch_bounds__(256) void dw_wgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
-                                                        float* __restrict__ dw, DwGeom g, long pix_per_block) {
+                                                        float* __restrict__ dw, DwGeom g, long pix_per_block,
+                                                        long block_stride) {
   __shared__ float red[256][9];
   const int cch = g.C >> 3;
   const int CHB = cch < 256 ? cch : 256;
@@ -122,8 +123,10 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const bf16_t* __restrict_
 #pragma unroll
         for (int k = 0; k < 8; ++k) acc[k] += red[tid + rr * CHB][k];
       const int T = g.kh * g.kw;
+      // block_stride > 0 (deterministic mode): each pixel block owns a partial row, summed in order later
+      float* dst = dw + blockIdx.x * block_stride;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) atomicAdd(dw + (long)(chunk * 8 + k) * T + tap, acc[k]);
+      for (int k = 0; k < 8; ++k) atomicAdd(dst + (long)(chunk * 8 + k) * T + tap, acc[k]);
     }
     __syncthreads();
   }
@@ -227,17 +230,32 @@ int dw_dgrad_launch(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H,
   return 0;
 }
 
-int dw_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, int N, int H, int W, int C, int OH, int OW,
-                    int kh, int kw, int sh, int sw, int pt, int pl, hipStream_t s) {
-  DwGeom g{N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl};
-  const long npix = (long)N * OH * OW;
-  const int T = kh * kw;
+static long dw_wgrad_ppb(long npix, int T, long* pblocks_out) {
   long pblocks = 2048 / T;
   if (pblocks < 8) pblocks = 8;
   long ppb = (npix + pblocks - 1) / pblocks;
   if (ppb < 64) ppb = 64;
-  pblocks = (npix + ppb - 1) / ppb;
-  hipLaunchKernelGGL(dw_wgrad_kernel, dim3((unsigned)pblocks, T), dim3(256), 0, s, dy, x, dw, g, ppb);
+  *pblocks_out = (npix + ppb - 1) / ppb;
+  return ppb;
+}
+
+long dw_wgrad_partial_rows(int N, int OH, int OW, int kh, int kw) {
+  long pb;
+  dw_wgrad_ppb((long)N * OH * OW, kh * kw, &pb);
+  return pb;
+}
+
+// part: null -> atomics straight into dw; else [pblocks][C*T] zeroed partial rows (deterministic mode),
+// which the caller reduces in order (colsum)
+int dw_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, int N, int H, int W, int C, int OH, int OW,
+                    int kh, int kw, int sh, int sw, int pt, int pl, float* part, hipStream_t s) {
+  DwGeom g{N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl};
+  const long npix = (long)N * OH * OW;
+  const int T = kh * kw;
+  long pblocks;
+  const long ppb = dw_wgrad_ppb(npix, T, &pblocks);
+  hipLaunchKernelGGL(dw_wgrad_kernel, dim3((unsigned)pblocks, T), dim3(256), 0, s, dy, x, part ? part : dw, g, ppb,
+                     part ? (long)C * T : 0L);
   HIP_CHECK_LAUNCH();
   return 0;
 }

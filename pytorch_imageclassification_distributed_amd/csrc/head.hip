@@ -92,11 +92,11 @@ __global__ void bias_act_kernel(float* C, const float* __restrict__ bias, int M,
 // block = 64 columns x 4 row lanes over a CS_ROWS-row chunk; one atomic per column per block
 constexpr int CS_ROWS = 32;
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ X, const float* __restrict__ mask,
-                                                     float* out, int M, int N, long ld) {
+                                                     float* out, int M, int N, long ld, int rows_per_block) {
   __shared__ float red[4][64];
   const int c = threadIdx.x & 63, r = threadIdx.x >> 6;
   const int n = blockIdx.x * 64 + c;
-  const int m0 = blockIdx.y * CS_ROWS, m1 = min(M, m0 + CS_ROWS);
+  const int m0 = blockIdx.y * rows_per_block, m1 = min(M, m0 + rows_per_block);
   float s = 0.f;
   if (n < N)
     for (int m = m0 + r; m < m1; m += 4) {
@@ -166,7 +166,7 @@ int sgemm_launch(const float* A, const float* B, float* C, const float* bias, co
   // split K until the grid covers the chip (these GEMMs are skinny: M = batch, N <= 2048)
   const int tiles = cdiv(N, TS) * cdiv(M, TS);
   int splits = 1;
-  while (tiles * splits < 256 && K / (splits * 2) >= 4 * TK) splits *= 2;
+  while (!g_imgcls_det && tiles * splits < 256 && K / (splits * 2) >= 4 * TK) splits *= 2;
   const int kchunk = cdiv(cdiv(K, splits), TK) * TK;
   splits = cdiv(K, kchunk);
   SgemmArgs a{A, B, C, bias, mask, M, N, K, sam, sak, sbk, sbn, ldc, smm, smk, relu, accumulate, kchunk, splits > 1};
@@ -189,7 +189,8 @@ int sgemm_launch(const float* A, const float* B, float* C, const float* bias, co
 int colsum_launch(const float* X, const float* mask, float* out, int M, int N, long ld, int accumulate,
                   hipStream_t s) {
   if (!accumulate && hipMemsetAsync(out, 0, sizeof(float) * (size_t)N, s) != hipSuccess) return 1;
-  hipLaunchKernelGGL(colsum_kernel, dim3(cdiv(N, 64), cdiv(M, CS_ROWS)), dim3(256), 0, s, X, mask, out, M, N, ld);
+  const int rpb = g_imgcls_det ? (M > 0 ? M : 1) : CS_ROWS;  // deterministic: one ordered pass per column
+  hipLaunchKernelGGL(colsum_kernel, dim3(cdiv(N, 64), cdiv(M, rpb)), dim3(256), 0, s, X, mask, out, M, N, ld, rpb);
   HIP_CHECK_LAUNCH();
   return 0;
 }

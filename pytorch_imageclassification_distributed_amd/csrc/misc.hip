@@ -204,6 +204,9 @@ int weight_t_tiles_launch(const void* jobs, const void* tiles, int ntiles, hipSt
   return 0;
 }
 
+int g_imgcls_det = 0;
+void set_deterministic(int v) { g_imgcls_det = v; }
+
 int weight_t_job_bytes() { return (int)sizeof(WtJob); }
 
 int grad_unpad_launch(const float* g, float* o, long rows, int Cp, int Ci, hipStream_t s) {

@@ -62,6 +62,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--exact-val", action="store_true", help="mask DistributedSampler padding in validation (A15)")
     p.add_argument("--pretrained", default=None, help="local torchvision-layout state_dict to initialise the backbone")
+    p.add_argument("--deterministic", action="store_true",
+                   help="bitwise-reproducible GPU kernels (no split-K / cross-block fp32 atomics; slower)")
     p.add_argument("--timeout-min", type=float, default=10.0, help="process-group timeout (minutes)")
     return p
 

@@ -55,6 +55,12 @@ class Trainer:
         if args.compute != "auto":
             Fx.set_backend(args.compute)
         self.hip = self.dev.type == "cuda" and Fx.get_backend() != "torch"
+        if getattr(args, "deterministic", False):
+            torch.backends.cudnn.deterministic = True
+            torch.backends.cudnn.benchmark = False
+            if self.hip:
+                from ..ops import hip as _hip
+                _hip.set_deterministic(True)
         self.name = args.model
         self.image_size = args.image_size or DEFAULT_IMAGE_SIZE.get(args.model, 224)
         self._build_data()

@@ -31,6 +31,24 @@ CL = torch.channels_last
 BF16 = torch.bfloat16
 ACT = {None: 0, "relu": 1, "silu": 2}
 G_STATS = 64  # rotating partial rows for BN statistics atomics
+DETERMINISTIC = os.environ.get("IMGCLS_DETERMINISTIC", "0") == "1"
+
+
+def set_deterministic(flag: bool = True) -> None:
+    """Bitwise-reproducible mode: every fp32 atomic site gets one contribution per address - BN partial
+    rows >= producing blocks, no split-K (wgrad, head GEMMs), ordered column sums.  Slower."""
+    global DETERMINISTIC
+    DETERMINISTIC = bool(flag)
+    C.set_deterministic(DETERMINISTIC)
+
+
+C.set_deterministic(DETERMINISTIC)
+
+
+def stat_groups(rows: int) -> int:
+    """Partial-sum rows for BN statistics over ``rows`` pixels: 64 rotating rows normally; in
+    deterministic mode at least one per producing block (128-row conv tiles, <=1024 reduce blocks)."""
+    return max(-(-rows // 128), 1024) if DETERMINISTIC else G_STATS
 FUSE_BN_BWD = os.environ.get("IMGCLS_FUSE_BN_BWD", "1") == "1"  # BN-backward reduce in the consumer's dgrad
 FUSED_BWD_COUNT = [0]  # number of BN-backward reduces served by a conv epilogue (tests / diagnostics)
 
@@ -45,10 +63,10 @@ class _Workspace:
         self.zero = torch.zeros(64, dtype=BF16, device=dev)  # zero page for padded LDS-DMA chunks
         self.parts: list = []  # zeroed partial-stat buffers for fused BN-backward reduces
 
-    def take_part(self, c: int) -> torch.Tensor:
+    def take_part(self, c: int, groups: int = G_STATS) -> torch.Tensor:
         """A zeroed partial-sum buffer for a fused BN-backward reduce; handed back by ``give_part``
         after ``bn_partials`` has read (and re-zeroed) it, so the pool never needs a memset."""
-        need = G_STATS * 2 * c
+        need = groups * 2 * c
         for i, b in enumerate(self.parts):
             if b.numel() >= need:
                 return self.parts.pop(i)
@@ -57,8 +75,8 @@ class _Workspace:
     def give_part(self, b: torch.Tensor) -> None:
         self.parts.append(b)
 
-    def stats_buf(self, c: int) -> torch.Tensor:
-        need = G_STATS * 2 * c
+    def stats_buf(self, c: int, groups: int = G_STATS) -> torch.Tensor:
+        need = groups * 2 * c
         if self.stats.numel() < need:
             # consumers re-zero what they read, so a fresh buffer only needs one memset
             self.stats = torch.zeros(max(need, G_STATS * 2 * 2048), dtype=torch.float32, device=self.dev)
@@ -277,7 +295,8 @@ CONV_STAGES = os.environ.get("IMGCLS_CONV_STAGES", "auto")  # auto (timed per sh
 _STAGES_TUNED: dict = {}
 
 
-def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(None, None, None, None, 0, 1)):
+def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(None, None, None, None, 0, 1),
+               groups=G_STATS):
     """One implicit-GEMM launch.  The kernel configuration - LDS-DMA ring depth (1 = high occupancy,
     2 = pipelined) x output-channel tile (64 / 128: more tiles balance 256 CUs better on small
     layers) - is chosen once per GEMM geometry by timing the candidates on scratch outputs (a
@@ -290,13 +309,13 @@ def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(
         cfg = _STAGES_TUNED.get(key)
         if cfg is None:
             cfg = (0, 0) if torch.cuda.is_current_stream_capturing() else _tune_conv(
-                A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd)
+                A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups)
             if cfg[0]:
                 _STAGES_TUNED[key] = cfg
-    C.conv_gemm(A, B, out, stats, bias, *geo, dh, dw, tb, G_STATS, zero, addend, *bwd, *cfg)
+    C.conv_gemm(A, B, out, stats, bias, *geo, dh, dw, tb, groups, zero, addend, *bwd, *cfg)
 
 
-def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd):
+def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups):
     scratch = torch.empty_like(out)
     sst = torch.zeros_like(stats) if stats is not None else None
     bwd = tuple(bwd)
@@ -306,7 +325,7 @@ def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd):
     cands = [(st, tn) for st in (1, 2) for tn in ((64,) if ncols <= 64 else (64, 128))]
     times = {}
     for cfg in cands:
-        times[cfg] = _time_ms(lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, G_STATS, zero,
+        times[cfg] = _time_ms(lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, groups, zero,
                                                   addend, *bwd, *cfg))
     return min(times, key=times.get)
 
@@ -321,7 +340,7 @@ def conv_forward_raw(x, w_param, g: ConvGeom, stats=None, bias=None, out=None, c
         raise NotImplementedError("anisotropic stride")
     geo = (g.N * g.OH * g.OW, g.Co, g.T * g.Cx, g.Cx, g.OH, g.OW, g.H, g.W, g.sh, g.T * g.Cx, g.OH, g.OW,
            1, 0, 0, ldc, c_off)
-    _conv_gemm(x, wb, y, stats, bias, geo, dh, dw, tb, ws(dev).zero)
+    _conv_gemm(x, wb, y, stats, bias, geo, dh, dw, tb, ws(dev).zero, groups=stat_groups(geo[0]))
     return y
 
 
@@ -333,8 +352,9 @@ def conv_dgrad_raw(dy, w_param, g: ConvGeom, addend=None, link=None):
     dev = dy.device
     bwd = (None, None, None, None, 0, 1)
     if link is not None:
-        link.part = ws(dev).take_part(g.Ci)
-        bwd = (link.y, link.res, link.coef, link.part, link.act, G_STATS)
+        grp = stat_groups(g.N * g.H * g.W)
+        link.part = ws(dev).take_part(g.Ci, grp)
+        bwd = (link.y, link.res, link.coef, link.part, link.act, grp)
     wt = weight_bf16_t(w_param, g.Co, g.T, g.Ci)
     dx = _empty_cl(g.N, g.Ci, g.H, g.W, dev)
     for ph, pw, gh, gw, dh, dw, tb in _dgrad_phases(g):
@@ -374,6 +394,8 @@ def _wgrad_config(dy, x, g: ConvGeom, m, ntot, tiles):
 
     Tuning runs on a scratch gradient buffer, outside any graph capture, the first time a shape
     is seen (warmup), like a conv-algorithm "find" step."""
+    if DETERMINISTIC:  # one split: every dW element receives exactly one atomic contribution
+        return 1, (WGRAD_STAGES or 2)
     blocks = (WGRAD_TARGET_BLOCKS,) if WGRAD_TARGET_BLOCKS > 0 else WGRAD_CANDIDATES
     stages = (WGRAD_STAGES,) if WGRAD_STAGES > 0 else (1, 2)
     if len(blocks) == 1 and len(stages) == 1:
@@ -455,7 +477,7 @@ class ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, conv, want_stats, slot=None, fuse_bwd=False):
         g = ConvGeom(x, conv)
-        stats = ws(x.device).stats_buf(g.Co) if want_stats else None
+        stats = ws(x.device).stats_buf(g.Co, stat_groups(g.N * g.OH * g.OW)) if want_stats else None
         y = conv_forward_raw(x, w, g, stats=stats)
         ctx.g = g
         ctx.slot = slot
@@ -533,19 +555,20 @@ class BNActFn(torch.autograd.Function):
         coef = torch.empty(4 * c, dtype=torch.float32, device=dev)
         group = None
         count_t = None
+        grp = stat_groups(rows)
         if bn.training:
-            part = ws(dev).stats_buf(c)
+            part = ws(dev).stats_buf(c, grp)
             if not stats_ready:
-                C.bn_stats(y, rows, c, part, G_STATS)
+                C.bn_stats(y, rows, c, part, grp)
             group = _sync_group(bn)
             mom = bn.momentum if bn.momentum is not None else 0.1
             track = bn.track_running_stats and bn.running_mean is not None
             rs = (bn.running_mean, bn.running_var, bn.num_batches_tracked) if track else (None, None, None)
             if group is None:  # one launch: partial rows -> coefficients + running stats
-                C.bn_reduce_finalize(part, G_STATS, c, float(rows), gamma, beta, *rs, mom, bn.eps, coef)
+                C.bn_reduce_finalize(part, grp, c, float(rows), gamma, beta, *rs, mom, bn.eps, coef)
             else:
                 sums = torch.empty(2 * c + 1, dtype=torch.float64, device=dev)
-                C.bn_partials(part, G_STATS, c, sums, None, None)
+                C.bn_partials(part, grp, c, sums, None, None)
                 sums[2 * c:].fill_(float(rows))
                 dist.all_reduce(sums, group=group)
                 count_t = sums[2 * c:]
@@ -577,23 +600,24 @@ class BNActFn(torch.autograd.Function):
         c, rows = ctx.c, ctx.rows
         g = _cl(gout)
         link = ctx.link
+        grp = stat_groups(rows)
         if link is not None and link.done:
             # the consuming conv's dgrad epilogue already produced dz and the partial sums
             part, dz = link.part, g
             FUSED_BWD_COUNT[0] += 1
             link.y = link.coef = link.res = link.part = None
         else:
-            part = ws(dev).stats_buf(c)
+            part = ws(dev).stats_buf(c, grp)
             dz = torch.empty_like(y, memory_format=CL) if ctx.has_res else None
-            C.bn_bwd_reduce(g, y, coef, res, dz, rows, c, ctx.act, part, G_STATS)
+            C.bn_bwd_reduce(g, y, coef, res, dz, rows, c, ctx.act, part, grp)
         dgamma = grad_buffer(ctx.params[0], zero=False)
         dbeta = grad_buffer(ctx.params[1], zero=False)
         k = torch.empty(2 * c, dtype=torch.float32, device=dev)
         if ctx.training and ctx.group is None:  # one launch: partial rows -> dgamma, dbeta, k
-            C.bn_reduce_bwd(part, G_STATS, c, float(rows), dgamma, dbeta, k)
+            C.bn_reduce_bwd(part, grp, c, float(rows), dgamma, dbeta, k)
         else:
             sums = torch.empty(2 * c, dtype=torch.float64, device=dev)
-            C.bn_partials(part, G_STATS, c, sums, dgamma, dbeta)
+            C.bn_partials(part, grp, c, sums, dgamma, dbeta)
             if ctx.group is not None:
                 dist.all_reduce(sums, group=ctx.group)
             if ctx.training:
@@ -659,11 +683,12 @@ class ConvBiasFn(torch.autograd.Function):
         dw = conv_wgrad_raw(dy, x, w, g) if ctx.needs_input_grad[1] else None
         db = None
         if ctx.has_b and ctx.needs_input_grad[2]:
-            part = ws(dy.device).stats_buf(g.Co)
-            C.bn_stats(dy, g.N * g.OH * g.OW, g.Co, part, G_STATS)
+            grp = stat_groups(g.N * g.OH * g.OW)
+            part = ws(dy.device).stats_buf(g.Co, grp)
+            C.bn_stats(dy, g.N * g.OH * g.OW, g.Co, part, grp)
             sums = torch.empty(2 * g.Co, dtype=torch.float64, device=dy.device)
             db = grad_buffer(ctx.bias, zero=False)
-            C.bn_partials(part, G_STATS, g.Co, sums, None, db)
+            C.bn_partials(part, grp, g.Co, sums, None, db)
         return dx, dw, db, None
 
 
