@@ -62,6 +62,13 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--exact-val", action="store_true", help="mask DistributedSampler padding in validation (A15)")
     p.add_argument("--pretrained", default=None, help="local torchvision-layout state_dict to initialise the backbone")
+    p.add_argument("--step-timers", action="store_true",
+                   help="per-phase step timing (data/forward/backward/comm/optimizer) into --metrics-file")
+    p.add_argument("--profile-steps", type=int, default=0, help="torch.profiler trace over this many train steps")
+    p.add_argument("--profile-start", type=int, default=5, help="first profiled global step")
+    p.add_argument("--profile-dir", default="profiles/trace", help="where trace_rank<r>.json is written")
+    p.add_argument("--broadcast-buffers", action="store_true",
+                   help="DDP broadcast_buffers parity (X3): broadcast BN buffers from rank 0 before each forward")
     p.add_argument("--deterministic", action="store_true",
                    help="bitwise-reproducible GPU kernels (no split-K / cross-block fp32 atomics; slower)")
     p.add_argument("--timeout-min", type=float, default=10.0, help="process-group timeout (minutes)")

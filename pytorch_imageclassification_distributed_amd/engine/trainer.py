@@ -25,6 +25,7 @@ from __future__ import annotations
 import math
 import os
 import sys
+import time
 
 import torch
 import torch.distributed as dist
@@ -39,6 +40,7 @@ from ..ops.grad_arena import GradArena
 from ..parallel import GradReducer, convert_sync_batchnorm
 from ..utils import (BEST, LATEST, AccuracyCounter, DeviceMeter, JsonlLogger, load_checkpoint,
                      load_model_state, resolve_resume, save_checkpoint)
+from ..utils.timers import PhaseTimer
 from .config import parse_class_weights
 from .optim import FusedAdam, MultiStepLR
 
@@ -109,7 +111,8 @@ class Trainer:
             if ctx.world_size > 1:
                 net = nn.parallel.DistributedDataParallel(model, device_ids=[ctx.local_rank],
                                                           output_device=ctx.local_rank,
-                                                          bucket_cap_mb=a.bucket_mb)
+                                                          bucket_cap_mb=a.bucket_mb,
+                                                          broadcast_buffers=getattr(a, "broadcast_buffers", False))
             self.net = net
         else:
             if self.hip:
@@ -131,6 +134,10 @@ class Trainer:
         self.class_weight = torch.tensor(w, dtype=torch.float32, device=self.dev) if w else None
         self.best_score = 0.0
         self.start_epoch = 0
+        self.global_step = 0
+        self.timer = PhaseTimer(getattr(a, "step_timers", False), self.dev)
+        self.log = JsonlLogger(getattr(a, "metrics_file", None), self.ctx.is_main)
+        self._prof = None
 
     # ------------------------------------------------------------------ step
     def compute_loss(self, images, labels):
@@ -142,14 +149,29 @@ class Trainer:
         return Fx.cross_entropy(out, labels, self.class_weight)
 
     def train_step(self, images, labels):
-        """forward + loss + backward + (overlapped) all-reduce + Adam.  Returns the local loss."""
-        loss = self.compute_loss(images, labels)
-        self.optimizer.zero_grad(set_to_none=True)
-        if self.arena is not None:
-            self.arena.begin()  # one memset; backward kernels write into persistent slots
-        loss.backward()
-        scale = self.reducer.finish() if self.reducer is not None else 1.0
-        self.optimizer.step(grad_scale=scale)
+        """forward + loss + backward + (overlapped) all-reduce + Adam.  Returns the local loss.
+
+        Phases are bracketed for ``--step-timers`` (device events) and named for ``--profile-steps``
+        (torch.profiler ranges: imgcls::forward / backward / comm_wait / optimizer)."""
+        rf = torch.profiler.record_function
+        timer = self.timer
+        if self.reducer is not None and getattr(self.args, "broadcast_buffers", False):
+            self.reducer.sync_buffers()
+        with rf("imgcls::forward"):
+            loss = self.compute_loss(images, labels)
+        timer.mark("forward")
+        with rf("imgcls::backward"):
+            self.optimizer.zero_grad(set_to_none=True)
+            if self.arena is not None:
+                self.arena.begin()  # one memset; backward kernels write into persistent slots
+            loss.backward()
+        timer.mark("backward")
+        with rf("imgcls::comm_wait"):
+            scale = self.reducer.finish() if self.reducer is not None else 1.0
+        timer.mark("comm_wait")
+        with rf("imgcls::optimizer"):
+            self.optimizer.step(grad_scale=scale)
+        timer.mark("optimizer")
         return loss.detach()
 
     def reduce_loss(self, loss):
@@ -159,6 +181,29 @@ class Trainer:
             dist.all_reduce(red, op=dist.ReduceOp.SUM)
             red /= self.ctx.world_size
         return red
+
+    def _profile_tick(self):
+        """Start / stop the torch.profiler window [profile_start, profile_start + profile_steps)."""
+        a = self.args
+        n = getattr(a, "profile_steps", 0)
+        if n <= 0:
+            return
+        if self.global_step == a.profile_start and self._prof is None:
+            acts = [torch.profiler.ProfilerActivity.CPU]
+            if self.dev.type == "cuda":
+                acts.append(torch.profiler.ProfilerActivity.CUDA)
+            self._prof = torch.profiler.profile(activities=acts)
+            self._prof.__enter__()
+        elif self.global_step == a.profile_start + n and self._prof is not None:
+            if self.dev.type == "cuda":
+                torch.cuda.synchronize()
+            self._prof.__exit__(None, None, None)
+            os.makedirs(a.profile_dir, exist_ok=True)
+            path = os.path.join(a.profile_dir, f"trace_rank{self.ctx.rank}.json")
+            self._prof.export_chrome_trace(path)
+            if self.ctx.is_main:
+                print(f"profiler trace written to {path}", flush=True)
+            self._prof = False  # one window per run
 
     # ------------------------------------------------------------------ epochs
     def _loader(self, loader):
@@ -175,6 +220,8 @@ class Trainer:
             from tqdm import tqdm
             bar = tqdm(total=len(self.train_loader) if a.steps_per_epoch is None
                        else min(len(self.train_loader), a.steps_per_epoch), file=sys.stdout)
+        t_log, n_log = time.perf_counter(), 0
+        self.timer.mark("data")
         for index, data in enumerate(it):
             if a.steps_per_epoch is not None and index >= a.steps_per_epoch:
                 break
@@ -182,12 +229,26 @@ class Trainer:
             if images.device != self.dev:
                 images = images.to(self.dev, non_blocking=True)
                 labels = labels.to(self.dev, non_blocking=True)
+            self.timer.mark("data")
+            self._profile_tick()
             loss = self.train_step(images, labels)
             meter.update(self.reduce_loss(loss), images.size(0))
+            self.global_step += 1
+            n_log += images.size(0)
+            if (index + 1) % max(a.log_interval, 1) == 0:
+                if bar is not None:
+                    bar.set_description(f"Epoch: {epoch}; Loss {meter.val:.4f}|({meter.avg:.4f})")
+                if self.timer.enabled:
+                    tot = self.timer.flush()
+                    now = time.perf_counter()
+                    steps = max(a.log_interval, 1)
+                    self.log.log(kind="step", epoch=epoch, step=self.global_step,
+                                 images_per_sec=n_log * self.ctx.world_size / max(now - t_log, 1e-9),
+                                 **{f"ms_{k}": v / steps for k, v in tot.items()})
+                    self.timer.reset()
+                    t_log, n_log = now, 0
             if bar is not None:
                 bar.update(1)
-                if (index + 1) % max(a.log_interval, 1) == 0:
-                    bar.set_description(f"Epoch: {epoch}; Loss {meter.val:.4f}|({meter.avg:.4f})")
         if bar is not None:
             bar.set_description(f"Epoch: {epoch}; Loss {meter.val:.4f}|({meter.avg:.4f})")
             bar.close()
@@ -249,7 +310,7 @@ class Trainer:
     def fit(self):
         a = self.args
         self.maybe_resume()
-        log = JsonlLogger(a.metrics_file, self.ctx.is_main)
+        log = self.log
         history = []
         for epoch in range(self.start_epoch, a.epochs):
             self.train_sampler.set_epoch(epoch)
@@ -271,7 +332,10 @@ class Trainer:
             rec = dict(epoch=epoch, train_loss=train_loss, val_acc=val_acc, best=self.best_score,
                        lr=self.optimizer.param_groups[0]["lr"])
             history.append(rec)
-            log.log(**rec)
+            log.log(kind="epoch", **rec)
             if not math.isfinite(train_loss):
                 raise FloatingPointError(f"non-finite training loss at epoch {epoch}")
+        if self._prof:  # run ended inside the profiling window
+            self.global_step = a.profile_start + a.profile_steps
+            self._profile_tick()
         return history

@@ -74,6 +74,9 @@ def init_distributed(device: str = "auto", backend: str | None = None,
         kw = {}
         if backend == "nccl":
             kw["device_id"] = dev
+            # a failed / hung collective aborts the communicator and raises in every surviving rank
+            # instead of hanging until the job is killed
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         dist.init_process_group(backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(minutes=timeout_min), **kw)
     return DistContext(dist.get_rank(), dist.get_world_size(), lr, dev, dist.get_backend())

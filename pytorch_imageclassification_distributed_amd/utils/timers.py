@@ -15,27 +15,40 @@ import torch
 
 
 class PhaseTimer:
+    """``mark(name)`` closes the interval that started at the previous mark and books it under
+    ``name``.  GPU: HIP events, read back only in ``flush`` (one sync per log interval).  CPU: host
+    clock.  ``flush`` returns {phase: total ms} accumulated since the last ``reset``."""
+
     def __init__(self, enabled: bool, device: torch.device):
-        self.enabled = enabled and device.type == "cuda"
-        self.events: list[tuple[str, torch.cuda.Event]] = []
+        self.enabled = enabled
+        self.gpu = device.type == "cuda"
+        self.events: list = []
         self.totals: dict[str, float] = {}
 
     def mark(self, name: str) -> None:
         if not self.enabled:
             return
-        ev = torch.cuda.Event(enable_timing=True)
-        ev.record()
+        if self.gpu:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+        else:
+            ev = time.perf_counter()
         self.events.append((name, ev))
 
     def flush(self) -> dict:
         if not self.enabled or len(self.events) < 2:
-            self.events.clear()
             return self.totals
-        self.events[-1][1].synchronize()
+        if self.gpu:
+            self.events[-1][1].synchronize()
         for (_n0, e0), (n1, e1) in zip(self.events[:-1], self.events[1:]):
-            self.totals[n1] = self.totals.get(n1, 0.0) + e0.elapsed_time(e1)
-        self.events.clear()
+            dt = e0.elapsed_time(e1) if self.gpu else (e1 - e0) * 1e3
+            self.totals[n1] = self.totals.get(n1, 0.0) + dt
+        self.events = self.events[-1:]  # the last mark opens the next interval
         return self.totals
+
+    def reset(self) -> None:
+        self.totals = {}
+        self.events = self.events[-1:]
 
 
 class JsonlLogger:

@@ -142,3 +142,66 @@ def test_train_cli_two_processes(tmp_path):
     assert [r["val_acc"] for r in h0] == [r["val_acc"] for r in h1]  # combined accuracy on all ranks
     assert [r["train_loss"] for r in h0] == pytest.approx([r["train_loss"] for r in h1])  # globally averaged loss
     assert (tmp_path / "resnet18" / "best_model").exists()
+
+
+# ---------------------------------------------------------------------------
+def _w_fault(rank, world, port, marker, timeout_min):
+    import time
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    from pytorch_imageclassification_distributed_amd.parallel import init_distributed
+    init_distributed(device="cpu", backend="gloo", timeout_min=timeout_min)
+    dist.barrier()
+    if rank == 1:
+        os._exit(17)  # injected fault: the rank disappears without a clean shutdown
+    t0 = time.time()
+    try:
+        for _ in range(1000):
+            dist.all_reduce(torch.ones(1024))
+            time.sleep(0.01)
+        outcome = "no-error"
+    except Exception as e:  # noqa: BLE001 - any collective error is the expected outcome
+        outcome = type(e).__name__
+    with open(marker, "w") as f:
+        f.write(f"{outcome} {time.time() - t0:.2f}")
+    os._exit(0)
+
+
+def test_rank_failure_is_detected(tmp_path):
+    """Fault injection: when a peer dies mid-run the surviving rank's collective fails
+    within the process-group timeout instead of hanging."""
+    ctxm = mp.get_context("spawn")
+    port, marker = _port(), str(tmp_path / "rank0.txt")
+    procs = [ctxm.Process(target=_w_fault, args=(r, 2, port, marker, 0.5)) for r in range(2)]
+    for p_ in procs:
+        p_.start()
+    for p_ in procs:
+        p_.join(timeout=120)
+    alive = [p_ for p_ in procs if p_.is_alive()]
+    for p_ in alive:
+        p_.kill()
+    assert not alive, "a rank hung after its peer died"
+    outcome, secs = open(marker).read().split()
+    assert outcome != "no-error"
+    assert float(secs) < 60
+
+
+def _w_buffers(rank, world, port):
+    _setup(rank, world, port)
+    import torch.nn as nn
+    from pytorch_imageclassification_distributed_amd.parallel import GradReducer
+    m = nn.Sequential(nn.Conv2d(3, 4, 1), nn.BatchNorm2d(4))
+    torch.manual_seed(0)
+    for p_ in m.parameters():
+        nn.init.normal_(p_)
+    red = GradReducer(m, broadcast=False)
+    m[1].running_mean.fill_(float(rank + 1))
+    m[1].num_batches_tracked.fill_(rank + 5)
+    red.sync_buffers()
+    assert torch.all(m[1].running_mean == 1.0) and int(m[1].num_batches_tracked) == 5
+
+
+def test_broadcast_buffers():
+    """DDP broadcast_buffers parity (X3): rank 0's BN buffers overwrite the other ranks'."""
+    _run(_w_buffers)

@@ -51,3 +51,25 @@ def test_inception_aux_loss_path(tmp_path):
                        "--synthetic-val-size", "2", "--no-progress", "--epochs", "1", "--ckpt-dir", str(tmp_path),
                        "--resume", "none", "--val-batchsize", "2"])
     assert torch.isfinite(torch.tensor(hist[0]["train_loss"]))
+
+
+def test_step_timers_metrics_and_profiler(tmp_path):
+    """--step-timers writes per-phase step timing + throughput to the JSONL metrics file;
+    --profile-steps writes a torch.profiler chrome trace containing the phase ranges."""
+    import json
+    metrics = tmp_path / "m.jsonl"
+    prof = tmp_path / "prof"
+    train.main(ARGS + ["--epochs", "1", "--ckpt-dir", str(tmp_path), "--resume", "none", "--steps-per-epoch", "5",
+                       "--val-steps", "1", "--step-timers", "--log-interval", "2", "--metrics-file", str(metrics),
+                       "--profile-steps", "2", "--profile-start", "1", "--profile-dir", str(prof)])
+    recs = [json.loads(line) for line in metrics.read_text().splitlines()]
+    steps = [r for r in recs if r["kind"] == "step"]
+    assert len(steps) == 2 and [r["step"] for r in steps] == [2, 4]
+    for r in steps:
+        assert r["images_per_sec"] > 0
+        assert {"ms_forward", "ms_backward", "ms_comm_wait", "ms_optimizer", "ms_data"} <= set(r)
+        assert r["ms_forward"] > 0 and r["ms_backward"] > 0
+    assert [r for r in recs if r["kind"] == "epoch"]
+    trace = json.loads((prof / "trace_rank0.json").read_text())
+    names = {e.get("name") for e in trace.get("traceEvents", [])}
+    assert {"imgcls::forward", "imgcls::backward", "imgcls::optimizer"} <= names
