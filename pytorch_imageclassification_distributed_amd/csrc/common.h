@@ -13,6 +13,8 @@
 // address receives exactly one contribution (split-K off, per-block partial rows reduced in order).
 extern int g_imgcls_det;
 
+
+
 typedef uint16_t bf16_t;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -89,3 +91,72 @@ DEVI float act_grad(float z, float g, int act) {
 #define HIP_CHECK_LAUNCH() do { hipError_t e__ = hipGetLastError(); if (e__ != hipSuccess) return (int)e__; } while (0)
 
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+// out[n][c] (+)= scale * sum_{p in split} a[n][p][c] (* b[n][p][c] when PROD), NHWC bf16 inputs, fp32 out.
+// block = CHB channel-chunk lanes (8 channels each) x RP pixel lanes, LDS tree over RP; grid =
+// (N, channel slices, pixel splits); splits > 1 accumulate with one atomic per channel per block.
+template <bool PROD>
+__global__ __launch_bounds__(256) void spatial_reduce_kernel(const bf16_t* __restrict__ a,
+                                                             const bf16_t* __restrict__ b, float* __restrict__ out,
+                                                             int HW, int C, int rows_per_split, float scale,
+                                                             int atomic) {
+  __shared__ float red[256][9];
+  const int cch = C >> 3;
+  const int CHB = cch < 64 ? cch : 64;
+  const int RP = 256 / CHB;
+  const int tid = threadIdx.x, lc = tid % CHB, lr = tid / CHB;
+  const int chunk = blockIdx.y * CHB + lc;
+  const int n = blockIdx.x;
+  const int p0 = blockIdx.z * rows_per_split, p1 = min(HW, p0 + rows_per_split);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (lr < RP && chunk < cch) {
+    const long base = (long)n * HW * C + chunk * 8;
+#pragma unroll 4
+    for (int p = p0 + lr; p < p1; p += RP) {
+      float va[8];
+      unpack8(*(const uint4*)(a + base + (long)p * C), va);
+      if (PROD) {
+        float vb[8];
+        unpack8(*(const uint4*)(b + base + (long)p * C), vb);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += va[k] * vb[k];
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += va[k];
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[tid][k] = acc[k];
+  __syncthreads();
+  if (lr == 0 && chunk < cch) {
+    for (int r = 1; r < RP; ++r)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += red[tid + r * CHB][k];
+    float* o = out + (long)n * C + chunk * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (atomic) atomicAdd(o + k, acc[k] * scale);
+      else o[k] = acc[k] * scale;
+    }
+  }
+}
+
+// launch helper: splits HW so the grid has >= ~1024 blocks (one pass in deterministic mode)
+template <bool PROD>
+inline int spatial_reduce_launch(const bf16_t* a, const bf16_t* b, float* out, int N, int HW, int C, float scale,
+                                 hipStream_t s) {
+  const int cch = C / 8;
+  const int CHB = cch < 64 ? cch : 64;
+  const int slices = (cch + CHB - 1) / CHB;
+  const int RP = 256 / CHB;
+  int splits = 1;
+  if (!g_imgcls_det)
+    while ((long)N * slices * splits < 1024 && HW / (splits * 2) >= 8 * RP) splits *= 2;
+  const int rps = (HW + splits - 1) / splits;
+  splits = (HW + rps - 1) / rps;
+  if (splits > 1 && hipMemsetAsync(out, 0, sizeof(float) * (size_t)N * C, s) != hipSuccess) return 1;
+  hipLaunchKernelGGL(spatial_reduce_kernel<PROD>, dim3(N, slices, splits), dim3(256), 0, s, a, b, out, HW, C, rps,
+                     scale, splits > 1 ? 1 : 0);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}

@@ -149,26 +149,6 @@ __global__ void se_scale_kernel(const bf16_t* __restrict__ x, const float* __res
   }
 }
 
-// ds[n,c] = sum_p dy[n,p,c] * x[n,p,c]   (one thread per (n, chunk))
-__global__ void se_ds_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, float* __restrict__ ds,
-                             int N, int HW, int C) {
-  const int cch = C >> 3;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N * cch) return;
-  const int n = i / cch, c0 = (i - n * cch) * 8;
-  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int p = 0; p < HW; ++p) {
-    float a[8], b[8];
-    const long o = ((long)n * HW + p) * C + c0;
-    unpack8(*(const uint4*)(dy + o), a);
-    unpack8(*(const uint4*)(x + o), b);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) acc[k] += a[k] * b[k];
-  }
-#pragma unroll
-  for (int k = 0; k < 8; ++k) ds[(long)n * C + c0 + k] = acc[k];
-}
-
 // dx = dy * s[n,c] + dp[n,c] / HW
 __global__ void se_dx_kernel(const bf16_t* __restrict__ dy, const float* __restrict__ s, const float* __restrict__ dp,
                              bf16_t* __restrict__ dx, int N, int HW, int C) {
@@ -267,9 +247,7 @@ int se_scale_launch(const bf16_t* x, const float* sc, bf16_t* y, int N, int HW, 
 }
 
 int se_ds_launch(const bf16_t* dy, const bf16_t* x, float* ds, int N, int HW, int C, hipStream_t s) {
-  hipLaunchKernelGGL(se_ds_kernel, dim3(cdiv((long)N * (C / 8), 256)), dim3(256), 0, s, dy, x, ds, N, HW, C);
-  HIP_CHECK_LAUNCH();
-  return 0;
+  return spatial_reduce_launch<true>(dy, x, ds, N, HW, C, 1.f, s);
 }
 
 int se_dx_launch(const bf16_t* dy, const float* sc, const float* dp, bf16_t* dx, int N, int HW, int C,

@@ -153,25 +153,6 @@ __global__ void avgpool_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __rest
   }
 }
 
-// one thread per (n, 8-channel chunk); loops over HW
-__global__ void gap_fwd_kernel(const bf16_t* __restrict__ x, float* __restrict__ y, int N, int HW, int C) {
-  const int cch = C >> 3;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N * cch) return;
-  const int n = i / cch, c0 = (i - n * cch) * 8;
-  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const bf16_t* p = x + (long)n * HW * C + c0;
-  for (int s = 0; s < HW; ++s) {
-    float v[8];
-    unpack8(*(const uint4*)(p + (long)s * C), v);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) acc[k] += v[k];
-  }
-  const float inv = 1.f / HW;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) y[(long)n * C + c0 + k] = acc[k] * inv;
-}
-
 __global__ void gap_bwd_kernel(const float* __restrict__ dy, bf16_t* __restrict__ dx, int N, int HW, int C) {
   const int cch = C >> 3;
   const long total = (long)N * HW * cch;
@@ -229,9 +210,7 @@ int avgpool_bwd_launch(const bf16_t* dy, bf16_t* dx, int N, int H, int W, int C,
 }
 
 int gap_fwd_launch(const bf16_t* x, float* y, int N, int HW, int C, hipStream_t s) {
-  hipLaunchKernelGGL(gap_fwd_kernel, dim3(cdiv((long)N * (C / 8), 256)), dim3(256), 0, s, x, y, N, HW, C);
-  HIP_CHECK_LAUNCH();
-  return 0;
+  return spatial_reduce_launch<false>(x, nullptr, y, N, HW, C, 1.f / HW, s);
 }
 
 int gap_bwd_launch(const float* dy, bf16_t* dx, int N, int HW, int C, hipStream_t s) {
