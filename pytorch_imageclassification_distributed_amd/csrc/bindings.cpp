@@ -366,19 +366,14 @@ void dw_dgrad(Tensor dy, Tensor w, Tensor dx, int N, int H, int W, int C, int OH
 void dw_wgrad(Tensor dy, Tensor x, Tensor dw, int N, int H, int W, int C, int OH, int OW, int kh, int kw, int sh,
               int sw, int pt, int pl) {
   req(dw, F32, "dw");
-  if (g_imgcls_det) {  // per-block partial rows, then an ordered column sum (no cross-block atomics)
-    const long rows = dw_wgrad_partial_rows(N, OH, OW, kh, kw);
-    const int cols = C * kh * kw;
-    Tensor part = at::zeros({rows, (long)cols}, dw.options());
-    check(dw_wgrad_launch(ptr<bf16_t>(dy), ptr<bf16_t>(x), ptr<float>(dw), N, H, W, C, OH, OW, kh, kw, sh, sw, pt,
-                          pl, ptr<float>(part), cur()),
-          "dw_wgrad");
-    check(colsum_launch(ptr<float>(part), nullptr, ptr<float>(dw), (int)rows, cols, cols, 1, cur()), "dw_wgrad");
-    return;
-  }
+  // per-block partial rows (plain stores), then an ordered column sum into dw - no contended atomics
+  const long rows = dw_wgrad_partial_rows(N, OH, OW, kh, kw);
+  const int cols = C * kh * kw;
+  Tensor part = at::empty({rows, (long)cols}, dw.options());
   check(dw_wgrad_launch(ptr<bf16_t>(dy), ptr<bf16_t>(x), ptr<float>(dw), N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl,
-                        nullptr, cur()),
+                        ptr<float>(part), cur()),
         "dw_wgrad");
+  check(colsum_launch(ptr<float>(part), nullptr, ptr<float>(dw), (int)rows, cols, cols, 0, cur()), "dw_wgrad");
 }
 
 void se_scale(Tensor x, Tensor s, Tensor y, int N, int HW, int C) {

@@ -79,24 +79,123 @@ __global__ void dw_dgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __r
   }
 }
 
-// grid: (pixel blocks, taps); block = CHB chunk lanes x RP pixel lanes; dw layout [C][taps] fp32
+// Fixed-size (K x K) forms of the two kernels above: taps fully unrolled, every load unconditional
+// (clamped address, zeroed value), so a lane keeps all K*K 16-B loads in flight at once.
+template <int K>
+__global__ __launch_bounds__(256) void dw_fwd_k_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+                                                       bf16_t* __restrict__ y, DwGeom g) {
+  const int cch = g.C >> 3;
+  const long total = (long)g.N * g.OH * g.OW * cch;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cch) * 8;
+    long t = i / cch;
+    const int ow = (int)(t % g.OW); t /= g.OW;
+    const int oh = (int)(t % g.OH);
+    const int n = (int)(t / g.OH);
+    const bf16_t* xn = x + (long)n * g.H * g.W * g.C + c0;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < K; ++r) {
+      const int ih = oh * g.sh - g.pt + r;
+      const int ihc = min(max(ih, 0), g.H - 1);
+      uint4 raw[K];
+#pragma unroll
+      for (int c = 0; c < K; ++c) {
+        const int iwc = min(max(ow * g.sw - g.pl + c, 0), g.W - 1);
+        raw[c] = *(const uint4*)(xn + ((long)ihc * g.W + iwc) * g.C);
+      }
+#pragma unroll
+      for (int c = 0; c < K; ++c) {
+        const int iw = ow * g.sw - g.pl + c;
+        const bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+        float xv[8], wv[8];
+        unpack8(ok ? raw[c] : make_uint4(0u, 0u, 0u, 0u), xv);
+        unpack8(*(const uint4*)(w + (long)(r * K + c) * g.C + c0), wv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += xv[k] * wv[k];
+      }
+    }
+    *(uint4*)(y + (((long)n * g.OH + oh) * g.OW + ow) * g.C + c0) = pack8(acc);
+  }
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void dw_dgrad_k_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ w,
+                                                         bf16_t* __restrict__ dx, DwGeom g) {
+  const int cch = g.C >> 3;
+  const long total = (long)g.N * g.H * g.W * cch;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cch) * 8;
+    long t = i / cch;
+    const int wi = (int)(t % g.W); t /= g.W;
+    const int h = (int)(t % g.H);
+    const int n = (int)(t / g.H);
+    const bf16_t* dyn = dy + (long)n * g.OH * g.OW * g.C + c0;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < K; ++r) {
+      const int a = h + g.pt - r;
+      const int oh = a / g.sh;  // a >= 0 guarded below; C division truncates toward zero
+      const bool rok = a >= 0 && a - oh * g.sh == 0 && oh < g.OH;
+      const int ohc = min(max(oh, 0), g.OH - 1);
+      uint4 raw[K];
+#pragma unroll
+      for (int c = 0; c < K; ++c) {
+        const int b = wi + g.pl - c;
+        const int owc = min(max(b / g.sw, 0), g.OW - 1);
+        raw[c] = *(const uint4*)(dyn + ((long)ohc * g.OW + owc) * g.C);
+      }
+#pragma unroll
+      for (int c = 0; c < K; ++c) {
+        const int b = wi + g.pl - c;
+        const int ow = b / g.sw;
+        const bool ok = rok && b >= 0 && b - ow * g.sw == 0 && ow < g.OW;
+        float dv[8], wv[8];
+        unpack8(ok ? raw[c] : make_uint4(0u, 0u, 0u, 0u), dv);
+        unpack8(*(const uint4*)(w + (long)(r * K + c) * g.C + c0), wv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += dv[k] * wv[k];
+      }
+    }
+    *(uint4*)(dx + (((long)n * g.H + h) * g.W + wi) * g.C + c0) = pack8(acc);
+  }
+}
+
+// grid: (pixel blocks, tap groups of <= DW_TG taps); block = CHB chunk lanes x RP pixel lanes.
+// Each lane loads its dY chunk once per pixel and multiplies it with the x chunks of every tap in the
+// group (neighbouring lanes hit neighbouring pixels, so the shifted x loads are cache hits); per-tap
+// sums are reduced over the pixel lanes in LDS and STORED into the block's own partial row
+// part[block][C*taps] (no cross-block atomics: thousands of blocks adding into the same C*taps
+// addresses serialise in L2); the rows are then summed in order by colsum.  dw layout [C][taps].
+constexpr int DW_TG = 9;
+
 __global__ __launch_bounds__(256) void dw_wgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
-                                                        float* __restrict__ dw, DwGeom g, long pix_per_block,
-                                                        long block_stride) {
+                                                        float* __restrict__ part, DwGeom g, long pix_per_block) {
   __shared__ float red[256][9];
   const int cch = g.C >> 3;
   const int CHB = cch < 256 ? cch : 256;
   const int RP = 256 / CHB;
   const int tid = threadIdx.x;
   const int lc = tid % CHB, lr = tid / CHB;
-  const int tap = blockIdx.y;
-  const int r = tap / g.kw, q = tap - r * g.kw;
+  const int T = g.kh * g.kw;
+  const int t0 = blockIdx.y * DW_TG;
+  const int nt = min(DW_TG, T - t0);
   const long npix = (long)g.N * g.OH * g.OW;
-  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int dh[DW_TG], dwo[DW_TG];
+#pragma unroll
+  for (int j = 0; j < DW_TG; ++j) {
+    const int tap = t0 + (j < nt ? j : 0);
+    dh[j] = tap / g.kw - g.pt;
+    dwo[j] = tap % g.kw - g.pl;
+  }
+  float* dst = part + blockIdx.x * (long)g.C * T;
   for (int cb = 0; cb < cch; cb += CHB) {
     const int chunk = cb + lc;
+    float acc[DW_TG][8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+    for (int j = 0; j < DW_TG; ++j)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[j][k] = 0.f;
     if (lr < RP && chunk < cch) {
       const int c0 = chunk * 8;
       const long pbeg = blockIdx.x * pix_per_block;
@@ -106,29 +205,47 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const bf16_t* __restrict_
         const int ow = (int)(t % g.OW); t /= g.OW;
         const int oh = (int)(t % g.OH);
         const int n = (int)(t / g.OH);
-        const int ih = oh * g.sh - g.pt + r, iw = ow * g.sw - g.pl + q;
-        if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) continue;
-        float dv[8], xv[8];
+        float dv[8];
         unpack8(*(const uint4*)(dy + pix * g.C + c0), dv);
-        unpack8(*(const uint4*)(x + (((long)n * g.H + ih) * g.W + iw) * g.C + c0), xv);
+        const bf16_t* xn = x + (long)n * g.H * g.W * g.C + c0;
+        // unconditional loads (clamped address, zeroed value) so all taps' loads are in flight together
+        uint4 raw[DW_TG];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] += dv[k] * xv[k];
+        for (int j = 0; j < DW_TG; ++j) {
+          const int ih = oh * g.sh + dh[j], iw = ow * g.sw + dwo[j];
+          const int ihc = min(max(ih, 0), g.H - 1), iwc = min(max(iw, 0), g.W - 1);
+          raw[j] = *(const uint4*)(xn + ((long)ihc * g.W + iwc) * g.C);
+        }
+#pragma unroll
+        for (int j = 0; j < DW_TG; ++j) {
+          const int ih = oh * g.sh + dh[j], iw = ow * g.sw + dwo[j];
+          const bool ok = j < nt && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+          float xv[8];
+          unpack8(ok ? raw[j] : make_uint4(0u, 0u, 0u, 0u), xv);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[j][k] += dv[k] * xv[k];
+        }
       }
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) red[tid][k] = acc[k];
-    __syncthreads();
-    if (lr == 0 && chunk < cch) {
-      for (int rr = 1; rr < RP; ++rr)
+    for (int j = 0; j < DW_TG; ++j) {
+      if (j < nt) {  // nt is block-uniform: the barriers below are reached by every lane
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] += red[tid + rr * CHB][k];
-      const int T = g.kh * g.kw;
-      // block_stride > 0 (deterministic mode): each pixel block owns a partial row, summed in order later
-      float* dst = dw + blockIdx.x * block_stride;
+        for (int k = 0; k < 8; ++k) red[tid][k] = acc[j][k];
+        __syncthreads();
+        if (lr == 0 && chunk < cch) {
+          float v[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) atomicAdd(dst + (long)(chunk * 8 + k) * T + tap, acc[k]);
+          for (int k = 0; k < 8; ++k) v[k] = red[tid][k];
+          for (int rr = 1; rr < RP; ++rr)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] += red[tid + rr * CHB][k];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) dst[(long)(chunk * 8 + k) * T + t0 + j] = v[k];
+        }
+        __syncthreads();
+      }
     }
-    __syncthreads();
   }
 }
 
@@ -197,7 +314,10 @@ __global__ void act32_bwd_kernel(const float* __restrict__ x, const float* __res
 int dw_fwd_launch(const bf16_t* x, const bf16_t* w, bf16_t* y, float* /*stats*/, int N, int H, int W, int C, int OH,
                   int OW, int kh, int kw, int sh, int sw, int pt, int pl, hipStream_t s) {
   DwGeom g{N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl};
-  hipLaunchKernelGGL(dw_fwd_kernel, dim3(grid_for((long)N * OH * OW * (C / 8))), dim3(256), 0, s, x, w, y, g);
+  const dim3 grid(grid_for((long)N * OH * OW * (C / 8)));
+  if (kh == 3 && kw == 3) hipLaunchKernelGGL(dw_fwd_k_kernel<3>, grid, dim3(256), 0, s, x, w, y, g);
+  else if (kh == 5 && kw == 5) hipLaunchKernelGGL(dw_fwd_k_kernel<5>, grid, dim3(256), 0, s, x, w, y, g);
+  else hipLaunchKernelGGL(dw_fwd_kernel, grid, dim3(256), 0, s, x, w, y, g);
   HIP_CHECK_LAUNCH();
   return 0;
 }
@@ -205,13 +325,17 @@ int dw_fwd_launch(const bf16_t* x, const bf16_t* w, bf16_t* y, float* /*stats*/,
 int dw_dgrad_launch(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int W, int C, int OH, int OW,
                     int kh, int kw, int sh, int sw, int pt, int pl, hipStream_t s) {
   DwGeom g{N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl};
-  hipLaunchKernelGGL(dw_dgrad_kernel, dim3(grid_for((long)N * H * W * (C / 8))), dim3(256), 0, s, dy, w, dx, g);
+  const dim3 grid(grid_for((long)N * H * W * (C / 8)));
+  if (kh == 3 && kw == 3) hipLaunchKernelGGL(dw_dgrad_k_kernel<3>, grid, dim3(256), 0, s, dy, w, dx, g);
+  else if (kh == 5 && kw == 5) hipLaunchKernelGGL(dw_dgrad_k_kernel<5>, grid, dim3(256), 0, s, dy, w, dx, g);
+  else hipLaunchKernelGGL(dw_dgrad_kernel, grid, dim3(256), 0, s, dy, w, dx, g);
   HIP_CHECK_LAUNCH();
   return 0;
 }
 
 static long dw_wgrad_ppb(long npix, int T, long* pblocks_out) {
-  long pblocks = 2048 / T;
+  const int groups = (T + DW_TG - 1) / DW_TG;
+  long pblocks = 1024 / groups;
   if (pblocks < 8) pblocks = 8;
   long ppb = (npix + pblocks - 1) / pblocks;
   if (ppb < 64) ppb = 64;
@@ -225,17 +349,16 @@ long dw_wgrad_partial_rows(int N, int OH, int OW, int kh, int kw) {
   return pb;
 }
 
-// part: null -> atomics straight into dw; else [pblocks][C*T] zeroed partial rows (deterministic mode),
-// which the caller reduces in order (colsum)
-int dw_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, int N, int H, int W, int C, int OH, int OW,
+// part: [dw_wgrad_partial_rows][C*T] scratch, fully overwritten; the caller reduces it into dw (colsum)
+int dw_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* /*dw*/, int N, int H, int W, int C, int OH, int OW,
                     int kh, int kw, int sh, int sw, int pt, int pl, float* part, hipStream_t s) {
   DwGeom g{N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl};
   const long npix = (long)N * OH * OW;
   const int T = kh * kw;
   long pblocks;
   const long ppb = dw_wgrad_ppb(npix, T, &pblocks);
-  hipLaunchKernelGGL(dw_wgrad_kernel, dim3((unsigned)pblocks, T), dim3(256), 0, s, dy, x, part ? part : dw, g, ppb,
-                     part ? (long)C * T : 0L);
+  hipLaunchKernelGGL(dw_wgrad_kernel, dim3((unsigned)pblocks, (T + DW_TG - 1) / DW_TG), dim3(256), 0, s, dy, x,
+                     part, g, ppb);
   HIP_CHECK_LAUNCH();
   return 0;
 }

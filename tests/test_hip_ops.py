@@ -187,7 +187,9 @@ def test_conv_bn_act(act, use_res):
 def test_depthwise_bn_silu():
     hip = _hip()
     torch.manual_seed(3)
-    for (c, k, s, hw) in [(96, 3, 2, 28), (144, 5, 1, 14), (32, 3, 1, 16)]:
+    # k3/k5 take the unrolled kernels (odd and even sizes, both strides); k7 the generic ones
+    for (c, k, s, hw) in [(96, 3, 2, 28), (144, 5, 1, 14), (32, 3, 1, 16), (40, 5, 2, 15), (24, 3, 2, 9),
+                          (16, 7, 1, 12), (48, 7, 2, 13)]:
         conv = nn.Conv2d(c, c, k, s, 0, groups=c, bias=False).to(DEV).to(memory_format=CL)
         conv.tf_same = True
         bn = nn.BatchNorm2d(c, eps=1e-3, momentum=0.01).to(DEV)
