@@ -17,7 +17,7 @@ using at::Tensor;
 using OT = std::optional<Tensor>;
 
 // ---- launcher prototypes (defined in *.hip) ----
-int bn_partials_launch(float*, int, int, double*, float*, float*, hipStream_t);
+int bn_partials_launch(float*, int, int, double*, float*, float*, double, hipStream_t);
 int bn_reduce_finalize_launch(float*, int, int, double, const float*, const float*, float*, float*, long long*, float,
                               float, float*, hipStream_t);
 int bn_reduce_bwd_launch(float*, int, int, double, float*, float*, float*, hipStream_t);
@@ -153,9 +153,11 @@ void conv_wgrad(Tensor dY, Tensor X, Tensor dW, int M, int Cout, int Cin, int Nt
   check(conv_wgrad_launch(p, splits, cur()), "conv_wgrad");
 }
 
-void bn_partials(Tensor part, int G, int C, Tensor sums, OT dgamma, OT dbeta) {
+void bn_partials(Tensor part, int G, int C, Tensor sums, OT dgamma, OT dbeta, double count) {
   req(part, F32, "part"); req(sums, at::kDouble, "sums");
-  check(bn_partials_launch(ptr<float>(part), G, C, ptr<double>(sums), optr<float>(dgamma), optr<float>(dbeta), cur()),
+  TORCH_CHECK(count < 0 || sums.numel() >= 2 * C + 1, "bn_partials: sums has no count slot");
+  check(bn_partials_launch(ptr<float>(part), G, C, ptr<double>(sums), optr<float>(dgamma), optr<float>(dbeta), count,
+                           cur()),
         "bn_partials");
 }
 
@@ -413,7 +415,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_deterministic", [](bool v) { set_deterministic(v ? 1 : 0); });
   m.def("conv_set_single_stage", &conv_set_single_stage);
   m.def("conv_set_wgrad_variant", &conv_set_wgrad_variant);
-  m.def("bn_partials", &bn_partials);
+  m.def("bn_partials", &bn_partials, pybind11::arg("part"), pybind11::arg("G"), pybind11::arg("C"),
+        pybind11::arg("sums"), pybind11::arg("dgamma"), pybind11::arg("dbeta"), pybind11::arg("count") = -1.0);
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_reduce_finalize", &bn_reduce_finalize);
   m.def("bn_reduce_bwd", &bn_reduce_bwd);

@@ -24,7 +24,8 @@ namespace {
 // block = 64 channels x 4 row-groups; each row-group sums G/4 partial rows
 __global__ __launch_bounds__(256) void bn_partials_kernel(float* __restrict__ part, int G, int C,
                                                           double* __restrict__ sums, float* __restrict__ dgamma,
-                                                          float* __restrict__ dbeta) {
+                                                          float* __restrict__ dbeta, double count) {
+  if (count >= 0.0 && blockIdx.x == 0 && threadIdx.x == 0) sums[2 * C] = count;  // SyncBN payload tail
   __shared__ double red[2][4][64];
   const int lc = threadIdx.x & 63, lg = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lc;
@@ -362,9 +363,10 @@ int grid_for(long work, int per_block = 256, int cap = 4096) {
 
 }  // namespace
 
-int bn_partials_launch(float* part, int G, int C, double* sums, float* dgamma, float* dbeta,
+int bn_partials_launch(float* part, int G, int C, double* sums, float* dgamma, float* dbeta, double count,
                        hipStream_t s) {
-  hipLaunchKernelGGL(bn_partials_kernel, dim3(cdiv(C, 64)), dim3(256), 0, s, part, G, C, sums, dgamma, dbeta);
+  hipLaunchKernelGGL(bn_partials_kernel, dim3(cdiv(C, 64)), dim3(256), 0, s, part, G, C, sums, dgamma, dbeta,
+                     count);
   HIP_CHECK_LAUNCH();
   return 0;
 }

@@ -118,7 +118,10 @@ class Trainer:
             if self.hip:
                 model = model.to(memory_format=torch.channels_last)
             if a.sync_bn:
-                convert_sync_batchnorm(model)
+                # a communicator of its own: the 2x53 latency-bound SyncBN collectives must not queue
+                # behind the reducer's 32 MiB gradient buckets on the default group's RCCL stream
+                grp = dist.new_group(list(range(ctx.world_size))) if ctx.world_size > 1 else None
+                convert_sync_batchnorm(model, grp)
             if ctx.world_size > 1:
                 comm = torch.bfloat16 if a.comm_dtype == "bf16" else None
                 self.reducer = GradReducer(model, bucket_cap_mb=a.bucket_mb, comm_dtype=comm)

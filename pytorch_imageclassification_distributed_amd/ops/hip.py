@@ -568,8 +568,7 @@ class BNActFn(torch.autograd.Function):
                 C.bn_reduce_finalize(part, grp, c, float(rows), gamma, beta, *rs, mom, bn.eps, coef)
             else:
                 sums = torch.empty(2 * c + 1, dtype=torch.float64, device=dev)
-                C.bn_partials(part, grp, c, sums, None, None)
-                sums[2 * c:].fill_(float(rows))
+                C.bn_partials(part, grp, c, sums, None, None, float(rows))  # + local count in the tail
                 dist.all_reduce(sums, group=group)
                 count_t = sums[2 * c:]
                 C.bn_finalize(sums, count_t, float(rows), gamma, beta, *rs, mom, bn.eps, c, coef)
