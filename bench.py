@@ -52,6 +52,8 @@ def parse():
     p.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--dist-backend", default="auto", help="auto (RCCL) | gloo (functional multi-rank runs on one GPU)")
     p.add_argument("--profile-steps", type=int, default=0)
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
+                   help="fp8: MX-FP8 forward convolutions (BASELINE config 5); bf16 elsewhere")
     return p.parse_args()
 
 
@@ -76,7 +78,7 @@ def main():
         "--batchsize", str(a.batch), "--num-classes", str(a.num_classes),
         "--num-workers", "0", "--synthetic-train-size", "8", "--synthetic-val-size", "8",
         "--compute", a.compute, "--bucket-mb", str(a.bucket_mb), "--comm-dtype", a.comm_dtype,
-        "--lr", "1e-4",
+        "--lr", "1e-4", "--dtype", a.dtype,
     ] + ([] if sync_bn else ["--no-sync-bn"]))
     tr = Trainer(targs, ctx)
     tr.net.train()
@@ -117,15 +119,15 @@ def main():
     if ctx.rank == 0:
         imgs = a.batch * ctx.world_size * a.steps
         value = imgs / dt
-        base = load_baseline(ctx.world_size, a.batch)
-        metric = METRIC if (a.model, a.image_size) == ("resnet50", 224) else \
-            f"images/sec (whole node) {a.model} {a.image_size}x{a.image_size} bf16 MI355X"
+        base = load_baseline(ctx.world_size, a.batch) if a.dtype == "bf16" else None
+        metric = METRIC if (a.model, a.image_size, a.dtype) == ("resnet50", 224, "bf16") else \
+            f"images/sec (whole node) {a.model} {a.image_size}x{a.image_size} {a.dtype} MI355X"
         print(json.dumps({
             "metric": metric, "value": round(value, 2), "unit": "images/sec",
             "n_gpus": ctx.world_size, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": round(value / base, 4) if base else None,
-            "dtype": "bf16", "data": "synthetic (on-device random images, random-init weights)",
+            "dtype": a.dtype, "data": "synthetic (on-device random images, random-init weights)",
             "config": {"model": a.model, "global_batch": a.batch * ctx.world_size,
                        "per_gpu_batch": a.batch, "seq_len": None, "image_size": a.image_size,
                        "num_classes": a.num_classes, "parallelism": f"dp{ctx.world_size}",

@@ -24,7 +24,8 @@ int bn_reduce_bwd_launch(float*, int, int, double, float*, float*, float*, hipSt
 int bn_finalize_launch(const double*, const double*, double, const float*, const float*, float*, float*,
                        long long*, float, float, int, float*, hipStream_t);
 int bn_eval_coef_launch(const float*, const float*, const float*, const float*, float, int, float*, hipStream_t);
-int bn_apply_launch(const bf16_t*, const float*, const bf16_t*, bf16_t*, long, int, int, int, int, hipStream_t);
+int bn_apply_launch(const bf16_t*, const float*, const bf16_t*, bf16_t*, long, int, int, int, int, uint8_t*, uint8_t*,
+                    hipStream_t);
 int bn_bwd_reduce_launch(const bf16_t*, const bf16_t*, const float*, const bf16_t*, bf16_t*, long, int, int,
                          float*, int, hipStream_t);
 int bn_bwd_k_launch(const double*, const double*, double, int, float*, hipStream_t);
@@ -53,6 +54,9 @@ int cast_bf16_launch(const float*, bf16_t*, long, hipStream_t);
 int weight_pad_launch(const bf16_t*, bf16_t*, long, int, int, hipStream_t);
 int weight_t_launch(const bf16_t*, bf16_t*, int, int, int, hipStream_t);
 int weight_t_tiles_launch(const void*, const void*, int, hipStream_t);
+int mx_quant_act_launch(const bf16_t*, uint8_t*, uint8_t*, long, int, hipStream_t);
+int mx_quant_w_launch(const void*, const void*, int, hipStream_t);
+int mx_wjob_bytes();
 int weight_t_job_bytes();
 int grad_unpad_launch(const float*, float*, long, int, int, hipStream_t);
 int copy_channels_launch(const bf16_t*, int, int, bf16_t*, int, int, long, int, hipStream_t);
@@ -101,8 +105,12 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
                int IH, int IW, int sA, int ldb, int OH, int OW, int so, int oh0, int ow0, int ldc, int c_off,
                std::vector<int> dh, std::vector<int> dw, std::vector<int> tb, int stats_groups, Tensor zero,
                OT addend, OT bwd_y, OT bwd_res, OT bwd_coef, OT bwd_part, int bwd_act, int bwd_groups,
-               int stages, int tile_n) {
-  req(A, BF, "A"); req(B, BF, "B"); req(C, BF, "C");
+               int stages, int tile_n, OT a_sc, OT b_sc) {
+  const bool fp8 = a_sc.has_value() && a_sc->defined();
+  TORCH_CHECK(A.scalar_type() == (fp8 ? at::kFloat8_e4m3fn : BF) && B.scalar_type() == A.scalar_type(),
+              "conv_gemm: A and B must both be bf16, or both float8_e4m3fn with scales");
+  TORCH_CHECK(A.is_cuda() && B.is_cuda(), "conv_gemm: A/B must be GPU tensors");
+  req(C, BF, "C");
   TORCH_CHECK(zero.is_cuda() && zero.nbytes() >= 16, "conv_gemm: zero page must be >= 16 device bytes");
   TORCH_CHECK(CA % 8 == 0 && Ncols % 8 == 0 && ldc % 8 == 0 && c_off % 8 == 0, "conv_gemm: channel counts must be multiples of 8");
   TORCH_CHECK((int)dh.size() <= CONV_MAX_TAPS && dh.size() == dw.size() && dh.size() == tb.size(), "bad taps");
@@ -127,6 +135,16 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
   p.stages = stages;
   TORCH_CHECK(tile_n == 0 || tile_n == 64 || tile_n == 128, "conv_gemm: tile_n must be 0, 64 or 128");
   p.tile_n = tile_n;
+  if (fp8) {
+    TORCH_CHECK(b_sc.has_value() && b_sc->defined() && a_sc->scalar_type() == at::kByte &&
+                    b_sc->scalar_type() == at::kByte,
+                "conv_gemm: fp8 needs uint8 E8M0 scales for both operands");
+    TORCH_CHECK(CA % 128 == 0 && K % 128 == 0, "conv_gemm: fp8 path needs CA % 128 == 0");
+    TORCH_CHECK(a_sc->numel() * 32 >= A.numel() && b_sc->numel() * 32 >= B.numel(), "conv_gemm: scale sizes");
+    TORCH_CHECK(!p.bwd_y && !p.addend, "conv_gemm: fp8 is forward-only");
+    p.a_sc = a_sc->data_ptr<uint8_t>();
+    p.b_sc = b_sc->data_ptr<uint8_t>();
+  }
   if (p.bwd_y) {
     TORCH_CHECK(bwd_y->numel() == C.numel() && p.bwd_coef && p.bwd_part && c_off == 0,
                 "conv_gemm: fused BN-backward needs y matching C, coefficients and a partial buffer");
@@ -194,11 +212,21 @@ void bn_eval_coef(OT gamma, OT beta, Tensor rmean, Tensor rvar, double eps, int 
         "bn_eval_coef");
 }
 
-void bn_apply(Tensor y, Tensor coef, OT res, Tensor out, long rows, int C, int ldo, int c_off, int act) {
+void bn_apply(Tensor y, Tensor coef, OT res, Tensor out, long rows, int C, int ldo, int c_off, int act, OT q,
+              OT qs) {
   req(y, BF, "y"); req(out, BF, "out"); req(coef, F32, "coef");
   TORCH_CHECK(C % 8 == 0, "bn_apply: C % 8");
+  uint8_t* qp = nullptr;
+  uint8_t* qsp = nullptr;
+  if (q.has_value() && q->defined()) {  // + MX-FP8 copy of the output
+    TORCH_CHECK(q->scalar_type() == at::kFloat8_e4m3fn && qs.has_value() && qs->scalar_type() == at::kByte &&
+                    q->numel() == rows * C && qs->numel() == rows * C / 32 && C % 32 == 0 && ldo == C && c_off == 0,
+                "bn_apply: MX output needs fp8 [rows*C], uint8 [rows*C/32], a dense output and C % 32 == 0");
+    qp = (uint8_t*)q->data_ptr();
+    qsp = qs->data_ptr<uint8_t>();
+  }
   check(bn_apply_launch(ptr<bf16_t>(y), ptr<float>(coef), optr<bf16_t>(res), ptr<bf16_t>(out), rows, C, ldo, c_off,
-                        act, cur()),
+                        act, qp, qsp, cur()),
         "bn_apply");
 }
 
@@ -307,6 +335,20 @@ void cast_bf16(Tensor x, Tensor y) {
 
 void weight_pad(Tensor w, Tensor o, long rows, int Ci, int Cp) {
   check(weight_pad_launch(ptr<bf16_t>(w), ptr<bf16_t>(o), rows, Ci, Cp, cur()), "weight_pad");
+}
+
+void mx_quant_act(Tensor x, Tensor q, Tensor sc, long rows, int C) {
+  req(x, BF, "x");
+  TORCH_CHECK(q.scalar_type() == at::kFloat8_e4m3fn && sc.scalar_type() == at::kByte, "mx_quant_act: q fp8, sc uint8");
+  TORCH_CHECK(C % 32 == 0 && x.numel() == rows * C && q.numel() == rows * C && sc.numel() == rows * C / 32,
+              "mx_quant_act: shapes");
+  check(mx_quant_act_launch(ptr<bf16_t>(x), (uint8_t*)q.data_ptr(), sc.data_ptr<uint8_t>(), rows, C, cur()),
+        "mx_quant_act");
+}
+
+void mx_quant_w(Tensor jobs, Tensor tiles, int ntiles) {
+  TORCH_CHECK(jobs.is_cuda() && tiles.is_cuda() && tiles.numel() >= (int64_t)ntiles * 2, "mx_quant_w: bad tables");
+  check(mx_quant_w_launch(jobs.data_ptr(), tiles.data_ptr(), ntiles, cur()), "mx_quant_w");
 }
 
 void weight_t_tiles(Tensor jobs, Tensor tiles, int ntiles) {
@@ -421,7 +463,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_reduce_finalize", &bn_reduce_finalize);
   m.def("bn_reduce_bwd", &bn_reduce_bwd);
   m.def("bn_eval_coef", &bn_eval_coef);
-  m.def("bn_apply", &bn_apply);
+  m.def("bn_apply", &bn_apply, pybind11::arg("y"), pybind11::arg("coef"), pybind11::arg("res"), pybind11::arg("out"),
+        pybind11::arg("rows"), pybind11::arg("C"), pybind11::arg("ldo"), pybind11::arg("c_off"), pybind11::arg("act"),
+        pybind11::arg("q") = pybind11::none(), pybind11::arg("qs") = pybind11::none());
   m.def("bn_bwd_reduce", &bn_bwd_reduce);
   m.def("bn_bwd_k", &bn_bwd_k);
   m.def("bn_bwd_elemt", &bn_bwd_elemt);
@@ -438,6 +482,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("adam", &adam);
   m.def("adam_tick", &adam_tick);
   m.def("weight_t_tiles", &weight_t_tiles);
+  m.def("mx_quant_act", &mx_quant_act);
+  m.def("mx_quant_w", &mx_quant_w);
+  m.def("mx_wjob_bytes", &mx_wjob_bytes);
   m.def("weight_t_job_bytes", &weight_t_job_bytes);
   m.def("prepare_input", &prepare_input);
   m.def("cast_bf16", &cast_bf16);

@@ -194,6 +194,51 @@ __global__ void bn_apply_kernel(const bf16_t* __restrict__ y, const float* __res
   }
 }
 
+// apply + MX-FP8 copy of the output for the fp8 forward convolution that consumes it (no separate
+// quantisation pass): the 4 lanes of a 32-channel block are consecutive lanes (C % 32 == 0), the
+// grid stride is a multiple of 4, so the block max is two xor-shuffles away.
+__global__ void bn_apply_mx_kernel(const bf16_t* __restrict__ y, const float* __restrict__ coef,
+                                   const bf16_t* __restrict__ res, bf16_t* __restrict__ out, uint8_t* __restrict__ q,
+                                   uint8_t* __restrict__ qs, long rows, int C, int act) {
+  const int cch = C >> 3;
+  const long total = rows * cch;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i - (threadIdx.x & 3) < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const bool live = i < total;
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const long row = i / cch;
+    const int c0 = (int)(i - row * cch) * 8;
+    if (live) {
+      float sc[8], sh[8], r[8];
+      unpack8(*(const uint4*)(y + row * C + c0), v);
+      *(float4*)sc = *(const float4*)(coef + c0);
+      *(float4*)(sc + 4) = *(const float4*)(coef + c0 + 4);
+      *(float4*)sh = *(const float4*)(coef + C + c0);
+      *(float4*)(sh + 4) = *(const float4*)(coef + C + c0 + 4);
+      if (res) unpack8(*(const uint4*)(res + row * C + c0), r);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float z = v[k] * sc[k] + sh[k];
+        if (res) z += r[k];
+        v[k] = apply_act(z, act);
+      }
+      const uint4 o = pack8(v);
+      *(uint4*)(out + row * C + c0) = o;
+      unpack8(o, v);  // quantise the bf16 value the backward pass will see
+    }
+    float amax = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) amax = fmaxf(amax, fabsf(v[k]));
+    amax = fmaxf(amax, __shfl_xor(amax, 1));
+    amax = fmaxf(amax, __shfl_xor(amax, 2));
+    const int e = mx_exponent(amax);
+    if (live) {
+      *(uint2*)(q + i * 8) = to_fp8x8(v, ldexpf(1.f, -e));
+      if ((i & 3) == 0) qs[i >> 2] = (uint8_t)(e + 127);
+    }
+  }
+}
+
 // ---- backward reduce -------------------------------------------------------
 // grid: (row blocks, channel-chunk slices); block 256 = CHB chunk lanes x RP row lanes
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
@@ -405,8 +450,15 @@ int bn_eval_coef_launch(const float* gamma, const float* beta, const float* rmea
 }
 
 int bn_apply_launch(const bf16_t* y, const float* coef, const bf16_t* res, bf16_t* out, long rows, int C,
-                    int ldo, int c_off, int act, hipStream_t s) {
+                    int ldo, int c_off, int act, uint8_t* q, uint8_t* qs, hipStream_t s) {
   const long work = rows * (C / 8);
+  if (q) {
+    if (C % 32 || ldo != C || c_off) return 2;
+    hipLaunchKernelGGL(bn_apply_mx_kernel, dim3(grid_for(work, 256, 8192)), dim3(256), 0, s, y, coef, res, out, q,
+                       qs, rows, C, act);
+    HIP_CHECK_LAUNCH();
+    return 0;
+  }
   hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(work, 256, 8192)), dim3(256), 0, s, y, coef, res, out,
                      rows, C, ldo, c_off, act);
   HIP_CHECK_LAUNCH();

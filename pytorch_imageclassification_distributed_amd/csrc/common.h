@@ -160,3 +160,28 @@ inline int spatial_reduce_launch(const bf16_t* a, const bf16_t* b, float* out, i
                      scale, splits > 1 ? 1 : 0);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
+
+// ---- MX-FP8 element/scale helpers (OCP e4m3fn, E8M0 per 32 channels; mxfp8.hip) ----
+constexpr float E4M3_MAX = 448.f;
+
+// E8M0 exponent byte for a block with maximum |x| = amax: smallest e with amax * 2^-e <= 448.
+DEVI int mx_exponent(float amax) {
+  if (!(amax > 0.f)) return 0;  // all-zero (or NaN) block: scale 2^0
+  int ex;
+  const float m = frexpf(amax / E4M3_MAX, &ex);  // amax/448 = m * 2^ex, m in [0.5, 1)
+  int e = (m > 0.5f) ? ex : ex - 1;               // ceil(log2(amax / 448))
+  return e < -127 ? -127 : (e > 127 ? 127 : e);
+}
+
+// 8 floats -> 8 e4m3 bytes (two dwords), x scaled by 2^-e; clamped so rounding cannot overflow
+DEVI uint2 to_fp8x8(const float* v, float inv) {
+  float s[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s[k] = fminf(fmaxf(v[k] * inv, -E4M3_MAX), E4M3_MAX);
+  int lo = __builtin_amdgcn_cvt_pk_fp8_f32(s[0], s[1], 0, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(s[2], s[3], lo, true);
+  int hi = __builtin_amdgcn_cvt_pk_fp8_f32(s[4], s[5], 0, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(s[6], s[7], hi, true);
+  return make_uint2((unsigned)lo, (unsigned)hi);
+}
+

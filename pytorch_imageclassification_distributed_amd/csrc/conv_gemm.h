@@ -42,6 +42,10 @@ struct ConvParams {
   float* bwd_part;
   int bwd_act, bwd_groups;
   int stages;  // LDS-DMA ring depth: 1 (high occupancy) or 2; 0 = k-step heuristic
+  // MX-FP8 forward (A, B are e4m3 bytes; CA % 128 == 0): E8M0 scales, one per 32 channels -
+  // a_sc [IH*IW*N pixels][CA/32], b_sc [Ncols][K/32].  Null = bf16 operands.
+  const uint8_t* a_sc;
+  const uint8_t* b_sc;
   int tile_n;  // output-channel tile: 64 or 128; 0 = 64 iff Ncols <= 64
   int tap_dh[CONV_MAX_TAPS];
   int tap_dw[CONV_MAX_TAPS];

@@ -483,6 +483,189 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? (BN == 128 ? 3 : 4) : 1) void con
 }
 
 // ---------------------------------------------------------------------------
+// forward, MX-FP8 operands (BASELINE config 5): v_mfma_scale_f32_16x16x128_f8f6f4 runs twice the
+// bf16 rate and applies the per-32-channel E8M0 block scales itself.  A k-step is 128 channels =
+// 128 bytes per row, i.e. the SAME LDS image geometry (128-B rows, 8 swizzled 16-B chunks) as the
+// bf16 kernel's 64-channel step, filled by the same LDS-DMA gather; each row's 4 scale bytes ride
+// along in a 4-B LDS-DMA per row (waves 0-1: activation rows, waves 2-3: weight rows).
+// Operand k order (scripts/probes/fp8_mfma_scales_map.hip): lane group g = lane>>4 feeds chunks g
+// and g+4 of its row and the scale of channels [32g, 32g+32).  Requires CA % 128 == 0 (a k-step
+// never straddles a tap), Ncols % 8 == 0.  Epilogue identical to the bf16 kernels (BN stats, ...).
+// ---------------------------------------------------------------------------
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+DEVI void glds4(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 4, 0, 0);
+}
+
+template <int BN, int STAGES>
+__global__ __launch_bounds__(NT, STAGES == 1 ? (BN == 128 ? 3 : 4) : 1) void conv_fp8_kernel(const ConvParams p) {
+  constexpr int A_BYTES = BM * 128;
+  constexpr int B_BYTES = BN * 128;
+  constexpr int S_BYTES = 2 * 128 * 4;  // activation + weight scale rows (128 rows each, 4 B per row)
+  constexpr int STAGE = A_BYTES + B_BYTES + S_BYTES;
+  constexpr int WTM = BM / 2, WTN = BN / 2;
+  constexpr int RM = WTM / 16, RN = WTN / 16;
+  constexpr int AL = BM / 32, BL = BN / 32;
+  constexpr int LPS = AL + BL + 1;  // LDS-DMA instructions per wave per stage
+  constexpr int TAP_BYTES = 3 * CONV_MAX_TAPS * 4;
+  constexpr int CST = BN + 8;
+  constexpr int MAIN = STAGES * STAGE > BM * CST * 2 ? STAGES * STAGE : BM * CST * 2;
+  __shared__ __attribute__((aligned(16))) char smem[MAIN + TAP_BYTES];
+  int* s_dh = (int*)(smem + MAIN);
+  int* s_dw = s_dh + CONV_MAX_TAPS;
+  int* s_tb = s_dw + CONV_MAX_TAPS;
+  const uint8_t* A8 = (const uint8_t*)p.A;
+  const uint8_t* B8 = (const uint8_t*)p.B;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int gm = (p.M + BM - 1) / BM, gn = (p.Ncols + BN - 1) / BN;
+  const int lin = xcd_remap(blockIdx.x, gm * gn);
+  const int bm = lin / gn, bn = lin - bm * gn;
+  const int m0 = bm * BM, n0 = bn * BN;
+  if (tid < p.ntaps) {
+    s_dh[tid] = p.tap_dh[tid];
+    s_dw[tid] = p.tap_dw[tid];
+    s_tb[tid] = p.tap_b[tid];
+  }
+  const int lrow = lane >> 3, pch = lane & 7;
+  const int ghw = p.GH * p.GW;
+  const int csb = p.CA >> 5;  // scale bytes per pixel
+  int a_base[AL], a_ih[AL], a_iw[AL], a_ch[AL];
+#pragma unroll
+  for (int i = 0; i < AL; ++i) {
+    const int row = wid * (BM / 4) + i * 8 + lrow;
+    a_ch[i] = pch ^ ((row >> 1) & 7);
+    const int m = m0 + row;
+    if (m < p.M) {
+      const int n = m / ghw, r = m - n * ghw;
+      const int gh = r / p.GW, gw = r - gh * p.GW;
+      a_base[i] = n * p.IH * p.IW;  // pixel index base (bytes = pixel * CA)
+      a_ih[i] = gh * p.sA;
+      a_iw[i] = gw * p.sA;
+    } else {
+      a_base[i] = 0;
+      a_ih[i] = -(1 << 28);
+      a_iw[i] = 0;
+    }
+  }
+  int b_off[BL], b_ch[BL];
+#pragma unroll
+  for (int i = 0; i < BL; ++i) {
+    const int row = wid * (BN / 4) + i * 8 + lrow;
+    b_ch[i] = pch ^ ((row >> 1) & 7);
+    const int n = n0 + row;
+    b_off[i] = n < p.Ncols ? n * p.ldb : -1;
+  }
+  // scale rows: waves 0-1 -> activation rows wid*64 + lane, waves 2-3 -> weight rows (wid-2)*64 + lane
+  const bool s_act = wid < 2;
+  const int srow = (wid & 1) * 64 + lane;
+  int s_base = 0, s_ih = -(1 << 28), s_iw = 0, s_woff = -1;
+  if (s_act) {
+    const int m = m0 + srow;
+    if (m < p.M) {
+      const int n = m / ghw, r = m - n * ghw;
+      const int gh = r / p.GW, gw = r - gh * p.GW;
+      s_base = n * p.IH * p.IW;
+      s_ih = gh * p.sA;
+      s_iw = gw * p.sA;
+    }
+  } else if (srow < BN && n0 + srow < p.Ncols) {
+    s_woff = (n0 + srow) * (p.ldb >> 5);
+  }
+  __syncthreads();
+
+  auto issue = [&](int kt, int buf) {
+    char* sa = smem + buf * STAGE;
+    char* sb = sa + A_BYTES;
+    char* ss = sb + B_BYTES;
+    const int k0 = kt * 128;
+    const int tap = k0 / p.CA, ci0 = k0 - tap * p.CA;
+    const int dh = s_dh[tap], dw = s_dw[tap], tb = s_tb[tap];
+    const uint8_t* srca[AL];
+    const uint8_t* srcb[BL];
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      const int ih = a_ih[i] + dh, iw = a_iw[i] + dw;
+      const bool ok = (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+      srca[i] = ok ? A8 + (long)(a_base[i] + ih * p.IW + iw) * p.CA + ci0 + a_ch[i] * 16 : (const uint8_t*)p.zero;
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i)
+      srcb[i] = b_off[i] >= 0 ? B8 + b_off[i] + tb * p.CA + ci0 + b_ch[i] * 16 : (const uint8_t*)p.zero;
+    const uint8_t* srcs;
+    if (s_act) {
+      const int ih = s_ih + dh, iw = s_iw + dw;
+      const bool ok = (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+      srcs = ok ? p.a_sc + (long)(s_base + ih * p.IW + iw) * csb + (ci0 >> 5) : (const uint8_t*)p.zero;
+    } else {
+      srcs = s_woff >= 0 ? p.b_sc + s_woff + (k0 >> 5) : (const uint8_t*)p.zero;
+    }
+#pragma unroll
+    for (int i = 0; i < AL; ++i) glds16(srca[i], sa + (wid * (BM / 4) + i * 8) * 128);
+#pragma unroll
+    for (int i = 0; i < BL; ++i) glds16(srcb[i], sb + (wid * (BN / 4) + i * 8) * 128);
+    glds4(srcs, ss + wid * 256);  // [0,512): activation rows x 4 B; [512,1024): weight rows x 4 B
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = p.K / 128;
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) issue(s, s);
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    if constexpr (STAGES == 1) {
+      if (kt > 0) __builtin_amdgcn_s_barrier();
+      issue(kt, 0);
+      wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+    } else {
+      if (kt + STAGES - 2 < nk) wait_vmcnt<(STAGES - 2) * LPS>();
+      else wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+    }
+    const char* sa = smem + (kt % STAGES) * STAGE;
+    const char* sb = sa + A_BYTES;
+    const unsigned char* ss = (const unsigned char*)(sb + B_BYTES);
+    i32x8 xa[RM], wb[RN];
+    int sx[RM], sw[RN];
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+      const int row = wm * WTM + i * 16 + fr;
+      const int4 lo = *(const int4*)(sa + swz(row, fq));
+      const int4 hi = *(const int4*)(sa + swz(row, fq + 4));
+      xa[i] = (i32x8){lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      sx[i] = ss[row * 4 + fq];
+    }
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      const int row = wn * WTN + j * 16 + fr;
+      const int4 lo = *(const int4*)(sb + swz(row, fq));
+      const int4 hi = *(const int4*)(sb + swz(row, fq + 4));
+      wb[j] = (i32x8){lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      sw[j] = ss[512 + row * 4 + fq];
+    }
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wb[j], xa[i], acc[i][j], 0, 0, 0, sw[j], 0,
+                                                                     sx[i]);
+  }
+  __syncthreads();
+  conv_epilogue<BN>(p, acc, smem, tid, lane, wid, wm, wn, m0, n0, bm, ghw);
+}
+
+// ---------------------------------------------------------------------------
 // weight gradient
 // ---------------------------------------------------------------------------
 constexpr int WBN = 128;      // columns (tap*Cin) per tile
@@ -826,9 +1009,23 @@ static void launch_bn(const ConvParams& p, int gm, hipStream_t stream) {
   }
 }
 
+template <int BN>
+static void launch_fp8(const ConvParams& p, int gm, hipStream_t stream) {
+  const int gn = cdiv(p.Ncols, BN);
+  if (p.stages == 2) hipLaunchKernelGGL((conv_fp8_kernel<BN, 2>), dim3(gm * gn), dim3(NT), 0, stream, p);
+  else hipLaunchKernelGGL((conv_fp8_kernel<BN, 1>), dim3(gm * gn), dim3(NT), 0, stream, p);
+}
+
 int conv_gemm_launch(const ConvParams& p, hipStream_t stream) {
   if (p.M <= 0 || p.Ncols <= 0) return 0;
   const int gm = cdiv(p.M, BM);
+  if (p.a_sc) {
+    if (p.CA % 128 || p.K % 128 || !p.b_sc) return 3;
+    if (p.Ncols <= 64 || p.tile_n == 64) launch_fp8<64>(p, gm, stream);
+    else launch_fp8<128>(p, gm, stream);
+    HIP_CHECK_LAUNCH();
+    return 0;
+  }
   if (p.Ncols <= 64 || p.tile_n == 64) launch_bn<64>(p, gm, stream);
   else launch_bn<128>(p, gm, stream);
   HIP_CHECK_LAUNCH();

@@ -57,6 +57,9 @@ class Trainer:
         if args.compute != "auto":
             Fx.set_backend(args.compute)
         self.hip = self.dev.type == "cuda" and Fx.get_backend() != "torch"
+        if self.hip:
+            from ..ops import hip as _hipmod
+            _hipmod.set_fp8(getattr(args, "dtype", "bf16") == "fp8")
         if getattr(args, "deterministic", False):
             torch.backends.cudnn.deterministic = True
             torch.backends.cudnn.benchmark = False

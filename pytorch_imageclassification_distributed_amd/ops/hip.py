@@ -100,7 +100,8 @@ def ws(dev) -> _Workspace:
 class _Shadow:
     # t: bf16 KRSC copy; tt: bf16 [Ci][T][Co] copy for dgrad (lazily, conv weights only).
     # stamp counts re-casts of t; tt is current when tt_stamp == stamp or the optimizer maintains it.
-    __slots__ = ("t", "ptr", "version", "fused", "ref", "stamp", "tt", "tgeom", "tt_stamp", "tfused")
+    __slots__ = ("t", "ptr", "version", "fused", "ref", "stamp", "tt", "tgeom", "tt_stamp", "tfused",
+                 "mq", "ms", "m_stamp", "mfused")
 
 
 _SHADOWS: dict = {}
@@ -129,6 +130,7 @@ def weight_bf16(p: torch.Tensor) -> torch.Tensor:
         e.fused = False
         e.ref = weakref.ref(p)
         e.stamp, e.tt, e.tgeom, e.tt_stamp, e.tfused = 0, None, None, -1, False
+        e.mq, e.ms, e.m_stamp, e.mfused = None, None, -1, False
         _SHADOWS[key] = e
         _SHADOW_GEN[0] += 1
     src = p.detach()
@@ -167,6 +169,74 @@ def shadow_for_optimizer(p: torch.Tensor):
         return None
     e.fused = True
     return e.t
+
+
+# ---------------------------------------------------------------------------
+# MX-FP8 (forward convolutions, --dtype fp8)
+# ---------------------------------------------------------------------------
+FP8_FWD = os.environ.get("IMGCLS_FP8", "0") == "1"
+FP8 = torch.float8_e4m3fn
+_MXW_DT = np.dtype([("w", "<u8"), ("q", "<u8"), ("s", "<u8"), ("n", "<i8")])
+
+
+def set_fp8(flag: bool = True) -> None:
+    """MX-FP8 forward convolutions (e4m3 elements, E8M0 scale per 32 channels) wherever the input
+    channel count is a multiple of 128; everything else (stem, 64-channel layers, backward) stays bf16."""
+    global FP8_FWD
+    FP8_FWD = bool(flag)
+
+
+def _mx_tiles(jobs):
+    return [(j, t) for j, (_w, _q, _s, n) in enumerate(jobs) for t in range(-(-n // 2048))]
+
+
+def _mx_quant_weights(jobs, dev):
+    arr = np.array(jobs, dtype=_MXW_DT)
+    tiles = _mx_tiles(jobs)
+    C.mx_quant_w(_upload(arr.view(np.uint8).copy(), dev), _upload(np.asarray(tiles, dtype=np.int32).reshape(-1), dev),
+                 len(tiles))
+
+
+def weight_mx(p: torch.Tensor):
+    """(fp8 [Co*K], E8M0 [Co*K/32]) MX copy of a KRSC conv weight, quantised from the fp32 master.
+    Kept current by the fused optimizer (one batched launch after Adam) once registered."""
+    weight_bf16(p)  # creates / refreshes the shadow entry (version tracking lives there)
+    e = _SHADOWS[id(p)]
+    if e.mq is not None and (e.mfused or e.m_stamp == e.stamp):
+        return e.mq, e.ms
+    if e.mq is None:
+        if C.mx_wjob_bytes() != _MXW_DT.itemsize:
+            raise RuntimeError("mx_quant_w: job record layout mismatch between Python and the kernel")
+        e.mq = torch.empty(p.numel(), dtype=FP8, device=p.device)
+        e.ms = torch.empty(p.numel() // 32, dtype=torch.uint8, device=p.device)
+        e.mfused = False
+        _SHADOW_GEN[0] += 1
+    _mx_quant_weights([(p.data_ptr(), e.mq.data_ptr(), e.ms.data_ptr(), p.numel())], p.device)
+    e.m_stamp = e.stamp
+    return e.mq, e.ms
+
+
+def shadow_mx_for_optimizer(p: torch.Tensor):
+    e = _SHADOWS.get(id(p))
+    if e is None or e.ref() is not p or e.mq is None or not _krsc_compatible(p):
+        return None
+    e.mfused = True
+    return e.mq, e.ms
+
+
+def act_mx(x: torch.Tensor):
+    """MX-FP8 copy (fp8 [N*H*W*C], E8M0 [N*H*W*C/32]) of an NHWC bf16 activation, cached on the tensor
+    so the several convolutions reading one activation quantise it once."""
+    mx = getattr(x, "_imgcls_mx", None)
+    if mx is not None and mx[2] == x._version:
+        return mx[0], mx[1]
+    n = x.numel()
+    c = x.shape[1]
+    q = torch.empty(n, dtype=FP8, device=x.device)
+    sc = torch.empty(n // 32, dtype=torch.uint8, device=x.device)
+    C.mx_quant_act(x, q, sc, n // c, c)
+    x._imgcls_mx = (q, sc, x._version)
+    return q, sc
 
 
 def shadow_t_for_optimizer(p: torch.Tensor):
@@ -296,7 +366,7 @@ _STAGES_TUNED: dict = {}
 
 
 def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(None, None, None, None, 0, 1),
-               groups=G_STATS):
+               groups=G_STATS, scales=(None, None)):
     """One implicit-GEMM launch.  The kernel configuration - LDS-DMA ring depth (1 = high occupancy,
     2 = pipelined) x output-channel tile (64 / 128: more tiles balance 256 CUs better on small
     layers) - is chosen once per GEMM geometry by timing the candidates on scratch outputs (a
@@ -305,17 +375,17 @@ def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(
         cfg = (int(CONV_STAGES), 0)
     else:
         key = (tuple(geo), out.shape[1], tuple(dh), tuple(dw), stats is not None, bias is not None,
-               addend is not None, bwd[0] is not None, bwd[1] is not None, bwd[4])
+               addend is not None, bwd[0] is not None, bwd[1] is not None, bwd[4], scales[0] is not None)
         cfg = _STAGES_TUNED.get(key)
         if cfg is None:
             cfg = (0, 0) if torch.cuda.is_current_stream_capturing() else _tune_conv(
-                A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups)
+                A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups, scales)
             if cfg[0]:
                 _STAGES_TUNED[key] = cfg
-    C.conv_gemm(A, B, out, stats, bias, *geo, dh, dw, tb, groups, zero, addend, *bwd, *cfg)
+    C.conv_gemm(A, B, out, stats, bias, *geo, dh, dw, tb, groups, zero, addend, *bwd, *cfg, *scales)
 
 
-def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups):
+def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups, scales=(None, None)):
     scratch = torch.empty_like(out)
     sst = torch.zeros_like(stats) if stats is not None else None
     bwd = tuple(bwd)
@@ -326,12 +396,18 @@ def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, group
     times = {}
     for cfg in cands:
         times[cfg] = _time_ms(lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, groups, zero,
-                                                  addend, *bwd, *cfg))
+                                                  addend, *bwd, *cfg, *scales))
     return min(times, key=times.get)
+
+
+def fp8_eligible(g: "ConvGeom") -> bool:
+    return FP8_FWD and g.Cx == g.Ci and g.Cx % 128 == 0 and g.Co % 8 == 0
 
 
 def conv_forward_raw(x, w_param, g: ConvGeom, stats=None, bias=None, out=None, c_off=0):
     dev = x.device
+    if fp8_eligible(g):
+        return _conv_forward_fp8(x, w_param, g, stats, bias, out, c_off)
     wb = _weight_for_input(w_param, g.Cx)
     y = out if out is not None else _empty_cl(g.N, g.Co, g.OH, g.OW, dev)
     ldc = y.shape[1]
@@ -341,6 +417,19 @@ def conv_forward_raw(x, w_param, g: ConvGeom, stats=None, bias=None, out=None, c
     geo = (g.N * g.OH * g.OW, g.Co, g.T * g.Cx, g.Cx, g.OH, g.OW, g.H, g.W, g.sh, g.T * g.Cx, g.OH, g.OW,
            1, 0, 0, ldc, c_off)
     _conv_gemm(x, wb, y, stats, bias, geo, dh, dw, tb, ws(dev).zero, groups=stat_groups(geo[0]))
+    return y
+
+
+def _conv_forward_fp8(x, w_param, g: ConvGeom, stats, bias, out, c_off):
+    dev = x.device
+    xq, xs = act_mx(x)
+    wq, wsc = weight_mx(w_param)
+    y = out if out is not None else _empty_cl(g.N, g.Co, g.OH, g.OW, dev)
+    dh, dw, tb = _fwd_taps(g)
+    geo = (g.N * g.OH * g.OW, g.Co, g.T * g.Cx, g.Cx, g.OH, g.OW, g.H, g.W, g.sh, g.T * g.Cx, g.OH, g.OW,
+           1, 0, 0, y.shape[1], c_off)
+    _conv_gemm(xq, wq, y, stats, bias, geo, dh, dw, tb, ws(dev).zero, groups=stat_groups(geo[0]),
+               scales=(xs, wsc))
     return y
 
 
@@ -577,7 +666,13 @@ class BNActFn(torch.autograd.Function):
                 raise RuntimeError("eval-mode BN received fused statistics")
             C.bn_eval_coef(gamma, beta, bn.running_mean, bn.running_var, bn.eps, c, coef)
         out = _empty_cl(n, c, h, w, dev)
-        C.bn_apply(y, coef, res, out, rows, c, c, 0, a)
+        if FP8_FWD and c % 128 == 0:  # the consuming conv reads an MX-FP8 copy: produce it here
+            q = torch.empty(rows * c, dtype=FP8, device=dev)
+            qs = torch.empty(rows * c // 32, dtype=torch.uint8, device=dev)
+            C.bn_apply(y, coef, res, out, rows, c, c, 0, a, q, qs)
+            out._imgcls_mx = (q, qs, out._version)
+        else:
+            C.bn_apply(y, coef, res, out, rows, c, c, 0, a)
         ctx.act, ctx.group, ctx.rows, ctx.c = a, group, rows, c
         ctx.training = bn.training
         ctx.count_t = count_t
@@ -1099,6 +1194,7 @@ def adam_build_table(opt, items):
         raise RuntimeError("weight_t_tiles: job record layout mismatch between Python and the kernel")
     groups = {}
     wt_jobs = []
+    mx_jobs = []
     for gi, group, p in items:
         groups.setdefault(gi, (group, []))[1].append(p)
     tables = []
@@ -1113,6 +1209,9 @@ def adam_build_table(opt, items):
             stt = shadow_t_for_optimizer(p) if sh is not None else None
             if stt is not None:
                 wt_jobs.append((sh.data_ptr(), stt[0].data_ptr()) + tuple(stt[1:]) + (0,))
+            smx = shadow_mx_for_optimizer(p) if sh is not None else None
+            if smx is not None:
+                mx_jobs.append((p.data_ptr(), smx[0].data_ptr(), smx[1].data_ptr(), p.numel()))
             for ck in range(-(-p.numel() // _ADAM_CHUNK)):
                 chunks.append((t, ck))
             if not _same_memory_order(p, p.grad):
@@ -1133,11 +1232,17 @@ def adam_build_table(opt, items):
                  for t in range(taps) for co0 in range(0, co, 64) for ci0 in range(0, ci, 64)]
         wt = (_upload(jobs.view(np.uint8).copy(), tables[0][1].device),
               _upload(np.asarray(tiles, dtype=np.int32).reshape(-1), tables[0][1].device), len(tiles))
-    return (tables, shadow_generation(), wt)
+    mx = None
+    if mx_jobs:
+        dev0 = tables[0][1].device
+        tiles = _mx_tiles(mx_jobs)
+        mx = (_upload(np.array(mx_jobs, dtype=_MXW_DT).view(np.uint8).copy(), dev0),
+              _upload(np.asarray(tiles, dtype=np.int32).reshape(-1), dev0), len(tiles))
+    return (tables, shadow_generation(), wt, mx)
 
 
 def adam_step(opt, items, table, grad_scale):
-    tables, gen, wt = table
+    tables, gen, wt, mx = table
     if gen != shadow_generation():
         opt._table_key = None  # rebuild next step so new shadows are kept fresh
     for gi, tab, ck, nck, lr_step, ps in tables:
@@ -1147,4 +1252,6 @@ def adam_step(opt, items, table, grad_scale):
         C.adam(tab, ck, nck, lr_step, b1, b2, group["eps"], group["weight_decay"], float(grad_scale), _ADAM_CHUNK)
     if wt is not None:  # refresh every transposed dgrad shadow from the updated KRSC shadows: one launch
         C.weight_t_tiles(*wt)
+    if mx is not None:  # and every MX-FP8 forward copy from the updated fp32 masters: one launch
+        C.mx_quant_w(*mx)
     opt._host_steps = getattr(opt, "_host_steps", 0) + 1
