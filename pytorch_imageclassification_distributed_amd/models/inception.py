@@ -28,8 +28,10 @@ class BasicConv2d(nn.Module):
         self.conv = nn.Conv2d(cin, cout, bias=False, **kw)
         self.bn = nn.BatchNorm2d(cout, eps=0.001)
 
-    def forward(self, x):
-        return Fx.conv_bn_act(x, self.conv, self.bn, "relu")
+    def forward(self, x, exclusive=False, slot=None):
+        """``exclusive``: this conv is the only consumer of ``x`` (a chain-internal conv), which lets its
+        dgrad epilogue run the producer's BN-backward reduce; ``slot``: x feeds exactly two convs."""
+        return Fx.conv_bn_act(x, self.conv, self.bn, "relu", x_slot=slot, exclusive_input=exclusive)
 
 
 class InceptionA(nn.Module):
@@ -44,10 +46,11 @@ class InceptionA(nn.Module):
         self.branch_pool = BasicConv2d(cin, pool_features, kernel_size=1)
 
     def forward(self, x):
-        b1 = self.branch1x1(x)
-        b5 = self.branch5x5_2(self.branch5x5_1(x))
-        b3 = self.branch3x3dbl_3(self.branch3x3dbl_2(self.branch3x3dbl_1(x)))
-        bp = self.branch_pool(Fx.avg_pool2d(x, 3, 1, 1))
+        s = Fx.grad_slot(x, 4)  # x feeds three convs and the pool: summed inside their backward kernels
+        b1 = self.branch1x1(x, slot=s)
+        b5 = self.branch5x5_2(self.branch5x5_1(x, slot=s), True)
+        b3 = self.branch3x3dbl_3(self.branch3x3dbl_2(self.branch3x3dbl_1(x, slot=s), True), True)
+        bp = self.branch_pool(Fx.avg_pool2d(x, 3, 1, 1, slot=s))
         return Fx.cat_channels([b1, b5, b3, bp])
 
 
@@ -60,9 +63,10 @@ class InceptionB(nn.Module):
         self.branch3x3dbl_3 = BasicConv2d(96, 96, kernel_size=3, stride=2)
 
     def forward(self, x):
-        b3 = self.branch3x3(x)
-        bd = self.branch3x3dbl_3(self.branch3x3dbl_2(self.branch3x3dbl_1(x)))
-        bp = Fx.max_pool2d(x, 3, 2, 0)
+        s = Fx.grad_slot(x, 3)
+        b3 = self.branch3x3(x, slot=s)
+        bd = self.branch3x3dbl_3(self.branch3x3dbl_2(self.branch3x3dbl_1(x, slot=s), True), True)
+        bp = Fx.max_pool2d(x, 3, 2, 0, slot=s)
         return Fx.cat_channels([b3, bd, bp])
 
 
@@ -82,12 +86,13 @@ class InceptionC(nn.Module):
         self.branch_pool = BasicConv2d(cin, 192, kernel_size=1)
 
     def forward(self, x):
-        b1 = self.branch1x1(x)
-        b7 = self.branch7x7_3(self.branch7x7_2(self.branch7x7_1(x)))
-        bd = self.branch7x7dbl_1(x)
-        bd = self.branch7x7dbl_3(self.branch7x7dbl_2(bd))
-        bd = self.branch7x7dbl_5(self.branch7x7dbl_4(bd))
-        bp = self.branch_pool(Fx.avg_pool2d(x, 3, 1, 1))
+        s = Fx.grad_slot(x, 4)
+        b1 = self.branch1x1(x, slot=s)
+        b7 = self.branch7x7_3(self.branch7x7_2(self.branch7x7_1(x, slot=s), True), True)
+        bd = self.branch7x7dbl_1(x, slot=s)
+        bd = self.branch7x7dbl_3(self.branch7x7dbl_2(bd, True), True)
+        bd = self.branch7x7dbl_5(self.branch7x7dbl_4(bd, True), True)
+        bp = self.branch_pool(Fx.avg_pool2d(x, 3, 1, 1, slot=s))
         return Fx.cat_channels([b1, b7, bd, bp])
 
 
@@ -102,10 +107,11 @@ class InceptionD(nn.Module):
         self.branch7x7x3_4 = BasicConv2d(192, 192, kernel_size=3, stride=2)
 
     def forward(self, x):
-        b3 = self.branch3x3_2(self.branch3x3_1(x))
-        b7 = self.branch7x7x3_2(self.branch7x7x3_1(x))
-        b7 = self.branch7x7x3_4(self.branch7x7x3_3(b7))
-        bp = Fx.max_pool2d(x, 3, 2, 0)
+        s = Fx.grad_slot(x, 3)
+        b3 = self.branch3x3_2(self.branch3x3_1(x, slot=s), True)
+        b7 = self.branch7x7x3_2(self.branch7x7x3_1(x, slot=s), True)
+        b7 = self.branch7x7x3_4(self.branch7x7x3_3(b7, True), True)
+        bp = Fx.max_pool2d(x, 3, 2, 0, slot=s)
         return Fx.cat_channels([b3, b7, bp])
 
 
@@ -123,12 +129,15 @@ class InceptionE(nn.Module):
         self.branch_pool = BasicConv2d(cin, 192, kernel_size=1)
 
     def forward(self, x):
-        b1 = self.branch1x1(x)
-        b3 = self.branch3x3_1(x)
-        b3a, b3b = self.branch3x3_2a(b3), self.branch3x3_2b(b3)
-        bd = self.branch3x3dbl_2(self.branch3x3dbl_1(x))
-        bda, bdb = self.branch3x3dbl_3a(bd), self.branch3x3dbl_3b(bd)
-        bp = self.branch_pool(Fx.avg_pool2d(x, 3, 1, 1))
+        s = Fx.grad_slot(x, 4)
+        b1 = self.branch1x1(x, slot=s)
+        b3 = self.branch3x3_1(x, slot=s)
+        s3 = Fx.grad_slot(b3)  # b3 and bd each feed exactly two convs: paired gradient slots
+        b3a, b3b = self.branch3x3_2a(b3, slot=s3), self.branch3x3_2b(b3, slot=s3)
+        bd = self.branch3x3dbl_2(self.branch3x3dbl_1(x, slot=s), True)
+        sd = Fx.grad_slot(bd)
+        bda, bdb = self.branch3x3dbl_3a(bd, slot=sd), self.branch3x3dbl_3b(bd, slot=sd)
+        bp = self.branch_pool(Fx.avg_pool2d(x, 3, 1, 1, slot=s))
         return Fx.cat_channels([b1, b3a, b3b, bda, bdb, bp])
 
 
@@ -143,7 +152,7 @@ class InceptionAux(nn.Module):
 
     def forward(self, x):
         x = Fx.avg_pool2d(x, 5, 3, 0)
-        x = self.conv1(self.conv0(x))
+        x = self.conv1(self.conv0(x), True)
         x = Fx.global_avg_pool(x)
         return Fx.mlp(x, self.fc) if isinstance(self.fc, nn.Sequential) else Fx.linear(x, self.fc)
 
@@ -199,11 +208,11 @@ class Inception3(nn.Module):
     def forward(self, x):
         x = self._transform_input(x)
         x = self.Conv2d_1a_3x3(x)
-        x = self.Conv2d_2a_3x3(x)
-        x = self.Conv2d_2b_3x3(x)
+        x = self.Conv2d_2a_3x3(x, True)
+        x = self.Conv2d_2b_3x3(x, True)
         x = Fx.max_pool2d(x, 3, 2, 0)
         x = self.Conv2d_3b_1x1(x)
-        x = self.Conv2d_4a_3x3(x)
+        x = self.Conv2d_4a_3x3(x, True)
         x = Fx.max_pool2d(x, 3, 2, 0)
         x = self.Mixed_5b(x)
         x = self.Mixed_5c(x)

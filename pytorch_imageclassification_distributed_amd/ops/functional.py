@@ -103,10 +103,11 @@ def _torch_bn(x, bn):
 # ---------------------------------------------------------------------------
 # primitives
 # ---------------------------------------------------------------------------
-def grad_slot(x):
-    """A paired-gradient slot for a tensor with exactly two consumers (HIP path; None otherwise)."""
+def grad_slot(x, n: int = 2):
+    """A gradient slot for a tensor with exactly ``n`` consumers that each take ``slot=`` (HIP path;
+    None otherwise): their backward contributions are summed inside the consumers' own kernels."""
     if use_hip(x) and x.requires_grad and torch.is_grad_enabled():
-        return _hip().GradSlot()
+        return _hip().GradSlot(n)
     return None
 
 
@@ -132,16 +133,16 @@ def conv(x, conv_mod):
     return _torch_conv(x, conv_mod)
 
 
-def max_pool2d(x, kernel_size, stride, padding=0):
+def max_pool2d(x, kernel_size, stride, padding=0, slot=None):
     if use_hip(x):
-        return _hip().max_pool2d(x, kernel_size, stride, padding)
+        return _hip().max_pool2d(x, kernel_size, stride, padding, slot)
     return F.max_pool2d(x, kernel_size, stride, padding)
 
 
-def avg_pool2d(x, kernel_size, stride, padding=0):
+def avg_pool2d(x, kernel_size, stride, padding=0, slot=None):
     """count_include_pad=True semantics (torch default, used by torchvision Inception)."""
     if use_hip(x):
-        return _hip().avg_pool2d(x, kernel_size, stride, padding)
+        return _hip().avg_pool2d(x, kernel_size, stride, padding, slot)
     return F.avg_pool2d(x, kernel_size, stride, padding)
 
 

@@ -525,29 +525,37 @@ def conv_wgrad_raw(dy, x, w_param, g: ConvGeom):
 
 
 class GradSlot:
-    """Pairs the two backward contributions to one tensor's gradient (e.g. a ResNet block input
-    feeding conv1 and the identity / downsample branch).  The first consumer to run backward parks
-    its gradient here and reports none to autograd; the second adds the parked one - inside its
-    dgrad epilogue when it is a convolution - so autograd's separate accumulation pass disappears.
-    Order-independent; only valid when exactly two consumers share the slot."""
+    """Collects the backward contributions of the ``n`` consumers of one tensor (a ResNet block input
+    feeding conv1 and the identity / downsample branch: n=2; an Inception block input feeding three
+    convs and a pool: n=4).  Each consumer to run backward adds the running sum - inside its dgrad
+    epilogue when it is a convolution - and parks the result, reporting no gradient to autograd; the
+    consumer that completes the sum hands it over.  Autograd's separate accumulation passes disappear.
+    Order-independent; every one of the ``n`` consumers must deliver exactly once."""
 
-    __slots__ = ("t",)
+    __slots__ = ("t", "n", "seen")
 
-    def __init__(self):
+    def __init__(self, n: int = 2):
         self.t = None
+        self.n = n
+        self.seen = 0
+
+    def completes(self) -> bool:
+        """True when the next delivery is the last one (the producer's full gradient)."""
+        return self.seen == self.n - 1
 
     def deliver(self, grad, fused=False):
-        """Return what the consumer should hand to autograd."""
-        if self.t is None:
+        """Return what the consumer should hand to autograd.  ``fused``: ``grad`` already includes
+        the parked running sum (it was the consumer's dgrad addend)."""
+        self.seen += 1
+        if not fused and self.t is not None:
+            out = torch.empty_like(grad, memory_format=CL)
+            C.add(_cl(grad), _cl(self.t), out)
+            grad = out
+        if self.seen < self.n:
             self.t = grad
             return None
-        if fused:  # `grad` already contains the parked contribution
-            self.t = None
-            return grad
-        out = torch.empty_like(grad, memory_format=CL)
-        C.add(_cl(grad), _cl(self.t), out)
         self.t = None
-        return out
+        return grad
 
 
 class BwdLink:
@@ -585,18 +593,15 @@ class ConvFn(torch.autograd.Function):
             slot, link = ctx.slot, ctx.link
             if link is not None and link.done:
                 link = None
-            if slot is not None and slot.t is None:  # first of a pair: park the partial gradient
-                dx = slot.deliver(conv_dgrad_raw(dy, w, g))
-            elif slot is not None and g.Cx == g.Ci:  # second of a pair: fused accumulation (+ BN reduce)
-                dx = slot.deliver(conv_dgrad_raw(dy, w, g, addend=slot.t, link=link), fused=True)
-                if link is not None:
-                    link.done = True
-            else:
-                dx = conv_dgrad_raw(dy, w, g, link=link)
-                if link is not None:
-                    link.done = True
-                if slot is not None:
-                    dx = slot.deliver(dx)
+            if slot is not None and not slot.completes():
+                link = None  # the producer's BN reduce needs the full gradient
+            # running sum of the other consumers' contributions rides in as the dgrad addend
+            addend = slot.t if (slot is not None and g.Cx == g.Ci) else None
+            dx = conv_dgrad_raw(dy, w, g, addend=addend, link=link)
+            if link is not None:
+                link.done = True
+            if slot is not None:
+                dx = slot.deliver(dx, fused=addend is not None)
         dw = conv_wgrad_raw(dy, x, w, g) if ctx.needs_input_grad[1] else None
         return dx, dw, None, None, None, None
 
@@ -805,7 +810,7 @@ def _pool_args(k, s, p):
 
 class MaxPoolFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, k, s, p):
+    def forward(ctx, x, k, s, p, slot=None):
         n, c, h, w = x.shape
         oh = (h + 2 * p[0] - k[0]) // s[0] + 1
         ow = (w + 2 * p[1] - k[1]) // s[1] + 1
@@ -813,6 +818,7 @@ class MaxPoolFn(torch.autograd.Function):
         idx = torch.empty((n, oh, ow, c), dtype=torch.uint8, device=x.device)
         C.maxpool_fwd(x, y, idx, n, h, w, c, oh, ow, k[0], k[1], s[0], s[1], p[0], p[1])
         ctx.geo = (n, h, w, c, oh, ow, k, s, p)
+        ctx.slot = slot
         ctx.save_for_backward(idx)
         return y
 
@@ -822,23 +828,26 @@ class MaxPoolFn(torch.autograd.Function):
         n, h, w, c, oh, ow, k, s, p = ctx.geo
         dx = _empty_cl(n, c, h, w, dy.device)
         C.maxpool_bwd(_cl(dy), idx, dx, n, h, w, c, oh, ow, k[0], k[1], s[0], s[1], p[0], p[1])
-        return dx, None, None, None
+        if ctx.slot is not None:
+            dx = ctx.slot.deliver(dx)
+        return dx, None, None, None, None
 
 
-def max_pool2d(x, kernel_size, stride, padding=0):
+def max_pool2d(x, kernel_size, stride, padding=0, slot=None):
     k, s, p = _pool_args(kernel_size, stride, padding)
-    return MaxPoolFn.apply(_cl(x), k, s, p)
+    return MaxPoolFn.apply(_cl(x), k, s, p, slot)
 
 
 class AvgPoolFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, k, s, p):
+    def forward(ctx, x, k, s, p, slot=None):
         n, c, h, w = x.shape
         oh = (h + 2 * p[0] - k[0]) // s[0] + 1
         ow = (w + 2 * p[1] - k[1]) // s[1] + 1
         y = _empty_cl(n, c, oh, ow, x.device)
         C.avgpool_fwd(x, y, n, h, w, c, oh, ow, k[0], k[1], s[0], s[1], p[0], p[1])
         ctx.geo = (n, h, w, c, oh, ow, k, s, p)
+        ctx.slot = slot
         return y
 
     @staticmethod
@@ -846,12 +855,14 @@ class AvgPoolFn(torch.autograd.Function):
         n, h, w, c, oh, ow, k, s, p = ctx.geo
         dx = _empty_cl(n, c, h, w, dy.device)
         C.avgpool_bwd(_cl(dy), dx, n, h, w, c, oh, ow, k[0], k[1], s[0], s[1], p[0], p[1])
-        return dx, None, None, None
+        if ctx.slot is not None:
+            dx = ctx.slot.deliver(dx)
+        return dx, None, None, None, None
 
 
-def avg_pool2d(x, kernel_size, stride, padding=0):
+def avg_pool2d(x, kernel_size, stride, padding=0, slot=None):
     k, s, p = _pool_args(kernel_size, stride, padding)
-    return AvgPoolFn.apply(_cl(x), k, s, p)
+    return AvgPoolFn.apply(_cl(x), k, s, p, slot)
 
 
 class GapFn(torch.autograd.Function):

@@ -14,7 +14,7 @@ def _grads(block, x, use_slots):
     from pytorch_imageclassification_distributed_amd.ops import hip
     orig, orig_fuse = Fx.grad_slot, hip.FUSE_BN_BWD
     if not use_slots:
-        Fx.grad_slot = lambda t: None
+        Fx.grad_slot = lambda t, n=2: None
         hip.FUSE_BN_BWD = False
     try:
         for p in block.parameters():
@@ -151,3 +151,25 @@ def test_deterministic_mode(model_name):
         assert torch.equal(a, b)
     o3, _ = run()
     torch.testing.assert_close(o3, o1, rtol=0.05, atol=0.05 * o1.abs().max().item())
+
+
+@pytest.mark.parametrize("kind,expect", [("A", 3), ("B", 2), ("C", 6), ("D", 4), ("E", 3)])
+def test_inception_block_fusion(kind, expect):
+    """Inception blocks: chain-internal convs fuse their producer's BN-backward reduce and InceptionE's
+    paired slots fuse too; gradients equal the unfused path."""
+    from pytorch_imageclassification_distributed_amd.models import inception as inc
+    from pytorch_imageclassification_distributed_amd.ops import hip
+    torch.manual_seed(0)
+    blk, cin, hw = {"A": (inc.InceptionA(64, 32), 64, 17), "B": (inc.InceptionB(64), 64, 17),
+                    "C": (inc.InceptionC(128, 64), 128, 9), "D": (inc.InceptionD(128), 128, 9),
+                    "E": (inc.InceptionE(128), 128, 8)}[kind]
+    blk = blk.to(DEV).to(memory_format=torch.channels_last)
+    x = torch.randn(4, cin, hw, hw, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    gx0, gp0 = _grads(blk, x, False)
+    before = hip.FUSED_BWD_COUNT[0]
+    gx1, gp1 = _grads(blk, x, True)
+    assert hip.FUSED_BWD_COUNT[0] - before == expect
+    err = lambda a, b: ((a - b).abs().max() / b.abs().max().clamp(min=1e-6)).item()  # noqa: E731
+    assert err(gx1, gx0) < 3e-2, err(gx1, gx0)
+    for n in gp0:
+        assert err(gp1[n], gp0[n]) < 3e-2, (n, err(gp1[n], gp0[n]))
