@@ -44,6 +44,13 @@ def timeit(fn, iters=10, warm=2):
     return a.elapsed_time(b) / iters
 
 
+def _cfg_name(hip, c):
+    if c[2] < 0:
+        return f"st{c[0]}/n{c[1]}"
+    tm, bn, wm, wn, st = hip.conv_cfgs()[c[2]]
+    return f"{tm}x{bn}/{wm}x{wn}/s{st}"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
@@ -53,13 +60,17 @@ def main():
     ap.add_argument("--single", default="", help="comma list of 1-stage-ring k-step thresholds to A/B (0 = never)")
     ap.add_argument("--wvariants", default="", help="comma list of wgrad kernel variants to A/B (1,2)")
     ap.add_argument("--wblocks", default="", help="comma list of wgrad split-K target block counts to sweep")
+    ap.add_argument("--tune-log", action="store_true", help="print every fwd/dgrad tuning candidate's time")
+    ap.add_argument("--only", default="", help="comma list of shape indices (into R50) to run")
     a = ap.parse_args()
     from pytorch_imageclassification_distributed_amd.ops import hip
     dev = "cuda"
     n = a.batch
     rows = []
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0, "t_fwd": 0.0, "t_bwd": 0.0}
-    for (ci, co, k, s, p, h, cnt) in R50:
+    shapes = [R50[int(i)] for i in a.only.split(",")] if a.only else R50
+    for (ci, co, k, s, p, h, cnt) in shapes:
+        hip.TUNE_LOG.clear()
         conv = nn.Conv2d(ci, co, k, s, p, bias=False).to(dev).to(memory_format=torch.channels_last)
         x = torch.randn(n, ci, h, h, device=dev, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
         g = hip.ConvGeom(x, conv)
@@ -131,9 +142,15 @@ def main():
         if a.torch:
             msg += f" || miopen fwd {r['torch_fwd_ms']:7.3f}ms bwd {r['torch_bwd_ms']:7.3f}ms"
         print(msg, flush=True)
+        if a.tune_log:
+            for (m_, n_, k_, times) in hip.TUNE_LOG:
+                best = min(times, key=times.get)
+                print(f"      tune M={m_} N={n_} K={k_}: " + "  ".join(
+                    f"{'*' if c == best else ''}{_cfg_name(hip, c)}:{t * 1e3:.0f}us" for c, t in times.items()),
+                    flush=True)
     print("tuned wgrad (blocks, stages):", {f"{k[4]}<-{k[1]} k{k[5]}s{k[7]} {k[2]}x{k[3]}": v
                                              for k, v in hip._WGRAD_TUNED.items()})
-    print("tuned fwd/dgrad (ring depth, tile_n):", sorted(collections.Counter(hip._STAGES_TUNED.values()).items()))
+    print("tuned fwd/dgrad configs:", sorted(collections.Counter(_cfg_name(hip, c) for c in hip._STAGES_TUNED.values()).items()))
     print(json.dumps({"batch": n, "total_ms": tot, "rows": rows}))
 
 

@@ -50,6 +50,7 @@ int ce_bwd_launch(const float*, const long long*, const float*, const float*, co
 int adam_launch(const void*, const void*, int, const float*, float, float, float, float, float, int, hipStream_t);
 int adam_tick_launch(float*, float, hipStream_t);
 int prepare_input_launch(const float*, bf16_t*, int, int, int, int, const float*, const float*, hipStream_t);
+int prepare_input_s2d_launch(const float*, bf16_t*, int, int, int, hipStream_t);
 int cast_bf16_launch(const float*, bf16_t*, long, hipStream_t);
 int weight_pad_launch(const bf16_t*, bf16_t*, long, int, int, hipStream_t);
 int weight_t_launch(const bf16_t*, bf16_t*, int, int, int, hipStream_t);
@@ -105,7 +106,7 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
                int IH, int IW, int sA, int ldb, int OH, int OW, int so, int oh0, int ow0, int ldc, int c_off,
                std::vector<int> dh, std::vector<int> dw, std::vector<int> tb, int stats_groups, Tensor zero,
                OT addend, OT bwd_y, OT bwd_res, OT bwd_coef, OT bwd_part, int bwd_act, int bwd_groups,
-               int stages, int tile_n, OT a_sc, OT b_sc) {
+               int stages, int tile_n, int cfg, OT a_sc, OT b_sc) {
   const bool fp8 = a_sc.has_value() && a_sc->defined();
   TORCH_CHECK(A.scalar_type() == (fp8 ? at::kFloat8_e4m3fn : BF) && B.scalar_type() == A.scalar_type(),
               "conv_gemm: A and B must both be bf16, or both float8_e4m3fn with scales");
@@ -131,10 +132,13 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
   p.bwd_part = optr<float>(bwd_part);
   p.bwd_act = bwd_act;
   p.bwd_groups = bwd_groups > 0 ? bwd_groups : 1;
-  TORCH_CHECK(stages >= 0 && stages <= 2, "conv_gemm: stages must be 0 (auto), 1 or 2");
+  TORCH_CHECK(stages >= 0 && stages <= 3, "conv_gemm: stages must be 0 (auto), 1, 2 or 3");
   p.stages = stages;
   TORCH_CHECK(tile_n == 0 || tile_n == 64 || tile_n == 128, "conv_gemm: tile_n must be 0, 64 or 128");
+  TORCH_CHECK(cfg >= -1 && cfg < conv_num_cfgs(), "conv_gemm: cfg out of range");
+  TORCH_CHECK(cfg < 0 || !fp8, "conv_gemm: the configuration table is bf16-only");
   p.tile_n = tile_n;
+  p.cfg = cfg;
   if (fp8) {
     TORCH_CHECK(b_sc.has_value() && b_sc->defined() && a_sc->scalar_type() == at::kByte &&
                     b_sc->scalar_type() == at::kByte,
@@ -166,7 +170,7 @@ void conv_wgrad(Tensor dY, Tensor X, Tensor dW, int M, int Cout, int Cin, int Nt
   p.stride_h = sh; p.stride_w = sw; p.pad_t = pt; p.pad_l = pl; p.dil_h = dh; p.dil_w = dwd; p.KW = KW;
   p.k_per_split = k_per_split;
   p.zero = ptr<bf16_t>(zero);
-  TORCH_CHECK(stages >= 0 && stages <= 2, "conv_wgrad: stages must be 0, 1 or 2");
+  TORCH_CHECK(stages >= 0 && stages <= 3, "conv_wgrad: stages must be 0, 1, 2 or 3 (2-stage, 8 waves)");
   p.stages = stages;
   check(conv_wgrad_launch(p, splits, cur()), "conv_wgrad");
 }
@@ -321,6 +325,14 @@ void adam(Tensor table, Tensor chunks, int nchunks, Tensor lr_step, double b1, d
 }
 
 void adam_tick(Tensor lr_step, double lr) { check(adam_tick_launch(ptr<float>(lr_step), (float)lr, cur()), "adam_tick"); }
+
+void prepare_input_s2d(Tensor x, Tensor y, int N, int H, int W) {
+  req(x, F32, "x"); req(y, BF, "y");
+  TORCH_CHECK(x.is_contiguous() && x.numel() == (int64_t)N * 3 * H * W && H % 2 == 0 && W % 2 == 0,
+              "prepare_input_s2d: contiguous fp32 [N,3,H,W] with even H, W");
+  TORCH_CHECK(y.numel() == (int64_t)N * (H / 2) * (W / 2) * 16, "prepare_input_s2d: y is [N,16,H/2,W/2]");
+  check(prepare_input_s2d_launch(ptr<float>(x), ptr<bf16_t>(y), N, H, W, cur()), "prepare_input_s2d");
+}
 
 void prepare_input(Tensor x, Tensor y, int N, int C, int HW, int Cp, OT sc, OT sh) {
   req(x, F32, "x"); req(y, BF, "y");
@@ -487,6 +499,16 @@ PYBIND11_MODULE(_C, m) {
   m.def("mx_wjob_bytes", &mx_wjob_bytes);
   m.def("weight_t_job_bytes", &weight_t_job_bytes);
   m.def("prepare_input", &prepare_input);
+  m.def("prepare_input_s2d", &prepare_input_s2d);
+  m.def("conv_cfgs", []() {
+    std::vector<std::vector<int>> out;
+    for (int i = 0; i < conv_num_cfgs(); ++i) {
+      std::vector<int> c(5);
+      conv_cfg_info(i, c.data());
+      out.push_back(c);
+    }
+    return out;
+  });
   m.def("cast_bf16", &cast_bf16);
   m.def("weight_pad", &weight_pad);
   m.def("weight_t", &weight_t);

@@ -47,10 +47,12 @@ DEVI int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
 }
 
-template <int BN>
-DEVI void conv_epilogue(const ConvParams& p, f32x4 (&acc)[BM / 32][BN / 32], char* smem, int tid, int lane,
-                        int wid, int wm, int wn, int m0, int n0, int bm, int ghw) {
-  constexpr int WTM = BM / 2, WTN = BN / 2;
+// Epilogue of a TM x BN tile computed by WM x WN waves (each wave a (TM/WM) x (BN/WN) sub-tile).
+template <int TM, int BN, int WM, int WN>
+DEVI void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16], char* smem, int tid,
+                        int lane, int wid, int wm, int wn, int m0, int n0, int bm, int ghw) {
+  constexpr int NTH = 64 * WM * WN;
+  constexpr int WTM = TM / WM, WTN = BN / WN;
   constexpr int RM = WTM / 16, RN = WTN / 16;
   constexpr int CST = BN + 8;
   const int fr = lane & 15, fq = lane >> 4;
@@ -81,7 +83,8 @@ DEVI void conv_epilogue(const ConvParams& p, f32x4 (&acc)[BM / 32][BN / 32], cha
   // 2) stream the tile out: 16 B (8 channels of one pixel) per lane, coalesced rows;
   //    BN partial statistics accumulate on the way out (from the bf16-rounded values)
   constexpr int CPR = BN / 8;        // chunks per row
-  constexpr int RPP = NT / CPR;      // rows per pass
+  constexpr int RPP = NTH / CPR;     // rows per pass
+  static_assert(CPR <= 64 && NTH % CPR == 0, "epilogue row mapping");
   const int sch = tid % CPR, srow = tid / CPR;
   const int col = n0 + sch * 8;
   const bool col_ok = col < p.Ncols;
@@ -102,7 +105,7 @@ DEVI void conv_epilogue(const ConvParams& p, f32x4 (&acc)[BM / 32][BN / 32], cha
     }
   }
 #pragma unroll 4
-  for (int row = srow; row < BM; row += RPP) {
+  for (int row = srow; row < TM; row += RPP) {
     const int m = m0 + row;
     if (m < p.M && col_ok) {
       uint4 v = *(const uint4*)(ct + row * CST + sch * 8);
@@ -163,7 +166,7 @@ DEVI void conv_epilogue(const ConvParams& p, f32x4 (&acc)[BM / 32][BN / 32], cha
       }
     }
     __syncthreads();  // tile reads done; reuse LDS for the cross-wave reduction
-    float* red = (float*)smem;  // [4 waves][2][BN]
+    float* red = (float*)smem;  // [waves][2][BN]
     if (lane < CPR) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -175,7 +178,7 @@ DEVI void conv_epilogue(const ConvParams& p, f32x4 (&acc)[BM / 32][BN / 32], cha
     if (tid < BN && n0 + tid < p.Ncols) {
       float s = 0.f, q = 0.f;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
+      for (int w = 0; w < WM * WN; ++w) {
         s += red[(w * 2 + 0) * BN + tid];
         q += red[(w * 2 + 1) * BN + tid];
       }
@@ -309,7 +312,7 @@ __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(const ConvParams p) {
 #undef CONV_LOAD
 #undef CONV_STORE
 
-  conv_epilogue<BN>(p, acc, smem, tid, lane, wid, wm, wn, m0, n0, bm, ghw);
+  conv_epilogue<BM, BN, 2, 2>(p, acc, smem, tid, lane, wid, wm, wn, m0, n0, bm, ghw);
 }
 
 
@@ -331,32 +334,56 @@ DEVI void glds16(const void* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
-template <int BN, int STAGES, bool TAP_UNIFORM>
-__global__ __launch_bounds__(NT, STAGES == 1 ? (BN == 128 ? 3 : 4) : 1) void conv_gemm_glds_kernel(const ConvParams p) {
-  constexpr int A_BYTES = BM * BK * 2;
-  constexpr int B_BYTES = BN * BK * 2;
-  constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int WTM = BM / 2, WTN = BN / 2;
+// Tile TM x BN, WM x WN waves (NTH = 64*WM*WN threads).  128 x {64,128} on 4 waves is the workhorse
+// (1-stage ring: 3-4 blocks/CU hide latency by occupancy; 2-stage: in-block overlap).  256 x {64,128,256}
+// on 8 waves (2 per SIMD, one block per CU) keeps a deeper ring in flight across the barrier (3 stages =
+// 2 tiles ahead at BN <= 128) and halves the LDS-DMA bytes per FLOP of the 128-row tile.
+template <int TM, int BN, int WM, int WN, int STAGES>
+struct GldsCfg {
+  static constexpr int NW = WM * WN, NTH = 64 * NW;
+  static constexpr int A_BYTES = TM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  static constexpr int CST = BN + 8;
+  static constexpr int EPI = TM * CST * 2;
+  // the epilogue tile reuses the ring; a short ring is sized by the epilogue instead
+  static constexpr int MAIN = STAGES * STAGE > EPI ? STAGES * STAGE : EPI;
+  // waves per SIMD the register budget is sized for (launch bound): the LDS-limited blocks per CU x
+  // waves per block / 4, lowered until an estimate of the kernel's VGPRs fits (no spills):
+  // accumulators + fragments + per-row gather addresses + ~48 of bookkeeping
+  static constexpr int BLOCKS = (160 * 1024) / (MAIN + 3 * CONV_MAX_TAPS * 4);
+  static constexpr int OCC_LDS = BLOCKS * NW / 4 < 1 ? 1 : (BLOCKS * NW / 4 > 4 ? 4 : BLOCKS * NW / 4);
+  static constexpr int EST_VGPR = (TM / WM) * (BN / WN) / 64 + 4 * (TM / WM / 16 + BN / WN / 16) +
+                                  4 * (TM / 8 / NW) + 2 * (BN / 8 / NW) + 48;
+  static constexpr int OCC_REG = 512 / EST_VGPR < 1 ? 1 : 512 / EST_VGPR;
+  static constexpr int OCC = OCC_LDS < OCC_REG ? OCC_LDS : OCC_REG;
+};
+
+template <int TM, int BN, int WM, int WN, int STAGES, bool TAP_UNIFORM>
+__global__ __launch_bounds__((GldsCfg<TM, BN, WM, WN, STAGES>::NTH), (GldsCfg<TM, BN, WM, WN, STAGES>::OCC))
+void conv_gemm_glds_kernel(const ConvParams p) {
+  using Cfg = GldsCfg<TM, BN, WM, WN, STAGES>;
+  constexpr int NW = Cfg::NW;
+  constexpr int A_BYTES = Cfg::A_BYTES;
+  constexpr int STAGE = Cfg::STAGE;
+  constexpr int WTM = TM / WM, WTN = BN / WN;
   constexpr int RM = WTM / 16, RN = WTN / 16;
-  constexpr int AL = BM / 32;        // LDS-DMA instructions per wave per stage (A): 8 rows each
-  constexpr int BL = BN / 32;        // (B)
+  constexpr int AL = TM / 8 / NW;    // LDS-DMA instructions per wave per stage (A): 8 rows of 128 B each
+  constexpr int BL = BN / 8 / NW;    // (B)
   constexpr int LPS = AL + BL;
-  constexpr int TAP_BYTES = 3 * CONV_MAX_TAPS * 4;
-  constexpr int CST = BN + 8;
-  // the epilogue tile reuses the ring; a 1-stage ring (short K) is sized by the epilogue instead
-  constexpr int MAIN = STAGES * STAGE > BM * CST * 2 ? STAGES * STAGE : BM * CST * 2;
-  __shared__ __attribute__((aligned(16))) char smem[MAIN + TAP_BYTES];
+  constexpr int MAIN = Cfg::MAIN;
+  static_assert(AL >= 1 && BL >= 1 && AL * 8 * NW == TM && BL * 8 * NW == BN, "loader mapping");
+  static_assert(MAIN + 3 * CONV_MAX_TAPS * 4 <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(16))) char smem[MAIN + 3 * CONV_MAX_TAPS * 4];
   int* s_dh = (int*)(smem + MAIN);
   int* s_dw = s_dh + CONV_MAX_TAPS;
   int* s_tb = s_dw + CONV_MAX_TAPS;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform (M0 base)
-  const int wm = wid >> 1, wn = wid & 1;
-  const int gm = (p.M + BM - 1) / BM, gn = (p.Ncols + BN - 1) / BN;
+  const int wm = wid / WN, wn = wid % WN;
+  const int gm = (p.M + TM - 1) / TM, gn = (p.Ncols + BN - 1) / BN;
   const int lin = xcd_remap(blockIdx.x, gm * gn);
   const int bm = lin / gn, bn = lin - bm * gn;
-  const int m0 = bm * BM, n0 = bn * BN;
+  const int m0 = bm * TM, n0 = bn * BN;
   if (tid < p.ntaps) {
     s_dh[tid] = p.tap_dh[tid];
     s_dw[tid] = p.tap_dw[tid];
@@ -368,7 +395,7 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? (BN == 128 ? 3 : 4) : 1) void con
   int a_base[AL], a_ih[AL], a_iw[AL], a_ch[AL];
 #pragma unroll
   for (int i = 0; i < AL; ++i) {
-    const int row = wid * (BM / 4) + i * 8 + lrow;
+    const int row = wid * (TM / NW) + i * 8 + lrow;
     a_ch[i] = pch ^ ((row >> 1) & 7);
     const int m = m0 + row;
     if (m < p.M) {
@@ -386,7 +413,7 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? (BN == 128 ? 3 : 4) : 1) void con
   int b_off[BL], b_ch[BL];
 #pragma unroll
   for (int i = 0; i < BL; ++i) {
-    const int row = wid * (BN / 4) + i * 8 + lrow;
+    const int row = wid * (BN / NW) + i * 8 + lrow;
     b_ch[i] = pch ^ ((row >> 1) & 7);
     const int n = n0 + row;
     b_off[i] = n < p.Ncols ? n * p.ldb : -1;
@@ -433,9 +460,9 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? (BN == 128 ? 3 : 4) : 1) void con
       }
     }
 #pragma unroll
-    for (int i = 0; i < AL; ++i) glds16(srca[i], sa + (wid * (BM / 4) + i * 8) * 128);
+    for (int i = 0; i < AL; ++i) glds16(srca[i], sa + (wid * (TM / NW) + i * 8) * 128);
 #pragma unroll
-    for (int i = 0; i < BL; ++i) glds16(srcb[i], sb + (wid * (BN / 4) + i * 8) * 128);
+    for (int i = 0; i < BL; ++i) glds16(srcb[i], sb + (wid * (BN / NW) + i * 8) * 128);
   };
 
   f32x4 acc[RM][RN];
@@ -451,12 +478,14 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? (BN == 128 ? 3 : 4) : 1) void con
   const int fr = lane & 15, fq = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
     if constexpr (STAGES == 1) {
-      // no in-block overlap: latency is hidden by the 4 co-resident blocks this LDS size allows
+      // no in-block overlap: latency is hidden by the co-resident blocks this LDS size allows
       if (kt > 0) __builtin_amdgcn_s_barrier();
       issue(kt, 0);
       wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
     } else {
+      // tile kt landed (the STAGES-2 younger tiles may stay in flight across the barrier); the
+      // barrier also retires every wave's reads of the buffer the next issue overwrites
       if (kt + STAGES - 2 < nk) wait_vmcnt<(STAGES - 2) * LPS>();
       else wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
@@ -479,7 +508,7 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? (BN == 128 ? 3 : 4) : 1) void con
     }
   }
   __syncthreads();
-  conv_epilogue<BN>(p, acc, smem, tid, lane, wid, wm, wn, m0, n0, bm, ghw);
+  conv_epilogue<TM, BN, WM, WN>(p, acc, smem, tid, lane, wid, wm, wn, m0, n0, bm, ghw);
 }
 
 // ---------------------------------------------------------------------------
@@ -662,7 +691,7 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? (BN == 128 ? 3 : 4) : 1) void con
                                                                      sx[i]);
   }
   __syncthreads();
-  conv_epilogue<BN>(p, acc, smem, tid, lane, wid, wm, wn, m0, n0, bm, ghw);
+  conv_epilogue<BM, BN, 2, 2>(p, acc, smem, tid, lane, wid, wm, wn, m0, n0, bm, ghw);
 }
 
 // ---------------------------------------------------------------------------
@@ -824,32 +853,53 @@ DEVI int wswz(int row) {  // XOR mask on the 32-B block index
   return ROWB == 256 ? (row & 7) : ((row >> 1) & 3);
 }
 
-template <int WBM, int STAGES>
-__global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_wgrad_glds_kernel(const WgradParams p) {
-  constexpr int AROWB = WBM * 2;            // A image row bytes (128 / 256)
-  constexpr int BROWB = WBN * 2;            // 256
-  constexpr int A_BYTES = WBK * AROWB;
-  constexpr int B_BYTES = WBK * BROWB;
-  constexpr int STAGE = A_BYTES + B_BYTES;
+// KG wave groups of 4 split every k-step's pixels (KG = 2: a 128-pixel stage, 8 waves, the two
+// groups' partial tiles summed through LDS before the atomics): at one block per CU this halves the
+// atomic bytes per unit of work (atomics run at ~1.3 TB/s chip-wide, a real cost at high split counts).
+template <int WBM, int STAGES, int KG>
+struct WgCfg {
+  static constexpr int NTH = 256 * KG;
+  static constexpr int AROWB = WBM * 2, BROWB = WBN * 2;
+  static constexpr int STAGE = WBK * KG * (AROWB + BROWB);
+  static constexpr int LDT = WBN + 4;
+  static constexpr int EPI = (KG == 2 ? WBM : WBM / 2) * LDT * 4;
+  static constexpr int MAIN = STAGES * STAGE > EPI ? STAGES * STAGE : EPI;
+  static constexpr int OCC = KG == 2 ? 2 : (STAGES == 1 ? 3 : 2);
+};
+
+template <int WBM, int STAGES, int KG>
+__global__ __launch_bounds__((WgCfg<WBM, STAGES, KG>::NTH), (WgCfg<WBM, STAGES, KG>::OCC))
+void conv_wgrad_glds_kernel(const WgradParams p) {
+  using Cfg = WgCfg<WBM, STAGES, KG>;
+  constexpr int NTH = Cfg::NTH;
+  constexpr int AROWB = Cfg::AROWB;         // A image row bytes (128 / 256)
+  constexpr int BROWB = Cfg::BROWB;         // 256
+  constexpr int KPS = WBK * KG;             // pixels per stage
+  constexpr int A_BYTES = KPS * AROWB;
+  constexpr int STAGE = Cfg::STAGE;
   constexpr int WTM = WBM / 2, WTN = WBN / 2;
   constexpr int RM = WTM / 16, RN = WTN / 16;
   constexpr int ARPI = 1024 / AROWB;        // rows per LDS-DMA instruction (8 / 4)
   constexpr int AL = WBK / ARPI / 4;        // instructions per wave per stage (2 / 4)
   constexpr int BRPI = 1024 / BROWB;        // 4
   constexpr int BL = WBK / BRPI / 4;        // 4
-  constexpr int LDT = WBN + 4;              // floats per staged epilogue row
-  constexpr int EPI = (WBM / 2) * LDT * 4;
-  constexpr int MAIN = STAGES * STAGE > EPI ? STAGES * STAGE : EPI;
+  constexpr int LDT = Cfg::LDT;             // floats per staged epilogue row
+  constexpr int MAIN = Cfg::MAIN;
   __shared__ __attribute__((aligned(16))) char smem[MAIN];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid >> 1, wn = wid & 1;
+  const int grp = wid >> 2, lw = wid & 3;   // wave group (k half) and wave within the group
+  const int wm = lw >> 1, wn = lw & 1;
   const int gm = (p.Cout + WBM - 1) / WBM;
-  const int tile = blockIdx.x;
+  // XCD-aware order: the tiles of one pixel slice (which all read the same dY rows and overlapping X
+  // rows) are consecutive logical ids, and consecutive logical ids share an XCD (and its L2)
+  const int ntile = gridDim.x;
+  const int lin = xcd_remap(blockIdx.y * ntile + blockIdx.x, ntile * gridDim.y);
+  const int split = lin / ntile, tile = lin - split * ntile;
   const int bm = tile % gm, bn = tile / gm;
   const int co0 = bm * WBM, j0 = bn * WBN;
-  const int kbeg = blockIdx.y * p.k_per_split;
+  const int kbeg = split * p.k_per_split;
   const int kend = min(p.M, kbeg + p.k_per_split);
   const int ohw = p.OH * p.OW;
   const float inv_ohw = 1.f / (float)ohw, inv_ow = 1.f / (float)p.OW;
@@ -914,28 +964,30 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_wgrad_glds_kerne
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (kend - kbeg + WBK - 1) / WBK;
+  const int nk = (kend - kbeg + KPS - 1) / KPS;
   if (nk <= 0) return;
-  if (STAGES == 2) issue(kbeg, 0);
+  if (STAGES >= 2) issue(kbeg, 0);
+  if (STAGES >= 3 && nk > 1) issue(kbeg + KPS, 1);
   const int g = lane >> 4, li = lane & 15;
   const int tq = li >> 2, tp = li & 3;
   for (int kt = 0; kt < nk; ++kt) {
     if constexpr (STAGES == 1) {  // latency hidden by co-resident blocks instead of the ring
       if (kt > 0) __builtin_amdgcn_s_barrier();
-      issue(kbeg + kt * WBK, 0);
+      issue(kbeg + kt * KPS, 0);
       wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
     } else {
-      wait_vmcnt<0>();
+      if (kt + STAGES - 2 < nk) wait_vmcnt<(STAGES - 2) * (AL + BL)>();
+      else wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
-      if (kt + 1 < nk) issue(kbeg + (kt + 1) * WBK, (kt + 1) & 1);
+      if (kt + STAGES - 1 < nk) issue(kbeg + (kt + STAGES - 1) * KPS, (kt + STAGES - 1) % STAGES);
     }
-    const char* sa = smem + (STAGES == 1 ? 0 : (kt & 1) * STAGE);
+    const char* sa = smem + (kt % STAGES) * STAGE;
     const char* sb = sa + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       // permuted k order (identical for A and B): elements 0-3 <- rows 4g+q, 4-7 <- rows 16+4g+q
-      const int r0 = kk * 32 + 4 * g + tq, r1 = r0 + 16;
+      const int r0 = grp * WBK + kk * 32 + 4 * g + tq, r1 = r0 + 16;
       bf16x8 af[RM], bfg[RN];
 #pragma unroll
       for (int i = 0; i < RM; ++i) {
@@ -960,25 +1012,55 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? 3 : 2) void conv_wgrad_glds_kerne
   }
   const int fr = lane & 15, fq = lane >> 4;
   // acc[i][j][r] = dW[co0 + wm*WTM + i*16 + fr][j0 + wn*WTN + j*16 + fq*4 + r]: 4 consecutive columns
-  // per lane -> one 16-B LDS write; the fp32 tile is staged through LDS in row halves of WTM rows and
-  // added to global memory with atomics whose wave-instructions each cover 256 contiguous bytes.
+  // per lane -> one 16-B LDS write; the fp32 tile is staged through LDS and added to global memory
+  // with atomics whose wave-instructions each cover 256 contiguous bytes.
   float* st = (float*)smem;
-#pragma unroll
-  for (int half = 0; half < 2; ++half) {
+  if constexpr (KG == 2) {
+    // group 1 parks its partial tile, group 0 adds its own, then all 512 threads issue the atomics
     __syncthreads();
-    if (wm == half) {
+    if (grp == 1) {
 #pragma unroll
       for (int i = 0; i < RM; ++i)
 #pragma unroll
         for (int j = 0; j < RN; ++j)
-          *(f32x4*)(st + (i * 16 + fr) * LDT + wn * WTN + j * 16 + fq * 4) = acc[i][j];
+          *(f32x4*)(st + (wm * WTM + i * 16 + fr) * LDT + wn * WTN + j * 16 + fq * 4) = acc[i][j];
+    }
+    __syncthreads();
+    if (grp == 0) {
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j) {
+          f32x4* d = (f32x4*)(st + (wm * WTM + i * 16 + fr) * LDT + wn * WTN + j * 16 + fq * 4);
+          *d = *d + acc[i][j];
+        }
     }
     __syncthreads();
 #pragma unroll 4
-    for (int e = tid; e < WTM * WBN; e += NT) {  // consecutive lanes -> consecutive floats
+    for (int e = tid; e < WBM * WBN; e += NTH) {  // consecutive lanes -> consecutive floats
       const int row = e / WBN, c = e - row * WBN;
-      const int co = co0 + half * WTM + row, col = j0 + c;
+      const int co = co0 + row, col = j0 + c;
       if (co < p.Cout && col < p.Ntot) atomicAdd(p.dW + (long)co * p.Ntot + col, st[row * LDT + c]);
+    }
+  } else {
+    // fp32 tile staged in row halves of WTM rows
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      __syncthreads();
+      if (wm == half) {
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+            *(f32x4*)(st + (i * 16 + fr) * LDT + wn * WTN + j * 16 + fq * 4) = acc[i][j];
+      }
+      __syncthreads();
+#pragma unroll 4
+      for (int e = tid; e < WTM * WBN; e += NTH) {  // consecutive lanes -> consecutive floats
+        const int row = e / WBN, c = e - row * WBN;
+        const int co = co0 + half * WTM + row, col = j0 + c;
+        if (co < p.Cout && col < p.Ntot) atomicAdd(p.dW + (long)co * p.Ntot + col, st[row * LDT + c]);
+      }
     }
   }
 }
@@ -990,23 +1072,49 @@ void conv_set_variant(int v) { g_variant = v; }
 static int g_single_nk = 4;  // GEMMs with at most this many 64-wide k-steps use the 1-stage ring
 void conv_set_single_stage(int nk) { g_single_nk = nk; }
 
+template <int TM, int BN, int WM, int WN, int STAGES>
+static void launch_glds(const ConvParams& p, hipStream_t stream) {
+  const int grid = cdiv(p.M, TM) * cdiv(p.Ncols, BN);
+  constexpr int NTH = 64 * WM * WN;
+  if ((p.CA % BK) == 0)
+    hipLaunchKernelGGL((conv_gemm_glds_kernel<TM, BN, WM, WN, STAGES, true>), dim3(grid), dim3(NTH), 0, stream, p);
+  else
+    hipLaunchKernelGGL((conv_gemm_glds_kernel<TM, BN, WM, WN, STAGES, false>), dim3(grid), dim3(NTH), 0, stream, p);
+}
+
 template <int BN>
 static void launch_bn(const ConvParams& p, int gm, hipStream_t stream) {
-  const int gn = cdiv(p.Ncols, BN);
-  const bool uni = (p.CA % BK) == 0;
   const int v = g_variant == 0 ? 2 : g_variant;  // measured: 2-stage LDS-DMA wins (benchmarks/conv_bench.py --variants)
   if (v == 1) {
-    hipLaunchKernelGGL(conv_gemm_kernel<BN>, dim3(gm * gn), dim3(NT), 0, stream, p);
-  } else if (v == 2 && (p.stages == 1 || (p.stages == 0 && cdiv(p.K, BK) <= g_single_nk))) {
-    if (uni) hipLaunchKernelGGL((conv_gemm_glds_kernel<BN, 1, true>), dim3(gm * gn), dim3(NT), 0, stream, p);
-    else hipLaunchKernelGGL((conv_gemm_glds_kernel<BN, 1, false>), dim3(gm * gn), dim3(NT), 0, stream, p);
-  } else if (v == 2) {
-    if (uni) hipLaunchKernelGGL((conv_gemm_glds_kernel<BN, 2, true>), dim3(gm * gn), dim3(NT), 0, stream, p);
-    else hipLaunchKernelGGL((conv_gemm_glds_kernel<BN, 2, false>), dim3(gm * gn), dim3(NT), 0, stream, p);
+    hipLaunchKernelGGL(conv_gemm_kernel<BN>, dim3(gm * cdiv(p.Ncols, BN)), dim3(NT), 0, stream, p);
+  } else if (p.stages == 3 || v == 3) {
+    launch_glds<BM, BN, 2, 2, 3>(p, stream);
+  } else if (p.stages == 1 || (p.stages == 0 && cdiv(p.K, BK) <= g_single_nk)) {
+    launch_glds<BM, BN, 2, 2, 1>(p, stream);
   } else {
-    if (uni) hipLaunchKernelGGL((conv_gemm_glds_kernel<BN, 3, true>), dim3(gm * gn), dim3(NT), 0, stream, p);
-    else hipLaunchKernelGGL((conv_gemm_glds_kernel<BN, 3, false>), dim3(gm * gn), dim3(NT), 0, stream, p);
+    launch_glds<BM, BN, 2, 2, 2>(p, stream);
   }
+}
+
+// Tuned configurations (the per-shape "find" step in ops/hip.py times these on scratch outputs):
+// {tile rows, tile channels, waves along rows, waves along channels, LDS-DMA ring depth}.
+struct ConvCfg { int tm, bn, wm, wn, st; void (*launch)(const ConvParams&, hipStream_t); };
+#define CFG(TM, BN, WM, WN, ST) {TM, BN, WM, WN, ST, &launch_glds<TM, BN, WM, WN, ST>}
+// Measured on the ResNet-50 layers at batch 512 (benchmarks/conv_bench.py --tune-log): the 128-row
+// 4-wave tiles win on 64/128-channel outputs and short K (occupancy hides latency); the 256x256
+// 8-wave tiles (2 waves per SIMD, 64x128 or 128x64 per wave, half the LDS-DMA bytes per FLOP) win
+// 10-20 % on >= 256-channel outputs; configurations with one wave per SIMD never won and are gone.
+static const ConvCfg g_cfgs[] = {
+    CFG(128, 64, 2, 2, 1),  CFG(128, 128, 2, 2, 1), CFG(128, 64, 2, 2, 2), CFG(128, 128, 2, 2, 2),
+    CFG(256, 256, 2, 4, 2), CFG(256, 256, 4, 2, 2), CFG(256, 64, 4, 1, 1), CFG(128, 64, 2, 1, 1),
+};
+#undef CFG
+constexpr int kNumCfgs = sizeof(g_cfgs) / sizeof(g_cfgs[0]);
+
+int conv_num_cfgs() { return kNumCfgs; }
+void conv_cfg_info(int i, int* out5) {
+  const ConvCfg& c = g_cfgs[i];
+  out5[0] = c.tm; out5[1] = c.bn; out5[2] = c.wm; out5[3] = c.wn; out5[4] = c.st;
 }
 
 template <int BN>
@@ -1026,7 +1134,10 @@ int conv_gemm_launch(const ConvParams& p, hipStream_t stream) {
     HIP_CHECK_LAUNCH();
     return 0;
   }
-  if (p.Ncols <= 64 || p.tile_n == 64) launch_bn<64>(p, gm, stream);
+  if (p.cfg >= 0) {
+    if (p.cfg >= kNumCfgs) return 3;
+    g_cfgs[p.cfg].launch(p, stream);
+  } else if (p.Ncols <= 64 || p.tile_n == 64) launch_bn<64>(p, gm, stream);
   else launch_bn<128>(p, gm, stream);
   HIP_CHECK_LAUNCH();
   return 0;
@@ -1039,16 +1150,19 @@ int conv_wgrad_launch(const WgradParams& p, int splits, hipStream_t stream) {
   if (p.M <= 0) return 0;
   const int gn = cdiv(p.Ntot, WBN);
   const bool dma = g_wvariant != 1;
+  // stages: 1 | 2 (4 waves), 3 = 2-stage ring with the in-block 2-way pixel split (8 waves)
   if (p.Cout <= 64) {
-    const int gm = cdiv(p.Cout, 64);
-    if (dma && p.stages == 1) hipLaunchKernelGGL((conv_wgrad_glds_kernel<64, 1>), dim3(gm * gn, splits), dim3(NT), 0, stream, p);
-    else if (dma) hipLaunchKernelGGL((conv_wgrad_glds_kernel<64, 2>), dim3(gm * gn, splits), dim3(NT), 0, stream, p);
-    else hipLaunchKernelGGL(conv_wgrad_kernel<64>, dim3(gm * gn, splits), dim3(NT), 0, stream, p);
+    const dim3 grid(cdiv(p.Cout, 64) * gn, splits);
+    if (dma && p.stages == 1) hipLaunchKernelGGL((conv_wgrad_glds_kernel<64, 1, 1>), grid, dim3(256), 0, stream, p);
+    else if (dma && p.stages == 3) hipLaunchKernelGGL((conv_wgrad_glds_kernel<64, 2, 2>), grid, dim3(512), 0, stream, p);
+    else if (dma) hipLaunchKernelGGL((conv_wgrad_glds_kernel<64, 2, 1>), grid, dim3(256), 0, stream, p);
+    else hipLaunchKernelGGL(conv_wgrad_kernel<64>, grid, dim3(NT), 0, stream, p);
   } else {
-    const int gm = cdiv(p.Cout, 128);
-    if (dma && p.stages == 1) hipLaunchKernelGGL((conv_wgrad_glds_kernel<128, 1>), dim3(gm * gn, splits), dim3(NT), 0, stream, p);
-    else if (dma) hipLaunchKernelGGL((conv_wgrad_glds_kernel<128, 2>), dim3(gm * gn, splits), dim3(NT), 0, stream, p);
-    else hipLaunchKernelGGL(conv_wgrad_kernel<128>, dim3(gm * gn, splits), dim3(NT), 0, stream, p);
+    const dim3 grid(cdiv(p.Cout, 128) * gn, splits);
+    if (dma && p.stages == 1) hipLaunchKernelGGL((conv_wgrad_glds_kernel<128, 1, 1>), grid, dim3(256), 0, stream, p);
+    else if (dma && p.stages == 3) hipLaunchKernelGGL((conv_wgrad_glds_kernel<128, 2, 2>), grid, dim3(512), 0, stream, p);
+    else if (dma) hipLaunchKernelGGL((conv_wgrad_glds_kernel<128, 2, 1>), grid, dim3(256), 0, stream, p);
+    else hipLaunchKernelGGL(conv_wgrad_kernel<128>, grid, dim3(NT), 0, stream, p);
   }
   HIP_CHECK_LAUNCH();
   return 0;

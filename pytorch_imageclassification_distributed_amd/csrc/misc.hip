@@ -41,6 +41,33 @@ __global__ void prepare_input_kernel(const float* __restrict__ x, bf16_t* __rest
   }
 }
 
+// Space-to-depth input for a 7x7 stride-2 stem: y[n][i][j][(dy*2+dx)*3 + c] = x[n][c][2i+dy][2j+dx]
+// (12 channels, zero-padded to 16).  The stride-2 7x7 conv over x becomes a stride-1 4x4 conv over y
+// whose 64-wide k-steps are 4 horizontally adjacent pixels x 16 channels = 128 contiguous bytes.
+__global__ void prepare_input_s2d_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int N, int H, int W) {
+  const int Ho = H >> 1, Wo = W >> 1;
+  const long total = (long)N * Ho * Wo;
+  const long plane = (long)H * W;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long n = i / ((long)Ho * Wo);
+    const int r = (int)(i - n * Ho * Wo);
+    const int oh = r / Wo, ow = r - oh * Wo;
+    float v[16];
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float2 t = *(const float2*)(x + (n * 3 + c) * plane + (long)(2 * oh + dy) * W + 2 * ow);
+        v[(dy * 2 + 0) * 3 + c] = t.x;
+        v[(dy * 2 + 1) * 3 + c] = t.y;
+      }
+#pragma unroll
+    for (int k = 12; k < 16; ++k) v[k] = 0.f;
+    *(uint4*)(y + i * 16) = pack8(v);
+    *(uint4*)(y + i * 16 + 8) = pack8(v + 8);
+  }
+}
+
 __global__ void cast_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long n) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
     y[i] = f2bf(x[i]);
@@ -170,6 +197,13 @@ __global__ void scale_rows_kernel(const bf16_t* __restrict__ x, const float* __r
 }
 
 }  // namespace
+
+int prepare_input_s2d_launch(const float* x, bf16_t* y, int N, int H, int W, hipStream_t s) {
+  hipLaunchKernelGGL(prepare_input_s2d_kernel, dim3(grid_for((long)N * (H / 2) * (W / 2))), dim3(256), 0, s, x, y,
+                     N, H, W);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
 
 int prepare_input_launch(const float* x, bf16_t* y, int N, int C, int HW, int Cp, const float* sc,
                          const float* sh, hipStream_t s) {

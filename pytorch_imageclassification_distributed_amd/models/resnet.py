@@ -120,7 +120,7 @@ class ResNet(nn.Module):
         return Fx.global_avg_pool(x)
 
     def forward(self, x):
-        x = Fx.prepare_input(x)
+        x = Fx.prepare_input(x, stem=self.conv1)
         x = self.forward_features(x)
         return Fx.mlp(x, self.fc) if isinstance(self.fc, nn.Sequential) else Fx.linear(x, self.fc)
 

@@ -214,11 +214,12 @@ def cross_entropy(logits, labels, weight=None):
     return F.cross_entropy(logits.float(), labels, weight=weight)
 
 
-def prepare_input(x):
+def prepare_input(x, stem=None):
     """Move/convert a batch to the layout the active path expects.
 
-    HIP path: channels-last bf16 (NHWC in memory).  Reference path: unchanged.
+    HIP path: channels-last bf16 (NHWC in memory); with ``stem`` (a 7x7 stride-2 first conv) the
+    fp32 batch may be left for the space-to-depth stem to convert.  Reference path: unchanged.
     """
     if use_hip(x):
-        return _hip().prepare_input(x)
+        return _hip().prepare_input(x, stem=stem)
     return x

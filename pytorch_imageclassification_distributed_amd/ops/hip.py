@@ -363,26 +363,57 @@ def _time_ms(run, reps: int = 3, trials: int = 3) -> float:
 
 CONV_STAGES = os.environ.get("IMGCLS_CONV_STAGES", "auto")  # auto (timed per shape) | 0 (heuristic) | 1 | 2
 _STAGES_TUNED: dict = {}
+CONV_FORCE_CFG = None  # (stages, tile_n, tile_m) for every bf16 fwd/dgrad launch (tests)
+TUNE_LOG: list = []  # (M, Ncols, K, {cfg: ms}) per tuned geometry (benchmarks/conv_bench.py prints it)
 
 
 def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(None, None, None, None, 0, 1),
                groups=G_STATS, scales=(None, None)):
     """One implicit-GEMM launch.  The kernel configuration - LDS-DMA ring depth (1 = high occupancy,
-    2 = pipelined) x output-channel tile (64 / 128: more tiles balance 256 CUs better on small
-    layers) - is chosen once per GEMM geometry by timing the candidates on scratch outputs (a
-    conv-algorithm "find" step)."""
-    if CONV_STAGES != "auto":
-        cfg = (int(CONV_STAGES), 0)
+    2 / 3 = pipelined) x output-channel tile (64 / 128 / 256: more tiles balance 256 CUs better on
+    small layers) x pixel tile (128 rows on 4 waves, or 256 rows on 8 waves) - is chosen once per
+    GEMM geometry by timing the candidates on scratch outputs (a conv-algorithm "find" step)."""
+    if CONV_FORCE_CFG is not None and scales[0] is None:
+        cfg = CONV_FORCE_CFG
+    elif CONV_STAGES != "auto":
+        cfg = (int(CONV_STAGES), 0, -1)
     else:
         key = (tuple(geo), out.shape[1], tuple(dh), tuple(dw), stats is not None, bias is not None,
                addend is not None, bwd[0] is not None, bwd[1] is not None, bwd[4], scales[0] is not None)
         cfg = _STAGES_TUNED.get(key)
         if cfg is None:
-            cfg = (0, 0) if torch.cuda.is_current_stream_capturing() else _tune_conv(
+            cfg = (0, 0, -1) if torch.cuda.is_current_stream_capturing() else _tune_conv(
                 A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups, scales)
-            if cfg[0]:
+            if cfg[0] or cfg[2] >= 0:
                 _STAGES_TUNED[key] = cfg
     C.conv_gemm(A, B, out, stats, bias, *geo, dh, dw, tb, groups, zero, addend, *bwd, *cfg, *scales)
+
+
+_CFGS = None
+
+
+def conv_cfgs():
+    """The bf16 kernel configuration table: (tile rows, tile channels, waves M, waves N, ring depth)."""
+    global _CFGS
+    if _CFGS is None:
+        _CFGS = [tuple(c) for c in C.conv_cfgs()]
+    return _CFGS
+
+
+def _conv_candidates(m, ncols, fp8):
+    """(stages, tile_n, cfg) triples worth timing for an M x Ncols GEMM."""
+    if fp8:  # the MX-FP8 kernel: 128-row tiles, ring depth x channel tile
+        return [(st, tn, -1) for st in (1, 2) for tn in ((64,) if ncols <= 64 else (64, 128))]
+    out = []
+    for i, (tm, bn, _wm, _wn, _st) in enumerate(conv_cfgs()):
+        if bn > 64 and bn >= 2 * ncols:   # tile at least half empty
+            continue
+        if bn == 64 and ncols >= 512:     # 8+ column tiles re-read the pixel panel too often
+            continue
+        if tm == 256 and m < 256 * 16:    # too few row tiles to fill the chip
+            continue
+        out.append((0, 0, i))
+    return out
 
 
 def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups, scales=(None, None)):
@@ -391,12 +422,12 @@ def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, group
     bwd = tuple(bwd)
     if bwd[3] is not None:
         bwd = bwd[:3] + (torch.zeros_like(bwd[3]),) + bwd[4:]
-    ncols = geo[1]
-    cands = [(st, tn) for st in (1, 2) for tn in ((64,) if ncols <= 64 else (64, 128))]
+    cands = _conv_candidates(geo[0], geo[1], scales[0] is not None)
     times = {}
     for cfg in cands:
         times[cfg] = _time_ms(lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, groups, zero,
                                                   addend, *bwd, *cfg, *scales))
+    TUNE_LOG.append((geo[0], geo[1], geo[2], times))
     return min(times, key=times.get)
 
 
@@ -404,11 +435,12 @@ def fp8_eligible(g: "ConvGeom") -> bool:
     return FP8_FWD and g.Cx == g.Ci and g.Cx % 128 == 0 and g.Co % 8 == 0
 
 
-def conv_forward_raw(x, w_param, g: ConvGeom, stats=None, bias=None, out=None, c_off=0):
+def conv_forward_raw(x, w_param, g: ConvGeom, stats=None, bias=None, out=None, c_off=0, wb=None):
     dev = x.device
-    if fp8_eligible(g):
+    if wb is None and fp8_eligible(g):
         return _conv_forward_fp8(x, w_param, g, stats, bias, out, c_off)
-    wb = _weight_for_input(w_param, g.Cx)
+    if wb is None:
+        wb = _weight_for_input(w_param, g.Cx)
     y = out if out is not None else _empty_cl(g.N, g.Co, g.OH, g.OW, dev)
     ldc = y.shape[1]
     dh, dw, tb = _fwd_taps(g)
@@ -469,7 +501,7 @@ def _wgrad_split(m, tiles, target):
     return kps, splits
 
 
-WGRAD_STAGES = int(os.environ.get("IMGCLS_WGRAD_STAGES", "0"))  # 0 = tuned with the split count; 1 | 2
+WGRAD_STAGES = int(os.environ.get("IMGCLS_WGRAD_STAGES", "0"))  # 0 = tuned with the split count; 1 | 2 | 3
 
 
 def _wgrad_launch(dy, x, out, g: ConvGeom, m, ntot, kps, splits, stages=2):
@@ -497,10 +529,13 @@ def _wgrad_config(dy, x, g: ConvGeom, m, ntot, tiles):
         return blocks[len(blocks) // 2], stages[-1]
     scratch = torch.zeros(g.Co * ntot, dtype=torch.float32, device=dy.device)
     times = {}
-    for st in stages:
-        for cand in blocks:
-            kps, splits = _wgrad_split(m, tiles, cand)
-            times[(cand, st)] = _time_ms(lambda: _wgrad_launch(dy, x, scratch, g, m, ntot, kps, splits, st))
+    cands = [(cand, st) for st in stages for cand in blocks]
+    if WGRAD_STAGES == 0:
+        # 8-wave blocks (in-block 2-way pixel split, one block per CU): fewer, larger blocks
+        cands += [(cand, 3) for cand in blocks if cand <= 1024]
+    for cand, st in cands:
+        kps, splits = _wgrad_split(m, tiles, cand)
+        times[(cand, st)] = _time_ms(lambda: _wgrad_launch(dy, x, scratch, g, m, ntot, kps, splits, st))
     best = min(times, key=times.get)
     _WGRAD_TUNED[key] = best
     return best
@@ -604,6 +639,89 @@ class ConvFn(torch.autograd.Function):
                 dx = slot.deliver(dx, fused=addend is not None)
         dw = conv_wgrad_raw(dy, x, w, g) if ctx.needs_input_grad[1] else None
         return dx, dw, None, None, None, None
+
+
+# ---------------------------------------------------------------------------
+# space-to-depth stem: 7x7 stride-2 conv of a 3-channel image
+# ---------------------------------------------------------------------------
+# y = conv7x7/s2/p3(x) equals a stride-1 4x4 conv (pad 2 top/left, 1 bottom/right) over
+# s2d(x)[n][i][j][(dy*2+dx)*3 + c] = x[n][c][2i+dy][2j+dx] (16 channels, 12 used) with
+# W'[co][ta][tb][(dy*2+dx)*3 + c] = W[co][c][2ta+dy-1][2tb+dx-1] (0 outside the 7x7 window).
+# K shrinks from 49 taps x 8 padded channels (392, 37 % useful) to 256 (57 % useful), and every
+# 64-wide k-step of the implicit GEMM is 4 adjacent pixels x 16 channels = 128 contiguous bytes
+# (the 8-channel form gathers 16-byte pieces).
+STEM_S2D = os.environ.get("IMGCLS_STEM_S2D", "1") == "1"
+_S2D_INDEX: dict = {}
+
+
+def stem_s2d_eligible(x, conv) -> bool:
+    return (STEM_S2D and x.dim() == 4 and x.shape[1] == 3 and x.dtype == torch.float32
+            and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0 and conv.groups == 1 and conv.bias is None
+            and tuple(conv.kernel_size) == (7, 7) and tuple(conv.stride) == (2, 2)
+            and tuple(conv.padding) == (3, 3) and tuple(conv.dilation) == (1, 1)
+            and not getattr(conv, "tf_same", False))
+
+
+def _s2d_index(dev):
+    """KRSC position r*21 + s*3 + c of the 7x7x3 weight -> position in the 4x4x16 s2d weight."""
+    idx = _S2D_INDEX.get(dev)
+    if idx is None:
+        pos = []
+        for r in range(7):
+            for c_ in range(7):
+                for ch in range(3):
+                    ta, dy = divmod(r + 1, 2)
+                    tb, dx = divmod(c_ + 1, 2)
+                    pos.append(ta * 64 + tb * 16 + (dy * 2 + dx) * 3 + ch)
+        idx = _S2D_INDEX[dev] = torch.tensor(pos, dtype=torch.long, device=dev)
+    return idx
+
+
+def _s2d_geom(n, h, w, co) -> ConvGeom:
+    g = ConvGeom.__new__(ConvGeom)
+    g.N, g.Ci, g.Cx, g.H, g.W, g.Co = n, 16, 16, h // 2, w // 2, co
+    g.kh = g.kw = 4
+    g.sh = g.sw = g.dil = 1
+    g.pt, g.pb, g.pl, g.pr = 2, 1, 2, 1
+    g.OH, g.OW, g.T = h // 2, w // 2, 16
+    return g
+
+
+class StemS2dFn(torch.autograd.Function):
+    """The ResNet stem conv on the space-to-depth input (the image itself needs no gradient)."""
+
+    @staticmethod
+    def forward(ctx, x, w, conv, want_stats):
+        n, _, h, wd = x.shape
+        co = w.shape[0]
+        xs = _empty_cl(n, 16, h // 2, wd // 2, x.device)
+        C.prepare_input_s2d(x.contiguous(), xs, n, h, wd)
+        g = _s2d_geom(n, h, wd, co)
+        idx = _s2d_index(x.device)
+        wq = torch.zeros(co, 256, dtype=BF16, device=x.device)
+        wq[:, idx] = weight_bf16(w).view(co, 147)
+        stats = ws(x.device).stats_buf(co, stat_groups(g.N * g.OH * g.OW)) if want_stats else None
+        y = conv_forward_raw(xs, None, g, stats=stats, wb=wq.view(-1))
+        ctx.g = g
+        ctx.save_for_backward(xs, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xs, w = ctx.saved_tensors
+        g = ctx.g
+        dy = _cl(dy)
+        dw = None
+        if ctx.needs_input_grad[1]:
+            m, ntot = g.N * g.OH * g.OW, g.T * g.Cx
+            tiles = (-(-g.Co // (64 if g.Co <= 64 else 128))) * (-(-ntot // 128))
+            target, stages = _wgrad_config(dy, xs, g, m, ntot, tiles)
+            kps, splits = _wgrad_split(m, tiles, target)
+            full = torch.zeros(g.Co * ntot, dtype=torch.float32, device=dy.device)
+            _wgrad_launch(dy, xs, full, g, m, ntot, kps, splits, stages)
+            dw = grad_buffer(w, zero=False)
+            dw.permute(0, 2, 3, 1).reshape(g.Co, 147).copy_(full.view(g.Co, ntot)[:, _s2d_index(dy.device)])
+        return None, dw, None, None
 
 
 # ---------------------------------------------------------------------------
@@ -736,6 +854,14 @@ class BNActFn(torch.autograd.Function):
 def conv_bn_act(x, conv, bn, act, residual, x_slot=None, res_slot=None, exclusive_input=False):
     """``exclusive_input``: this conv is the only consumer of ``x`` (lets its dgrad fuse the BN-backward
     reduce of x's producer); a slot-paired consumer qualifies automatically."""
+    if stem_s2d_eligible(x, conv) and residual is None and not x.requires_grad:
+        ensure_channels_last_weight(conv)
+        y = StemS2dFn.apply(x, conv.weight, conv, bn.training)
+        link = BwdLink() if (FUSE_BN_BWD and bn.training and torch.is_grad_enabled()) else None
+        out = BNActFn.apply(y, bn.weight, bn.bias, None, bn, act, bn.training, None, link)
+        if link is not None:
+            out._imgcls_link = link
+        return out
     x = _cl(x)
     if residual is not None:
         residual = _cl(residual)
@@ -1000,8 +1126,12 @@ def cross_entropy(logits, labels, weight=None):
 _AFFINE_CACHE: dict = {}
 
 
-def prepare_input(x, scale=None, shift=None):
-    """fp32 NCHW batch -> bf16 NHWC padded to a multiple of 8 channels (one kernel)."""
+def prepare_input(x, scale=None, shift=None, stem=None):
+    """fp32 NCHW batch -> bf16 NHWC padded to a multiple of 8 channels (one kernel).  With ``stem``
+    (the first conv) eligible for the space-to-depth form, the fp32 batch is returned unchanged: the
+    stem converts it itself (``StemS2dFn``)."""
+    if stem is not None and scale is None and stem_s2d_eligible(x, stem):
+        return x
     if x.dtype == BF16 and x.is_contiguous(memory_format=CL) and x.shape[1] % 8 == 0:
         return x
     x = x.contiguous().float()

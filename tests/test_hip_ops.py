@@ -77,6 +77,53 @@ def test_conv_fwd_bwd(case):
     assert rel_err(conv.weight.grad, wr.grad) < 2e-2
 
 
+N_CFG_MAX = 24  # >= len(hip.conv_cfgs()); indices past the table skip
+
+
+@pytest.mark.parametrize("cfg", range(N_CFG_MAX))
+@pytest.mark.parametrize("case", [CONV_CASES[1], CONV_CASES[2], CONV_CASES[3], CONV_CASES[6], CONV_CASES[7],
+                                  CONV_CASES[10], CONV_CASES[12]])
+def test_conv_tile_configs(case, cfg):
+    """Every entry of the kernel configuration table the per-shape tuner can pick (tile rows x
+    channels, wave layout, ring depth) matches the fp32 reference (fwd, dgrad phases)."""
+    hip = _hip()
+    if cfg >= len(hip.conv_cfgs()):
+        pytest.skip("past the configuration table")
+    keep, hip.CONV_FORCE_CFG = hip.CONV_FORCE_CFG, (0, 0, cfg)
+    try:
+        test_conv_fwd_bwd(case)
+    finally:
+        hip.CONV_FORCE_CFG = keep
+
+
+@pytest.mark.parametrize("stages", [1, 2, 3])
+@pytest.mark.parametrize("case", [CONV_CASES[0], CONV_CASES[1], CONV_CASES[4], CONV_CASES[6], CONV_CASES[7],
+                                  CONV_CASES[8], CONV_CASES[12]])
+def test_conv_wgrad_ring_variants(case, stages):
+    """Weight-gradient kernel variants: 1-stage (occupancy), 2-stage ring, and the 8-wave in-block
+    2-way pixel split (stages=3) - each over the tuner's split counts."""
+    hip = _hip()
+    keep, hip.WGRAD_STAGES = hip.WGRAD_STAGES, stages
+    try:
+        test_conv_fwd_bwd(case)
+    finally:
+        hip.WGRAD_STAGES = keep
+
+
+@pytest.mark.parametrize("cfg", range(N_CFG_MAX))
+@pytest.mark.parametrize("act,use_res", [("relu", True), ("silu", False)])
+def test_conv_bn_act_tile_configs(act, use_res, cfg):
+    """Fused epilogues (BN statistics, residual) on every configuration of the table."""
+    hip = _hip()
+    if cfg >= len(hip.conv_cfgs()):
+        pytest.skip("past the configuration table")
+    keep, hip.CONV_FORCE_CFG = hip.CONV_FORCE_CFG, (0, 0, cfg)
+    try:
+        test_conv_bn_act(act, use_res)
+    finally:
+        hip.CONV_FORCE_CFG = keep
+
+
 @pytest.mark.parametrize("variant,single", [(1, 1), (2, 0), (2, 1000), (3, 1)])
 @pytest.mark.parametrize("case", [CONV_CASES[1], CONV_CASES[3], CONV_CASES[7], CONV_CASES[10], CONV_CASES[12]])
 def test_conv_kernel_variants(case, variant, single):
@@ -116,6 +163,37 @@ def test_stem_padded_input():
     y.backward(g.to(torch.bfloat16).contiguous(memory_format=CL))
     wr = torch.autograd.grad(F.conv2d(x, conv.weight, None, 2, 3), conv.weight, g)[0]
     assert rel_err(conv.weight.grad, wr) < 2e-2
+
+
+@pytest.mark.parametrize("hw", [(64, 64), (224, 224), (36, 50)])
+def test_stem_space_to_depth(hw):
+    """7x7 stride-2 stem on the space-to-depth input (4x4 stride-1 conv over 16 channels): forward
+    (conv -> BN -> ReLU), BN statistics and the weight gradient against fp32 torch."""
+    hip = _hip()
+    torch.manual_seed(5)
+    h, w = hw
+    conv = nn.Conv2d(3, 64, 7, 2, 3, bias=False).to(DEV).to(memory_format=CL)
+    bn = nn.BatchNorm2d(64).to(DEV)
+    with torch.no_grad():
+        conv.weight.copy_(bf(conv.weight))
+    conv_r = nn.Conv2d(3, 64, 7, 2, 3, bias=False).to(DEV)
+    bn_r = nn.BatchNorm2d(64).to(DEV)
+    conv_r.load_state_dict(conv.state_dict())
+    bn_r.load_state_dict(bn.state_dict())
+    x = bf(torch.randn(2, 3, h, w, device=DEV))
+    assert hip.stem_s2d_eligible(x, conv)
+    assert hip.prepare_input(x, stem=conv) is x
+    out = hip.conv_bn_act(x, conv, bn, "relu", None)
+    yc = conv_r(x)
+    ref = F.relu(bn_r(yc + (bf(yc) - yc).detach()))
+    assert out.shape == ref.shape
+    assert rel_err(out, ref) < 2e-2
+    assert torch.allclose(bn.running_mean, bn_r.running_mean, rtol=1e-2, atol=1e-3)
+    g = bf(torch.randn_like(ref))
+    out.backward(g.to(torch.bfloat16).contiguous(memory_format=CL))
+    ref.backward(g)
+    assert rel_err(conv.weight.grad, conv_r.weight.grad) < 3e-2
+    assert rel_err(bn.weight.grad, bn_r.weight.grad) < 3e-2
 
 
 @pytest.mark.parametrize("act,use_res", [("relu", False), ("relu", True), (None, False), ("silu", False)])
