@@ -44,7 +44,7 @@ def _torch_flags():
     cflags += [f"-I{p}" for p in inc]
     ldflags = [f"-L{p}" for p in libs] + [f"-Wl,-rpath,{p}" for p in libs]
     ldflags += ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
-                "-lamdhip64"]
+                "-lamdhip64", "-lz"]
     return cflags, ldflags
 
 

@@ -51,6 +51,7 @@ int adam_launch(const void*, const void*, int, const float*, float, float, float
 int adam_tick_launch(float*, float, hipStream_t);
 int prepare_input_launch(const float*, bf16_t*, int, int, int, int, const float*, const float*, hipStream_t);
 int prepare_input_s2d_launch(const float*, bf16_t*, int, int, int, hipStream_t);
+int normalize_u8_launch(const uint8_t*, float*, long, int, const float*, const float*, hipStream_t);
 int cast_bf16_launch(const float*, bf16_t*, long, hipStream_t);
 int weight_pad_launch(const bf16_t*, bf16_t*, long, int, int, hipStream_t);
 int weight_t_launch(const bf16_t*, bf16_t*, int, int, int, hipStream_t);
@@ -326,6 +327,20 @@ void adam(Tensor table, Tensor chunks, int nchunks, Tensor lr_step, double b1, d
 
 void adam_tick(Tensor lr_step, double lr) { check(adam_tick_launch(ptr<float>(lr_step), (float)lr, cur()), "adam_tick"); }
 
+void normalize_u8(Tensor x, Tensor y, std::vector<double> mean, std::vector<double> std_) {
+  req(x, at::kByte, "x"); req(y, F32, "y");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) == 3 && x.is_contiguous(), "normalize_u8: x is contiguous uint8 [N,H,W,3]");
+  TORCH_CHECK(y.dim() == 4 && y.size(1) == 3 && y.size(0) == x.size(0) && y.size(2) == x.size(1) &&
+                  y.size(3) == x.size(2) && y.is_contiguous(),
+              "normalize_u8: y is contiguous fp32 [N,3,H,W]");
+  TORCH_CHECK(mean.size() == 3 && std_.size() == 3, "normalize_u8: 3 means and 3 stds");
+  const float m[3] = {(float)mean[0], (float)mean[1], (float)mean[2]};
+  const float sd[3] = {(float)std_[0], (float)std_[1], (float)std_[2]};
+  check(normalize_u8_launch(x.data_ptr<uint8_t>(), ptr<float>(y), (long)x.size(0) * x.size(1) * x.size(2),
+                            (int)(x.size(1) * x.size(2)), m, sd, cur()),
+        "normalize_u8");
+}
+
 void prepare_input_s2d(Tensor x, Tensor y, int N, int H, int W) {
   req(x, F32, "x"); req(y, BF, "y");
   TORCH_CHECK(x.is_contiguous() && x.numel() == (int64_t)N * 3 * H * W && H % 2 == 0 && W % 2 == 0,
@@ -461,6 +476,8 @@ void bn_stats(Tensor y, long rows, int C, Tensor part, int G) {
 
 }  // namespace
 
+void register_loader(pybind11::module& m);  // loader.cpp: native image-folder loader
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "gfx950 (MI355X) HIP kernels for pytorch_imageclassification_distributed_amd";
   m.def("conv_gemm", &conv_gemm);
@@ -500,6 +517,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("weight_t_job_bytes", &weight_t_job_bytes);
   m.def("prepare_input", &prepare_input);
   m.def("prepare_input_s2d", &prepare_input_s2d);
+  m.def("normalize_u8", &normalize_u8);
+  register_loader(m);
   m.def("conv_cfgs", []() {
     std::vector<std::vector<int>> out;
     for (int i = 0; i < conv_num_cfgs(); ++i) {

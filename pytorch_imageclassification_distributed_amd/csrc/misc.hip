@@ -68,6 +68,19 @@ __global__ void prepare_input_s2d_kernel(const float* __restrict__ x, bf16_t* __
   }
 }
 
+// uint8 NHWC RGB batch (native loader) -> fp32 NCHW ((x / 255 - mean[c]) / std[c]), K25
+__global__ void normalize_u8_kernel(const uint8_t* __restrict__ x, float* __restrict__ y, long npix, int hw,
+                                    float m0, float m1, float m2, float s0, float s1, float s2) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < npix; i += (long)gridDim.x * blockDim.x) {
+    const long n = i / hw, p = i - n * hw;
+    const uint8_t* px = x + i * 3;
+    float* o = y + n * 3 * (long)hw + p;
+    o[0] = ((float)px[0] / 255.f - m0) / s0;
+    o[hw] = ((float)px[1] / 255.f - m1) / s1;
+    o[2 * (long)hw] = ((float)px[2] / 255.f - m2) / s2;
+  }
+}
+
 __global__ void cast_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long n) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
     y[i] = f2bf(x[i]);
@@ -197,6 +210,14 @@ __global__ void scale_rows_kernel(const bf16_t* __restrict__ x, const float* __r
 }
 
 }  // namespace
+
+int normalize_u8_launch(const uint8_t* x, float* y, long npix, int hw, const float* mean, const float* std_,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(normalize_u8_kernel, dim3(grid_for(npix)), dim3(256), 0, s, x, y, npix, hw, mean[0], mean[1],
+                     mean[2], std_[0], std_[1], std_[2]);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
 
 int prepare_input_s2d_launch(const float* x, bf16_t* y, int N, int H, int W, hipStream_t s) {
   hipLaunchKernelGGL(prepare_input_s2d_kernel, dim3(grid_for((long)N * (H / 2) * (W / 2))), dim3(256), 0, s, x, y,

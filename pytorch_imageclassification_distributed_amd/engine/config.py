@@ -32,6 +32,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--class-weights", default="auto",
                    help="comma list, 'auto' (reference weights if 7 classes else uniform) or 'none'")
     p.add_argument("--num-workers", type=int, default=6)
+    p.add_argument("--loader", default="auto", choices=["auto", "native", "python"],
+                   help="image-folder loading: native C++ threads (PNG), the Python DataLoader, or auto")
     p.add_argument("--val-batchsize", type=int, default=1)
     p.add_argument("--aux-weight", type=float, default=0.4)
     p.add_argument("--ckpt-dir", default="dtmodel/cp")

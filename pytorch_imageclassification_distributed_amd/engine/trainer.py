@@ -33,7 +33,7 @@ import torch.nn as nn
 from torch.utils.data import DataLoader
 from torch.utils.data.distributed import DistributedSampler
 
-from ..data import CudaPrefetcher, ImageDataset, SyntheticImageDataset
+from ..data import CudaPrefetcher, ImageDataset, NativeFolderLoader, SyntheticImageDataset, use_native
 from ..models import DEFAULT_IMAGE_SIZE, Classifier
 from ..ops import functional as Fx
 from ..ops.grad_arena import GradArena
@@ -87,12 +87,23 @@ class Trainer:
         pin = self.dev.type == "cuda"
         self.train_sampler = DistributedSampler(self.train_ds, num_replicas=self.ctx.world_size,
                                                 rank=self.ctx.rank, seed=a.seed)
+        self.val_sampler = DistributedSampler(self.val_ds, num_replicas=self.ctx.world_size,
+                                              rank=self.ctx.rank, seed=a.seed)
+        mode = getattr(a, "loader", "auto")
+        if mode == "native" and not (use_native(self.train_ds) and use_native(self.val_ds)):
+            raise SystemExit("--loader native needs PNG image folders and the built extension")
+        if mode == "native" or (mode == "auto" and use_native(self.train_ds) and use_native(self.val_ds)):
+            # C++ decode/augment threads -> pinned uint8 ring -> GPU normalisation (data/native.py)
+            workers = max(a.num_workers, 1)
+            self.train_loader = NativeFolderLoader(self.train_ds, self.train_sampler, a.batchsize, self.dev,
+                                                   workers=workers, seed=a.seed)
+            self.val_loader = NativeFolderLoader(self.val_ds, self.val_sampler, a.val_batchsize, self.dev,
+                                                 workers=workers, seed=a.seed)
+            return
         self.train_loader = DataLoader(self.train_ds, batch_size=a.batchsize, shuffle=False,
                                        num_workers=a.num_workers, pin_memory=pin,
                                        sampler=self.train_sampler, drop_last=False,
                                        persistent_workers=a.num_workers > 0)
-        self.val_sampler = DistributedSampler(self.val_ds, num_replicas=self.ctx.world_size,
-                                              rank=self.ctx.rank, seed=a.seed)
         self.val_loader = DataLoader(self.val_ds, batch_size=a.val_batchsize, shuffle=False,
                                      num_workers=a.num_workers, pin_memory=pin, sampler=self.val_sampler)
 
@@ -213,6 +224,8 @@ class Trainer:
 
     # ------------------------------------------------------------------ epochs
     def _loader(self, loader):
+        if isinstance(loader, NativeFolderLoader):  # copies + normalises on its own stream
+            return loader
         return CudaPrefetcher(loader, self.dev) if self.dev.type == "cuda" else loader
 
     def train_epoch(self, epoch: int):
