@@ -66,7 +66,7 @@ def main():
     # decode + resize + augment into the pinned uint8 ring only (the C++ worker threads)
     labels = [ds.mapping[f.replace("\\", "/").split("/")[-2]] for f in ds.image_files]
     from pytorch_imageclassification_distributed_amd import _ext
-    core = _ext.load().NativeLoader(ds.image_files, labels, a.size, a.batch, a.workers, True, 0, 4, False)
+    core = _ext.load().NativeLoader(ds.image_files, labels, a.size, a.batch, a.workers, True, 0, 4, False, False)
     for rep in range(2):
         core.start_epoch(list(range(len(ds))), rep, False)
         t0, n = time.perf_counter(), 0

@@ -8,7 +8,8 @@
 //   train fold: rot90(k ~ U{0..3}), vertical flip p=.5, horizontal flip p=.5, then the cascaded
 //   photometric jitter (saturation p=.05, else brightness p=.05, else contrast p=.05, factor
 //   U[0.9, 1.1], PIL ImageEnhance blend + clip + truncation to uint8).
-// The x/255 and ImageNet mean/std normalisation happen on the device (normalize_u8 kernel).
+// The x/255 and ImageNet mean/std normalisation happen on the device (normalize_u8 kernel), or in
+// the worker threads for CPU training (float_out).
 //
 // Replaces the reference's torch DataLoader worker processes (train.py:112-118): no pickling of
 // samples between processes, 4x fewer bytes per sample on the host->device link (uint8 instead
@@ -235,16 +236,21 @@ bool read_file(const std::string& path, std::vector<uint8_t>& buf) {
 // ----------------------------------------------------------------------------- loader
 class NativeLoader {
  public:
+  // float_out: slots hold the normalised fp32 [B,3,S,S] batch (CPU training: the worker threads do
+  // the x/255 - mean / std pass too); otherwise uint8 [B,S,S,3] for the GPU to normalise.
   NativeLoader(std::vector<std::string> files, std::vector<int64_t> labels, int size, int batch, int workers,
-               bool augment, int64_t seed, int ring, bool pin)
+               bool augment, int64_t seed, int ring, bool pin, bool float_out, std::vector<double> mean,
+               std::vector<double> stdv)
       : files_(std::move(files)), labels_(std::move(labels)), S_(size), B_(batch), aug_(augment),
-        seed_((uint64_t)seed), R_(std::max(ring, 2)) {
+        seed_((uint64_t)seed), R_(std::max(ring, 2)), float_out_(float_out) {
     TORCH_CHECK(files_.size() == labels_.size(), "NativeLoader: files/labels size mismatch");
     TORCH_CHECK(S_ > 0 && B_ > 0 && workers > 0, "NativeLoader: size, batch and workers must be positive");
-    auto u8 = at::TensorOptions().dtype(at::kByte).pinned_memory(pin);
+    TORCH_CHECK(mean.size() == 3 && stdv.size() == 3, "NativeLoader: 3 means and 3 stds");
+    for (int c = 0; c < 3; ++c) { mean_[c] = (float)mean[c]; std_[c] = (float)stdv[c]; }
+    auto img = at::TensorOptions().dtype(float_out ? at::kFloat : at::kByte).pinned_memory(pin);
     auto i64 = at::TensorOptions().dtype(at::kLong).pinned_memory(pin);
     for (int s = 0; s < R_; ++s) {
-      images_.push_back(at::empty({B_, S_, S_, 3}, u8));
+      images_.push_back(float_out ? at::empty({B_, 3, S_, S_}, img) : at::empty({B_, S_, S_, 3}, img));
       labs_.push_back(at::empty({B_}, i64));
     }
     done_.assign(R_, 0);
@@ -321,7 +327,7 @@ class NativeLoader {
   int batch_len(int64_t b) const { return (int)std::min<int64_t>(B_, total_ - b * B_); }
 
   void work() {
-    std::vector<uint8_t> file;
+    std::vector<uint8_t> file, u8;
     Image im;
     for (;;) {
       int64_t j, gen;
@@ -348,7 +354,16 @@ class NativeLoader {
       if (err.empty()) {
         Rng rng{seed_ * 0x9E3779B97F4A7C15ull ^ ((uint64_t)epoch_ << 32) ^ (uint64_t)idx};
         rng.next();
-        preprocess(im, S_, aug_, rng, images_[slot].data_ptr<uint8_t>() + (size_t)pos * S_ * S_ * 3);
+        const size_t npx = (size_t)S_ * S_;
+        if (float_out_) {
+          u8.resize(npx * 3);
+          preprocess(im, S_, aug_, rng, u8.data());
+          float* o = images_[slot].data_ptr<float>() + (size_t)pos * 3 * npx;
+          for (int c = 0; c < 3; ++c)  // numpy float32: (x / 255 - mean) / std  (dp/loader.py:86-91)
+            for (size_t p = 0; p < npx; ++p) o[c * npx + p] = ((float)u8[p * 3 + c] / 255.f - mean_[c]) / std_[c];
+        } else {
+          preprocess(im, S_, aug_, rng, images_[slot].data_ptr<uint8_t>() + (size_t)pos * npx * 3);
+        }
         labs_[slot].data_ptr<int64_t>()[pos] = labels_[idx];
       }
       {
@@ -369,6 +384,8 @@ class NativeLoader {
   const bool aug_;
   const uint64_t seed_;
   const int R_;
+  const bool float_out_;
+  float mean_[3], std_[3];
   std::vector<Tensor> images_, labs_;
   std::vector<int64_t> order_;
   std::vector<int> done_;
@@ -411,9 +428,12 @@ py::object decode_png_rgb(const std::string& path) {
 
 void register_loader(py::module& m) {
   py::class_<NativeLoader>(m, "NativeLoader")
-      .def(py::init<std::vector<std::string>, std::vector<int64_t>, int, int, int, bool, int64_t, int, bool>(),
+      .def(py::init<std::vector<std::string>, std::vector<int64_t>, int, int, int, bool, int64_t, int, bool, bool,
+                    std::vector<double>, std::vector<double>>(),
            py::arg("files"), py::arg("labels"), py::arg("size"), py::arg("batch"), py::arg("workers"),
-           py::arg("augment"), py::arg("seed"), py::arg("ring"), py::arg("pin"))
+           py::arg("augment"), py::arg("seed"), py::arg("ring"), py::arg("pin"), py::arg("float_out") = false,
+           py::arg("mean") = std::vector<double>{0.485, 0.456, 0.406},
+           py::arg("std") = std::vector<double>{0.229, 0.224, 0.225})
       .def("start_epoch", &NativeLoader::start_epoch, py::arg("order"), py::arg("epoch"), py::arg("drop_last"),
            py::call_guard<py::gil_scoped_release>())
       .def("next", &NativeLoader::next)

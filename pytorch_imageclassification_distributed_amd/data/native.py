@@ -15,7 +15,7 @@ Python side:
 * hands a slot back to the C++ workers once the copy that reads it has completed.
 
 Batches are dicts ``{'image': fp32 [n,3,S,S], 'label': int64 [n]}`` on the target device (CPU: the
-same math in torch ops).  PNG only (the reference reads PNG files, ``image_id`` strips ``.png``);
+worker threads write the normalised fp32 batch themselves).  PNG only (the reference reads PNG files, ``image_id`` strips ``.png``);
 ``use_native()`` tells whether a dataset qualifies.
 """
 from __future__ import annotations
@@ -52,7 +52,8 @@ class NativeFolderLoader:
         labels = [dataset.mapping[f.replace("\\", "/").split("/")[-2]] for f in dataset.image_files]
         cuda = self.device.type == "cuda"
         self.core = C.NativeLoader(list(dataset.image_files), labels, dataset.resize_size, batch_size,
-                                   max(int(workers), 1), bool(aug), int(seed), int(ring), cuda)
+                                   max(int(workers), 1), bool(aug), int(seed), int(ring), cuda, not cuda,
+                                   list(IMAGENET_MEAN), list(IMAGENET_STD))
         self.C = C
         self.stream = torch.cuda.Stream(device=self.device) if cuda else None
         self.epoch = 0
@@ -81,20 +82,16 @@ class NativeFolderLoader:
             self._pending.popleft()
 
     def _to_device(self, slot, img_u8, labels):
-        n, s = img_u8.shape[0], img_u8.shape[1]
-        if self.stream is None:
-            x = img_u8.permute(0, 3, 1, 2).float().div_(255.0)
-            mean = torch.tensor(IMAGENET_MEAN, dtype=torch.float32).view(1, 3, 1, 1)
-            std = torch.tensor(IMAGENET_STD, dtype=torch.float32).view(1, 3, 1, 1)
-            x = ((x - mean) / std).contiguous()
+        if self.stream is None:  # CPU: the worker threads already wrote the normalised fp32 batch
             self._pending.append((slot, None))
-            return {"image": x, "label": labels.clone()}
+            return {"image": img_u8.clone(), "label": labels.clone()}
         cur = torch.cuda.current_stream(self.device)
         with torch.cuda.stream(self.stream):
             u8 = img_u8.to(self.device, non_blocking=True)
             lab = labels.to(self.device, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(self.stream)
+            n, s = img_u8.shape[0], img_u8.shape[1]
             x = torch.empty((n, 3, s, s), dtype=torch.float32, device=self.device)
             self.C.normalize_u8(u8, x, list(IMAGENET_MEAN), list(IMAGENET_STD))
         cur.wait_stream(self.stream)
