@@ -587,3 +587,4 @@ def test_bn_apply_emits_mx_copy():
         hip.set_fp8(False)
     assert torch.equal(qs, qs2)
     assert torch.equal(q.view(torch.uint8), q2.view(torch.uint8))
+
