@@ -171,7 +171,8 @@ void conv_wgrad(Tensor dY, Tensor X, Tensor dW, int M, int Cout, int Cin, int Nt
   p.stride_h = sh; p.stride_w = sw; p.pad_t = pt; p.pad_l = pl; p.dil_h = dh; p.dil_w = dwd; p.KW = KW;
   p.k_per_split = k_per_split;
   p.zero = ptr<bf16_t>(zero);
-  TORCH_CHECK(stages >= 0 && stages <= 3, "conv_wgrad: stages must be 0, 1, 2 or 3 (2-stage, 8 waves)");
+  TORCH_CHECK(stages >= 0 && stages <= 4, "conv_wgrad: stages must be 0..4");
+  TORCH_CHECK(stages != 4 || Cout >= 256, "conv_wgrad: the 256x256 tile needs Cout >= 256");
   p.stages = stages;
   check(conv_wgrad_launch(p, splits, cur()), "conv_wgrad");
 }

@@ -62,7 +62,7 @@ struct WgradParams {
   int OH, OW, IH, IW, stride_h, stride_w, pad_t, pad_l, dil_h, dil_w, KW;
   int k_per_split;     // pixels (GEMM K) per split, multiple of 64
   const bf16_t* zero;  // >= 16 zero bytes (LDS-DMA source of padded chunks)
-  int stages;          // LDS-DMA ring depth: 1 (3 blocks/CU) or 2 (0 = 2)
+  int stages;          // 1 | 2: ring depth (4 waves); 3: 8 waves, in-block pixel split; 4: 256x256 tile, 8 waves
 };
 
 int conv_gemm_launch(const ConvParams& p, hipStream_t stream);

@@ -853,44 +853,52 @@ DEVI int wswz(int row) {  // XOR mask on the 32-B block index
   return ROWB == 256 ? (row & 7) : ((row >> 1) & 3);
 }
 
-// KG wave groups of 4 split every k-step's pixels (KG = 2: a 128-pixel stage, 8 waves, the two
-// groups' partial tiles summed through LDS before the atomics): at one block per CU this halves the
-// atomic bytes per unit of work (atomics run at ~1.3 TB/s chip-wide, a real cost at high split counts).
-template <int WBM, int STAGES, int KG>
+// Tile WBM (output channels) x TN (tap*Cin columns), WM x WN waves per k-group; KG wave groups
+// split every k-step's pixels (KG = 2: a 128-pixel stage, the groups' partial tiles summed through
+// LDS before the atomics).  Split-K partial tiles leave through fp32 atomics (~1.3 TB/s chip-wide):
+// the atomic bytes of a launch are blocks x tile bytes, so the 256 x 256 tile at one block per CU
+// moves fewer of them than many small-tile blocks while running the more efficient 8-wave loop.
+template <int WBM, int TN, int WM, int WN, int KG, int STAGES>
 struct WgCfg {
-  static constexpr int NTH = 256 * KG;
-  static constexpr int AROWB = WBM * 2, BROWB = WBN * 2;
+  static constexpr int NW = WM * WN * KG, NTH = 64 * NW;
+  static constexpr int AROWB = WBM * 2, BROWB = TN * 2;
   static constexpr int STAGE = WBK * KG * (AROWB + BROWB);
-  static constexpr int LDT = WBN + 4;
-  static constexpr int EPI = (KG == 2 ? WBM : WBM / 2) * LDT * 4;
+  static constexpr int LDT = TN + 4;
+  static constexpr int EPI = (KG == 2 ? WBM : WBM / WM) * LDT * 4;  // staged fp32 rows
   static constexpr int MAIN = STAGES * STAGE > EPI ? STAGES * STAGE : EPI;
-  static constexpr int OCC = KG == 2 ? 2 : (STAGES == 1 ? 3 : 2);
+  static constexpr int BLOCKS = (160 * 1024) / MAIN;
+  static constexpr int OCC0 = BLOCKS * NW / 4 < 1 ? 1 : (BLOCKS * NW / 4 > 3 ? 3 : BLOCKS * NW / 4);
+  static constexpr int ACC = (WBM / WM) * (TN / WN) / 64;
+  static constexpr int OCC = ACC >= 128 ? (OCC0 < 2 ? OCC0 : 2) : OCC0;
 };
 
-template <int WBM, int STAGES, int KG>
-__global__ __launch_bounds__((WgCfg<WBM, STAGES, KG>::NTH), (WgCfg<WBM, STAGES, KG>::OCC))
+template <int WBM, int TN, int WM, int WN, int KG, int STAGES>
+__global__ __launch_bounds__((WgCfg<WBM, TN, WM, WN, KG, STAGES>::NTH), (WgCfg<WBM, TN, WM, WN, KG, STAGES>::OCC))
 void conv_wgrad_glds_kernel(const WgradParams p) {
-  using Cfg = WgCfg<WBM, STAGES, KG>;
+  using Cfg = WgCfg<WBM, TN, WM, WN, KG, STAGES>;
+  constexpr int NW = Cfg::NW;
   constexpr int NTH = Cfg::NTH;
-  constexpr int AROWB = Cfg::AROWB;         // A image row bytes (128 / 256)
-  constexpr int BROWB = Cfg::BROWB;         // 256
+  constexpr int AROWB = Cfg::AROWB;         // A image row bytes (128 / 256 / 512)
+  constexpr int BROWB = Cfg::BROWB;         // 256 / 512
   constexpr int KPS = WBK * KG;             // pixels per stage
   constexpr int A_BYTES = KPS * AROWB;
   constexpr int STAGE = Cfg::STAGE;
-  constexpr int WTM = WBM / 2, WTN = WBN / 2;
+  constexpr int WTM = WBM / WM, WTN = TN / WN;
   constexpr int RM = WTM / 16, RN = WTN / 16;
-  constexpr int ARPI = 1024 / AROWB;        // rows per LDS-DMA instruction (8 / 4)
-  constexpr int AL = WBK / ARPI / 4;        // instructions per wave per stage (2 / 4)
-  constexpr int BRPI = 1024 / BROWB;        // 4
-  constexpr int BL = WBK / BRPI / 4;        // 4
+  constexpr int ARPI = 1024 / AROWB;        // rows per LDS-DMA instruction (8 / 4 / 2)
+  constexpr int AL = KPS / ARPI / NW;       // instructions per wave per stage
+  constexpr int BRPI = 1024 / BROWB;        // 4 / 2
+  constexpr int BL = KPS / BRPI / NW;
   constexpr int LDT = Cfg::LDT;             // floats per staged epilogue row
   constexpr int MAIN = Cfg::MAIN;
+  static_assert(AL >= 1 && BL >= 1 && AL * ARPI * NW == KPS && BL * BRPI * NW == KPS, "loader mapping");
+  static_assert(MAIN <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) char smem[MAIN];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = wid >> 2, lw = wid & 3;   // wave group (k half) and wave within the group
-  const int wm = lw >> 1, wn = lw & 1;
+  const int grp = wid / (WM * WN), lw = wid % (WM * WN);  // k group and wave within the group
+  const int wm = lw / WN, wn = lw % WN;
   const int gm = (p.Cout + WBM - 1) / WBM;
   // XCD-aware order: the tiles of one pixel slice (which all read the same dY rows and overlapping X
   // rows) are consecutive logical ids, and consecutive logical ids share an XCD (and its L2)
@@ -898,7 +906,7 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
   const int lin = xcd_remap(blockIdx.y * ntile + blockIdx.x, ntile * gridDim.y);
   const int split = lin / ntile, tile = lin - split * ntile;
   const int bm = tile % gm, bn = tile / gm;
-  const int co0 = bm * WBM, j0 = bn * WBN;
+  const int co0 = bm * WBM, j0 = bn * TN;
   const int kbeg = split * p.k_per_split;
   const int kend = min(p.M, kbeg + p.k_per_split);
   const int ohw = p.OH * p.OW;
@@ -916,7 +924,7 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
     a_cok[i] = a_col[i] < p.Cout;
   }
   // B (X gather): per instruction the logical column -> (tap, ci) is fixed over k-steps
-  const int b_lr = lane >> 4, b_pc = lane & 15;
+  const int b_lr = lane / (BROWB / 16), b_pc = lane % (BROWB / 16);
   int b_ci[BL], b_dh[BL], b_dw[BL];
   bool b_cok[BL];
 #pragma unroll
@@ -967,7 +975,6 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
   const int nk = (kend - kbeg + KPS - 1) / KPS;
   if (nk <= 0) return;
   if (STAGES >= 2) issue(kbeg, 0);
-  if (STAGES >= 3 && nk > 1) issue(kbeg + KPS, 1);
   const int g = lane >> 4, li = lane & 15;
   const int tq = li >> 2, tp = li & 3;
   for (int kt = 0; kt < nk; ++kt) {
@@ -977,12 +984,11 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
       wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
     } else {
-      if (kt + STAGES - 2 < nk) wait_vmcnt<(STAGES - 2) * (AL + BL)>();
-      else wait_vmcnt<0>();
+      wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
-      if (kt + STAGES - 1 < nk) issue(kbeg + (kt + STAGES - 1) * KPS, (kt + STAGES - 1) % STAGES);
+      if (kt + 1 < nk) issue(kbeg + (kt + 1) * KPS, (kt + 1) & 1);
     }
-    const char* sa = smem + (kt % STAGES) * STAGE;
+    const char* sa = smem + (STAGES == 1 ? 0 : (kt & 1) * STAGE);
     const char* sb = sa + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -1016,7 +1022,7 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
   // with atomics whose wave-instructions each cover 256 contiguous bytes.
   float* st = (float*)smem;
   if constexpr (KG == 2) {
-    // group 1 parks its partial tile, group 0 adds its own, then all 512 threads issue the atomics
+    // group 1 parks its partial tile, group 0 adds its own, then all threads issue the atomics
     __syncthreads();
     if (grp == 1) {
 #pragma unroll
@@ -1037,17 +1043,17 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
     }
     __syncthreads();
 #pragma unroll 4
-    for (int e = tid; e < WBM * WBN; e += NTH) {  // consecutive lanes -> consecutive floats
-      const int row = e / WBN, c = e - row * WBN;
+    for (int e = tid; e < WBM * TN; e += NTH) {  // consecutive lanes -> consecutive floats
+      const int row = e / TN, c = e - row * TN;
       const int co = co0 + row, col = j0 + c;
       if (co < p.Cout && col < p.Ntot) atomicAdd(p.dW + (long)co * p.Ntot + col, st[row * LDT + c]);
     }
   } else {
-    // fp32 tile staged in row halves of WTM rows
+    // fp32 tile staged in WM parts of WTM rows
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
+    for (int part = 0; part < WM; ++part) {
       __syncthreads();
-      if (wm == half) {
+      if (wm == part) {
 #pragma unroll
         for (int i = 0; i < RM; ++i)
 #pragma unroll
@@ -1056,9 +1062,9 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
       }
       __syncthreads();
 #pragma unroll 4
-      for (int e = tid; e < WTM * WBN; e += NTH) {  // consecutive lanes -> consecutive floats
-        const int row = e / WBN, c = e - row * WBN;
-        const int co = co0 + half * WTM + row, col = j0 + c;
+      for (int e = tid; e < WTM * TN; e += NTH) {  // consecutive lanes -> consecutive floats
+        const int row = e / TN, c = e - row * TN;
+        const int co = co0 + part * WTM + row, col = j0 + c;
         if (co < p.Cout && col < p.Ntot) atomicAdd(p.dW + (long)co * p.Ntot + col, st[row * LDT + c]);
       }
     }
@@ -1146,23 +1152,34 @@ int conv_gemm_launch(const ConvParams& p, hipStream_t stream) {
 static int g_wvariant = 0;
 void conv_set_wgrad_variant(int v) { g_wvariant = v; }
 
+template <int WBM, int TN, int WM, int WN, int KG, int ST>
+static void launch_wg(const WgradParams& p, int splits, hipStream_t stream) {
+  const dim3 grid(cdiv(p.Cout, WBM) * cdiv(p.Ntot, TN), splits);
+  hipLaunchKernelGGL((conv_wgrad_glds_kernel<WBM, TN, WM, WN, KG, ST>), grid, dim3(64 * WM * WN * KG), 0, stream, p);
+}
+
+int conv_wgrad_tile_n(int stages) { return stages == 4 ? 256 : WBN; }
+
 int conv_wgrad_launch(const WgradParams& p, int splits, hipStream_t stream) {
   if (p.M <= 0) return 0;
-  const int gn = cdiv(p.Ntot, WBN);
   const bool dma = g_wvariant != 1;
-  // stages: 1 | 2 (4 waves), 3 = 2-stage ring with the in-block 2-way pixel split (8 waves)
-  if (p.Cout <= 64) {
-    const dim3 grid(cdiv(p.Cout, 64) * gn, splits);
-    if (dma && p.stages == 1) hipLaunchKernelGGL((conv_wgrad_glds_kernel<64, 1, 1>), grid, dim3(256), 0, stream, p);
-    else if (dma && p.stages == 3) hipLaunchKernelGGL((conv_wgrad_glds_kernel<64, 2, 2>), grid, dim3(512), 0, stream, p);
-    else if (dma) hipLaunchKernelGGL((conv_wgrad_glds_kernel<64, 2, 1>), grid, dim3(256), 0, stream, p);
-    else hipLaunchKernelGGL(conv_wgrad_kernel<64>, grid, dim3(NT), 0, stream, p);
+  // stages: 1 | 2 (4 waves, 64/128 x 128 tile), 3 = 2-stage ring with the in-block 2-way pixel split
+  // (8 waves), 4 = 256 x 256 tile on 8 waves (2-stage ring, one block per CU; Cout >= 256 only)
+  if (dma && p.stages == 4) {
+    if (p.Cout < 256) return 2;
+    launch_wg<256, 256, 2, 4, 1, 2>(p, splits, stream);
+  } else if (p.Cout <= 64) {
+    if (dma && p.stages == 1) launch_wg<64, 128, 2, 2, 1, 1>(p, splits, stream);
+    else if (dma && p.stages == 3) launch_wg<64, 128, 2, 2, 2, 2>(p, splits, stream);
+    else if (dma) launch_wg<64, 128, 2, 2, 1, 2>(p, splits, stream);
+    else hipLaunchKernelGGL(conv_wgrad_kernel<64>, dim3(cdiv(p.Cout, 64) * cdiv(p.Ntot, WBN), splits), dim3(NT), 0,
+                            stream, p);
   } else {
-    const dim3 grid(cdiv(p.Cout, 128) * gn, splits);
-    if (dma && p.stages == 1) hipLaunchKernelGGL((conv_wgrad_glds_kernel<128, 1, 1>), grid, dim3(256), 0, stream, p);
-    else if (dma && p.stages == 3) hipLaunchKernelGGL((conv_wgrad_glds_kernel<128, 2, 2>), grid, dim3(512), 0, stream, p);
-    else if (dma) hipLaunchKernelGGL((conv_wgrad_glds_kernel<128, 2, 1>), grid, dim3(256), 0, stream, p);
-    else hipLaunchKernelGGL(conv_wgrad_kernel<128>, grid, dim3(NT), 0, stream, p);
+    if (dma && p.stages == 1) launch_wg<128, 128, 2, 2, 1, 1>(p, splits, stream);
+    else if (dma && p.stages == 3) launch_wg<128, 128, 2, 2, 2, 2>(p, splits, stream);
+    else if (dma) launch_wg<128, 128, 2, 2, 1, 2>(p, splits, stream);
+    else hipLaunchKernelGGL(conv_wgrad_kernel<128>, dim3(cdiv(p.Cout, 128) * cdiv(p.Ntot, WBN), splits), dim3(NT),
+                            0, stream, p);
   }
   HIP_CHECK_LAUNCH();
   return 0;

@@ -509,7 +509,21 @@ def _wgrad_launch(dy, x, out, g: ConvGeom, m, ntot, kps, splits, stages=2):
                  g.dil, g.dil, g.kw, kps, splits, ws(dy.device).zero, stages)
 
 
-def _wgrad_config(dy, x, g: ConvGeom, m, ntot, tiles):
+def _wgrad_tiles(co, ntot, stages):
+    """Output tiles of one wgrad launch: 256 x 256 for the 8-wave kernel (stages 4), else 64|128 x 128."""
+    if stages == 4:
+        return (-(-co // 256)) * (-(-ntot // 256))
+    return (-(-co // (64 if co <= 64 else 128))) * (-(-ntot // 128))
+
+
+def _wgrad_plan(g: ConvGeom, dy, x, m, ntot):
+    """(k_per_split, splits, stages) of the weight-gradient launch for this geometry."""
+    target, stages = _wgrad_config(dy, x, g, m, ntot)
+    kps, splits = _wgrad_split(m, _wgrad_tiles(g.Co, ntot, stages), target)
+    return kps, splits, stages
+
+
+def _wgrad_config(dy, x, g: ConvGeom, m, ntot):
     """(split-K block target, LDS ring depth): fixed by IMGCLS_WGRAD_BLOCKS / IMGCLS_WGRAD_STAGES,
     else timed jointly once per shape (cached).
 
@@ -533,8 +547,10 @@ def _wgrad_config(dy, x, g: ConvGeom, m, ntot, tiles):
     if WGRAD_STAGES == 0:
         # 8-wave blocks (in-block 2-way pixel split, one block per CU): fewer, larger blocks
         cands += [(cand, 3) for cand in blocks if cand <= 1024]
+        if g.Co >= 256 and ntot >= 256:  # 256 x 256 tiles on 8 waves, ~1-2 blocks per CU
+            cands += [(cand, 4) for cand in (256, 512)]
     for cand, st in cands:
-        kps, splits = _wgrad_split(m, tiles, cand)
+        kps, splits = _wgrad_split(m, _wgrad_tiles(g.Co, ntot, st), cand)
         times[(cand, st)] = _time_ms(lambda: _wgrad_launch(dy, x, scratch, g, m, ntot, kps, splits, st))
     best = min(times, key=times.get)
     _WGRAD_TUNED[key] = best
@@ -545,9 +561,7 @@ def conv_wgrad_raw(dy, x, w_param, g: ConvGeom):
     dev = dy.device
     m = g.N * g.OH * g.OW
     ntot = g.T * g.Cx
-    tiles = (-(-g.Co // (64 if g.Co <= 64 else 128))) * (-(-ntot // 128))
-    target, stages = _wgrad_config(dy, x, g, m, ntot, tiles)
-    kps, splits = _wgrad_split(m, tiles, target)
+    kps, splits, stages = _wgrad_plan(g, dy, x, m, ntot)
     if g.Cx == g.Ci:
         dw = grad_buffer(w_param)
         _wgrad_launch(dy, x, dw, g, m, ntot, kps, splits, stages)
@@ -714,9 +728,7 @@ class StemS2dFn(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             m, ntot = g.N * g.OH * g.OW, g.T * g.Cx
-            tiles = (-(-g.Co // (64 if g.Co <= 64 else 128))) * (-(-ntot // 128))
-            target, stages = _wgrad_config(dy, xs, g, m, ntot, tiles)
-            kps, splits = _wgrad_split(m, tiles, target)
+            kps, splits, stages = _wgrad_plan(g, dy, xs, m, ntot)
             full = torch.zeros(g.Co * ntot, dtype=torch.float32, device=dy.device)
             _wgrad_launch(dy, xs, full, g, m, ntot, kps, splits, stages)
             dw = grad_buffer(w, zero=False)

@@ -1,0 +1,88 @@
+"""Per-GEMM roofline of the convolutions in one ResNet-50 training step.
+
+Every implicit-GEMM launch of a steady-state step (forward, data-gradient phases, weight-gradient) is
+timed with HIP events around it (synchronising, so the numbers are per-launch, not overlapped), and
+compared with its roofline time max(FLOP / PEAK_TF, bytes / PEAK_BW).  Sorted by time lost to the
+roofline: the top rows are where kernel work pays most.
+
+    python scripts/conv_roofline.py [batch=256] [peak_tf=2300] [peak_tbps=6.0]
+"""
+import collections
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from pytorch_imageclassification_distributed_amd.data import DeviceSyntheticLoader
+from pytorch_imageclassification_distributed_amd.engine import Trainer, build_parser
+from pytorch_imageclassification_distributed_amd.ops import hip
+from pytorch_imageclassification_distributed_amd.parallel import init_distributed
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+PEAK_TF = float(sys.argv[2]) if len(sys.argv) > 2 else 2300.0
+PEAK_BW = float(sys.argv[3]) if len(sys.argv) > 3 else 6.0
+REC = []
+ON = [False]
+
+_orig_gemm, _orig_wg = hip._conv_gemm, hip._wgrad_launch
+
+
+def _timed(kind, fn, flop, nbytes, desc):
+    if not ON[0]:
+        return fn()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    a.record()
+    r = fn()
+    b.record()
+    b.synchronize()
+    REC.append((kind, desc, a.elapsed_time(b) * 1e3, flop, nbytes))
+    return r
+
+
+def gemm(A, B_, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(None,) * 4 + (0, 1), **kw):
+    m, n, k = geo[0], geo[1], geo[2]
+    kind = "dgrad" if (bwd[0] is not None or addend is not None or geo[12] > 1 or geo[13] or geo[14]) else "fwd"
+    nb = 2 * (A.numel() + B_.numel() + m * n) + (2 * m * n if addend is not None else 0) + \
+        (4 * m * n if bwd[0] is not None else 0)
+    return _timed(kind, lambda: _orig_gemm(A, B_, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, **kw),
+                  2.0 * m * n * k, nb, f"M={m} N={n} K={k} CA={geo[3]}")
+
+
+def wgrad(dy, x, out, g, m, ntot, kps, splits, stages=2):
+    nb = 2 * (dy.numel() + x.numel()) + 4 * out.numel() * splits
+    return _timed("wgrad", lambda: _orig_wg(dy, x, out, g, m, ntot, kps, splits, stages), 2.0 * m * g.Co * ntot, nb,
+                  f"Co={g.Co} Ntot={ntot} Mpix={m} splits={splits} st={stages}")
+
+
+hip._conv_gemm, hip._wgrad_launch = gemm, wgrad
+
+ctx = init_distributed(device="cuda")
+targs = build_parser().parse_args(["--synthetic", "--model", "resnet50", "--batchsize", str(B), "--num-classes", "7",
+                                   "--num-workers", "0", "--synthetic-train-size", "8", "--synthetic-val-size", "8",
+                                   "--no-sync-bn", "--lr", "1e-4"])
+tr = Trainer(targs, ctx)
+tr.net.train()
+batches = list(iter(DeviceSyntheticLoader(B, 7, 224, ctx.device, steps=2, ring=2, seed=1)))
+for i in range(4):
+    tr.train_step(batches[i % 2]["image"], batches[i % 2]["label"])
+torch.cuda.synchronize()
+ON[0] = True
+tr.train_step(batches[0]["image"], batches[0]["label"])
+ON[0] = False
+torch.cuda.synchronize()
+
+tot = collections.defaultdict(lambda: [0.0, 0.0])
+rows = []
+for kind, desc, us, flop, nb in REC:
+    roof = max(flop / (PEAK_TF * 1e12), nb / (PEAK_BW * 1e12)) * 1e6
+    rows.append((us - roof, kind, desc, us, roof, flop / us / 1e6, nb / us / 1e6))
+    tot[kind][0] += us
+    tot[kind][1] += roof
+print(f"batch {B}: {len(REC)} conv GEMM launches; roofline at {PEAK_TF:.0f} TF/s, {PEAK_BW:.1f} TB/s")
+for k, (t, r) in tot.items():
+    print(f"  {k:6s} {t / 1e3:7.3f} ms measured  {r / 1e3:7.3f} ms roofline")
+print(f"{'lost_us':>8} {'kind':6} {'us':>8} {'roof_us':>8} {'TF/s':>6} {'TB/s':>5}  shape")
+for lost, kind, desc, us, roof, tf, tb in sorted(rows, reverse=True)[:45]:
+    print(f"{lost:8.1f} {kind:6} {us:8.1f} {roof:8.1f} {tf:6.0f} {tb:5.2f}  {desc}")

@@ -96,13 +96,16 @@ def test_conv_tile_configs(case, cfg):
         hip.CONV_FORCE_CFG = keep
 
 
-@pytest.mark.parametrize("stages", [1, 2, 3])
-@pytest.mark.parametrize("case", [CONV_CASES[0], CONV_CASES[1], CONV_CASES[4], CONV_CASES[6], CONV_CASES[7],
-                                  CONV_CASES[8], CONV_CASES[12]])
+@pytest.mark.parametrize("stages", [1, 2, 3, 4])
+@pytest.mark.parametrize("case", [CONV_CASES[0], CONV_CASES[1], CONV_CASES[4], CONV_CASES[5], CONV_CASES[6],
+                                  CONV_CASES[7], CONV_CASES[8], CONV_CASES[12]])
 def test_conv_wgrad_ring_variants(case, stages):
-    """Weight-gradient kernel variants: 1-stage (occupancy), 2-stage ring, and the 8-wave in-block
-    2-way pixel split (stages=3) - each over the tuner's split counts."""
+    """Weight-gradient kernel variants: 1-stage (occupancy), 2-stage ring, the 8-wave in-block
+    2-way pixel split (stages=3) and the 256x256 8-wave tile (stages=4, Cout >= 256) - each over the
+    tuner's split counts."""
     hip = _hip()
+    if stages == 4 and case[4] < 256:
+        pytest.skip("256x256 wgrad tile needs Cout >= 256")
     keep, hip.WGRAD_STAGES = hip.WGRAD_STAGES, stages
     try:
         test_conv_fwd_bwd(case)
