@@ -940,25 +940,45 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
     b_dw[i] = c * p.dil_w - p.pad_l;
   }
 
-  auto issue = [&](int k0, int buf) {
+  // Address state advanced incrementally by one stage (KPS pixels) per issue - the gather's pixel ->
+  // (image, row, column) decomposition is done once per block, not per k-step (it dominated the
+  // kernel's VALU work: ~200 instructions per k-step per wave with per-step divisions and 64-bit math).
+  // All offsets are 32-bit element offsets (operands < 2^31 elements, checked on the host).
+  const int adv_q = KPS / p.OW, adv_r = KPS - adv_q * p.OW;  // KPS pixels = adv_q rows + adv_r columns
+  int a_m[AL];
+#pragma unroll
+  for (int i = 0; i < AL; ++i) a_m[i] = kbeg + (wid * AL + i) * ARPI + a_lr;
+  int b_m[BL], b_n[BL], b_oh[BL], b_ow[BL];
+#pragma unroll
+  for (int i = 0; i < BL; ++i) {
+    b_m[i] = kbeg + (wid * BL + i) * BRPI + b_lr;
+    int rem;
+    b_n[i] = fdiv(b_m[i], ohw, inv_ohw, rem);
+    b_oh[i] = fdiv(rem, p.OW, inv_ow, b_ow[i]);
+  }
+  const int img = p.IH * p.IW;
+
+  auto issue = [&](int buf) {
     char* sa = smem + buf * STAGE;
     char* sb = sa + A_BYTES;
     const bf16_t* srca[AL];
     const bf16_t* srcb[BL];
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
-      const int m = k0 + (wid * AL + i) * ARPI + a_lr;
-      srca[i] = (a_cok[i] && m < kend) ? p.dY + (long)m * p.Cout + a_col[i] : p.zero;
+      srca[i] = (a_cok[i] && a_m[i] < kend) ? p.dY + (a_m[i] * p.Cout + a_col[i]) : p.zero;
+      a_m[i] += KPS;
     }
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
-      const int m = k0 + (wid * BL + i) * BRPI + b_lr;
-      int rem, ow;
-      const int n = fdiv(m, ohw, inv_ohw, rem);
-      const int oh = fdiv(rem, p.OW, inv_ow, ow);
-      const int ih = oh * p.stride_h + b_dh[i], iw = ow * p.stride_w + b_dw[i];
-      const bool ok = b_cok[i] && m < kend && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
-      srcb[i] = ok ? p.X + (((long)n * p.IH + ih) * p.IW + iw) * p.Cin + b_ci[i] : p.zero;
+      const int ih = b_oh[i] * p.stride_h + b_dh[i], iw = b_ow[i] * p.stride_w + b_dw[i];
+      const bool ok = b_cok[i] && b_m[i] < kend && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+      srcb[i] = ok ? p.X + ((b_n[i] * img + ih * p.IW + iw) * p.Cin + b_ci[i]) : p.zero;
+      // advance by KPS pixels: adv_q output rows + adv_r columns, carrying into rows and images
+      b_m[i] += KPS;
+      b_ow[i] += adv_r;
+      b_oh[i] += adv_q;
+      if (b_ow[i] >= p.OW) { b_ow[i] -= p.OW; ++b_oh[i]; }
+      while (b_oh[i] >= p.OH) { b_oh[i] -= p.OH; ++b_n[i]; }
     }
 #pragma unroll
     for (int i = 0; i < AL; ++i) glds16(srca[i], sa + (wid * AL + i) * 1024);
@@ -974,19 +994,19 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
 
   const int nk = (kend - kbeg + KPS - 1) / KPS;
   if (nk <= 0) return;
-  if (STAGES >= 2) issue(kbeg, 0);
+  if (STAGES >= 2) issue(0);
   const int g = lane >> 4, li = lane & 15;
   const int tq = li >> 2, tp = li & 3;
   for (int kt = 0; kt < nk; ++kt) {
     if constexpr (STAGES == 1) {  // latency hidden by co-resident blocks instead of the ring
       if (kt > 0) __builtin_amdgcn_s_barrier();
-      issue(kbeg + kt * KPS, 0);
+      issue(0);
       wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
     } else {
       wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
-      if (kt + 1 < nk) issue(kbeg + (kt + 1) * KPS, (kt + 1) & 1);
+      if (kt + 1 < nk) issue((kt + 1) & 1);
     }
     const char* sa = smem + (STAGES == 1 ? 0 : (kt & 1) * STAGE);
     const char* sb = sa + A_BYTES;
