@@ -418,6 +418,17 @@ void conv_gemm_glds_kernel(const ConvParams p) {
     const int n = n0 + row;
     b_off[i] = n < p.Ncols ? n * p.ldb : -1;
   }
+  // non-uniform k-steps (CA not a multiple of 64: the stem's 8 / 16 channels, EfficientNet's 24, 40,
+  // 80, 112 ...): each lane's (tap, channel) of its chunk advanced incrementally per k-step - one
+  // step = adv_q taps + adv_r channels - instead of a division by CA per chunk per k-step
+  const int adv_q = BK / p.CA, adv_r = BK - adv_q * p.CA;
+  int a_tap[TAP_UNIFORM ? 1 : AL], a_ci[TAP_UNIFORM ? 1 : AL], b_tap[TAP_UNIFORM ? 1 : BL], b_ci[TAP_UNIFORM ? 1 : BL];
+  if constexpr (!TAP_UNIFORM) {
+#pragma unroll
+    for (int i = 0; i < AL; ++i) { a_tap[i] = (a_ch[i] * 8) / p.CA; a_ci[i] = a_ch[i] * 8 - a_tap[i] * p.CA; }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) { b_tap[i] = (b_ch[i] * 8) / p.CA; b_ci[i] = b_ch[i] * 8 - b_tap[i] * p.CA; }
+  }
   __syncthreads();
 
   // all addresses (incl. the LDS tap-table reads) are formed before the first LDS-DMA of
@@ -442,21 +453,25 @@ void conv_gemm_glds_kernel(const ConvParams p) {
       for (int i = 0; i < BL; ++i)
         srcb[i] = b_off[i] >= 0 ? p.B + b_off[i] + tb * p.CA + ci0 + b_ch[i] * 8 : p.zero;
     } else {
+      // called for kt = 0, 1, 2, ... in order: (tap, ci) of every chunk advance one k-step per call
 #pragma unroll
       for (int i = 0; i < AL; ++i) {
-        const int k = kt * BK + a_ch[i] * 8;
-        const int tap = k < p.K ? k / p.CA : 0;
-        const int ci = k - tap * p.CA;
+        const bool kin = a_tap[i] < p.ntaps;
+        const int tap = kin ? a_tap[i] : 0;
         const int ih = a_ih[i] + s_dh[tap], iw = a_iw[i] + s_dw[tap];
-        const bool ok = k < p.K && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
-        srca[i] = ok ? p.A + a_base[i] + (ih * p.IW + iw) * p.CA + ci : p.zero;
+        const bool ok = kin && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
+        srca[i] = ok ? p.A + a_base[i] + (ih * p.IW + iw) * p.CA + a_ci[i] : p.zero;
+        a_tap[i] += adv_q;
+        a_ci[i] += adv_r;
+        if (a_ci[i] >= p.CA) { a_ci[i] -= p.CA; ++a_tap[i]; }
       }
 #pragma unroll
       for (int i = 0; i < BL; ++i) {
-        const int k = kt * BK + b_ch[i] * 8;
-        const int tap = k < p.K ? k / p.CA : 0;
-        const int ci = k - tap * p.CA;
-        srcb[i] = (k < p.K && b_off[i] >= 0) ? p.B + b_off[i] + s_tb[tap] * p.CA + ci : p.zero;
+        const bool kin = b_tap[i] < p.ntaps;
+        srcb[i] = (kin && b_off[i] >= 0) ? p.B + b_off[i] + s_tb[kin ? b_tap[i] : 0] * p.CA + b_ci[i] : p.zero;
+        b_tap[i] += adv_q;
+        b_ci[i] += adv_r;
+        if (b_ci[i] >= p.CA) { b_ci[i] -= p.CA; ++b_tap[i]; }
       }
     }
 #pragma unroll
