@@ -607,16 +607,34 @@ class GradSlot:
         return grad
 
 
+SYNCBN_EARLY_COUNT = [0]  # SyncBN backward all-reduces launched from the consuming conv (tests)
+
+
+def _syncbn_bwd_start(link):
+    """Reduce the fused partial rows to this rank's [sum dz, sum dz*xhat] (+ dgamma, dbeta) and launch
+    the async cross-rank all-reduce; ``BNActFn.backward`` waits on it (a stream wait, no host sync)."""
+    c = link.c
+    dgamma = grad_buffer(link.params[0], zero=False)
+    dbeta = grad_buffer(link.params[1], zero=False)
+    sums = torch.empty(2 * c, dtype=torch.float64, device=link.y.device)
+    C.bn_partials(link.part, stat_groups(link.rows), c, sums, dgamma, dbeta)
+    work = dist.all_reduce(sums, group=link.group, async_op=True)
+    link.pending = (sums, work, dgamma, dbeta)
+    SYNCBN_EARLY_COUNT[0] += 1
+
+
 class BwdLink:
     """Ties a BN(+act) output to the conv that consumes it, so the consumer's dgrad epilogue can run
     the producer's BN-backward reduce (``done`` tells the producer its gradient arrives as dz)."""
 
-    __slots__ = ("y", "coef", "res", "act", "part", "done")
+    __slots__ = ("y", "coef", "res", "act", "part", "done", "group", "params", "pending", "c", "rows")
 
     def __init__(self):
         self.y = self.coef = self.res = self.part = None
         self.act = 0
         self.done = False
+        self.group = self.params = self.pending = None  # SyncBN: early backward all-reduce
+        self.c = self.rows = 0
 
 
 class ConvFn(torch.autograd.Function):
@@ -649,6 +667,10 @@ class ConvFn(torch.autograd.Function):
             dx = conv_dgrad_raw(dy, w, g, addend=addend, link=link)
             if link is not None:
                 link.done = True
+                if link.group is not None:
+                    # SyncBN: start the producer BN's backward all-reduce now, so its latency overlaps
+                    # this conv's weight gradient instead of sitting between two dependent kernels
+                    _syncbn_bwd_start(link)
             if slot is not None:
                 dx = slot.deliver(dx, fused=addend is not None)
         dw = conv_wgrad_raw(dy, x, w, g) if ctx.needs_input_grad[1] else None
@@ -815,6 +837,7 @@ class BNActFn(torch.autograd.Function):
         ctx.link = None
         if link is not None and bn.training:  # (grad mode is always off inside forward)
             link.y, link.coef, link.res, link.act = y, coef, res, a
+            link.group, link.params, link.c, link.rows = group, (gamma, beta), c, rows
             ctx.link = link
         ctx.has_res = res is not None
         ctx.params = (gamma, beta)
@@ -830,21 +853,29 @@ class BNActFn(torch.autograd.Function):
         g = _cl(gout)
         link = ctx.link
         grp = stat_groups(rows)
+        pending = None
         if link is not None and link.done:
             # the consuming conv's dgrad epilogue already produced dz and the partial sums
             part, dz = link.part, g
             FUSED_BWD_COUNT[0] += 1
-            link.y = link.coef = link.res = link.part = None
+            pending = link.pending
+            link.y = link.coef = link.res = link.part = link.pending = link.params = None
         else:
             part = ws(dev).stats_buf(c, grp)
             dz = torch.empty_like(y, memory_format=CL) if ctx.has_res else None
             C.bn_bwd_reduce(g, y, coef, res, dz, rows, c, ctx.act, part, grp)
-        dgamma = grad_buffer(ctx.params[0], zero=False)
-        dbeta = grad_buffer(ctx.params[1], zero=False)
         k = torch.empty(2 * c, dtype=torch.float32, device=dev)
-        if ctx.training and ctx.group is None:  # one launch: partial rows -> dgamma, dbeta, k
+        if pending is not None:  # SyncBN all-reduce launched early by the consuming conv's backward
+            sums, work, dgamma, dbeta = pending
+            work.wait()
+            C.bn_bwd_k(sums, ctx.count_t, float(rows), c, k)
+        elif ctx.training and ctx.group is None:  # one launch: partial rows -> dgamma, dbeta, k
+            dgamma = grad_buffer(ctx.params[0], zero=False)
+            dbeta = grad_buffer(ctx.params[1], zero=False)
             C.bn_reduce_bwd(part, grp, c, float(rows), dgamma, dbeta, k)
         else:
+            dgamma = grad_buffer(ctx.params[0], zero=False)
+            dbeta = grad_buffer(ctx.params[1], zero=False)
             sums = torch.empty(2 * c, dtype=torch.float64, device=dev)
             C.bn_partials(part, grp, c, sums, dgamma, dbeta)
             if ctx.group is not None:

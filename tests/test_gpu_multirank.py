@@ -20,7 +20,7 @@ def _port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, name="resnet18"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     import torch.nn.functional as F
@@ -36,14 +36,17 @@ def _worker(rank, world, port, out_dir):
 
     def model():
         torch.manual_seed(1)
-        return Classifier("resnet18", 7).to(dev).to(memory_format=torch.channels_last)
+        return Classifier(name, 7).to(dev).to(memory_format=torch.channels_last)
 
     m = model()
     convert_sync_batchnorm(m)
     red = GradReducer(m, bucket_cap_mb=4, first_bucket_mb=1)
     xs, ys = x[rank * 8:(rank + 1) * 8], y[rank * 8:(rank + 1) * 8]
+    from pytorch_imageclassification_distributed_amd.ops import hip
+    early0 = hip.SYNCBN_EARLY_COUNT[0]
     Fx.cross_entropy(m(xs), ys).backward()
     scale = red.finish()
+    assert hip.SYNCBN_EARLY_COUNT[0] > early0  # fused links started their SyncBN all-reduce early
     grads = {n: (p.grad * scale).float().cpu() for n, p in m.named_parameters()}
     rm = m.encoder.bn1.running_mean.cpu()
     if rank == 0:
@@ -56,5 +59,8 @@ def _worker(rank, world, port, out_dir):
     destroy()
 
 
-def test_two_ranks_one_gpu_matches_full_batch(tmp_path):
-    mp.spawn(_worker, args=(2, _port(), str(tmp_path)), nprocs=2, join=True)
+@pytest.mark.parametrize("name", ["resnet18", "resnet50"])
+def test_two_ranks_one_gpu_matches_full_batch(tmp_path, name):
+    """ResNet-18 (BasicBlock) and ResNet-50 (Bottleneck: fused BN-backward links whose SyncBN
+    all-reduce is launched early by the consuming conv, residual gradient slots)."""
+    mp.spawn(_worker, args=(2, _port(), str(tmp_path), name), nprocs=2, join=True)
