@@ -136,8 +136,7 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
   TORCH_CHECK(stages >= 0 && stages <= 3, "conv_gemm: stages must be 0 (auto), 1, 2 or 3");
   p.stages = stages;
   TORCH_CHECK(tile_n == 0 || tile_n == 64 || tile_n == 128, "conv_gemm: tile_n must be 0, 64 or 128");
-  TORCH_CHECK(cfg >= -1 && cfg < conv_num_cfgs(), "conv_gemm: cfg out of range");
-  TORCH_CHECK(cfg < 0 || !fp8, "conv_gemm: the configuration table is bf16-only");
+  TORCH_CHECK(cfg >= -1 && cfg < (fp8 ? conv_num_fp8_cfgs() : conv_num_cfgs()), "conv_gemm: cfg out of range");
   p.tile_n = tile_n;
   p.cfg = cfg;
   if (fp8) {
@@ -522,6 +521,15 @@ PYBIND11_MODULE(_C, m) {
   m.def("prepare_input_s2d", &prepare_input_s2d);
   m.def("normalize_u8", &normalize_u8);
   register_loader(m);
+  m.def("conv_fp8_cfgs", []() {
+    std::vector<std::vector<int>> out;
+    for (int i = 0; i < conv_num_fp8_cfgs(); ++i) {
+      std::vector<int> c(5);
+      conv_fp8_cfg_info(i, c.data());
+      out.push_back(c);
+    }
+    return out;
+  });
   m.def("conv_cfgs", []() {
     std::vector<std::vector<int>> out;
     for (int i = 0; i < conv_num_cfgs(); ++i) {

@@ -47,7 +47,7 @@ struct ConvParams {
   const uint8_t* a_sc;
   const uint8_t* b_sc;
   int tile_n;  // output-channel tile: 64 or 128; 0 = 64 iff Ncols <= 64 (heuristic / fp8 path)
-  int cfg;     // bf16: index into the tuned configuration table (conv_cfg_info), -1 = stages/tile_n
+  int cfg;     // index into the tuned configuration table (conv_cfg_info; MX-FP8: conv_fp8_cfg_info), -1 = stages/tile_n
   int tap_dh[CONV_MAX_TAPS];
   int tap_dw[CONV_MAX_TAPS];
   int tap_b[CONV_MAX_TAPS];
@@ -69,6 +69,8 @@ int conv_gemm_launch(const ConvParams& p, hipStream_t stream);
 void conv_set_variant(int v);  // 0 = auto, 1 = register-staged, 2 = LDS-DMA 2-stage, 3 = LDS-DMA 3-stage
 void conv_set_single_stage(int nk);  // GEMMs with K <= nk*64 use the 1-stage (high-occupancy) ring
 int conv_num_cfgs();
+int conv_num_fp8_cfgs();
+void conv_fp8_cfg_info(int i, int* out5);
 void conv_cfg_info(int i, int* out5);  // {tile rows, tile channels, waves M, waves N, ring depth}
 int conv_wgrad_launch(const WgradParams& p, int splits, hipStream_t stream);
 void conv_set_wgrad_variant(int v);  // 0 = auto, 1 = register-staged, 2 = LDS-DMA

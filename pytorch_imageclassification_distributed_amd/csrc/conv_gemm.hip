@@ -542,19 +542,38 @@ DEVI void glds4(const void* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 4, 0, 0);
 }
 
-template <int BN, int STAGES>
-__global__ __launch_bounds__(NT, STAGES == 1 ? (BN == 128 ? 3 : 4) : 1) void conv_fp8_kernel(const ConvParams p) {
-  constexpr int A_BYTES = BM * 128;
+template <int TM, int BN, int WM, int WN, int STAGES>
+struct Fp8Cfg {
+  static constexpr int NW = WM * WN, NTH = 64 * NW;
+  static constexpr int STAGE = TM * 128 + BN * 128 + NW * 256;
+  static constexpr int EPI = TM * (BN + 8) * 2;
+  static constexpr int MAIN = STAGES * STAGE > EPI ? STAGES * STAGE : EPI;
+  static constexpr int BLOCKS = (160 * 1024) / (MAIN + 3 * CONV_MAX_TAPS * 4);
+  static constexpr int OCC_LDS = BLOCKS * NW / 4 < 1 ? 1 : (BLOCKS * NW / 4 > 4 ? 4 : BLOCKS * NW / 4);
+  static constexpr int OCC = (TM / WM) * (BN / WN) >= 8192 ? (OCC_LDS < 2 ? OCC_LDS : 2)
+                                                           : (OCC_LDS < 3 ? OCC_LDS : 3);
+};
+
+// TM x BN tile on WM x WN waves.  Scale rows: waves [0, TM/64) fetch the activation rows' 4 scale
+// bytes, the next BN/64 waves the weight rows', the rest fetch a zero page into a spare slot (every
+// wave issues the same LDS-DMA count per stage, so the counted vmcnt waits stay uniform).
+template <int TM, int BN, int WM, int WN, int STAGES>
+__global__ __launch_bounds__((Fp8Cfg<TM, BN, WM, WN, STAGES>::NTH), (Fp8Cfg<TM, BN, WM, WN, STAGES>::OCC))
+void conv_fp8_kernel(const ConvParams p) {
+  using Cfg = Fp8Cfg<TM, BN, WM, WN, STAGES>;
+  constexpr int NW = Cfg::NW;
+  constexpr int A_BYTES = TM * 128;
   constexpr int B_BYTES = BN * 128;
-  constexpr int S_BYTES = 2 * 128 * 4;  // activation + weight scale rows (128 rows each, 4 B per row)
-  constexpr int STAGE = A_BYTES + B_BYTES + S_BYTES;
-  constexpr int WTM = BM / 2, WTN = BN / 2;
+  constexpr int STAGE = Cfg::STAGE;
+  constexpr int WTM = TM / WM, WTN = BN / WN;
   constexpr int RM = WTM / 16, RN = WTN / 16;
-  constexpr int AL = BM / 32, BL = BN / 32;
+  constexpr int AL = TM / 8 / NW, BL = BN / 8 / NW;
   constexpr int LPS = AL + BL + 1;  // LDS-DMA instructions per wave per stage
   constexpr int TAP_BYTES = 3 * CONV_MAX_TAPS * 4;
-  constexpr int CST = BN + 8;
-  constexpr int MAIN = STAGES * STAGE > BM * CST * 2 ? STAGES * STAGE : BM * CST * 2;
+  constexpr int MAIN = Cfg::MAIN;
+  static_assert(AL >= 1 && BL >= 1 && AL * 8 * NW == TM && BL * 8 * NW == BN, "loader mapping");
+  static_assert(TM / 64 + BN / 64 <= NW, "one scale-row LDS-DMA per wave");
+  static_assert(MAIN + TAP_BYTES <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) char smem[MAIN + TAP_BYTES];
   int* s_dh = (int*)(smem + MAIN);
   int* s_dw = s_dh + CONV_MAX_TAPS;
@@ -564,11 +583,11 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? (BN == 128 ? 3 : 4) : 1) void con
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid >> 1, wn = wid & 1;
-  const int gm = (p.M + BM - 1) / BM, gn = (p.Ncols + BN - 1) / BN;
+  const int wm = wid / WN, wn = wid % WN;
+  const int gm = (p.M + TM - 1) / TM, gn = (p.Ncols + BN - 1) / BN;
   const int lin = xcd_remap(blockIdx.x, gm * gn);
   const int bm = lin / gn, bn = lin - bm * gn;
-  const int m0 = bm * BM, n0 = bn * BN;
+  const int m0 = bm * TM, n0 = bn * BN;
   if (tid < p.ntaps) {
     s_dh[tid] = p.tap_dh[tid];
     s_dw[tid] = p.tap_dw[tid];
@@ -580,7 +599,7 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? (BN == 128 ? 3 : 4) : 1) void con
   int a_base[AL], a_ih[AL], a_iw[AL], a_ch[AL];
 #pragma unroll
   for (int i = 0; i < AL; ++i) {
-    const int row = wid * (BM / 4) + i * 8 + lrow;
+    const int row = wid * (TM / NW) + i * 8 + lrow;
     a_ch[i] = pch ^ ((row >> 1) & 7);
     const int m = m0 + row;
     if (m < p.M) {
@@ -598,14 +617,14 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? (BN == 128 ? 3 : 4) : 1) void con
   int b_off[BL], b_ch[BL];
 #pragma unroll
   for (int i = 0; i < BL; ++i) {
-    const int row = wid * (BN / 4) + i * 8 + lrow;
+    const int row = wid * (BN / NW) + i * 8 + lrow;
     b_ch[i] = pch ^ ((row >> 1) & 7);
     const int n = n0 + row;
     b_off[i] = n < p.Ncols ? n * p.ldb : -1;
   }
   // scale rows: waves 0-1 -> activation rows wid*64 + lane, waves 2-3 -> weight rows (wid-2)*64 + lane
-  const bool s_act = wid < 2;
-  const int srow = (wid & 1) * 64 + lane;
+  const bool s_act = wid < TM / 64;
+  const int srow = (s_act ? wid : wid - TM / 64) * 64 + lane;
   int s_base = 0, s_ih = -(1 << 28), s_iw = 0, s_woff = -1;
   if (s_act) {
     const int m = m0 + srow;
@@ -616,7 +635,7 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? (BN == 128 ? 3 : 4) : 1) void con
       s_ih = gh * p.sA;
       s_iw = gw * p.sA;
     }
-  } else if (srow < BN && n0 + srow < p.Ncols) {
+  } else if (wid < TM / 64 + BN / 64 && n0 + srow < p.Ncols) {
     s_woff = (n0 + srow) * (p.ldb >> 5);
   }
   __syncthreads();
@@ -648,10 +667,10 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? (BN == 128 ? 3 : 4) : 1) void con
       srcs = s_woff >= 0 ? p.b_sc + s_woff + (k0 >> 5) : (const uint8_t*)p.zero;
     }
 #pragma unroll
-    for (int i = 0; i < AL; ++i) glds16(srca[i], sa + (wid * (BM / 4) + i * 8) * 128);
+    for (int i = 0; i < AL; ++i) glds16(srca[i], sa + (wid * (TM / NW) + i * 8) * 128);
 #pragma unroll
-    for (int i = 0; i < BL; ++i) glds16(srcb[i], sb + (wid * (BN / 4) + i * 8) * 128);
-    glds4(srcs, ss + wid * 256);  // [0,512): activation rows x 4 B; [512,1024): weight rows x 4 B
+    for (int i = 0; i < BL; ++i) glds16(srcb[i], sb + (wid * (BN / NW) + i * 8) * 128);
+    glds4(srcs, ss + wid * 256);  // [0, 4*TM): activation rows x 4 B; then weight rows x 4 B; then spare
   };
 
   f32x4 acc[RM][RN];
@@ -696,7 +715,7 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? (BN == 128 ? 3 : 4) : 1) void con
       const int4 lo = *(const int4*)(sb + swz(row, fq));
       const int4 hi = *(const int4*)(sb + swz(row, fq + 4));
       wb[j] = (i32x8){lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-      sw[j] = ss[512 + row * 4 + fq];
+      sw[j] = ss[TM * 4 + row * 4 + fq];
     }
 #pragma unroll
     for (int i = 0; i < RM; ++i)
@@ -706,7 +725,7 @@ __global__ __launch_bounds__(NT, STAGES == 1 ? (BN == 128 ? 3 : 4) : 1) void con
                                                                      sx[i]);
   }
   __syncthreads();
-  conv_epilogue<BM, BN, 2, 2>(p, acc, smem, tid, lane, wid, wm, wn, m0, n0, bm, ghw);
+  conv_epilogue<TM, BN, WM, WN>(p, acc, smem, tid, lane, wid, wm, wn, m0, n0, bm, ghw);
 }
 
 // ---------------------------------------------------------------------------
@@ -1158,11 +1177,32 @@ void conv_cfg_info(int i, int* out5) {
   out5[0] = c.tm; out5[1] = c.bn; out5[2] = c.wm; out5[3] = c.wn; out5[4] = c.st;
 }
 
+template <int TM, int BN, int WM, int WN, int ST>
+static void launch_fp8_cfg(const ConvParams& p, hipStream_t stream) {
+  const int grid = cdiv(p.M, TM) * cdiv(p.Ncols, BN);
+  hipLaunchKernelGGL((conv_fp8_kernel<TM, BN, WM, WN, ST>), dim3(grid), dim3(64 * WM * WN), 0, stream, p);
+}
+
+// MX-FP8 configurations (same role as g_cfgs for bf16)
+#define FCFG(TM, BN, WM, WN, ST) {TM, BN, WM, WN, ST, &launch_fp8_cfg<TM, BN, WM, WN, ST>}
+static const ConvCfg g_fp8_cfgs[] = {
+    FCFG(128, 64, 2, 2, 1), FCFG(128, 128, 2, 2, 1), FCFG(128, 64, 2, 2, 2), FCFG(128, 128, 2, 2, 2),
+    FCFG(256, 256, 2, 4, 2),  // (4 x 2 waves of 64 x 128 spills at 2 waves per SIMD with 8-VGPR fp8 fragments)
+};
+#undef FCFG
+constexpr int kNumFp8Cfgs = sizeof(g_fp8_cfgs) / sizeof(g_fp8_cfgs[0]);
+
+int conv_num_fp8_cfgs() { return kNumFp8Cfgs; }
+void conv_fp8_cfg_info(int i, int* out5) {
+  const ConvCfg& c = g_fp8_cfgs[i];
+  out5[0] = c.tm; out5[1] = c.bn; out5[2] = c.wm; out5[3] = c.wn; out5[4] = c.st;
+}
+
 template <int BN>
 static void launch_fp8(const ConvParams& p, int gm, hipStream_t stream) {
-  const int gn = cdiv(p.Ncols, BN);
-  if (p.stages == 2) hipLaunchKernelGGL((conv_fp8_kernel<BN, 2>), dim3(gm * gn), dim3(NT), 0, stream, p);
-  else hipLaunchKernelGGL((conv_fp8_kernel<BN, 1>), dim3(gm * gn), dim3(NT), 0, stream, p);
+  (void)gm;
+  if (p.stages == 2) launch_fp8_cfg<128, BN, 2, 2, 2>(p, stream);
+  else launch_fp8_cfg<128, BN, 2, 2, 1>(p, stream);
 }
 
 int conv_gemm_launch(const ConvParams& p, hipStream_t stream) {
@@ -1170,7 +1210,10 @@ int conv_gemm_launch(const ConvParams& p, hipStream_t stream) {
   const int gm = cdiv(p.M, BM);
   if (p.a_sc) {
     if (p.CA % 128 || p.K % 128 || !p.b_sc) return 3;
-    if (p.Ncols <= 64 || p.tile_n == 64) launch_fp8<64>(p, gm, stream);
+    if (p.cfg >= 0) {
+      if (p.cfg >= kNumFp8Cfgs) return 3;
+      g_fp8_cfgs[p.cfg].launch(p, stream);
+    } else if (p.Ncols <= 64 || p.tile_n == 64) launch_fp8<64>(p, gm, stream);
     else launch_fp8<128>(p, gm, stream);
     HIP_CHECK_LAUNCH();
     return 0;

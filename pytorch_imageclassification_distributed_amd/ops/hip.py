@@ -363,7 +363,8 @@ def _time_ms(run, reps: int = 3, trials: int = 3) -> float:
 
 CONV_STAGES = os.environ.get("IMGCLS_CONV_STAGES", "auto")  # auto (timed per shape) | 0 (heuristic) | 1 | 2
 _STAGES_TUNED: dict = {}
-CONV_FORCE_CFG = None  # (stages, tile_n, tile_m) for every bf16 fwd/dgrad launch (tests)
+CONV_FORCE_CFG = None  # (stages, tile_n, cfg) for every bf16 fwd/dgrad launch (tests)
+CONV_FORCE_FP8_CFG = None  # (stages, tile_n, cfg) for every MX-FP8 forward launch (tests)
 TUNE_LOG: list = []  # (M, Ncols, K, {cfg: ms}) per tuned geometry (benchmarks/conv_bench.py prints it)
 
 
@@ -375,6 +376,8 @@ def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(
     GEMM geometry by timing the candidates on scratch outputs (a conv-algorithm "find" step)."""
     if CONV_FORCE_CFG is not None and scales[0] is None:
         cfg = CONV_FORCE_CFG
+    elif CONV_FORCE_FP8_CFG is not None and scales[0] is not None:
+        cfg = CONV_FORCE_FP8_CFG
     elif CONV_STAGES != "auto":
         cfg = (int(CONV_STAGES), 0, -1)
     else:
@@ -400,12 +403,21 @@ def conv_cfgs():
     return _CFGS
 
 
+_FP8_CFGS = None
+
+
+def conv_fp8_cfgs():
+    """The MX-FP8 forward kernel's configuration table (same fields as ``conv_cfgs``)."""
+    global _FP8_CFGS
+    if _FP8_CFGS is None:
+        _FP8_CFGS = [tuple(c) for c in C.conv_fp8_cfgs()]
+    return _FP8_CFGS
+
+
 def _conv_candidates(m, ncols, fp8):
     """(stages, tile_n, cfg) triples worth timing for an M x Ncols GEMM."""
-    if fp8:  # the MX-FP8 kernel: 128-row tiles, ring depth x channel tile
-        return [(st, tn, -1) for st in (1, 2) for tn in ((64,) if ncols <= 64 else (64, 128))]
     out = []
-    for i, (tm, bn, _wm, _wn, _st) in enumerate(conv_cfgs()):
+    for i, (tm, bn, _wm, _wn, _st) in enumerate(conv_fp8_cfgs() if fp8 else conv_cfgs()):
         if bn > 64 and bn >= 2 * ncols:   # tile at least half empty
             continue
         if bn == 64 and ncols >= 512:     # 8+ column tiles re-read the pixel panel too often

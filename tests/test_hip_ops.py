@@ -531,6 +531,20 @@ def test_fp8_conv_forward(shape):
     assert rel_err(y8, y16.float()) < 8e-2
 
 
+@pytest.mark.parametrize("cfg", range(8))
+@pytest.mark.parametrize("shape", [(256, 128, 1, 1, 14), (128, 256, 3, 1, 12), (256, 512, 1, 2, 14)])
+def test_fp8_conv_tile_configs(shape, cfg):
+    """Every entry of the MX-FP8 kernel's configuration table (incl. the 256x256 8-wave tile)."""
+    hip = _hip()
+    if cfg >= len(hip.conv_fp8_cfgs()):
+        pytest.skip("past the configuration table")
+    keep, hip.CONV_FORCE_FP8_CFG = hip.CONV_FORCE_FP8_CFG, (0, 0, cfg)
+    try:
+        test_fp8_conv_forward(shape)
+    finally:
+        hip.CONV_FORCE_FP8_CFG = keep
+
+
 def test_fp8_resnet50_step():
     """--dtype fp8 end to end on ResNet-50.  Train-mode gradients at random init are chaotic (BN
     gradient explosion amplifies any perturbation), so the checks are the well-posed ones: the
