@@ -19,7 +19,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 # (C, H) of ResNet-50 BN outputs (with how many layers share the shape)
-SHAPES = [(64, 112, 1), (64, 56, 6), (256, 56, 4), (128, 56, 1), (128, 28, 7), (512, 28, 5), (256, 28, 1),
+SHAPES = [(32, 112, 1), (96, 112, 1), (64, 112, 1), (64, 56, 6), (256, 56, 4), (128, 56, 1), (128, 28, 7), (512, 28, 5), (256, 28, 1),
           (256, 14, 11), (1024, 14, 7), (512, 14, 1), (512, 7, 5), (2048, 7, 4)]
 
 
@@ -61,6 +61,14 @@ def main():
         row["bwd_TBps"] = round(4 * nbytes / tb / 1e9, 2)
         tot[0] += ta * cnt
         tot[1] += tb * cnt
+        part = torch.zeros(64 * 2 * c, device=dev)
+        for nb in (1024, 2048, 4096, 8192):
+            C.bn_set_reduce_blocks(nb)
+            tr = timeit(lambda: C.bn_bwd_reduce(g, y, coef, res, o, rows, c, 1, part, 64))
+            ts = timeit(lambda: C.bn_stats(y, rows, c, part, 64))
+            row[f"bwdred{nb}_us"] = round(tr * 1e3, 1)
+            row[f"stats{nb}_us"] = round(ts * 1e3, 1)
+        C.bn_set_reduce_blocks(0)
         print(row, flush=True)
         out.append(row)
     print(json.dumps({"batch": a.batch, "total_ms_apply_bwd": [round(x, 3) for x in tot]}))

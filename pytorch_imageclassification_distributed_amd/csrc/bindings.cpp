@@ -479,6 +479,7 @@ void bn_stats(Tensor y, long rows, int C, Tensor part, int G) {
 }  // namespace
 
 void register_loader(pybind11::module& m);  // loader.cpp: native image-folder loader
+void bn_set_reduce_blocks(int n);           // bn.hip: target blocks of the row-reduction kernels
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "gfx950 (MI355X) HIP kernels for pytorch_imageclassification_distributed_amd";
@@ -521,6 +522,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("prepare_input_s2d", &prepare_input_s2d);
   m.def("normalize_u8", &normalize_u8);
   register_loader(m);
+  m.def("bn_set_reduce_blocks", &bn_set_reduce_blocks);
   m.def("conv_fp8_cfgs", []() {
     std::vector<std::vector<int>> out;
     for (int i = 0; i < conv_num_fp8_cfgs(); ++i) {
