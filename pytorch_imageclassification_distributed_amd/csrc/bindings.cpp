@@ -27,10 +27,10 @@ int bn_eval_coef_launch(const float*, const float*, const float*, const float*, 
 int bn_apply_launch(const bf16_t*, const float*, const bf16_t*, bf16_t*, long, int, int, int, int, uint8_t*, uint8_t*,
                     hipStream_t);
 int bn_bwd_reduce_launch(const bf16_t*, const bf16_t*, const float*, const bf16_t*, bf16_t*, long, int, int,
-                         float*, int, hipStream_t);
+                         float*, int, int, hipStream_t);
 int bn_bwd_k_launch(const double*, const double*, double, int, float*, hipStream_t);
 int bn_bwd_elemt_launch(const bf16_t*, const bf16_t*, const float*, const float*, const bf16_t*, const bf16_t*,
-                        bf16_t*, long, int, int, hipStream_t);
+                        bf16_t*, long, int, int, int, hipStream_t);
 int maxpool_fwd_launch(const bf16_t*, bf16_t*, uint8_t*, int, int, int, int, int, int, int, int, int, int, int,
                        int, hipStream_t);
 int maxpool_bwd_launch(const bf16_t*, const uint8_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int,
@@ -237,11 +237,13 @@ void bn_apply(Tensor y, Tensor coef, OT res, Tensor out, long rows, int C, int l
         "bn_apply");
 }
 
+// ldg: row stride (elements) of g - a channel slice of a wider NHWC gradient (concat backward); 0 = C
 void bn_bwd_reduce(Tensor g, Tensor y, Tensor coef, OT res, OT dz_out, long rows, int C, int act, Tensor part,
-                   int G) {
+                   int G, int ldg) {
   req(g, BF, "g"); req(y, BF, "y");
+  TORCH_CHECK(ldg == 0 || (ldg >= C && ldg % 8 == 0), "bn_bwd_reduce: bad ldg");
   check(bn_bwd_reduce_launch(ptr<bf16_t>(g), ptr<bf16_t>(y), ptr<float>(coef), optr<bf16_t>(res),
-                             optr<bf16_t>(dz_out), rows, C, act, ptr<float>(part), G, cur()),
+                             optr<bf16_t>(dz_out), rows, C, act, ptr<float>(part), G, ldg, cur()),
         "bn_bwd_reduce");
 }
 
@@ -249,9 +251,11 @@ void bn_bwd_k(Tensor sums, OT count_t, double n, int C, Tensor k) {
   check(bn_bwd_k_launch(ptr<double>(sums), optr<double>(count_t), n, C, ptr<float>(k), cur()), "bn_bwd_k");
 }
 
-void bn_bwd_elemt(OT g, Tensor y, Tensor coef, Tensor k, OT res, OT dz_in, Tensor dy, long rows, int C, int act) {
+void bn_bwd_elemt(OT g, Tensor y, Tensor coef, Tensor k, OT res, OT dz_in, Tensor dy, long rows, int C, int act,
+                  int ldg) {
+  TORCH_CHECK(ldg == 0 || (ldg >= C && ldg % 8 == 0), "bn_bwd_elemt: bad ldg");
   check(bn_bwd_elemt_launch(optr<bf16_t>(g), ptr<bf16_t>(y), ptr<float>(coef), ptr<float>(k), optr<bf16_t>(res),
-                            optr<bf16_t>(dz_in), ptr<bf16_t>(dy), rows, C, act, cur()),
+                            optr<bf16_t>(dz_in), ptr<bf16_t>(dy), rows, C, act, ldg, cur()),
         "bn_bwd_elemt");
 }
 
@@ -498,9 +502,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_apply", &bn_apply, pybind11::arg("y"), pybind11::arg("coef"), pybind11::arg("res"), pybind11::arg("out"),
         pybind11::arg("rows"), pybind11::arg("C"), pybind11::arg("ldo"), pybind11::arg("c_off"), pybind11::arg("act"),
         pybind11::arg("q") = pybind11::none(), pybind11::arg("qs") = pybind11::none());
-  m.def("bn_bwd_reduce", &bn_bwd_reduce);
+  m.def("bn_bwd_reduce", &bn_bwd_reduce, pybind11::arg("g"), pybind11::arg("y"), pybind11::arg("coef"), pybind11::arg("res"),
+        pybind11::arg("dz_out"), pybind11::arg("rows"), pybind11::arg("C"), pybind11::arg("act"), pybind11::arg("part"), pybind11::arg("G"),
+        pybind11::arg("ldg") = 0);
   m.def("bn_bwd_k", &bn_bwd_k);
-  m.def("bn_bwd_elemt", &bn_bwd_elemt);
+  m.def("bn_bwd_elemt", &bn_bwd_elemt, pybind11::arg("g"), pybind11::arg("y"), pybind11::arg("coef"), pybind11::arg("k"), pybind11::arg("res"),
+        pybind11::arg("dz_in"), pybind11::arg("dy"), pybind11::arg("rows"), pybind11::arg("C"), pybind11::arg("act"), pybind11::arg("ldg") = 0);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("avgpool_fwd", &avgpool_fwd);

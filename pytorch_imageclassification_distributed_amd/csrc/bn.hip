@@ -244,7 +244,7 @@ __global__ void bn_apply_mx_kernel(const bf16_t* __restrict__ y, const float* __
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     const bf16_t* __restrict__ g, const bf16_t* __restrict__ y, const float* __restrict__ coef,
     const bf16_t* __restrict__ res, bf16_t* __restrict__ dz_out, long rows, int C, int act,
-    long rows_per_block, float* __restrict__ part, int G) {
+    long rows_per_block, float* __restrict__ part, int G, int ldg) {
   __shared__ float red[2][256][9];
   const int cch = C >> 3;
   const int CHB = cch < 256 ? cch : 256;
@@ -269,7 +269,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
 #pragma unroll 4
     for (long row = rbeg + lr; row < rend; row += RP) {
       float gv[8], yv[8], rv[8];
-      unpack8(*(const uint4*)(g + row * C + c0), gv);
+      unpack8(*(const uint4*)(g + row * ldg + c0), gv);
       unpack8(*(const uint4*)(y + row * C + c0), yv);
       if (res) unpack8(*(const uint4*)(res + row * C + c0), rv);
 #pragma unroll
@@ -363,7 +363,7 @@ DEVI void load8f(const float* p, float* v) {
 __global__ void bn_bwd_elemt_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ y,
                                     const float* __restrict__ coef, const float* __restrict__ kk,
                                     const bf16_t* __restrict__ res, const bf16_t* __restrict__ dz_in,
-                                    bf16_t* __restrict__ dy, long rows, int C, int act) {
+                                    bf16_t* __restrict__ dy, long rows, int C, int act, int ldg) {
   const int cch = C >> 3;
   const long total = rows * cch;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
@@ -379,7 +379,7 @@ __global__ void bn_bwd_elemt_kernel(const bf16_t* __restrict__ g, const bf16_t* 
     if (dz_in) {
       unpack8(*(const uint4*)(dz_in + row * C + c0), gv);
     } else {
-      unpack8(*(const uint4*)(g + row * C + c0), gv);
+      unpack8(*(const uint4*)(g + row * ldg + c0), gv);
       if (act != ACT_NONE) {
         float sh[8], rv[8];
         load8f(coef + C + c0, sh);
@@ -470,7 +470,7 @@ int bn_apply_launch(const bf16_t* y, const float* coef, const bf16_t* res, bf16_
 }
 
 int bn_bwd_reduce_launch(const bf16_t* g, const bf16_t* y, const float* coef, const bf16_t* res,
-                         bf16_t* dz_out, long rows, int C, int act, float* part, int G, hipStream_t s) {
+                         bf16_t* dz_out, long rows, int C, int act, float* part, int G, int ldg, hipStream_t s) {
   const int cch = C / 8;
   const int CHB = cch < 256 ? cch : 256;
   const int slices = cdiv(cch, CHB);
@@ -482,7 +482,7 @@ int bn_bwd_reduce_launch(const bf16_t* g, const bf16_t* y, const float* coef, co
   if (rpb < 4L * RP) rpb = 4L * RP;
   rblocks = (rows + rpb - 1) / rpb;
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3((unsigned)rblocks, slices), dim3(256), 0, s, g, y, coef, res,
-                     dz_out, rows, C, act, rpb, part, G);
+                     dz_out, rows, C, act, rpb, part, G, ldg > 0 ? ldg : C);
   HIP_CHECK_LAUNCH();
   return 0;
 }
@@ -495,10 +495,10 @@ int bn_bwd_k_launch(const double* sums, const double* count_p, double n, int C, 
 
 int bn_bwd_elemt_launch(const bf16_t* g, const bf16_t* y, const float* coef, const float* k,
                         const bf16_t* res, const bf16_t* dz_in, bf16_t* dy, long rows, int C, int act,
-                        hipStream_t s) {
+                        int ldg, hipStream_t s) {
   const long work = rows * (C / 8);
   hipLaunchKernelGGL(bn_bwd_elemt_kernel, dim3(grid_for(work, 256, 8192)), dim3(256), 0, s, g, y, coef, k,
-                     res, dz_in, dy, rows, C, act);
+                     res, dz_in, dy, rows, C, act, ldg > 0 ? ldg : C);
   HIP_CHECK_LAUNCH();
   return 0;
 }

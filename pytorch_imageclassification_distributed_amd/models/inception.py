@@ -28,10 +28,11 @@ class BasicConv2d(nn.Module):
         self.conv = nn.Conv2d(cin, cout, bias=False, **kw)
         self.bn = nn.BatchNorm2d(cout, eps=0.001)
 
-    def forward(self, x, exclusive=False, slot=None):
+    def forward(self, x, exclusive=False, slot=None, out=None):
         """``exclusive``: this conv is the only consumer of ``x`` (a chain-internal conv), which lets its
-        dgrad epilogue run the producer's BN-backward reduce; ``slot``: x feeds exactly two convs."""
-        return Fx.conv_bn_act(x, self.conv, self.bn, "relu", x_slot=slot, exclusive_input=exclusive)
+        dgrad epilogue run the producer's BN-backward reduce; ``slot``: x feeds exactly two convs;
+        ``out``: (concat plan, branch) - write the result into the block's concat output in place."""
+        return Fx.conv_bn_act(x, self.conv, self.bn, "relu", x_slot=slot, exclusive_input=exclusive, out=out)
 
 
 class InceptionA(nn.Module):
@@ -47,11 +48,12 @@ class InceptionA(nn.Module):
 
     def forward(self, x):
         s = Fx.grad_slot(x, 4)  # x feeds three convs and the pool: summed inside their backward kernels
-        b1 = self.branch1x1(x, slot=s)
-        b5 = self.branch5x5_2(self.branch5x5_1(x, slot=s), True)
-        b3 = self.branch3x3dbl_3(self.branch3x3dbl_2(self.branch3x3dbl_1(x, slot=s), True), True)
-        bp = self.branch_pool(Fx.avg_pool2d(x, 3, 1, 1, slot=s))
-        return Fx.cat_channels([b1, b5, b3, bp])
+        cat = Fx.concat_buffer([64, 64, 96, self.branch_pool.conv.out_channels])  # branches write in place
+        b1 = self.branch1x1(x, slot=s, out=(cat, 0))
+        b5 = self.branch5x5_2(self.branch5x5_1(x, slot=s), True, out=(cat, 1))
+        b3 = self.branch3x3dbl_3(self.branch3x3dbl_2(self.branch3x3dbl_1(x, slot=s), True), True, out=(cat, 2))
+        bp = self.branch_pool(Fx.avg_pool2d(x, 3, 1, 1, slot=s), out=(cat, 3))
+        return Fx.cat_channels([b1, b5, b3, bp], cat)
 
 
 class InceptionB(nn.Module):
@@ -64,10 +66,11 @@ class InceptionB(nn.Module):
 
     def forward(self, x):
         s = Fx.grad_slot(x, 3)
-        b3 = self.branch3x3(x, slot=s)
-        bd = self.branch3x3dbl_3(self.branch3x3dbl_2(self.branch3x3dbl_1(x, slot=s), True), True)
+        cat = Fx.concat_buffer([384, 96, x.shape[1]])  # the pool branch is copied in
+        b3 = self.branch3x3(x, slot=s, out=(cat, 0))
+        bd = self.branch3x3dbl_3(self.branch3x3dbl_2(self.branch3x3dbl_1(x, slot=s), True), True, out=(cat, 1))
         bp = Fx.max_pool2d(x, 3, 2, 0, slot=s)
-        return Fx.cat_channels([b3, bd, bp])
+        return Fx.cat_channels([b3, bd, bp], cat)
 
 
 class InceptionC(nn.Module):
@@ -87,13 +90,14 @@ class InceptionC(nn.Module):
 
     def forward(self, x):
         s = Fx.grad_slot(x, 4)
-        b1 = self.branch1x1(x, slot=s)
-        b7 = self.branch7x7_3(self.branch7x7_2(self.branch7x7_1(x, slot=s), True), True)
+        cat = Fx.concat_buffer([192, 192, 192, 192])
+        b1 = self.branch1x1(x, slot=s, out=(cat, 0))
+        b7 = self.branch7x7_3(self.branch7x7_2(self.branch7x7_1(x, slot=s), True), True, out=(cat, 1))
         bd = self.branch7x7dbl_1(x, slot=s)
         bd = self.branch7x7dbl_3(self.branch7x7dbl_2(bd, True), True)
-        bd = self.branch7x7dbl_5(self.branch7x7dbl_4(bd, True), True)
-        bp = self.branch_pool(Fx.avg_pool2d(x, 3, 1, 1, slot=s))
-        return Fx.cat_channels([b1, b7, bd, bp])
+        bd = self.branch7x7dbl_5(self.branch7x7dbl_4(bd, True), True, out=(cat, 2))
+        bp = self.branch_pool(Fx.avg_pool2d(x, 3, 1, 1, slot=s), out=(cat, 3))
+        return Fx.cat_channels([b1, b7, bd, bp], cat)
 
 
 class InceptionD(nn.Module):
@@ -108,11 +112,12 @@ class InceptionD(nn.Module):
 
     def forward(self, x):
         s = Fx.grad_slot(x, 3)
-        b3 = self.branch3x3_2(self.branch3x3_1(x, slot=s), True)
+        cat = Fx.concat_buffer([320, 192, x.shape[1]])
+        b3 = self.branch3x3_2(self.branch3x3_1(x, slot=s), True, out=(cat, 0))
         b7 = self.branch7x7x3_2(self.branch7x7x3_1(x, slot=s), True)
-        b7 = self.branch7x7x3_4(self.branch7x7x3_3(b7, True), True)
+        b7 = self.branch7x7x3_4(self.branch7x7x3_3(b7, True), True, out=(cat, 1))
         bp = Fx.max_pool2d(x, 3, 2, 0, slot=s)
-        return Fx.cat_channels([b3, b7, bp])
+        return Fx.cat_channels([b3, b7, bp], cat)
 
 
 class InceptionE(nn.Module):
@@ -130,15 +135,16 @@ class InceptionE(nn.Module):
 
     def forward(self, x):
         s = Fx.grad_slot(x, 4)
-        b1 = self.branch1x1(x, slot=s)
+        cat = Fx.concat_buffer([320, 384, 384, 384, 384, 192])
+        b1 = self.branch1x1(x, slot=s, out=(cat, 0))
         b3 = self.branch3x3_1(x, slot=s)
         s3 = Fx.grad_slot(b3)  # b3 and bd each feed exactly two convs: paired gradient slots
-        b3a, b3b = self.branch3x3_2a(b3, slot=s3), self.branch3x3_2b(b3, slot=s3)
+        b3a, b3b = self.branch3x3_2a(b3, slot=s3, out=(cat, 1)), self.branch3x3_2b(b3, slot=s3, out=(cat, 2))
         bd = self.branch3x3dbl_2(self.branch3x3dbl_1(x, slot=s), True)
         sd = Fx.grad_slot(bd)
-        bda, bdb = self.branch3x3dbl_3a(bd, slot=sd), self.branch3x3dbl_3b(bd, slot=sd)
-        bp = self.branch_pool(Fx.avg_pool2d(x, 3, 1, 1, slot=s))
-        return Fx.cat_channels([b1, b3a, b3b, bda, bdb, bp])
+        bda, bdb = self.branch3x3dbl_3a(bd, slot=sd, out=(cat, 3)), self.branch3x3dbl_3b(bd, slot=sd, out=(cat, 4))
+        bp = self.branch_pool(Fx.avg_pool2d(x, 3, 1, 1, slot=s), out=(cat, 5))
+        return Fx.cat_channels([b1, b3a, b3b, bda, bdb, bp], cat)
 
 
 class InceptionAux(nn.Module):

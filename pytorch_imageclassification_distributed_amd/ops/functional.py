@@ -111,7 +111,8 @@ def grad_slot(x, n: int = 2):
     return None
 
 
-def conv_bn_act(x, conv, bn, act="relu", residual=None, x_slot=None, res_slot=None, exclusive_input=False):
+def conv_bn_act(x, conv, bn, act="relu", residual=None, x_slot=None, res_slot=None, exclusive_input=False,
+                out=None):
     """act(bn(conv(x)) [+ residual]).
 
     Reference equivalents: torchvision ``BasicConv2d`` (conv -> BN -> ReLU),
@@ -119,7 +120,8 @@ def conv_bn_act(x, conv, bn, act="relu", residual=None, x_slot=None, res_slot=No
     efficientnet_pytorch ``MBConvBlock`` (conv -> BN -> swish).
     """
     if use_hip(x):
-        return _hip().conv_bn_act(x, conv, bn, act, residual, x_slot, res_slot, exclusive_input)
+        hout = (out[0].hip(), out[1]) if (out is not None and _hip().CONCAT_INPLACE) else None
+        return _hip().conv_bn_act(x, conv, bn, act, residual, x_slot, res_slot, exclusive_input, hout)
     y = _torch_bn(_torch_conv(x, conv), bn)
     if residual is not None:
         y = y + residual
@@ -174,9 +176,29 @@ def dropout(x, p, training):
     return F.dropout(x, p, True)
 
 
-def cat_channels(xs):
+class ConcatPlan:
+    """A channel concat whose branches write their outputs in place: pass ``out=(plan, i)`` to the
+    branch's final ``conv_bn_act`` and ``buf=plan`` to ``cat_channels`` (HIP path: ``hip.ConcatBuffer``;
+    the reference path ignores the plan and concatenates with ``torch.cat``)."""
+
+    def __init__(self, channels):
+        self.channels = list(channels)
+        self._hip = None
+
+    def hip(self):
+        if self._hip is None:
+            self._hip = _hip().ConcatBuffer(self.channels)
+        return self._hip
+
+
+def concat_buffer(channels) -> ConcatPlan:
+    return ConcatPlan(channels)
+
+
+def cat_channels(xs, buf=None):
     if use_hip(xs[0]):
-        return _hip().cat_channels(xs)
+        h = _hip()
+        return h.cat_channels(xs, buf.hip() if (buf is not None and h.CONCAT_INPLACE) else None)
     return torch.cat(xs, 1)
 
 

@@ -805,7 +805,7 @@ class DwConvFn(torch.autograd.Function):
 # ---------------------------------------------------------------------------
 class BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, y, gamma, beta, res, bn, act, stats_ready, res_slot=None, link=None):
+    def forward(ctx, y, gamma, beta, res, bn, act, stats_ready, res_slot=None, link=None, cat=None):
         dev = y.device
         n, c, h, w = y.shape
         rows = n * h * w
@@ -834,13 +834,19 @@ class BNActFn(torch.autograd.Function):
             if stats_ready:
                 raise RuntimeError("eval-mode BN received fused statistics")
             C.bn_eval_coef(gamma, beta, bn.running_mean, bn.running_var, bn.eps, c, coef)
-        out = _empty_cl(n, c, h, w, dev)
-        if FP8_FWD and c % 128 == 0:  # the consuming conv reads an MX-FP8 copy: produce it here
+        if cat is not None:  # write straight into this branch's channel slice of the concat output
+            cbuf, idx = cat
+            base = cbuf.ensure(n, h, w, dev)
+            C.bn_apply(y, coef, res, base, rows, c, cbuf.total, cbuf.offs[idx], a)
+            out = cbuf.part(idx, c)
+        elif FP8_FWD and c % 128 == 0:  # the consuming conv reads an MX-FP8 copy: produce it here
+            out = _empty_cl(n, c, h, w, dev)
             q = torch.empty(rows * c, dtype=FP8, device=dev)
             qs = torch.empty(rows * c // 32, dtype=torch.uint8, device=dev)
             C.bn_apply(y, coef, res, out, rows, c, c, 0, a, q, qs)
             out._imgcls_mx = (q, qs, out._version)
         else:
+            out = _empty_cl(n, c, h, w, dev)
             C.bn_apply(y, coef, res, out, rows, c, c, 0, a)
         ctx.act, ctx.group, ctx.rows, ctx.c = a, group, rows, c
         ctx.training = bn.training
@@ -862,7 +868,8 @@ class BNActFn(torch.autograd.Function):
         res = res if ctx.has_res else None
         dev = y.device
         c, rows = ctx.c, ctx.rows
-        g = _cl(gout)
+        ldg = channel_slice_stride(gout)  # a concat's gradient arrives as a channel slice: read in place
+        g = gout if ldg else _cl(gout)
         link = ctx.link
         grp = stat_groups(rows)
         pending = None
@@ -875,7 +882,7 @@ class BNActFn(torch.autograd.Function):
         else:
             part = ws(dev).stats_buf(c, grp)
             dz = torch.empty_like(y, memory_format=CL) if ctx.has_res else None
-            C.bn_bwd_reduce(g, y, coef, res, dz, rows, c, ctx.act, part, grp)
+            C.bn_bwd_reduce(g, y, coef, res, dz, rows, c, ctx.act, part, grp, ldg)
         k = torch.empty(2 * c, dtype=torch.float32, device=dev)
         if pending is not None:  # SyncBN all-reduce launched early by the consuming conv's backward
             sums, work, dgamma, dbeta = pending
@@ -899,16 +906,18 @@ class BNActFn(torch.autograd.Function):
         if link is not None and link.done:
             ws(dev).give_part(part)
         dy = torch.empty_like(y, memory_format=CL)
-        C.bn_bwd_elemt(None if dz is not None else g, y, coef, k, res, dz, dy, rows, c, ctx.act)
+        C.bn_bwd_elemt(None if dz is not None else g, y, coef, k, res, dz, dy, rows, c, ctx.act,
+                       0 if dz is not None else ldg)
         dres = dz if ctx.has_res else None
         if dres is not None and ctx.res_slot is not None:
             dres = ctx.res_slot.deliver(dres)
-        return dy, dgamma, dbeta, dres, None, None, None, None, None
+        return dy, dgamma, dbeta, dres, None, None, None, None, None, None
 
 
-def conv_bn_act(x, conv, bn, act, residual, x_slot=None, res_slot=None, exclusive_input=False):
+def conv_bn_act(x, conv, bn, act, residual, x_slot=None, res_slot=None, exclusive_input=False, out=None):
     """``exclusive_input``: this conv is the only consumer of ``x`` (lets its dgrad fuse the BN-backward
-    reduce of x's producer); a slot-paired consumer qualifies automatically."""
+    reduce of x's producer); a slot-paired consumer qualifies automatically.  ``out`` = (ConcatBuffer,
+    branch index): the result is written into that branch's channel slice of the concat output."""
     if stem_s2d_eligible(x, conv) and residual is None and not x.requires_grad:
         ensure_channels_last_weight(conv)
         y = StemS2dFn.apply(x, conv.weight, conv, bn.training)
@@ -935,10 +944,10 @@ def conv_bn_act(x, conv, bn, act, residual, x_slot=None, res_slot=None, exclusiv
     if conv.bias is not None:
         raise NotImplementedError("conv bias before BatchNorm")
     link = BwdLink() if (FUSE_BN_BWD and bn.training and torch.is_grad_enabled()) else None
-    out = BNActFn.apply(y, bn.weight, bn.bias, residual, bn, act, ready, res_slot, link)
+    res_out = BNActFn.apply(y, bn.weight, bn.bias, residual, bn, act, ready, res_slot, link, out)
     if link is not None:
-        out._imgcls_link = link
-    return out
+        res_out._imgcls_link = link
+    return res_out
 
 
 class ConvBiasFn(torch.autograd.Function):
@@ -1204,19 +1213,74 @@ def prepare_input(x, scale=None, shift=None, stem=None):
     return y
 
 
+def channel_slice_stride(t) -> int:
+    """Row stride (channels) when ``t`` is a channel slice of a wider channels-last tensor (a concat
+    output's per-branch gradient), else 0."""
+    if t.dim() != 4 or t.stride(1) != 1:
+        return 0
+    n, c, h, w = t.shape
+    ld = t.stride(3)
+    if ld == c or ld % 8 or c % 8 or t.stride(2) != w * ld or (n > 1 and t.stride(0) != h * w * ld):
+        return 0
+    return ld if t.data_ptr() % 16 == 0 else 0
+
+
+CONCAT_INPLACE = os.environ.get("IMGCLS_CONCAT_INPLACE", "1") == "1"  # 0: copy branches into the concat
+
+
+class ConcatBuffer:
+    """Output of a channel concat (Inception blocks) that the branches write in place:
+    each branch's final BN-apply stores straight into its channel slice (``conv_bn_act(out=(buf, i))``),
+    ``cat_channels(parts, buf)`` then only copies branches that were produced elsewhere (pools), and its
+    backward hands every in-place branch its gradient slice without a copy (BN backward reads it with
+    a row stride).  Allocated lazily by the first branch (which knows the batch and spatial size)."""
+
+    def __init__(self, channels):
+        self.cs = list(channels)
+        self.offs = [sum(self.cs[:i]) for i in range(len(self.cs))]
+        self.total = sum(self.cs)
+        self.buf = None
+        self.ptrs = [None] * len(self.cs)
+
+    def ensure(self, n, h, w, dev):
+        if self.buf is None:
+            self.buf = _empty_cl(n, self.total, h, w, dev)
+        elif tuple(self.buf.shape) != (n, self.total, h, w):
+            raise RuntimeError("concat branches disagree on the output shape")
+        return self.buf
+
+    def part(self, i, c):
+        """Branch i's slice as a tensor sharing the buffer's storage but not an autograd view of it
+        (several custom Functions write into one base; views would trip autograd's view+inplace check)."""
+        if c != self.cs[i]:
+            raise RuntimeError(f"concat branch {i}: {c} channels, planned {self.cs[i]}")
+        b = self.buf
+        n, _, h, w = b.shape
+        t = torch.empty(0, dtype=b.dtype, device=b.device)
+        t.set_(b.untyped_storage(), b.storage_offset() + self.offs[i], (n, c, h, w),
+               (h * w * self.total, 1, w * self.total, self.total))
+        self.ptrs[i] = t.data_ptr()
+        return t
+
+
 class CatFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, *xs):
+    def forward(ctx, cbuf, *xs):
         n, _, h, w = xs[0].shape
         cs = [t.shape[1] for t in xs]
-        tot = sum(cs)
-        y = _empty_cl(n, tot, h, w, xs[0].device)
-        off = 0
+        if cbuf is None:
+            cbuf = ConcatBuffer(cs)
+        elif cs != cbuf.cs:
+            raise RuntimeError(f"cat_channels: parts {cs} != planned {cbuf.cs}")
+        y = cbuf.ensure(n, h, w, xs[0].device)
         rows = n * h * w
-        for t, c in zip(xs, cs):
-            C.copy_channels(t, c, 0, y, tot, off, rows, c)
-            off += c
-        ctx.cs = cs
+        inplace = []
+        for i, (t, c) in enumerate(zip(xs, cs)):
+            done = cbuf.ptrs[i] is not None and t.data_ptr() == cbuf.ptrs[i]
+            if not done:
+                C.copy_channels(_cl(t), c, 0, y, cbuf.total, cbuf.offs[i], rows, c)
+            inplace.append(done)
+        ctx.cs, ctx.inplace = cs, inplace
         ctx.geo = (n, h, w)
         return y
 
@@ -1226,16 +1290,19 @@ class CatFn(torch.autograd.Function):
         n, h, w = ctx.geo
         tot = sum(ctx.cs)
         outs, off = [], 0
-        for c in ctx.cs:
-            g = _empty_cl(n, c, h, w, gy.device)
-            C.copy_channels(gy, tot, off, g, c, 0, n * h * w, c)
-            outs.append(g)
+        for c, inplace in zip(ctx.cs, ctx.inplace):
+            if inplace:  # BN backward reads the slice in place (row stride tot)
+                outs.append(gy[:, off:off + c])
+            else:
+                g = _empty_cl(n, c, h, w, gy.device)
+                C.copy_channels(gy, tot, off, g, c, 0, n * h * w, c)
+                outs.append(g)
             off += c
-        return tuple(outs)
+        return (None,) + tuple(outs)
 
 
-def cat_channels(xs):
-    return CatFn.apply(*[_cl(t) for t in xs])
+def cat_channels(xs, buf=None):
+    return CatFn.apply(buf, *xs)
 
 
 class AddFn(torch.autograd.Function):

@@ -173,3 +173,37 @@ def test_inception_block_fusion(kind, expect):
     assert err(gx1, gx0) < 3e-2, err(gx1, gx0)
     for n in gp0:
         assert err(gp1[n], gp0[n]) < 3e-2, (n, err(gp1[n], gp0[n]))
+
+
+@pytest.mark.parametrize("kind", ["A", "B", "C", "D", "E"])
+def test_inception_concat_in_place(kind):
+    """Inception blocks: branches writing their BN output straight into the concat buffer (and reading
+    their gradient slices in place) == copying branches into a fresh concat (forward and gradients)."""
+    from pytorch_imageclassification_distributed_amd.models import inception as I
+    from pytorch_imageclassification_distributed_amd.ops import hip
+    torch.manual_seed(0)
+    blk, cin, hw = {"A": (I.InceptionA(192, 32), 192, 17), "B": (I.InceptionB(288), 288, 17),
+                    "C": (I.InceptionC(768, 128), 768, 9), "D": (I.InceptionD(768), 768, 9),
+                    "E": (I.InceptionE(1280), 1280, 5)}[kind]
+    blk = blk.to(DEV).to(memory_format=torch.channels_last)
+    x = torch.randn(4, cin, hw, hw, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+
+    def run(inplace):
+        keep, hip.CONCAT_INPLACE = hip.CONCAT_INPLACE, inplace
+        try:
+            for p in blk.parameters():
+                p.grad = None
+            xx = x.clone().requires_grad_(True)
+            out = blk(xx)
+            (out.float() * torch.linspace(-1, 1, out.numel(), device=DEV).view_as(out)).sum().backward()
+            return out.float(), xx.grad.float(), {n: p.grad.float().clone() for n, p in blk.named_parameters()}
+        finally:
+            hip.CONCAT_INPLACE = keep
+
+    o0, gx0, gp0 = run(False)
+    o1, gx1, gp1 = run(True)
+    err = lambda a, b: ((a - b).abs().max() / b.abs().max().clamp(min=1e-6)).item()  # noqa: E731
+    assert err(o1, o0) < 1e-2
+    assert err(gx1, gx0) < 2e-2, err(gx1, gx0)
+    for n in gp0:
+        assert err(gp1[n], gp0[n]) < 2e-2, (n, err(gp1[n], gp0[n]))
