@@ -1,6 +1,8 @@
 """BatchNorm elementwise kernels (apply fwd, backward elementwise) on the ResNet-50 BN shapes: achieved
 HBM bandwidth (apply moves 3 bf16 tensors incl. the residual, backward 4).
 
+The row reductions (bwd reduce, stats) are swept over block count x channel-chunk lanes per block.
+
 A channel-group-stationary variant (each thread pinned to one 8-channel group, coefficients in
 registers, two rows in flight) was measured slower than these flat grid-stride kernels (11.3 vs 10.1 ms
 of backward per ResNet-50 step at batch 512) and removed.
@@ -62,13 +64,16 @@ def main():
         tot[0] += ta * cnt
         tot[1] += tb * cnt
         part = torch.zeros(64 * 2 * c, device=dev)
-        for nb in (1024, 2048, 4096, 8192):
-            C.bn_set_reduce_blocks(nb)
-            tr = timeit(lambda: C.bn_bwd_reduce(g, y, coef, res, o, rows, c, 1, part, 64))
-            ts = timeit(lambda: C.bn_stats(y, rows, c, part, 64))
-            row[f"bwdred{nb}_us"] = round(tr * 1e3, 1)
-            row[f"stats{nb}_us"] = round(ts * 1e3, 1)
-        C.bn_set_reduce_blocks(0)
+        for nb in (1024, 2048):
+            for chb in (8, 32, 256):  # channel-chunk lanes per block (32 = default; 256 = the former layout)
+                if chb > 8 and chb > c // 8:
+                    continue
+                C.bn_set_reduce_blocks(nb, chb)
+                tr = timeit(lambda: C.bn_bwd_reduce(g, y, coef, res, o, rows, c, 1, part, 64))
+                ts = timeit(lambda: C.bn_stats(y, rows, c, part, 64))
+                row[f"bwdred{nb}_chb{chb}_us"] = round(tr * 1e3, 1)
+                row[f"stats{nb}_chb{chb}_us"] = round(ts * 1e3, 1)
+        C.bn_set_reduce_blocks(0, 0)
         print(row, flush=True)
         out.append(row)
     print(json.dumps({"batch": a.batch, "total_ms_apply_bwd": [round(x, 3) for x in tot]}))

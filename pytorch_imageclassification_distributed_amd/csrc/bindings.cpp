@@ -31,6 +31,7 @@ int bn_bwd_reduce_launch(const bf16_t*, const bf16_t*, const float*, const bf16_
 int bn_bwd_k_launch(const double*, const double*, double, int, float*, hipStream_t);
 int bn_bwd_elemt_launch(const bf16_t*, const bf16_t*, const float*, const float*, const bf16_t*, const bf16_t*,
                         bf16_t*, long, int, int, int, hipStream_t);
+int bn_act_maxpool_launch(const bf16_t*, const float*, bf16_t*, uint8_t*, int, int, const int*, int, hipStream_t);
 int maxpool_fwd_launch(const bf16_t*, bf16_t*, uint8_t*, int, int, int, int, int, int, int, int, int, int, int,
                        int, hipStream_t);
 int maxpool_bwd_launch(const bf16_t*, const uint8_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int,
@@ -259,6 +260,36 @@ void bn_bwd_elemt(OT g, Tensor y, Tensor coef, Tensor k, OT res, OT dz_in, Tenso
         "bn_bwd_elemt");
 }
 
+// max pool over act(BN(y)): geo = [H, W, OH, OW, kh, kw, sh, sw, ph, pw]; y [N,H,W,C], pooled / idx [N,OH,OW,C]
+std::vector<int> pool_geo(const std::vector<int64_t>& geo, const Tensor& y, const Tensor& pooled, const Tensor& idx,
+                          int64_t N, int64_t C, const char* what) {
+  TORCH_CHECK(geo.size() == 10, what, ": geo = [H, W, OH, OW, kh, kw, sh, sw, ph, pw]");
+  std::vector<int> g(geo.begin(), geo.end());
+  TORCH_CHECK(g[4] > 0 && g[5] > 0 && g[4] * g[5] <= 255 && g[6] > 0 && g[7] > 0 && g[8] >= 0 && g[9] >= 0 &&
+                  2 * g[8] <= g[4] && 2 * g[9] <= g[5],
+              what, ": bad pooling window");
+  TORCH_CHECK(g[2] == (g[0] + 2 * g[8] - g[4]) / g[6] + 1 && g[3] == (g[1] + 2 * g[9] - g[5]) / g[7] + 1 && g[2] > 0 &&
+                  g[3] > 0,
+              what, ": OH/OW do not match the window");
+  TORCH_CHECK(C % 8 == 0 && C > 0 && N > 0, what, ": C % 8");
+  req(y, BF, "y"); req(pooled, BF, "pooled");
+  TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == at::kByte, what, ": idx must be a uint8 GPU tensor");
+  TORCH_CHECK(y.numel() == N * g[0] * g[1] * C && pooled.numel() == N * g[2] * g[3] * C && idx.numel() == pooled.numel(),
+              what, ": tensor sizes do not match the geometry");
+  TORCH_CHECK(y.is_contiguous(at::MemoryFormat::ChannelsLast) || y.is_contiguous(), what, ": y must be dense NHWC");
+  return g;
+}
+
+void bn_act_maxpool(Tensor y, Tensor coef, Tensor out, Tensor idx, int64_t N, int64_t C, std::vector<int64_t> geo,
+                    int act) {
+  const auto g = pool_geo(geo, y, out, idx, N, C, "bn_act_maxpool");
+  req(coef, F32, "coef");
+  TORCH_CHECK(coef.numel() >= 4 * C, "bn_act_maxpool: coef [4*C]");
+  check(bn_act_maxpool_launch(ptr<bf16_t>(y), ptr<float>(coef), ptr<bf16_t>(out), ptr<uint8_t>(idx), (int)N, (int)C,
+                              g.data(), act, cur()),
+        "bn_act_maxpool");
+}
+
 void maxpool_fwd(Tensor x, Tensor y, OT idx, int N, int H, int W, int C, int OH, int OW, int kh, int kw, int sh,
                  int sw, int ph, int pw) {
   req(x, BF, "x"); req(y, BF, "y");
@@ -483,7 +514,7 @@ void bn_stats(Tensor y, long rows, int C, Tensor part, int G) {
 }  // namespace
 
 void register_loader(pybind11::module& m);  // loader.cpp: native image-folder loader
-void bn_set_reduce_blocks(int n);           // bn.hip: target blocks of the row-reduction kernels
+void bn_set_reduce_blocks(int n, int chb);  // bn.hip: target blocks / channel lanes of the row reductions
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "gfx950 (MI355X) HIP kernels for pytorch_imageclassification_distributed_amd";
@@ -529,7 +560,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("prepare_input_s2d", &prepare_input_s2d);
   m.def("normalize_u8", &normalize_u8);
   register_loader(m);
-  m.def("bn_set_reduce_blocks", &bn_set_reduce_blocks);
+  m.def("bn_set_reduce_blocks", &bn_set_reduce_blocks, pybind11::arg("n"), pybind11::arg("chb") = 0);
+  m.def("bn_act_maxpool", &bn_act_maxpool);
   m.def("conv_fp8_cfgs", []() {
     std::vector<std::vector<int>> out;
     for (int i = 0; i < conv_num_fp8_cfgs(); ++i) {

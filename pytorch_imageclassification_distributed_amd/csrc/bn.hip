@@ -239,15 +239,69 @@ __global__ void bn_apply_mx_kernel(const bf16_t* __restrict__ y, const float* __
   }
 }
 
+// ---- max pool over act(BN(y)) (network stems) --------------------------------
+// The window max of the activation is taken straight from y, so the full-resolution activation is never
+// written or re-read.  (The backward keeps maxpool_bwd -> bn_bwd_reduce -> bn_bwd_elemt: gathering the
+// pooled gradient inside both BN-backward passes was measured slower, 815 vs 720 us at batch 256 - the
+// 4-window gather costs as much as the full-resolution write + read it saves, and would run twice.)
+struct PoolWin {  // max pool window over a [N, H, W, C] input -> [N, OH, OW, C]
+  int H, W, OH, OW, kh, kw, sh, sw, ph, pw;
+};
+
+// out = max over the window of act(y*scale + shift) (rounded to bf16 first, so the max and its index
+// are those of the activation tensor the unfused path would pool), idx = window position of the max
+__global__ void bn_act_maxpool_kernel(const bf16_t* __restrict__ y, const float* __restrict__ coef,
+                                      bf16_t* __restrict__ out, uint8_t* __restrict__ idx, int N, int C,
+                                      PoolWin g, int act) {
+  const int cch = C >> 3;
+  const long total = (long)N * g.OH * g.OW * cch;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cch) * 8;
+    long t = i / cch;
+    const int ow = (int)(t % g.OW); t /= g.OW;
+    const int oh = (int)(t % g.OH);
+    const long n = t / g.OH;
+    float sc[8], sh[8], best[8];
+    int bi[8];
+    *(float4*)sc = *(const float4*)(coef + c0);
+    *(float4*)(sc + 4) = *(const float4*)(coef + c0 + 4);
+    *(float4*)sh = *(const float4*)(coef + C + c0);
+    *(float4*)(sh + 4) = *(const float4*)(coef + C + c0 + 4);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; bi[k] = 0; }
+    for (int r = 0; r < g.kh; ++r) {
+      const int ih = oh * g.sh - g.ph + r;
+      if ((unsigned)ih >= (unsigned)g.H) continue;
+      for (int c = 0; c < g.kw; ++c) {
+        const int iw = ow * g.sw - g.pw + c;
+        if ((unsigned)iw >= (unsigned)g.W) continue;
+        float v[8];
+        unpack8(*(const uint4*)(y + ((n * g.H + ih) * g.W + iw) * C + c0), v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = apply_act(v[k] * sc[k] + sh[k], act);
+        unpack8(pack8(v), v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (v[k] > best[k] || (v[k] != v[k])) { best[k] = v[k]; bi[k] = r * g.kw + c; }
+      }
+    }
+    const long o = ((n * g.OH + oh) * g.OW + ow) * C + c0;
+    *(uint4*)(out + o) = pack8(best);
+    uint2 pk;
+    pk.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
+    pk.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
+    *(uint2*)(idx + o) = pk;
+  }
+}
+
 // ---- backward reduce -------------------------------------------------------
 // grid: (row blocks, channel-chunk slices); block 256 = CHB chunk lanes x RP row lanes
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     const bf16_t* __restrict__ g, const bf16_t* __restrict__ y, const float* __restrict__ coef,
     const bf16_t* __restrict__ res, bf16_t* __restrict__ dz_out, long rows, int C, int act,
-    long rows_per_block, float* __restrict__ part, int G, int ldg) {
+    long rows_per_block, float* __restrict__ part, int G, int ldg, int CHB) {
   __shared__ float red[2][256][9];
   const int cch = C >> 3;
-  const int CHB = cch < 256 ? cch : 256;
   const int RP = 256 / CHB;
   const int tid = threadIdx.x;
   const int lc = tid % CHB, lr = tid / CHB;
@@ -310,10 +364,10 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
 
 // ---- standalone statistics pass (outputs not produced by the GEMM epilogue) --
 __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict__ y, long rows, int C,
-                                                       long rows_per_block, float* __restrict__ part, int G) {
+                                                       long rows_per_block, float* __restrict__ part, int G,
+                                                       int CHB) {
   __shared__ float red[2][256][9];
   const int cch = C >> 3;
-  const int CHB = cch < 256 ? cch : 256;
   const int RP = 256 / CHB;
   const int tid = threadIdx.x;
   const int lc = tid % CHB, lr = tid / CHB;
@@ -404,6 +458,39 @@ __global__ void bn_bwd_elemt_kernel(const bf16_t* __restrict__ g, const bf16_t* 
 // target block count of the row-reduction kernels (bn_stats, bn_bwd_reduce); 0 = measured default:
 // 2048 for C <= 256 (~10 % faster than 1024), 1024 above (more blocks only add partial-row atomics)
 static int g_reduce_blocks = 0;
+// channel-chunk lanes per block (8 channels each); 0 = auto: the smallest divisor of C/8 in [8, 32]
+// (C/8 itself below 8; 32 when none divides), so a block ends in 2 x 64 .. 2 x 256 partial-row atomics
+// whatever C is.  With all C/8 chunks in one block (the former layout) a C = 2048 layer issued 4096
+// atomics per block and the reduce ran atomic-bound at 1.2 TB/s: 123 -> 42 us at batch 256
+// (profiles/r1d_bn_reduce_chunk_sweep_b256.txt); a divisor keeps every lane of every slice busy.
+static int g_reduce_chb = 0;
+
+int auto_chb(int cch) {
+  if (cch <= 8) return cch;
+  for (int d = 8; d <= 32; ++d)
+    if (cch % d == 0) return d;
+  return 32;
+}
+
+struct RedGrid {
+  dim3 grid;
+  long rpb;
+  int chb;
+};
+
+RedGrid reduce_grid(long rows, int C) {
+  const int cch = C / 8;
+  const int CHB = g_reduce_chb > 0 ? (cch < g_reduce_chb ? cch : g_reduce_chb) : auto_chb(cch);
+  const int slices = cdiv(cch, CHB);
+  const int RP = 256 / CHB;
+  // aim for ~g_reduce_blocks blocks in total, at least 4 row passes per block
+  long rblocks = (g_reduce_blocks > 0 ? g_reduce_blocks : (C <= 256 ? 2048 : 1024)) / slices;
+  if (rblocks < 1) rblocks = 1;
+  long rpb = (rows + rblocks - 1) / rblocks;
+  if (rpb < 4L * RP) rpb = 4L * RP;
+  rblocks = (rows + rpb - 1) / rpb;
+  return RedGrid{dim3((unsigned)rblocks, slices), rpb, CHB};
+}
 
 int grid_for(long work, int per_block = 256, int cap = 4096) {
   long b = (work + per_block - 1) / per_block;
@@ -471,18 +558,9 @@ int bn_apply_launch(const bf16_t* y, const float* coef, const bf16_t* res, bf16_
 
 int bn_bwd_reduce_launch(const bf16_t* g, const bf16_t* y, const float* coef, const bf16_t* res,
                          bf16_t* dz_out, long rows, int C, int act, float* part, int G, int ldg, hipStream_t s) {
-  const int cch = C / 8;
-  const int CHB = cch < 256 ? cch : 256;
-  const int slices = cdiv(cch, CHB);
-  const int RP = 256 / CHB;
-  // aim for ~g_reduce_blocks blocks in total, at least 4 row passes per block
-  long rblocks = (g_reduce_blocks > 0 ? g_reduce_blocks : (C <= 256 ? 2048 : 1024)) / slices;
-  if (rblocks < 1) rblocks = 1;
-  long rpb = (rows + rblocks - 1) / rblocks;
-  if (rpb < 4L * RP) rpb = 4L * RP;
-  rblocks = (rows + rpb - 1) / rpb;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3((unsigned)rblocks, slices), dim3(256), 0, s, g, y, coef, res,
-                     dz_out, rows, C, act, rpb, part, G, ldg > 0 ? ldg : C);
+  const RedGrid rg = reduce_grid(rows, C);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, rg.grid, dim3(256), 0, s, g, y, coef, res, dz_out, rows, C, act,
+                     rg.rpb, part, G, ldg > 0 ? ldg : C, rg.chb);
   HIP_CHECK_LAUNCH();
   return 0;
 }
@@ -504,18 +582,24 @@ int bn_bwd_elemt_launch(const bf16_t* g, const bf16_t* y, const float* coef, con
 }
 
 int bn_stats_launch(const bf16_t* y, long rows, int C, float* part, int G, hipStream_t s) {
-  const int cch = C / 8;
-  const int CHB = cch < 256 ? cch : 256;
-  const int slices = cdiv(cch, CHB);
-  const int RP = 256 / CHB;
-  long rblocks = (g_reduce_blocks > 0 ? g_reduce_blocks : (C <= 256 ? 2048 : 1024)) / slices;
-  if (rblocks < 1) rblocks = 1;
-  long rpb = (rows + rblocks - 1) / rblocks;
-  if (rpb < 4L * RP) rpb = 4L * RP;
-  rblocks = (rows + rpb - 1) / rpb;
-  hipLaunchKernelGGL(bn_stats_kernel, dim3((unsigned)rblocks, slices), dim3(256), 0, s, y, rows, C, rpb, part, G);
+  const RedGrid rg = reduce_grid(rows, C);
+  hipLaunchKernelGGL(bn_stats_kernel, rg.grid, dim3(256), 0, s, y, rows, C, rg.rpb, part, G, rg.chb);
   HIP_CHECK_LAUNCH();
   return 0;
 }
 
-void bn_set_reduce_blocks(int n) { g_reduce_blocks = n > 0 ? n : 0; }
+// geo = {H, W, OH, OW, kh, kw, sh, sw, ph, pw} of the max pool over act(BN(y)), y = [N, H, W, C]
+int bn_act_maxpool_launch(const bf16_t* y, const float* coef, bf16_t* out, uint8_t* idx, int N, int C,
+                          const int* geo, int act, hipStream_t s) {
+  const PoolWin g{geo[0], geo[1], geo[2], geo[3], geo[4], geo[5], geo[6], geo[7], geo[8], geo[9]};
+  const long work = (long)N * g.OH * g.OW * (C / 8);
+  hipLaunchKernelGGL(bn_act_maxpool_kernel, dim3(grid_for(work, 256, 8192)), dim3(256), 0, s, y, coef, out, idx, N,
+                     C, g, act);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+void bn_set_reduce_blocks(int n, int chb) {
+  g_reduce_blocks = n > 0 ? n : 0;
+  g_reduce_chb = chb > 0 ? chb : 0;
+}

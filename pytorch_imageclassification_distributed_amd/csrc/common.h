@@ -92,6 +92,23 @@ DEVI float act_grad(float z, float g, int act) {
 
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
+// x / d for 32-bit x by a runtime divisor: one mul_hi + add + shift (Granlund-Montgomery round-up
+// method with a 33-bit sum; exact for every 32-bit x - tests/test_native_math.py checks the formula)
+struct FastDiv {
+  uint32_t d, m, l;
+};
+
+static inline FastDiv make_fastdiv(uint32_t d) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  const uint64_t m = ((1ull << 32) * ((1ull << l) - d)) / d + 1;
+  return FastDiv{d, (uint32_t)m, l};
+}
+
+DEVI uint32_t fdiv(uint32_t x, const FastDiv& f) {
+  return (uint32_t)(((uint64_t)__umulhi(x, f.m) + x) >> f.l);
+}
+
 // out[n][c] (+)= scale * sum_{p in split} a[n][p][c] (* b[n][p][c] when PROD), NHWC bf16 inputs, fp32 out.
 // block = CHB channel-chunk lanes (8 channels each) x RP pixel lanes, LDS tree over RP; grid =
 // (N, channel slices, pixel splits); splits > 1 accumulate with one atomic per channel per block.

@@ -91,6 +91,60 @@ __global__ void maxpool_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t*
   }
 }
 
+// Windows with (k-1)/s <= 1 (the 3x3 stride-2 pools of the ResNet / Inception stems and blocks): at most
+// 2 x 2 outputs cover a pixel, so all four candidates' loads are issued together (clamped addresses,
+// masked values) instead of a dependent load chain per window, and the index math is 32-bit with
+// multiply-shift division.
+struct PoolDiv {
+  FastDiv cch, W, H, sh, sw;
+};
+
+__global__ void maxpool_bwd2x2_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                      bf16_t* __restrict__ dx, PoolGeom g, PoolDiv fd, uint32_t total) {
+  const int cch = g.C >> 3;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const uint32_t row = fdiv(i, fd.cch);
+    const int c0 = (int)(i - row * cch) * 8;
+    const uint32_t t = fdiv(row, fd.W);
+    const int w = (int)(row - t * g.W);
+    const uint32_t n = fdiv(t, fd.H);
+    const int h = (int)(t - n * g.H);
+    const int hp = h + g.ph, wp = w + g.pw;
+    const int oh1 = (int)fdiv((uint32_t)hp, fd.sh), ow1 = (int)fdiv((uint32_t)wp, fd.sw);
+    const int rh1 = hp - oh1 * g.sh, rw1 = wp - ow1 * g.sw;  // window offsets of (h, w) in outputs oh1, ow1
+    uint4 v[4];
+    uint2 pk[4];
+    bool ok[4];
+    int me[4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int oh = oh1 - a, ow = ow1 - b, r = rh1 + a * g.sh, c = rw1 + b * g.sw, j = a * 2 + b;
+        ok[j] = oh >= 0 && oh < g.OH && ow >= 0 && ow < g.OW && r < g.kh && c < g.kw;
+        me[j] = r * g.kw + c;
+        const int ohc = min(max(oh, 0), g.OH - 1), owc = min(max(ow, 0), g.OW - 1);
+        const long o = (((long)n * g.OH + ohc) * g.OW + owc) * g.C + c0;
+        v[j] = *(const uint4*)(dy + o);
+        pk[j] = *(const uint2*)(idx + o);
+      }
+    }
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!ok[j]) continue;
+      float f[8];
+      unpack8(v[j], f);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if ((int)((pk[j].x >> (8 * k)) & 0xff) == me[j]) acc[k] += f[k];
+        if ((int)((pk[j].y >> (8 * k)) & 0xff) == me[j]) acc[4 + k] += f[4 + k];
+      }
+    }
+    *(uint4*)(dx + (long)row * g.C + c0) = pack8(acc);
+  }
+}
+
 __global__ void avgpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, PoolGeom g) {
   const int cch = g.C >> 3;
   const long total = (long)g.N * g.OH * g.OW * cch;
@@ -187,8 +241,14 @@ int maxpool_fwd_launch(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, i
 int maxpool_bwd_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W, int C, int OH,
                        int OW, int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t s) {
   PoolGeom g{N, H, W, C, OH, OW, kh, kw, sh, sw, ph, pw};
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for((long)N * H * W * (C / 8))), dim3(256), 0, s, dy, idx,
-                     dx, g);
+  const long total = (long)N * H * W * (C / 8);
+  if ((kh - 1) / sh <= 1 && (kw - 1) / sw <= 1 && total < (1L << 31)) {
+    const PoolDiv fd{make_fastdiv(C / 8), make_fastdiv(W), make_fastdiv(H), make_fastdiv(sh), make_fastdiv(sw)};
+    hipLaunchKernelGGL(maxpool_bwd2x2_kernel, dim3(grid_for(total)), dim3(256), 0, s, dy, idx, dx, g, fd,
+                       (uint32_t)total);
+  } else {
+    hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, s, dy, idx, dx, g);
+  }
   HIP_CHECK_LAUNCH();
   return 0;
 }

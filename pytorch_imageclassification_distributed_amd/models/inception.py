@@ -28,11 +28,13 @@ class BasicConv2d(nn.Module):
         self.conv = nn.Conv2d(cin, cout, bias=False, **kw)
         self.bn = nn.BatchNorm2d(cout, eps=0.001)
 
-    def forward(self, x, exclusive=False, slot=None, out=None):
+    def forward(self, x, exclusive=False, slot=None, out=None, pool=None):
         """``exclusive``: this conv is the only consumer of ``x`` (a chain-internal conv), which lets its
         dgrad epilogue run the producer's BN-backward reduce; ``slot``: x feeds exactly two convs;
-        ``out``: (concat plan, branch) - write the result into the block's concat output in place."""
-        return Fx.conv_bn_act(x, self.conv, self.bn, "relu", x_slot=slot, exclusive_input=exclusive, out=out)
+        ``out``: (concat plan, branch) - write the result into the block's concat output in place;
+        ``pool``: (kernel, stride, padding) of a max pool applied to the result (stem)."""
+        return Fx.conv_bn_act(x, self.conv, self.bn, "relu", x_slot=slot, exclusive_input=exclusive, out=out,
+                              pool=pool)
 
 
 class InceptionA(nn.Module):
@@ -215,11 +217,9 @@ class Inception3(nn.Module):
         x = self._transform_input(x)
         x = self.Conv2d_1a_3x3(x)
         x = self.Conv2d_2a_3x3(x, True)
-        x = self.Conv2d_2b_3x3(x, True)
-        x = Fx.max_pool2d(x, 3, 2, 0)
+        x = self.Conv2d_2b_3x3(x, True, pool=(3, 2, 0))
         x = self.Conv2d_3b_1x1(x)
-        x = self.Conv2d_4a_3x3(x, True)
-        x = Fx.max_pool2d(x, 3, 2, 0)
+        x = self.Conv2d_4a_3x3(x, True, pool=(3, 2, 0))
         x = self.Mixed_5b(x)
         x = self.Mixed_5c(x)
         x = self.Mixed_5d(x)

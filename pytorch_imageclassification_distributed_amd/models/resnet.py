@@ -111,8 +111,7 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward_features(self, x):
-        x = Fx.conv_bn_act(x, self.conv1, self.bn1, "relu")
-        x = Fx.max_pool2d(x, 3, 2, 1)
+        x = Fx.conv_bn_act(x, self.conv1, self.bn1, "relu", pool=(3, 2, 1))  # conv1-bn1-relu-maxpool
         x = self.layer1(x)
         x = self.layer2(x)
         x = self.layer3(x)

@@ -112,13 +112,21 @@ def grad_slot(x, n: int = 2):
 
 
 def conv_bn_act(x, conv, bn, act="relu", residual=None, x_slot=None, res_slot=None, exclusive_input=False,
-                out=None):
+                out=None, pool=None):
     """act(bn(conv(x)) [+ residual]).
 
     Reference equivalents: torchvision ``BasicConv2d`` (conv -> BN -> ReLU),
     ResNet ``Bottleneck``/``BasicBlock`` tails (BN -> +identity -> ReLU) and
     efficientnet_pytorch ``MBConvBlock`` (conv -> BN -> swish).
+    ``pool`` = (kernel, stride, padding): a max pool follows the activation (the ResNet / Inception
+    stems); the HIP path fuses it into the BN passes.
     """
+    if pool is not None:  # stem: max_pool2d(act(bn(conv(x))), *pool) - kernel, stride, padding
+        if residual is not None or x_slot is not None or out is not None:
+            raise ValueError("conv_bn_act(pool=...) takes a plain conv -> BN -> act")
+        if use_hip(x):
+            return _hip().conv_bn_act_pool(x, conv, bn, act, pool, exclusive_input)
+        return F.max_pool2d(_act(_torch_bn(_torch_conv(x, conv), bn), act), *pool)
     if use_hip(x):
         hout = (out[0].hip(), out[1]) if (out is not None and _hip().CONCAT_INPLACE) else None
         return _hip().conv_bn_act(x, conv, bn, act, residual, x_slot, res_slot, exclusive_input, hout)

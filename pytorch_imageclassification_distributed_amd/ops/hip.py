@@ -803,6 +803,57 @@ class DwConvFn(torch.autograd.Function):
 # ---------------------------------------------------------------------------
 # BatchNorm (+ residual) (+ activation)
 # ---------------------------------------------------------------------------
+def _bn_coef(y, gamma, beta, bn, stats_ready):
+    """Batch (training) or running (eval) statistics of ``y`` -> coef [4, C] = scale, shift, mean, invstd.
+    Returns (coef, SyncBN group or None, all-reduced count tensor or None)."""
+    dev = y.device
+    n, c, h, w = y.shape
+    rows = n * h * w
+    coef = torch.empty(4 * c, dtype=torch.float32, device=dev)
+    group = count_t = None
+    if bn.training:
+        grp = stat_groups(rows)
+        part = ws(dev).stats_buf(c, grp)
+        if not stats_ready:
+            C.bn_stats(y, rows, c, part, grp)
+        group = _sync_group(bn)
+        mom = bn.momentum if bn.momentum is not None else 0.1
+        track = bn.track_running_stats and bn.running_mean is not None
+        rs = (bn.running_mean, bn.running_var, bn.num_batches_tracked) if track else (None, None, None)
+        if group is None:  # one launch: partial rows -> coefficients + running stats
+            C.bn_reduce_finalize(part, grp, c, float(rows), gamma, beta, *rs, mom, bn.eps, coef)
+        else:
+            sums = torch.empty(2 * c + 1, dtype=torch.float64, device=dev)
+            C.bn_partials(part, grp, c, sums, None, None, float(rows))  # + local count in the tail
+            dist.all_reduce(sums, group=group)
+            count_t = sums[2 * c:]
+            C.bn_finalize(sums, count_t, float(rows), gamma, beta, *rs, mom, bn.eps, c, coef)
+    else:
+        if stats_ready:
+            raise RuntimeError("eval-mode BN received fused statistics")
+        C.bn_eval_coef(gamma, beta, bn.running_mean, bn.running_var, bn.eps, c, coef)
+    return coef, group, count_t
+
+
+def _bn_bwd_k(part, grp, c, rows, training, group, count_t, params, dev):
+    """BN-backward partial rows -> (k [2, C] for bn_bwd_elemt, dgamma, dbeta); SyncBN all-reduces the sums."""
+    k = torch.empty(2 * c, dtype=torch.float32, device=dev)
+    dgamma = grad_buffer(params[0], zero=False)
+    dbeta = grad_buffer(params[1], zero=False)
+    if training and group is None:  # one launch: partial rows -> dgamma, dbeta, k
+        C.bn_reduce_bwd(part, grp, c, float(rows), dgamma, dbeta, k)
+        return k, dgamma, dbeta
+    sums = torch.empty(2 * c, dtype=torch.float64, device=dev)
+    C.bn_partials(part, grp, c, sums, dgamma, dbeta)
+    if group is not None:
+        dist.all_reduce(sums, group=group)
+    if training:
+        C.bn_bwd_k(sums, count_t, float(rows), c, k)
+    else:  # running statistics are constants: dy = scale * dz
+        k.zero_()
+    return k, dgamma, dbeta
+
+
 class BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, y, gamma, beta, res, bn, act, stats_ready, res_slot=None, link=None, cat=None):
@@ -810,30 +861,7 @@ class BNActFn(torch.autograd.Function):
         n, c, h, w = y.shape
         rows = n * h * w
         a = ACT[act]
-        coef = torch.empty(4 * c, dtype=torch.float32, device=dev)
-        group = None
-        count_t = None
-        grp = stat_groups(rows)
-        if bn.training:
-            part = ws(dev).stats_buf(c, grp)
-            if not stats_ready:
-                C.bn_stats(y, rows, c, part, grp)
-            group = _sync_group(bn)
-            mom = bn.momentum if bn.momentum is not None else 0.1
-            track = bn.track_running_stats and bn.running_mean is not None
-            rs = (bn.running_mean, bn.running_var, bn.num_batches_tracked) if track else (None, None, None)
-            if group is None:  # one launch: partial rows -> coefficients + running stats
-                C.bn_reduce_finalize(part, grp, c, float(rows), gamma, beta, *rs, mom, bn.eps, coef)
-            else:
-                sums = torch.empty(2 * c + 1, dtype=torch.float64, device=dev)
-                C.bn_partials(part, grp, c, sums, None, None, float(rows))  # + local count in the tail
-                dist.all_reduce(sums, group=group)
-                count_t = sums[2 * c:]
-                C.bn_finalize(sums, count_t, float(rows), gamma, beta, *rs, mom, bn.eps, c, coef)
-        else:
-            if stats_ready:
-                raise RuntimeError("eval-mode BN received fused statistics")
-            C.bn_eval_coef(gamma, beta, bn.running_mean, bn.running_var, bn.eps, c, coef)
+        coef, group, count_t = _bn_coef(y, gamma, beta, bn, stats_ready)
         if cat is not None:  # write straight into this branch's channel slice of the concat output
             cbuf, idx = cat
             base = cbuf.ensure(n, h, w, dev)
@@ -883,26 +911,13 @@ class BNActFn(torch.autograd.Function):
             part = ws(dev).stats_buf(c, grp)
             dz = torch.empty_like(y, memory_format=CL) if ctx.has_res else None
             C.bn_bwd_reduce(g, y, coef, res, dz, rows, c, ctx.act, part, grp, ldg)
-        k = torch.empty(2 * c, dtype=torch.float32, device=dev)
         if pending is not None:  # SyncBN all-reduce launched early by the consuming conv's backward
             sums, work, dgamma, dbeta = pending
             work.wait()
+            k = torch.empty(2 * c, dtype=torch.float32, device=dev)
             C.bn_bwd_k(sums, ctx.count_t, float(rows), c, k)
-        elif ctx.training and ctx.group is None:  # one launch: partial rows -> dgamma, dbeta, k
-            dgamma = grad_buffer(ctx.params[0], zero=False)
-            dbeta = grad_buffer(ctx.params[1], zero=False)
-            C.bn_reduce_bwd(part, grp, c, float(rows), dgamma, dbeta, k)
         else:
-            dgamma = grad_buffer(ctx.params[0], zero=False)
-            dbeta = grad_buffer(ctx.params[1], zero=False)
-            sums = torch.empty(2 * c, dtype=torch.float64, device=dev)
-            C.bn_partials(part, grp, c, sums, dgamma, dbeta)
-            if ctx.group is not None:
-                dist.all_reduce(sums, group=ctx.group)
-            if ctx.training:
-                C.bn_bwd_k(sums, ctx.count_t, float(rows), c, k)
-            else:  # running statistics are constants: dy = scale * dz
-                k.zero_()
+            k, dgamma, dbeta = _bn_bwd_k(part, grp, c, rows, ctx.training, ctx.group, ctx.count_t, ctx.params, dev)
         if link is not None and link.done:
             ws(dev).give_part(part)
         dy = torch.empty_like(y, memory_format=CL)
@@ -912,6 +927,68 @@ class BNActFn(torch.autograd.Function):
         if dres is not None and ctx.res_slot is not None:
             dres = ctx.res_slot.deliver(dres)
         return dy, dgamma, dbeta, dres, None, None, None, None, None, None
+
+
+class BNActPoolFn(torch.autograd.Function):
+    """maxpool(act(BN(y))) for network stems (ResNet conv1 -> bn1 -> relu -> maxpool 3/2/1, Inception
+    Conv2d_2b / Conv2d_4a -> maxpool 3/2/0).  The forward pools straight from ``y`` (the
+    full-resolution activation is never written or re-read).  The backward is maxpool_bwd -> BN backward:
+    gathering the pooled gradient inside both BN-backward passes measured slower (docs/DESIGN.md)."""
+
+    @staticmethod
+    def forward(ctx, y, gamma, beta, bn, act, stats_ready, pool):
+        dev = y.device
+        n, c, h, w = y.shape
+        (kh, kw), (sh, sw), (ph, pw) = pool
+        oh = (h + 2 * ph - kh) // sh + 1
+        ow = (w + 2 * pw - kw) // sw + 1
+        a = ACT[act]
+        coef, group, count_t = _bn_coef(y, gamma, beta, bn, stats_ready)
+        out = _empty_cl(n, c, oh, ow, dev)
+        idx = torch.empty((n, oh, ow, c), dtype=torch.uint8, device=dev)
+        geo = [h, w, oh, ow, kh, kw, sh, sw, ph, pw]
+        C.bn_act_maxpool(y, coef, out, idx, n, c, geo, a)
+        ctx.act, ctx.group, ctx.count_t, ctx.geo = a, group, count_t, geo
+        ctx.training = bn.training
+        ctx.params = (gamma, beta)
+        ctx.save_for_backward(y, coef, idx)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        y, coef, idx = ctx.saved_tensors
+        dev = y.device
+        n, c, h, w = y.shape
+        rows = n * h * w
+        _, _, oh, ow, kh, kw, sh, sw, ph, pw = ctx.geo
+        g = _empty_cl(n, c, h, w, dev)
+        C.maxpool_bwd(_cl(gout), idx, g, n, h, w, c, oh, ow, kh, kw, sh, sw, ph, pw)
+        grp = stat_groups(rows)
+        part = ws(dev).stats_buf(c, grp)
+        C.bn_bwd_reduce(g, y, coef, None, None, rows, c, ctx.act, part, grp)
+        k, dgamma, dbeta = _bn_bwd_k(part, grp, c, rows, ctx.training, ctx.group, ctx.count_t, ctx.params, dev)
+        dy = torch.empty_like(y, memory_format=CL)
+        C.bn_bwd_elemt(g, y, coef, k, None, None, dy, rows, c, ctx.act)
+        return dy, dgamma, dbeta, None, None, None, None
+
+
+STEM_POOL_FUSE = os.environ.get("IMGCLS_STEM_POOL_FUSE", "1") == "1"
+
+
+def conv_bn_act_pool(x, conv, bn, act, pool, exclusive_input=False):
+    """max_pool2d(act(bn(conv(x))), *pool) with the pool fused into the BN passes (stems).
+    ``exclusive_input`` as for ``conv_bn_act`` (the conv's dgrad may run x's producer BN reduce)."""
+    k, s, p = _pool_args(*pool)
+    if not STEM_POOL_FUSE or k[0] * k[1] > 255 or 2 * p[0] > k[0] or 2 * p[1] > k[1]:
+        return max_pool2d(conv_bn_act(x, conv, bn, act, None, exclusive_input=exclusive_input), *pool)
+    ensure_channels_last_weight(conv)
+    if stem_s2d_eligible(x, conv) and not x.requires_grad:
+        y = StemS2dFn.apply(x, conv.weight, conv, bn.training)
+    else:
+        if conv.groups != 1 or conv.bias is not None:
+            raise NotImplementedError("conv_bn_act_pool: grouped conv / conv bias")
+        y = ConvFn.apply(_cl(x), conv.weight, conv, bn.training, None, exclusive_input and FUSE_BN_BWD)
+    return BNActPoolFn.apply(y, bn.weight, bn.bias, bn, act, bn.training, (k, s, p))
 
 
 def conv_bn_act(x, conv, bn, act, residual, x_slot=None, res_slot=None, exclusive_input=False, out=None):

@@ -1,11 +1,22 @@
 """Longest individual kernel launches of ONE steady-state step (rocprofv3 kernel trace).
 
-usage: python scripts/step_launches.py gpurun_out/prof_q/hip_kernel_trace.csv [top=40] [filter-regex]"""
+usage: python scripts/step_launches.py gpurun_out/prof_q/hip_kernel_trace.csv|run_results.db [top=40] [filter-regex]"""
 import csv
 import re
 import sys
 
-rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
+
+def _load(path):
+    """kernel_trace.csv (rocprofv3 --output-format csv) or the rocpd SQLite database (its default)."""
+    if path.endswith(".db"):
+        import sqlite3
+        q = ("select name, start, end, grid_x, grid_y, workgroup_x from kernels order by start")
+        keys = ("Kernel_Name", "Start_Timestamp", "End_Timestamp", "Grid_Size_X", "Grid_Size_Y", "Workgroup_Size_X")
+        return [dict(zip(keys, map(str, r))) for r in sqlite3.connect(path).execute(q)]
+    return list(csv.DictReader(open(path)))
+
+
+rows = sorted(_load(sys.argv[1]), key=lambda r: int(r["Start_Timestamp"]))
 top = int(sys.argv[2]) if len(sys.argv) > 2 else 40
 flt = re.compile(sys.argv[3]) if len(sys.argv) > 3 else None
 idx = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"]]

@@ -295,6 +295,74 @@ def test_depthwise_bn_silu():
         assert rel_err(conv.weight.grad, wr.grad) < 3e-2
 
 
+@pytest.mark.parametrize("case", [
+    # N, Cin, H, Cout, conv k/s/p, pool k/s/p
+    (2, 3, 64, 64, (7, 2, 3), (3, 2, 1)),     # ResNet stem (space-to-depth conv path)
+    (2, 32, 35, 64, (3, 1, 1), (3, 2, 0)),    # Inception Conv2d_2b -> maxpool (odd size, no padding)
+    (1, 16, 17, 48, (3, 1, 0), (3, 2, 1)),
+])
+def test_conv_bn_act_pool(case):
+    """Stem fusion: max_pool2d(relu(bn(conv(x)))) - forward, running stats and every gradient, against
+    the fp32 reference and (tightly) against the unfused HIP composition conv_bn_act -> max_pool2d."""
+    import copy
+    hip = _hip()
+    n, cin, h, co, (k, s, p), pool = case
+    torch.manual_seed(7)
+    conv = nn.Conv2d(cin, co, k, s, p, bias=False).to(DEV).to(memory_format=CL)
+    bn = nn.BatchNorm2d(co).to(DEV)
+    with torch.no_grad():
+        conv.weight.copy_(bf(conv.weight))
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    conv_u, bn_u = copy.deepcopy(conv), copy.deepcopy(bn)
+    conv_r = nn.Conv2d(cin, co, k, s, p, bias=False).to(DEV)
+    bn_r = nn.BatchNorm2d(co).to(DEV)
+    conv_r.load_state_dict(conv.state_dict())
+    bn_r.load_state_dict(bn.state_dict())
+    x = bf(torch.randn(n, cin, h, h, device=DEV))
+    stem = cin == 3
+
+    def inp():
+        return x if stem else x.to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
+
+    xb, xu = inp(), inp()
+    out = hip.conv_bn_act_pool(xb, conv, bn, "relu", pool)
+    unf = hip.max_pool2d(hip.conv_bn_act(xu, conv_u, bn_u, "relu", None), *pool)
+    xr = x.clone().requires_grad_(not stem)
+    yc = conv_r(xr)
+    yc = yc + (bf(yc) - yc).detach()
+    act = F.relu(bn_r(yc))
+    # pooled at bf16, as the unfused bn_apply -> maxpool path stores the activation: bf16 ties pick the
+    # same (first) window position in both
+    ref = F.max_pool2d(act + (bf(act) - act).detach(), *pool)
+    assert out.shape == ref.shape
+    assert torch.equal(out, unf)
+    assert rel_err(out, ref) < 2e-2
+    assert torch.allclose(bn.running_mean, bn_r.running_mean, rtol=1e-2, atol=1e-3)
+    assert torch.allclose(bn.running_var, bn_r.running_var, rtol=1e-2, atol=1e-3)
+    g = bf(torch.randn_like(ref))
+    gb = g.to(torch.bfloat16).contiguous(memory_format=CL)
+    out.backward(gb)
+    unf.backward(gb)
+    ref.backward(g)
+    # the fused gather matches the unfused maxpool_bwd -> BN backward (which rounds the full-resolution
+    # gradient to bf16 in between)
+    for a_, b_ in ((bn.weight.grad, bn_u.weight.grad), (bn.bias.grad, bn_u.bias.grad),
+                   (conv.weight.grad, conv_u.weight.grad)) + (() if stem else ((xb.grad, xu.grad),)):
+        assert rel_err(a_, b_) < 1e-2
+    # vs fp32: a 1-ulp difference in the bf16 conv output can flip relu'(z) at |z| ~ 0 for a routed pixel;
+    # the max-pool concentrates the gradient, so single elements move - compare mean errors
+    for a_, b_ in ((bn.weight.grad, bn_r.weight.grad), (bn.bias.grad, bn_r.bias.grad),
+                   (conv.weight.grad, conv_r.weight.grad)) + (() if stem else ((xb.grad, xr.grad),)):
+        assert mean_err(a_, b_) < 6e-2  # (the unfused path, checked equal above, measures the same)
+    bn.eval()
+    bn_u.eval()
+    with torch.no_grad():
+        fused = hip.conv_bn_act_pool(xb.detach() if not stem else xb, conv, bn, "relu", pool)
+        plain = hip.max_pool2d(hip.conv_bn_act(xb.detach() if not stem else xb, conv, bn, "relu", None), *pool)
+    assert torch.equal(fused, plain)
+
+
 @pytest.mark.parametrize("kind", ["max311", "max320", "avg311", "avg530"])
 def test_pools(kind):
     hip = _hip()
