@@ -32,6 +32,7 @@ int bn_bwd_k_launch(const double*, const double*, double, int, float*, hipStream
 int bn_bwd_elemt_launch(const bf16_t*, const bf16_t*, const float*, const float*, const bf16_t*, const bf16_t*,
                         bf16_t*, long, int, int, int, hipStream_t);
 int bn_act_maxpool_launch(const bf16_t*, const float*, bf16_t*, uint8_t*, int, int, const int*, int, hipStream_t);
+int stem_s2d_conv_launch(const bf16_t*, const bf16_t*, bf16_t*, float*, int, int, int, int, hipStream_t);
 int maxpool_fwd_launch(const bf16_t*, bf16_t*, uint8_t*, int, int, int, int, int, int, int, int, int, int, int,
                        int, hipStream_t);
 int maxpool_bwd_launch(const bf16_t*, const uint8_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int,
@@ -288,6 +289,25 @@ void bn_act_maxpool(Tensor y, Tensor coef, Tensor out, Tensor idx, int64_t N, in
   check(bn_act_maxpool_launch(ptr<bf16_t>(y), ptr<float>(coef), ptr<bf16_t>(out), ptr<uint8_t>(idx), (int)N, (int)C,
                               g.data(), act, cur()),
         "bn_act_maxpool");
+}
+
+// ResNet stem on the space-to-depth input: x [N, H, W, 16] bf16, w [64, 256] bf16, y [N, H, W, 64] bf16,
+// part: BN statistics rows [G, 2, 64] (or None)
+void stem_conv(Tensor x, Tensor w, Tensor y, OT part, int G, int64_t N, int64_t H, int64_t W) {
+  req(x, BF, "x"); req(w, BF, "w"); req(y, BF, "y");
+  TORCH_CHECK(N > 0 && H > 0 && W > 0 && N * H * W < (1LL << 31), "stem_conv: bad geometry");
+  TORCH_CHECK(x.numel() == N * H * W * 16 && w.numel() == 64 * 256 && y.numel() == N * H * W * 64,
+              "stem_conv: tensor sizes do not match [N,H,W,16] x [64,256] -> [N,H,W,64]");
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast) || x.is_contiguous(), "stem_conv: x must be dense");
+  TORCH_CHECK(y.is_contiguous(at::MemoryFormat::ChannelsLast) || y.is_contiguous(), "stem_conv: y must be dense");
+  float* pp = nullptr;
+  if (part.has_value() && part->defined()) {
+    req(*part, F32, "part");
+    TORCH_CHECK(G > 0 && part->numel() >= (int64_t)G * 2 * 64, "stem_conv: part [G, 2, 64]");
+    pp = part->data_ptr<float>();
+  }
+  check(stem_s2d_conv_launch(ptr<bf16_t>(x), ptr<bf16_t>(w), ptr<bf16_t>(y), pp, G, (int)N, (int)H, (int)W, cur()),
+        "stem_conv");
 }
 
 void maxpool_fwd(Tensor x, Tensor y, OT idx, int N, int H, int W, int C, int OH, int OW, int kh, int kw, int sh,
@@ -562,6 +582,7 @@ PYBIND11_MODULE(_C, m) {
   register_loader(m);
   m.def("bn_set_reduce_blocks", &bn_set_reduce_blocks, pybind11::arg("n"), pybind11::arg("chb") = 0);
   m.def("bn_act_maxpool", &bn_act_maxpool);
+  m.def("stem_conv", &stem_conv);
   m.def("conv_fp8_cfgs", []() {
     std::vector<std::vector<int>> out;
     for (int i = 0; i < conv_num_fp8_cfgs(); ++i) {

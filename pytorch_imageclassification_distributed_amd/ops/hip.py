@@ -699,6 +699,7 @@ class ConvFn(torch.autograd.Function):
 # 64-wide k-step of the implicit GEMM is 4 adjacent pixels x 16 channels = 128 contiguous bytes
 # (the 8-channel form gathers 16-byte pieces).
 STEM_S2D = os.environ.get("IMGCLS_STEM_S2D", "1") == "1"
+STEM_DIRECT = os.environ.get("IMGCLS_STEM_DIRECT", "1") == "1"  # stem.hip instead of the implicit GEMM
 _S2D_INDEX: dict = {}
 
 
@@ -748,8 +749,13 @@ class StemS2dFn(torch.autograd.Function):
         idx = _s2d_index(x.device)
         wq = torch.zeros(co, 256, dtype=BF16, device=x.device)
         wq[:, idx] = weight_bf16(w).view(co, 147)
-        stats = ws(x.device).stats_buf(co, stat_groups(g.N * g.OH * g.OW)) if want_stats else None
-        y = conv_forward_raw(xs, None, g, stats=stats, wb=wq.view(-1))
+        grp = stat_groups(g.N * g.OH * g.OW)
+        stats = ws(x.device).stats_buf(co, grp) if want_stats else None
+        if STEM_DIRECT and co == 64:  # halo-tile direct kernel (csrc/stem.hip)
+            y = _empty_cl(g.N, co, g.OH, g.OW, x.device)
+            C.stem_conv(xs, wq, y, stats, grp, g.N, g.OH, g.OW)
+        else:
+            y = conv_forward_raw(xs, None, g, stats=stats, wb=wq.view(-1))
         ctx.g = g
         ctx.save_for_backward(xs, w)
         return y

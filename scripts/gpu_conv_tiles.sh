@@ -9,3 +9,6 @@ echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_conv.log; fatal $rc pytest
 [ $rc -eq 0 ] || exit 1
 timeout -k 10 500 python benchmarks/conv_bench.py --batch ${CONV_BATCH:-512} --tune-log $CONV_ARGS > gpurun_out/conv_tiles.txt 2>&1; rc=$?
 echo "conv_bench rc=$rc"; grep -v '^{' gpurun_out/conv_tiles.txt | tail -80; fatal $rc conv_bench
+[ "${CONV_BENCH_TOO:-0}" = 1 ] || exit 0
+timeout -k 10 400 python bench.py --steps 20 --warmup 8 > gpurun_out/bench_r50.log 2>&1; rc=$?
+echo "bench rc=$rc"; tail -1 gpurun_out/bench_r50.log | cut -c1-200; fatal $rc bench

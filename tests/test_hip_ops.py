@@ -199,6 +199,38 @@ def test_stem_space_to_depth(hw):
     assert rel_err(bn.weight.grad, bn_r.weight.grad) < 3e-2
 
 
+@pytest.mark.parametrize("hw", [(224, 224), (36, 50), (30, 18)])
+def test_stem_direct_matches_gemm(hw):
+    """The halo-tile stem kernel (csrc/stem.hip, partial edge tiles included) against the implicit-GEMM
+    path on the same space-to-depth input: output and fused BN statistics."""
+    hip = _hip()
+    torch.manual_seed(6)
+    h, w = hw
+    n = 3
+    x = torch.randn(n, 3, h, w, device=DEV)
+    xs = hip._empty_cl(n, 16, h // 2, w // 2, DEV)
+    hip.C.prepare_input_s2d(x, xs, n, h, w)
+    g = hip._s2d_geom(n, h, w, 64)
+    idx = hip._s2d_index(torch.device(DEV))  # KRSC position r*21 + s*3 + c -> s2d weight column
+    wq = torch.zeros(64, 256, device=DEV)
+    wq[:, idx] = torch.randn(64, 147, device=DEV) * 0.05  # taps outside the 7x7 window stay zero
+    wq = wq.to(torch.bfloat16)
+    m = g.N * g.OH * g.OW
+    grp = hip.stat_groups(m)
+    st_d = torch.zeros(grp * 2 * 64, device=DEV)
+    y_d = hip._empty_cl(n, 64, g.OH, g.OW, DEV)
+    hip.C.stem_conv(xs, wq.view(-1), y_d, st_d, grp, n, g.OH, g.OW)
+    st_g = torch.zeros(grp * 2 * 64, device=DEV)
+    y_g = hip.conv_forward_raw(xs, None, g, stats=st_g, wb=wq.view(-1))
+    assert rel_err(y_d, y_g) < 1e-2
+    sd, sg = st_d.view(grp, 2, 64).sum(0), st_g.view(grp, 2, 64).sum(0)
+    assert rel_err(sd[0], sg[0]) < 1e-2 and rel_err(sd[1], sg[1]) < 1e-2
+    # against fp32: the s2d conv equals the 7x7 stride-2 conv of the bf16-rounded image
+    wr = wq.float()[:, idx].view(64, 7, 7, 3).permute(0, 3, 1, 2).contiguous()
+    yr = F.conv2d(bf(x), wr, None, 2, 3)
+    assert rel_err(y_d, yr) < 1e-2
+
+
 @pytest.mark.parametrize("act,use_res", [("relu", False), ("relu", True), (None, False), ("silu", False)])
 def test_conv_bn_act(act, use_res):
     hip = _hip()
