@@ -28,13 +28,14 @@ class BasicConv2d(nn.Module):
         self.conv = nn.Conv2d(cin, cout, bias=False, **kw)
         self.bn = nn.BatchNorm2d(cout, eps=0.001)
 
-    def forward(self, x, exclusive=False, slot=None, out=None, pool=None):
+    def forward(self, x, exclusive=False, slot=None, out=None, pool=None, prepool=None):
         """``exclusive``: this conv is the only consumer of ``x`` (a chain-internal conv), which lets its
         dgrad epilogue run the producer's BN-backward reduce; ``slot``: x feeds exactly two convs;
         ``out``: (concat plan, branch) - write the result into the block's concat output in place;
-        ``pool``: (kernel, stride, padding) of a max pool applied to the result (stem)."""
+        ``pool``: (kernel, stride, padding) of a max pool applied to the result (stem); ``prepool``: of an
+        average pool applied to ``x`` first (``branch_pool``)."""
         return Fx.conv_bn_act(x, self.conv, self.bn, "relu", x_slot=slot, exclusive_input=exclusive, out=out,
-                              pool=pool)
+                              pool=pool, prepool=prepool)
 
 
 class InceptionA(nn.Module):
@@ -54,7 +55,7 @@ class InceptionA(nn.Module):
         b1 = self.branch1x1(x, slot=s, out=(cat, 0))
         b5 = self.branch5x5_2(self.branch5x5_1(x, slot=s), True, out=(cat, 1))
         b3 = self.branch3x3dbl_3(self.branch3x3dbl_2(self.branch3x3dbl_1(x, slot=s), True), True, out=(cat, 2))
-        bp = self.branch_pool(Fx.avg_pool2d(x, 3, 1, 1, slot=s), out=(cat, 3))
+        bp = self.branch_pool(x, slot=s, prepool=(3, 1, 1), out=(cat, 3))
         return Fx.cat_channels([b1, b5, b3, bp], cat)
 
 
@@ -98,7 +99,7 @@ class InceptionC(nn.Module):
         bd = self.branch7x7dbl_1(x, slot=s)
         bd = self.branch7x7dbl_3(self.branch7x7dbl_2(bd, True), True)
         bd = self.branch7x7dbl_5(self.branch7x7dbl_4(bd, True), True, out=(cat, 2))
-        bp = self.branch_pool(Fx.avg_pool2d(x, 3, 1, 1, slot=s), out=(cat, 3))
+        bp = self.branch_pool(x, slot=s, prepool=(3, 1, 1), out=(cat, 3))
         return Fx.cat_channels([b1, b7, bd, bp], cat)
 
 
@@ -145,7 +146,7 @@ class InceptionE(nn.Module):
         bd = self.branch3x3dbl_2(self.branch3x3dbl_1(x, slot=s), True)
         sd = Fx.grad_slot(bd)
         bda, bdb = self.branch3x3dbl_3a(bd, slot=sd, out=(cat, 3)), self.branch3x3dbl_3b(bd, slot=sd, out=(cat, 4))
-        bp = self.branch_pool(Fx.avg_pool2d(x, 3, 1, 1, slot=s), out=(cat, 5))
+        bp = self.branch_pool(x, slot=s, prepool=(3, 1, 1), out=(cat, 5))
         return Fx.cat_channels([b1, b3a, b3b, bda, bdb, bp], cat)
 
 

@@ -112,7 +112,7 @@ def grad_slot(x, n: int = 2):
 
 
 def conv_bn_act(x, conv, bn, act="relu", residual=None, x_slot=None, res_slot=None, exclusive_input=False,
-                out=None, pool=None):
+                out=None, pool=None, prepool=None):
     """act(bn(conv(x)) [+ residual]).
 
     Reference equivalents: torchvision ``BasicConv2d`` (conv -> BN -> ReLU),
@@ -120,7 +120,18 @@ def conv_bn_act(x, conv, bn, act="relu", residual=None, x_slot=None, res_slot=No
     efficientnet_pytorch ``MBConvBlock`` (conv -> BN -> swish).
     ``pool`` = (kernel, stride, padding): a max pool follows the activation (the ResNet / Inception
     stems); the HIP path fuses it into the BN passes.
+    ``prepool`` = (kernel, stride, padding): an average pool (count_include_pad) precedes the conv (the
+    Inception ``branch_pool``); for a 1x1 conv the HIP path runs the conv first and pools its narrower
+    output - both are linear, so conv1x1(avgpool(x)) == avgpool(conv1x1(x)).
     """
+    if prepool is not None:
+        if residual is not None or pool is not None:
+            raise ValueError("conv_bn_act(prepool=...) takes a plain avgpool -> conv -> BN -> act")
+        if use_hip(x):
+            return _hip().pool_conv_bn_act(x, conv, bn, act, prepool, x_slot,
+                                           (out[0].hip(), out[1]) if (out is not None and _hip().CONCAT_INPLACE)
+                                           else None, out)
+        x = F.avg_pool2d(x, *prepool)
     if pool is not None:  # stem: max_pool2d(act(bn(conv(x))), *pool) - kernel, stride, padding
         if residual is not None or x_slot is not None or out is not None:
             raise ValueError("conv_bn_act(pool=...) takes a plain conv -> BN -> act")

@@ -997,6 +997,29 @@ def conv_bn_act_pool(x, conv, bn, act, pool, exclusive_input=False):
     return BNActPoolFn.apply(y, bn.weight, bn.bias, bn, act, bn.training, (k, s, p))
 
 
+POOL_CONV_SWAP = os.environ.get("IMGCLS_POOL_CONV_SWAP", "1") == "1"
+
+
+def pool_conv_bn_act(x, conv, bn, act, prepool, x_slot=None, out=None, out_plan=None):
+    """act(bn(conv(avg_pool2d(x, *prepool)))) (count_include_pad pooling).  A 1x1 stride-1 conv commutes
+    with the pool, so the conv runs first and the pool moves the conv's output: the Inception
+    ``branch_pool`` convs narrow 192-2048 channels to 32-192, so the pool's forward and backward passes
+    move 4-11x fewer bytes, and the conv's dgrad (not an avgpool backward) delivers into the block
+    input's gradient slot.  BN statistics are taken after the pool."""
+    k, s, p = _pool_args(*prepool)
+    pointwise = (tuple(conv.kernel_size) == (1, 1) and tuple(conv.stride) == (1, 1)
+                 and tuple(conv.padding) == (0, 0) and conv.groups == 1 and conv.bias is None
+                 and not getattr(conv, "tf_same", False))
+    if not (POOL_CONV_SWAP and pointwise):
+        from .functional import conv_bn_act as _f_conv_bn_act
+        return _f_conv_bn_act(avg_pool2d(x, *prepool, slot=x_slot), conv, bn, act, out=out_plan)
+    x = _cl(x)
+    ensure_channels_last_weight(conv)
+    y = ConvFn.apply(x, conv.weight, conv, False, x_slot, False)
+    yp = AvgPoolFn.apply(y, k, s, p, None)
+    return BNActFn.apply(yp, bn.weight, bn.bias, None, bn, act, False, None, None, out)
+
+
 def conv_bn_act(x, conv, bn, act, residual, x_slot=None, res_slot=None, exclusive_input=False, out=None):
     """``exclusive_input``: this conv is the only consumer of ``x`` (lets its dgrad fuse the BN-backward
     reduce of x's producer); a slot-paired consumer qualifies automatically.  ``out`` = (ConcatBuffer,

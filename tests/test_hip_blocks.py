@@ -1,5 +1,7 @@
 """Residual blocks on the HIP path: gradients with the fused paired-gradient slots must equal the
 gradients autograd produces when the two contributions are summed separately."""
+import copy
+
 import pytest
 import torch
 
@@ -207,3 +209,51 @@ def test_inception_concat_in_place(kind):
     assert err(gx1, gx0) < 2e-2, err(gx1, gx0)
     for n in gp0:
         assert err(gp1[n], gp0[n]) < 2e-2, (n, err(gp1[n], gp0[n]))
+
+
+@pytest.mark.parametrize("kind", ["A", "C", "E"])
+def test_inception_pool_conv_swap(kind):
+    """Inception branch_pool: the HIP path's conv1x1 -> avgpool order (conv on the wide input, pool on
+    the narrow output) against the fp32 torch reference's avgpool -> conv1x1, forward and gradients -
+    and no further from it than the HIP path with the pool first (the bf16 block's own error level)."""
+    from pytorch_imageclassification_distributed_amd.models import inception as I
+    from pytorch_imageclassification_distributed_amd.ops import functional as Fx
+    from pytorch_imageclassification_distributed_amd.ops import hip
+    torch.manual_seed(1)
+    blk, cin, hw = {"A": (I.InceptionA(192, 32), 192, 17), "C": (I.InceptionC(768, 128), 768, 9),
+                    "E": (I.InceptionE(1280), 1280, 5)}[kind]
+    blk = blk.to(DEV).to(memory_format=torch.channels_last)
+    with torch.no_grad():
+        for p in blk.parameters():
+            p.copy_(p.to(torch.bfloat16).float())
+    x = torch.randn(4, cin, hw, hw, device=DEV).to(torch.bfloat16).float()
+    wgt = None
+
+    def run(swap, backend="auto"):
+        nonlocal wgt
+        m = copy.deepcopy(blk)
+        keep_b, keep_s = Fx.get_backend(), hip.POOL_CONV_SWAP
+        Fx.set_backend(backend)
+        hip.POOL_CONV_SWAP = swap
+        try:
+            xx = (x.clone() if backend == "torch" else
+                  x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)).requires_grad_(True)
+            out = m(xx)
+            if wgt is None:
+                wgt = torch.linspace(-1, 1, out.numel(), device=DEV).view_as(out)
+            (out.float() * wgt).sum().backward()
+            return out.float(), xx.grad.float(), {n: p.grad.float() for n, p in m.named_parameters()}
+        finally:
+            Fx.set_backend(keep_b)
+            hip.POOL_CONV_SWAP = keep_s
+
+    o_r, gx_r, gp_r = run(False, "torch")
+    o_s, gx_s, gp_s = run(True)
+    o_p, gx_p, gp_p = run(False)
+    err = lambda a, b: ((a - b).abs().max() / b.abs().max().clamp(min=1e-6)).item()  # noqa: E731
+    merr = lambda a, b: ((a - b).abs().mean() / b.abs().mean().clamp(min=1e-9)).item()  # noqa: E731
+    assert err(o_s, o_r) < 3e-2
+    assert merr(gx_s, gx_r) < max(3e-2, 1.3 * merr(gx_p, gx_r)), (merr(gx_s, gx_r), merr(gx_p, gx_r))
+    for n in gp_r:
+        if "branch_pool" in n:
+            assert merr(gp_s[n], gp_r[n]) < max(3e-2, 1.3 * merr(gp_p[n], gp_r[n])), n
