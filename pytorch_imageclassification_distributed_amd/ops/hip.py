@@ -997,6 +997,47 @@ def conv_bn_act_pool(x, conv, bn, act, pool, exclusive_input=False):
     return BNActPoolFn.apply(y, bn.weight, bn.bias, bn, act, bn.training, (k, s, p))
 
 
+def dense_conv_eligible(x, conv) -> bool:
+    """The kernel covers the whole unpadded input: one output pixel per image (a dense layer)."""
+    return (x.dim() == 4 and tuple(x.shape[2:]) == tuple(conv.kernel_size) and conv.groups == 1
+            and conv.bias is None and tuple(conv.padding) == (0, 0) and tuple(conv.dilation) == (1, 1)
+            and not getattr(conv, "tf_same", False) and x.shape[1] == conv.in_channels)
+
+
+class DenseConvFn(torch.autograd.Function):
+    """A convolution whose kernel covers its whole unpadded input is a dense layer:
+    Y[n][co] = X[n][(h, w, ci)] . W[co][(h, w, ci)] - NHWC activations and KRSC weights flatten alike
+    (Inception's aux classifier conv1: 5x5 over a 5x5 map).  As an implicit-GEMM transposed conv its
+    data gradient walked all 25 taps per input pixel, 24 of them in the zero padding (279 us of 64
+    blocks at batch 128); as three plain library GEMMs (hipBLASLt; dW accumulated in fp32) it costs
+    microseconds."""
+
+    @staticmethod
+    def forward(ctx, x, w, conv):
+        n, c, h, wd = x.shape
+        co = w.shape[0]
+        xf = _cl(x).permute(0, 2, 3, 1).reshape(n, h * wd * c)
+        wf = weight_bf16(w).view(co, h * wd * c)
+        y = torch.mm(xf, wf.t())
+        ctx.save_for_backward(x, w)
+        return y.view(n, 1, 1, co).permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        n, c, h, wd = x.shape
+        co = w.shape[0]
+        dyf = dy.reshape(n, co).to(BF16)
+        xf = _cl(x).permute(0, 2, 3, 1).reshape(n, h * wd * c)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.mm(dyf, weight_bf16(w).view(co, h * wd * c)).view(n, h, wd, c).permute(0, 3, 1, 2)
+        if ctx.needs_input_grad[1]:
+            dw = grad_buffer(w, zero=False)
+            dw.permute(0, 2, 3, 1).copy_(torch.mm(dyf.t().float(), xf.float()).view(co, h, wd, c))
+        return dx, dw, None
+
+
 POOL_CONV_SWAP = os.environ.get("IMGCLS_POOL_CONV_SWAP", "1") == "1"
 
 
@@ -1041,6 +1082,9 @@ def conv_bn_act(x, conv, bn, act, residual, x_slot=None, res_slot=None, exclusiv
         if not (conv.groups == conv.in_channels == conv.out_channels):
             raise NotImplementedError("grouped (non-depthwise) convolution")
         y = DwConvFn.apply(x, conv.weight, conv)
+        ready = False
+    elif dense_conv_eligible(x, conv) and x.shape[2] * x.shape[3] > 1:
+        y = DenseConvFn.apply(x, conv.weight, conv)
         ready = False
     else:
         if conv.groups != 1:

@@ -231,6 +231,38 @@ def test_stem_direct_matches_gemm(hw):
     assert rel_err(y_d, yr) < 1e-2
 
 
+def test_dense_conv_bn_act():
+    """A conv whose kernel covers its whole input (Inception aux conv1, 5x5 on 5x5) runs as dense GEMMs:
+    forward, BN statistics and every gradient against fp32 torch."""
+    hip = _hip()
+    torch.manual_seed(9)
+    n, c, hw, co = 16, 128, 5, 96
+    conv = nn.Conv2d(c, co, hw, bias=False).to(DEV).to(memory_format=CL)
+    bn = nn.BatchNorm2d(co, eps=1e-3).to(DEV)
+    with torch.no_grad():
+        conv.weight.copy_(bf(conv.weight))
+    conv_r = nn.Conv2d(c, co, hw, bias=False).to(DEV)
+    bn_r = nn.BatchNorm2d(co, eps=1e-3).to(DEV)
+    conv_r.load_state_dict(conv.state_dict())
+    bn_r.load_state_dict(bn.state_dict())
+    x = bf(torch.randn(n, c, hw, hw, device=DEV))
+    xb = x.to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
+    assert hip.dense_conv_eligible(xb, conv)
+    out = hip.conv_bn_act(xb, conv, bn, "relu", None)
+    xr = x.clone().requires_grad_(True)
+    yc = conv_r(xr)
+    ref = F.relu(bn_r(yc + (bf(yc) - yc).detach()))
+    assert out.shape == ref.shape == (n, co, 1, 1)
+    assert rel_err(out, ref) < 2e-2
+    assert torch.allclose(bn.running_mean, bn_r.running_mean, rtol=1e-2, atol=1e-3)
+    g = bf(torch.randn_like(ref))
+    out.backward(g.to(torch.bfloat16).contiguous(memory_format=CL))
+    ref.backward(g)
+    assert rel_err(xb.grad, xr.grad) < 3e-2
+    assert rel_err(conv.weight.grad, conv_r.weight.grad) < 3e-2
+    assert rel_err(bn.weight.grad, bn_r.weight.grad) < 3e-2
+
+
 @pytest.mark.parametrize("act,use_res", [("relu", False), ("relu", True), (None, False), ("silu", False)])
 def test_conv_bn_act(act, use_res):
     hip = _hip()
