@@ -1167,6 +1167,8 @@ struct ConvCfg { int tm, bn, wm, wn, st; void (*launch)(const ConvParams&, hipSt
 static const ConvCfg g_cfgs[] = {
     CFG(128, 64, 2, 2, 1),  CFG(128, 128, 2, 2, 1), CFG(128, 64, 2, 2, 2), CFG(128, 128, 2, 2, 2),
     CFG(256, 256, 2, 4, 2), CFG(256, 256, 4, 2, 2), CFG(256, 64, 4, 1, 1), CFG(128, 64, 2, 1, 1),
+    // 32-channel tiles for 32 / 48 / 96-channel GEMMs (the Inception stem: a 64-wide tile is half empty)
+    CFG(256, 32, 4, 1, 1), CFG(128, 32, 4, 1, 1), CFG(256, 32, 4, 1, 2),
 };
 #undef CFG
 constexpr int kNumCfgs = sizeof(g_cfgs) / sizeof(g_cfgs[0]);

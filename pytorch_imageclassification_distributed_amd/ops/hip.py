@@ -422,6 +422,8 @@ def _conv_candidates(m, ncols, fp8):
             continue
         if bn == 64 and ncols >= 512:     # 8+ column tiles re-read the pixel panel too often
             continue
+        if bn == 32 and (ncols % 64 == 0 or ncols > 96):  # 32-wide tiles only where 64 would waste columns
+            continue
         if tm == 256 and m < 256 * 16:    # too few row tiles to fill the chip
             continue
         out.append((0, 0, i))
