@@ -14,3 +14,5 @@ run effb0 --model efficientnet-b0 --image-size 224 --batch 256 --steps 20 --warm
 run r101 --model resnet101 --image-size 224 --batch 256 --steps 15 --warmup 6
 run effb3 --model efficientnet-b3 --image-size 300 --batch 128 --steps 15 --warmup 6
 run r50fp8 --dtype fp8 --steps 20 --warmup 8
+run r50 --steps 20 --warmup 8
+run r50b256 --batch 256 --steps 20 --warmup 8
