@@ -71,6 +71,7 @@ def main():
     shapes = [R50[int(i)] for i in a.only.split(",")] if a.only else R50
     for (ci, co, k, s, p, h, cnt) in shapes:
         hip.TUNE_LOG.clear()
+        hip.WGRAD_TUNE_LOG.clear()
         conv = nn.Conv2d(ci, co, k, s, p, bias=False).to(dev).to(memory_format=torch.channels_last)
         x = torch.randn(n, ci, h, h, device=dev, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
         g = hip.ConvGeom(x, conv)
@@ -147,6 +148,11 @@ def main():
                 best = min(times, key=times.get)
                 print(f"      tune M={m_} N={n_} K={k_}: " + "  ".join(
                     f"{'*' if c == best else ''}{_cfg_name(hip, c)}:{t * 1e3:.0f}us" for c, t in times.items()),
+                    flush=True)
+            for (co_, nt_, m_, times) in hip.WGRAD_TUNE_LOG:
+                best = min(times, key=times.get)
+                print(f"      wgrad Co={co_} Ntot={nt_} pix={m_}: " + "  ".join(
+                    f"{'*' if c == best else ''}b{c[0]}/st{c[1]}:{t * 1e3:.0f}us" for c, t in times.items()),
                     flush=True)
     print("tuned wgrad (blocks, stages):", {f"{k[4]}<-{k[1]} k{k[5]}s{k[7]} {k[2]}x{k[3]}": v
                                              for k, v in hip._WGRAD_TUNED.items()})

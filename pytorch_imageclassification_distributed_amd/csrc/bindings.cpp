@@ -174,7 +174,8 @@ void conv_wgrad(Tensor dY, Tensor X, Tensor dW, int M, int Cout, int Cin, int Nt
   p.stride_h = sh; p.stride_w = sw; p.pad_t = pt; p.pad_l = pl; p.dil_h = dh; p.dil_w = dwd; p.KW = KW;
   p.k_per_split = k_per_split;
   p.zero = ptr<bf16_t>(zero);
-  TORCH_CHECK(stages >= 0 && stages <= 4, "conv_wgrad: stages must be 0..4");
+  TORCH_CHECK(stages >= 0 && stages <= 6, "conv_wgrad: stages must be 0..6");
+  TORCH_CHECK(stages < 5 || Cout <= 32, "conv_wgrad: stages 5 / 6 (32-row tile) need Cout <= 32");
   TORCH_CHECK(stages != 4 || Cout >= 256, "conv_wgrad: the 256x256 tile needs Cout >= 256");
   p.stages = stages;
   check(conv_wgrad_launch(p, splits, cur()), "conv_wgrad");

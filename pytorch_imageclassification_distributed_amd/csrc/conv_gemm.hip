@@ -884,7 +884,7 @@ DEVI int fdiv(int n, int d, float inv, int& rem) {
 
 template <int ROWB>
 DEVI int wswz(int row) {  // XOR mask on the 32-B block index
-  return ROWB == 256 ? (row & 7) : ((row >> 1) & 3);
+  return ROWB == 256 ? (row & 7) : ROWB == 128 ? ((row >> 1) & 3) : ((row >> 2) & 1);
 }
 
 // Tile WBM (output channels) x TN (tap*Cin columns), WM x WN waves per k-group; KG wave groups
@@ -1244,10 +1244,15 @@ int conv_wgrad_launch(const WgradParams& p, int splits, hipStream_t stream) {
   if (p.M <= 0) return 0;
   const bool dma = g_wvariant != 1;
   // stages: 1 | 2 (4 waves, 64/128 x 128 tile), 3 = 2-stage ring with the in-block 2-way pixel split
-  // (8 waves), 4 = 256 x 256 tile on 8 waves (2-stage ring, one block per CU; Cout >= 256 only)
+  // (8 waves), 4 = 256 x 256 tile on 8 waves (2-stage ring, one block per CU; Cout >= 256 only),
+  // 5 / 6 = 32 x 128 tile with a 1 / 2-stage ring (Cout <= 32 only)
   if (dma && p.stages == 4) {
     if (p.Cout < 256) return 2;
     launch_wg<256, 256, 2, 4, 1, 2>(p, splits, stream);
+  } else if (dma && (p.stages == 5 || p.stages == 6)) {  // 32-row tile (Cout <= 32: no empty half tile)
+    if (p.Cout > 32) return 2;
+    if (p.stages == 5) launch_wg<32, 128, 2, 2, 1, 1>(p, splits, stream);
+    else launch_wg<32, 128, 2, 2, 1, 2>(p, splits, stream);
   } else if (p.Cout <= 64) {
     if (dma && p.stages == 1) launch_wg<64, 128, 2, 2, 1, 1>(p, splits, stream);
     else if (dma && p.stages == 3) launch_wg<64, 128, 2, 2, 2, 2>(p, splits, stream);

@@ -502,6 +502,7 @@ def conv_dgrad_raw(dy, w_param, g: ConvGeom, addend=None, link=None):
 
 
 WGRAD_TARGET_BLOCKS = int(os.environ.get("IMGCLS_WGRAD_BLOCKS", "0"))  # 0 = autotune per shape
+WGRAD_TUNE_LOG: list = []  # (Co, Ntot, pixels, {(blocks, stages): ms}) per tuned wgrad shape
 WGRAD_MIN_K = int(os.environ.get("IMGCLS_WGRAD_MIN_K", "512"))
 WGRAD_CANDIDATES = (256, 512, 1024, 2048)
 _WGRAD_TUNED: dict = {}
@@ -524,10 +525,11 @@ def _wgrad_launch(dy, x, out, g: ConvGeom, m, ntot, kps, splits, stages=2):
 
 
 def _wgrad_tiles(co, ntot, stages):
-    """Output tiles of one wgrad launch: 256 x 256 for the 8-wave kernel (stages 4), else 64|128 x 128."""
+    """Output tiles of one wgrad launch: 256 x 256 for the 8-wave kernel (stages 4), 32 x 128 for stages
+    5 / 6, else 64|128 x 128."""
     if stages == 4:
         return (-(-co // 256)) * (-(-ntot // 256))
-    return (-(-co // (64 if co <= 64 else 128))) * (-(-ntot // 128))
+    return (-(-co // (32 if stages in (5, 6) else 64 if co <= 64 else 128))) * (-(-ntot // 128))
 
 
 def _wgrad_plan(g: ConvGeom, dy, x, m, ntot):
@@ -563,11 +565,14 @@ def _wgrad_config(dy, x, g: ConvGeom, m, ntot):
         cands += [(cand, 3) for cand in blocks if cand <= 1024]
         if g.Co >= 256 and ntot >= 256:  # 256 x 256 tiles on 8 waves, ~1-2 blocks per CU
             cands += [(cand, 4) for cand in (256, 512)]
+        if g.Co <= 32:  # 32-row tiles: a 64-row tile would be half empty
+            cands += [(cand, st) for st in (5, 6) for cand in blocks]
     for cand, st in cands:
         kps, splits = _wgrad_split(m, _wgrad_tiles(g.Co, ntot, st), cand)
         times[(cand, st)] = _time_ms(lambda: _wgrad_launch(dy, x, scratch, g, m, ntot, kps, splits, st))
     best = min(times, key=times.get)
     _WGRAD_TUNED[key] = best
+    WGRAD_TUNE_LOG.append((g.Co, ntot, m, times))
     return best
 
 

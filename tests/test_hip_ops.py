@@ -51,6 +51,8 @@ CONV_CASES = [
     (2, 48, 35, 35, 64, (5, 5), 1, (2, 2)),
     (2, 96, 35, 35, 96, (3, 3), 2, (0, 0)),
     (1, 32, 15, 13, 40, (3, 3), 1, (0, 0)),
+    (2, 32, 37, 37, 32, (3, 3), 1, (0, 0)),   # 32-row wgrad tile (Inception Conv2d_2a)
+    (2, 24, 20, 20, 24, (3, 3), 1, (1, 1)),   # ... with a partial 24-of-32 channel tile (EfficientNet widths)
 ]
 
 
@@ -96,16 +98,19 @@ def test_conv_tile_configs(case, cfg):
         hip.CONV_FORCE_CFG = keep
 
 
-@pytest.mark.parametrize("stages", [1, 2, 3, 4])
+@pytest.mark.parametrize("stages", [1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("case", [CONV_CASES[0], CONV_CASES[1], CONV_CASES[4], CONV_CASES[5], CONV_CASES[6],
-                                  CONV_CASES[7], CONV_CASES[8], CONV_CASES[12]])
+                                  CONV_CASES[7], CONV_CASES[8], CONV_CASES[12], CONV_CASES[13], CONV_CASES[14]])
 def test_conv_wgrad_ring_variants(case, stages):
     """Weight-gradient kernel variants: 1-stage (occupancy), 2-stage ring, the 8-wave in-block
-    2-way pixel split (stages=3) and the 256x256 8-wave tile (stages=4, Cout >= 256) - each over the
+    2-way pixel split (stages=3), the 256x256 8-wave tile (stages=4, Cout >= 256) and the 32-row tile
+    (stages=5 / 6, Cout <= 32) - each over the
     tuner's split counts."""
     hip = _hip()
     if stages == 4 and case[4] < 256:
         pytest.skip("256x256 wgrad tile needs Cout >= 256")
+    if stages >= 5 and case[4] > 32:
+        pytest.skip("32-row wgrad tile needs Cout <= 32")
     keep, hip.WGRAD_STAGES = hip.WGRAD_STAGES, stages
     try:
         test_conv_fwd_bwd(case)
