@@ -47,6 +47,9 @@ def timeit(fn, iters=10, warm=2):
 def _cfg_name(hip, c):
     if c[2] < 0:
         return f"st{c[0]}/n{c[1]}"
+    if c[2] >= hip.DIRECT_BASE:
+        cip, cot = hip.DIRECT_CFGS[c[2] - hip.DIRECT_BASE]
+        return f"direct{cip}/{cot}"
     tm, bn, wm, wn, st = hip.conv_cfgs()[c[2]]
     return f"{tm}x{bn}/{wm}x{wn}/s{st}"
 

@@ -32,6 +32,8 @@ int bn_bwd_k_launch(const double*, const double*, double, int, float*, hipStream
 int bn_bwd_elemt_launch(const bf16_t*, const bf16_t*, const float*, const float*, const bf16_t*, const bf16_t*,
                         bf16_t*, long, int, int, int, hipStream_t);
 int bn_act_maxpool_launch(const bf16_t*, const float*, bf16_t*, uint8_t*, int, int, const int*, int, hipStream_t);
+int direct_conv_launch(const bf16_t*, const bf16_t*, bf16_t*, float*, int, int, int, int, int, int, int, int, int,
+                       int, int, hipStream_t);
 int stem_s2d_conv_launch(const bf16_t*, const bf16_t*, bf16_t*, float*, int, int, int, int, hipStream_t);
 int maxpool_fwd_launch(const bf16_t*, bf16_t*, uint8_t*, int, int, int, int, int, int, int, int, int, int, int,
                        int, hipStream_t);
@@ -311,6 +313,27 @@ void stem_conv(Tensor x, Tensor w, Tensor y, OT part, int G, int64_t N, int64_t 
         "stem_conv");
 }
 
+// stride-1 3x3 conv as a halo-tile direct kernel: x [N,H,W,Cin], w [Cout,3,3,Cin] (KRSC), y [N,OH,OW,Cout]
+void direct_conv(Tensor x, Tensor w, Tensor y, OT part, int G, int64_t N, int64_t H, int64_t W, int64_t Cin,
+                 int64_t OH, int64_t OW, int64_t Cout, int pt, int pl, int cfg) {
+  req(x, BF, "x"); req(w, BF, "w"); req(y, BF, "y");
+  TORCH_CHECK(N > 0 && H > 0 && W > 0 && OH > 0 && OW > 0 && Cin > 0 && Cout > 0 && Cin % 8 == 0 && Cout % 8 == 0 &&
+                  Cin <= 64 && pt >= 0 && pl >= 0 && pt <= 2 && pl <= 2 && OH <= H + 2 * pt && OW <= W + 2 * pl,
+              "direct_conv: bad geometry");
+  TORCH_CHECK(x.numel() == N * H * W * Cin && w.numel() == Cout * 9 * Cin && y.numel() == N * OH * OW * Cout &&
+                  N * std::max(H * W * Cin, OH * OW * Cout) < (1LL << 31),
+              "direct_conv: tensor sizes do not match the geometry");
+  float* pp = nullptr;
+  if (part.has_value() && part->defined()) {
+    req(*part, F32, "part");
+    TORCH_CHECK(G > 0 && part->numel() >= (int64_t)G * 2 * Cout, "direct_conv: part [G, 2, Cout]");
+    pp = part->data_ptr<float>();
+  }
+  check(direct_conv_launch(ptr<bf16_t>(x), ptr<bf16_t>(w), ptr<bf16_t>(y), pp, G, (int)N, (int)H, (int)W, (int)Cin,
+                           (int)OH, (int)OW, (int)Cout, pt, pl, cfg, cur()),
+        "direct_conv");
+}
+
 void maxpool_fwd(Tensor x, Tensor y, OT idx, int N, int H, int W, int C, int OH, int OW, int kh, int kw, int sh,
                  int sw, int ph, int pw) {
   req(x, BF, "x"); req(y, BF, "y");
@@ -584,6 +607,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_set_reduce_blocks", &bn_set_reduce_blocks, pybind11::arg("n"), pybind11::arg("chb") = 0);
   m.def("bn_act_maxpool", &bn_act_maxpool);
   m.def("stem_conv", &stem_conv);
+  m.def("direct_conv", &direct_conv);
   m.def("conv_fp8_cfgs", []() {
     std::vector<std::vector<int>> out;
     for (int i = 0; i < conv_num_fp8_cfgs(); ++i) {

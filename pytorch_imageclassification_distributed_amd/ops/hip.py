@@ -389,6 +389,10 @@ def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(
                 A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups, scales)
             if cfg[0] or cfg[2] >= 0:
                 _STAGES_TUNED[key] = cfg
+    if cfg[2] >= DIRECT_BASE:
+        _direct_launch(A, B, out, stats, groups, _direct_geom(geo, dh, dw, out, bias, addend, bwd, scales),
+                       cfg[2] - DIRECT_BASE)
+        return
     C.conv_gemm(A, B, out, stats, bias, *geo, dh, dw, tb, groups, zero, addend, *bwd, *cfg, *scales)
 
 
@@ -430,6 +434,33 @@ def _conv_candidates(m, ncols, fp8):
     return out
 
 
+DIRECT_CONV = os.environ.get("IMGCLS_DIRECT_CONV", "1") == "1"
+DIRECT_BASE = 100  # cfg[2] >= DIRECT_BASE: the halo-tile direct kernel (csrc/direct_conv.hip), variant cfg - base
+# variant -> (padded input channels, output-channel tile)
+DIRECT_CFGS = {0: (32, 32), 1: (32, 64), 2: (64, 32), 3: (64, 64)}
+
+
+def _direct_geom(geo, dh, dw, out, bias, addend, bwd, scales):
+    """(N, H, W, Cin, OH, OW, Cout, pt, pl) when this launch is a plain stride-1 3x3 forward conv the
+    direct kernel handles (<= 64 input channels, dense output, no fused extras), else None."""
+    m, co, k, cx, gh, gw, ih, iw, sa = geo[:9]
+    if not DIRECT_CONV or scales[0] is not None or bias is not None or addend is not None or bwd[0] is not None:
+        return None
+    if sa != 1 or geo[12] != 1 or geo[13] or geo[14] or geo[15] != co or geo[16] or len(dh) != 9:
+        return None
+    pt, pl = -dh[0], -dw[0]
+    if list(dh) != [r - pt for r in range(3) for _ in range(3)] or list(dw) != [c - pl for _ in range(3)
+                                                                             for c in range(3)]:
+        return None
+    if cx % 8 or cx > 64 or co % 8 or k != 9 * cx or m % (gh * gw) or out.shape[1] != co:
+        return None
+    return (m // (gh * gw), ih, iw, cx, gh, gw, co, pt, pl)
+
+
+def _direct_launch(A, B, out, stats, groups, dg, variant):
+    C.direct_conv(A, B, out, stats, groups, *dg, variant)
+
+
 def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups, scales=(None, None)):
     scratch = torch.empty_like(out)
     sst = torch.zeros_like(stats) if stats is not None else None
@@ -441,6 +472,11 @@ def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, group
     for cfg in cands:
         times[cfg] = _time_ms(lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, groups, zero,
                                                   addend, *bwd, *cfg, *scales))
+    dg = _direct_geom(geo, dh, dw, out, bias, addend, bwd, scales)
+    if dg is not None:
+        for v, (cip, cot) in DIRECT_CFGS.items():
+            if dg[3] <= cip and (cot == 32 or dg[6] > 32):
+                times[(0, 0, DIRECT_BASE + v)] = _time_ms(lambda: _direct_launch(A, B, scratch, sst, groups, dg, v))
     TUNE_LOG.append((geo[0], geo[1], geo[2], times))
     return min(times, key=times.get)
 

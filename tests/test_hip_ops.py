@@ -236,6 +236,43 @@ def test_stem_direct_matches_gemm(hw):
     assert rel_err(y_d, yr) < 1e-2
 
 
+@pytest.mark.parametrize("case", [
+    # N, Cin, H, W, Cout, pad
+    (2, 32, 37, 37, 32, 0),   # Inception Conv2d_2a (valid)
+    (2, 32, 35, 35, 64, 1),   # Inception Conv2d_2b
+    (2, 64, 56, 56, 64, 1),   # ResNet layer1
+    (1, 24, 19, 45, 40, 1),   # partial channel tiles, odd sizes
+    (3, 8, 9, 17, 16, 0),
+])
+def test_direct_conv(case):
+    """Halo-tile direct 3x3 conv (csrc/direct_conv.hip), every variant that fits, against fp32 torch:
+    output and fused BN statistics."""
+    hip = _hip()
+    n, cin, h, w, co, p = case
+    torch.manual_seed(11)
+    x = bf(torch.randn(n, cin, h, w, device=DEV))
+    wt = bf(torch.randn(co, cin, 3, 3, device=DEV) * 0.1)
+    yr = F.conv2d(x, wt, None, 1, p)
+    oh, ow = yr.shape[2], yr.shape[3]
+    xb = x.to(torch.bfloat16).contiguous(memory_format=CL)
+    wk = wt.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+    grp = hip.stat_groups(n * oh * ow)
+    ran = 0
+    for v, (cip, cot) in hip.DIRECT_CFGS.items():
+        if cin > cip:
+            continue
+        y = hip._empty_cl(n, co, oh, ow, DEV)
+        st = torch.zeros(grp * 2 * co, device=DEV)
+        hip.C.direct_conv(xb, wk, y, st, grp, n, h, w, cin, oh, ow, co, p, p, v)
+        assert rel_err(y, yr) < 1e-2, v
+        sm = st.view(grp, 2, co).sum(0)
+        yb = bf(yr)
+        assert rel_err(sm[0], yb.sum((0, 2, 3))) < 1e-2, v
+        assert rel_err(sm[1], (yb * yb).sum((0, 2, 3))) < 1e-2, v
+        ran += 1
+    assert ran > 0
+
+
 def test_dense_conv_bn_act():
     """A conv whose kernel covers its whole input (Inception aux conv1, 5x5 on 5x5) runs as dense GEMMs:
     forward, BN statistics and every gradient against fp32 torch."""
