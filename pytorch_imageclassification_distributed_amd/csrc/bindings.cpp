@@ -33,7 +33,7 @@ int bn_bwd_elemt_launch(const bf16_t*, const bf16_t*, const float*, const float*
                         bf16_t*, long, int, int, int, hipStream_t);
 int bn_act_maxpool_launch(const bf16_t*, const float*, bf16_t*, uint8_t*, int, int, const int*, int, hipStream_t);
 int direct_conv_launch(const bf16_t*, const bf16_t*, bf16_t*, float*, int, int, int, int, int, int, int, int, int,
-                       int, int, hipStream_t);
+                       int, int, const bf16_t*, const float*, int, hipStream_t);
 int stem_s2d_conv_launch(const bf16_t*, const bf16_t*, bf16_t*, float*, int, int, int, int, hipStream_t);
 int maxpool_fwd_launch(const bf16_t*, bf16_t*, uint8_t*, int, int, int, int, int, int, int, int, int, int, int,
                        int, hipStream_t);
@@ -315,7 +315,7 @@ void stem_conv(Tensor x, Tensor w, Tensor y, OT part, int G, int64_t N, int64_t 
 
 // stride-1 3x3 conv as a halo-tile direct kernel: x [N,H,W,Cin], w [Cout,3,3,Cin] (KRSC), y [N,OH,OW,Cout]
 void direct_conv(Tensor x, Tensor w, Tensor y, OT part, int G, int64_t N, int64_t H, int64_t W, int64_t Cin,
-                 int64_t OH, int64_t OW, int64_t Cout, int pt, int pl, int cfg) {
+                 int64_t OH, int64_t OW, int64_t Cout, int pt, int pl, int cfg, OT y_bn, OT coef, int act) {
   req(x, BF, "x"); req(w, BF, "w"); req(y, BF, "y");
   TORCH_CHECK(N > 0 && H > 0 && W > 0 && OH > 0 && OW > 0 && Cin > 0 && Cout > 0 && Cin % 8 == 0 && Cout % 8 == 0 &&
                   Cin <= 64 && pt >= 0 && pl >= 0 && pt <= 2 && pl <= 2 && OH <= H + 2 * pt && OW <= W + 2 * pl,
@@ -329,8 +329,16 @@ void direct_conv(Tensor x, Tensor w, Tensor y, OT part, int G, int64_t N, int64_
     TORCH_CHECK(G > 0 && part->numel() >= (int64_t)G * 2 * Cout, "direct_conv: part [G, 2, Cout]");
     pp = part->data_ptr<float>();
   }
+  const bool bwd = y_bn.has_value() && y_bn->defined();
+  if (bwd) {  // fused BN-backward epilogue: y_bn shaped like the output, coef [4*Cout], partial rows required
+    req(*y_bn, BF, "y_bn");
+    TORCH_CHECK(y_bn->numel() == y.numel() && coef.has_value() && coef->defined() &&
+                    coef->scalar_type() == F32 && coef->numel() >= 4 * Cout && pp != nullptr,
+                "direct_conv: the BN-backward epilogue needs y_bn like y, coef [4*Cout] and part");
+  }
   check(direct_conv_launch(ptr<bf16_t>(x), ptr<bf16_t>(w), ptr<bf16_t>(y), pp, G, (int)N, (int)H, (int)W, (int)Cin,
-                           (int)OH, (int)OW, (int)Cout, pt, pl, cfg, cur()),
+                           (int)OH, (int)OW, (int)Cout, pt, pl, cfg, bwd ? ptr<bf16_t>(*y_bn) : nullptr,
+                           bwd ? ptr<float>(*coef) : nullptr, act, cur()),
         "direct_conv");
 }
 
@@ -607,7 +615,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_set_reduce_blocks", &bn_set_reduce_blocks, pybind11::arg("n"), pybind11::arg("chb") = 0);
   m.def("bn_act_maxpool", &bn_act_maxpool);
   m.def("stem_conv", &stem_conv);
-  m.def("direct_conv", &direct_conv);
+  m.def("direct_conv", &direct_conv, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"),
+        pybind11::arg("part"), pybind11::arg("G"), pybind11::arg("N"), pybind11::arg("H"), pybind11::arg("W"),
+        pybind11::arg("Cin"), pybind11::arg("OH"), pybind11::arg("OW"), pybind11::arg("Cout"), pybind11::arg("pt"),
+        pybind11::arg("pl"), pybind11::arg("cfg"), pybind11::arg("y_bn") = pybind11::none(),
+        pybind11::arg("coef") = pybind11::none(), pybind11::arg("act") = 0);
   m.def("conv_fp8_cfgs", []() {
     std::vector<std::vector<int>> out;
     for (int i = 0; i < conv_num_fp8_cfgs(); ++i) {

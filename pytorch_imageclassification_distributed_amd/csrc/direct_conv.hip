@@ -21,7 +21,13 @@ struct DirectArgs {
   const bf16_t* x;  // [N, H, W, Cin]
   const bf16_t* w;  // [Cout, KH, KW, Cin]
   bf16_t* y;        // [N, OH, OW, Cout]
-  float* part;      // [G, 2, Cout] or null
+  float* part;      // [G, 2, Cout] or null: BN statistics of y (forward) / BN-backward partials (BWD)
+  // BWD (data gradient of the consumer of a BN output): y_bn [N, OH, OW, Cout] is that BN's input and
+  // coef its [scale, shift, mean, invstd]; the epilogue writes dz = act'(y_bn*scale + shift) * dX and
+  // accumulates (sum dz, sum dz * xhat) - the GEMM epilogue's BwdLink contract (ops/hip.py)
+  const bf16_t* y_bn;
+  const float* coef;
+  int act;
   int N, H, W, Cin, OH, OW, Cout, pt, pl, G;
   int tiles_w, tiles_hw, ntiles, nco;
 };
@@ -87,7 +93,7 @@ DEVI void dstore(char* patch, int tid, const uint4* reg) {
   }
 }
 
-template <int CIP, int KH, int KW, int COT>
+template <int CIP, int KH, int KW, int COT, bool BWD>
 __global__ __launch_bounds__(256, (DC<CIP, KH, KW, COT>::OCC)) void direct_conv_kernel(const DirectArgs a) {
   using D = DC<CIP, KH, KW, COT>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -117,11 +123,25 @@ __global__ __launch_bounds__(256, (DC<CIP, KH, KW, COT>::OCC)) void direct_conv_
   if (t + tstride < a.ntiles) dload<CIP, KH, KW, COT>(a, t + tstride, tid, regA);
   __syncthreads();
 
-  float s[D::CB][4], q[D::CB][4];
+  float s[D::CB][4], q[D::CB][4];  // forward statistics: channel cb*16 + 4*lg + i
 #pragma unroll
   for (int cb = 0; cb < D::CB; ++cb)
 #pragma unroll
     for (int i = 0; i < 4; ++i) { s[cb][i] = 0.f; q[cb][i] = 0.f; }
+  // BWD: each lane's read-back chunk c = lane % CH is fixed, so it owns 8 channels for the whole kernel
+  const int rc = lane % D::CH, rco = co0 + rc * 8;
+  float bs[8], bq[8], bsc[8], bsh[8], bmu[8], bis[8];
+  if constexpr (BWD) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      bs[k] = 0.f; bq[k] = 0.f;
+      const bool ok = rco + k < a.Cout;
+      bsc[k] = ok ? a.coef[rco + k] : 0.f;
+      bsh[k] = ok ? a.coef[a.Cout + rco + k] : 0.f;
+      bmu[k] = ok ? a.coef[2 * a.Cout + rco + k] : 0.f;
+      bis[k] = ok ? a.coef[3 * a.Cout + rco + k] : 0.f;
+    }
+  }
 
   int buf = 0;
   // `rl` receives tile t + 2 stride, `rs` holds tile t + stride (alternating register sets, no copies)
@@ -168,7 +188,7 @@ __global__ __launch_bounds__(256, (DC<CIP, KH, KW, COT>::OCC)) void direct_conv_
         pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
         const int c = cb * 2 + (lg >> 1);
         *(uint2*)(stg + p * (COT * 2) + ((c ^ (p & (D::CH - 1))) * 16) + (lg & 1) * 8) = pk;
-        if (live) {
+        if (!BWD && live) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) { s[cb][i] += v[i]; q[cb][i] += v[i] * v[i]; }
         }
@@ -178,9 +198,25 @@ __global__ __launch_bounds__(256, (DC<CIP, KH, KW, COT>::OCC)) void direct_conv_
     for (int j = 0; j < 32 * D::CH / 64; ++j) {
       const int p = j * (64 / D::CH) + lane / D::CH, c = lane % D::CH;
       const int oh = oh0 + wave * 2 + (p >> 4), ow = ow0 + (p & 15), co = co0 + c * 8;
-      const uint4 v = *(const uint4*)(stg + p * (COT * 2) + ((c ^ (p & (D::CH - 1))) * 16));
-      if (oh < a.OH && ow < a.OW && co < a.Cout)
-        *(uint4*)(a.y + (((long)n * a.OH + oh) * a.OW + ow) * a.Cout + co) = v;
+      uint4 v = *(const uint4*)(stg + p * (COT * 2) + ((c ^ (p & (D::CH - 1))) * 16));
+      if (oh < a.OH && ow < a.OW && co < a.Cout) {
+        const long o = (((long)n * a.OH + oh) * a.OW + ow) * a.Cout + co;
+        if constexpr (BWD) {  // dz = act'(z) * dX with z recomputed from the BN input, + BN-backward sums
+          float gv[8], yv[8];
+          unpack8(v, gv);
+          unpack8(*(const uint4*)(a.y_bn + o), yv);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float dz = a.act != ACT_NONE ? act_grad(yv[k] * bsc[k] + bsh[k], gv[k], a.act) : gv[k];
+            gv[k] = dz;
+          }
+          v = pack8(gv);
+          unpack8(v, gv);  // statistics of the stored (bf16) dz, as the GEMM epilogue takes them
+#pragma unroll
+          for (int k = 0; k < 8; ++k) { bs[k] += gv[k]; bq[k] += gv[k] * (yv[k] - bmu[k]) * bis[k]; }
+        }
+        *(uint4*)(a.y + o) = v;
+      }
     }
 
     if (tn < a.ntiles) dstore<CIP, KH, KW, COT>(pbuf + (buf ^ 1) * D::PATCH_B, tid, rs);
@@ -195,6 +231,36 @@ __global__ __launch_bounds__(256, (DC<CIP, KH, KW, COT>::OCC)) void direct_conv_
   }
 
   if (a.part == nullptr) return;
+  if constexpr (BWD) {
+    // lanes with equal lane % CH own the same 8 channels: fold them, then the 4 waves, one partial row
+#pragma unroll
+    for (int o = D::CH; o < 64; o <<= 1)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        bs[k] += __shfl_xor(bs[k], o, 64);
+        bq[k] += __shfl_xor(bq[k], o, 64);
+      }
+    float* red = (float*)pbuf;  // [4 waves][2][COT]
+    __syncthreads();
+    if (lane < D::CH) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        red[(wave * 2 + 0) * COT + rc * 8 + k] = bs[k];
+        red[(wave * 2 + 1) * COT + rc * 8 + k] = bq[k];
+      }
+    }
+    __syncthreads();
+    if (tid < 2 * COT) {
+      const int which = tid / COT, c = tid - which * COT;
+      if (co0 + c < a.Cout) {
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) v += red[(w * 2 + which) * COT + c];
+        atomicAdd(a.part + (size_t)((blockIdx.x / a.nco) % a.G) * 2 * a.Cout + which * a.Cout + co0 + c, v);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int o = 1; o < 16; o <<= 1)
 #pragma unroll
@@ -228,7 +294,7 @@ __global__ __launch_bounds__(256, (DC<CIP, KH, KW, COT>::OCC)) void direct_conv_
 }
 
 template <int CIP, int KH, int KW, int COT>
-int launch_direct(DirectArgs a, hipStream_t s) {
+int launch_direct(DirectArgs a, bool bwd, hipStream_t s) {
   using D = DC<CIP, KH, KW, COT>;
   static int cus = 0;
   if (cus == 0) {
@@ -242,7 +308,8 @@ int launch_direct(DirectArgs a, hipStream_t s) {
   if (per_co > a.ntiles) per_co = a.ntiles;
   if (per_co < 1) per_co = 1;
   const int grid = per_co * a.nco;
-  hipLaunchKernelGGL((direct_conv_kernel<CIP, KH, KW, COT>), dim3(grid), dim3(256), D::LDS_B, s, a);
+  if (bwd) hipLaunchKernelGGL((direct_conv_kernel<CIP, KH, KW, COT, true>), dim3(grid), dim3(256), D::LDS_B, s, a);
+  else hipLaunchKernelGGL((direct_conv_kernel<CIP, KH, KW, COT, false>), dim3(grid), dim3(256), D::LDS_B, s, a);
   HIP_CHECK_LAUNCH();
   return 0;
 }
@@ -253,17 +320,19 @@ int launch_direct(DirectArgs a, hipStream_t s) {
 int direct_conv_num_cfgs() { return 4; }
 
 int direct_conv_launch(const bf16_t* x, const bf16_t* w, bf16_t* y, float* part, int G, int N, int H, int W,
-                       int Cin, int OH, int OW, int Cout, int pt, int pl, int cfg, hipStream_t s) {
-  DirectArgs a{x, w, y, part, N, H, W, Cin, OH, OW, Cout, pt, pl, G > 0 ? G : 1, 0, 0, 0, 1};
+                       int Cin, int OH, int OW, int Cout, int pt, int pl, int cfg, const bf16_t* y_bn,
+                       const float* coef, int act, hipStream_t s) {
+  DirectArgs a{x, w, y, part, y_bn, coef, act, N, H, W, Cin, OH, OW, Cout, pt, pl, G > 0 ? G : 1, 0, 0, 0, 1};
+  const bool bwd = y_bn != nullptr;
   a.tiles_w = cdiv(OW, 16);
   a.tiles_hw = cdiv(OH, 8) * a.tiles_w;
   a.ntiles = N * a.tiles_hw;
   if (a.ntiles <= 0) return 0;
   switch (cfg) {
-    case 0: return Cin <= 32 ? launch_direct<32, 3, 3, 32>(a, s) : 3;
-    case 1: return Cin <= 32 ? launch_direct<32, 3, 3, 64>(a, s) : 3;
-    case 2: return Cin <= 64 ? launch_direct<64, 3, 3, 32>(a, s) : 3;
-    case 3: return Cin <= 64 ? launch_direct<64, 3, 3, 64>(a, s) : 3;
+    case 0: return Cin <= 32 ? launch_direct<32, 3, 3, 32>(a, bwd, s) : 3;
+    case 1: return Cin <= 32 ? launch_direct<32, 3, 3, 64>(a, bwd, s) : 3;
+    case 2: return Cin <= 64 ? launch_direct<64, 3, 3, 32>(a, bwd, s) : 3;
+    case 3: return Cin <= 64 ? launch_direct<64, 3, 3, 64>(a, bwd, s) : 3;
     default: return 3;
   }
 }

@@ -374,7 +374,9 @@ def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(
     2 / 3 = pipelined) x output-channel tile (64 / 128 / 256: more tiles balance 256 CUs better on
     small layers) x pixel tile (128 rows on 4 waves, or 256 rows on 8 waves) - is chosen once per
     GEMM geometry by timing the candidates on scratch outputs (a conv-algorithm "find" step)."""
-    if CONV_FORCE_CFG is not None and scales[0] is None:
+    if DIRECT_FORCE is not None and _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales) is not None:
+        cfg = (0, 0, DIRECT_BASE + DIRECT_FORCE)  # (tests) every eligible launch on this direct variant
+    elif CONV_FORCE_CFG is not None and scales[0] is None:
         cfg = CONV_FORCE_CFG
     elif CONV_FORCE_FP8_CFG is not None and scales[0] is not None:
         cfg = CONV_FORCE_FP8_CFG
@@ -382,7 +384,8 @@ def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(
         cfg = (int(CONV_STAGES), 0, -1)
     else:
         key = (tuple(geo), out.shape[1], tuple(dh), tuple(dw), stats is not None, bias is not None,
-               addend is not None, bwd[0] is not None, bwd[1] is not None, bwd[4], scales[0] is not None)
+               addend is not None, bwd[0] is not None, bwd[1] is not None, bwd[4], scales[0] is not None,
+               DIRECT_CONV)
         cfg = _STAGES_TUNED.get(key)
         if cfg is None:
             cfg = (0, 0, -1) if torch.cuda.is_current_stream_capturing() else _tune_conv(
@@ -390,8 +393,8 @@ def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(
             if cfg[0] or cfg[2] >= 0:
                 _STAGES_TUNED[key] = cfg
     if cfg[2] >= DIRECT_BASE:
-        _direct_launch(A, B, out, stats, groups, _direct_geom(geo, dh, dw, out, bias, addend, bwd, scales),
-                       cfg[2] - DIRECT_BASE)
+        _direct_launch(A, B, out, stats, groups, _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales),
+                       cfg[2] - DIRECT_BASE, bwd)
         return
     C.conv_gemm(A, B, out, stats, bias, *geo, dh, dw, tb, groups, zero, addend, *bwd, *cfg, *scales)
 
@@ -435,30 +438,48 @@ def _conv_candidates(m, ncols, fp8):
 
 
 DIRECT_CONV = os.environ.get("IMGCLS_DIRECT_CONV", "1") == "1"
+DIRECT_FORCE = None  # tests: force a direct-kernel variant on every eligible launch
+DIRECT_DGRAD = os.environ.get("IMGCLS_DIRECT_DGRAD", "0") == "1"  # data gradients with the BN-backward epilogue
 DIRECT_BASE = 100  # cfg[2] >= DIRECT_BASE: the halo-tile direct kernel (csrc/direct_conv.hip), variant cfg - base
 # variant -> (padded input channels, output-channel tile)
 DIRECT_CFGS = {0: (32, 32), 1: (32, 64), 2: (64, 32), 3: (64, 64)}
 
 
-def _direct_geom(geo, dh, dw, out, bias, addend, bwd, scales):
-    """(N, H, W, Cin, OH, OW, Cout, pt, pl) when this launch is a plain stride-1 3x3 forward conv the
-    direct kernel handles (<= 64 input channels, dense output, no fused extras), else None."""
+def _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales):
+    """(N, H, W, Cin, OH, OW, Cout, pt, pl, tap order) when this launch is a stride-1 3x3 conv the direct
+    kernel handles - a forward conv, or the single-phase data gradient of a stride-1 3x3 conv (a 3x3 conv
+    of dY with the transposed, flipped weights), optionally with the fused BN-backward epilogue - with
+    <= 64 input channels, a dense output and no addend / residual; else None.  The tap order maps the
+    kernel's (th, tw) to the GEMM's weight tap (identity for the forward conv)."""
     m, co, k, cx, gh, gw, ih, iw, sa = geo[:9]
-    if not DIRECT_CONV or scales[0] is not None or bias is not None or addend is not None or bwd[0] is not None:
+    if not DIRECT_CONV or scales[0] is not None or bias is not None or addend is not None or bwd[1] is not None:
+        return None
+    if bwd[0] is not None and not DIRECT_DGRAD:
         return None
     if sa != 1 or geo[12] != 1 or geo[13] or geo[14] or geo[15] != co or geo[16] or len(dh) != 9:
         return None
-    pt, pl = -dh[0], -dw[0]
-    if list(dh) != [r - pt for r in range(3) for _ in range(3)] or list(dw) != [c - pl for _ in range(3)
-                                                                             for c in range(3)]:
-        return None
     if cx % 8 or cx > 64 or co % 8 or k != 9 * cx or m % (gh * gw) or out.shape[1] != co:
         return None
-    return (m // (gh * gw), ih, iw, cx, gh, gw, co, pt, pl)
+    pt, pl = -min(dh), -min(dw)
+    order = [None] * 9
+    for t in range(9):
+        th, tw = dh[t] + pt, dw[t] + pl
+        if not (0 <= th < 3 and 0 <= tw < 3) or order[th * 3 + tw] is not None:
+            return None
+        order[th * 3 + tw] = tb[t]
+    if pt > 2 or pl > 2:
+        return None
+    return (m // (gh * gw), ih, iw, cx, gh, gw, co, pt, pl, tuple(order))
 
 
-def _direct_launch(A, B, out, stats, groups, dg, variant):
-    C.direct_conv(A, B, out, stats, groups, *dg, variant)
+def _direct_launch(A, B, out, stats, groups, dg, variant, bwd):
+    n, ih, iw, cx, gh, gw, co, pt, pl, order = dg
+    w = B if order == tuple(range(9)) else B.view(co, 9, cx)[:, list(order), :].contiguous()
+    if bwd[0] is not None:  # fused BN-backward epilogue (BwdLink): partial rows instead of statistics
+        C.direct_conv(A, w, out, bwd[3], bwd[5], n, ih, iw, cx, gh, gw, co, pt, pl, variant,
+                      y_bn=bwd[0], coef=bwd[2], act=bwd[4])
+    else:
+        C.direct_conv(A, w, out, stats, groups, n, ih, iw, cx, gh, gw, co, pt, pl, variant)
 
 
 def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups, scales=(None, None)):
@@ -472,11 +493,12 @@ def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, group
     for cfg in cands:
         times[cfg] = _time_ms(lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, groups, zero,
                                                   addend, *bwd, *cfg, *scales))
-    dg = _direct_geom(geo, dh, dw, out, bias, addend, bwd, scales)
+    dg = _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales)
     if dg is not None:
         for v, (cip, cot) in DIRECT_CFGS.items():
             if dg[3] <= cip and (cot == 32 or dg[6] > 32):
-                times[(0, 0, DIRECT_BASE + v)] = _time_ms(lambda: _direct_launch(A, B, scratch, sst, groups, dg, v))
+                times[(0, 0, DIRECT_BASE + v)] = _time_ms(
+                    lambda: _direct_launch(A, B, scratch, sst, groups, dg, v, bwd))
     TUNE_LOG.append((geo[0], geo[1], geo[2], times))
     return min(times, key=times.get)
 

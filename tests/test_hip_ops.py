@@ -4,6 +4,7 @@ Inputs are rounded to bf16 first (the HIP path stores activations/weights in
 bf16), the reference then runs in fp32 on those exact values, so the remaining
 error is the kernels' fp32-accumulation order plus the bf16 rounding of outputs.
 """
+import copy
 import math
 
 import pytest
@@ -271,6 +272,51 @@ def test_direct_conv(case):
         assert rel_err(sm[1], (yb * yb).sum((0, 2, 3))) < 1e-2, v
         ran += 1
     assert ran > 0
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("case", [(2, 32, 23, 32, 0), (2, 32, 21, 64, 1), (2, 64, 20, 64, 1)])
+def test_direct_conv_chain(case, variant):
+    """conv -> BN -> ReLU -> 3x3 conv -> BN with every eligible launch forced onto one direct-kernel
+    variant: forward, and the second conv's data gradient with the fused BN-backward epilogue (the first
+    BN's reduce) - against the GEMM configurations."""
+    hip = _hip()
+    n, c, hw, co, p = case
+    cip, cot = hip.DIRECT_CFGS[variant]
+    if c > cip or co > cip:
+        pytest.skip("channels exceed the variant's padded input width")
+    torch.manual_seed(12)
+    mods = [nn.Conv2d(c, c, 3, 1, p, bias=False), nn.BatchNorm2d(c), nn.Conv2d(c, co, 3, 1, p, bias=False),
+            nn.BatchNorm2d(co)]
+    mods = [m.to(DEV).to(memory_format=CL) for m in mods]
+    with torch.no_grad():
+        for m in (mods[0], mods[2]):
+            m.weight.copy_(bf(m.weight))
+    x = bf(torch.randn(n, c, hw, hw, device=DEV))
+
+    def run(force):
+        keep, hip.DIRECT_FORCE = hip.DIRECT_FORCE, force
+        keep_d, hip.DIRECT_CONV = hip.DIRECT_CONV, force is not None  # baseline: GEMM configurations only
+        keep_g, hip.DIRECT_DGRAD = hip.DIRECT_DGRAD, True
+        try:
+            ms = [copy.deepcopy(m) for m in mods]
+            xb = x.to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
+            a1 = hip.conv_bn_act(xb, ms[0], ms[1], "relu", None)
+            out = hip.conv_bn_act(a1, ms[2], ms[3], None, None, exclusive_input=True)
+            g = torch.linspace(-1, 1, out.numel(), device=DEV).view_as(out).to(torch.bfloat16)
+            out.backward(g.contiguous(memory_format=CL))
+            return out.float(), xb.grad.float(), [p_.grad.float() for m in ms for p_ in m.parameters()]
+        finally:
+            hip.DIRECT_FORCE = keep
+            hip.DIRECT_CONV = keep_d
+            hip.DIRECT_DGRAD = keep_g
+
+    o0, gx0, gp0 = run(None)
+    o1, gx1, gp1 = run(variant)
+    assert rel_err(o1, o0) < 2e-2
+    assert rel_err(gx1, gx0) < 3e-2
+    for a_, b_ in zip(gp1, gp0):
+        assert rel_err(a_, b_) < 3e-2
 
 
 def test_dense_conv_bn_act():
