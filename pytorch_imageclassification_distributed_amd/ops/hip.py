@@ -439,7 +439,7 @@ def _conv_candidates(m, ncols, fp8):
 
 DIRECT_CONV = os.environ.get("IMGCLS_DIRECT_CONV", "1") == "1"
 DIRECT_FORCE = None  # tests: force a direct-kernel variant on every eligible launch
-DIRECT_DGRAD = os.environ.get("IMGCLS_DIRECT_DGRAD", "0") == "1"  # data gradients with the BN-backward epilogue
+DIRECT_DGRAD = os.environ.get("IMGCLS_DIRECT_DGRAD", "1") == "1"  # data gradients (+ BN-backward epilogue)
 DIRECT_BASE = 100  # cfg[2] >= DIRECT_BASE: the halo-tile direct kernel (csrc/direct_conv.hip), variant cfg - base
 # variant -> (padded input channels, output-channel tile)
 DIRECT_CFGS = {0: (32, 32), 1: (32, 64), 2: (64, 32), 3: (64, 64)}
@@ -472,9 +472,19 @@ def _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales):
     return (m // (gh * gw), ih, iw, cx, gh, gw, co, pt, pl, tuple(order))
 
 
+_ORDER_IDX: dict = {}
+
+
 def _direct_launch(A, B, out, stats, groups, dg, variant, bwd):
     n, ih, iw, cx, gh, gw, co, pt, pl, order = dg
-    w = B if order == tuple(range(9)) else B.view(co, 9, cx)[:, list(order), :].contiguous()
+    if order == tuple(range(9)):
+        w = B
+    else:  # tap permutation of the transposed weight; a cached device index (a host list would sync)
+        key = (order, B.device)
+        idx = _ORDER_IDX.get(key)
+        if idx is None:
+            idx = _ORDER_IDX[key] = torch.tensor(order, dtype=torch.long, device=B.device)
+        w = B.view(co, 9, cx).index_select(1, idx)
     if bwd[0] is not None:  # fused BN-backward epilogue (BwdLink): partial rows instead of statistics
         C.direct_conv(A, w, out, bwd[3], bwd[5], n, ih, iw, cx, gh, gw, co, pt, pl, variant,
                       y_bn=bwd[0], coef=bwd[2], act=bwd[4])
