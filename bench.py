@@ -52,6 +52,10 @@ def parse():
     p.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--dist-backend", default="auto", help="auto (RCCL) | gloo (functional multi-rank runs on one GPU)")
     p.add_argument("--profile-steps", type=int, default=0)
+    p.add_argument("--tune-db", default="", help="kernel-choice find-db to seed the per-shape tuner with "
+                   "(default: $IMGCLS_TUNE_DB, else tuning/mi355x_find_db.json; 'none' disables); shapes it "
+                   "does not list are still timed")
+    p.add_argument("--tune-save", default="", help="write the kernel choices of this run to this file")
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
                    help="fp8: MX-FP8 forward convolutions (BASELINE config 5); bf16 elsewhere")
     return p.parse_args()
@@ -82,6 +86,11 @@ def main():
     ] + ([] if sync_bn else ["--no-sync-bn"]))
     tr = Trainer(targs, ctx)
     tr.net.train()
+    tune_db = a.tune_db or os.environ.get("IMGCLS_TUNE_DB", "") or os.path.join(HERE, "tuning", "mi355x_find_db.json")
+    if a.compute == "hip" and tune_db and tune_db != "none" and os.path.exists(tune_db):
+        from pytorch_imageclassification_distributed_amd.ops import hip
+        n = hip.load_tuning(tune_db)
+        print(f"[bench] rank {ctx.rank}: {n} kernel choices from {tune_db}", file=sys.stderr, flush=True)
     data = DeviceSyntheticLoader(a.batch, a.num_classes, a.image_size, ctx.device,
                                  steps=a.warmup + a.steps, ring=2, seed=1234 + ctx.rank)
     batches = list(iter(data))
@@ -111,6 +120,9 @@ def main():
     barrier(ctx)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    if a.tune_save and ctx.rank == 0:
+        from pytorch_imageclassification_distributed_amd.ops import hip
+        print(f"[bench] saved {hip.save_tuning(a.tune_save)} kernel choices to {a.tune_save}", file=sys.stderr)
     t = torch.tensor([dt], dtype=torch.float64, device=ctx.device)
     if ctx.world_size > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -363,6 +363,54 @@ def _time_ms(run, reps: int = 3, trials: int = 3) -> float:
 
 CONV_STAGES = os.environ.get("IMGCLS_CONV_STAGES", "auto")  # auto (timed per shape) | 0 (heuristic) | 1 | 2
 _STAGES_TUNED: dict = {}
+
+
+def save_tuning(path: str) -> int:
+    """Write the per-shape kernel choices found so far (conv fwd/dgrad configurations, wgrad split and
+    variant) to a JSON "find-db"; returns the entry count.  ``load_tuning`` seeds a later process with
+    them, so its choices are the same (and it skips the timing) - like a conv-algorithm find-db."""
+    import json
+    db = {"conv": [[repr(k), list(v)] for k, v in _STAGES_TUNED.items()],
+          "wgrad": [[repr(k), list(v)] for k, v in _WGRAD_TUNED.items()]}
+    d = os.path.dirname(os.path.abspath(path))
+    os.makedirs(d, exist_ok=True)
+    with open(path, "w") as f:
+        json.dump(db, f, indent=0)
+    return len(db["conv"]) + len(db["wgrad"])
+
+
+def load_tuning(path: str) -> int:
+    """Seed the tuning caches from a ``save_tuning`` file (entries already present win; entries naming a
+    configuration this build does not have are skipped).  Keys are parsed with ast.literal_eval."""
+    import ast
+    import json
+    try:
+        with open(path) as f:
+            db = json.load(f)
+    except (OSError, ValueError):
+        return 0
+    n = 0
+    ncfg, nfp8 = len(conv_cfgs()), len(conv_fp8_cfgs())
+    for ks, v in db.get("conv", []):
+        try:
+            k, v = ast.literal_eval(ks), tuple(int(x) for x in v)
+        except (ValueError, SyntaxError, TypeError):
+            continue
+        fp8 = bool(k[10]) if len(k) > 10 else False
+        ok = (v[2] - DIRECT_BASE in DIRECT_CFGS if v[2] >= DIRECT_BASE else
+              v[2] < (nfp8 if fp8 else ncfg)) and len(v) == 3
+        if ok and k not in _STAGES_TUNED:
+            _STAGES_TUNED[k] = v
+            n += 1
+    for ks, v in db.get("wgrad", []):
+        try:
+            k, v = ast.literal_eval(ks), tuple(int(x) for x in v)
+        except (ValueError, SyntaxError, TypeError):
+            continue
+        if len(v) == 2 and 1 <= v[1] <= 6 and v[0] > 0 and k not in _WGRAD_TUNED:
+            _WGRAD_TUNED[k] = v
+            n += 1
+    return n
 CONV_FORCE_CFG = None  # (stages, tile_n, cfg) for every bf16 fwd/dgrad launch (tests)
 CONV_FORCE_FP8_CFG = None  # (stages, tile_n, cfg) for every MX-FP8 forward launch (tests)
 TUNE_LOG: list = []  # (M, Ncols, K, {cfg: ms}) per tuned geometry (benchmarks/conv_bench.py prints it)
