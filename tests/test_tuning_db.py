@@ -1,0 +1,59 @@
+"""Kernel-choice find-db (ops/hip.py save_tuning / load_tuning, bench.py --tune-db): round trip, entries
+naming configurations this build lacks are skipped, existing choices win, the committed file parses."""
+import json
+import os
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture
+def hip():
+    try:
+        from pytorch_imageclassification_distributed_amd.ops import hip as h
+    except Exception as e:  # noqa: BLE001  (no extension built)
+        pytest.skip(f"extension not importable: {e}")
+    keep = (dict(h._STAGES_TUNED), dict(h._WGRAD_TUNED))
+    h._STAGES_TUNED.clear()
+    h._WGRAD_TUNED.clear()
+    yield h
+    h._STAGES_TUNED.clear()
+    h._WGRAD_TUNED.clear()
+    h._STAGES_TUNED.update(keep[0])
+    h._WGRAD_TUNED.update(keep[1])
+
+
+def test_round_trip(hip, tmp_path):
+    k1 = ((1024, 64, 576, 64, 8, 8, 8, 8, 1, 576, 8, 8, 1, 0, 0, 64, 0), 64, (-1, -1, -1, 0, 0, 0, 1, 1, 1),
+          (-1, 0, 1) * 3, True, False, False, False, False, 0, False, True)
+    k2 = k1[:1] + (128,) + k1[2:]
+    hip._STAGES_TUNED[k1] = (0, 0, 1)
+    hip._STAGES_TUNED[k2] = (0, 0, hip.DIRECT_BASE + 3)
+    wk = (2, 64, 8, 8, 64, 3, 3, 1, 1, 1, 1, (256, 512), (1, 2))
+    hip._WGRAD_TUNED[wk] = (512, 1)
+    path = str(tmp_path / "db.json")
+    assert hip.save_tuning(path) == 3
+    hip._STAGES_TUNED.clear()
+    hip._WGRAD_TUNED.clear()
+    assert hip.load_tuning(path) == 3
+    assert hip._STAGES_TUNED[k1] == (0, 0, 1) and hip._STAGES_TUNED[k2] == (0, 0, hip.DIRECT_BASE + 3)
+    assert hip._WGRAD_TUNED[wk] == (512, 1)
+
+
+def test_invalid_and_existing_entries(hip, tmp_path):
+    k = ((64, 64, 64, 64, 1, 1, 1, 1, 1, 64, 1, 1, 1, 0, 0, 64, 0), 64, (0,), (0,), False, False, False, False,
+         False, 0, False, True)
+    db = {"conv": [[repr(k), [0, 0, 999]], [repr(k[:1] + (32,) + k[2:]), [0, 0, 0]], ["not python", [0, 0, 0]]],
+          "wgrad": [["(1, 2)", [512, 9]]]}
+    path = tmp_path / "db.json"
+    path.write_text(json.dumps(db))
+    hip._STAGES_TUNED[k[:1] + (32,) + k[2:]] = (0, 0, 2)
+    assert hip.load_tuning(str(path)) == 0  # bad index, existing key, unparsable key, bad wgrad variant
+    assert hip._STAGES_TUNED[k[:1] + (32,) + k[2:]] == (0, 0, 2)
+    assert hip.load_tuning(str(tmp_path / "missing.json")) == 0
+
+
+def test_committed_db_parses(hip):
+    path = os.path.join(ROOT, "tuning", "mi355x_find_db.json")
+    assert hip.load_tuning(path) > 100
