@@ -318,7 +318,7 @@ void direct_conv(Tensor x, Tensor w, Tensor y, OT part, int G, int64_t N, int64_
                  int64_t OH, int64_t OW, int64_t Cout, int pt, int pl, int cfg, OT y_bn, OT coef, int act) {
   req(x, BF, "x"); req(w, BF, "w"); req(y, BF, "y");
   TORCH_CHECK(N > 0 && H > 0 && W > 0 && OH > 0 && OW > 0 && Cin > 0 && Cout > 0 && Cin % 8 == 0 && Cout % 8 == 0 &&
-                  Cin <= 64 && pt >= 0 && pl >= 0 && pt <= 2 && pl <= 2 && OH <= H + 2 * pt && OW <= W + 2 * pl,
+                  Cin <= 96 && pt >= 0 && pl >= 0 && pt <= 2 && pl <= 2 && OH <= H + 2 * pt && OW <= W + 2 * pl,
               "direct_conv: bad geometry");
   TORCH_CHECK(x.numel() == N * H * W * Cin && w.numel() == Cout * 9 * Cin && y.numel() == N * OH * OW * Cout &&
                   N * std::max(H * W * Cin, OH * OW * Cout) < (1LL << 31),

@@ -316,8 +316,9 @@ int launch_direct(DirectArgs a, bool bwd, hipStream_t s) {
 
 }  // namespace
 
-// cfg: 0 = CIP 32 / COT 32, 1 = CIP 32 / COT 64, 2 = CIP 64 / COT 32, 3 = CIP 64 / COT 64 (3x3 only)
-int direct_conv_num_cfgs() { return 4; }
+// cfg: 0 = CIP 32 / COT 32, 1 = CIP 32 / COT 64, 2 = CIP 64 / COT 32, 3 = CIP 64 / COT 64,
+// 4 = CIP 96 / COT 32 (Inception Conv2d_4a: 80 channels) - 3x3 only
+int direct_conv_num_cfgs() { return 5; }
 
 int direct_conv_launch(const bf16_t* x, const bf16_t* w, bf16_t* y, float* part, int G, int N, int H, int W,
                        int Cin, int OH, int OW, int Cout, int pt, int pl, int cfg, const bf16_t* y_bn,
@@ -333,6 +334,7 @@ int direct_conv_launch(const bf16_t* x, const bf16_t* w, bf16_t* y, float* part,
     case 1: return Cin <= 32 ? launch_direct<32, 3, 3, 64>(a, bwd, s) : 3;
     case 2: return Cin <= 64 ? launch_direct<64, 3, 3, 32>(a, bwd, s) : 3;
     case 3: return Cin <= 64 ? launch_direct<64, 3, 3, 64>(a, bwd, s) : 3;
+    case 4: return Cin <= 96 ? launch_direct<96, 3, 3, 32>(a, bwd, s) : 3;
     default: return 3;
   }
 }

@@ -490,14 +490,14 @@ DIRECT_FORCE = None  # tests: force a direct-kernel variant on every eligible la
 DIRECT_DGRAD = os.environ.get("IMGCLS_DIRECT_DGRAD", "1") == "1"  # data gradients (+ BN-backward epilogue)
 DIRECT_BASE = 100  # cfg[2] >= DIRECT_BASE: the halo-tile direct kernel (csrc/direct_conv.hip), variant cfg - base
 # variant -> (padded input channels, output-channel tile)
-DIRECT_CFGS = {0: (32, 32), 1: (32, 64), 2: (64, 32), 3: (64, 64)}
+DIRECT_CFGS = {0: (32, 32), 1: (32, 64), 2: (64, 32), 3: (64, 64), 4: (96, 32)}
 
 
 def _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales):
     """(N, H, W, Cin, OH, OW, Cout, pt, pl, tap order) when this launch is a stride-1 3x3 conv the direct
     kernel handles - a forward conv, or the single-phase data gradient of a stride-1 3x3 conv (a 3x3 conv
     of dY with the transposed, flipped weights), optionally with the fused BN-backward epilogue - with
-    <= 64 input channels, a dense output and no addend / residual; else None.  The tap order maps the
+    <= 96 input channels, a dense output and no addend / residual; else None.  The tap order maps the
     kernel's (th, tw) to the GEMM's weight tap (identity for the forward conv)."""
     m, co, k, cx, gh, gw, ih, iw, sa = geo[:9]
     if not DIRECT_CONV or scales[0] is not None or bias is not None or addend is not None or bwd[1] is not None:
@@ -506,7 +506,7 @@ def _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales):
         return None
     if sa != 1 or geo[12] != 1 or geo[13] or geo[14] or geo[15] != co or geo[16] or len(dh) != 9:
         return None
-    if cx % 8 or cx > 64 or co % 8 or k != 9 * cx or m % (gh * gw) or out.shape[1] != co:
+    if cx % 8 or cx > 96 or co % 8 or k != 9 * cx or m % (gh * gw) or out.shape[1] != co:
         return None
     pt, pl = -min(dh), -min(dw)
     order = [None] * 9

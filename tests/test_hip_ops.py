@@ -244,6 +244,7 @@ def test_stem_direct_matches_gemm(hw):
     (2, 64, 56, 56, 64, 1),   # ResNet layer1
     (1, 24, 19, 45, 40, 1),   # partial channel tiles, odd sizes
     (3, 8, 9, 17, 16, 0),
+    (2, 80, 19, 19, 48, 0),   # Inception Conv2d_4a channels (96-padded variant)
 ])
 def test_direct_conv(case):
     """Halo-tile direct 3x3 conv (csrc/direct_conv.hip), every variant that fits, against fp32 torch:
@@ -274,8 +275,8 @@ def test_direct_conv(case):
     assert ran > 0
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
-@pytest.mark.parametrize("case", [(2, 32, 23, 32, 0), (2, 32, 21, 64, 1), (2, 64, 20, 64, 1)])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("case", [(2, 32, 23, 32, 0), (2, 32, 21, 64, 1), (2, 64, 20, 64, 1), (2, 80, 13, 80, 0)])
 def test_direct_conv_chain(case, variant):
     """conv -> BN -> ReLU -> 3x3 conv -> BN with every eligible launch forced onto one direct-kernel
     variant: forward, and the second conv's data gradient with the fused BN-backward epilogue (the first
