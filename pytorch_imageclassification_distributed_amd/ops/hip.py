@@ -620,7 +620,7 @@ def conv_dgrad_raw(dy, w_param, g: ConvGeom, addend=None, link=None):
 WGRAD_TARGET_BLOCKS = int(os.environ.get("IMGCLS_WGRAD_BLOCKS", "0"))  # 0 = autotune per shape
 WGRAD_TUNE_LOG: list = []  # (Co, Ntot, pixels, {(blocks, stages): ms}) per tuned wgrad shape
 WGRAD_MIN_K = int(os.environ.get("IMGCLS_WGRAD_MIN_K", "512"))
-WGRAD_CANDIDATES = (256, 512, 1024, 2048)
+WGRAD_CANDIDATES = tuple(int(v) for v in os.environ.get("IMGCLS_WGRAD_CANDS", "256,384,512,768,1024,1536,2048").split(","))
 _WGRAD_TUNED: dict = {}
 
 
