@@ -80,10 +80,26 @@ def test_conv_fwd_bwd(case):
     assert rel_err(conv.weight.grad, wr.grad) < 2e-2
 
 
-N_CFG_MAX = 24  # >= len(hip.conv_cfgs()); indices past the table skip
+def _table_len(name, default):
+    """Length of a kernel configuration table, read from the built extension at collection time so
+    the parametrisation is exact; without the extension fall back to an upper bound (indices past the
+    table then skip)."""
+    try:
+        return len(getattr(_hip(), name)())
+    except Exception:  # extension not built / not importable here
+        return default
 
 
-@pytest.mark.parametrize("cfg", range(N_CFG_MAX))
+N_CFG = _table_len("conv_cfgs", 24)
+N_FP8_CFG = _table_len("conv_fp8_cfgs", 8)
+
+
+def _wgrad_stage_ok(case, stages):
+    # stages 4 = 256x256 8-wave tile (Cout >= 256), 5/6 = 32-row tile (Cout <= 32)
+    return not ((stages == 4 and case[4] < 256) or (stages >= 5 and case[4] > 32))
+
+
+@pytest.mark.parametrize("cfg", range(N_CFG))
 @pytest.mark.parametrize("case", [CONV_CASES[1], CONV_CASES[2], CONV_CASES[3], CONV_CASES[6], CONV_CASES[7],
                                   CONV_CASES[10], CONV_CASES[12]])
 def test_conv_tile_configs(case, cfg):
@@ -99,19 +115,15 @@ def test_conv_tile_configs(case, cfg):
         hip.CONV_FORCE_CFG = keep
 
 
-@pytest.mark.parametrize("stages", [1, 2, 3, 4, 5, 6])
-@pytest.mark.parametrize("case", [CONV_CASES[0], CONV_CASES[1], CONV_CASES[4], CONV_CASES[5], CONV_CASES[6],
-                                  CONV_CASES[7], CONV_CASES[8], CONV_CASES[12], CONV_CASES[13], CONV_CASES[14]])
+@pytest.mark.parametrize("case,stages", [
+    (c, st) for c in [CONV_CASES[i] for i in (0, 1, 4, 5, 6, 7, 8, 12, 13, 14)] for st in (1, 2, 3, 4, 5, 6)
+    if _wgrad_stage_ok(c, st)])
 def test_conv_wgrad_ring_variants(case, stages):
     """Weight-gradient kernel variants: 1-stage (occupancy), 2-stage ring, the 8-wave in-block
     2-way pixel split (stages=3), the 256x256 8-wave tile (stages=4, Cout >= 256) and the 32-row tile
     (stages=5 / 6, Cout <= 32) - each over the
     tuner's split counts."""
     hip = _hip()
-    if stages == 4 and case[4] < 256:
-        pytest.skip("256x256 wgrad tile needs Cout >= 256")
-    if stages >= 5 and case[4] > 32:
-        pytest.skip("32-row wgrad tile needs Cout <= 32")
     keep, hip.WGRAD_STAGES = hip.WGRAD_STAGES, stages
     try:
         test_conv_fwd_bwd(case)
@@ -119,7 +131,7 @@ def test_conv_wgrad_ring_variants(case, stages):
         hip.WGRAD_STAGES = keep
 
 
-@pytest.mark.parametrize("cfg", range(N_CFG_MAX))
+@pytest.mark.parametrize("cfg", range(N_CFG))
 @pytest.mark.parametrize("act,use_res", [("relu", True), ("silu", False)])
 def test_conv_bn_act_tile_configs(act, use_res, cfg):
     """Fused epilogues (BN statistics, residual) on every configuration of the table."""
@@ -275,8 +287,17 @@ def test_direct_conv(case):
     assert ran > 0
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
-@pytest.mark.parametrize("case", [(2, 32, 23, 32, 0), (2, 32, 21, 64, 1), (2, 64, 20, 64, 1), (2, 80, 13, 80, 0)])
+def _direct_fits(case, variant):
+    try:
+        cip = _hip().DIRECT_CFGS[variant][0]
+    except Exception:  # extension not importable: keep the case, the test skips it at run time
+        return True
+    return case[1] <= cip and case[3] <= cip
+
+
+@pytest.mark.parametrize("case,variant", [
+    (c, v) for c in [(2, 32, 23, 32, 0), (2, 32, 21, 64, 1), (2, 64, 20, 64, 1), (2, 80, 13, 80, 0)]
+    for v in range(5) if _direct_fits(c, v)])
 def test_direct_conv_chain(case, variant):
     """conv -> BN -> ReLU -> 3x3 conv -> BN with every eligible launch forced onto one direct-kernel
     variant: forward, and the second conv's data gradient with the fused BN-backward epilogue (the first
@@ -752,7 +773,7 @@ def test_fp8_conv_forward(shape):
     assert rel_err(y8, y16.float()) < 8e-2
 
 
-@pytest.mark.parametrize("cfg", range(8))
+@pytest.mark.parametrize("cfg", range(N_FP8_CFG))
 @pytest.mark.parametrize("shape", [(256, 128, 1, 1, 14), (128, 256, 3, 1, 12), (256, 512, 1, 2, 14)])
 def test_fp8_conv_tile_configs(shape, cfg):
     """Every entry of the MX-FP8 kernel's configuration table (incl. the 256x256 8-wave tile)."""
