@@ -16,6 +16,7 @@
 //   [SyncBN: all-reduce of the two sums]
 //   bn_bwd_elemt  -> dy = scale * (dz - sum_dz/n - xhat * sum_dzxhat/n)
 // Eval (K7): bn_eval_coef -> scale/shift from running stats, then bn_apply.
+#include <numeric>
 #include "common.h"
 
 namespace {
@@ -168,21 +169,28 @@ __global__ void bn_eval_coef_kernel(const float* __restrict__ gamma, const float
 }
 
 // ---- apply: out = act(y*scale + shift [+ res]) -----------------------------
+// Channel-fixed mapping: the launcher sizes the grid so the thread count is a multiple of C/8, so a
+// thread keeps ONE 8-channel chunk for its whole grid-stride loop (same addresses per iteration as the
+// flat i -> (row, chunk) walk).  The per-channel coefficients are then loaded once per thread instead
+// of once per 16-byte vector, and the 64-bit i / cch division leaves the loop (grid_chan below).
 __global__ void bn_apply_kernel(const bf16_t* __restrict__ y, const float* __restrict__ coef,
                                 const bf16_t* __restrict__ res, bf16_t* __restrict__ out, long rows,
                                 int C, int ldo, int c_off, int act) {
   const int cch = C >> 3;
-  const long total = rows * cch;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const long row = i / cch;
-    const int c0 = (int)(i - row * cch) * 8;
-    float v[8], sc[8], sh[8];
+  const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (cch == 0) return;
+  const long rstride = ((long)gridDim.x * blockDim.x) / cch;
+  long row = t / cch;
+  if (row >= rows) return;
+  const int c0 = (int)(t - row * cch) * 8;
+  float sc[8], sh[8];
+  *(float4*)sc = *(const float4*)(coef + c0);
+  *(float4*)(sc + 4) = *(const float4*)(coef + c0 + 4);
+  *(float4*)sh = *(const float4*)(coef + C + c0);
+  *(float4*)(sh + 4) = *(const float4*)(coef + C + c0 + 4);
+  for (; row < rows; row += rstride) {
+    float v[8], r[8];
     unpack8(*(const uint4*)(y + row * C + c0), v);
-    *(float4*)sc = *(const float4*)(coef + c0);
-    *(float4*)(sc + 4) = *(const float4*)(coef + c0 + 4);
-    *(float4*)sh = *(const float4*)(coef + C + c0);
-    *(float4*)(sh + 4) = *(const float4*)(coef + C + c0 + 4);
-    float r[8];
     if (res) unpack8(*(const uint4*)(res + row * C + c0), r);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -414,29 +422,37 @@ DEVI void load8f(const float* p, float* v) {
   *(float4*)(v + 4) = *(const float4*)(p + 4);
 }
 
+// channel-fixed mapping as bn_apply_kernel: five (six with an activation) per-channel coefficient
+// vectors per thread instead of per 16-byte vector - at C >= 512 those loads were the bound
+// (3.5-4.6 TB/s against 4.7-6 TB/s at C <= 256, profiles/r1c_bn_elementwise_bandwidth_b512.txt)
 __global__ void bn_bwd_elemt_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ y,
                                     const float* __restrict__ coef, const float* __restrict__ kk,
                                     const bf16_t* __restrict__ res, const bf16_t* __restrict__ dz_in,
                                     bf16_t* __restrict__ dy, long rows, int C, int act, int ldg) {
   const int cch = C >> 3;
-  const long total = rows * cch;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const long row = i / cch;
-    const int c0 = (int)(i - row * cch) * 8;
-    float gv[8], yv[8], sc[8], mu[8], is[8], k1[8], k2[8];
+  const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (cch == 0) return;
+  const long rstride = ((long)gridDim.x * blockDim.x) / cch;
+  long row = t / cch;
+  if (row >= rows) return;
+  const int c0 = (int)(t - row * cch) * 8;
+  const bool fuse_act = !dz_in && act != ACT_NONE;
+  float sc[8], sh[8], mu[8], is[8], k1[8], k2[8];
+  load8f(coef + c0, sc);
+  load8f(coef + 2 * C + c0, mu);
+  load8f(coef + 3 * C + c0, is);
+  load8f(kk + c0, k1);
+  load8f(kk + C + c0, k2);
+  if (fuse_act) load8f(coef + C + c0, sh);
+  for (; row < rows; row += rstride) {
+    float gv[8], yv[8];
     unpack8(*(const uint4*)(y + row * C + c0), yv);
-    load8f(coef + c0, sc);
-    load8f(coef + 2 * C + c0, mu);
-    load8f(coef + 3 * C + c0, is);
-    load8f(kk + c0, k1);
-    load8f(kk + C + c0, k2);
     if (dz_in) {
       unpack8(*(const uint4*)(dz_in + row * C + c0), gv);
     } else {
       unpack8(*(const uint4*)(g + row * ldg + c0), gv);
-      if (act != ACT_NONE) {
-        float sh[8], rv[8];
-        load8f(coef + C + c0, sh);
+      if (fuse_act) {
+        float rv[8];
         if (res) unpack8(*(const uint4*)(res + row * C + c0), rv);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -497,6 +513,16 @@ int grid_for(long work, int per_block = 256, int cap = 4096) {
   return (int)(b < 1 ? 1 : (b > cap ? cap : b));
 }
 
+// grid for the channel-fixed elementwise kernels: grid_for's block count rounded up so that
+// blocks * 256 is a multiple of C/8 (threads past the last row return at once)
+int grid_chan(long rows, int C) {
+  const int cch = C / 8;
+  if (cch <= 0) return 1;
+  const int m = cch / std::gcd(cch, 256);
+  const int b = grid_for(rows * cch, 256, 8192);
+  return (b + m - 1) / m * m;
+}
+
 }  // namespace
 
 int bn_partials_launch(float* part, int G, int C, double* sums, float* dgamma, float* dbeta, double count,
@@ -550,7 +576,7 @@ int bn_apply_launch(const bf16_t* y, const float* coef, const bf16_t* res, bf16_
     HIP_CHECK_LAUNCH();
     return 0;
   }
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(work, 256, 8192)), dim3(256), 0, s, y, coef, res, out,
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_chan(rows, C)), dim3(256), 0, s, y, coef, res, out,
                      rows, C, ldo, c_off, act);
   HIP_CHECK_LAUNCH();
   return 0;
@@ -574,8 +600,7 @@ int bn_bwd_k_launch(const double* sums, const double* count_p, double n, int C, 
 int bn_bwd_elemt_launch(const bf16_t* g, const bf16_t* y, const float* coef, const float* k,
                         const bf16_t* res, const bf16_t* dz_in, bf16_t* dy, long rows, int C, int act,
                         int ldg, hipStream_t s) {
-  const long work = rows * (C / 8);
-  hipLaunchKernelGGL(bn_bwd_elemt_kernel, dim3(grid_for(work, 256, 8192)), dim3(256), 0, s, g, y, coef, k,
+  hipLaunchKernelGGL(bn_bwd_elemt_kernel, dim3(grid_chan(rows, C)), dim3(256), 0, s, g, y, coef, k,
                      res, dz_in, dy, rows, C, act, ldg > 0 ? ldg : C);
   HIP_CHECK_LAUNCH();
   return 0;
