@@ -252,9 +252,47 @@ __global__ void bn_apply_mx_kernel(const bf16_t* __restrict__ y, const float* __
 // written or re-read.  (The backward keeps maxpool_bwd -> bn_bwd_reduce -> bn_bwd_elemt: gathering the
 // pooled gradient inside both BN-backward passes was measured slower, 815 vs 720 us at batch 256 - the
 // 4-window gather costs as much as the full-resolution write + read it saves, and would run twice.)
+DEVI void load8f(const float* p, float* v) {
+  *(float4*)v = *(const float4*)p;
+  *(float4*)(v + 4) = *(const float4*)(p + 4);
+}
+
 struct PoolWin {  // max pool window over a [N, H, W, C] input -> [N, OH, OW, C]
   int H, W, OH, OW, kh, kw, sh, sw, ph, pw;
 };
+
+// out = max over the window of act(y*scale + shift) (rounded to bf16 first, so the max and its index
+// are those of the activation tensor the unfused path would pool), idx = window position of the max
+DEVI void bn_act_pool_one(const bf16_t* __restrict__ y, bf16_t* __restrict__ out, uint8_t* __restrict__ idx,
+                          int C, const PoolWin& g, int act, long n, int oh, int ow, int c0, const float* sc,
+                          const float* sh) {
+  float best[8];
+  int bi[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; bi[k] = 0; }
+  for (int r = 0; r < g.kh; ++r) {
+    const int ih = oh * g.sh - g.ph + r;
+    if ((unsigned)ih >= (unsigned)g.H) continue;
+    for (int c = 0; c < g.kw; ++c) {
+      const int iw = ow * g.sw - g.pw + c;
+      if ((unsigned)iw >= (unsigned)g.W) continue;
+      float v[8];
+      unpack8(*(const uint4*)(y + ((n * g.H + ih) * g.W + iw) * C + c0), v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = apply_act(v[k] * sc[k] + sh[k], act);
+      unpack8(pack8(v), v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (v[k] > best[k] || (v[k] != v[k])) { best[k] = v[k]; bi[k] = r * g.kw + c; }
+    }
+  }
+  const long o = ((n * g.OH + oh) * g.OW + ow) * C + c0;
+  *(uint4*)(out + o) = pack8(best);
+  uint2 pk;
+  pk.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
+  pk.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
+  *(uint2*)(idx + o) = pk;
+}
 
 // out = max over the window of act(y*scale + shift) (rounded to bf16 first, so the max and its index
 // are those of the activation tensor the unfused path would pool), idx = window position of the max
@@ -269,36 +307,38 @@ __global__ void bn_act_maxpool_kernel(const bf16_t* __restrict__ y, const float*
     const int ow = (int)(t % g.OW); t /= g.OW;
     const int oh = (int)(t % g.OH);
     const long n = t / g.OH;
-    float sc[8], sh[8], best[8];
-    int bi[8];
-    *(float4*)sc = *(const float4*)(coef + c0);
-    *(float4*)(sc + 4) = *(const float4*)(coef + c0 + 4);
-    *(float4*)sh = *(const float4*)(coef + C + c0);
-    *(float4*)(sh + 4) = *(const float4*)(coef + C + c0 + 4);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; bi[k] = 0; }
-    for (int r = 0; r < g.kh; ++r) {
-      const int ih = oh * g.sh - g.ph + r;
-      if ((unsigned)ih >= (unsigned)g.H) continue;
-      for (int c = 0; c < g.kw; ++c) {
-        const int iw = ow * g.sw - g.pw + c;
-        if ((unsigned)iw >= (unsigned)g.W) continue;
-        float v[8];
-        unpack8(*(const uint4*)(y + ((n * g.H + ih) * g.W + iw) * C + c0), v);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = apply_act(v[k] * sc[k] + sh[k], act);
-        unpack8(pack8(v), v);
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (v[k] > best[k] || (v[k] != v[k])) { best[k] = v[k]; bi[k] = r * g.kw + c; }
-      }
-    }
-    const long o = ((n * g.OH + oh) * g.OW + ow) * C + c0;
-    *(uint4*)(out + o) = pack8(best);
-    uint2 pk;
-    pk.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
-    pk.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
-    *(uint2*)(idx + o) = pk;
+    float sc[8], sh[8];
+    load8f(coef + c0, sc);
+    load8f(coef + C + c0, sh);
+    bn_act_pool_one(y, out, idx, C, g, act, n, oh, ow, c0, sc, sh);
+  }
+}
+
+// < 2^31 work items (every stem in the zoo): 32-bit multiply-shift index math instead of five 64-bit
+// divisions per vector, and - the grid stride being a multiple of C/8 (grid_chan) - one fixed channel
+// chunk per thread with its BN coefficients loaded once
+struct PoolIdx {
+  FastDiv cch, OW, OH;
+};
+
+__global__ void bn_act_maxpool32_kernel(const bf16_t* __restrict__ y, const float* __restrict__ coef,
+                                        bf16_t* __restrict__ out, uint8_t* __restrict__ idx, int C, PoolWin g,
+                                        PoolIdx fd, uint32_t total, int act) {
+  const int cch = C >> 3;
+  const uint32_t t0 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t0 >= total) return;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  const int c0 = (int)(t0 - fdiv(t0, fd.cch) * cch) * 8;
+  float sc[8], sh[8];
+  load8f(coef + c0, sc);
+  load8f(coef + C + c0, sh);
+  for (uint32_t i = t0; i < total; i += stride) {
+    const uint32_t pix = fdiv(i, fd.cch);
+    const uint32_t t = fdiv(pix, fd.OW);
+    const int ow = (int)(pix - t * g.OW);
+    const uint32_t n = fdiv(t, fd.OH);
+    const int oh = (int)(t - n * g.OH);
+    bn_act_pool_one(y, out, idx, C, g, act, (long)n, oh, ow, c0, sc, sh);
   }
 }
 
@@ -417,10 +457,6 @@ __global__ void bn_bwd_k_kernel(const double* __restrict__ sums, const double* _
   kout[C + c] = (float)(sums[C + c] / n);
 }
 
-DEVI void load8f(const float* p, float* v) {
-  *(float4*)v = *(const float4*)p;
-  *(float4*)(v + 4) = *(const float4*)(p + 4);
-}
 
 // channel-fixed mapping as bn_apply_kernel: five (six with an activation) per-channel coefficient
 // vectors per thread instead of per 16-byte vector - at C >= 512 those loads were the bound
@@ -618,6 +654,13 @@ int bn_act_maxpool_launch(const bf16_t* y, const float* coef, bf16_t* out, uint8
                           const int* geo, int act, hipStream_t s) {
   const PoolWin g{geo[0], geo[1], geo[2], geo[3], geo[4], geo[5], geo[6], geo[7], geo[8], geo[9]};
   const long work = (long)N * g.OH * g.OW * (C / 8);
+  if (work < (1L << 31)) {
+    const PoolIdx fd{make_fastdiv(C / 8), make_fastdiv(g.OW), make_fastdiv(g.OH)};
+    hipLaunchKernelGGL(bn_act_maxpool32_kernel, dim3(grid_chan((long)N * g.OH * g.OW, C)), dim3(256), 0, s, y, coef,
+                       out, idx, C, g, fd, (uint32_t)work, act);
+    HIP_CHECK_LAUNCH();
+    return 0;
+  }
   hipLaunchKernelGGL(bn_act_maxpool_kernel, dim3(grid_for(work, 256, 8192)), dim3(256), 0, s, y, coef, out, idx, N,
                      C, g, act);
   HIP_CHECK_LAUNCH();
