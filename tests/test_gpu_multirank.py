@@ -23,6 +23,12 @@ def _port():
 def _worker(rank, world, port, out_dir, name="resnet18"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    # Fixed kernel choices (shape heuristic, one weight-gradient plan) in every process: ResNet-50 train-mode
+    # gradients at random init are chaotic - 0.1 % fp32 weight noise alone drops some BN-bias gradient
+    # cosines to 0.26 - so per-process timed tuner picks (two ranks contending for one GPU time the
+    # candidates differently) made the comparison flaky (scripts/dbg_tune_random.py).
+    os.environ.update(IMGCLS_CONV_STAGES="0", IMGCLS_WGRAD_BLOCKS="512", IMGCLS_WGRAD_STAGES="2",
+                      IMGCLS_DIRECT_CONV="0")
     import torch.nn.functional as F
     from pytorch_imageclassification_distributed_amd.models import Classifier
     from pytorch_imageclassification_distributed_amd.ops import functional as Fx
@@ -36,7 +42,12 @@ def _worker(rank, world, port, out_dir, name="resnet18"):
 
     def model():
         torch.manual_seed(1)
-        return Classifier(name, 7).to(dev).to(memory_format=torch.channels_last)
+        m = Classifier(name, 7)
+        with torch.no_grad():  # damp the Bottleneck residual branches (the chaos above); grads stay non-zero
+            for n, p in m.named_parameters():
+                if n.endswith("bn3.weight"):
+                    p.mul_(0.1)
+        return m.to(dev).to(memory_format=torch.channels_last)
 
     m = model()
     convert_sync_batchnorm(m)
