@@ -145,6 +145,67 @@ __global__ void maxpool_bwd2x2_kernel(const bf16_t* __restrict__ dy, const uint8
   }
 }
 
+// Stride-2 windows with k <= 3: the input pixels h = 2m - ph + {0, 1} (same for w) share the candidate
+// outputs {m - 1, m} x {m' - 1, m'}, so one lane owns that 2 x 2 input quad and loads the four candidate
+// dy / argmax vectors once for all four pixels (the per-pixel form above issues 16 loads per quad).
+struct QuadDiv {
+  FastDiv cch, MW, MH;
+};
+
+__global__ void maxpool_bwd_quad_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                        bf16_t* __restrict__ dx, PoolGeom g, QuadDiv fd, int MH, int MW,
+                                        uint32_t total) {
+  const int cch = g.C >> 3;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const uint32_t q = fdiv(i, fd.cch);
+    const int c0 = (int)(i - q * cch) * 8;
+    const uint32_t t = fdiv(q, fd.MW);
+    const int mw = (int)(q - t * MW);
+    const uint32_t n = fdiv(t, fd.MH);
+    const int mh = (int)(t - n * MH);
+    uint4 v[4];
+    uint2 pk[4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int ohc = min(max(mh - a, 0), g.OH - 1), owc = min(max(mw - b, 0), g.OW - 1);
+        const long o = (((long)n * g.OH + ohc) * g.OW + owc) * g.C + c0;
+        v[a * 2 + b] = *(const uint4*)(dy + o);
+        pk[a * 2 + b] = *(const uint2*)(idx + o);
+      }
+    }
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh) {
+      const int h = 2 * mh - g.ph + dh;
+      if ((unsigned)h >= (unsigned)g.H) continue;
+#pragma unroll
+      for (int dw = 0; dw < 2; ++dw) {
+        const int w = 2 * mw - g.pw + dw;
+        if ((unsigned)w >= (unsigned)g.W) continue;
+        float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            const int oh = mh - a, ow = mw - b, r = dh + 2 * a, c = dw + 2 * b;
+            if (oh < 0 || oh >= g.OH || ow < 0 || ow >= g.OW || r >= g.kh || c >= g.kw) continue;
+            const int me = r * g.kw + c, j = a * 2 + b;
+            float f[8];
+            unpack8(v[j], f);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              if ((int)((pk[j].x >> (8 * k)) & 0xff) == me) acc[k] += f[k];
+              if ((int)((pk[j].y >> (8 * k)) & 0xff) == me) acc[4 + k] += f[4 + k];
+            }
+          }
+        }
+        *(uint4*)(dx + (((long)n * g.H + h) * g.W + w) * g.C + c0) = pack8(acc);
+      }
+    }
+  }
+}
+
 __global__ void avgpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, PoolGeom g) {
   const int cch = g.C >> 3;
   const long total = (long)g.N * g.OH * g.OW * cch;
@@ -242,7 +303,13 @@ int maxpool_bwd_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, 
                        int OW, int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t s) {
   PoolGeom g{N, H, W, C, OH, OW, kh, kw, sh, sw, ph, pw};
   const long total = (long)N * H * W * (C / 8);
-  if ((kh - 1) / sh <= 1 && (kw - 1) / sw <= 1 && total < (1L << 31)) {
+  const int MH = (H + ph + 1) / 2, MW = (W + pw + 1) / 2;
+  const long qtotal = (long)N * MH * MW * (C / 8);
+  if (sh == 2 && sw == 2 && kh <= 3 && kw <= 3 && ph <= 1 && pw <= 1 && qtotal < (1L << 31) && C >= 8) {
+    const QuadDiv fd{make_fastdiv(C / 8), make_fastdiv(MW), make_fastdiv(MH)};
+    hipLaunchKernelGGL(maxpool_bwd_quad_kernel, dim3(grid_for(qtotal)), dim3(256), 0, s, dy, idx, dx, g, fd, MH, MW,
+                       (uint32_t)qtotal);
+  } else if ((kh - 1) / sh <= 1 && (kw - 1) / sw <= 1 && total < (1L << 31)) {
     const PoolDiv fd{make_fastdiv(C / 8), make_fastdiv(W), make_fastdiv(H), make_fastdiv(sh), make_fastdiv(sw)};
     hipLaunchKernelGGL(maxpool_bwd2x2_kernel, dim3(grid_for(total)), dim3(256), 0, s, dy, idx, dx, g, fd,
                        (uint32_t)total);

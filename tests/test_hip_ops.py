@@ -537,11 +537,14 @@ def test_conv_bn_act_pool(case):
     assert torch.equal(fused, plain)
 
 
-@pytest.mark.parametrize("kind", ["max311", "max320", "avg311", "avg530"])
-def test_pools(kind):
+@pytest.mark.parametrize("hw", [17, 16])
+@pytest.mark.parametrize("kind", ["max311", "max320", "max321", "max220", "max120", "avg311", "avg530"])
+def test_pools(kind, hw):
+    """max320 / max321 / max220 / max120 take the stride-2 quad-gather backward, max311 the 2x2-candidate
+    one; odd and even input sizes (the quad grid's last row / column is half outside the input on one)."""
     hip = _hip()
     torch.manual_seed(4)
-    x = bf(torch.randn(2, 64, 17, 17, device=DEV))
+    x = bf(torch.randn(2, 64, hw, hw + 1, device=DEV))
     xb = x.to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
     xr = x.clone().requires_grad_(True)
     k, s, p = int(kind[3]), int(kind[4]), int(kind[5])
