@@ -109,6 +109,34 @@ DEVI uint32_t fdiv(uint32_t x, const FastDiv& f) {
   return (uint32_t)(((uint64_t)__umulhi(x, f.m) + x) >> f.l);
 }
 
+// Index decode of the flat (pixel, 8-channel chunk) loop: 32-bit multiply-shift division when the
+// work fits (every layer of the zoo at batch 512), otherwise the 64-bit divisions.
+struct PixIdx {
+  FastDiv cch, X, Y;
+  int ok;
+};
+
+static inline PixIdx make_pixidx(long total, int cch, int X, int Y) {
+  if (cch <= 0 || X <= 0 || Y <= 0) return PixIdx{make_fastdiv(1), make_fastdiv(1), make_fastdiv(1), 0};
+  return PixIdx{make_fastdiv(cch), make_fastdiv(X), make_fastdiv(Y), total < (1L << 31) ? 1 : 0};
+}
+
+DEVI void pix_decode(long i, int cch, int X, int Y, const PixIdx& fd, int& c0, int& x, int& y, int& n) {
+  if (fd.ok) {
+    const uint32_t u = (uint32_t)i, p = fdiv(u, fd.cch), t = fdiv(p, fd.X), nn = fdiv(t, fd.Y);
+    c0 = (int)(u - p * cch) * 8;
+    x = (int)(p - t * X);
+    y = (int)(t - nn * Y);
+    n = (int)nn;
+  } else {
+    c0 = (int)(i % cch) * 8;
+    long t = i / cch;
+    x = (int)(t % X); t /= X;
+    y = (int)(t % Y);
+    n = (int)(t / Y);
+  }
+}
+
 // out[n][c] (+)= scale * sum_{p in split} a[n][p][c] (* b[n][p][c] when PROD), NHWC bf16 inputs, fp32 out.
 // block = CHB channel-chunk lanes (8 channels each) x RP pixel lanes, LDS tree over RP; grid =
 // (N, channel slices, pixel splits); splits > 1 accumulate with one atomic per channel per block.

@@ -79,44 +79,16 @@ __global__ void dw_dgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __r
   }
 }
 
-// Index decode of the flat (pixel, 8-channel chunk) loop: 32-bit multiply-shift division when the
-// work fits (every EfficientNet layer up to B7 at batch 512), otherwise the 64-bit divisions.
-struct DwIdx {
-  FastDiv cch, X, Y;
-  int ok;
-};
-
-DwIdx make_dwidx(long total, int cch, int X, int Y) {
-  if (cch <= 0 || X <= 0 || Y <= 0) return DwIdx{make_fastdiv(1), make_fastdiv(1), make_fastdiv(1), 0};
-  return DwIdx{make_fastdiv(cch), make_fastdiv(X), make_fastdiv(Y), total < (1L << 31) ? 1 : 0};
-}
-
-DEVI void dw_decode(long i, int cch, int X, int Y, const DwIdx& fd, int& c0, int& x, int& y, int& n) {
-  if (fd.ok) {
-    const uint32_t u = (uint32_t)i, p = fdiv(u, fd.cch), t = fdiv(p, fd.X), nn = fdiv(t, fd.Y);
-    c0 = (int)(u - p * cch) * 8;
-    x = (int)(p - t * X);
-    y = (int)(t - nn * Y);
-    n = (int)nn;
-  } else {
-    c0 = (int)(i % cch) * 8;
-    long t = i / cch;
-    x = (int)(t % X); t /= X;
-    y = (int)(t % Y);
-    n = (int)(t / Y);
-  }
-}
-
 // Fixed-size (K x K) forms of the two kernels above: taps fully unrolled, every load unconditional
 // (clamped address, zeroed value), so a lane keeps all K*K 16-B loads in flight at once.
 template <int K>
 __global__ __launch_bounds__(256) void dw_fwd_k_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
-                                                       bf16_t* __restrict__ y, DwGeom g, DwIdx fd) {
+                                                       bf16_t* __restrict__ y, DwGeom g, PixIdx fd) {
   const int cch = g.C >> 3;
   const long total = (long)g.N * g.OH * g.OW * cch;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     int c0, ow, oh, n;
-    dw_decode(i, cch, g.OW, g.OH, fd, c0, ow, oh, n);
+    pix_decode(i, cch, g.OW, g.OH, fd, c0, ow, oh, n);
     const bf16_t* xn = x + (long)n * g.H * g.W * g.C + c0;
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
@@ -146,12 +118,12 @@ __global__ __launch_bounds__(256) void dw_fwd_k_kernel(const bf16_t* __restrict_
 
 template <int K>
 __global__ __launch_bounds__(256) void dw_dgrad_k_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ w,
-                                                         bf16_t* __restrict__ dx, DwGeom g, DwIdx fd) {
+                                                         bf16_t* __restrict__ dx, DwGeom g, PixIdx fd) {
   const int cch = g.C >> 3;
   const long total = (long)g.N * g.H * g.W * cch;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     int c0, wi, h, n;
-    dw_decode(i, cch, g.W, g.H, fd, c0, wi, h, n);
+    pix_decode(i, cch, g.W, g.H, fd, c0, wi, h, n);
     const bf16_t* dyn = dy + (long)n * g.OH * g.OW * g.C + c0;
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
@@ -273,12 +245,12 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const bf16_t* __restrict_
 
 // y[n,p,c] = x[n,p,c] * s[n,c]
 __global__ void se_scale_kernel(const bf16_t* __restrict__ x, const float* __restrict__ s, bf16_t* __restrict__ y,
-                                int N, int HW, int C, DwIdx fd) {
+                                int N, int HW, int C, PixIdx fd) {
   const int cch = C >> 3;
   const long total = (long)N * HW * cch;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     int c0, p, n, z;
-    dw_decode(i, cch, HW, N, fd, c0, p, n, z);
+    pix_decode(i, cch, HW, N, fd, c0, p, n, z);
     const long pix = (long)n * HW + p;
     float v[8], sv[8];
     unpack8(*(const uint4*)(x + pix * C + c0), v);
@@ -292,13 +264,13 @@ __global__ void se_scale_kernel(const bf16_t* __restrict__ x, const float* __res
 
 // dx = dy * s[n,c] + dp[n,c] / HW
 __global__ void se_dx_kernel(const bf16_t* __restrict__ dy, const float* __restrict__ s, const float* __restrict__ dp,
-                             bf16_t* __restrict__ dx, int N, int HW, int C, DwIdx fd) {
+                             bf16_t* __restrict__ dx, int N, int HW, int C, PixIdx fd) {
   const int cch = C >> 3;
   const long total = (long)N * HW * cch;
   const float inv = 1.f / HW;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     int c0, p, n, z;
-    dw_decode(i, cch, HW, N, fd, c0, p, n, z);
+    pix_decode(i, cch, HW, N, fd, c0, p, n, z);
     const long pix = (long)n * HW + p;
     float v[8], sv[8], pv[8];
     unpack8(*(const uint4*)(dy + pix * C + c0), v);
@@ -344,9 +316,9 @@ int dw_fwd_launch(const bf16_t* x, const bf16_t* w, bf16_t* y, float* /*stats*/,
   DwGeom g{N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl};
   const dim3 grid(grid_for((long)N * OH * OW * (C / 8)));
   if (kh == 3 && kw == 3) hipLaunchKernelGGL(dw_fwd_k_kernel<3>, grid, dim3(256), 0, s, x, w, y, g,
-                                                  make_dwidx((long)N * OH * OW * (C / 8), C / 8, OW, OH));
+                                                  make_pixidx((long)N * OH * OW * (C / 8), C / 8, OW, OH));
   else if (kh == 5 && kw == 5) hipLaunchKernelGGL(dw_fwd_k_kernel<5>, grid, dim3(256), 0, s, x, w, y, g,
-                                                  make_dwidx((long)N * OH * OW * (C / 8), C / 8, OW, OH));
+                                                  make_pixidx((long)N * OH * OW * (C / 8), C / 8, OW, OH));
   else hipLaunchKernelGGL(dw_fwd_kernel, grid, dim3(256), 0, s, x, w, y, g);
   HIP_CHECK_LAUNCH();
   return 0;
@@ -357,9 +329,9 @@ int dw_dgrad_launch(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H,
   DwGeom g{N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl};
   const dim3 grid(grid_for((long)N * H * W * (C / 8)));
   if (kh == 3 && kw == 3) hipLaunchKernelGGL(dw_dgrad_k_kernel<3>, grid, dim3(256), 0, s, dy, w, dx, g,
-                                                  make_dwidx((long)N * H * W * (C / 8), C / 8, W, H));
+                                                  make_pixidx((long)N * H * W * (C / 8), C / 8, W, H));
   else if (kh == 5 && kw == 5) hipLaunchKernelGGL(dw_dgrad_k_kernel<5>, grid, dim3(256), 0, s, dy, w, dx, g,
-                                                  make_dwidx((long)N * H * W * (C / 8), C / 8, W, H));
+                                                  make_pixidx((long)N * H * W * (C / 8), C / 8, W, H));
   else hipLaunchKernelGGL(dw_dgrad_kernel, grid, dim3(256), 0, s, dy, w, dx, g);
   HIP_CHECK_LAUNCH();
   return 0;
@@ -397,7 +369,7 @@ int dw_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* /*dw*/, int N, int
 
 int se_scale_launch(const bf16_t* x, const float* sc, bf16_t* y, int N, int HW, int C, hipStream_t s) {
   hipLaunchKernelGGL(se_scale_kernel, dim3(grid_for((long)N * HW * (C / 8))), dim3(256), 0, s, x, sc, y, N, HW, C,
-                     make_dwidx((long)N * HW * (C / 8), C / 8, HW, N));
+                     make_pixidx((long)N * HW * (C / 8), C / 8, HW, N));
   HIP_CHECK_LAUNCH();
   return 0;
 }
@@ -409,7 +381,7 @@ int se_ds_launch(const bf16_t* dy, const bf16_t* x, float* ds, int N, int HW, in
 int se_dx_launch(const bf16_t* dy, const float* sc, const float* dp, bf16_t* dx, int N, int HW, int C,
                  hipStream_t s) {
   hipLaunchKernelGGL(se_dx_kernel, dim3(grid_for((long)N * HW * (C / 8))), dim3(256), 0, s, dy, sc, dp, dx, N, HW, C,
-                     make_dwidx((long)N * HW * (C / 8), C / 8, HW, N));
+                     make_pixidx((long)N * HW * (C / 8), C / 8, HW, N));
   HIP_CHECK_LAUNCH();
   return 0;
 }

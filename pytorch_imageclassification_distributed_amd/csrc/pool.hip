@@ -15,15 +15,12 @@ struct PoolGeom {
 };
 
 __global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
-                                   uint8_t* __restrict__ idx, PoolGeom g) {
+                                   uint8_t* __restrict__ idx, PoolGeom g, PixIdx fd) {
   const int cch = g.C >> 3;
   const long total = (long)g.N * g.OH * g.OW * cch;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % cch) * 8;
-    long t = i / cch;
-    const int ow = (int)(t % g.OW); t /= g.OW;
-    const int oh = (int)(t % g.OH);
-    const int n = (int)(t / g.OH);
+    int c0, ow, oh, n;
+    pix_decode(i, cch, g.OW, g.OH, fd, c0, ow, oh, n);
     float best[8];
     int bi[8];
 #pragma unroll
@@ -206,16 +203,13 @@ __global__ void maxpool_bwd_quad_kernel(const bf16_t* __restrict__ dy, const uin
   }
 }
 
-__global__ void avgpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, PoolGeom g) {
+__global__ void avgpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, PoolGeom g, PixIdx fd) {
   const int cch = g.C >> 3;
   const long total = (long)g.N * g.OH * g.OW * cch;
   const float inv = 1.f / (g.kh * g.kw);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % cch) * 8;
-    long t = i / cch;
-    const int ow = (int)(t % g.OW); t /= g.OW;
-    const int oh = (int)(t % g.OH);
-    const int n = (int)(t / g.OH);
+    int c0, ow, oh, n;
+    pix_decode(i, cch, g.OW, g.OH, fd, c0, ow, oh, n);
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int r = 0; r < g.kh; ++r) {
       const int ih = oh * g.sh - g.ph + r;
@@ -235,16 +229,13 @@ __global__ void avgpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restr
   }
 }
 
-__global__ void avgpool_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx, PoolGeom g) {
+__global__ void avgpool_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx, PoolGeom g, PixIdx fd) {
   const int cch = g.C >> 3;
   const long total = (long)g.N * g.H * g.W * cch;
   const float inv = 1.f / (g.kh * g.kw);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % cch) * 8;
-    long t = i / cch;
-    const int w = (int)(t % g.W); t /= g.W;
-    const int h = (int)(t % g.H);
-    const int n = (int)(t / g.H);
+    int c0, w, h, n;
+    pix_decode(i, cch, g.W, g.H, fd, c0, w, h, n);
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const int oh_lo = max(0, (h + g.ph - g.kh + g.sh) / g.sh);
     const int oh_hi = min(g.OH - 1, (h + g.ph) / g.sh);
@@ -294,7 +285,7 @@ int maxpool_fwd_launch(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, i
                        int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t s) {
   PoolGeom g{N, H, W, C, OH, OW, kh, kw, sh, sw, ph, pw};
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((long)N * OH * OW * (C / 8))), dim3(256), 0, s, x, y,
-                     idx, g);
+                     idx, g, make_pixidx((long)N * OH * OW * (C / 8), C / 8, OW, OH));
   HIP_CHECK_LAUNCH();
   return 0;
 }
@@ -323,7 +314,8 @@ int maxpool_bwd_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, 
 int avgpool_fwd_launch(const bf16_t* x, bf16_t* y, int N, int H, int W, int C, int OH, int OW, int kh, int kw,
                        int sh, int sw, int ph, int pw, hipStream_t s) {
   PoolGeom g{N, H, W, C, OH, OW, kh, kw, sh, sw, ph, pw};
-  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(grid_for((long)N * OH * OW * (C / 8))), dim3(256), 0, s, x, y, g);
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(grid_for((long)N * OH * OW * (C / 8))), dim3(256), 0, s, x, y, g,
+                     make_pixidx((long)N * OH * OW * (C / 8), C / 8, OW, OH));
   HIP_CHECK_LAUNCH();
   return 0;
 }
@@ -331,7 +323,8 @@ int avgpool_fwd_launch(const bf16_t* x, bf16_t* y, int N, int H, int W, int C, i
 int avgpool_bwd_launch(const bf16_t* dy, bf16_t* dx, int N, int H, int W, int C, int OH, int OW, int kh,
                        int kw, int sh, int sw, int ph, int pw, hipStream_t s) {
   PoolGeom g{N, H, W, C, OH, OW, kh, kw, sh, sw, ph, pw};
-  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_for((long)N * H * W * (C / 8))), dim3(256), 0, s, dy, dx, g);
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_for((long)N * H * W * (C / 8))), dim3(256), 0, s, dy, dx, g,
+                     make_pixidx((long)N * H * W * (C / 8), C / 8, W, H));
   HIP_CHECK_LAUNCH();
   return 0;
 }
