@@ -169,6 +169,11 @@ __global__ void bn_eval_coef_kernel(const float* __restrict__ gamma, const float
 }
 
 // ---- apply: out = act(y*scale + shift [+ res]) -----------------------------
+DEVI void load8f(const float* p, float* v) {
+  *(float4*)v = *(const float4*)p;
+  *(float4*)(v + 4) = *(const float4*)(p + 4);
+}
+
 // Channel-fixed mapping: the launcher sizes the grid so the thread count is a multiple of C/8, so a
 // thread keeps ONE 8-channel chunk for its whole grid-stride loop (same addresses per iteration as the
 // flat i -> (row, chunk) walk).  The per-channel coefficients are then loaded once per thread instead
@@ -208,42 +213,40 @@ __global__ void bn_apply_kernel(const bf16_t* __restrict__ y, const float* __res
 __global__ void bn_apply_mx_kernel(const bf16_t* __restrict__ y, const float* __restrict__ coef,
                                    const bf16_t* __restrict__ res, bf16_t* __restrict__ out, uint8_t* __restrict__ q,
                                    uint8_t* __restrict__ qs, long rows, int C, int act) {
+  // channel-fixed mapping (grid_chan) as bn_apply_kernel; C % 32 == 0 makes every 4-lane MX block share
+  // its row, so whole groups leave the loop together and the xor-shuffles below stay within live lanes
   const int cch = C >> 3;
-  const long total = rows * cch;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i - (threadIdx.x & 3) < total;
-       i += (long)gridDim.x * blockDim.x) {
-    const bool live = i < total;
-    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    const long row = i / cch;
-    const int c0 = (int)(i - row * cch) * 8;
-    if (live) {
-      float sc[8], sh[8], r[8];
-      unpack8(*(const uint4*)(y + row * C + c0), v);
-      *(float4*)sc = *(const float4*)(coef + c0);
-      *(float4*)(sc + 4) = *(const float4*)(coef + c0 + 4);
-      *(float4*)sh = *(const float4*)(coef + C + c0);
-      *(float4*)(sh + 4) = *(const float4*)(coef + C + c0 + 4);
-      if (res) unpack8(*(const uint4*)(res + row * C + c0), r);
+  if (cch == 0) return;
+  const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const long rstride = ((long)gridDim.x * blockDim.x) / cch;
+  long row = t / cch;
+  if (row >= rows) return;
+  const int ch = (int)(t - row * cch), c0 = ch * 8;
+  float sc[8], sh[8];
+  load8f(coef + c0, sc);
+  load8f(coef + C + c0, sh);
+  for (; row < rows; row += rstride) {
+    float v[8], r[8];
+    unpack8(*(const uint4*)(y + row * C + c0), v);
+    if (res) unpack8(*(const uint4*)(res + row * C + c0), r);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        float z = v[k] * sc[k] + sh[k];
-        if (res) z += r[k];
-        v[k] = apply_act(z, act);
-      }
-      const uint4 o = pack8(v);
-      *(uint4*)(out + row * C + c0) = o;
-      unpack8(o, v);  // quantise the bf16 value the backward pass will see
+    for (int k = 0; k < 8; ++k) {
+      float z = v[k] * sc[k] + sh[k];
+      if (res) z += r[k];
+      v[k] = apply_act(z, act);
     }
+    const uint4 o = pack8(v);
+    *(uint4*)(out + row * C + c0) = o;
+    unpack8(o, v);  // quantise the bf16 value the backward pass will see
     float amax = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) amax = fmaxf(amax, fabsf(v[k]));
     amax = fmaxf(amax, __shfl_xor(amax, 1));
     amax = fmaxf(amax, __shfl_xor(amax, 2));
     const int e = mx_exponent(amax);
-    if (live) {
-      *(uint2*)(q + i * 8) = to_fp8x8(v, ldexpf(1.f, -e));
-      if ((i & 3) == 0) qs[i >> 2] = (uint8_t)(e + 127);
-    }
+    const long i = row * cch + ch;
+    *(uint2*)(q + i * 8) = to_fp8x8(v, ldexpf(1.f, -e));
+    if ((i & 3) == 0) qs[i >> 2] = (uint8_t)(e + 127);
   }
 }
 
@@ -252,11 +255,6 @@ __global__ void bn_apply_mx_kernel(const bf16_t* __restrict__ y, const float* __
 // written or re-read.  (The backward keeps maxpool_bwd -> bn_bwd_reduce -> bn_bwd_elemt: gathering the
 // pooled gradient inside both BN-backward passes was measured slower, 815 vs 720 us at batch 256 - the
 // 4-window gather costs as much as the full-resolution write + read it saves, and would run twice.)
-DEVI void load8f(const float* p, float* v) {
-  *(float4*)v = *(const float4*)p;
-  *(float4*)(v + 4) = *(const float4*)(p + 4);
-}
-
 struct PoolWin {  // max pool window over a [N, H, W, C] input -> [N, OH, OW, C]
   int H, W, OH, OW, kh, kw, sh, sw, ph, pw;
 };
@@ -604,10 +602,9 @@ int bn_eval_coef_launch(const float* gamma, const float* beta, const float* rmea
 
 int bn_apply_launch(const bf16_t* y, const float* coef, const bf16_t* res, bf16_t* out, long rows, int C,
                     int ldo, int c_off, int act, uint8_t* q, uint8_t* qs, hipStream_t s) {
-  const long work = rows * (C / 8);
   if (q) {
     if (C % 32 || ldo != C || c_off) return 2;
-    hipLaunchKernelGGL(bn_apply_mx_kernel, dim3(grid_for(work, 256, 8192)), dim3(256), 0, s, y, coef, res, out, q,
+    hipLaunchKernelGGL(bn_apply_mx_kernel, dim3(grid_chan(rows, C)), dim3(256), 0, s, y, coef, res, out, q,
                        qs, rows, C, act);
     HIP_CHECK_LAUNCH();
     return 0;
