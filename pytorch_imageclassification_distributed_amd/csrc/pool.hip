@@ -259,14 +259,15 @@ __global__ void avgpool_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __rest
   }
 }
 
-__global__ void gap_bwd_kernel(const float* __restrict__ dy, bf16_t* __restrict__ dx, int N, int HW, int C) {
+__global__ void gap_bwd_kernel(const float* __restrict__ dy, bf16_t* __restrict__ dx, int N, int HW, int C,
+                               PixIdx fd) {
   const int cch = C >> 3;
   const long total = (long)N * HW * cch;
   const float inv = 1.f / HW;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % cch) * 8;
-    const long pix = i / cch;
-    const int n = (int)(pix / HW);
+    int c0, p, n, z;
+    pix_decode(i, cch, HW, N, fd, c0, p, n, z);
+    const long pix = (long)n * HW + p;
     float v[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = dy[(long)n * C + c0 + k] * inv;
@@ -334,7 +335,8 @@ int gap_fwd_launch(const bf16_t* x, float* y, int N, int HW, int C, hipStream_t 
 }
 
 int gap_bwd_launch(const float* dy, bf16_t* dx, int N, int HW, int C, hipStream_t s) {
-  hipLaunchKernelGGL(gap_bwd_kernel, dim3(grid_for((long)N * HW * (C / 8))), dim3(256), 0, s, dy, dx, N, HW, C);
+  hipLaunchKernelGGL(gap_bwd_kernel, dim3(grid_for((long)N * HW * (C / 8))), dim3(256), 0, s, dy, dx, N, HW, C,
+                     make_pixidx((long)N * HW * (C / 8), C / 8, HW, N));
   HIP_CHECK_LAUNCH();
   return 0;
 }
