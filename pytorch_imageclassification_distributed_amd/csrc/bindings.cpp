@@ -78,6 +78,7 @@ int dw_wgrad_launch(const bf16_t*, const bf16_t*, float*, int, int, int, int, in
                     int, float*, hipStream_t);
 long dw_wgrad_partial_rows(int, int, int, int, int);
 void set_deterministic(int);
+void set_force_div64(int);
 int se_scale_launch(const bf16_t*, const float*, bf16_t*, int, int, int, hipStream_t);
 int se_ds_launch(const bf16_t*, const bf16_t*, float*, int, int, int, hipStream_t);
 int se_dx_launch(const bf16_t*, const float*, const float*, bf16_t*, int, int, int, hipStream_t);
@@ -574,6 +575,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_set_variant", &conv_set_variant);
   m.def("set_deterministic", [](bool v) { set_deterministic(v ? 1 : 0); });
+  m.def("set_force_div64", [](bool v) { set_force_div64(v ? 1 : 0); });
   m.def("conv_set_single_stage", &conv_set_single_stage);
   m.def("conv_set_wgrad_variant", &conv_set_wgrad_variant);
   m.def("bn_partials", &bn_partials, pybind11::arg("part"), pybind11::arg("G"), pybind11::arg("C"),

@@ -651,7 +651,8 @@ int bn_act_maxpool_launch(const bf16_t* y, const float* coef, bf16_t* out, uint8
                           const int* geo, int act, hipStream_t s) {
   const PoolWin g{geo[0], geo[1], geo[2], geo[3], geo[4], geo[5], geo[6], geo[7], geo[8], geo[9]};
   const long work = (long)N * g.OH * g.OW * (C / 8);
-  if (work < (1L << 31)) {
+  if (work <= 0) return 0;
+  if (work < (1L << 31) && !g_imgcls_div64) {
     const PoolIdx fd{make_fastdiv(C / 8), make_fastdiv(g.OW), make_fastdiv(g.OH)};
     hipLaunchKernelGGL(bn_act_maxpool32_kernel, dim3(grid_chan((long)N * g.OH * g.OW, C)), dim3(256), 0, s, y, coef,
                        out, idx, C, g, fd, (uint32_t)work, act);

@@ -12,6 +12,9 @@
 // Deterministic mode (set from Python): every fp32 atomic accumulation site is reorganised so each
 // address receives exactly one contribution (split-K off, per-block partial rows reduced in order).
 extern int g_imgcls_det;
+// Test hook: force the 64-bit index paths (PixIdx.ok = 0, no 32-bit multiply-shift kernels) so the
+// fallback used above 2^31 work items is exercised at test sizes (tests/test_hip_ops.py).
+extern int g_imgcls_div64;
 
 
 
@@ -99,6 +102,7 @@ struct FastDiv {
 };
 
 static inline FastDiv make_fastdiv(uint32_t d) {
+  if (d == 0) d = 1;  // empty / degenerate geometry: a valid divisor, callers launch no work then
   uint32_t l = 0;
   while ((1ull << l) < d) ++l;
   const uint64_t m = ((1ull << 32) * ((1ull << l) - d)) / d + 1;
@@ -118,7 +122,7 @@ struct PixIdx {
 
 static inline PixIdx make_pixidx(long total, int cch, int X, int Y) {
   if (cch <= 0 || X <= 0 || Y <= 0) return PixIdx{make_fastdiv(1), make_fastdiv(1), make_fastdiv(1), 0};
-  return PixIdx{make_fastdiv(cch), make_fastdiv(X), make_fastdiv(Y), total < (1L << 31) ? 1 : 0};
+  return PixIdx{make_fastdiv(cch), make_fastdiv(X), make_fastdiv(Y), (total < (1L << 31) && !g_imgcls_div64) ? 1 : 0};
 }
 
 DEVI void pix_decode(long i, int cch, int X, int Y, const PixIdx& fd, int& c0, int& x, int& y, int& n) {

@@ -261,6 +261,8 @@ int weight_t_tiles_launch(const void* jobs, const void* tiles, int ntiles, hipSt
 
 int g_imgcls_det = 0;
 void set_deterministic(int v) { g_imgcls_det = v; }
+int g_imgcls_div64 = 0;
+void set_force_div64(int v) { g_imgcls_div64 = v; }
 
 int weight_t_job_bytes() { return (int)sizeof(WtJob); }
 

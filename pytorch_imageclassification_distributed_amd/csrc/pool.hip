@@ -297,11 +297,13 @@ int maxpool_bwd_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, 
   const long total = (long)N * H * W * (C / 8);
   const int MH = (H + ph + 1) / 2, MW = (W + pw + 1) / 2;
   const long qtotal = (long)N * MH * MW * (C / 8);
-  if (sh == 2 && sw == 2 && kh <= 3 && kw <= 3 && ph <= 1 && pw <= 1 && qtotal < (1L << 31) && C >= 8) {
+  if (total <= 0) return 0;
+  if (sh == 2 && sw == 2 && kh <= 3 && kw <= 3 && ph <= 1 && pw <= 1 && qtotal < (1L << 31) && C >= 8 &&
+      !g_imgcls_div64) {
     const QuadDiv fd{make_fastdiv(C / 8), make_fastdiv(MW), make_fastdiv(MH)};
     hipLaunchKernelGGL(maxpool_bwd_quad_kernel, dim3(grid_for(qtotal)), dim3(256), 0, s, dy, idx, dx, g, fd, MH, MW,
                        (uint32_t)qtotal);
-  } else if ((kh - 1) / sh <= 1 && (kw - 1) / sw <= 1 && total < (1L << 31)) {
+  } else if ((kh - 1) / sh <= 1 && (kw - 1) / sw <= 1 && total < (1L << 31) && !g_imgcls_div64) {
     const PoolDiv fd{make_fastdiv(C / 8), make_fastdiv(W), make_fastdiv(H), make_fastdiv(sh), make_fastdiv(sw)};
     hipLaunchKernelGGL(maxpool_bwd2x2_kernel, dim3(grid_for(total)), dim3(256), 0, s, dy, idx, dx, g, fd,
                        (uint32_t)total);

@@ -153,6 +153,11 @@ class Trainer:
         self.start_epoch = 0
         self.global_step = 0
         self.timer = PhaseTimer(getattr(a, "step_timers", False), self.dev)
+        self.step_stream = None
+        if self.hip and os.environ.get("IMGCLS_HIPRIO_STEP", "1") == "1":
+            lo, hi = torch.cuda.Stream.priority_range()
+            if hi < lo:  # the device has a priority above the default
+                self.step_stream = torch.cuda.Stream(device=self.dev, priority=hi)
         self.log = JsonlLogger(getattr(a, "metrics_file", None), self.ctx.is_main)
         self._prof = None
 
@@ -169,7 +174,25 @@ class Trainer:
         """forward + loss + backward + (overlapped) all-reduce + Adam.  Returns the local loss.
 
         Phases are bracketed for ``--step-timers`` (device events) and named for ``--profile-steps``
-        (torch.profiler ranges: imgcls::forward / backward / comm_wait / optimizer)."""
+        (torch.profiler ranges: imgcls::forward / backward / comm_wait / optimizer).
+
+        On the HIP path the step runs on a high-priority HIP stream: the weight gradients go to a
+        normal-priority side stream (ops/hip.py, "weight gradients on a side stream"), so the
+        dispatcher hands free CUs to the critical dgrad -> BN-backward chain first and the weight
+        GEMMs fill the rest (ResNet-50 b512: +1.5 % over one stream; the side stream at equal priority
+        was 1.8 % slower than one stream)."""
+        st = self.step_stream
+        if st is None:
+            return self._train_step(images, labels)
+        caller = torch.cuda.current_stream(self.dev)
+        st.wait_stream(caller)
+        with torch.cuda.stream(st):
+            loss = self._train_step(images, labels)
+        caller.wait_stream(st)
+        loss.record_stream(caller)
+        return loss
+
+    def _train_step(self, images, labels):
         rf = torch.profiler.record_function
         timer = self.timer
         if self.reducer is not None and getattr(self.args, "broadcast_buffers", False):
@@ -182,6 +205,9 @@ class Trainer:
             if self.arena is not None:
                 self.arena.begin()  # one memset; backward kernels write into persistent slots
             loss.backward()
+            if self.hip:
+                from ..ops import hip as _hip
+                _hip.join_side_streams()  # (normally already done by the engine callback)
         timer.mark("backward")
         with rf("imgcls::comm_wait"):
             scale = self.reducer.finish() if self.reducer is not None else 1.0

@@ -84,6 +84,13 @@ class GradArena:
                 del p._imgcls_arena
 
 
+def arena_slot(p):
+    """``p``'s armed arena slot (zeroed, persistent: autograd adopts it as ``p.grad`` without touching
+    it), or None when ``p`` has no arena or its slot was already handed out this step."""
+    a = getattr(p, "_imgcls_arena", None)
+    return a.take(p) if a is not None else None
+
+
 def grad_buffer(p, zero: bool = True) -> torch.Tensor:
     """Output buffer for ``p``'s gradient: its armed arena slot (already zero), else a new tensor
     with ``p``'s shape and memory layout."""

@@ -23,7 +23,7 @@ import torch
 import torch.distributed as dist
 
 from .. import _ext
-from .grad_arena import grad_buffer
+from .grad_arena import arena_slot, grad_buffer
 
 C = _ext.load()
 
@@ -43,6 +43,12 @@ def set_deterministic(flag: bool = True) -> None:
 
 
 C.set_deterministic(DETERMINISTIC)
+
+
+def set_force_div64(flag: bool = True) -> None:
+    """Test hook: take the 64-bit index-division paths of the pool / depthwise / SE / GAP / stem-pool
+    kernels (normally used only above 2^31 work items) at any size."""
+    C.set_force_div64(bool(flag))
 
 
 def stat_groups(rows: int) -> int:
@@ -692,16 +698,97 @@ def _wgrad_config(dy, x, g: ConvGeom, m, ntot):
     return best
 
 
+# ---------------------------------------------------------------------------
+# weight gradients on a side stream
+# ---------------------------------------------------------------------------
+# A weight gradient is off the backward critical path: only the optimizer (and the bucket all-reduce)
+# read it, while the next layer's backward needs only the data gradient.  Each conv's wgrad GEMM is
+# therefore enqueued on a second HIP stream behind an event on the compute stream, so it runs beside the
+# dgrad -> BN-backward chain of the layers below (filling the last partial wave of a 1-2 wave launch, and
+# pairing compute-bound wgrad tiles with bandwidth-bound BN kernels on the same CUs).  Only gradients
+# that land in an armed arena slot go there (autograd adopts the slot without reading it); the compute
+# stream waits for the side stream when backward ends (an engine callback), and the reducer issues each
+# bucket's all-reduce behind both streams.  IMGCLS_WGRAD_STREAM=0 keeps everything on one stream.
+WGRAD_STREAM = os.environ.get("IMGCLS_WGRAD_STREAM", "1") == "1"
+_SIDE: dict = {}  # device index -> _SideStream
+
+
+class _SideStream:
+    __slots__ = ("stream", "joins")
+
+    def __init__(self, dev):
+        self.stream = torch.cuda.Stream(device=dev)
+        self.joins = set()  # compute streams that must wait for this stream when backward ends
+
+
+def side_stream(dev):
+    """The weight-gradient stream of ``dev``, or None (disabled, CPU, or inside a graph capture)."""
+    if not WGRAD_STREAM or dev.type != "cuda" or torch.cuda.is_current_stream_capturing():
+        return None
+    s = _SIDE.get(dev.index)
+    if s is None:
+        s = _SIDE[dev.index] = _SideStream(dev)
+    return s
+
+
+def join_side_streams() -> None:
+    """Make every compute stream that handed work to a side stream wait for it (no host sync)."""
+    for s in _SIDE.values():
+        for main in s.joins:
+            main.wait_stream(s.stream)
+        s.joins.clear()
+
+
+def _on_side(dev, launch, *keep):
+    """Run ``launch()`` on the side stream of ``dev`` behind the current stream's work so far; the
+    tensors in ``keep`` stay allocated until the side stream is done with them."""
+    s = side_stream(dev)
+    if s is None:
+        launch()
+        return
+    main = torch.cuda.current_stream(dev)
+    if not s.joins:
+        # first side launch of this backward: join when the engine finishes the whole graph
+        torch.autograd.Variable._execution_engine.queue_callback(join_side_streams)
+    s.joins.add(main)
+    s.stream.wait_stream(main)
+    with torch.cuda.stream(s.stream):
+        launch()
+    for t in keep:
+        t.record_stream(s.stream)
+
+
+def comm_stream(dev):
+    """Stream to issue a gradient all-reduce on: the side stream after it has waited for the compute
+    stream (so the collective follows every gradient of both), or None for the current stream."""
+    s = _SIDE.get(dev.index) if dev.type == "cuda" else None
+    if s is None or not s.joins:
+        return None
+    s.stream.wait_stream(torch.cuda.current_stream(dev))
+    return s.stream
+
+
 def conv_wgrad_raw(dy, x, w_param, g: ConvGeom):
     dev = dy.device
     m = g.N * g.OH * g.OW
     ntot = g.T * g.Cx
     kps, splits, stages = _wgrad_plan(g, dy, x, m, ntot)
     if g.Cx == g.Ci:
+        dw = arena_slot(w_param)
+        if dw is not None:
+            _on_side(dev, lambda: _wgrad_launch(dy, x, dw, g, m, ntot, kps, splits, stages), dy, x)
+            return dw
         dw = grad_buffer(w_param)
         _wgrad_launch(dy, x, dw, g, m, ntot, kps, splits, stages)
         return dw
     full = torch.zeros(g.Co * ntot, dtype=torch.float32, device=dev)
+    dw = arena_slot(w_param)
+    if dw is not None:
+        def launch():
+            _wgrad_launch(dy, x, full, g, m, ntot, kps, splits, stages)
+            C.grad_unpad(full, dw, g.Co * g.T, g.Cx, g.Ci)
+        _on_side(dev, launch, dy, x, full)
+        return dw
     _wgrad_launch(dy, x, full, g, m, ntot, kps, splits, stages)
     dw = grad_buffer(w_param, zero=False)
     C.grad_unpad(full, dw, g.Co * g.T, g.Cx, g.Ci)
@@ -893,9 +980,17 @@ class StemS2dFn(torch.autograd.Function):
             m, ntot = g.N * g.OH * g.OW, g.T * g.Cx
             kps, splits, stages = _wgrad_plan(g, dy, xs, m, ntot)
             full = torch.zeros(g.Co * ntot, dtype=torch.float32, device=dy.device)
-            _wgrad_launch(dy, xs, full, g, m, ntot, kps, splits, stages)
-            dw = grad_buffer(w, zero=False)
-            dw.permute(0, 2, 3, 1).reshape(g.Co, 147).copy_(full.view(g.Co, ntot)[:, _s2d_index(dy.device)])
+            idx = _s2d_index(dy.device)
+            slot = arena_slot(w)
+            dw = slot if slot is not None else grad_buffer(w, zero=False)
+
+            def launch():
+                _wgrad_launch(dy, xs, full, g, m, ntot, kps, splits, stages)
+                dw.permute(0, 2, 3, 1).reshape(g.Co, 147).copy_(full.view(g.Co, ntot)[:, idx])
+            if slot is not None:
+                _on_side(dy.device, launch, dy, xs, full)
+            else:
+                launch()
         return None, dw, None, None
 
 

@@ -31,11 +31,21 @@ MI355X design:
 """
 from __future__ import annotations
 
+import contextlib
+
 import torch
 import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops.grad_arena import GradArena
+
+
+def _comm_stream(dev):
+    """The HIP path's side stream for a bucket all-reduce (ops.hip.comm_stream), else None."""
+    if dev.type != "cuda":
+        return None
+    from ..ops import hip
+    return hip.comm_stream(dev)
 
 
 def broadcast_module_state(module: nn.Module, src: int = 0, group=None) -> None:
@@ -141,11 +151,19 @@ class GradReducer:
             return
         s, e, _ = self.buckets[b]
         t = self.flat[s:e]
-        if self.comm_dtype is not None and self.comm_dtype != torch.float32:
-            c = t.to(self.comm_dtype)
-            self.works.append((dist.all_reduce(c, group=self.group, async_op=True), t, c))
-        else:
-            self.works.append((dist.all_reduce(t, group=self.group, async_op=True), None, None))
+        # weight gradients may still be in flight on the HIP path's side stream: issue the collective
+        # from that stream once it has waited for the compute stream (ProcessGroupNCCL orders its RCCL
+        # stream behind the current one), so it follows the bucket's gradients from both streams
+        side = _comm_stream(t.device)
+        main = torch.cuda.current_stream(t.device) if side is not None else None
+        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            if self.comm_dtype is not None and self.comm_dtype != torch.float32:
+                c = t.to(self.comm_dtype)
+                if main is not None:
+                    c.record_stream(main)  # copied back on the compute stream in finish()
+                self.works.append((dist.all_reduce(c, group=self.group, async_op=True), t, c))
+            else:
+                self.works.append((dist.all_reduce(t, group=self.group, async_op=True), None, None))
 
     # ------------------------------------------------------------------ step
     @torch.no_grad()

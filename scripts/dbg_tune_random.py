@@ -1,6 +1,8 @@
 """Random kernel-choice sweep: the per-shape tuner picks a random candidate for every conv / wgrad
-shape (timings replaced by random numbers), ResNet-50 gradients are compared with the CPU fp32 path
-per trial, and every (shape, choice) is logged with the trial's worst cosine -> gpurun_out/."""
+shape (timings replaced by random numbers), ResNet-50 gradients are compared per trial with one GPU
+run on fixed heuristic choices (no tuner, no direct conv, one wgrad plan), and every (shape, choice) is
+logged with the trial's worst cosine -> gpurun_out/.  The CPU fp32 conditioning experiment (weight
+noise instead of kernel choices) is scripts/cpu_weight_noise.py."""
 import json
 import random
 import sys

@@ -20,15 +20,16 @@ def _port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir, name="resnet18"):
+def _worker(rank, world, port, out_dir, name="resnet18", damp=True, det=False, direct=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     # Fixed kernel choices (shape heuristic, one weight-gradient plan) in every process: ResNet-50 train-mode
     # gradients at random init are chaotic - 0.1 % fp32 weight noise alone drops some BN-bias gradient
-    # cosines to 0.26 - so per-process timed tuner picks (two ranks contending for one GPU time the
-    # candidates differently) made the comparison flaky (scripts/dbg_tune_random.py).
+    # cosines to 0.14-0.28 on the CPU fp32 path (scripts/cpu_weight_noise.py,
+    # profiles/r2_cpu_weight_noise_resnet50.txt) - so per-process timed tuner picks (two ranks contending
+    # for one GPU time the candidates differently) made the comparison flaky (scripts/dbg_tune_random.py).
     os.environ.update(IMGCLS_CONV_STAGES="0", IMGCLS_WGRAD_BLOCKS="512", IMGCLS_WGRAD_STAGES="2",
-                      IMGCLS_DIRECT_CONV="0")
+                      IMGCLS_DIRECT_CONV="1" if direct else "0")
     import torch.nn.functional as F
     from pytorch_imageclassification_distributed_amd.models import Classifier
     from pytorch_imageclassification_distributed_amd.ops import functional as Fx
@@ -36,6 +37,11 @@ def _worker(rank, world, port, out_dir, name="resnet18"):
                                                                       init_distributed)
     ctx = init_distributed(device="cuda", backend="gloo")
     dev = ctx.device
+    from pytorch_imageclassification_distributed_amd.ops import hip
+    if det:
+        hip.set_deterministic(True)
+    if direct:  # every eligible 3x3 conv (fwd and fused dgrad) on the 64 x 64 direct variant
+        hip.DIRECT_FORCE = 3
     torch.manual_seed(0)
     x = torch.randn(16, 3, 64, 64, device=dev).to(torch.bfloat16).float()
     y = torch.randint(0, 7, (16,), device=dev)
@@ -43,17 +49,17 @@ def _worker(rank, world, port, out_dir, name="resnet18"):
     def model():
         torch.manual_seed(1)
         m = Classifier(name, 7)
-        with torch.no_grad():  # damp the Bottleneck residual branches (the chaos above); grads stay non-zero
-            for n, p in m.named_parameters():
-                if n.endswith("bn3.weight"):
-                    p.mul_(0.1)
+        if damp:
+            with torch.no_grad():  # damp the Bottleneck residual branches (the chaos above); grads stay non-zero
+                for n, p in m.named_parameters():
+                    if n.endswith("bn3.weight"):
+                        p.mul_(0.1)
         return m.to(dev).to(memory_format=torch.channels_last)
 
     m = model()
     convert_sync_batchnorm(m)
     red = GradReducer(m, bucket_cap_mb=4, first_bucket_mb=1)
     xs, ys = x[rank * 8:(rank + 1) * 8], y[rank * 8:(rank + 1) * 8]
-    from pytorch_imageclassification_distributed_amd.ops import hip
     early0 = hip.SYNCBN_EARLY_COUNT[0]
     Fx.cross_entropy(m(xs), ys).backward()
     scale = red.finish()
@@ -70,8 +76,13 @@ def _worker(rank, world, port, out_dir, name="resnet18"):
     destroy()
 
 
-@pytest.mark.parametrize("name", ["resnet18", "resnet50"])
-def test_two_ranks_one_gpu_matches_full_batch(tmp_path, name):
+@pytest.mark.parametrize("name,damp,det,direct", [
+    ("resnet18", False, False, False),
+    ("resnet50", True, False, False),
+    ("resnet50", True, False, True),   # direct (halo-tile) 3x3 convs and their fused dgrad on the SyncBN path
+    ("resnet50", False, True, False),  # undamped, deterministic mode in both runs (no atomics-order noise)
+])
+def test_two_ranks_one_gpu_matches_full_batch(tmp_path, name, damp, det, direct):
     """ResNet-18 (BasicBlock) and ResNet-50 (Bottleneck: fused BN-backward links whose SyncBN
     all-reduce is launched early by the consuming conv, residual gradient slots)."""
-    mp.spawn(_worker, args=(2, _port(), str(tmp_path), name), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _port(), str(tmp_path), name, damp, det, direct), nprocs=2, join=True)

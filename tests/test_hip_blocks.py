@@ -155,6 +155,54 @@ def test_deterministic_mode(model_name):
     torch.testing.assert_close(o3, o1, rtol=0.05, atol=0.05 * o1.abs().max().item())
 
 
+@pytest.mark.parametrize("model_name", ["resnet50", "inceptionv3"])
+def test_wgrad_side_stream(model_name):
+    """Weight gradients on the side stream (arena slots) are bitwise the single-stream ones in
+    deterministic mode, over three steps with begin() / Adam in between: the side stream starts
+    behind the arena memset, its inputs outlive their autograd lifetime (record_stream), and the
+    compute stream joins it before anything reads a gradient."""
+    from pytorch_imageclassification_distributed_amd.engine.optim import FusedAdam
+    from pytorch_imageclassification_distributed_amd.models import Classifier
+    from pytorch_imageclassification_distributed_amd.ops import hip
+    from pytorch_imageclassification_distributed_amd.ops.grad_arena import GradArena
+
+    def run(side):
+        torch.manual_seed(0)
+        m = Classifier(model_name, 7).to(DEV).to(memory_format=torch.channels_last).train()
+        params = [p for p in m.parameters() if p.requires_grad]
+        arena = GradArena(params, list(reversed(range(len(params)))))
+        opt = FusedAdam(params, lr=1e-3)
+        hw = 96 if model_name == "resnet50" else 299
+        x = torch.randn(4, 3, hw, hw, device=DEV)
+        hip.WGRAD_STREAM = side
+        out = []
+        for _ in range(3):
+            opt.zero_grad(set_to_none=True)
+            arena.begin()
+            torch.manual_seed(1)
+            y = m(x)
+            y = sum(t.float().square().mean() for t in y) if isinstance(y, tuple) else y.float().square().mean()
+            y.backward()
+            out.append([p.grad.clone() for p in params])
+            opt.step()
+        return out, [p.detach().clone() for p in params]
+
+    keep = hip.WGRAD_STREAM
+    hip.set_deterministic(True)
+    try:
+        g_side, p_side = run(True)
+        assert hip._SIDE, "side stream never used"
+        g_one, p_one = run(False)
+    finally:
+        hip.set_deterministic(False)
+        hip.WGRAD_STREAM = keep
+    for step, (a_, b_) in enumerate(zip(g_side, g_one)):
+        for i, (a, b) in enumerate(zip(a_, b_)):
+            assert torch.equal(a, b), (step, i)
+    for a, b in zip(p_side, p_one):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("kind,expect", [("A", 3), ("B", 2), ("C", 6), ("D", 4), ("E", 3)])
 def test_inception_block_fusion(kind, expect):
     """Inception blocks: chain-internal convs fuse their producer's BN-backward reduce and InceptionE's

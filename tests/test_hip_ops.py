@@ -559,6 +559,30 @@ def test_pools(kind, hw):
     assert rel_err(xb.grad, xr.grad) < 2e-2
 
 
+@pytest.mark.parametrize("which", ["pools", "depthwise", "se", "stem_pool", "gap"])
+def test_div64_fallback_paths(which):
+    """The 64-bit index decode (taken above 2^31 work items, never at test sizes) forced on by the
+    set_force_div64 hook: the same numerics tests must pass on that branch."""
+    hip = _hip()
+    hip.set_force_div64(True)
+    try:
+        if which == "pools":
+            for kind in ("max311", "max320", "max321", "avg311", "avg530"):
+                for hw in (16, 17):
+                    test_pools(kind, hw)
+        elif which == "depthwise":
+            test_depthwise_bn_silu()
+        elif which == "se":
+            test_se_gate_and_misc()
+        elif which == "stem_pool":
+            test_conv_bn_act_pool((2, 3, 64, 64, (7, 2, 3), (3, 2, 1)))
+            test_conv_bn_act_pool((2, 32, 35, 64, (3, 1, 1), (3, 2, 0)))
+        else:
+            test_gap_head_ce()
+    finally:
+        hip.set_force_div64(False)
+
+
 def test_gap_head_ce():
     hip = _hip()
     from pytorch_imageclassification_distributed_amd.models import mlp_head
