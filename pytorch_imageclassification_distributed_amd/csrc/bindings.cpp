@@ -125,6 +125,9 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
   TORCH_CHECK(K == (int)dh.size() * CA, "conv_gemm: K != ntaps*CA");
   ConvParams p{};
   p.A = ptr<bf16_t>(A); p.B = ptr<bf16_t>(B); p.C = ptr<bf16_t>(C);
+  p.a_elems = A.numel(); p.b_elems = B.numel();
+  TORCH_CHECK(2LL * IH * IW * CA < (1LL << 31) && 2LL * B.numel() < (1LL << 31),
+              "conv_gemm: an input image or the weight matrix exceeds 2 GiB (32-bit buffer offsets)");
   p.stats = optr<float>(stats); p.bias = optr<float>(bias);
   p.M = M; p.Ncols = Ncols; p.K = K; p.CA = CA; p.GH = GH; p.GW = GW; p.IH = IH; p.IW = IW; p.sA = sA;
   p.ldb = ldb; p.OH = OH; p.OW = OW; p.so = so; p.oh0 = oh0; p.ow0 = ow0; p.ldc = ldc; p.c_off = c_off;

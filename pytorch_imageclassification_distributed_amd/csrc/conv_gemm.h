@@ -46,6 +46,7 @@ struct ConvParams {
   // a_sc [IH*IW*N pixels][CA/32], b_sc [Ncols][K/32].  Null = bf16 operands.
   const uint8_t* a_sc;
   const uint8_t* b_sc;
+  long long a_elems, b_elems;  // A / B extents (bounds of the buffer-resource loads)
   int tile_n;  // output-channel tile: 64 or 128; 0 = 64 iff Ncols <= 64 (heuristic / fp8 path)
   int cfg;     // index into the tuned configuration table (conv_cfg_info; MX-FP8: conv_fp8_cfg_info), -1 = stages/tile_n
   int tap_dh[CONV_MAX_TAPS];

@@ -357,6 +357,26 @@ struct GldsCfg {
   static constexpr int OCC = OCC_LDS < OCC_REG ? OCC_LDS : OCC_REG;
 };
 
+// Buffer-resource LDS-DMA (buffer_load_dwordx4 ... lds): 32-bit byte offsets against a per-block base,
+// and an out-of-range offset (OOB) lands zeros in LDS - the implicit-GEMM zero padding costs one select,
+// not a 64-bit pointer select against a zero page.
+constexpr unsigned OOB = 0x80000000u;  // >= every num_records used (all < 2^31)
+
+DEVI __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL),
+                                           0x00020000);
+}
+
+DEVI void blds16(__amdgpu_buffer_rsrc_t r, unsigned voff, char* lds_wave_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, 0, 0, 0);
+}
+
+// tap table entry: dh, dw (signed 8 bit) and the weight tap index, one dword
+DEVI int tap_pack(int dh, int dw, int tb) { return (dh & 0xff) | ((dw & 0xff) << 8) | (tb << 16); }
+DEVI int tap_dh(int pk) { return (pk << 24) >> 24; }
+DEVI int tap_dw(int pk) { return (pk << 16) >> 24; }
+DEVI int tap_tb(int pk) { return (int)((unsigned)pk >> 16); }
+
 template <int TM, int BN, int WM, int WN, int STAGES, bool TAP_UNIFORM>
 __global__ __launch_bounds__((GldsCfg<TM, BN, WM, WN, STAGES>::NTH), (GldsCfg<TM, BN, WM, WN, STAGES>::OCC))
 void conv_gemm_glds_kernel(const ConvParams p) {
@@ -371,11 +391,9 @@ void conv_gemm_glds_kernel(const ConvParams p) {
   constexpr int LPS = AL + BL;
   constexpr int MAIN = Cfg::MAIN;
   static_assert(AL >= 1 && BL >= 1 && AL * 8 * NW == TM && BL * 8 * NW == BN, "loader mapping");
-  static_assert(MAIN + 3 * CONV_MAX_TAPS * 4 <= 160 * 1024, "LDS budget");
-  __shared__ __attribute__((aligned(16))) char smem[MAIN + 3 * CONV_MAX_TAPS * 4];
-  int* s_dh = (int*)(smem + MAIN);
-  int* s_dw = s_dh + CONV_MAX_TAPS;
-  int* s_tb = s_dw + CONV_MAX_TAPS;
+  static_assert(MAIN + CONV_MAX_TAPS * 4 <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(16))) char smem[MAIN + CONV_MAX_TAPS * 4];
+  int* s_tap = (int*)(smem + MAIN);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform (M0 base)
@@ -384,39 +402,42 @@ void conv_gemm_glds_kernel(const ConvParams p) {
   const int lin = xcd_remap(blockIdx.x, gm * gn);
   const int bm = lin / gn, bn = lin - bm * gn;
   const int m0 = bm * TM, n0 = bn * BN;
-  if (tid < p.ntaps) {
-    s_dh[tid] = p.tap_dh[tid];
-    s_dw[tid] = p.tap_dw[tid];
-    s_tb[tid] = p.tap_b[tid];
-  }
+  if (tid < p.ntaps) s_tap[tid] = tap_pack(p.tap_dh[tid], p.tap_dw[tid], p.tap_b[tid]);
   // lane -> (row within an 8-row group, physical chunk); logical chunk per instruction
   const int lrow = lane >> 3, pch = lane & 7;
   const int ghw = p.GH * p.GW;
-  int a_base[AL], a_ih[AL], a_iw[AL], a_ch[AL];
+  // A offsets are 32-bit, relative to the first image this block touches (host: image bytes < 2^31)
+  const int img = p.IH * p.IW * p.CA;
+  const int n_img0 = m0 / ghw;
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.A + (long)n_img0 * img, 2 * (p.a_elems - (long)n_img0 * img));
+  const __amdgpu_buffer_rsrc_t rsB = make_rsrc(p.B, 2 * p.b_elems);
+  int a_pix[AL], a_ih[AL], a_iw[AL];
 #pragma unroll
   for (int i = 0; i < AL; ++i) {
     const int row = wid * (TM / NW) + i * 8 + lrow;
-    a_ch[i] = pch ^ ((row >> 1) & 7);
+    const int ch = pch ^ ((row >> 1) & 7);
     const int m = m0 + row;
     if (m < p.M) {
       const int n = m / ghw, r = m - n * ghw;
       const int gh = r / p.GW, gw = r - gh * p.GW;
-      a_base[i] = n * p.IH * p.IW * p.CA;
       a_ih[i] = gh * p.sA;
       a_iw[i] = gw * p.sA;
+      a_pix[i] = (n - n_img0) * img + (a_ih[i] * p.IW + a_iw[i]) * p.CA + (TAP_UNIFORM ? ch * 8 : 0);
     } else {
-      a_base[i] = 0;
+      a_pix[i] = 0;
       a_ih[i] = -(1 << 28);
       a_iw[i] = 0;
     }
   }
-  int b_off[BL], b_ch[BL];
+  // B row byte offsets (OOB for rows past Ncols: every k-step offset added stays out of range)
+  unsigned b_row[BL];
+  int b_ch[BL];
 #pragma unroll
   for (int i = 0; i < BL; ++i) {
     const int row = wid * (BN / NW) + i * 8 + lrow;
     b_ch[i] = pch ^ ((row >> 1) & 7);
     const int n = n0 + row;
-    b_off[i] = n < p.Ncols ? n * p.ldb : -1;
+    b_row[i] = n < p.Ncols ? 2u * (unsigned)(n * p.ldb + (TAP_UNIFORM ? b_ch[i] * 8 : 0)) : OOB;
   }
   // non-uniform k-steps (CA not a multiple of 64: the stem's 8 / 16 channels, EfficientNet's 24, 40,
   // 80, 112 ...): each lane's (tap, channel) of its chunk advanced incrementally per k-step - one
@@ -425,42 +446,48 @@ void conv_gemm_glds_kernel(const ConvParams p) {
   int a_tap[TAP_UNIFORM ? 1 : AL], a_ci[TAP_UNIFORM ? 1 : AL], b_tap[TAP_UNIFORM ? 1 : BL], b_ci[TAP_UNIFORM ? 1 : BL];
   if constexpr (!TAP_UNIFORM) {
 #pragma unroll
-    for (int i = 0; i < AL; ++i) { a_tap[i] = (a_ch[i] * 8) / p.CA; a_ci[i] = a_ch[i] * 8 - a_tap[i] * p.CA; }
+    for (int i = 0; i < AL; ++i) {
+      const int row = wid * (TM / NW) + i * 8 + lrow;
+      const int ch = pch ^ ((row >> 1) & 7);
+      a_tap[i] = (ch * 8) / p.CA;
+      a_ci[i] = ch * 8 - a_tap[i] * p.CA;
+    }
 #pragma unroll
     for (int i = 0; i < BL; ++i) { b_tap[i] = (b_ch[i] * 8) / p.CA; b_ci[i] = b_ch[i] * 8 - b_tap[i] * p.CA; }
   }
   __syncthreads();
 
-  // all addresses (incl. the LDS tap-table reads) are formed before the first LDS-DMA of
-  // the stage: a DMA into the same __shared__ array would otherwise force the compiler
-  // to re-read the tables behind an lgkmcnt wait between every two DMAs
-  auto issue = [&](int kt, int buf) {
+  // uniform k walk (TAP_UNIFORM): tap / channel offset of the next issue, its packed table entry read
+  // one issue ahead so the LDS latency hides behind a k-step of MFMAs
+  int u_tap = 0, u_ci = 0;
+  int u_pk = s_tap[0];
+  auto issue = [&](int buf) {
     char* sa = smem + buf * STAGE;
     char* sb = sa + A_BYTES;
-    const bf16_t* srca[AL];
-    const bf16_t* srcb[BL];
-    if (TAP_UNIFORM) {
-      const int k0 = kt * BK;
-      const int tap = k0 / p.CA, ci0 = k0 - tap * p.CA;
-      const int dh = s_dh[tap], dw = s_dw[tap], tb = s_tb[tap];
+    unsigned va[AL], vb[BL];
+    if constexpr (TAP_UNIFORM) {
+      const int pk = __builtin_amdgcn_readfirstlane(u_pk);
+      const int dh = tap_dh(pk), dw = tap_dw(pk);
+      const int a_t = (dh * p.IW + dw) * p.CA + u_ci;
+      const unsigned b_t = 2u * (unsigned)(tap_tb(pk) * p.CA + u_ci);
 #pragma unroll
       for (int i = 0; i < AL; ++i) {
-        const int ih = a_ih[i] + dh, iw = a_iw[i] + dw;
-        const bool ok = (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
-        srca[i] = ok ? p.A + a_base[i] + (ih * p.IW + iw) * p.CA + ci0 + a_ch[i] * 8 : p.zero;
+        const bool ok = (unsigned)(a_ih[i] + dh) < (unsigned)p.IH && (unsigned)(a_iw[i] + dw) < (unsigned)p.IW;
+        va[i] = ok ? 2u * (unsigned)(a_pix[i] + a_t) : OOB;
       }
 #pragma unroll
-      for (int i = 0; i < BL; ++i)
-        srcb[i] = b_off[i] >= 0 ? p.B + b_off[i] + tb * p.CA + ci0 + b_ch[i] * 8 : p.zero;
+      for (int i = 0; i < BL; ++i) vb[i] = b_row[i] + b_t;
+      u_ci += BK;
+      if (u_ci >= p.CA) { u_ci -= p.CA; ++u_tap; }
     } else {
       // called for kt = 0, 1, 2, ... in order: (tap, ci) of every chunk advance one k-step per call
 #pragma unroll
       for (int i = 0; i < AL; ++i) {
         const bool kin = a_tap[i] < p.ntaps;
-        const int tap = kin ? a_tap[i] : 0;
-        const int ih = a_ih[i] + s_dh[tap], iw = a_iw[i] + s_dw[tap];
+        const int pk = s_tap[kin ? a_tap[i] : 0];
+        const int ih = a_ih[i] + tap_dh(pk), iw = a_iw[i] + tap_dw(pk);
         const bool ok = kin && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
-        srca[i] = ok ? p.A + a_base[i] + (ih * p.IW + iw) * p.CA + a_ci[i] : p.zero;
+        va[i] = ok ? 2u * (unsigned)(a_pix[i] + (tap_dh(pk) * p.IW + tap_dw(pk)) * p.CA + a_ci[i]) : OOB;
         a_tap[i] += adv_q;
         a_ci[i] += adv_r;
         if (a_ci[i] >= p.CA) { a_ci[i] -= p.CA; ++a_tap[i]; }
@@ -468,16 +495,17 @@ void conv_gemm_glds_kernel(const ConvParams p) {
 #pragma unroll
       for (int i = 0; i < BL; ++i) {
         const bool kin = b_tap[i] < p.ntaps;
-        srcb[i] = (kin && b_off[i] >= 0) ? p.B + b_off[i] + s_tb[kin ? b_tap[i] : 0] * p.CA + b_ci[i] : p.zero;
+        vb[i] = kin ? b_row[i] + 2u * (unsigned)(tap_tb(s_tap[kin ? b_tap[i] : 0]) * p.CA + b_ci[i]) : OOB;
         b_tap[i] += adv_q;
         b_ci[i] += adv_r;
         if (b_ci[i] >= p.CA) { b_ci[i] -= p.CA; ++b_tap[i]; }
       }
     }
 #pragma unroll
-    for (int i = 0; i < AL; ++i) glds16(srca[i], sa + (wid * (TM / NW) + i * 8) * 128);
+    for (int i = 0; i < AL; ++i) blds16(rsA, va[i], sa + (wid * (TM / NW) + i * 8) * 128);
 #pragma unroll
-    for (int i = 0; i < BL; ++i) glds16(srcb[i], sb + (wid * (BN / NW) + i * 8) * 128);
+    for (int i = 0; i < BL; ++i) blds16(rsB, vb[i], sb + (wid * (BN / NW) + i * 8) * 128);
+    if constexpr (TAP_UNIFORM) u_pk = s_tap[u_tap < p.ntaps ? u_tap : 0];
   };
 
   f32x4 acc[RM][RN];
@@ -489,13 +517,16 @@ void conv_gemm_glds_kernel(const ConvParams p) {
   const int nk = (p.K + BK - 1) / BK;
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
-    if (s < nk) issue(s, s);
+    if (s < nk) issue(s);
   const int fr = lane & 15, fq = lane >> 4;
+  // MFMA order: the outer loop runs over the wider fragment dimension, so the first MFMAs of a k-half
+  // need only the narrow side plus one fragment of the wide side (counted lgkmcnt waits, not 0)
+  constexpr bool JOUT = RN >= RM;
   for (int kt = 0; kt < nk; ++kt) {
     if constexpr (STAGES == 1) {
       // no in-block overlap: latency is hidden by the co-resident blocks this LDS size allows
       if (kt > 0) __builtin_amdgcn_s_barrier();
-      issue(kt, 0);
+      issue(0);
       wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
     } else {
@@ -504,22 +535,49 @@ void conv_gemm_glds_kernel(const ConvParams p) {
       if (kt + STAGES - 2 < nk) wait_vmcnt<(STAGES - 2) * LPS>();
       else wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
-      if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
     }
     const char* sa = smem + (kt % STAGES) * STAGE;
     const char* sb = sa + A_BYTES;
+    bf16x8 af[RM], bfg[RN];
+#pragma unroll
+    for (int i = 0; i < RM; ++i) af[i] = *(const bf16x8*)(sa + swz(wm * WTM + i * 16 + fr, fq));
+#pragma unroll
+    for (int j = 0; j < RN; ++j) bfg[j] = *(const bf16x8*)(sb + swz(wn * WTN + j * 16 + fr, fq));
+    // the next tile's gather is issued while this k-step's first fragments are in flight
+    if constexpr (STAGES > 1)
+      if (kt + STAGES - 1 < nk) issue((kt + STAGES - 1) % STAGES);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[RM], bfg[RN];
+      bf16x8 af2[RM], bf2[RN];
+      if (kk == 0) {
 #pragma unroll
-      for (int i = 0; i < RM; ++i) af[i] = *(const bf16x8*)(sa + swz(wm * WTM + i * 16 + fr, kk * 4 + fq));
+        for (int i = 0; i < RM; ++i) af2[i] = *(const bf16x8*)(sa + swz(wm * WTM + i * 16 + fr, 4 + fq));
+      }
+      if constexpr (JOUT) {
 #pragma unroll
-      for (int j = 0; j < RN; ++j) bfg[j] = *(const bf16x8*)(sb + swz(wn * WTN + j * 16 + fr, kk * 4 + fq));
+        for (int j = 0; j < RN; ++j) {
 #pragma unroll
-      for (int i = 0; i < RM; ++i)
+          for (int i = 0; i < RM; ++i)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[j], af[i], acc[i][j], 0, 0, 0);
+          if (kk == 0) bf2[j] = *(const bf16x8*)(sb + swz(wn * WTN + j * 16 + fr, 4 + fq));
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < RM; ++i) {
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[j], af[i], acc[i][j], 0, 0, 0);
+        }
 #pragma unroll
         for (int j = 0; j < RN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[j], af[i], acc[i][j], 0, 0, 0);
+          if (kk == 0) bf2[j] = *(const bf16x8*)(sb + swz(wn * WTN + j * 16 + fr, 4 + fq));
+      }
+      if (kk == 0) {
+#pragma unroll
+        for (int i = 0; i < RM; ++i) af[i] = af2[i];
+#pragma unroll
+        for (int j = 0; j < RN; ++j) bfg[j] = bf2[j];
+      }
     }
   }
   __syncthreads();

@@ -84,5 +84,5 @@ print(f"batch {B}: {len(REC)} conv GEMM launches; roofline at {PEAK_TF:.0f} TF/s
 for k, (t, r) in tot.items():
     print(f"  {k:6s} {t / 1e3:7.3f} ms measured  {r / 1e3:7.3f} ms roofline")
 print(f"{'lost_us':>8} {'kind':6} {'us':>8} {'roof_us':>8} {'TF/s':>6} {'TB/s':>5}  shape")
-for lost, kind, desc, us, roof, tf, tb in sorted(rows, reverse=True)[:45]:
+for lost, kind, desc, us, roof, tf, tb in sorted(rows, reverse=True):
     print(f"{lost:8.1f} {kind:6} {us:8.1f} {roof:8.1f} {tf:6.0f} {tb:5.2f}  {desc}")
