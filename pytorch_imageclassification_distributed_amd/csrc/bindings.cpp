@@ -172,6 +172,9 @@ void conv_wgrad(Tensor dY, Tensor X, Tensor dW, int M, int Cout, int Cin, int Nt
   req(dY, BF, "dY"); req(X, BF, "X"); req(dW, F32, "dW");
   TORCH_CHECK(Cin % 8 == 0 && Cout % 8 == 0, "conv_wgrad: channels must be multiples of 8");
   TORCH_CHECK(k_per_split % 64 == 0, "conv_wgrad: k_per_split must be a multiple of 64");
+  TORCH_CHECK(2LL * k_per_split * Cout < (1LL << 31) - (1LL << 20) &&
+                  2LL * IH * IW * Cin * (k_per_split / (OH * OW) + 2) < (1LL << 31),
+              "conv_wgrad: a split's operands exceed 2 GiB (32-bit buffer offsets); use more splits");
   TORCH_CHECK(dY.numel() < (1LL << 31) - (1LL << 20) && X.numel() < (1LL << 31),
               "conv_wgrad: operands too large for 32-bit element offsets");
   WgradParams p{};

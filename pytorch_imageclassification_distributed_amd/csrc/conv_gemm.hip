@@ -1035,47 +1035,58 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
   // Address state advanced incrementally by one stage (KPS pixels) per issue - the gather's pixel ->
   // (image, row, column) decomposition is done once per block, not per k-step (it dominated the
   // kernel's VALU work: ~200 instructions per k-step per wave with per-step divisions and 64-bit math).
-  // All offsets are 32-bit element offsets (operands < 2^31 elements, checked on the host).
+  // Loads are buffer-resource LDS-DMAs with 32-bit byte offsets against per-block bases (the split's
+  // first dY row, the first image its pixels touch); an out-of-range offset lands zeros.
   const int adv_q = KPS / p.OW, adv_r = KPS - adv_q * p.OW;  // KPS pixels = adv_q rows + adv_r columns
-  int a_m[AL];
+  const int img = p.IH * p.IW;
+  const int n_lo = kbeg / ohw;
+  const float inv_oh = 1.f / (float)p.OH;
+  const __amdgpu_buffer_rsrc_t rsY = make_rsrc(p.dY + (long)kbeg * p.Cout, 2L * (kend - kbeg) * p.Cout);
+  const __amdgpu_buffer_rsrc_t rsX =
+      make_rsrc(p.X + (long)n_lo * img * p.Cin, 2L * ((long)(p.M / ohw) - n_lo) * img * p.Cin);
+  unsigned a_off[AL];  // rows past kend fall out of rsY's range by themselves
 #pragma unroll
-  for (int i = 0; i < AL; ++i) a_m[i] = kbeg + (wid * AL + i) * ARPI + a_lr;
+  for (int i = 0; i < AL; ++i)
+    a_off[i] = a_cok[i] ? 2u * (unsigned)(((wid * AL + i) * ARPI + a_lr) * p.Cout + a_col[i]) : OOB;
   int b_m[BL], b_n[BL], b_oh[BL], b_ow[BL];
 #pragma unroll
   for (int i = 0; i < BL; ++i) {
     b_m[i] = kbeg + (wid * BL + i) * BRPI + b_lr;
     int rem;
-    b_n[i] = fdiv(b_m[i], ohw, inv_ohw, rem);
+    b_n[i] = fdiv(b_m[i], ohw, inv_ohw, rem) - n_lo;
     b_oh[i] = fdiv(rem, p.OW, inv_ow, b_ow[i]);
   }
-  const int img = p.IH * p.IW;
 
   auto issue = [&](int buf) {
     char* sa = smem + buf * STAGE;
     char* sb = sa + A_BYTES;
-    const bf16_t* srca[AL];
-    const bf16_t* srcb[BL];
+    unsigned va[AL], vb[BL];
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
-      srca[i] = (a_cok[i] && a_m[i] < kend) ? p.dY + (a_m[i] * p.Cout + a_col[i]) : p.zero;
-      a_m[i] += KPS;
+      va[i] = a_off[i];
+      a_off[i] += (a_off[i] != OOB ? 2u * KPS * p.Cout : 0u);
     }
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
       const int ih = b_oh[i] * p.stride_h + b_dh[i], iw = b_ow[i] * p.stride_w + b_dw[i];
       const bool ok = b_cok[i] && b_m[i] < kend && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
-      srcb[i] = ok ? p.X + ((b_n[i] * img + ih * p.IW + iw) * p.Cin + b_ci[i]) : p.zero;
-      // advance by KPS pixels: adv_q output rows + adv_r columns, carrying into rows and images
+      vb[i] = ok ? 2u * (unsigned)(((b_n[i] * p.IH + ih) * p.IW + iw) * p.Cin + b_ci[i]) : OOB;
+      // advance by KPS pixels: adv_q output rows + adv_r columns, carrying into rows and images (the
+      // image carry by one float-reciprocal division, not a data-dependent loop)
       b_m[i] += KPS;
       b_ow[i] += adv_r;
       b_oh[i] += adv_q;
       if (b_ow[i] >= p.OW) { b_ow[i] -= p.OW; ++b_oh[i]; }
-      while (b_oh[i] >= p.OH) { b_oh[i] -= p.OH; ++b_n[i]; }
+      if (b_oh[i] >= p.OH) {
+        int r;
+        b_n[i] += fdiv(b_oh[i], p.OH, inv_oh, r);
+        b_oh[i] = r;
+      }
     }
 #pragma unroll
-    for (int i = 0; i < AL; ++i) glds16(srca[i], sa + (wid * AL + i) * 1024);
+    for (int i = 0; i < AL; ++i) blds16(rsY, va[i], sa + (wid * AL + i) * 1024);
 #pragma unroll
-    for (int i = 0; i < BL; ++i) glds16(srcb[i], sb + (wid * BL + i) * 1024);
+    for (int i = 0; i < BL; ++i) blds16(rsX, vb[i], sb + (wid * BL + i) * 1024);
   };
 
   f32x4 acc[RM][RN];
@@ -1089,6 +1100,25 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
   if (STAGES >= 2) issue(0);
   const int g = lane >> 4, li = lane & 15;
   const int tq = li >> 2, tp = li & 3;
+  // fragments of k-half kk: permuted k order (identical for A and B): elements 0-3 <- rows 4g+q,
+  // elements 4-7 <- rows 16+4g+q
+  auto frags = [&](const char* sa, const char* sb, int kk, bf16x8 (&af)[RM], bf16x8 (&bfg)[RN]) {
+    const int r0 = grp * WBK + kk * 32 + 4 * g + tq, r1 = r0 + 16;
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+      const int blk = (wm * WTM + i * 16) >> 4;
+      const bf16x4 lo = tr_read(sa + r0 * AROWB + ((blk ^ wswz<AROWB>(r0)) << 5) + tp * 8);
+      const bf16x4 hi = tr_read(sa + r1 * AROWB + ((blk ^ wswz<AROWB>(r1)) << 5) + tp * 8);
+      af[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      const int blk = (wn * WTN + j * 16) >> 4;
+      const bf16x4 lo = tr_read(sb + r0 * BROWB + ((blk ^ wswz<BROWB>(r0)) << 5) + tp * 8);
+      const bf16x4 hi = tr_read(sb + r1 * BROWB + ((blk ^ wswz<BROWB>(r1)) << 5) + tp * 8);
+      bfg[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+  };
   for (int kt = 0; kt < nk; ++kt) {
     if constexpr (STAGES == 1) {  // latency hidden by co-resident blocks instead of the ring
       if (kt > 0) __builtin_amdgcn_s_barrier();
@@ -1098,29 +1128,17 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
     } else {
       wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
-      if (kt + 1 < nk) issue((kt + 1) & 1);
     }
     const char* sa = smem + (STAGES == 1 ? 0 : (kt & 1) * STAGE);
     const char* sb = sa + A_BYTES;
+    bf16x8 af[RM], bfg[RN];
+    frags(sa, sb, 0, af, bfg);
+    // the next stage's gather is issued while the first fragments are in flight
+    if constexpr (STAGES >= 2)
+      if (kt + 1 < nk) issue((kt + 1) & 1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      // permuted k order (identical for A and B): elements 0-3 <- rows 4g+q, 4-7 <- rows 16+4g+q
-      const int r0 = grp * WBK + kk * 32 + 4 * g + tq, r1 = r0 + 16;
-      bf16x8 af[RM], bfg[RN];
-#pragma unroll
-      for (int i = 0; i < RM; ++i) {
-        const int blk = (wm * WTM + i * 16) >> 4;
-        const bf16x4 lo = tr_read(sa + r0 * AROWB + ((blk ^ wswz<AROWB>(r0)) << 5) + tp * 8);
-        const bf16x4 hi = tr_read(sa + r1 * AROWB + ((blk ^ wswz<AROWB>(r1)) << 5) + tp * 8);
-        af[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-      }
-#pragma unroll
-      for (int j = 0; j < RN; ++j) {
-        const int blk = (wn * WTN + j * 16) >> 4;
-        const bf16x4 lo = tr_read(sb + r0 * BROWB + ((blk ^ wswz<BROWB>(r0)) << 5) + tp * 8);
-        const bf16x4 hi = tr_read(sb + r1 * BROWB + ((blk ^ wswz<BROWB>(r1)) << 5) + tp * 8);
-        bfg[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-      }
+      if (kk == 1) frags(sa, sb, 1, af, bfg);
 #pragma unroll
       for (int i = 0; i < RM; ++i)
 #pragma unroll
