@@ -168,7 +168,7 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
 
 void conv_wgrad(Tensor dY, Tensor X, Tensor dW, int M, int Cout, int Cin, int Ntot, int OH, int OW, int IH, int IW,
                 int sh, int sw, int pt, int pl, int dh, int dwd, int KW, int k_per_split, int splits, Tensor zero,
-                int stages) {
+                int stages, OT ws) {
   req(dY, BF, "dY"); req(X, BF, "X"); req(dW, F32, "dW");
   TORCH_CHECK(Cin % 8 == 0 && Cout % 8 == 0, "conv_wgrad: channels must be multiples of 8");
   TORCH_CHECK(k_per_split % 64 == 0, "conv_wgrad: k_per_split must be a multiple of 64");
@@ -183,10 +183,17 @@ void conv_wgrad(Tensor dY, Tensor X, Tensor dW, int M, int Cout, int Cin, int Nt
   p.stride_h = sh; p.stride_w = sw; p.pad_t = pt; p.pad_l = pl; p.dil_h = dh; p.dil_w = dwd; p.KW = KW;
   p.k_per_split = k_per_split;
   p.zero = ptr<bf16_t>(zero);
-  TORCH_CHECK(stages >= 0 && stages <= 6, "conv_wgrad: stages must be 0..6");
-  TORCH_CHECK(stages < 5 || Cout <= 32, "conv_wgrad: stages 5 / 6 (32-row tile) need Cout <= 32");
-  TORCH_CHECK(stages != 4 || Cout >= 256, "conv_wgrad: the 256x256 tile needs Cout >= 256");
+  TORCH_CHECK(stages >= 0 && stages <= 9, "conv_wgrad: stages must be 0..9");
+  TORCH_CHECK((stages != 5 && stages != 6) || Cout <= 32, "conv_wgrad: stages 5 / 6 (32-row tile) need Cout <= 32");
+  TORCH_CHECK((stages != 4 && stages != 7 && stages != 9) || Cout >= 256, "conv_wgrad: the 256x256 tile needs Cout >= 256");
   p.stages = stages;
+  p.ws = nullptr;
+  if (ws.has_value() && ws->defined() && splits > 1) {
+    TORCH_CHECK(ws->scalar_type() == F32 && ws->is_cuda() && ws->numel() >= (long long)splits * Cout * Ntot &&
+                    dW.is_non_overlapping_and_dense() && dW.numel() == (long long)Cout * Ntot && Ntot % 8 == 0,
+                "conv_wgrad: workspace must be fp32 [>= splits*Cout*Ntot] with a contiguous dW");
+    p.ws = ws->data_ptr<float>();
+  }
   check(conv_wgrad_launch(p, splits, cur()), "conv_wgrad");
 }
 
@@ -578,7 +585,12 @@ void bn_set_reduce_blocks(int n, int chb);  // bn.hip: target blocks / channel l
 PYBIND11_MODULE(_C, m) {
   m.doc() = "gfx950 (MI355X) HIP kernels for pytorch_imageclassification_distributed_amd";
   m.def("conv_gemm", &conv_gemm);
-  m.def("conv_wgrad", &conv_wgrad);
+  m.def("conv_wgrad", &conv_wgrad, pybind11::arg("dY"), pybind11::arg("X"), pybind11::arg("dW"), pybind11::arg("M"),
+        pybind11::arg("Cout"), pybind11::arg("Cin"), pybind11::arg("Ntot"), pybind11::arg("OH"), pybind11::arg("OW"),
+        pybind11::arg("IH"), pybind11::arg("IW"), pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("pt"),
+        pybind11::arg("pl"), pybind11::arg("dh"), pybind11::arg("dwd"), pybind11::arg("KW"),
+        pybind11::arg("k_per_split"), pybind11::arg("splits"), pybind11::arg("zero"), pybind11::arg("stages"),
+        pybind11::arg("ws") = pybind11::none());
   m.def("conv_set_variant", &conv_set_variant);
   m.def("set_deterministic", [](bool v) { set_deterministic(v ? 1 : 0); });
   m.def("set_force_div64", [](bool v) { set_force_div64(v ? 1 : 0); });

@@ -64,6 +64,7 @@ struct WgradParams {
   int k_per_split;     // pixels (GEMM K) per split, multiple of 64
   const bf16_t* zero;  // >= 16 zero bytes (LDS-DMA source of padded chunks)
   int stages;          // 1 | 2: ring depth (4 waves); 3: 8 waves, in-block pixel split; 4: 256x256 tile, 8 waves
+  float* ws;           // optional [splits][Cout][Ntot] fp32 partial-tile workspace (plain stores + reduce), else atomics
 };
 
 int conv_gemm_launch(const ConvParams& p, hipStream_t stream);

@@ -940,9 +940,13 @@ DEVI int fdiv(int n, int d, float inv, int& rem) {
   return q;
 }
 
+// XOR mask on the 32-B block index of an image row: the 8 rows a 32-lane half of a transposed read
+// touches must land in 8 distinct 8-bank groups.  Rows of 256 B and 512 B all start on bank 0, so the
+// mask is the row's low 3 bits (row & 7); 128-B rows alternate bank halves (4 blocks per row), 64-B
+// rows cycle through 4 bank quarters (2 blocks per row).
 template <int ROWB>
-DEVI int wswz(int row) {  // XOR mask on the 32-B block index
-  return ROWB == 256 ? (row & 7) : ROWB == 128 ? ((row >> 1) & 3) : ((row >> 2) & 1);
+DEVI int wswz(int row) {
+  return ROWB >= 256 ? (row & 7) : ROWB == 128 ? ((row >> 1) & 3) : ((row >> 2) & 1);
 }
 
 // Tile WBM (output channels) x TN (tap*Cin columns), WM x WN waves per k-group; KG wave groups
@@ -950,11 +954,11 @@ DEVI int wswz(int row) {  // XOR mask on the 32-B block index
 // LDS before the atomics).  Split-K partial tiles leave through fp32 atomics (~1.3 TB/s chip-wide):
 // the atomic bytes of a launch are blocks x tile bytes, so the 256 x 256 tile at one block per CU
 // moves fewer of them than many small-tile blocks while running the more efficient 8-wave loop.
-template <int WBM, int TN, int WM, int WN, int KG, int STAGES>
+template <int WBM, int TN, int WM, int WN, int KG, int STAGES, int BKP = WBK>
 struct WgCfg {
   static constexpr int NW = WM * WN * KG, NTH = 64 * NW;
   static constexpr int AROWB = WBM * 2, BROWB = TN * 2;
-  static constexpr int STAGE = WBK * KG * (AROWB + BROWB);
+  static constexpr int STAGE = BKP * KG * (AROWB + BROWB);
   static constexpr int LDT = TN + 4;
   static constexpr int EPI = (KG == 2 ? WBM : WBM / WM) * LDT * 4;  // staged fp32 rows
   static constexpr int MAIN = STAGES * STAGE > EPI ? STAGES * STAGE : EPI;
@@ -964,15 +968,19 @@ struct WgCfg {
   static constexpr int OCC = ACC >= 128 ? (OCC0 < 2 ? OCC0 : 2) : OCC0;
 };
 
-template <int WBM, int TN, int WM, int WN, int KG, int STAGES>
-__global__ __launch_bounds__((WgCfg<WBM, TN, WM, WN, KG, STAGES>::NTH), (WgCfg<WBM, TN, WM, WN, KG, STAGES>::OCC))
+// BKP = pixels per k-group per stage: 64, or 32 for a deeper ring of smaller stages (a 4-deep ring of
+// 32-pixel stages keeps two stages in flight across each barrier at the LDS size of a 2-deep 64 ring).
+template <int WBM, int TN, int WM, int WN, int KG, int STAGES, int BKP = WBK>
+__global__ __launch_bounds__((WgCfg<WBM, TN, WM, WN, KG, STAGES, BKP>::NTH),
+                             (WgCfg<WBM, TN, WM, WN, KG, STAGES, BKP>::OCC))
 void conv_wgrad_glds_kernel(const WgradParams p) {
-  using Cfg = WgCfg<WBM, TN, WM, WN, KG, STAGES>;
+  using Cfg = WgCfg<WBM, TN, WM, WN, KG, STAGES, BKP>;
   constexpr int NW = Cfg::NW;
   constexpr int NTH = Cfg::NTH;
   constexpr int AROWB = Cfg::AROWB;         // A image row bytes (128 / 256 / 512)
   constexpr int BROWB = Cfg::BROWB;         // 256 / 512
-  constexpr int KPS = WBK * KG;             // pixels per stage
+  constexpr int KPS = BKP * KG;             // pixels per stage
+  constexpr int KH = BKP / 32;              // 32-deep MFMA k-halves per stage and k-group
   constexpr int A_BYTES = KPS * AROWB;
   constexpr int STAGE = Cfg::STAGE;
   constexpr int WTM = WBM / WM, WTN = TN / WN;
@@ -1097,13 +1105,15 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
 
   const int nk = (kend - kbeg + KPS - 1) / KPS;
   if (nk <= 0) return;
-  if (STAGES >= 2) issue(0);
+#pragma unroll
+  for (int s0 = 0; s0 < STAGES - 1; ++s0)
+    if (s0 < nk) issue(s0);
   const int g = lane >> 4, li = lane & 15;
   const int tq = li >> 2, tp = li & 3;
   // fragments of k-half kk: permuted k order (identical for A and B): elements 0-3 <- rows 4g+q,
   // elements 4-7 <- rows 16+4g+q
   auto frags = [&](const char* sa, const char* sb, int kk, bf16x8 (&af)[RM], bf16x8 (&bfg)[RN]) {
-    const int r0 = grp * WBK + kk * 32 + 4 * g + tq, r1 = r0 + 16;
+    const int r0 = grp * BKP + kk * 32 + 4 * g + tq, r1 = r0 + 16;
 #pragma unroll
     for (int i = 0; i < RM; ++i) {
       const int blk = (wm * WTM + i * 16) >> 4;
@@ -1126,19 +1136,22 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
       wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
     } else {
-      wait_vmcnt<0>();
+      // stage kt landed; the STAGES-2 younger stages stay in flight across the barrier, which also
+      // retires every wave's reads of the slot the next issue overwrites
+      if (kt + STAGES - 2 < nk) wait_vmcnt<(STAGES - 2) * (AL + BL)>();
+      else wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
     }
-    const char* sa = smem + (STAGES == 1 ? 0 : (kt & 1) * STAGE);
+    const char* sa = smem + (STAGES == 1 ? 0 : (kt % STAGES) * STAGE);
     const char* sb = sa + A_BYTES;
     bf16x8 af[RM], bfg[RN];
     frags(sa, sb, 0, af, bfg);
     // the next stage's gather is issued while the first fragments are in flight
     if constexpr (STAGES >= 2)
-      if (kt + 1 < nk) issue((kt + 1) & 1);
+      if (kt + STAGES - 1 < nk) issue((kt + STAGES - 1) % STAGES);
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      if (kk == 1) frags(sa, sb, 1, af, bfg);
+    for (int kk = 0; kk < KH; ++kk) {
+      if (kk > 0) frags(sa, sb, kk, af, bfg);
 #pragma unroll
       for (int i = 0; i < RM; ++i)
 #pragma unroll
@@ -1151,6 +1164,29 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
   // per lane -> one 16-B LDS write; the fp32 tile is staged through LDS and added to global memory
   // with atomics whose wave-instructions each cover 256 contiguous bytes.
   float* st = (float*)smem;
+  // ROWS staged rows [r0, r0+ROWS) of the tile leave either as fp32 atomics into dW (~1.3 TB/s chip-wide,
+  // memory-side), or - with a workspace - as plain 16-B stores into this split's slab of
+  // ws[splits][Cout][Ntot], summed by wgrad_reduce_kernel afterwards (4-5x the store bandwidth; the
+  // atomics of a one-wave grid otherwise form a serial tail after every block's main loop)
+  float* const slab = p.ws != nullptr ? p.ws + (long)split * p.Cout * p.Ntot : nullptr;
+  auto tile_out = [&](int r0, int ROWS) {
+    if (slab != nullptr) {
+#pragma unroll 4
+      for (int e = tid * 4; e < ROWS * TN; e += NTH * 4) {  // consecutive lanes -> consecutive 16 B
+        const int row = e / TN, c = e - row * TN;
+        const int co = co0 + r0 + row, col = j0 + c;
+        if (co < p.Cout && col < p.Ntot)
+          *(f32x4*)(slab + (long)co * p.Ntot + col) = *(const f32x4*)(st + row * LDT + c);
+      }
+    } else {
+#pragma unroll 4
+      for (int e = tid; e < ROWS * TN; e += NTH) {  // consecutive lanes -> consecutive floats
+        const int row = e / TN, c = e - row * TN;
+        const int co = co0 + r0 + row, col = j0 + c;
+        if (co < p.Cout && col < p.Ntot) atomicAdd(p.dW + (long)co * p.Ntot + col, st[row * LDT + c]);
+      }
+    }
+  };
   if constexpr (KG == 2) {
     // group 1 parks its partial tile, group 0 adds its own, then all threads issue the atomics
     __syncthreads();
@@ -1172,12 +1208,7 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
         }
     }
     __syncthreads();
-#pragma unroll 4
-    for (int e = tid; e < WBM * TN; e += NTH) {  // consecutive lanes -> consecutive floats
-      const int row = e / TN, c = e - row * TN;
-      const int co = co0 + row, col = j0 + c;
-      if (co < p.Cout && col < p.Ntot) atomicAdd(p.dW + (long)co * p.Ntot + col, st[row * LDT + c]);
-    }
+    tile_out(0, WBM);
   } else {
     // fp32 tile staged in WM parts of WTM rows
 #pragma unroll
@@ -1191,13 +1222,26 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
             *(f32x4*)(st + (i * 16 + fr) * LDT + wn * WTN + j * 16 + fq * 4) = acc[i][j];
       }
       __syncthreads();
-#pragma unroll 4
-      for (int e = tid; e < WTM * TN; e += NTH) {  // consecutive lanes -> consecutive floats
-        const int row = e / TN, c = e - row * TN;
-        const int co = co0 + part * WTM + row, col = j0 + c;
-        if (co < p.Cout && col < p.Ntot) atomicAdd(p.dW + (long)co * p.Ntot + col, st[row * LDT + c]);
-      }
+      tile_out(part * WTM, WTM);
     }
+  }
+}
+
+// dW += sum over splits of the workspace slabs ws[s][n] (16 B per lane, 8 slabs in flight)
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const f32x4* __restrict__ ws, f32x4* __restrict__ dW,
+                                                           long n4, int splits) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    f32x4 a = dW[i];
+    int s = 0;
+    for (; s + 8 <= splits; s += 8) {
+      f32x4 v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = ws[(long)(s + k) * n4 + i];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a += v[k];
+    }
+    for (; s < splits; ++s) a += ws[(long)s * n4 + i];
+    dW[i] = a;
   }
 }
 
@@ -1308,21 +1352,31 @@ int conv_gemm_launch(const ConvParams& p, hipStream_t stream) {
 static int g_wvariant = 0;
 void conv_set_wgrad_variant(int v) { g_wvariant = v; }
 
-template <int WBM, int TN, int WM, int WN, int KG, int ST>
+template <int WBM, int TN, int WM, int WN, int KG, int ST, int BKP = WBK>
 static void launch_wg(const WgradParams& p, int splits, hipStream_t stream) {
   const dim3 grid(cdiv(p.Cout, WBM) * cdiv(p.Ntot, TN), splits);
-  hipLaunchKernelGGL((conv_wgrad_glds_kernel<WBM, TN, WM, WN, KG, ST>), grid, dim3(64 * WM * WN * KG), 0, stream, p);
+  hipLaunchKernelGGL((conv_wgrad_glds_kernel<WBM, TN, WM, WN, KG, ST, BKP>), grid, dim3(64 * WM * WN * KG), 0,
+                     stream, p);
 }
 
-int conv_wgrad_tile_n(int stages) { return stages == 4 ? 256 : WBN; }
+int conv_wgrad_tile_n(int stages) { return (stages == 4 || stages == 7 || stages == 9) ? 256 : WBN; }
 
-int conv_wgrad_launch(const WgradParams& p, int splits, hipStream_t stream) {
-  if (p.M <= 0) return 0;
+int conv_wgrad_launch(const WgradParams& p_in, int splits, hipStream_t stream) {
+  if (p_in.M <= 0) return 0;
   const bool dma = g_wvariant != 1;
+  WgradParams p = p_in;
+  if (!dma || splits <= 1) p.ws = nullptr;  // the register-staged kernel always adds atomically
   // stages: 1 | 2 (4 waves, 64/128 x 128 tile), 3 = 2-stage ring with the in-block 2-way pixel split
   // (8 waves), 4 = 256 x 256 tile on 8 waves (2-stage ring, one block per CU; Cout >= 256 only),
   // 5 / 6 = 32 x 128 tile with a 1 / 2-stage ring (Cout <= 32 only)
-  if (dma && p.stages == 4) {
+  if (dma && (p.stages == 7 || p.stages == 9)) {  // 256 x 256, 8 waves, 4- / 3-deep ring of 32-pixel stages
+    if (p.Cout < 256) return 2;
+    if (p.stages == 7) launch_wg<256, 256, 2, 4, 1, 4, 32>(p, splits, stream);
+    else launch_wg<256, 256, 2, 4, 1, 3, 32>(p, splits, stream);
+  } else if (dma && p.stages == 8) {  // 64 / 128 x 128, 4 waves, 4-deep ring of 32-pixel stages
+    if (p.Cout <= 64) launch_wg<64, 128, 2, 2, 1, 4, 32>(p, splits, stream);
+    else launch_wg<128, 128, 2, 2, 1, 4, 32>(p, splits, stream);
+  } else if (dma && p.stages == 4) {
     if (p.Cout < 256) return 2;
     launch_wg<256, 256, 2, 4, 1, 2>(p, splits, stream);
   } else if (dma && (p.stages == 5 || p.stages == 6)) {  // 32-row tile (Cout <= 32: no empty half tile)
@@ -1343,5 +1397,12 @@ int conv_wgrad_launch(const WgradParams& p, int splits, hipStream_t stream) {
                             0, stream, p);
   }
   HIP_CHECK_LAUNCH();
+  if (p.ws != nullptr) {
+    const long n4 = (long)p.Cout * p.Ntot / 4;
+    const long blocks = (n4 + 255) / 256;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, stream,
+                       (const f32x4*)p.ws, (f32x4*)p.dW, n4, splits);
+    HIP_CHECK_LAUNCH();
+  }
   return 0;
 }

@@ -413,7 +413,7 @@ def load_tuning(path: str) -> int:
             k, v = ast.literal_eval(ks), tuple(int(x) for x in v)
         except (ValueError, SyntaxError, TypeError):
             continue
-        if len(v) == 2 and 1 <= v[1] <= 6 and v[0] > 0 and k not in _WGRAD_TUNED:
+        if len(v) == 2 and 1 <= v[1] <= 9 and v[0] > 0 and k not in _WGRAD_TUNED:
             _WGRAD_TUNED[k] = v
             n += 1
     return n
@@ -641,15 +641,30 @@ def _wgrad_split(m, tiles, target):
 WGRAD_STAGES = int(os.environ.get("IMGCLS_WGRAD_STAGES", "0"))  # 0 = tuned with the split count; 1 | 2 | 3
 
 
+WGRAD_WS = os.environ.get("IMGCLS_WGRAD_WS", "1") == "1"  # split-K partials: workspace slabs + reduce (0: atomics)
+_WGRAD_WS: dict = {}  # (device index, stream id) -> fp32 workspace, grown on demand
+
+
+def _wgrad_ws(dev, n):
+    """Split-K workspace of at least ``n`` floats for launches on the current stream (one per stream:
+    launches on one stream run in order, so consecutive layers share it)."""
+    key = (dev.index, torch.cuda.current_stream(dev).stream_id)
+    buf = _WGRAD_WS.get(key)
+    if buf is None or buf.numel() < n:
+        buf = _WGRAD_WS[key] = torch.empty(max(n, 1 << 20), dtype=torch.float32, device=dev)
+    return buf
+
+
 def _wgrad_launch(dy, x, out, g: ConvGeom, m, ntot, kps, splits, stages=2):
+    wsp = _wgrad_ws(dy.device, splits * g.Co * ntot) if (WGRAD_WS and splits > 1 and ntot % 8 == 0) else None
     C.conv_wgrad(dy, x, out, m, g.Co, g.Cx, ntot, g.OH, g.OW, g.H, g.W, g.sh, g.sw, g.pt, g.pl,
-                 g.dil, g.dil, g.kw, kps, splits, ws(dy.device).zero, stages)
+                 g.dil, g.dil, g.kw, kps, splits, ws(dy.device).zero, stages, wsp)
 
 
 def _wgrad_tiles(co, ntot, stages):
-    """Output tiles of one wgrad launch: 256 x 256 for the 8-wave kernel (stages 4), 32 x 128 for stages
-    5 / 6, else 64|128 x 128."""
-    if stages == 4:
+    """Output tiles of one wgrad launch: 256 x 256 for the 8-wave kernels (stages 4, 7, 9), 32 x 128 for
+    stages 5 / 6, else 64|128 x 128."""
+    if stages in (4, 7, 9):
         return (-(-co // 256)) * (-(-ntot // 256))
     return (-(-co // (32 if stages in (5, 6) else 64 if co <= 64 else 128))) * (-(-ntot // 128))
 
@@ -686,7 +701,9 @@ def _wgrad_config(dy, x, g: ConvGeom, m, ntot):
         # 8-wave blocks (in-block 2-way pixel split, one block per CU): fewer, larger blocks
         cands += [(cand, 3) for cand in blocks if cand <= 1024]
         if g.Co >= 256 and ntot >= 256:  # 256 x 256 tiles on 8 waves, ~1-2 blocks per CU
-            cands += [(cand, 4) for cand in (256, 512)]
+            cands += [(cand, st) for st in (4, 7, 9) for cand in (256, 512)]
+        # 4-deep ring of 32-pixel stages (two stages in flight across every barrier), 4 waves
+        cands += [(cand, 8) for cand in blocks if cand <= 1024]
         if g.Co <= 32:  # 32-row tiles: a 64-row tile would be half empty
             cands += [(cand, st) for st in (5, 6) for cand in blocks]
     for cand, st in cands:
