@@ -189,6 +189,202 @@ DEVI void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Specialised epilogues.  The generic conv_epilogue above tests every optional feature per row (bias,
+// addend, fused BN-backward with residual / activation, statistics, pixel remap), which the compiler
+// turns into ~380 basic blocks: the loads of consecutive rows then sit in different blocks and leave
+// one at a time.  The common feature sets get a branch-free body instead (mode bits below, selected
+// once per block): U rows' loads are issued together (out-of-range rows read row 0 and are masked at
+// the store), coefficients arrive as 16-B vectors.
+// ---------------------------------------------------------------------------
+enum : int { EP_STATS = 1, EP_ADD = 2, EP_BWD = 4, EP_RES = 8, EP_DIRECT = 16, EP_RELU = 32, EP_GENERIC = -1 };
+
+DEVI int epi_mode(const ConvParams& p) {
+  if (p.bias != nullptr) return EP_GENERIC;
+  const bool direct = (p.so == 1 && p.oh0 == 0 && p.ow0 == 0 && p.GH == p.OH && p.GW == p.OW);
+  int m = direct ? EP_DIRECT : 0;
+  if (p.stats != nullptr) {
+    if (p.addend != nullptr || p.bwd_y != nullptr) return EP_GENERIC;
+    return m | EP_STATS;
+  }
+  if (p.addend != nullptr) m |= EP_ADD;
+  if (p.bwd_y != nullptr) {
+    if (p.bwd_act != ACT_RELU) return EP_GENERIC;
+    m |= EP_BWD | EP_RELU | (p.bwd_res != nullptr ? EP_RES : 0);
+  }
+  return m;
+}
+
+template <int TM, int BN, int WM, int WN, int MODE, int UR>
+DEVI void conv_epi(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16], char* smem, int tid,
+                   int lane, int wid, int wm, int wn, int m0, int n0, int bm) {
+  constexpr bool STATS = MODE & EP_STATS, ADD = MODE & EP_ADD, BWD = MODE & EP_BWD, RES = MODE & EP_RES;
+  constexpr bool DIRECT = MODE & EP_DIRECT, RELU = MODE & EP_RELU;
+  constexpr int NTH = 64 * WM * WN;
+  constexpr int WTM = TM / WM, WTN = BN / WN;
+  constexpr int RM = WTM / 16, RN = WTN / 16;
+  constexpr int CST = BN + 8;
+  const int fr = lane & 15, fq = lane >> 4;
+  bf16_t* ct = (bf16_t*)smem;
+#pragma unroll
+  for (int i = 0; i < RM; ++i) {
+    const int row = wm * WTM + i * 16 + fr;
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      const int col = wn * WTN + j * 16 + fq * 4;
+      uint2 pk;
+      pk.x = pack2(acc[i][j][0], acc[i][j][1]);
+      pk.y = pack2(acc[i][j][2], acc[i][j][3]);
+      *(uint2*)(ct + row * CST + col) = pk;
+    }
+  }
+  constexpr int CPR = BN / 8;        // 16-B chunks per row
+  constexpr int RPP = NTH / CPR;     // rows per pass
+  constexpr int IT = TM / RPP;       // rows per thread
+  constexpr int U = IT < UR ? IT : UR;  // rows whose loads are in flight together (register budget)
+  static_assert(CPR <= 64 && NTH % CPR == 0 && IT % U == 0, "epilogue row mapping");
+  const int sch = tid % CPR, srow = tid / CPR;
+  const int col = n0 + sch * 8;
+  const bool col_ok = col < p.Ncols;
+  const int col_l = col_ok ? col : 0;
+  float s8[8], q8[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { s8[k] = 0.f; q8[k] = 0.f; }
+  __syncthreads();
+  float bsc[8], bsh[8], bmu[8], bis[8];
+  if constexpr (BWD) {
+    const int C = p.Ncols;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x4 a = *(const f32x4*)(p.bwd_coef + col_l + 4 * h);
+      const f32x4 b = *(const f32x4*)(p.bwd_coef + C + col_l + 4 * h);
+      const f32x4 c = *(const f32x4*)(p.bwd_coef + 2 * C + col_l + 4 * h);
+      const f32x4 d = *(const f32x4*)(p.bwd_coef + 3 * C + col_l + 4 * h);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { bsc[4 * h + k] = a[k]; bsh[4 * h + k] = b[k]; bmu[4 * h + k] = c[k]; bis[4 * h + k] = d[k]; }
+    }
+  }
+  const int ghw = p.GH * p.GW;
+#pragma unroll 1
+  for (int it0 = 0; it0 < IT; it0 += U) {  // not unrolled: the scheduler would hoist every row's loads
+    uint4 v[U], ad[U], yv[U], rv[U];
+    long pix[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int row = srow + (it0 + u) * RPP;
+      const int m = m0 + row;
+      ok[u] = col_ok && m < p.M;
+      const int ml = ok[u] ? m : 0;
+      if constexpr (DIRECT) {
+        pix[u] = ml;
+      } else {
+        const int n = ml / ghw, r = ml - n * ghw;
+        const int gh = r / p.GW, gw = r - gh * p.GW;
+        pix[u] = ((long)n * p.OH + gh * p.so + p.oh0) * p.OW + gw * p.so + p.ow0;
+      }
+      v[u] = *(const uint4*)(ct + row * CST + sch * 8);
+      if constexpr (ADD) ad[u] = *(const uint4*)(p.addend + pix[u] * p.ldc + p.c_off + col_l);
+      if constexpr (BWD) yv[u] = *(const uint4*)(p.bwd_y + pix[u] * p.ldc + col_l);
+      if constexpr (RES) rv[u] = *(const uint4*)(p.bwd_res + pix[u] * p.ldc + col_l);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float f[8];
+      unpack8(v[u], f);
+      if constexpr (ADD) {
+        float a[8];
+        unpack8(ad[u], a);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) f[k] += a[k];
+        v[u] = pack8(f);
+        unpack8(v[u], f);  // the sum is rounded to bf16 before the BN-backward math, as in the generic path
+      }
+      if constexpr (BWD) {
+        float yf[8], rf[8];
+        unpack8(yv[u], yf);
+        if constexpr (RES) unpack8(rv[u], rf);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float dz = f[k];
+          if constexpr (RELU) {
+            float z = yf[k] * bsc[k] + bsh[k];
+            if constexpr (RES) z += rf[k];
+            dz = z > 0.f ? dz : 0.f;
+          }
+          f[k] = dz;
+          if (ok[u]) {
+            s8[k] += dz;
+            q8[k] += dz * (yf[k] - bmu[k]) * bis[k];
+          }
+        }
+        v[u] = pack8(f);
+      }
+      if (ok[u]) *(uint4*)(p.C + pix[u] * p.ldc + p.c_off + col) = v[u];
+      if constexpr (STATS) {
+        if (ok[u]) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) { s8[k] += f[k]; q8[k] += f[k] * f[k]; }
+        }
+      }
+    }
+  }
+  if constexpr (STATS || BWD) {
+    float* const stat_dst = STATS ? p.stats : p.bwd_part;
+    const int stat_groups = STATS ? p.stats_groups : p.bwd_groups;
+#pragma unroll
+    for (int o = CPR; o < 64; o <<= 1) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s8[k] += __shfl_xor(s8[k], o, 64);
+        q8[k] += __shfl_xor(q8[k], o, 64);
+      }
+    }
+    __syncthreads();  // tile reads done; reuse LDS for the cross-wave reduction
+    float* red = (float*)smem;  // [waves][2][BN]
+    if (lane < CPR) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        red[(wid * 2 + 0) * BN + sch * 8 + k] = s8[k];
+        red[(wid * 2 + 1) * BN + sch * 8 + k] = q8[k];
+      }
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < p.Ncols) {
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM * WN; ++w) {
+        s += red[(w * 2 + 0) * BN + tid];
+        q += red[(w * 2 + 1) * BN + tid];
+      }
+      float* dst = stat_dst + (size_t)(bm % stat_groups) * 2 * p.Ncols + n0 + tid;
+      atomicAdd(dst, s);
+      atomicAdd(dst + p.Ncols, q);
+    }
+  }
+}
+
+// UR: rows of operands in flight per thread - 2 where the launch bound leaves >= 200 VGPRs, else 1 (two
+// rows of four 16-B operands plus the BN-backward coefficients cost ~150 VGPRs)
+template <int TM, int BN, int WM, int WN, int UR>
+DEVI void conv_epilogue_dispatch(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16], char* smem, int tid,
+                                 int lane, int wid, int wm, int wn, int m0, int n0, int bm, int ghw) {
+#define EPI_CASE(M_) case (M_): conv_epi<TM, BN, WM, WN, (M_), UR>(p, acc, smem, tid, lane, wid, wm, wn, m0, n0, bm); break;
+  switch (epi_mode(p)) {
+    EPI_CASE(EP_STATS | EP_DIRECT)
+    EPI_CASE(EP_STATS)
+    EPI_CASE(EP_DIRECT)
+    EPI_CASE(0)
+    EPI_CASE(EP_ADD | EP_DIRECT)
+    EPI_CASE(EP_BWD | EP_RELU | EP_DIRECT)
+    EPI_CASE(EP_BWD | EP_RELU | EP_RES | EP_DIRECT)
+    EPI_CASE(EP_BWD | EP_RELU | EP_ADD | EP_DIRECT)
+    EPI_CASE(EP_BWD | EP_RELU | EP_RES | EP_ADD | EP_DIRECT)
+    default: conv_epilogue<TM, BN, WM, WN>(p, acc, smem, tid, lane, wid, wm, wn, m0, n0, bm, ghw);
+  }
+#undef EPI_CASE
+}
+
 template <int BN>
 __global__ __launch_bounds__(NT, 2) void conv_gemm_kernel(const ConvParams p) {
   constexpr int A_BYTES = BM * BK * 2;
@@ -581,7 +777,7 @@ void conv_gemm_glds_kernel(const ConvParams p) {
     }
   }
   __syncthreads();
-  conv_epilogue<TM, BN, WM, WN>(p, acc, smem, tid, lane, wid, wm, wn, m0, n0, bm, ghw);
+  conv_epilogue_dispatch<TM, BN, WM, WN, (512 / Cfg::OCC >= 200 ? 2 : 1)>(p, acc, smem, tid, lane, wid, wm, wn, m0, n0, bm, ghw);
 }
 
 // ---------------------------------------------------------------------------
