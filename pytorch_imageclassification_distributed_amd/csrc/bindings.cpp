@@ -126,6 +126,8 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
   ConvParams p{};
   p.A = ptr<bf16_t>(A); p.B = ptr<bf16_t>(B); p.C = ptr<bf16_t>(C);
   p.a_elems = A.numel(); p.b_elems = B.numel();
+  p.fd_ghw = make_fastdiv((uint32_t)(GH * GW)); p.fd_gw = make_fastdiv((uint32_t)GW);
+  TORCH_CHECK((long long)M < (1LL << 31), "conv_gemm: M must fit 32 bits");
   TORCH_CHECK(2LL * IH * IW * CA < (1LL << 31) && 2LL * B.numel() < (1LL << 31),
               "conv_gemm: an input image or the weight matrix exceeds 2 GiB (32-bit buffer offsets)");
   p.stats = optr<float>(stats); p.bias = optr<float>(bias);

@@ -47,6 +47,7 @@ struct ConvParams {
   const uint8_t* a_sc;
   const uint8_t* b_sc;
   long long a_elems, b_elems;  // A / B extents (bounds of the buffer-resource loads)
+  FastDiv fd_ghw, fd_gw;       // multiply-shift division by GH*GW and GW (epilogue pixel remap)
   int tile_n;  // output-channel tile: 64 or 128; 0 = 64 iff Ncols <= 64 (heuristic / fp8 path)
   int cfg;     // index into the tuned configuration table (conv_cfg_info; MX-FP8: conv_fp8_cfg_info), -1 = stages/tile_n
   int tap_dh[CONV_MAX_TAPS];

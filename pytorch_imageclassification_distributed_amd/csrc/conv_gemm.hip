@@ -279,8 +279,8 @@ DEVI void conv_epi(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16]
       if constexpr (DIRECT) {
         pix[u] = ml;
       } else {
-        const int n = ml / ghw, r = ml - n * ghw;
-        const int gh = r / p.GW, gw = r - gh * p.GW;
+        const int n = (int)fdiv((uint32_t)ml, p.fd_ghw), r = ml - n * ghw;
+        const int gh = (int)fdiv((uint32_t)r, p.fd_gw), gw = r - gh * p.GW;
         pix[u] = ((long)n * p.OH + gh * p.so + p.oh0) * p.OW + gw * p.so + p.ow0;
       }
       v[u] = *(const uint4*)(ct + row * CST + sch * 8);
@@ -380,6 +380,12 @@ DEVI void conv_epilogue_dispatch(const ConvParams& p, f32x4 (&acc)[TM / WM / 16]
     EPI_CASE(EP_BWD | EP_RELU | EP_RES | EP_DIRECT)
     EPI_CASE(EP_BWD | EP_RELU | EP_ADD | EP_DIRECT)
     EPI_CASE(EP_BWD | EP_RELU | EP_RES | EP_ADD | EP_DIRECT)
+    // stride-2 data gradients (sub-pixel phases, remapped pixels)
+    EPI_CASE(EP_ADD)
+    EPI_CASE(EP_BWD | EP_RELU)
+    EPI_CASE(EP_BWD | EP_RELU | EP_RES)
+    EPI_CASE(EP_BWD | EP_RELU | EP_ADD)
+    EPI_CASE(EP_BWD | EP_RELU | EP_RES | EP_ADD)
     default: conv_epilogue<TM, BN, WM, WN>(p, acc, smem, tid, lane, wid, wm, wn, m0, n0, bm, ghw);
   }
 #undef EPI_CASE
