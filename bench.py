@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--compute", default="hip", choices=["hip", "torch"])
     p.add_argument("--sync-bn", default="auto", choices=["auto", "on", "off"])
     p.add_argument("--bucket-mb", type=float, default=32.0)
+    p.add_argument("--syncbn-comm", default="auto", choices=["auto", "peer", "rccl"],
+                   help="SyncBN statistics transport (parallel/peer.py): one-shot xGMI peer kernel or RCCL")
     p.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--dist-backend", default="auto", help="auto (RCCL) | gloo (functional multi-rank runs on one GPU)")
     p.add_argument("--profile-steps", type=int, default=0)
@@ -82,7 +84,7 @@ def main():
         "--batchsize", str(a.batch), "--num-classes", str(a.num_classes),
         "--num-workers", "0", "--synthetic-train-size", "8", "--synthetic-val-size", "8",
         "--compute", a.compute, "--bucket-mb", str(a.bucket_mb), "--comm-dtype", a.comm_dtype,
-        "--lr", "1e-4", "--dtype", a.dtype,
+        "--lr", "1e-4", "--dtype", a.dtype, "--syncbn-comm", a.syncbn_comm,
     ] + ([] if sync_bn else ["--no-sync-bn"]))
     tr = Trainer(targs, ctx)
     tr.net.train()
@@ -143,7 +145,8 @@ def main():
             "config": {"model": a.model, "global_batch": a.batch * ctx.world_size,
                        "per_gpu_batch": a.batch, "seq_len": None, "image_size": a.image_size,
                        "num_classes": a.num_classes, "parallelism": f"dp{ctx.world_size}",
-                       "sync_bn": sync_bn, "compute": a.compute, "optimizer": "adam",
+                       "sync_bn": sync_bn, "syncbn_comm": ("peer" if tr.syncbn_peer else "rccl") if sync_bn else None,
+                       "compute": a.compute, "optimizer": "adam",
                        "final_loss": round(loss_val, 5)},
         }), flush=True)
     destroy()

@@ -85,6 +85,16 @@ int se_dx_launch(const bf16_t*, const float*, const float*, bf16_t*, int, int, i
 int act32_fwd_launch(const float*, float*, long, int, hipStream_t);
 int act32_bwd_launch(const float*, const float*, float*, long, int, hipStream_t);
 int bn_stats_launch(const bf16_t*, long, int, float*, int, hipStream_t);
+size_t peer_buffer_bytes();
+int peer_max_world();
+int peer_max_elems();
+int peer_alloc(void**);
+int peer_free(void*);
+int peer_ipc_handle(void*, char*);
+int peer_ipc_open(const char*, void**);
+int peer_ipc_close(void*);
+int peer_allreduce_f64_launch(const double*, double*, int, const unsigned long long*, int, int, unsigned long long,
+                              unsigned long long, int*, hipStream_t);
 
 namespace {
 
@@ -579,6 +589,82 @@ void bn_stats(Tensor y, long rows, int C, Tensor part, int G) {
   check(bn_stats_launch(ptr<bf16_t>(y), rows, C, ptr<float>(part), G, cur()), "bn_stats");
 }
 
+// One rank's end of the one-shot peer all-reduce (peer.hip): its IPC-exported buffer, the peers'
+// buffers mapped into this process, the call sequence number and the device error word.  The
+// handshake (exchanging handles over the process group) lives in parallel/peer.py.
+class PeerComm {
+ public:
+  PeerComm(int rank, int world, double timeout_s) : rank_(rank), world_(world) {
+    TORCH_CHECK(world >= 1 && world <= peer_max_world() && rank >= 0 && rank < world, "PeerComm: bad rank/world");
+    check(peer_alloc(&buf_), "peer_alloc");
+    check((int)hipMalloc((void**)&err_, sizeof(int)), "peer err word");
+    check((int)hipMemset(err_, 0, sizeof(int)), "peer err word");
+    int khz = 0;
+    int dev = 0;
+    check((int)hipGetDevice(&dev), "hipGetDevice");
+    check((int)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev), "wall clock rate");
+    timeout_ticks_ = (unsigned long long)(timeout_s * (double)khz * 1000.0);
+    bases_.assign(world, 0ull);
+    mapped_.assign(world, nullptr);
+    bases_[rank] = (unsigned long long)buf_;
+  }
+  ~PeerComm() { close(); }
+
+  pybind11::bytes handle() {
+    char h[64];
+    check(peer_ipc_handle(buf_, h), "hipIpcGetMemHandle");
+    return pybind11::bytes(h, 64);
+  }
+
+  void open(const std::vector<std::string>& handles) {
+    TORCH_CHECK((int)handles.size() == world_, "PeerComm.open: need one handle per rank");
+    for (int q = 0; q < world_; ++q) {
+      if (q == rank_) continue;
+      TORCH_CHECK(handles[q].size() == 64, "PeerComm.open: bad handle size");
+      void* p = nullptr;
+      check(peer_ipc_open(handles[q].data(), &p), "hipIpcOpenMemHandle");
+      mapped_[q] = p;
+      bases_[q] = (unsigned long long)p;
+    }
+  }
+
+  void all_reduce_(Tensor in, Tensor out) {
+    req(in, at::kDouble, "in");
+    req(out, at::kDouble, "out");
+    TORCH_CHECK(in.is_contiguous() && out.is_contiguous() && in.numel() == out.numel(), "PeerComm: contiguous, equal sizes");
+    TORCH_CHECK(in.numel() <= peer_max_elems(), "PeerComm: at most ", peer_max_elems(), " elements per call");
+    for (int q = 0; q < world_; ++q) TORCH_CHECK(bases_[q] != 0ull, "PeerComm: peers not opened");
+    ++seq_;
+    check(peer_allreduce_f64_launch(ptr<double>(in), ptr<double>(out), (int)in.numel(), bases_.data(), rank_, world_,
+                                    seq_, timeout_ticks_, err_, cur()),
+          "peer_allreduce_f64");
+  }
+
+  int error() {
+    int v = 0;
+    check((int)hipMemcpy(&v, err_, sizeof(int), hipMemcpyDeviceToHost), "peer err read");
+    return v;
+  }
+
+  void close() {
+    for (auto& p : mapped_)
+      if (p) { peer_ipc_close(p); p = nullptr; }
+    if (buf_) { peer_free(buf_); buf_ = nullptr; }
+    if (err_) { hipFree(err_); err_ = nullptr; }
+    for (auto& b : bases_) b = 0ull;
+  }
+
+  unsigned long long seq() const { return seq_; }
+
+ private:
+  int rank_, world_;
+  void* buf_ = nullptr;
+  int* err_ = nullptr;
+  unsigned long long seq_ = 0, timeout_ticks_ = 0;
+  std::vector<unsigned long long> bases_;
+  std::vector<void*> mapped_;
+};
+
 }  // namespace
 
 void register_loader(pybind11::module& m);  // loader.cpp: native image-folder loader
@@ -678,4 +764,15 @@ PYBIND11_MODULE(_C, m) {
   m.def("act32_fwd", &act32_fwd);
   m.def("act32_bwd", &act32_bwd);
   m.def("bn_stats", &bn_stats);
+  pybind11::class_<PeerComm>(m, "PeerComm")
+      .def(pybind11::init<int, int, double>(), pybind11::arg("rank"), pybind11::arg("world"),
+           pybind11::arg("timeout_s") = 120.0)
+      .def("handle", &PeerComm::handle)
+      .def("open", &PeerComm::open)
+      .def("all_reduce_", &PeerComm::all_reduce_)
+      .def("error", &PeerComm::error)
+      .def("close", &PeerComm::close)
+      .def_property_readonly("seq", &PeerComm::seq);
+  m.attr("PEER_MAX_ELEMS") = peer_max_elems();
+  m.attr("PEER_MAX_WORLD") = peer_max_world();
 }

@@ -1,0 +1,159 @@
+// One-shot peer all-reduce over xGMI for the SyncBN statistics.
+//
+// The reference's SyncBatchNorm issues two small blocking collectives per BN layer and step
+// (torch/nn/modules/_functions.py:74 all_gather of [mean, invstd, count], :159 all_reduce of
+// [sum_dy, sum_dy_xmu]); on ResNet-50 that is 2 x 53 latency-bound calls of <= 33 KB.  A ring
+// all-reduce pays 2(W-1) dependent hops for them.  Here every rank owns one IPC-exported buffer
+// that all its peers map (hipIpcOpenMemHandle), and one kernel does the whole exchange:
+//
+//   push:  block g of rank r writes its chunk of the input into slot [parity][r] of EVERY rank's
+//          buffer (system-scope write-through stores straight over the xGMI link to that GPU), waits
+//          for those stores to complete, then raises flag [g][r] = seq on every rank;
+//   wait:  it polls its own flags [g][q] for all q until they reach seq (bounded spin);
+//   sum:   it adds slot [parity][q] chunk g over q = 0..W-1 in rank order - the same order on every
+//          rank, so all ranks get bitwise identical statistics (as a ring all-reduce does).
+//
+// All remote accesses are stores and all loads hit the local buffer, which is allocated uncached,
+// so no cache line of another GPU can be stale.  Blocks are independent (chunk g only needs the
+// peers' chunk g), so there is no inter-block synchronisation.  The data slots are double-buffered
+// by call parity: a peer can only start call s+2 (which reuses call s's parity) after it has seen
+// this rank's flag for s+1, which is raised after this rank finished reading call s.
+//
+// The spin is bounded (a timeout in wall-clock ticks); a block that times out records the error in a
+// device word that the host checks (parallel/peer.py), so a dead peer never leaves a kernel running.
+#include <cstring>
+
+#include "common.h"
+
+namespace {
+
+constexpr int kMaxWorld = 16;
+constexpr int kChunk = 512;       // doubles per block
+constexpr int kMaxBlocks = 32;    // => at most 16384 doubles per call
+constexpr int kThreads = 256;     // 2 doubles per thread per chunk
+constexpr size_t kFlagBytes = 8192;                                   // [kMaxBlocks][kMaxWorld] u64 (4 KB used)
+constexpr size_t kSlotDoubles = (size_t)kChunk * kMaxBlocks;          // one rank's payload
+constexpr size_t kBufBytes = kFlagBytes + 2 * kMaxWorld * kSlotDoubles * sizeof(double);
+
+struct PeerTable {
+  unsigned long long base[kMaxWorld];  // every rank's buffer, as mapped in this process
+};
+
+// global (not flat) address space, so the accesses lower to global_load/store ... sc0 sc1
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+DEVI void st_sys(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+DEVI unsigned long long ld_sys(const unsigned long long* p) {
+  return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(kThreads) void peer_allreduce_f64_kernel(
+    const double* in, double* out, int n, PeerTable tab, int rank, int world,
+    unsigned long long seq, unsigned long long timeout_ticks, int* __restrict__ err) {
+  const int g = blockIdx.x;
+  const int par = (int)(seq & 1ull);
+  const int beg = g * kChunk;
+  const int cnt = min(kChunk, n - beg);
+  const int t = threadIdx.x;
+
+  // 1) push this block's chunk into slot [par][rank] of every rank (self included)
+  unsigned long long v[2];
+  bool has[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = t + k * kThreads;
+    has[k] = i < cnt;
+    v[k] = has[k] ? __double_as_longlong(in[beg + i]) : 0ull;
+  }
+  const size_t slot_off = kFlagBytes + (((size_t)par * kMaxWorld + rank) * kSlotDoubles + beg) * sizeof(double);
+  for (int p = 0; p < world; ++p) {
+    unsigned long long* dst = (unsigned long long*)(tab.base[p] + slot_off);
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (has[k]) st_sys(dst + t + k * kThreads, v[k]);
+  }
+  // every storing wave waits for its stores to be acknowledged before the flag may be raised
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t < world) {
+    unsigned long long* flag = (unsigned long long*)(tab.base[t] + ((size_t)g * kMaxWorld + rank) * 8);
+    st_sys(flag, seq);
+  }
+
+  // 2) wait until every rank's chunk g of this call has arrived (lane q polls flag [g][q])
+  if (t < 64) {
+    const unsigned long long* mine = (const unsigned long long*)(tab.base[rank] + (size_t)g * kMaxWorld * 8);
+    bool done = t >= world;
+    const unsigned long long t0 = wall_clock64();
+    bool timed_out = false;
+    while (true) {
+      if (!done) done = ld_sys(mine + t) >= seq;
+      if (__all(done)) break;
+      if (wall_clock64() - t0 > timeout_ticks) { timed_out = true; break; }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (t == 0 && timed_out) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+
+  // 3) rank-ordered sum of the W payloads (system-scope loads of the local, uncached buffer)
+  const unsigned long long* slots = (const unsigned long long*)(tab.base[rank] + kFlagBytes) +
+                                    (size_t)par * kMaxWorld * kSlotDoubles + beg;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    if (!has[k]) continue;
+    const int i = t + k * kThreads;
+    double s = 0.0;
+    for (int q = 0; q < world; ++q) s += __longlong_as_double(ld_sys(slots + (size_t)q * kSlotDoubles + i));
+    out[beg + i] = s;
+  }
+}
+
+}  // namespace
+
+size_t peer_buffer_bytes() { return kBufBytes; }
+int peer_max_world() { return kMaxWorld; }
+int peer_max_elems() { return (int)kSlotDoubles; }
+
+// Uncached device memory: every access bypasses the caches, so stores arriving over xGMI from the
+// peers are seen by this GPU's loads without any invalidation.
+int peer_alloc(void** p) {
+  hipError_t e = hipExtMallocWithFlags(p, kBufBytes, hipDeviceMallocUncached);
+  if (e != hipSuccess) return (int)e;
+  return (int)hipMemset(*p, 0, kBufBytes);
+}
+
+int peer_free(void* p) { return (int)hipFree(p); }
+
+int peer_ipc_handle(void* p, char* out64) {
+  hipIpcMemHandle_t h;
+  hipError_t e = hipIpcGetMemHandle(&h, p);
+  if (e != hipSuccess) return (int)e;
+  static_assert(sizeof(h) == 64, "hipIpcMemHandle_t size");
+  memcpy(out64, &h, sizeof(h));
+  return 0;
+}
+
+int peer_ipc_open(const char* in64, void** p) {
+  hipIpcMemHandle_t h;
+  memcpy(&h, in64, sizeof(h));
+  return (int)hipIpcOpenMemHandle(p, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+int peer_ipc_close(void* p) { return (int)hipIpcCloseMemHandle(p); }
+
+int peer_allreduce_f64_launch(const double* in, double* out, int n, const unsigned long long* bases, int rank,
+                              int world, unsigned long long seq, unsigned long long timeout_ticks, int* err,
+                              hipStream_t st) {
+  if (n <= 0) return 0;
+  if (world < 1 || world > kMaxWorld || rank < 0 || rank >= world || n > (int)kSlotDoubles) return (int)hipErrorInvalidValue;
+  PeerTable tab;
+  for (int i = 0; i < kMaxWorld; ++i) tab.base[i] = i < world ? bases[i] : 0ull;
+  const int blocks = (n + kChunk - 1) / kChunk;
+  hipLaunchKernelGGL(peer_allreduce_f64_kernel, dim3(blocks), dim3(kThreads), 0, st, in, out, n, tab, rank, world,
+                     seq, timeout_ticks, err);
+  return (int)hipGetLastError();
+}

@@ -52,6 +52,9 @@ def build_parser() -> argparse.ArgumentParser:
                         "(e4m3 + E8M0 per 32 channels) where Cin % 128 == 0, bf16 elsewhere and in backward")
     p.add_argument("--sync-bn", dest="sync_bn", action="store_true", default=True)
     p.add_argument("--no-sync-bn", dest="sync_bn", action="store_false")
+    p.add_argument("--syncbn-comm", default="auto", choices=["auto", "peer", "rccl"],
+                   help="SyncBN statistics transport: one-shot peer all-reduce over xGMI IPC buffers (peer), "
+                        "torch.distributed / RCCL (rccl), or peer when all ranks share a host and it self-checks (auto)")
     p.add_argument("--bucket-mb", type=float, default=32.0)
     p.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--steps-per-epoch", type=int, default=None, help="cap on train steps per epoch")

@@ -37,7 +37,7 @@ from ..data import CudaPrefetcher, ImageDataset, NativeFolderLoader, SyntheticIm
 from ..models import DEFAULT_IMAGE_SIZE, Classifier
 from ..ops import functional as Fx
 from ..ops.grad_arena import GradArena
-from ..parallel import GradReducer, convert_sync_batchnorm
+from ..parallel import GradReducer, convert_sync_batchnorm, setup_peer_syncbn
 from ..utils import (BEST, LATEST, AccuracyCounter, DeviceMeter, JsonlLogger, load_checkpoint,
                      load_model_state, resolve_resume, save_checkpoint)
 from ..utils.timers import PhaseTimer
@@ -112,6 +112,7 @@ class Trainer:
         a, ctx = self.args, self.ctx
         model = Classifier(self.name, self.num_classes, pretrained=a.pretrained).to(self.dev)
         self.ddp = None
+        self.syncbn_peer = False
         self.reducer = None
         self.arena = None
         self.autocast = False
@@ -136,6 +137,9 @@ class Trainer:
                 # behind the reducer's 32 MiB gradient buckets on the default group's RCCL stream
                 grp = dist.new_group(list(range(ctx.world_size))) if ctx.world_size > 1 else None
                 convert_sync_batchnorm(model, grp)
+                # one-shot xGMI peer all-reduce for the 2x53 statistics exchanges (parallel/peer.py)
+                self.syncbn_peer = self.hip and grp is not None and setup_peer_syncbn(
+                    grp, self.dev, getattr(a, "syncbn_comm", "auto"))
             if ctx.world_size > 1:
                 comm = torch.bfloat16 if a.comm_dtype == "bf16" else None
                 self.reducer = GradReducer(model, bucket_cap_mb=a.bucket_mb, comm_dtype=comm)

@@ -23,6 +23,7 @@ import torch
 import torch.distributed as dist
 
 from .. import _ext
+from ..parallel.peer import stats_all_reduce_, stats_all_reduce_async
 from .grad_arena import arena_slot, grad_buffer
 
 C = _ext.load()
@@ -857,7 +858,7 @@ def _syncbn_bwd_start(link):
     dbeta = grad_buffer(link.params[1], zero=False)
     sums = torch.empty(2 * c, dtype=torch.float64, device=link.y.device)
     C.bn_partials(link.part, stat_groups(link.rows), c, sums, dgamma, dbeta)
-    work = dist.all_reduce(sums, group=link.group, async_op=True)
+    work = stats_all_reduce_async(sums, link.group)
     link.pending = (sums, work, dgamma, dbeta)
     SYNCBN_EARLY_COUNT[0] += 1
 
@@ -1066,7 +1067,7 @@ def _bn_coef(y, gamma, beta, bn, stats_ready):
         else:
             sums = torch.empty(2 * c + 1, dtype=torch.float64, device=dev)
             C.bn_partials(part, grp, c, sums, None, None, float(rows))  # + local count in the tail
-            dist.all_reduce(sums, group=group)
+            stats_all_reduce_(sums, group)
             count_t = sums[2 * c:]
             C.bn_finalize(sums, count_t, float(rows), gamma, beta, *rs, mom, bn.eps, c, coef)
     else:
@@ -1087,7 +1088,7 @@ def _bn_bwd_k(part, grp, c, rows, training, group, count_t, params, dev):
     sums = torch.empty(2 * c, dtype=torch.float64, device=dev)
     C.bn_partials(part, grp, c, sums, dgamma, dbeta)
     if group is not None:
-        dist.all_reduce(sums, group=group)
+        stats_all_reduce_(sums, group)
     if training:
         C.bn_bwd_k(sums, count_t, float(rows), c, k)
     else:  # running statistics are constants: dy = scale * dz

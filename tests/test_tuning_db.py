@@ -45,7 +45,7 @@ def test_invalid_and_existing_entries(hip, tmp_path):
     k = ((64, 64, 64, 64, 1, 1, 1, 1, 1, 64, 1, 1, 1, 0, 0, 64, 0), 64, (0,), (0,), False, False, False, False,
          False, 0, False, True)
     db = {"conv": [[repr(k), [0, 0, 999]], [repr(k[:1] + (32,) + k[2:]), [0, 0, 0]], ["not python", [0, 0, 0]]],
-          "wgrad": [["(1, 2)", [512, 9]]]}
+          "wgrad": [["(1, 2)", [512, 99]]]}
     path = tmp_path / "db.json"
     path.write_text(json.dumps(db))
     hip._STAGES_TUNED[k[:1] + (32,) + k[2:]] = (0, 0, 2)
