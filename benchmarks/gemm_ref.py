@@ -62,7 +62,7 @@ def main():
         for i, (tm, bn, wm, wn, st) in enumerate(cfgs):
             if bn > 64 and bn >= 2 * N:
                 continue
-            res[f"{tm}x{bn}/{wm}x{wn}/s{st}"] = timeit(
+            res[f"{tm}x{bn}/{wm}x{wn}/s{st}#{i}"] = timeit(
                 lambda: hip.C.conv_gemm(A, B.view(-1), out, None, None, *geo, [0], [0], [0], hip.G_STATS, zero,
                                         None, None, None, None, None, 0, 1, 0, 0, i, None, None))
         ref = torch.mm(A, B.t())

@@ -579,7 +579,9 @@ DEVI int tap_dh(int pk) { return (pk << 24) >> 24; }
 DEVI int tap_dw(int pk) { return (pk << 16) >> 24; }
 DEVI int tap_tb(int pk) { return (int)((unsigned)pk >> 16); }
 
-template <int TM, int BN, int WM, int WN, int STAGES, bool TAP_UNIFORM>
+// PRIO: s_setprio(1) around each k-half's MFMA cluster (guide T5: keeps hipcc from moving MFMAs across
+// the barrier in among the loads); a separate table entry, chosen per shape by the tuner
+template <int TM, int BN, int WM, int WN, int STAGES, bool TAP_UNIFORM, int PRIO = 0>
 __global__ __launch_bounds__((GldsCfg<TM, BN, WM, WN, STAGES>::NTH), (GldsCfg<TM, BN, WM, WN, STAGES>::OCC))
 void conv_gemm_glds_kernel(const ConvParams p) {
   using Cfg = GldsCfg<TM, BN, WM, WN, STAGES>;
@@ -755,6 +757,7 @@ void conv_gemm_glds_kernel(const ConvParams p) {
 #pragma unroll
         for (int i = 0; i < RM; ++i) af2[i] = *(const bf16x8*)(sa + swz(wm * WTM + i * 16 + fr, 4 + fq));
       }
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
       if constexpr (JOUT) {
 #pragma unroll
         for (int j = 0; j < RN; ++j) {
@@ -774,6 +777,7 @@ void conv_gemm_glds_kernel(const ConvParams p) {
         for (int j = 0; j < RN; ++j)
           if (kk == 0) bf2[j] = *(const bf16x8*)(sb + swz(wn * WTN + j * 16 + fr, 4 + fq));
       }
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
       if (kk == 0) {
 #pragma unroll
         for (int i = 0; i < RM; ++i) af[i] = af2[i];
@@ -1454,14 +1458,14 @@ void conv_set_variant(int v) { g_variant = v; }
 static int g_single_nk = 4;  // GEMMs with at most this many 64-wide k-steps use the 1-stage ring
 void conv_set_single_stage(int nk) { g_single_nk = nk; }
 
-template <int TM, int BN, int WM, int WN, int STAGES>
+template <int TM, int BN, int WM, int WN, int STAGES, int PRIO = 0>
 static void launch_glds(const ConvParams& p, hipStream_t stream) {
   const int grid = cdiv(p.M, TM) * cdiv(p.Ncols, BN);
   constexpr int NTH = 64 * WM * WN;
   if ((p.CA % BK) == 0)
-    hipLaunchKernelGGL((conv_gemm_glds_kernel<TM, BN, WM, WN, STAGES, true>), dim3(grid), dim3(NTH), 0, stream, p);
+    hipLaunchKernelGGL((conv_gemm_glds_kernel<TM, BN, WM, WN, STAGES, true, PRIO>), dim3(grid), dim3(NTH), 0, stream, p);
   else
-    hipLaunchKernelGGL((conv_gemm_glds_kernel<TM, BN, WM, WN, STAGES, false>), dim3(grid), dim3(NTH), 0, stream, p);
+    hipLaunchKernelGGL((conv_gemm_glds_kernel<TM, BN, WM, WN, STAGES, false, PRIO>), dim3(grid), dim3(NTH), 0, stream, p);
 }
 
 template <int BN>
@@ -1482,6 +1486,7 @@ static void launch_bn(const ConvParams& p, int gm, hipStream_t stream) {
 // {tile rows, tile channels, waves along rows, waves along channels, LDS-DMA ring depth}.
 struct ConvCfg { int tm, bn, wm, wn, st; void (*launch)(const ConvParams&, hipStream_t); };
 #define CFG(TM, BN, WM, WN, ST) {TM, BN, WM, WN, ST, &launch_glds<TM, BN, WM, WN, ST>}
+#define CFGP(TM, BN, WM, WN, ST) {TM, BN, WM, WN, ST, &launch_glds<TM, BN, WM, WN, ST, 1>}
 // Measured on the ResNet-50 layers at batch 512 (benchmarks/conv_bench.py --tune-log): the 128-row
 // 4-wave tiles win on 64/128-channel outputs and short K (occupancy hides latency); the 256x256
 // 8-wave tiles (2 waves per SIMD, 64x128 or 128x64 per wave, half the LDS-DMA bytes per FLOP) win
@@ -1491,8 +1496,11 @@ static const ConvCfg g_cfgs[] = {
     CFG(256, 256, 2, 4, 2), CFG(256, 256, 4, 2, 2), CFG(256, 64, 4, 1, 1), CFG(128, 64, 2, 1, 1),
     // 32-channel tiles for 32 / 48 / 96-channel GEMMs (the Inception stem: a 64-wide tile is half empty)
     CFG(256, 32, 4, 1, 1), CFG(128, 32, 4, 1, 1), CFG(256, 32, 4, 1, 2),
+    // s_setprio around the MFMA clusters (T5) on the pipelined tiles
+    CFGP(256, 256, 2, 4, 2), CFGP(256, 256, 4, 2, 2), CFGP(128, 128, 2, 2, 2), CFGP(128, 64, 2, 2, 2),
 };
 #undef CFG
+#undef CFGP
 constexpr int kNumCfgs = sizeof(g_cfgs) / sizeof(g_cfgs[0]);
 
 int conv_num_cfgs() { return kNumCfgs; }
