@@ -83,10 +83,27 @@ class GradReducer:
         self._ready_order: list[int] = []
         self.works: list = []
         self.arena: GradArena | None = None
+        self._verify_param_shapes()
         if broadcast:
             broadcast_module_state(module, 0, group)
         self._build(list(reversed(range(len(self.params)))))
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+
+    def _verify_param_shapes(self) -> None:
+        """DDP's ``_verify_param_shape_across_processes`` (X1, torch/nn/parallel/distributed.py:862): every
+        rank must hold the same parameter list, or the flat-buffer buckets would pair different tensors."""
+        if self.world == 1:
+            return
+        mine = [(tuple(p.shape), str(p.dtype)) for p in self.params]
+        allp = [None] * self.world
+        dist.all_gather_object(allp, mine, group=self.group)
+        for r, theirs in enumerate(allp):
+            if theirs != mine:
+                bad = next((i for i, (a, b) in enumerate(zip(mine, theirs)) if a != b), min(len(mine), len(theirs)))
+                raise RuntimeError(
+                    f"GradReducer: parameter list differs between this rank and rank {r} "
+                    f"({len(mine)} vs {len(theirs)} tensors; first mismatch at index {bad}: "
+                    f"{mine[bad] if bad < len(mine) else None} vs {theirs[bad] if bad < len(theirs) else None})")
 
     # ------------------------------------------------------------------ layout
     def _build(self, order: list[int]) -> None:
@@ -194,6 +211,13 @@ class GradReducer:
             self._rebuild_pending = False
             seen = set(self._ready_order)
             order = self._ready_order + [i for i in reversed(range(len(self.params))) if i not in seen]
+            if self.world > 1:
+                # every rank must lay out the same buckets (a bucket is one collective): take rank 0's
+                # observed order, as DDP's bucket rebuild does (sync_bucket_indices)
+                box = [order]
+                dist.broadcast_object_list(box, src=dist.get_global_rank(self.group, 0) if self.group else 0,
+                                           group=self.group)
+                order = box[0]
             self._build(order)
             self._ready_order = []
         return 1.0 / self.world

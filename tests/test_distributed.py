@@ -205,3 +205,39 @@ def _w_buffers(rank, world, port):
 def test_broadcast_buffers():
     """DDP broadcast_buffers parity (X3): rank 0's BN buffers overwrite the other ranks'."""
     _run(_w_buffers)
+
+
+# ---------------------------------------------------------------------------
+def _w_shapes(rank, world, port):
+    _setup(rank, world, port)
+    from pytorch_imageclassification_distributed_amd.models import Classifier
+    from pytorch_imageclassification_distributed_amd.parallel import GradReducer
+    m = Classifier("resnet18", 4 if rank == 0 else 5)  # head differs on rank 1
+    with pytest.raises(RuntimeError, match="parameter list differs"):
+        GradReducer(m)
+
+
+def test_grad_reducer_verifies_param_shapes():
+    """X1: DDP's _verify_param_shape_across_processes - mismatched models fail loudly at construction."""
+    _run(_w_shapes)
+
+
+def _w_order(rank, world, port):
+    _setup(rank, world, port)
+    import torch.nn.functional as F
+    from pytorch_imageclassification_distributed_amd.parallel import GradReducer
+    m = _model(0)
+    red = GradReducer(m, bucket_cap_mb=0.5, first_bucket_mb=0.1)
+    x, y = torch.randn(4, 3, 16, 16), torch.randint(0, 4, (4,))
+    F.cross_entropy(m(x), y).backward()
+    if rank == 1:  # pretend this rank saw a different gradient-ready order
+        red._ready_order = list(reversed(red._ready_order))
+    red.finish()
+    import torch.distributed as dist
+    layouts = [None] * world
+    dist.all_gather_object(layouts, [(s, e, list(i)) for s, e, i in red.buckets])
+    assert layouts[0] == layouts[1]  # rank 0's observed order is the one every rank rebuilt with
+
+
+def test_bucket_rebuild_uses_rank0_order():
+    _run(_w_order)
