@@ -76,7 +76,8 @@ int dw_dgrad_launch(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, i
                     int, hipStream_t);
 int dw_wgrad_launch(const bf16_t*, const bf16_t*, float*, int, int, int, int, int, int, int, int, int, int, int,
                     int, float*, hipStream_t);
-long dw_wgrad_partial_rows(int, int, int, int, int);
+long dw_wgrad_partial_rows(int, int, int, int, int, int, int);
+void dw_set_rowstrip(int);
 void set_deterministic(int);
 void set_force_div64(int);
 int se_scale_launch(const bf16_t*, const float*, bf16_t*, int, int, int, hipStream_t);
@@ -553,7 +554,7 @@ void dw_wgrad(Tensor dy, Tensor x, Tensor dw, int N, int H, int W, int C, int OH
               int sw, int pt, int pl) {
   req(dw, F32, "dw");
   // per-block partial rows (plain stores), then an ordered column sum into dw - no contended atomics
-  const long rows = dw_wgrad_partial_rows(N, OH, OW, kh, kw);
+  const long rows = dw_wgrad_partial_rows(N, OH, OW, kh, kw, sh, sw);
   const int cols = C * kh * kw;
   Tensor part = at::empty({rows, (long)cols}, dw.options());
   check(dw_wgrad_launch(ptr<bf16_t>(dy), ptr<bf16_t>(x), ptr<float>(dw), N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl,
@@ -758,6 +759,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("dw_fwd", &dw_fwd);
   m.def("dw_dgrad", &dw_dgrad);
   m.def("dw_wgrad", &dw_wgrad);
+  m.def("dw_set_rowstrip", [](bool v) { dw_set_rowstrip(v ? 1 : 0); });
   m.def("se_scale", &se_scale);
   m.def("se_ds", &se_ds);
   m.def("se_dx", &se_dx);

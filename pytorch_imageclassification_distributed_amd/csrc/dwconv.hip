@@ -155,6 +155,218 @@ __global__ __launch_bounds__(256) void dw_dgrad_k_kernel(const bf16_t* __restric
   }
 }
 
+// ---------------------------------------------------------------------------
+// Row-strip kernels (K x K, stride S in {1, 2}).  The per-pixel kernels above issue K*K 16-B loads for
+// every 16-B output, so the neighbouring outputs' shared inputs are re-fetched through L1/L2 K*K times
+// (1.6-2.2 TB/s at best, 0.6 TB/s for the stride-2 data gradient whose gather form wastes 3/4 of its
+// taps).  Here a lane owns 8 channels of R consecutive outputs along one row and slides along the
+// input row: per kernel row it loads (R-1)*S + K chunks once and reuses them for all R outputs.
+// ---------------------------------------------------------------------------
+
+// y[n][oh][ow0 + o] for o < R.  FLIP: correlate with the 180-degree rotated filter (the stride-1 data
+// gradient is this kernel on dY with padding K-1-p).
+template <int K, int S, int R, bool FLIP>
+__global__ __launch_bounds__(256) void dw_fwd_rs_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+                                                        bf16_t* __restrict__ y, DwGeom g, PixIdx fd, int OWB) {
+  constexpr int NJ = (R - 1) * S + K;
+  const int cch = g.C >> 3;
+  const long total = (long)g.N * g.OH * OWB * cch;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    int c0, owb, oh, n;
+    pix_decode(i, cch, OWB, g.OH, fd, c0, owb, oh, n);
+    const int ow0 = owb * R;
+    const int iw0 = ow0 * S - g.pl;
+    const bf16_t* xn = x + (long)n * g.H * g.W * g.C + c0;
+    float acc[R][8];
+#pragma unroll
+    for (int o = 0; o < R; ++o)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[o][k] = 0.f;
+#pragma unroll
+    for (int r = 0; r < K; ++r) {
+      const int ih = oh * S - g.pt + r;
+      if ((unsigned)ih >= (unsigned)g.H) continue;
+      const bf16_t* xr = xn + (long)ih * g.W * g.C;
+      uint4 raw[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) raw[j] = *(const uint4*)(xr + (long)min(max(iw0 + j, 0), g.W - 1) * g.C);
+      float wv[K][8];
+#pragma unroll
+      for (int c = 0; c < K; ++c) {
+        const int tap = FLIP ? (K - 1 - r) * K + (K - 1 - c) : r * K + c;
+        unpack8(*(const uint4*)(w + (long)tap * g.C + c0), wv[c]);
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        float xv[8];
+        unpack8((unsigned)(iw0 + j) < (unsigned)g.W ? raw[j] : make_uint4(0u, 0u, 0u, 0u), xv);
+#pragma unroll
+        for (int o = 0; o < R; ++o) {
+          const int c = j - o * S;
+          if (c >= 0 && c < K) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[o][k] += xv[k] * wv[c][k];
+          }
+        }
+      }
+    }
+    bf16_t* yo = y + (((long)n * g.OH + oh) * g.OW + ow0) * g.C + c0;
+#pragma unroll
+    for (int o = 0; o < R; ++o)
+      if (ow0 + o < g.OW) *(uint4*)(yo + (long)o * g.C) = pack8(acc[o]);
+  }
+}
+
+// Stride-2 data gradient in phase form: a lane owns 8 channels of the 2R input pixels w0 .. w0+2R-1 of
+// input row h (w0 a multiple of 2R).  Only taps whose output position is integral contribute: kernel
+// rows with (h + pt - r) even, and for the column parity q the taps c with (q + pl - c) even, so the
+// loop visits ~K/2 x K/2 taps instead of K x K.  dY columns are loaded once per valid kernel row and
+// shared by both parities and all R outputs; PLP = pl & 1 makes every register index compile-time.
+template <int K, int R, int PLP>
+__global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ w,
+                                                          bf16_t* __restrict__ dx, DwGeom g, PixIdx fd, int WB) {
+  // dY columns ow = w0/2 + OB + j, j < NJ, cover (w0 + q + 2j' + pl - c) / 2 for all q, j' < R, c < K
+  constexpr int OB = (PLP - (K - 1)) >= 0 ? (PLP - (K - 1)) / 2 : -((K - 1 - PLP + 1) / 2);  // floor((PLP-K+1)/2)
+  constexpr int NJ = (1 + PLP + 2 * (R - 1)) / 2 - OB + 1;
+  const int cch = g.C >> 3;
+  const int ph = (g.pl - PLP) / 2;  // pl = 2 ph + PLP
+  const long total = (long)g.N * g.H * WB * cch;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    int c0, wb, h, n;
+    pix_decode(i, cch, WB, g.H, fd, c0, wb, h, n);
+    const int w0 = wb * 2 * R;
+    const int ob = w0 / 2 + ph + OB;  // first dY column of the strip
+    const bf16_t* dyn = dy + (long)n * g.OH * g.OW * g.C + c0;
+    float acc[2][R][8];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int o = 0; o < R; ++o)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[q][o][k] = 0.f;
+#pragma unroll
+    for (int r = 0; r < K; ++r) {
+      const int a = h + g.pt - r;
+      if (a < 0 || (a & 1)) continue;
+      const int oh = a >> 1;
+      if (oh >= g.OH) continue;
+      const bf16_t* dr = dyn + (long)oh * g.OW * g.C;
+      uint4 raw[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) raw[j] = *(const uint4*)(dr + (long)min(max(ob + j, 0), g.OW - 1) * g.C);
+      float wv[K][8];
+#pragma unroll
+      for (int c = 0; c < K; ++c) unpack8(*(const uint4*)(w + (long)(r * K + c) * g.C + c0), wv[c]);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        float dv[8];
+        unpack8((unsigned)(ob + j) < (unsigned)g.OW ? raw[j] : make_uint4(0u, 0u, 0u, 0u), dv);
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int c = (q + PLP) & 1; c < K; c += 2)
+#pragma unroll
+            for (int o = 0; o < R; ++o) {
+              // dY column of output (q, o) through tap c, relative to the strip start
+              if (j == o + (q + PLP - c) / 2 - OB) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) acc[q][o][k] += dv[k] * wv[c][k];
+              }
+            }
+      }
+    }
+    bf16_t* xo = dx + (((long)n * g.H + h) * g.W + w0) * g.C + c0;
+#pragma unroll
+    for (int o = 0; o < R; ++o)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        if (w0 + 2 * o + q < g.W) *(uint4*)(xo + (long)(2 * o + q) * g.C) = pack8(acc[q][o]);
+  }
+}
+
+// Weight gradient, one kernel row per blockIdx.y: a lane owns 8 channels and walks strips of R
+// consecutive outputs of its block's rows: R dY loads + (R-1)*S+K input loads per strip and row
+// (instead of K*K input loads per output), K x 8 accumulators.  Per-block sums are reduced over the
+// strip lanes in LDS and stored into the block's partial row (colsum reduces the rows in order).
+template <int K, int S, int R>
+__global__ __launch_bounds__(256) void dw_wgrad_rs_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                          float* __restrict__ part, DwGeom g, int OWB,
+                                                          long items_per_block) {
+  constexpr int NJ = (R - 1) * S + K;
+  __shared__ float red[256][9];
+  const int cch = g.C >> 3;
+  const int CHB = cch < 256 ? cch : 256;
+  const int RP = 256 / CHB;
+  const int tid = threadIdx.x;
+  const int lc = tid % CHB, lr = tid / CHB;
+  const int r = blockIdx.y;
+  constexpr int T = K * K;
+  const long nitems = (long)g.N * g.OH * OWB;
+  float* dst = part + blockIdx.x * (long)g.C * T;
+  for (int cb = 0; cb < cch; cb += CHB) {
+    const int chunk = cb + lc;
+    float acc[K][8];
+#pragma unroll
+    for (int c = 0; c < K; ++c)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[c][k] = 0.f;
+    if (lr < RP && chunk < cch) {
+      const int c0 = chunk * 8;
+      const long ibeg = blockIdx.x * items_per_block;
+      const long iend = ibeg + items_per_block < nitems ? ibeg + items_per_block : nitems;
+      for (long it = ibeg + lr; it < iend; it += RP) {
+        uint32_t t = (uint32_t)it;  // host: N * OH * OWB < 2^31
+        const int owb = (int)(t % (uint32_t)OWB); t /= (uint32_t)OWB;
+        const int oh = (int)(t % (uint32_t)g.OH);
+        const int n = (int)(t / (uint32_t)g.OH);
+        const int ih = oh * S - g.pt + r;
+        if ((unsigned)ih >= (unsigned)g.H) continue;
+        const int ow0 = owb * R, iw0 = ow0 * S - g.pl;
+        const bf16_t* dyr = dy + (((long)n * g.OH + oh) * g.OW) * g.C + c0;
+        const bf16_t* xr = x + (((long)n * g.H + ih) * g.W) * g.C + c0;
+        uint4 draw[R], xraw[NJ];
+#pragma unroll
+        for (int o = 0; o < R; ++o) draw[o] = *(const uint4*)(dyr + (long)min(ow0 + o, g.OW - 1) * g.C);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) xraw[j] = *(const uint4*)(xr + (long)min(max(iw0 + j, 0), g.W - 1) * g.C);
+        float dv[R][8];
+#pragma unroll
+        for (int o = 0; o < R; ++o) unpack8(ow0 + o < g.OW ? draw[o] : make_uint4(0u, 0u, 0u, 0u), dv[o]);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          float xv[8];
+          unpack8((unsigned)(iw0 + j) < (unsigned)g.W ? xraw[j] : make_uint4(0u, 0u, 0u, 0u), xv);
+#pragma unroll
+          for (int o = 0; o < R; ++o) {
+            const int c = j - o * S;
+            if (c >= 0 && c < K) {
+#pragma unroll
+              for (int k = 0; k < 8; ++k) acc[c][k] += dv[o][k] * xv[k];
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) red[tid][k] = acc[c][k];
+      __syncthreads();
+      if (lr == 0 && chunk < cch) {
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = red[tid][k];
+        for (int rr = 1; rr < RP; ++rr)
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] += red[tid + rr * CHB][k];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) dst[(long)(chunk * 8 + k) * T + r * K + c] = v[k];
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // grid: (pixel blocks, tap groups of <= DW_TG taps); block = CHB chunk lanes x RP pixel lanes.
 // Each lane loads its dY chunk once per pixel and multiplies it with the x chunks of every tap in the
 // group (neighbouring lanes hit neighbouring pixels, so the shifted x loads are cache hits); per-tap
@@ -311,9 +523,40 @@ __global__ void act32_bwd_kernel(const float* __restrict__ x, const float* __res
 
 }  // namespace
 
+// row-strip kernels on (default) or off (the per-pixel kernels; A/B and tests)
+static int g_dw_rs = 1;
+void dw_set_rowstrip(int v) { g_dw_rs = v; }
+
+static bool rs_ok(int kh, int kw, int sh, int sw) {
+  return g_dw_rs && kh == kw && (kh == 3 || kh == 5) && sh == sw && (sh == 1 || sh == 2);
+}
+
+template <int K, int S, int R, bool FLIP>
+static void launch_fwd_rs(const bf16_t* x, const bf16_t* w, bf16_t* y, const DwGeom& g, hipStream_t s) {
+  const int OWB = (g.OW + R - 1) / R;
+  const long total = (long)g.N * g.OH * OWB * (g.C / 8);
+  hipLaunchKernelGGL((dw_fwd_rs_kernel<K, S, R, FLIP>), dim3(grid_for(total)), dim3(256), 0, s, x, w, y, g,
+                     make_pixidx(total, g.C / 8, OWB, g.OH), OWB);
+}
+
+// forward (FLIP = false) or stride-1 data gradient (FLIP = true, g = the dY -> dX geometry)
+template <bool FLIP>
+static void fwd_rs(const bf16_t* x, const bf16_t* w, bf16_t* y, const DwGeom& g, hipStream_t s) {
+  if (g.kh == 3 && g.sh == 1) launch_fwd_rs<3, 1, 8, FLIP>(x, w, y, g, s);
+  else if (g.kh == 5 && g.sh == 1) launch_fwd_rs<5, 1, 8, FLIP>(x, w, y, g, s);
+  else if (g.kh == 3) launch_fwd_rs<3, 2, 4, FLIP>(x, w, y, g, s);
+  else launch_fwd_rs<5, 2, 4, FLIP>(x, w, y, g, s);
+}
+
 int dw_fwd_launch(const bf16_t* x, const bf16_t* w, bf16_t* y, float* /*stats*/, int N, int H, int W, int C, int OH,
                   int OW, int kh, int kw, int sh, int sw, int pt, int pl, hipStream_t s) {
   DwGeom g{N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl};
+  if ((long)N * OH * OW * (C / 8) <= 0) return 0;
+  if (rs_ok(kh, kw, sh, sw)) {
+    fwd_rs<false>(x, w, y, g, s);
+    HIP_CHECK_LAUNCH();
+    return 0;
+  }
   const dim3 grid(grid_for((long)N * OH * OW * (C / 8)));
   if (kh == 3 && kw == 3) hipLaunchKernelGGL(dw_fwd_k_kernel<3>, grid, dim3(256), 0, s, x, w, y, g,
                                                   make_pixidx((long)N * OH * OW * (C / 8), C / 8, OW, OH));
@@ -324,9 +567,33 @@ int dw_fwd_launch(const bf16_t* x, const bf16_t* w, bf16_t* y, float* /*stats*/,
   return 0;
 }
 
+template <int K, int R, int PLP>
+static void launch_dgrad_s2(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const DwGeom& g, hipStream_t s) {
+  const int WB = (g.W + 2 * R - 1) / (2 * R);
+  const long total = (long)g.N * g.H * WB * (g.C / 8);
+  hipLaunchKernelGGL((dw_dgrad_s2_kernel<K, R, PLP>), dim3(grid_for(total)), dim3(256), 0, s, dy, w, dx, g,
+                     make_pixidx(total, g.C / 8, WB, g.H), WB);
+}
+
 int dw_dgrad_launch(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int W, int C, int OH, int OW,
                     int kh, int kw, int sh, int sw, int pt, int pl, hipStream_t s) {
   DwGeom g{N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl};
+  if ((long)N * H * W * (C / 8) <= 0) return 0;
+  if (rs_ok(kh, kw, sh, sw) && pt <= kh - 1 && pl <= kw - 1) {
+    if (sh == 1) {
+      // dX = dY correlated with the rotated filter, padding K-1-p (right/bottom padding follows from the sizes)
+      const DwGeom gt{N, OH, OW, C, H, W, kh, kw, 1, 1, kh - 1 - pt, kw - 1 - pl};
+      fwd_rs<true>(dy, w, dx, gt, s);
+    } else if (kh == 3) {
+      if (pl & 1) launch_dgrad_s2<3, 4, 1>(dy, w, dx, g, s);
+      else launch_dgrad_s2<3, 4, 0>(dy, w, dx, g, s);
+    } else {
+      if (pl & 1) launch_dgrad_s2<5, 4, 1>(dy, w, dx, g, s);
+      else launch_dgrad_s2<5, 4, 0>(dy, w, dx, g, s);
+    }
+    HIP_CHECK_LAUNCH();
+    return 0;
+  }
   const dim3 grid(grid_for((long)N * H * W * (C / 8)));
   if (kh == 3 && kw == 3) hipLaunchKernelGGL(dw_dgrad_k_kernel<3>, grid, dim3(256), 0, s, dy, w, dx, g,
                                                   make_pixidx((long)N * H * W * (C / 8), C / 8, W, H));
@@ -347,9 +614,22 @@ static long dw_wgrad_ppb(long npix, int T, long* pblocks_out) {
   return ppb;
 }
 
-long dw_wgrad_partial_rows(int N, int OH, int OW, int kh, int kw) {
+// row-strip weight gradient: R = 4 outputs per strip, one kernel row per blockIdx.y
+constexpr int DW_WR = 4;
+
+static long dw_wgrad_rs_ipb(int N, int OH, int OW, int K, long* pblocks_out) {
+  const long items = (long)N * OH * ((OW + DW_WR - 1) / DW_WR);
+  long pblocks = 2048 / K;
+  long ipb = (items + pblocks - 1) / pblocks;
+  if (ipb < 16) ipb = 16;
+  *pblocks_out = (items + ipb - 1) / ipb;
+  return ipb;
+}
+
+long dw_wgrad_partial_rows(int N, int OH, int OW, int kh, int kw, int sh, int sw) {
   long pb;
-  dw_wgrad_ppb((long)N * OH * OW, kh * kw, &pb);
+  if (rs_ok(kh, kw, sh, sw)) dw_wgrad_rs_ipb(N, OH, OW, kh, &pb);
+  else dw_wgrad_ppb((long)N * OH * OW, kh * kw, &pb);
   return pb;
 }
 
@@ -357,6 +637,18 @@ long dw_wgrad_partial_rows(int N, int OH, int OW, int kh, int kw) {
 int dw_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* /*dw*/, int N, int H, int W, int C, int OH, int OW,
                     int kh, int kw, int sh, int sw, int pt, int pl, float* part, hipStream_t s) {
   DwGeom g{N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl};
+  if (rs_ok(kh, kw, sh, sw)) {
+    long pblocks;
+    const long ipb = dw_wgrad_rs_ipb(N, OH, OW, kh, &pblocks);
+    const int OWB = (OW + DW_WR - 1) / DW_WR;
+    const dim3 grid((unsigned)pblocks, kh);
+    if (kh == 3 && sh == 1) hipLaunchKernelGGL((dw_wgrad_rs_kernel<3, 1, DW_WR>), grid, dim3(256), 0, s, dy, x, part, g, OWB, ipb);
+    else if (kh == 5 && sh == 1) hipLaunchKernelGGL((dw_wgrad_rs_kernel<5, 1, DW_WR>), grid, dim3(256), 0, s, dy, x, part, g, OWB, ipb);
+    else if (kh == 3) hipLaunchKernelGGL((dw_wgrad_rs_kernel<3, 2, DW_WR>), grid, dim3(256), 0, s, dy, x, part, g, OWB, ipb);
+    else hipLaunchKernelGGL((dw_wgrad_rs_kernel<5, 2, DW_WR>), grid, dim3(256), 0, s, dy, x, part, g, OWB, ipb);
+    HIP_CHECK_LAUNCH();
+    return 0;
+  }
   const long npix = (long)N * OH * OW;
   const int T = kh * kw;
   long pblocks;
