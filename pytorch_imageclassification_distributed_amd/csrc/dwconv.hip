@@ -284,32 +284,36 @@ __global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(const bf16_t* __restri
   }
 }
 
-// Weight gradient, one kernel row per blockIdx.y: a lane owns 8 channels and walks strips of R
-// consecutive outputs of its block's rows: R dY loads + (R-1)*S+K input loads per strip and row
-// (instead of K*K input loads per output), K x 8 accumulators.  Per-block sums are reduced over the
+// Weight gradient: a lane owns 8 channels and walks strips of R consecutive outputs of its block's
+// rows: R dY loads + (R-1)*S+K input loads per strip and kernel row (instead of K*K input loads per
+// output).  KR kernel rows per pass (blockIdx.y = pass): KR = K keeps the dY strip in registers for all
+// rows (K = 3), KR = 1 bounds the accumulators to K x 8 (K = 5).  Per-block sums are reduced over the
 // strip lanes in LDS and stored into the block's partial row (colsum reduces the rows in order).
-template <int K, int S, int R>
+template <int K, int S, int R, int KR>
 __global__ __launch_bounds__(256) void dw_wgrad_rs_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                           float* __restrict__ part, DwGeom g, int OWB,
                                                           long items_per_block) {
   constexpr int NJ = (R - 1) * S + K;
-  __shared__ float red[256][9];
+  constexpr int KE = K * 8, KS = KE + 1;  // one kernel row's accumulators per lane, padded LDS row
+  __shared__ float red[256 * KS];
   const int cch = g.C >> 3;
   const int CHB = cch < 256 ? cch : 256;
   const int RP = 256 / CHB;
   const int tid = threadIdx.x;
   const int lc = tid % CHB, lr = tid / CHB;
-  const int r = blockIdx.y;
+  const int r0 = blockIdx.y * KR;
   constexpr int T = K * K;
   const long nitems = (long)g.N * g.OH * OWB;
   float* dst = part + blockIdx.x * (long)g.C * T;
   for (int cb = 0; cb < cch; cb += CHB) {
     const int chunk = cb + lc;
-    float acc[K][8];
+    float acc[KR][K][8];
 #pragma unroll
-    for (int c = 0; c < K; ++c)
+    for (int q = 0; q < KR; ++q)
 #pragma unroll
-      for (int k = 0; k < 8; ++k) acc[c][k] = 0.f;
+      for (int c = 0; c < K; ++c)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[q][c][k] = 0.f;
     if (lr < RP && chunk < cch) {
       const int c0 = chunk * 8;
       const long ibeg = blockIdx.x * items_per_block;
@@ -319,48 +323,53 @@ __global__ __launch_bounds__(256) void dw_wgrad_rs_kernel(const bf16_t* __restri
         const int owb = (int)(t % (uint32_t)OWB); t /= (uint32_t)OWB;
         const int oh = (int)(t % (uint32_t)g.OH);
         const int n = (int)(t / (uint32_t)g.OH);
-        const int ih = oh * S - g.pt + r;
-        if ((unsigned)ih >= (unsigned)g.H) continue;
         const int ow0 = owb * R, iw0 = ow0 * S - g.pl;
         const bf16_t* dyr = dy + (((long)n * g.OH + oh) * g.OW) * g.C + c0;
-        const bf16_t* xr = x + (((long)n * g.H + ih) * g.W) * g.C + c0;
-        uint4 draw[R], xraw[NJ];
+        uint4 draw[R];
 #pragma unroll
         for (int o = 0; o < R; ++o) draw[o] = *(const uint4*)(dyr + (long)min(ow0 + o, g.OW - 1) * g.C);
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) xraw[j] = *(const uint4*)(xr + (long)min(max(iw0 + j, 0), g.W - 1) * g.C);
         float dv[R][8];
 #pragma unroll
         for (int o = 0; o < R; ++o) unpack8(ow0 + o < g.OW ? draw[o] : make_uint4(0u, 0u, 0u, 0u), dv[o]);
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          float xv[8];
-          unpack8((unsigned)(iw0 + j) < (unsigned)g.W ? xraw[j] : make_uint4(0u, 0u, 0u, 0u), xv);
+        for (int q = 0; q < KR; ++q) {
+          const int ih = oh * S - g.pt + r0 + q;
+          if ((unsigned)ih >= (unsigned)g.H) continue;
+          const bf16_t* xr = x + (((long)n * g.H + ih) * g.W) * g.C + c0;
+          uint4 xraw[NJ];
 #pragma unroll
-          for (int o = 0; o < R; ++o) {
-            const int c = j - o * S;
-            if (c >= 0 && c < K) {
+          for (int j = 0; j < NJ; ++j) xraw[j] = *(const uint4*)(xr + (long)min(max(iw0 + j, 0), g.W - 1) * g.C);
 #pragma unroll
-              for (int k = 0; k < 8; ++k) acc[c][k] += dv[o][k] * xv[k];
+          for (int j = 0; j < NJ; ++j) {
+            float xv[8];
+            unpack8((unsigned)(iw0 + j) < (unsigned)g.W ? xraw[j] : make_uint4(0u, 0u, 0u, 0u), xv);
+#pragma unroll
+            for (int o = 0; o < R; ++o) {
+              const int c = j - o * S;
+              if (c >= 0 && c < K) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) acc[q][c][k] += dv[o][k] * xv[k];
+              }
             }
           }
         }
       }
     }
+    // every (chunk lane, tap, channel) sum over the RP strip lanes is one thread's loop: all 256 threads
+    // share the reduction instead of the CHB row-0 lanes walking RP rows each
 #pragma unroll
-    for (int c = 0; c < K; ++c) {
+    for (int q = 0; q < KR; ++q) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) red[tid][k] = acc[c][k];
+      for (int c = 0; c < K; ++c)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) red[tid * KS + c * 8 + k] = acc[q][c][k];
       __syncthreads();
-      if (lr == 0 && chunk < cch) {
-        float v[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = red[tid][k];
-        for (int rr = 1; rr < RP; ++rr)
-#pragma unroll
-          for (int k = 0; k < 8; ++k) v[k] += red[tid + rr * CHB][k];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) dst[(long)(chunk * 8 + k) * T + r * K + c] = v[k];
+      for (int o = tid; o < CHB * KE; o += 256) {
+        const int l = o / KE, e = o - l * KE;
+        float v = 0.f;
+        for (int rr = 0; rr < RP; ++rr) v += red[(rr * CHB + l) * KS + e];
+        const int ch = cb + l;
+        if (ch < cch) dst[(long)(ch * 8 + (e & 7)) * T + (r0 + q) * K + (e >> 3)] = v;
       }
       __syncthreads();
     }
@@ -619,7 +628,7 @@ constexpr int DW_WR = 4;
 
 static long dw_wgrad_rs_ipb(int N, int OH, int OW, int K, long* pblocks_out) {
   const long items = (long)N * OH * ((OW + DW_WR - 1) / DW_WR);
-  long pblocks = 2048 / K;
+  long pblocks = K == 3 ? 1024 : 2048 / K;  // blocks per pass; K = 3 runs one pass, K = 5 five
   long ipb = (items + pblocks - 1) / pblocks;
   if (ipb < 16) ipb = 16;
   *pblocks_out = (items + ipb - 1) / ipb;
@@ -641,11 +650,12 @@ int dw_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* /*dw*/, int N, int
     long pblocks;
     const long ipb = dw_wgrad_rs_ipb(N, OH, OW, kh, &pblocks);
     const int OWB = (OW + DW_WR - 1) / DW_WR;
-    const dim3 grid((unsigned)pblocks, kh);
-    if (kh == 3 && sh == 1) hipLaunchKernelGGL((dw_wgrad_rs_kernel<3, 1, DW_WR>), grid, dim3(256), 0, s, dy, x, part, g, OWB, ipb);
-    else if (kh == 5 && sh == 1) hipLaunchKernelGGL((dw_wgrad_rs_kernel<5, 1, DW_WR>), grid, dim3(256), 0, s, dy, x, part, g, OWB, ipb);
-    else if (kh == 3) hipLaunchKernelGGL((dw_wgrad_rs_kernel<3, 2, DW_WR>), grid, dim3(256), 0, s, dy, x, part, g, OWB, ipb);
-    else hipLaunchKernelGGL((dw_wgrad_rs_kernel<5, 2, DW_WR>), grid, dim3(256), 0, s, dy, x, part, g, OWB, ipb);
+    // K = 3: all kernel rows in one pass (one dY read); K = 5: one kernel row per blockIdx.y
+    const dim3 g3((unsigned)pblocks, 1), g5((unsigned)pblocks, 5);
+    if (kh == 3 && sh == 1) hipLaunchKernelGGL((dw_wgrad_rs_kernel<3, 1, DW_WR, 3>), g3, dim3(256), 0, s, dy, x, part, g, OWB, ipb);
+    else if (kh == 5 && sh == 1) hipLaunchKernelGGL((dw_wgrad_rs_kernel<5, 1, DW_WR, 1>), g5, dim3(256), 0, s, dy, x, part, g, OWB, ipb);
+    else if (kh == 3) hipLaunchKernelGGL((dw_wgrad_rs_kernel<3, 2, DW_WR, 3>), g3, dim3(256), 0, s, dy, x, part, g, OWB, ipb);
+    else hipLaunchKernelGGL((dw_wgrad_rs_kernel<5, 2, DW_WR, 1>), g5, dim3(256), 0, s, dy, x, part, g, OWB, ipb);
     HIP_CHECK_LAUNCH();
     return 0;
   }
