@@ -73,7 +73,9 @@ int scale_rows_launch(const bf16_t*, const float*, bf16_t*, long, long, hipStrea
 int dw_fwd_launch(const bf16_t*, const bf16_t*, bf16_t*, float*, int, int, int, int, int, int, int, int, int,
                   int, int, int, hipStream_t);
 int dw_dgrad_launch(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int, int,
-                    int, hipStream_t);
+                    int, const bf16_t*, const float*, float*, int, int, hipStream_t);
+bool dw_dgrad_link_ok(int, int, int, int, int, int);
+int dw_dgrad_link_blocks(int, int, int, int, int, int, int, int);
 int dw_wgrad_launch(const bf16_t*, const bf16_t*, float*, int, int, int, int, int, int, int, int, int, int, int,
                     int, float*, hipStream_t);
 long dw_wgrad_partial_rows(int, int, int, int, int, int, int);
@@ -86,6 +88,10 @@ int se_dx_launch(const bf16_t*, const float*, const float*, bf16_t*, int, int, i
 int act32_fwd_launch(const float*, float*, long, int, hipStream_t);
 int act32_bwd_launch(const float*, const float*, float*, long, int, hipStream_t);
 int bn_stats_launch(const bf16_t*, long, int, float*, int, hipStream_t);
+int se_mlp_fwd_launch(const float*, const float*, const float*, const float*, const float*, float*, float*, int, int,
+                      int, hipStream_t);
+int se_mlp_bwd_launch(const float*, const float*, const float*, const float*, const float*, const float*, float*,
+                      float*, float*, float*, float*, float*, float*, int, int, int, hipStream_t);
 size_t peer_buffer_bytes();
 int peer_max_world();
 int peer_max_elems();
@@ -543,10 +549,17 @@ void dw_fwd(Tensor x, Tensor w, Tensor y, OT stats, int N, int H, int W, int C, 
         "dw_fwd");
 }
 
+// link_y / link_coef / link_part / G / act: the producer BN's fused backward reduce (dx receives dz)
 void dw_dgrad(Tensor dy, Tensor w, Tensor dx, int N, int H, int W, int C, int OH, int OW, int kh, int kw, int sh,
-              int sw, int pt, int pl) {
+              int sw, int pt, int pl, OT link_y, OT link_coef, OT link_part, int G, int act) {
+  const bf16_t* ly = optr<bf16_t>(link_y);
+  if (ly) {
+    TORCH_CHECK(link_y->numel() == dx.numel() && link_coef.has_value() && link_part.has_value() &&
+                link_coef->numel() >= 4L * C && link_part->numel() >= 2L * C * G, "dw_dgrad: link tensors");
+    TORCH_CHECK(dw_dgrad_link_ok(kh, kw, sh, sw, pt, pl), "dw_dgrad: no fused BN-backward kernel for this geometry");
+  }
   check(dw_dgrad_launch(ptr<bf16_t>(dy), ptr<bf16_t>(w), ptr<bf16_t>(dx), N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl,
-                        cur()),
+                        ly, optr<float>(link_coef), optr<float>(link_part), G, act, cur()),
         "dw_dgrad");
 }
 
@@ -588,6 +601,29 @@ void bn_stats(Tensor y, long rows, int C, Tensor part, int G) {
   req(y, BF, "y");
   TORCH_CHECK(C % 8 == 0, "bn_stats: C % 8");
   check(bn_stats_launch(ptr<bf16_t>(y), rows, C, ptr<float>(part), G, cur()), "bn_stats");
+}
+
+void f32(const Tensor& t, long n, const char* name) {
+  req(t, F32, name);
+  TORCH_CHECK(t.is_contiguous() && t.numel() >= n, name, ": contiguous fp32 with >= ", n, " elements");
+}
+
+void se_mlp_fwd(Tensor p, Tensor wr, Tensor br, Tensor we, Tensor be, Tensor h, Tensor s, int N, int C, int nsq) {
+  f32(p, (long)N * C, "p"); f32(wr, (long)nsq * C, "wr"); f32(br, nsq, "br"); f32(we, (long)C * nsq, "we");
+  f32(be, C, "be"); f32(h, (long)N * nsq, "h"); f32(s, (long)N * C, "s");
+  check(se_mlp_fwd_launch(ptr<float>(p), ptr<float>(wr), ptr<float>(br), ptr<float>(we), ptr<float>(be), ptr<float>(h),
+                          ptr<float>(s), N, C, nsq, cur()), "se_mlp_fwd");
+}
+
+void se_mlp_bwd(Tensor ds, Tensor s, Tensor h, Tensor p, Tensor wr, Tensor we, Tensor de, Tensor dh, Tensor dp,
+                Tensor dwr, Tensor dbr, Tensor dwe, Tensor dbe, int N, int C, int nsq) {
+  const long nc = (long)N * C, nh = (long)N * nsq, w = (long)C * nsq;
+  f32(ds, nc, "ds"); f32(s, nc, "s"); f32(h, nh, "h"); f32(p, nc, "p"); f32(wr, w, "wr"); f32(we, w, "we");
+  f32(de, nc, "de"); f32(dh, nh, "dh"); f32(dp, nc, "dp"); f32(dwr, w, "dwr"); f32(dbr, nsq, "dbr");
+  f32(dwe, w, "dwe"); f32(dbe, C, "dbe");
+  check(se_mlp_bwd_launch(ptr<float>(ds), ptr<float>(s), ptr<float>(h), ptr<float>(p), ptr<float>(wr), ptr<float>(we),
+                          ptr<float>(de), ptr<float>(dh), ptr<float>(dp), ptr<float>(dwr), ptr<float>(dbr),
+                          ptr<float>(dwe), ptr<float>(dbe), N, C, nsq, cur()), "se_mlp_bwd");
 }
 
 // One rank's end of the one-shot peer all-reduce (peer.hip): its IPC-exported buffer, the peers'
@@ -757,7 +793,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("dropout_bwd", &dropout_bwd);
   m.def("scale_rows", &scale_rows);
   m.def("dw_fwd", &dw_fwd);
-  m.def("dw_dgrad", &dw_dgrad);
+  m.def("dw_dgrad", &dw_dgrad, pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("dx"), pybind11::arg("N"),
+        pybind11::arg("H"), pybind11::arg("W"), pybind11::arg("C"), pybind11::arg("OH"), pybind11::arg("OW"),
+        pybind11::arg("kh"), pybind11::arg("kw"), pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("pt"),
+        pybind11::arg("pl"), pybind11::arg("link_y") = pybind11::none(), pybind11::arg("link_coef") = pybind11::none(),
+        pybind11::arg("link_part") = pybind11::none(), pybind11::arg("G") = 1, pybind11::arg("act") = 0);
+  m.def("dw_dgrad_link_ok", &dw_dgrad_link_ok);
+  m.def("dw_dgrad_link_blocks", &dw_dgrad_link_blocks);
   m.def("dw_wgrad", &dw_wgrad);
   m.def("dw_set_rowstrip", [](bool v) { dw_set_rowstrip(v ? 1 : 0); });
   m.def("se_scale", &se_scale);
@@ -766,6 +808,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("act32_fwd", &act32_fwd);
   m.def("act32_bwd", &act32_bwd);
   m.def("bn_stats", &bn_stats);
+  m.def("se_mlp_fwd", &se_mlp_fwd);
+  m.def("se_mlp_bwd", &se_mlp_bwd);
   pybind11::class_<PeerComm>(m, "PeerComm")
       .def(pybind11::init<int, int, double>(), pybind11::arg("rank"), pybind11::arg("world"),
            pybind11::arg("timeout_s") = 120.0)

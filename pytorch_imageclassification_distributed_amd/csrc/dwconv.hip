@@ -155,6 +155,66 @@ __global__ __launch_bounds__(256) void dw_dgrad_k_kernel(const bf16_t* __restric
   }
 }
 
+// Fused BN-backward reduce of the producer of the depthwise input (x = act(BN(y)), this conv its only
+// consumer), as the GEMM dgrad epilogue does (conv_gemm.hip): the data-gradient kernel writes
+// dz = act'(z) * dX instead of dX and accumulates sum dz, sum dz * xhat per channel, one atomic per
+// (block, channel) into G rotating partial rows (bn_partials reduces them) - the standalone
+// bn_bwd_reduce pass over (g, y) disappears.
+struct DwLink {
+  const bf16_t* y;     // producer BN input [N][H][W][C]
+  const float* coef;   // [4][C] scale, shift, mean, invstd
+  float* part;         // [G][2][C] zeroed partial rows
+  int G, act;
+};
+
+// the lane's coefficients: its channel chunk is fixed (the launcher makes the grid stride a multiple of
+// C/8), so they are loaded once per lane
+struct LinkCoef {
+  float sc[8], sh[8], mu[8], is[8];
+};
+
+DEVI void link_coef(const DwLink& L, int C, LinkCoef& k) {
+  const int c0 = (int)(((long)blockIdx.x * blockDim.x + threadIdx.x) % (C >> 3)) * 8;
+  *(float4*)k.sc = *(const float4*)(L.coef + c0);         *(float4*)(k.sc + 4) = *(const float4*)(L.coef + c0 + 4);
+  *(float4*)k.sh = *(const float4*)(L.coef + C + c0);     *(float4*)(k.sh + 4) = *(const float4*)(L.coef + C + c0 + 4);
+  *(float4*)k.mu = *(const float4*)(L.coef + 2 * C + c0); *(float4*)(k.mu + 4) = *(const float4*)(L.coef + 2 * C + c0 + 4);
+  *(float4*)k.is = *(const float4*)(L.coef + 3 * C + c0); *(float4*)(k.is + 4) = *(const float4*)(L.coef + 3 * C + c0 + 4);
+}
+
+// dz for 8 channels of one pixel (in place), accumulating the partial sums
+DEVI void link_dz(const DwLink& L, const LinkCoef& k, long pix, int C, int c0, float* g, float* s8, float* q8) {
+  float yv[8];
+  unpack8(*(const uint4*)(L.y + pix * C + c0), yv);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float dz = act_grad(yv[e] * k.sc[e] + k.sh[e], g[e], L.act);
+    g[e] = dz;
+    s8[e] += dz;
+    q8[e] += dz * (yv[e] - k.mu[e]) * k.is[e];
+  }
+}
+
+// block end: lanes with equal tid % cch share a chunk; one representative per chunk adds its 16 sums
+DEVI void link_flush(const DwLink& L, int C, const float* s8, const float* q8) {
+  __shared__ float red[256][17];
+  const int tid = threadIdx.x, cch = C >> 3;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { red[tid][k] = s8[k]; red[tid][8 + k] = q8[k]; }
+  __syncthreads();
+  if (tid < cch) {
+    float v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = red[tid][k];
+    for (int t = tid + cch; t < 256; t += cch)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v[k] += red[t][k];
+    const int chunk = (int)(((long)blockIdx.x * 256 + tid) % cch);
+    float* dst = L.part + (size_t)(blockIdx.x % L.G) * 2 * C + chunk * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { atomicAdd(dst + k, v[k]); atomicAdd(dst + C + k, v[8 + k]); }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Row-strip kernels (K x K, stride S in {1, 2}).  The per-pixel kernels above issue K*K 16-B loads for
 // every 16-B output, so the neighbouring outputs' shared inputs are re-fetched through L1/L2 K*K times
@@ -165,12 +225,16 @@ __global__ __launch_bounds__(256) void dw_dgrad_k_kernel(const bf16_t* __restric
 
 // y[n][oh][ow0 + o] for o < R.  FLIP: correlate with the 180-degree rotated filter (the stride-1 data
 // gradient is this kernel on dY with padding K-1-p).
-template <int K, int S, int R, bool FLIP>
+template <int K, int S, int R, bool FLIP, bool LINK = false>
 __global__ __launch_bounds__(256) void dw_fwd_rs_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
-                                                        bf16_t* __restrict__ y, DwGeom g, PixIdx fd, int OWB) {
+                                                        bf16_t* __restrict__ y, DwGeom g, PixIdx fd, int OWB,
+                                                        DwLink L) {
   constexpr int NJ = (R - 1) * S + K;
   const int cch = g.C >> 3;
   const long total = (long)g.N * g.OH * OWB * cch;
+  float s8[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  LinkCoef lk;
+  if constexpr (LINK) link_coef(L, g.C, lk);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     int c0, owb, oh, n;
     pix_decode(i, cch, OWB, g.OH, fd, c0, owb, oh, n);
@@ -210,11 +274,16 @@ __global__ __launch_bounds__(256) void dw_fwd_rs_kernel(const bf16_t* __restrict
         }
       }
     }
-    bf16_t* yo = y + (((long)n * g.OH + oh) * g.OW + ow0) * g.C + c0;
+    const long pix0 = ((long)n * g.OH + oh) * g.OW + ow0;
+    bf16_t* yo = y + pix0 * g.C + c0;
 #pragma unroll
     for (int o = 0; o < R; ++o)
-      if (ow0 + o < g.OW) *(uint4*)(yo + (long)o * g.C) = pack8(acc[o]);
+      if (ow0 + o < g.OW) {
+        if constexpr (LINK) link_dz(L, lk, pix0 + o, g.C, c0, acc[o], s8, q8);
+        *(uint4*)(yo + (long)o * g.C) = pack8(acc[o]);
+      }
   }
+  if constexpr (LINK) link_flush(L, g.C, s8, q8);
 }
 
 // Stride-2 data gradient in phase form: a lane owns 8 channels of the 2R input pixels w0 .. w0+2R-1 of
@@ -222,15 +291,19 @@ __global__ __launch_bounds__(256) void dw_fwd_rs_kernel(const bf16_t* __restrict
 // rows with (h + pt - r) even, and for the column parity q the taps c with (q + pl - c) even, so the
 // loop visits ~K/2 x K/2 taps instead of K x K.  dY columns are loaded once per valid kernel row and
 // shared by both parities and all R outputs; PLP = pl & 1 makes every register index compile-time.
-template <int K, int R, int PLP>
+template <int K, int R, int PLP, bool LINK = false>
 __global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ w,
-                                                          bf16_t* __restrict__ dx, DwGeom g, PixIdx fd, int WB) {
+                                                          bf16_t* __restrict__ dx, DwGeom g, PixIdx fd, int WB,
+                                                          DwLink L) {
   // dY columns ow = w0/2 + OB + j, j < NJ, cover (w0 + q + 2j' + pl - c) / 2 for all q, j' < R, c < K
   constexpr int OB = (PLP - (K - 1)) >= 0 ? (PLP - (K - 1)) / 2 : -((K - 1 - PLP + 1) / 2);  // floor((PLP-K+1)/2)
   constexpr int NJ = (1 + PLP + 2 * (R - 1)) / 2 - OB + 1;
   const int cch = g.C >> 3;
   const int ph = (g.pl - PLP) / 2;  // pl = 2 ph + PLP
   const long total = (long)g.N * g.H * WB * cch;
+  float s8[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  LinkCoef lk;
+  if constexpr (LINK) link_coef(L, g.C, lk);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     int c0, wb, h, n;
     pix_decode(i, cch, WB, g.H, fd, c0, wb, h, n);
@@ -275,13 +348,18 @@ __global__ __launch_bounds__(256) void dw_dgrad_s2_kernel(const bf16_t* __restri
             }
       }
     }
-    bf16_t* xo = dx + (((long)n * g.H + h) * g.W + w0) * g.C + c0;
+    const long pix0 = ((long)n * g.H + h) * g.W + w0;
+    bf16_t* xo = dx + pix0 * g.C + c0;
 #pragma unroll
     for (int o = 0; o < R; ++o)
 #pragma unroll
       for (int q = 0; q < 2; ++q)
-        if (w0 + 2 * o + q < g.W) *(uint4*)(xo + (long)(2 * o + q) * g.C) = pack8(acc[q][o]);
+        if (w0 + 2 * o + q < g.W) {
+          if constexpr (LINK) link_dz(L, lk, pix0 + 2 * o + q, g.C, c0, acc[q][o], s8, q8);
+          *(uint4*)(xo + (long)(2 * o + q) * g.C) = pack8(acc[q][o]);
+        }
   }
+  if constexpr (LINK) link_flush(L, g.C, s8, q8);
 }
 
 // Weight gradient: a lane owns 8 channels and walks strips of R consecutive outputs of its block's
@@ -540,21 +618,34 @@ static bool rs_ok(int kh, int kw, int sh, int sw) {
   return g_dw_rs && kh == kw && (kh == 3 || kh == 5) && sh == sw && (sh == 1 || sh == 2);
 }
 
-template <int K, int S, int R, bool FLIP>
-static void launch_fwd_rs(const bf16_t* x, const bf16_t* w, bf16_t* y, const DwGeom& g, hipStream_t s) {
+// blocks for a LINK launch: at most 2048 (one 16-value atomic flush per chunk and block), a multiple of
+// cch / gcd(cch, 256) so the grid stride is a multiple of cch (every lane keeps one channel chunk)
+static int link_grid(long total, int cch) {
+  const int b = grid_for(total, 2048);
+  int gcd = cch, m = 256;
+  while (m) { const int t = gcd % m; gcd = m; m = t; }
+  const int unit = cch / gcd;
+  return ((b + unit - 1) / unit) * unit;
+}
+
+template <int K, int S, int R, bool FLIP, bool LINK>
+static void launch_fwd_rs(const bf16_t* x, const bf16_t* w, bf16_t* y, const DwGeom& g, const DwLink& L,
+                          hipStream_t s) {
   const int OWB = (g.OW + R - 1) / R;
   const long total = (long)g.N * g.OH * OWB * (g.C / 8);
-  hipLaunchKernelGGL((dw_fwd_rs_kernel<K, S, R, FLIP>), dim3(grid_for(total)), dim3(256), 0, s, x, w, y, g,
-                     make_pixidx(total, g.C / 8, OWB, g.OH), OWB);
+  const int grid = LINK ? link_grid(total, g.C / 8) : grid_for(total);
+  hipLaunchKernelGGL((dw_fwd_rs_kernel<K, S, R, FLIP, LINK>), dim3(grid), dim3(256), 0, s, x, w, y, g,
+                     make_pixidx(total, g.C / 8, OWB, g.OH), OWB, L);
 }
 
 // forward (FLIP = false) or stride-1 data gradient (FLIP = true, g = the dY -> dX geometry)
-template <bool FLIP>
-static void fwd_rs(const bf16_t* x, const bf16_t* w, bf16_t* y, const DwGeom& g, hipStream_t s) {
-  if (g.kh == 3 && g.sh == 1) launch_fwd_rs<3, 1, 8, FLIP>(x, w, y, g, s);
-  else if (g.kh == 5 && g.sh == 1) launch_fwd_rs<5, 1, 8, FLIP>(x, w, y, g, s);
-  else if (g.kh == 3) launch_fwd_rs<3, 2, 4, FLIP>(x, w, y, g, s);
-  else launch_fwd_rs<5, 2, 4, FLIP>(x, w, y, g, s);
+template <bool FLIP, bool LINK = false>
+static void fwd_rs(const bf16_t* x, const bf16_t* w, bf16_t* y, const DwGeom& g, hipStream_t s,
+                   const DwLink& L = DwLink{nullptr, nullptr, nullptr, 1, 0}) {
+  if (g.kh == 3 && g.sh == 1) launch_fwd_rs<3, 1, 8, FLIP, LINK>(x, w, y, g, L, s);
+  else if (g.kh == 5 && g.sh == 1) launch_fwd_rs<5, 1, 8, FLIP, LINK>(x, w, y, g, L, s);
+  else if (g.kh == 3) launch_fwd_rs<3, 2, 4, FLIP, LINK>(x, w, y, g, L, s);
+  else launch_fwd_rs<5, 2, 4, FLIP, LINK>(x, w, y, g, L, s);
 }
 
 int dw_fwd_launch(const bf16_t* x, const bf16_t* w, bf16_t* y, float* /*stats*/, int N, int H, int W, int C, int OH,
@@ -576,33 +667,57 @@ int dw_fwd_launch(const bf16_t* x, const bf16_t* w, bf16_t* y, float* /*stats*/,
   return 0;
 }
 
-template <int K, int R, int PLP>
-static void launch_dgrad_s2(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const DwGeom& g, hipStream_t s) {
+template <int K, int R, int PLP, bool LINK>
+static void launch_dgrad_s2(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const DwGeom& g, const DwLink& L,
+                            hipStream_t s) {
   const int WB = (g.W + 2 * R - 1) / (2 * R);
   const long total = (long)g.N * g.H * WB * (g.C / 8);
-  hipLaunchKernelGGL((dw_dgrad_s2_kernel<K, R, PLP>), dim3(grid_for(total)), dim3(256), 0, s, dy, w, dx, g,
-                     make_pixidx(total, g.C / 8, WB, g.H), WB);
+  const int grid = LINK ? link_grid(total, g.C / 8) : grid_for(total);
+  hipLaunchKernelGGL((dw_dgrad_s2_kernel<K, R, PLP, LINK>), dim3(grid), dim3(256), 0, s, dy, w, dx, g,
+                     make_pixidx(total, g.C / 8, WB, g.H), WB, L);
+}
+
+template <bool LINK>
+static void dgrad_rs(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const DwGeom& g, const DwLink& L, hipStream_t s) {
+  if (g.sh == 1) {
+    // dX = dY correlated with the rotated filter, padding K-1-p (right/bottom padding follows from the sizes)
+    const DwGeom gt{g.N, g.OH, g.OW, g.C, g.H, g.W, g.kh, g.kw, 1, 1, g.kh - 1 - g.pt, g.kw - 1 - g.pl};
+    fwd_rs<true, LINK>(dy, w, dx, gt, s, L);
+  } else if (g.kh == 3) {
+    if (g.pl & 1) launch_dgrad_s2<3, 4, 1, LINK>(dy, w, dx, g, L, s);
+    else launch_dgrad_s2<3, 4, 0, LINK>(dy, w, dx, g, L, s);
+  } else {
+    if (g.pl & 1) launch_dgrad_s2<5, 4, 1, LINK>(dy, w, dx, g, L, s);
+    else launch_dgrad_s2<5, 4, 0, LINK>(dy, w, dx, g, L, s);
+  }
+}
+
+bool dw_dgrad_link_ok(int kh, int kw, int sh, int sw, int pt, int pl) {
+  return rs_ok(kh, kw, sh, sw) && pt <= kh - 1 && pl <= kw - 1;
+}
+
+// partial rows (== blocks) of a LINK data-gradient launch of this geometry
+int dw_dgrad_link_blocks(int N, int H, int W, int C, int OH, int OW, int kh, int sh) {
+  const int cch = C / 8;
+  long total;
+  if (sh == 1) total = (long)N * H * ((W + 7) / 8) * cch;             // fwd_rs<FLIP> over dX, R = 8
+  else total = (long)N * H * ((W + 7) / 8) * cch;                     // s2 phases: WB = ceil(W / 2R), R = 4
+  (void)OH; (void)OW; (void)kh;
+  return link_grid(total, cch);
 }
 
 int dw_dgrad_launch(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int W, int C, int OH, int OW,
-                    int kh, int kw, int sh, int sw, int pt, int pl, hipStream_t s) {
+                    int kh, int kw, int sh, int sw, int pt, int pl, const bf16_t* ly, const float* lcoef,
+                    float* lpart, int lG, int lact, hipStream_t s) {
   DwGeom g{N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl};
   if ((long)N * H * W * (C / 8) <= 0) return 0;
-  if (rs_ok(kh, kw, sh, sw) && pt <= kh - 1 && pl <= kw - 1) {
-    if (sh == 1) {
-      // dX = dY correlated with the rotated filter, padding K-1-p (right/bottom padding follows from the sizes)
-      const DwGeom gt{N, OH, OW, C, H, W, kh, kw, 1, 1, kh - 1 - pt, kw - 1 - pl};
-      fwd_rs<true>(dy, w, dx, gt, s);
-    } else if (kh == 3) {
-      if (pl & 1) launch_dgrad_s2<3, 4, 1>(dy, w, dx, g, s);
-      else launch_dgrad_s2<3, 4, 0>(dy, w, dx, g, s);
-    } else {
-      if (pl & 1) launch_dgrad_s2<5, 4, 1>(dy, w, dx, g, s);
-      else launch_dgrad_s2<5, 4, 0>(dy, w, dx, g, s);
-    }
+  if (dw_dgrad_link_ok(kh, kw, sh, sw, pt, pl)) {
+    if (ly != nullptr) dgrad_rs<true>(dy, w, dx, g, DwLink{ly, lcoef, lpart, lG > 0 ? lG : 1, lact}, s);
+    else dgrad_rs<false>(dy, w, dx, g, DwLink{nullptr, nullptr, nullptr, 1, 0}, s);
     HIP_CHECK_LAUNCH();
     return 0;
   }
+  if (ly != nullptr) return 2;  // the per-pixel kernels have no fused BN-backward epilogue
   const dim3 grid(grid_for((long)N * H * W * (C / 8)));
   if (kh == 3 && kw == 3) hipLaunchKernelGGL(dw_dgrad_k_kernel<3>, grid, dim3(256), 0, s, dy, w, dx, g,
                                                   make_pixidx((long)N * H * W * (C / 8), C / 8, W, H));

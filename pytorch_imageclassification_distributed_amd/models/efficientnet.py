@@ -95,12 +95,16 @@ class MBConvBlock(nn.Module):
     def forward(self, inputs, drop_connect_rate=None):
         a = self._block_args
         x = inputs
+        skip = self.id_skip and a.stride == 1 and a.input_filters == a.output_filters
+        # exclusive_input: the conv is the tensor's only consumer, so (HIP path) its data-gradient kernel
+        # can run the backward reduce of the BN that produced the tensor (the block input feeds the skip
+        # connection too when ``skip``)
         if a.expand_ratio != 1:
-            x = Fx.conv_bn_act(x, self._expand_conv, self._bn0, "silu")
-        x = Fx.conv_bn_act(x, self._depthwise_conv, self._bn1, "silu")
+            x = Fx.conv_bn_act(x, self._expand_conv, self._bn0, "silu", exclusive_input=not skip)
+        x = Fx.conv_bn_act(x, self._depthwise_conv, self._bn1, "silu",
+                           exclusive_input=a.expand_ratio != 1 or not skip)
         if self.has_se:
             x = Fx.se_gate(x, self._se_reduce, self._se_expand)
-        skip = self.id_skip and a.stride == 1 and a.input_filters == a.output_filters
         if skip and not (drop_connect_rate and self.training):
             return Fx.conv_bn_act(x, self._project_conv, self._bn2, None, residual=inputs)
         x = Fx.conv_bn_act(x, self._project_conv, self._bn2, None)

@@ -857,7 +857,7 @@ def _syncbn_bwd_start(link):
     dgamma = grad_buffer(link.params[0], zero=False)
     dbeta = grad_buffer(link.params[1], zero=False)
     sums = torch.empty(2 * c, dtype=torch.float64, device=link.y.device)
-    C.bn_partials(link.part, stat_groups(link.rows), c, sums, dgamma, dbeta)
+    C.bn_partials(link.part, link.part_rows(), c, sums, dgamma, dbeta)
     work = stats_all_reduce_async(sums, link.group)
     link.pending = (sums, work, dgamma, dbeta)
     SYNCBN_EARLY_COUNT[0] += 1
@@ -867,7 +867,7 @@ class BwdLink:
     """Ties a BN(+act) output to the conv that consumes it, so the consumer's dgrad epilogue can run
     the producer's BN-backward reduce (``done`` tells the producer its gradient arrives as dz)."""
 
-    __slots__ = ("y", "coef", "res", "act", "part", "done", "group", "params", "pending", "c", "rows")
+    __slots__ = ("y", "coef", "res", "act", "part", "done", "group", "params", "pending", "c", "rows", "groups")
 
     def __init__(self):
         self.y = self.coef = self.res = self.part = None
@@ -875,6 +875,10 @@ class BwdLink:
         self.done = False
         self.group = self.params = self.pending = None  # SyncBN: early backward all-reduce
         self.c = self.rows = 0
+        self.groups = 0  # partial rows in ``part`` (0: stat_groups(rows), the GEMM epilogue's rotating rows)
+
+    def part_rows(self) -> int:
+        return self.groups or stat_groups(self.rows)
 
 
 class ConvFn(torch.autograd.Function):
@@ -1017,12 +1021,16 @@ class StemS2dFn(torch.autograd.Function):
 # ---------------------------------------------------------------------------
 class DwConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, conv):
+    def forward(ctx, x, w, conv, fuse_bwd=False):
         g = ConvGeom(x, conv)
         wt = weight_bf16_t(w, g.Co, g.T, 1)
         y = _empty_cl(g.N, g.Co, g.OH, g.OW, x.device)
         C.dw_fwd(x, wt, y, None, g.N, g.H, g.W, g.Co, g.OH, g.OW, g.kh, g.kw, g.sh, g.sw, g.pt, g.pl)
         ctx.g = g
+        # producer BN of x (this conv its only consumer): its backward reduce rides in the dgrad kernel
+        link = getattr(x, "_imgcls_link", None) if fuse_bwd else None
+        ctx.link = link if (link is not None and link.y is not None and link.res is None
+                            and C.dw_dgrad_link_ok(g.kh, g.kw, g.sh, g.sw, g.pt, g.pl)) else None
         ctx.save_for_backward(x, w, wt)
         return y
 
@@ -1034,12 +1042,25 @@ class DwConvFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = _empty_cl(g.N, g.Co, g.H, g.W, x.device)
-            C.dw_dgrad(dy, wt, dx, g.N, g.H, g.W, g.Co, g.OH, g.OW, g.kh, g.kw, g.sh, g.sw, g.pt, g.pl)
+            link = ctx.link
+            if link is not None and not link.done:
+                grp = stat_groups(g.N * g.H * g.W)
+                if DETERMINISTIC:  # one partial row per block: every address gets one contribution
+                    grp = max(grp, C.dw_dgrad_link_blocks(g.N, g.H, g.W, g.Co, g.OH, g.OW, g.kh, g.sh))
+                link.part = ws(dx.device).take_part(g.Co, grp)
+                link.groups = grp
+                C.dw_dgrad(dy, wt, dx, g.N, g.H, g.W, g.Co, g.OH, g.OW, g.kh, g.kw, g.sh, g.sw, g.pt, g.pl,
+                           link.y, link.coef, link.part, grp, link.act)
+                link.done = True  # dx holds dz; the producer BN skips its reduce
+                if link.group is not None:
+                    _syncbn_bwd_start(link)
+            else:
+                C.dw_dgrad(dy, wt, dx, g.N, g.H, g.W, g.Co, g.OH, g.OW, g.kh, g.kw, g.sh, g.sw, g.pt, g.pl)
         dw = None
         if ctx.needs_input_grad[1]:
-            dw = grad_buffer(w)
+            dw = grad_buffer(w, zero=False)  # dw_wgrad overwrites it (ordered column sum of partial rows)
             C.dw_wgrad(dy, x, dw, g.N, g.H, g.W, g.Co, g.OH, g.OW, g.kh, g.kw, g.sh, g.sw, g.pt, g.pl)
-        return dx, dw, None
+        return dx, dw, None, None
 
 
 # ---------------------------------------------------------------------------
@@ -1146,6 +1167,7 @@ class BNActFn(torch.autograd.Function):
         if link is not None and link.done:
             # the consuming conv's dgrad epilogue already produced dz and the partial sums
             part, dz = link.part, g
+            grp = link.part_rows()
             FUSED_BWD_COUNT[0] += 1
             pending = link.pending
             link.y = link.coef = link.res = link.part = link.pending = link.params = None
@@ -1317,7 +1339,7 @@ def conv_bn_act(x, conv, bn, act, residual, x_slot=None, res_slot=None, exclusiv
     if depthwise:
         if not (conv.groups == conv.in_channels == conv.out_channels):
             raise NotImplementedError("grouped (non-depthwise) convolution")
-        y = DwConvFn.apply(x, conv.weight, conv)
+        y = DwConvFn.apply(x, conv.weight, conv, exclusive_input and FUSE_BN_BWD and DW_LINK)
         ready = False
     elif dense_conv_eligible(x, conv) and x.shape[2] * x.shape[3] > 1:
         y = DenseConvFn.apply(x, conv.weight, conv)
@@ -1757,7 +1779,17 @@ def drop_connect(x, p):
     return ScaleRowsFn.apply(_cl(x), scale)
 
 
+# depthwise dgrad runs its producer BN's backward reduce: measured 0.6 % slower on EfficientNet-B0 (the extra
+# y loads and coefficients lift the row-strip kernels to 2 waves per SIMD), so opt-in
+DW_LINK = os.environ.get("IMGCLS_DW_LINK", "0") == "1"
+SE_FUSED = os.environ.get("IMGCLS_SE_FUSED", "1") == "1"  # csrc/se.hip MLP kernels (0: GEMM + activation launches)
+
+
 class SEFn(torch.autograd.Function):
+    """Squeeze-excitation gate y = x * sigmoid(W_e silu(W_r mean_hw(x) + b_r) + b_e) (efficientnet_pytorch
+    MBConvBlock).  Fused path: spatial mean -> one MLP kernel -> scale (forward); spatial dot -> per-image
+    MLP backward -> weight gradients -> dx (backward)."""
+
     @staticmethod
     def forward(ctx, x, wr, br, we, be):
         n, c, h, w = x.shape
@@ -1766,19 +1798,26 @@ class SEFn(torch.autograd.Function):
         wr2, we2 = wr.reshape(nsq, c).contiguous(), we.reshape(c, nsq).contiguous()
         p = torch.empty((n, c), dtype=torch.float32, device=x.device)
         C.gap_fwd(x, p, n, hw, c)
+        fused = SE_FUSED and br is not None and be is not None and nsq <= 160
         hpre = torch.empty((n, nsq), dtype=torch.float32, device=x.device)
-        _mm(p, wr2, hpre, n, nsq, c, c, 1, 1, c, bias=br)
-        a = torch.empty_like(hpre)
-        C.act32_fwd(hpre, a, 0)
-        e = torch.empty((n, c), dtype=torch.float32, device=x.device)
-        _mm(a, we2, e, n, c, nsq, nsq, 1, 1, nsq, bias=be)
-        s = torch.empty_like(e)
-        C.act32_fwd(e, s, 1)
+        s = torch.empty((n, c), dtype=torch.float32, device=x.device)
+        if fused:
+            we2 = we2.t().contiguous()  # W_e^T [nsq][C]: channel-contiguous weight reads in both kernels
+            C.se_mlp_fwd(p, wr2, br.contiguous(), we2, be.contiguous(), hpre, s, n, c, nsq)
+            a = hpre  # (unused by the fused backward, which recomputes silu(h))
+        else:
+            _mm(p, wr2, hpre, n, nsq, c, c, 1, 1, c, bias=br)
+            a = torch.empty_like(hpre)
+            C.act32_fwd(hpre, a, 0)
+            e = torch.empty((n, c), dtype=torch.float32, device=x.device)
+            _mm(a, we2, e, n, c, nsq, nsq, 1, 1, nsq, bias=be)
+            C.act32_fwd(e, s, 1)
         y = torch.empty_like(x, memory_format=CL)
         C.se_scale(x, s, y, n, hw, c)
         ctx.save_for_backward(x, p, hpre, a, s, wr2, we2)
         ctx.geo = (n, c, hw, nsq)
         ctx.params = (wr, br, we, be)
+        ctx.fused = fused
         return y
 
     @staticmethod
@@ -1789,23 +1828,28 @@ class SEFn(torch.autograd.Function):
         dev = dy.device
         ds = torch.empty((n, c), dtype=torch.float32, device=dev)
         C.se_ds(dy, x, ds, n, hw, c)
-        de = torch.empty_like(ds)
-        C.act32_bwd(s, ds, de, 2)
         wr, br, we, be = ctx.params
         dwe = grad_buffer(we, zero=False)  # [c][nsq](1x1) in memory for either weight layout
-        _mm(de, a, dwe, c, nsq, n, 1, c, nsq, 1)
         dbe = grad_buffer(be, zero=False)
-        C.colsum(de, None, dbe, n, c, c, False)
-        da = torch.empty((n, nsq), dtype=torch.float32, device=dev)
-        _mm(de, we2, da, n, nsq, c, c, 1, nsq, 1)
-        dh = torch.empty_like(da)
-        C.act32_bwd(hpre, da, dh, 0)
         dwr = grad_buffer(wr, zero=False)
-        _mm(dh, p, dwr, nsq, c, n, 1, nsq, c, 1)
         dbr = grad_buffer(br, zero=False)
-        C.colsum(dh, None, dbr, n, nsq, nsq, False)
         dp = torch.empty((n, c), dtype=torch.float32, device=dev)
-        _mm(dh, wr2, dp, n, c, nsq, nsq, 1, c, 1)
+        if ctx.fused:
+            de = torch.empty_like(ds)
+            dh = torch.empty((n, nsq), dtype=torch.float32, device=dev)
+            C.se_mlp_bwd(ds, s, hpre, p, wr2, we2, de, dh, dp, dwr, dbr, dwe, dbe, n, c, nsq)
+        else:
+            de = torch.empty_like(ds)
+            C.act32_bwd(s, ds, de, 2)
+            _mm(de, a, dwe, c, nsq, n, 1, c, nsq, 1)
+            C.colsum(de, None, dbe, n, c, c, False)
+            da = torch.empty((n, nsq), dtype=torch.float32, device=dev)
+            _mm(de, we2, da, n, nsq, c, c, 1, nsq, 1)
+            dh = torch.empty_like(da)
+            C.act32_bwd(hpre, da, dh, 0)
+            _mm(dh, p, dwr, nsq, c, n, 1, nsq, c, 1)
+            C.colsum(dh, None, dbr, n, nsq, nsq, False)
+            _mm(dh, wr2, dp, n, c, nsq, nsq, 1, c, 1)
         dx = torch.empty_like(dy, memory_format=CL)
         C.se_dx(dy, s, dp, dx, n, hw, c)
         return dx, dwr, dbr, dwe, dbe

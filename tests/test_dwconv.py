@@ -69,3 +69,58 @@ def test_depthwise_fwd_dgrad_wgrad(case, rowstrip):
     assert rel(y, yr) < 1e-2, ("fwd", rel(y, yr))
     assert rel(dx, xr.grad) < 1e-2, ("dgrad", rel(dx, xr.grad))
     assert rel(dw, wr.grad) < 1e-4, ("wgrad", rel(dw, wr.grad))
+
+
+@pytest.mark.parametrize("k,s,hw,c", [(3, 1, 14, 96), (5, 2, 15, 40), (3, 2, 16, 144), (5, 1, 7, 672)])
+def test_depthwise_fused_bn_backward(k, s, hw, c):
+    """1x1 conv -> BN -> SiLU -> depthwise (exclusive consumer) -> BN -> SiLU: the depthwise data-gradient
+    kernel emits dz and the first BN's backward partial sums (BwdLink); gradients match fp32 autograd and
+    the unfused path."""
+    import torch.nn as nn
+    from pytorch_imageclassification_distributed_amd.ops import hip
+    from pytorch_imageclassification_distributed_amd.ops.functional import conv_padding
+    torch.manual_seed(k * 100 + c)
+    cin = 32
+    pw = nn.Conv2d(cin, c, 1, bias=False).to(DEV).to(memory_format=CL)
+    bn0 = nn.BatchNorm2d(c, eps=1e-3).to(DEV)
+    dw = nn.Conv2d(c, c, k, s, 0, groups=c, bias=False).to(DEV).to(memory_format=CL)
+    dw.tf_same = True
+    bn1 = nn.BatchNorm2d(c, eps=1e-3).to(DEV)
+    with torch.no_grad():
+        pw.weight.copy_(bf(pw.weight))
+        dw.weight.copy_(bf(dw.weight))
+        bn0.weight.uniform_(0.5, 1.5)
+        bn0.bias.uniform_(-0.5, 0.5)
+    x = bf(torch.randn(4, cin, hw, hw, device=DEV))
+    g = None
+    grads = {}
+    keep = hip.DW_LINK
+    hip.DW_LINK = True  # opt-in in the trainer (measured slower on EfficientNet-B0); tested here
+    for fused in (True, False):
+        for m in (pw, bn0, dw, bn1):
+            for p_ in m.parameters():
+                p_.grad = None
+        xb = x.to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
+        before = hip.FUSED_BWD_COUNT[0]
+        a = hip.conv_bn_act(xb, pw, bn0, "silu", None)
+        out = hip.conv_bn_act(a, dw, bn1, "silu", None, exclusive_input=fused)
+        if g is None:
+            g = bf(torch.randn(out.shape, device=DEV))
+        out.backward(g.to(torch.bfloat16).contiguous(memory_format=CL))
+        torch.cuda.synchronize()
+        assert (hip.FUSED_BWD_COUNT[0] > before) == fused
+        grads[fused] = [xb.grad.float()] + [p_.grad.float().clone() for m in (pw, bn0, dw, bn1) for p_ in m.parameters()]
+    hip.DW_LINK = keep
+    # fp32 reference
+    xr = x.clone().requires_grad_(True)
+    ps = [p_.detach().clone().requires_grad_(True) for m in (pw, bn0, dw, bn1) for p_ in m.parameters()]
+    pt, pb, pl, pr = conv_padding(dw, hw, hw)
+    z0 = F.conv2d(xr, ps[0])
+    a0 = F.silu(F.batch_norm(z0, None, None, ps[1], ps[2], training=True, eps=1e-3))
+    z1 = F.conv2d(F.pad(a0, (pl, pr, pt, pb)), ps[3], None, s, 0, 1, c)
+    ref = F.silu(F.batch_norm(z1, None, None, ps[4], ps[5], training=True, eps=1e-3))
+    ref.backward(g)
+    refs = [xr.grad] + [p_.grad for p_ in ps]
+    for i, r in enumerate(refs):
+        assert rel(grads[True][i], r) < 3e-2, (i, rel(grads[True][i], r))
+        assert rel(grads[True][i], grads[False][i]) < 3e-2, (i, rel(grads[True][i], grads[False][i]))

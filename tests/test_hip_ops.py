@@ -875,3 +875,40 @@ def test_bn_apply_emits_mx_copy():
     assert torch.equal(qs, qs2)
     assert torch.equal(q.view(torch.uint8), q2.view(torch.uint8))
 
+
+
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("n,c,nsq,hw", [(2, 96, 4, 9), (40, 144, 6, 7), (3, 1152, 48, 5), (33, 240, 10, 4),
+                                        (5, 2560, 160, 2)])
+def test_se_gate_fused_grads(n, c, nsq, hw, fused):
+    """SE MLP (csrc/se.hip fused kernels and the GEMM/activation fallback) against fp32 autograd: output,
+    input gradient and all four weight / bias gradients; batches above the 32-image LDS chunk and hidden
+    sizes that are not multiples of 4."""
+    hip = _hip()
+    torch.manual_seed(n * 7 + c)
+    red = nn.Conv2d(c, nsq, 1).to(DEV)
+    exp = nn.Conv2d(nsq, c, 1).to(DEV)
+    x = bf(torch.randn(n, c, hw, hw, device=DEV))
+    xb = x.to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
+    keep = hip.SE_FUSED
+    hip.SE_FUSED = fused
+    try:
+        y = hip.se_gate(xb, red, exp)
+        g = bf(torch.randn_like(y.float()))
+        y.backward(g.to(torch.bfloat16).contiguous(memory_format=CL))
+        torch.cuda.synchronize()
+    finally:
+        hip.SE_FUSED = keep
+    xr = x.clone().requires_grad_(True)
+    wr = red.weight.detach().clone().requires_grad_(True)
+    br = red.bias.detach().clone().requires_grad_(True)
+    we = exp.weight.detach().clone().requires_grad_(True)
+    be = exp.bias.detach().clone().requires_grad_(True)
+    hid = F.silu(F.linear(xr.mean((2, 3)), wr.flatten(1), br))
+    yr = torch.sigmoid(F.linear(hid, we.flatten(1), be))[:, :, None, None] * xr
+    yr.backward(g)
+    assert rel_err(y, yr) < 1e-2
+    assert rel_err(xb.grad, xr.grad) < 2e-2
+    for mine, ref in ((red.weight.grad, wr.grad), (red.bias.grad, br.grad), (exp.weight.grad, we.grad),
+                      (exp.bias.grad, be.grad)):
+        assert rel_err(mine.reshape(ref.shape), ref) < 2e-2
