@@ -76,6 +76,7 @@ int dw_dgrad_launch(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, i
                     int, const bf16_t*, const float*, float*, int, int, hipStream_t);
 bool dw_dgrad_link_ok(int, int, int, int, int, int);
 int dw_dgrad_link_blocks(int, int, int, int, int, int, int, int);
+int se_dx_link_blocks(int, int, int);
 int dw_wgrad_launch(const bf16_t*, const bf16_t*, float*, int, int, int, int, int, int, int, int, int, int, int,
                     int, float*, hipStream_t);
 long dw_wgrad_partial_rows(int, int, int, int, int, int, int);
@@ -84,7 +85,8 @@ void set_deterministic(int);
 void set_force_div64(int);
 int se_scale_launch(const bf16_t*, const float*, bf16_t*, int, int, int, hipStream_t);
 int se_ds_launch(const bf16_t*, const bf16_t*, float*, int, int, int, hipStream_t);
-int se_dx_launch(const bf16_t*, const float*, const float*, bf16_t*, int, int, int, hipStream_t);
+int se_dx_launch(const bf16_t*, const float*, const float*, bf16_t*, int, int, int, const bf16_t*, const float*, float*,
+                 int, int, hipStream_t);
 int act32_fwd_launch(const float*, float*, long, int, hipStream_t);
 int act32_bwd_launch(const float*, const float*, float*, long, int, hipStream_t);
 int bn_stats_launch(const bf16_t*, long, int, float*, int, hipStream_t);
@@ -584,8 +586,15 @@ void se_ds(Tensor dy, Tensor x, Tensor ds, int N, int HW, int C) {
   check(se_ds_launch(ptr<bf16_t>(dy), ptr<bf16_t>(x), ptr<float>(ds), N, HW, C, cur()), "se_ds");
 }
 
-void se_dx(Tensor dy, Tensor s, Tensor dp, Tensor dx, int N, int HW, int C) {
-  check(se_dx_launch(ptr<bf16_t>(dy), ptr<float>(s), ptr<float>(dp), ptr<bf16_t>(dx), N, HW, C, cur()), "se_dx");
+// link_*: the SE input's producer BN backward reduce fused (dx receives dz), as dw_dgrad
+void se_dx(Tensor dy, Tensor s, Tensor dp, Tensor dx, int N, int HW, int C, OT link_y, OT link_coef, OT link_part,
+           int G, int act) {
+  if (optr<bf16_t>(link_y))
+    TORCH_CHECK(link_y->numel() == dx.numel() && link_coef.has_value() && link_part.has_value() &&
+                link_coef->numel() >= 4L * C && link_part->numel() >= 2L * C * G, "se_dx: link tensors");
+  check(se_dx_launch(ptr<bf16_t>(dy), ptr<float>(s), ptr<float>(dp), ptr<bf16_t>(dx), N, HW, C, optr<bf16_t>(link_y),
+                     optr<float>(link_coef), optr<float>(link_part), G, act, cur()),
+        "se_dx");
 }
 
 void act32_fwd(Tensor x, Tensor y, int kind) {
@@ -800,11 +809,15 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("link_part") = pybind11::none(), pybind11::arg("G") = 1, pybind11::arg("act") = 0);
   m.def("dw_dgrad_link_ok", &dw_dgrad_link_ok);
   m.def("dw_dgrad_link_blocks", &dw_dgrad_link_blocks);
+  m.def("se_dx_link_blocks", &se_dx_link_blocks);
   m.def("dw_wgrad", &dw_wgrad);
   m.def("dw_set_rowstrip", [](bool v) { dw_set_rowstrip(v ? 1 : 0); });
   m.def("se_scale", &se_scale);
   m.def("se_ds", &se_ds);
-  m.def("se_dx", &se_dx);
+  m.def("se_dx", &se_dx, pybind11::arg("dy"), pybind11::arg("s"), pybind11::arg("dp"), pybind11::arg("dx"),
+        pybind11::arg("N"), pybind11::arg("HW"), pybind11::arg("C"), pybind11::arg("link_y") = pybind11::none(),
+        pybind11::arg("link_coef") = pybind11::none(), pybind11::arg("link_part") = pybind11::none(),
+        pybind11::arg("G") = 1, pybind11::arg("act") = 0);
   m.def("act32_fwd", &act32_fwd);
   m.def("act32_bwd", &act32_bwd);
   m.def("bn_stats", &bn_stats);

@@ -210,8 +210,13 @@ DEVI void link_flush(const DwLink& L, int C, const float* s8, const float* q8) {
       for (int k = 0; k < 16; ++k) v[k] += red[t][k];
     const int chunk = (int)(((long)blockIdx.x * 256 + tid) % cch);
     float* dst = L.part + (size_t)(blockIdx.x % L.G) * 2 * C + chunk * 8;
+    if (L.G >= (int)gridDim.x) {  // a row per block: plain stores (rows a block does not touch stay zero)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { atomicAdd(dst + k, v[k]); atomicAdd(dst + C + k, v[8 + k]); }
+      for (int k = 0; k < 8; ++k) { dst[k] = v[k]; dst[C + k] = v[8 + k]; }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { atomicAdd(dst + k, v[k]); atomicAdd(dst + C + k, v[8 + k]); }
+    }
   }
 }
 
@@ -583,6 +588,62 @@ __global__ void se_dx_kernel(const bf16_t* __restrict__ dy, const float* __restr
   }
 }
 
+// se_dx with the SE input's producer BN backward reduce fused (x = act(BN(y)), the SE gate its only
+// consumer): dz = act'(z) * (dy * s + dp / HW) is written instead of dx, and sum dz, sum dz * xhat per
+// channel go into the link's partial rows.  Channel-fixed lanes (grid stride a multiple of C/8).
+__global__ __launch_bounds__(256) void se_dx_link_kernel(const bf16_t* __restrict__ dy, const float* __restrict__ s,
+                                                         const float* __restrict__ dp, bf16_t* __restrict__ dx,
+                                                         int N, int HW, int C, FastDiv fhw, DwLink L) {
+  const int cch = C >> 3;
+  const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const int rstride = (int)(((long)gridDim.x * blockDim.x) / cch);
+  const int c0 = (int)(t % cch) * 8;
+  const int rows = N * HW;
+  const float inv = 1.f / HW;
+  LinkCoef lk;
+  link_coef(L, C, lk);
+  float s8[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // 4 rows per iteration, every load issued before any use (a lane walks ~rows*C/8/threads rows; one
+  // dependent round trip per row left the kernel latency-bound)
+  constexpr int U = 4;
+  for (int row = (int)(t / cch); row < rows; row += U * rstride) {
+    uint4 dr[U], yr[U];
+    float4 sa[U], sb[U], pa[U], pb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = row + u * rstride < rows ? row + u * rstride : row;
+      const int n = (int)fdiv((uint32_t)r, fhw);
+      dr[u] = *(const uint4*)(dy + (long)r * C + c0);
+      yr[u] = *(const uint4*)(L.y + (long)r * C + c0);
+      sa[u] = *(const float4*)(s + (long)n * C + c0);
+      sb[u] = *(const float4*)(s + (long)n * C + c0 + 4);
+      pa[u] = *(const float4*)(dp + (long)n * C + c0);
+      pb[u] = *(const float4*)(dp + (long)n * C + c0 + 4);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (row + u * rstride >= rows) break;
+      float v[8], yv[8];
+      unpack8(dr[u], v);
+      unpack8(yr[u], yv);
+      const float* sv = (const float*)&sa[u];
+      const float* sw = (const float*)&sb[u];
+      const float* pv = (const float*)&pa[u];
+      const float* pw = (const float*)&pb[u];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float g = v[k] * (k < 4 ? sv[k] : sw[k - 4]) + (k < 4 ? pv[k] : pw[k - 4]) * inv;
+        const float dz = act_grad(yv[k] * lk.sc[k] + lk.sh[k], g, L.act);
+        v[k] = dz;
+        s8[k] += dz;
+        q8[k] += dz * (yv[k] - lk.mu[k]) * lk.is[k];
+      }
+      *(uint4*)(dx + (long)(row + u * rstride) * C + c0) = pack8(v);
+    }
+  }
+  link_flush(L, C, s8, q8);
+}
+
 // fp32 activations for the SE MLP: 0 = silu, 1 = sigmoid
 __global__ void act32_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, long n, int kind) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
@@ -795,8 +856,29 @@ int se_ds_launch(const bf16_t* dy, const bf16_t* x, float* ds, int N, int HW, in
   return spatial_reduce_launch<true>(dy, x, ds, N, HW, C, 1.f, s);
 }
 
+// blocks of a linked se_dx launch (<= ~1024; a multiple of C/8 / gcd(C/8, 256) so lanes keep one channel
+// chunk): the caller gives the link that many partial rows and every block stores its own row
+int se_dx_link_blocks(int N, int HW, int C) {
+  const int cch = C / 8;
+  if (cch <= 0) return 1;
+  int gcd = cch, m = 256;
+  while (m) { const int t = gcd % m; gcd = m; m = t; }
+  const int unit = cch / gcd;
+  const int b = grid_for((long)N * HW * cch, 1024);
+  return (b + unit - 1) / unit * unit;
+}
+
 int se_dx_launch(const bf16_t* dy, const float* sc, const float* dp, bf16_t* dx, int N, int HW, int C,
-                 hipStream_t s) {
+                 const bf16_t* ly, const float* lcoef, float* lpart, int lG, int lact, hipStream_t s) {
+  if ((long)N * HW * (C / 8) <= 0) return 0;
+  if (ly != nullptr) {
+    if ((long)N * HW >= (1L << 31)) return 2;
+    const int b = se_dx_link_blocks(N, HW, C);
+    hipLaunchKernelGGL(se_dx_link_kernel, dim3(b), dim3(256), 0, s, dy, sc, dp, dx, N, HW, C, make_fastdiv(HW),
+                       DwLink{ly, lcoef, lpart, lG > 0 ? lG : 1, lact});
+    HIP_CHECK_LAUNCH();
+    return 0;
+  }
   hipLaunchKernelGGL(se_dx_kernel, dim3(grid_for((long)N * HW * (C / 8))), dim3(256), 0, s, dy, sc, dp, dx, N, HW, C,
                      make_pixidx((long)N * HW * (C / 8), C / 8, HW, N));
   HIP_CHECK_LAUNCH();

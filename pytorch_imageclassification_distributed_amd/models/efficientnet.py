@@ -104,7 +104,7 @@ class MBConvBlock(nn.Module):
         x = Fx.conv_bn_act(x, self._depthwise_conv, self._bn1, "silu",
                            exclusive_input=a.expand_ratio != 1 or not skip)
         if self.has_se:
-            x = Fx.se_gate(x, self._se_reduce, self._se_expand)
+            x = Fx.se_gate(x, self._se_reduce, self._se_expand, exclusive_input=True)
         if skip and not (drop_connect_rate and self.training):
             return Fx.conv_bn_act(x, self._project_conv, self._bn2, None, residual=inputs)
         x = Fx.conv_bn_act(x, self._project_conv, self._bn2, None)

@@ -227,10 +227,11 @@ def add(x, y):
     return x + y
 
 
-def se_gate(x, se_reduce, se_expand):
-    """Squeeze-and-excitation: x * sigmoid(expand(swish(reduce(avgpool(x)))))."""
+def se_gate(x, se_reduce, se_expand, exclusive_input=False):
+    """Squeeze-and-excitation: x * sigmoid(expand(swish(reduce(avgpool(x))))).  ``exclusive_input``: the gate
+    is x's only consumer (HIP path: its backward runs the backward reduce of the BN that produced x)."""
     if use_hip(x):
-        return _hip().se_gate(x, se_reduce, se_expand)
+        return _hip().se_gate(x, se_reduce, se_expand, exclusive_input)
     s = F.adaptive_avg_pool2d(x, 1)
     s = se_expand(F.silu(se_reduce(s)))
     return torch.sigmoid(s) * x

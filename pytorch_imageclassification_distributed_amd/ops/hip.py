@@ -1791,9 +1791,12 @@ class SEFn(torch.autograd.Function):
     MLP backward -> weight gradients -> dx (backward)."""
 
     @staticmethod
-    def forward(ctx, x, wr, br, we, be):
+    def forward(ctx, x, wr, br, we, be, fuse_bwd=False):
         n, c, h, w = x.shape
         hw = h * w
+        # producer BN of x (the gate is x's only consumer): its backward reduce rides in se_dx
+        link = getattr(x, "_imgcls_link", None) if fuse_bwd else None
+        ctx.link = link if (link is not None and link.y is not None and link.res is None) else None
         nsq = wr.shape[0]
         wr2, we2 = wr.reshape(nsq, c).contiguous(), we.reshape(c, nsq).contiguous()
         p = torch.empty((n, c), dtype=torch.float32, device=x.device)
@@ -1851,12 +1854,28 @@ class SEFn(torch.autograd.Function):
             C.colsum(dh, None, dbr, n, nsq, nsq, False)
             _mm(dh, wr2, dp, n, c, nsq, nsq, 1, c, 1)
         dx = torch.empty_like(dy, memory_format=CL)
-        C.se_dx(dy, s, dp, dx, n, hw, c)
-        return dx, dwr, dbr, dwe, dbe
+        link = ctx.link
+        if link is not None and not link.done:
+            grp = C.se_dx_link_blocks(n, hw, c)  # one partial row per block, plain stores (no atomics)
+            link.part = ws(dev).take_part(c, grp)
+            link.groups = grp
+            C.se_dx(dy, s, dp, dx, n, hw, c, link.y, link.coef, link.part, grp, link.act)
+            link.done = True  # dx holds dz; the producer BN skips its reduce
+            if link.group is not None:
+                _syncbn_bwd_start(link)
+        else:
+            C.se_dx(dy, s, dp, dx, n, hw, c)
+        return dx, dwr, dbr, dwe, dbe, None
 
 
-def se_gate(x, se_reduce, se_expand):
-    return SEFn.apply(_cl(x), se_reduce.weight, se_reduce.bias, se_expand.weight, se_expand.bias)
+SE_LINK = os.environ.get("IMGCLS_SE_LINK", "1") == "1"  # se_dx runs the gate input's producer BN backward reduce
+
+
+def se_gate(x, se_reduce, se_expand, exclusive_input=False):
+    """``exclusive_input``: the gate is x's only consumer (x = act(BN(y)) in an MBConv block), so its
+    backward may emit dz and the producer BN's partial sums."""
+    return SEFn.apply(_cl(x), se_reduce.weight, se_reduce.bias, se_expand.weight, se_expand.bias,
+                      exclusive_input and FUSE_BN_BWD and SE_LINK)
 
 
 # ---------------------------------------------------------------------------

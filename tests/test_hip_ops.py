@@ -912,3 +912,41 @@ def test_se_gate_fused_grads(n, c, nsq, hw, fused):
     for mine, ref in ((red.weight.grad, wr.grad), (red.bias.grad, br.grad), (exp.weight.grad, we.grad),
                       (exp.bias.grad, be.grad)):
         assert rel_err(mine.reshape(ref.shape), ref) < 2e-2
+
+
+@pytest.mark.parametrize("n,c,hw", [(4, 96, 14), (3, 1152, 7), (2, 2064, 5)])
+def test_se_gate_fused_bn_backward(n, c, hw):
+    """BN -> SiLU -> SE gate (exclusive consumer): se_dx emits dz and the BN's backward partial sums (BwdLink);
+    gradients of the input and of every parameter match fp32 autograd."""
+    hip = _hip()
+    torch.manual_seed(c)
+    nsq = max(1, c // 24)
+    conv = nn.Conv2d(c, c, 1, bias=False).to(DEV).to(memory_format=CL)
+    bn = nn.BatchNorm2d(c, eps=1e-3).to(DEV)
+    red = nn.Conv2d(c, nsq, 1).to(DEV)
+    exp = nn.Conv2d(nsq, c, 1).to(DEV)
+    with torch.no_grad():
+        conv.weight.copy_(bf(conv.weight))
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    x = bf(torch.randn(n, c, hw, hw, device=DEV))
+    xb = x.to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
+    before = hip.FUSED_BWD_COUNT[0]
+    a = hip.conv_bn_act(xb, conv, bn, "silu", None)
+    y = hip.se_gate(a, red, exp, exclusive_input=True)
+    g = bf(torch.randn(y.shape, device=DEV))
+    y.backward(g.to(torch.bfloat16).contiguous(memory_format=CL))
+    torch.cuda.synchronize()
+    assert hip.FUSED_BWD_COUNT[0] > before
+    xr = x.clone().requires_grad_(True)
+    ps = [p_.detach().clone().requires_grad_(True) for m in (conv, bn, red, exp) for p_ in m.parameters()]
+    z = F.batch_norm(F.conv2d(xr, ps[0]), None, None, ps[1], ps[2], training=True, eps=1e-3)
+    ar = F.silu(z)
+    hid = F.silu(F.linear(ar.mean((2, 3)), ps[3].flatten(1), ps[4]))
+    yr = torch.sigmoid(F.linear(hid, ps[5].flatten(1), ps[6]))[:, :, None, None] * ar
+    yr.backward(g)
+    assert rel_err(y, yr) < 2e-2
+    assert rel_err(xb.grad, xr.grad) < 3e-2
+    mine = [p_.grad for m in (conv, bn, red, exp) for p_ in m.parameters()]
+    for i, (m_, r_) in enumerate(zip(mine, ps)):
+        assert rel_err(m_.reshape(r_.grad.shape), r_.grad) < 3e-2, i
