@@ -104,6 +104,10 @@ int peer_ipc_open(const char*, void**);
 int peer_ipc_close(void*);
 int peer_allreduce_f64_launch(const double*, double*, int, const unsigned long long*, int, int, unsigned long long,
                               unsigned long long, int*, hipStream_t);
+int peer_bn_max_channels();
+int peer_bn_launch(bool, float*, int, int, double, const float*, const float*, float*, float*, long long*, float, float,
+                   float*, float*, float*, double*, const unsigned long long*, int, int, unsigned long long,
+                   unsigned long long, int*, hipStream_t);
 
 namespace {
 
@@ -686,6 +690,28 @@ class PeerComm {
           "peer_allreduce_f64");
   }
 
+  // SyncBN forward, exchange fused: partial rows -> coef [4][C], running stats, total count (count_out)
+  void bn_fwd(Tensor part, int G, int C, double count, OT gamma, OT beta, OT rmean, OT rvar, OT nbt, double momentum,
+              double eps, Tensor coef, Tensor count_out) {
+    req(part, F32, "part");
+    req(coef, F32, "coef");
+    req(count_out, at::kDouble, "count_out");
+    TORCH_CHECK(part.numel() >= 2L * G * C && coef.numel() >= 4L * C, "PeerComm.bn_fwd: sizes");
+    launch_bn(true, part, G, C, count, optr<float>(gamma), optr<float>(beta), optr<float>(rmean), optr<float>(rvar),
+              optr<long long>(nbt), (float)momentum, (float)eps, ptr<float>(coef), nullptr, nullptr,
+              ptr<double>(count_out));
+  }
+
+  // SyncBN backward, exchange fused: partial rows -> k [2][C] (global sums / total count), local dgamma / dbeta
+  void bn_bwd(Tensor part, int G, int C, Tensor count_total, OT dgamma, OT dbeta, Tensor k) {
+    req(part, F32, "part");
+    req(k, F32, "k");
+    req(count_total, at::kDouble, "count_total");
+    TORCH_CHECK(part.numel() >= 2L * G * C && k.numel() >= 2L * C, "PeerComm.bn_bwd: sizes");
+    launch_bn(false, part, G, C, 0.0, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, ptr<float>(k),
+              optr<float>(dgamma), optr<float>(dbeta), ptr<double>(count_total));
+  }
+
   int error() {
     int v = 0;
     check((int)hipMemcpy(&v, err_, sizeof(int), hipMemcpyDeviceToHost), "peer err read");
@@ -703,6 +729,17 @@ class PeerComm {
   unsigned long long seq() const { return seq_; }
 
  private:
+  void launch_bn(bool fwd, Tensor& part, int G, int C, double count, const float* gamma, const float* beta,
+                 float* rmean, float* rvar, long long* nbt, float momentum, float eps, float* out, float* dgamma,
+                 float* dbeta, double* count_io) {
+    TORCH_CHECK(C <= peer_bn_max_channels(), "PeerComm: at most ", peer_bn_max_channels(), " BN channels");
+    for (int q = 0; q < world_; ++q) TORCH_CHECK(bases_[q] != 0ull, "PeerComm: peers not opened");
+    ++seq_;
+    check(peer_bn_launch(fwd, ptr<float>(part), G, C, count, gamma, beta, rmean, rvar, nbt, momentum, eps, out, dgamma,
+                         dbeta, count_io, bases_.data(), rank_, world_, seq_, timeout_ticks_, err_, cur()),
+          "peer_bn");
+  }
+
   int rank_, world_;
   void* buf_ = nullptr;
   int* err_ = nullptr;
@@ -829,9 +866,12 @@ PYBIND11_MODULE(_C, m) {
       .def("handle", &PeerComm::handle)
       .def("open", &PeerComm::open)
       .def("all_reduce_", &PeerComm::all_reduce_)
+      .def("bn_fwd", &PeerComm::bn_fwd)
+      .def("bn_bwd", &PeerComm::bn_bwd)
       .def("error", &PeerComm::error)
       .def("close", &PeerComm::close)
       .def_property_readonly("seq", &PeerComm::seq);
   m.attr("PEER_MAX_ELEMS") = peer_max_elems();
   m.attr("PEER_MAX_WORLD") = peer_max_world();
+  m.attr("PEER_BN_MAX_C") = peer_bn_max_channels();
 }

@@ -112,6 +112,129 @@ __global__ __launch_bounds__(kThreads) void peer_allreduce_f64_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// SyncBN with the exchange fused: one kernel per BN layer and direction replaces
+//   forward   bn_partials -> all-reduce [sum, sumsq, count] -> bn_finalize
+//   backward  bn_partials -> all-reduce [sum dz, sum dz*xhat] -> bn_bwd_k
+// Block g owns channels [256 g, 256 g + 256): it reduces those columns of the local partial rows (fp64,
+// rows re-zeroed for the next layer), pushes [sum, sumsq] (+ the local count) to every rank as the
+// generic kernel does, waits for the peers' chunk g, adds the W payloads in rank order and finishes the
+// layer's coefficients (forward: scale, shift, mean, invstd, running statistics, total count; backward:
+// k = sums / count and the local dgamma / dbeta).
+// ---------------------------------------------------------------------------
+constexpr int kBnCB = 256;      // channels per block
+constexpr int kBnStride = 520;  // doubles per block payload slot (2 * 256 + count)
+constexpr int kBnMaxBlocks = (int)kSlotDoubles / kBnStride;  // 31 blocks: C <= 7936
+static_assert(kBnMaxBlocks <= kMaxBlocks, "one flag per block");
+
+struct PeerBnArgs {
+  float* part;
+  int G, C;
+  double count;              // forward: this rank's element count per channel
+  const float* gamma;
+  const float* beta;
+  float* rmean;
+  float* rvar;
+  long long* nbt;
+  float momentum, eps;
+  float* out;                // forward: coef [4][C]; backward: k [2][C]
+  float* dgamma;             // backward: local sum dz * xhat
+  float* dbeta;              // backward: local sum dz
+  double* count_io;          // forward: total count (out); backward: total count (in)
+};
+
+template <bool FWD>
+__global__ __launch_bounds__(256) void peer_bn_kernel(PeerBnArgs a, PeerTable tab, int rank, int world,
+                                                      unsigned long long seq, unsigned long long timeout_ticks,
+                                                      int* __restrict__ err) {
+  const int g = blockIdx.x, t = threadIdx.x;
+  const int par = (int)(seq & 1ull);
+  const int C = a.C, c = g * kBnCB + t;
+  // 1) local column sums of the partial rows (re-zeroed)
+  double s = 0.0, q = 0.0;
+  if (c < C) {
+#pragma unroll 8
+    for (int r = 0; r < a.G; ++r) {
+      float* row = a.part + (size_t)r * 2 * C;
+      const float x = row[c], y = row[C + c];
+      row[c] = 0.f;
+      row[C + c] = 0.f;
+      s += (double)x;
+      q += (double)y;
+    }
+    if (!FWD) {
+      if (a.dbeta) a.dbeta[c] = (float)s;
+      if (a.dgamma) a.dgamma[c] = (float)q;
+    }
+  }
+  // 2) push [s, q] (+ count) into slot [par][rank], block g, of every rank
+  const size_t slot_off = kFlagBytes + (((size_t)par * kMaxWorld + rank) * kSlotDoubles + (size_t)g * kBnStride) * 8;
+  for (int p = 0; p < world; ++p) {
+    unsigned long long* dst = (unsigned long long*)(tab.base[p] + slot_off);
+    st_sys(dst + 2 * t, __double_as_longlong(s));
+    st_sys(dst + 2 * t + 1, __double_as_longlong(q));
+    if (t == 0) st_sys(dst + 2 * kBnCB, __double_as_longlong(a.count));
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t < world) {
+    unsigned long long* flag = (unsigned long long*)(tab.base[t] + ((size_t)g * kMaxWorld + rank) * 8);
+    st_sys(flag, seq);
+  }
+  // 3) wait for every rank's block g of this call
+  if (t < 64) {
+    const unsigned long long* mine = (const unsigned long long*)(tab.base[rank] + (size_t)g * kMaxWorld * 8);
+    bool done = t >= world;
+    const unsigned long long t0 = wall_clock64();
+    bool timed_out = false;
+    while (true) {
+      if (!done) done = ld_sys(mine + t) >= seq;
+      if (__all(done)) break;
+      if (wall_clock64() - t0 > timeout_ticks) { timed_out = true; break; }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (t == 0 && timed_out) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  // 4) rank-ordered sums, then the layer's coefficients for this block's channels
+  const unsigned long long* slots = (const unsigned long long*)(tab.base[rank] + kFlagBytes) +
+                                    (size_t)par * kMaxWorld * kSlotDoubles + (size_t)g * kBnStride;
+  double S = 0.0, Q = 0.0, n = 0.0;
+  for (int r = 0; r < world; ++r) {
+    const unsigned long long* sl = slots + (size_t)r * kSlotDoubles;
+    S += __longlong_as_double(ld_sys(sl + 2 * t));
+    Q += __longlong_as_double(ld_sys(sl + 2 * t + 1));
+    if (FWD) n += __longlong_as_double(ld_sys(sl + 2 * kBnCB));
+  }
+  if (FWD) {
+    if (g == 0 && t == 0) {
+      if (a.nbt) *a.nbt += 1;
+      if (a.count_io) *a.count_io = n;
+    }
+    if (c >= C) return;
+    const double mean = S / n;
+    double var = Q / n - mean * mean;
+    var = var < 0.0 ? 0.0 : var;
+    const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
+    const float gm = a.gamma ? a.gamma[c] : 1.f, bt = a.beta ? a.beta[c] : 0.f;
+    const float scale = gm * invstd;
+    a.out[c] = scale;
+    a.out[C + c] = bt - (float)mean * scale;
+    a.out[2 * C + c] = (float)mean;
+    a.out[3 * C + c] = invstd;
+    if (a.rmean) {
+      const double unb = n > 1.0 ? var * n / (n - 1.0) : var;
+      a.rmean[c] = (1.f - a.momentum) * a.rmean[c] + a.momentum * (float)mean;
+      a.rvar[c] = (1.f - a.momentum) * a.rvar[c] + a.momentum * (float)unb;
+    }
+  } else {
+    if (c >= C) return;
+    const double nn = *a.count_io;
+    a.out[c] = (float)(S / nn);
+    a.out[C + c] = (float)(Q / nn);
+  }
+}
+
 }  // namespace
 
 size_t peer_buffer_bytes() { return kBufBytes; }
@@ -155,5 +278,27 @@ int peer_allreduce_f64_launch(const double* in, double* out, int n, const unsign
   const int blocks = (n + kChunk - 1) / kChunk;
   hipLaunchKernelGGL(peer_allreduce_f64_kernel, dim3(blocks), dim3(kThreads), 0, st, in, out, n, tab, rank, world,
                      seq, timeout_ticks, err);
+  return (int)hipGetLastError();
+}
+
+int peer_bn_max_channels() { return kBnCB * kBnMaxBlocks; }
+
+int peer_bn_launch(bool fwd, float* part, int G, int C, double count, const float* gamma, const float* beta,
+                   float* rmean, float* rvar, long long* nbt, float momentum, float eps, float* out, float* dgamma,
+                   float* dbeta, double* count_io, const unsigned long long* bases, int rank, int world,
+                   unsigned long long seq, unsigned long long timeout_ticks, int* err, hipStream_t st) {
+  if (C <= 0) return 0;
+  if (world < 1 || world > kMaxWorld || rank < 0 || rank >= world || C > kBnCB * kBnMaxBlocks || G < 1)
+    return (int)hipErrorInvalidValue;
+  PeerTable tab;
+  for (int i = 0; i < kMaxWorld; ++i) tab.base[i] = i < world ? bases[i] : 0ull;
+  const PeerBnArgs a{part, G, C, count, gamma, beta, rmean, rvar, nbt, momentum, eps, out, dgamma, dbeta, count_io};
+  const int blocks = (C + kBnCB - 1) / kBnCB;
+  if (fwd)
+    hipLaunchKernelGGL(peer_bn_kernel<true>, dim3(blocks), dim3(256), 0, st, a, tab, rank, world, seq, timeout_ticks,
+                       err);
+  else
+    hipLaunchKernelGGL(peer_bn_kernel<false>, dim3(blocks), dim3(256), 0, st, a, tab, rank, world, seq, timeout_ticks,
+                       err);
   return (int)hipGetLastError();
 }

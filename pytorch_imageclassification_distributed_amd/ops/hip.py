@@ -23,6 +23,7 @@ import torch
 import torch.distributed as dist
 
 from .. import _ext
+from ..parallel.peer import PeerWork, peer_channel, side_stream as peer_side_stream
 from ..parallel.peer import stats_all_reduce_, stats_all_reduce_async
 from .grad_arena import arena_slot, grad_buffer
 
@@ -847,19 +848,36 @@ class GradSlot:
         return grad
 
 
+PEER_BN_MAX_C = int(getattr(C, "PEER_BN_MAX_C", 0))  # channels the fused SyncBN peer kernels handle
 SYNCBN_EARLY_COUNT = [0]  # SyncBN backward all-reduces launched from the consuming conv (tests)
 
 
 def _syncbn_bwd_start(link):
     """Reduce the fused partial rows to this rank's [sum dz, sum dz*xhat] (+ dgamma, dbeta) and launch
-    the async cross-rank all-reduce; ``BNActFn.backward`` waits on it (a stream wait, no host sync)."""
+    the async cross-rank all-reduce; ``BNActFn.backward`` waits on it (a stream wait, no host sync).
+    With the peer transport one side-stream kernel does the reduce, the exchange and k = sums / n."""
     c = link.c
+    dev = link.y.device
     dgamma = grad_buffer(link.params[0], zero=False)
     dbeta = grad_buffer(link.params[1], zero=False)
-    sums = torch.empty(2 * c, dtype=torch.float64, device=link.y.device)
-    C.bn_partials(link.part, link.part_rows(), c, sums, dgamma, dbeta)
-    work = stats_all_reduce_async(sums, link.group)
-    link.pending = (sums, work, dgamma, dbeta)
+    pc = peer_channel(link.group, 1)
+    if pc is not None and link.count_t is not None and c <= PEER_BN_MAX_C:
+        k = torch.empty(2 * c, dtype=torch.float32, device=dev)
+        cur = torch.cuda.current_stream(dev)
+        side = peer_side_stream(dev)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            pc.comm.bn_bwd(link.part, link.part_rows(), c, link.count_t, dgamma, dbeta, k)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        for t in (k, link.count_t, dgamma, dbeta):
+            t.record_stream(side)
+        link.pending = (None, PeerWork(ev), dgamma, dbeta, k)
+    else:
+        sums = torch.empty(2 * c, dtype=torch.float64, device=dev)
+        C.bn_partials(link.part, link.part_rows(), c, sums, dgamma, dbeta)
+        work = stats_all_reduce_async(sums, link.group)
+        link.pending = (sums, work, dgamma, dbeta, None)
     SYNCBN_EARLY_COUNT[0] += 1
 
 
@@ -867,7 +885,8 @@ class BwdLink:
     """Ties a BN(+act) output to the conv that consumes it, so the consumer's dgrad epilogue can run
     the producer's BN-backward reduce (``done`` tells the producer its gradient arrives as dz)."""
 
-    __slots__ = ("y", "coef", "res", "act", "part", "done", "group", "params", "pending", "c", "rows", "groups")
+    __slots__ = ("y", "coef", "res", "act", "part", "done", "group", "params", "pending", "c", "rows", "groups",
+                 "count_t")
 
     def __init__(self):
         self.y = self.coef = self.res = self.part = None
@@ -876,6 +895,7 @@ class BwdLink:
         self.group = self.params = self.pending = None  # SyncBN: early backward all-reduce
         self.c = self.rows = 0
         self.groups = 0  # partial rows in ``part`` (0: stat_groups(rows), the GEMM epilogue's rotating rows)
+        self.count_t = None  # SyncBN: all-reduced element count of the forward (fp64 device scalar)
 
     def part_rows(self) -> int:
         return self.groups or stat_groups(self.rows)
@@ -1086,11 +1106,16 @@ def _bn_coef(y, gamma, beta, bn, stats_ready):
         if group is None:  # one launch: partial rows -> coefficients + running stats
             C.bn_reduce_finalize(part, grp, c, float(rows), gamma, beta, *rs, mom, bn.eps, coef)
         else:
-            sums = torch.empty(2 * c + 1, dtype=torch.float64, device=dev)
-            C.bn_partials(part, grp, c, sums, None, None, float(rows))  # + local count in the tail
-            stats_all_reduce_(sums, group)
-            count_t = sums[2 * c:]
-            C.bn_finalize(sums, count_t, float(rows), gamma, beta, *rs, mom, bn.eps, c, coef)
+            pc = peer_channel(group, 0)
+            if pc is not None and c <= PEER_BN_MAX_C:  # one kernel: reduce + xGMI exchange + finalize
+                count_t = torch.empty(1, dtype=torch.float64, device=dev)
+                pc.comm.bn_fwd(part, grp, c, float(rows), gamma, beta, *rs, mom, bn.eps, coef, count_t)
+            else:
+                sums = torch.empty(2 * c + 1, dtype=torch.float64, device=dev)
+                C.bn_partials(part, grp, c, sums, None, None, float(rows))  # + local count in the tail
+                stats_all_reduce_(sums, group)
+                count_t = sums[2 * c:]
+                C.bn_finalize(sums, count_t, float(rows), gamma, beta, *rs, mom, bn.eps, c, coef)
     else:
         if stats_ready:
             raise RuntimeError("eval-mode BN received fused statistics")
@@ -1105,6 +1130,10 @@ def _bn_bwd_k(part, grp, c, rows, training, group, count_t, params, dev):
     dbeta = grad_buffer(params[1], zero=False)
     if training and group is None:  # one launch: partial rows -> dgamma, dbeta, k
         C.bn_reduce_bwd(part, grp, c, float(rows), dgamma, dbeta, k)
+        return k, dgamma, dbeta
+    pc = peer_channel(group, 0) if (training and group is not None) else None
+    if pc is not None and count_t is not None and c <= PEER_BN_MAX_C:  # reduce + exchange + k in one kernel
+        pc.comm.bn_bwd(part, grp, c, count_t, dgamma, dbeta, k)
         return k, dgamma, dbeta
     sums = torch.empty(2 * c, dtype=torch.float64, device=dev)
     C.bn_partials(part, grp, c, sums, dgamma, dbeta)
@@ -1147,6 +1176,7 @@ class BNActFn(torch.autograd.Function):
         if link is not None and bn.training:  # (grad mode is always off inside forward)
             link.y, link.coef, link.res, link.act = y, coef, res, a
             link.group, link.params, link.c, link.rows = group, (gamma, beta), c, rows
+            link.count_t = count_t
             ctx.link = link
         ctx.has_res = res is not None
         ctx.params = (gamma, beta)
@@ -1170,16 +1200,17 @@ class BNActFn(torch.autograd.Function):
             grp = link.part_rows()
             FUSED_BWD_COUNT[0] += 1
             pending = link.pending
-            link.y = link.coef = link.res = link.part = link.pending = link.params = None
+            link.y = link.coef = link.res = link.part = link.pending = link.params = link.count_t = None
         else:
             part = ws(dev).stats_buf(c, grp)
             dz = torch.empty_like(y, memory_format=CL) if ctx.has_res else None
             C.bn_bwd_reduce(g, y, coef, res, dz, rows, c, ctx.act, part, grp, ldg)
         if pending is not None:  # SyncBN all-reduce launched early by the consuming conv's backward
-            sums, work, dgamma, dbeta = pending
+            sums, work, dgamma, dbeta, k = pending
             work.wait()
-            k = torch.empty(2 * c, dtype=torch.float32, device=dev)
-            C.bn_bwd_k(sums, ctx.count_t, float(rows), c, k)
+            if k is None:
+                k = torch.empty(2 * c, dtype=torch.float32, device=dev)
+                C.bn_bwd_k(sums, ctx.count_t, float(rows), c, k)
         else:
             k, dgamma, dbeta = _bn_bwd_k(part, grp, c, rows, ctx.training, ctx.group, ctx.count_t, ctx.params, dev)
         if link is not None and link.done:

@@ -100,7 +100,7 @@ class PeerAllReduce:
             self.comm = None
 
 
-class _PeerWork:
+class PeerWork:
     """``dist.Work``-like handle: ``wait()`` orders the current stream after the side-stream call."""
 
     def __init__(self, ev: torch.cuda.Event):
@@ -177,6 +177,17 @@ def peer_errors() -> int:
     return sum(c.error() for chans in _CHANNELS.values() for c in chans)
 
 
+def peer_channel(group, which: int):
+    """The group's forward (0, compute stream) or backward (1, side stream) channel, or None."""
+    chans = _CHANNELS.get(id(group)) if group is not None else None
+    return chans[which] if chans is not None else None
+
+
+def side_stream(dev):
+    """High-priority stream of the backward channel (created on first use)."""
+    return _side_stream(dev)
+
+
 def stats_all_reduce_(t: torch.Tensor, group) -> None:
     """Blocking-in-stream-order sum of a SyncBN statistics vector (forward / backward)."""
     chans = _CHANNELS.get(id(group))
@@ -199,4 +210,4 @@ def stats_all_reduce_async(t: torch.Tensor, group):
         ev = torch.cuda.Event()
         ev.record(side)
     t.record_stream(side)
-    return _PeerWork(ev)
+    return PeerWork(ev)
