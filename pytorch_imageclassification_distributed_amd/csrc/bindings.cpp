@@ -751,7 +751,8 @@ class PeerComm {
 }  // namespace
 
 void register_loader(pybind11::module& m);  // loader.cpp: native image-folder loader
-void bn_set_reduce_blocks(int n, int chb);  // bn.hip: target blocks / channel lanes of the row reductions
+void bn_set_reduce_blocks(int n, int chb);
+void bn_set_unroll(int v);  // bn.hip: target blocks / channel lanes of the row reductions
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "gfx950 (MI355X) HIP kernels for pytorch_imageclassification_distributed_amd";
@@ -805,6 +806,7 @@ PYBIND11_MODULE(_C, m) {
   register_loader(m);
   m.def("bn_set_reduce_blocks", &bn_set_reduce_blocks, pybind11::arg("n"), pybind11::arg("chb") = 0);
   m.def("bn_act_maxpool", &bn_act_maxpool);
+  m.def("bn_set_unroll", [](bool v) { bn_set_unroll(v ? 1 : 0); });
   m.def("stem_conv", &stem_conv);
   m.def("direct_conv", &direct_conv, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"),
         pybind11::arg("part"), pybind11::arg("G"), pybind11::arg("N"), pybind11::arg("H"), pybind11::arg("W"),

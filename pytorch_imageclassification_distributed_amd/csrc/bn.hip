@@ -207,6 +207,55 @@ __global__ void bn_apply_kernel(const bf16_t* __restrict__ y, const float* __res
   }
 }
 
+// Memory-level parallelism: one row per loop iteration leaves each lane one (two with a residual) 16-B load
+// in flight behind a dependent store, which caps a CU at ~32 KB in flight and the kernel at ~4-5 TB/s.
+// The U-row forms issue the loads of U rows (stride rstride) before using any of them; a row past the
+// end re-reads the lane's first row and is not stored.  RES / MODE are template parameters so no load
+// sits behind a runtime select (which makes hipcc branch around and wait for each load).
+constexpr int BN_U = 4;
+
+template <bool RES>
+__global__ void bn_apply_u_kernel(const bf16_t* __restrict__ y, const float* __restrict__ coef,
+                                  const bf16_t* __restrict__ res, bf16_t* __restrict__ out, long rows, int C,
+                                  int ldo, int c_off, int act) {
+  const int cch = C >> 3;
+  const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (cch == 0) return;
+  const long rstride = ((long)gridDim.x * blockDim.x) / cch;
+  long row = t / cch;
+  if (row >= rows) return;
+  const int c0 = (int)(t - row * cch) * 8;
+  float sc[8], sh[8];
+  *(float4*)sc = *(const float4*)(coef + c0);
+  *(float4*)(sc + 4) = *(const float4*)(coef + c0 + 4);
+  *(float4*)sh = *(const float4*)(coef + C + c0);
+  *(float4*)(sh + 4) = *(const float4*)(coef + C + c0 + 4);
+  for (; row < rows; row += BN_U * rstride) {
+    uint4 yv[BN_U], rv[BN_U];
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      const long r = row + u * rstride < rows ? row + u * rstride : row;
+      yv[u] = *(const uint4*)(y + r * C + c0);
+      if constexpr (RES) rv[u] = *(const uint4*)(res + r * C + c0);
+    }
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      const long r = row + u * rstride;
+      if (r >= rows) break;
+      float v[8], rr[8];
+      unpack8(yv[u], v);
+      if constexpr (RES) unpack8(rv[u], rr);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float z = v[k] * sc[k] + sh[k];
+        if constexpr (RES) z += rr[k];
+        v[k] = apply_act(z, act);
+      }
+      *(uint4*)(out + r * ldo + c_off + c0) = pack8(v);
+    }
+  }
+}
+
 // apply + MX-FP8 copy of the output for the fp8 forward convolution that consumes it (no separate
 // quantisation pass): the 4 lanes of a 32-channel block are consecutive lanes (C % 32 == 0), the
 // grid stride is a multiple of 4, so the block max is two xor-shuffles away.
@@ -505,6 +554,64 @@ __global__ void bn_bwd_elemt_kernel(const bf16_t* __restrict__ g, const bf16_t* 
   }
 }
 
+// MODE 0: dz given (dz_in); 1: g with the activation recomputed (no residual); 2: same with a residual;
+// 3: g is already dz (no activation).  U rows in flight as bn_apply_u_kernel.
+template <int MODE>
+__global__ void bn_bwd_elemt_u_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ y,
+                                      const float* __restrict__ coef, const float* __restrict__ kk,
+                                      const bf16_t* __restrict__ res, const bf16_t* __restrict__ dz_in,
+                                      bf16_t* __restrict__ dy, long rows, int C, int act, int ldg) {
+  const int cch = C >> 3;
+  const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (cch == 0) return;
+  const long rstride = ((long)gridDim.x * blockDim.x) / cch;
+  long row = t / cch;
+  if (row >= rows) return;
+  const int c0 = (int)(t - row * cch) * 8;
+  float sc[8], sh[8], mu[8], is[8], k1[8], k2[8];
+  load8f(coef + c0, sc);
+  load8f(coef + 2 * C + c0, mu);
+  load8f(coef + 3 * C + c0, is);
+  load8f(kk + c0, k1);
+  load8f(kk + C + c0, k2);
+  if constexpr (MODE == 1 || MODE == 2) load8f(coef + C + c0, sh);
+  for (; row < rows; row += BN_U * rstride) {
+    uint4 yr[BN_U], gr[BN_U], rr[BN_U];
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      const long r = row + u * rstride < rows ? row + u * rstride : row;
+      yr[u] = *(const uint4*)(y + r * C + c0);
+      if constexpr (MODE == 0) gr[u] = *(const uint4*)(dz_in + r * C + c0);
+      else gr[u] = *(const uint4*)(g + r * ldg + c0);
+      if constexpr (MODE == 2) rr[u] = *(const uint4*)(res + r * C + c0);
+    }
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      const long r = row + u * rstride;
+      if (r >= rows) break;
+      float gv[8], yv[8];
+      unpack8(yr[u], yv);
+      unpack8(gr[u], gv);
+      if constexpr (MODE == 1 || MODE == 2) {
+        float rv[8];
+        if constexpr (MODE == 2) unpack8(rr[u], rv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float z = yv[k] * sc[k] + sh[k];
+          if constexpr (MODE == 2) z += rv[k];
+          gv[k] = act_grad(z, gv[k], act);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float xhat = (yv[k] - mu[k]) * is[k];
+        gv[k] = sc[k] * (gv[k] - k1[k] - xhat * k2[k]);
+      }
+      *(uint4*)(dy + r * C + c0) = pack8(gv);
+    }
+  }
+}
+
 // target block count of the row-reduction kernels (bn_stats, bn_bwd_reduce); 0 = measured default:
 // 2048 for C <= 256 (~10 % faster than 1024), 1024 above (more blocks only add partial-row atomics)
 static int g_reduce_blocks = 0;
@@ -549,6 +656,8 @@ int grid_for(long work, int per_block = 256, int cap = 4096) {
 
 // grid for the channel-fixed elementwise kernels: grid_for's block count rounded up so that
 // blocks * 256 is a multiple of C/8 (threads past the last row return at once)
+int g_bn_unroll = 1;  // U-row elementwise kernels (bn_set_unroll; A/B and tests)
+
 int grid_chan(long rows, int C) {
   const int cch = C / 8;
   if (cch <= 0) return 1;
@@ -609,8 +718,15 @@ int bn_apply_launch(const bf16_t* y, const float* coef, const bf16_t* res, bf16_
     HIP_CHECK_LAUNCH();
     return 0;
   }
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_chan(rows, C)), dim3(256), 0, s, y, coef, res, out,
-                     rows, C, ldo, c_off, act);
+  if (g_bn_unroll) {
+    if (res) hipLaunchKernelGGL(bn_apply_u_kernel<true>, dim3(grid_chan(rows, C)), dim3(256), 0, s, y, coef, res, out,
+                                rows, C, ldo, c_off, act);
+    else hipLaunchKernelGGL(bn_apply_u_kernel<false>, dim3(grid_chan(rows, C)), dim3(256), 0, s, y, coef, res, out,
+                            rows, C, ldo, c_off, act);
+  } else {
+    hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_chan(rows, C)), dim3(256), 0, s, y, coef, res, out,
+                       rows, C, ldo, c_off, act);
+  }
   HIP_CHECK_LAUNCH();
   return 0;
 }
@@ -633,8 +749,17 @@ int bn_bwd_k_launch(const double* sums, const double* count_p, double n, int C, 
 int bn_bwd_elemt_launch(const bf16_t* g, const bf16_t* y, const float* coef, const float* k,
                         const bf16_t* res, const bf16_t* dz_in, bf16_t* dy, long rows, int C, int act,
                         int ldg, hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_elemt_kernel, dim3(grid_chan(rows, C)), dim3(256), 0, s, g, y, coef, k,
-                     res, dz_in, dy, rows, C, act, ldg > 0 ? ldg : C);
+  const int lg = ldg > 0 ? ldg : C;
+  if (g_bn_unroll) {
+    const dim3 gr(grid_chan(rows, C));
+    if (dz_in) hipLaunchKernelGGL(bn_bwd_elemt_u_kernel<0>, gr, dim3(256), 0, s, g, y, coef, k, res, dz_in, dy, rows, C, act, lg);
+    else if (act == ACT_NONE) hipLaunchKernelGGL(bn_bwd_elemt_u_kernel<3>, gr, dim3(256), 0, s, g, y, coef, k, res, dz_in, dy, rows, C, act, lg);
+    else if (res) hipLaunchKernelGGL(bn_bwd_elemt_u_kernel<2>, gr, dim3(256), 0, s, g, y, coef, k, res, dz_in, dy, rows, C, act, lg);
+    else hipLaunchKernelGGL(bn_bwd_elemt_u_kernel<1>, gr, dim3(256), 0, s, g, y, coef, k, res, dz_in, dy, rows, C, act, lg);
+  } else {
+    hipLaunchKernelGGL(bn_bwd_elemt_kernel, dim3(grid_chan(rows, C)), dim3(256), 0, s, g, y, coef, k,
+                       res, dz_in, dy, rows, C, act, lg);
+  }
   HIP_CHECK_LAUNCH();
   return 0;
 }
@@ -669,3 +794,5 @@ void bn_set_reduce_blocks(int n, int chb) {
   g_reduce_blocks = n > 0 ? n : 0;
   g_reduce_chb = chb > 0 ? chb : 0;
 }
+
+void bn_set_unroll(int v) { g_bn_unroll = v; }

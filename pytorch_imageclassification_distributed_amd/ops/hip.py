@@ -848,7 +848,8 @@ class GradSlot:
         return grad
 
 
-PEER_BN_MAX_C = int(getattr(C, "PEER_BN_MAX_C", 0))  # channels the fused SyncBN peer kernels handle
+PEER_BN_MAX_C = int(getattr(C, "PEER_BN_MAX_C", 0))
+C.bn_set_unroll(os.environ.get("IMGCLS_BN_UNROLL", "1") == "1")  # U-row BN elementwise kernels  # channels the fused SyncBN peer kernels handle
 SYNCBN_EARLY_COUNT = [0]  # SyncBN backward all-reduces launched from the consuming conv (tests)
 
 
