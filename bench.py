@@ -58,6 +58,8 @@ def parse():
                    "(default: $IMGCLS_TUNE_DB, else tuning/mi355x_find_db.json; 'none' disables); shapes it "
                    "does not list are still timed")
     p.add_argument("--tune-save", default="", help="write the kernel choices of this run to this file")
+    p.add_argument("--graph", default="off", choices=["on", "off"],
+                   help="replay the whole training step as one captured HIP graph (single process)")
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
                    help="fp8: MX-FP8 forward convolutions (BASELINE config 5); bf16 elsewhere")
     return p.parse_args()
@@ -97,9 +99,14 @@ def main():
                                  steps=a.warmup + a.steps, ring=2, seed=1234 + ctx.rank)
     batches = list(iter(data))
 
+    use_graph = a.graph == "on" and a.compute == "hip" and ctx.world_size == 1
+
     def step(i):
         b = batches[i]
-        loss = tr.train_step(b["image"], b["label"])
+        if use_graph and i >= 2:  # two eager steps tune every kernel shape, then capture / replay
+            loss = tr.graph_step(b["image"], b["label"])
+        else:
+            loss = tr.train_step(b["image"], b["label"])
         return tr.reduce_loss(loss)
 
     for i in range(a.warmup):
@@ -107,7 +114,7 @@ def main():
     torch.cuda.synchronize()
     # host enqueue cost of one step (diagnostic, stderr): > ms_per_step would mean CPU-bound
     t_host = time.perf_counter()
-    last = step(0)
+    last = step(max(a.warmup - 1, 0))
     t_host = time.perf_counter() - t_host
     torch.cuda.synchronize()
     print(f"[bench] rank {ctx.rank}: host enqueue {t_host * 1e3:.1f} ms/step", file=sys.stderr, flush=True)
@@ -146,7 +153,7 @@ def main():
                        "per_gpu_batch": a.batch, "seq_len": None, "image_size": a.image_size,
                        "num_classes": a.num_classes, "parallelism": f"dp{ctx.world_size}",
                        "sync_bn": sync_bn, "syncbn_comm": ("peer" if tr.syncbn_peer else "rccl") if sync_bn else None,
-                       "compute": a.compute, "optimizer": "adam",
+                       "compute": a.compute, "optimizer": "adam", "hip_graph": use_graph,
                        "final_loss": round(loss_val, 5)},
         }), flush=True)
     destroy()

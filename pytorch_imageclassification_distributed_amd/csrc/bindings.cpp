@@ -649,16 +649,18 @@ class PeerComm {
     check(peer_alloc(&buf_), "peer_alloc");
     check((int)hipMalloc((void**)&err_, sizeof(int)), "peer err word");
     check((int)hipMemset(err_, 0, sizeof(int)), "peer err word");
-    int khz = 0;
     int dev = 0;
     check((int)hipGetDevice(&dev), "hipGetDevice");
-    check((int)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev), "wall clock rate");
-    timeout_ticks_ = (unsigned long long)(timeout_s * (double)khz * 1000.0);
+    check((int)hipDeviceGetAttribute(&khz_, hipDeviceAttributeWallClockRate, dev), "wall clock rate");
+    set_timeout(timeout_s);
     bases_.assign(world, 0ull);
     mapped_.assign(world, nullptr);
     bases_[rank] = (unsigned long long)buf_;
   }
   ~PeerComm() { close(); }
+
+  // bound on a call's wait for its peers (later launches); the bring-up self-check uses a short one
+  void set_timeout(double timeout_s) { timeout_ticks_ = (unsigned long long)(timeout_s * (double)khz_ * 1000.0); }
 
   pybind11::bytes handle() {
     char h[64];
@@ -741,6 +743,7 @@ class PeerComm {
   }
 
   int rank_, world_;
+  int khz_ = 0;
   void* buf_ = nullptr;
   int* err_ = nullptr;
   unsigned long long seq_ = 0, timeout_ticks_ = 0;
@@ -871,6 +874,7 @@ PYBIND11_MODULE(_C, m) {
       .def("bn_fwd", &PeerComm::bn_fwd)
       .def("bn_bwd", &PeerComm::bn_bwd)
       .def("error", &PeerComm::error)
+      .def("set_timeout", &PeerComm::set_timeout)
       .def("close", &PeerComm::close)
       .def_property_readonly("seq", &PeerComm::seq);
   m.attr("PEER_MAX_ELEMS") = peer_max_elems();

@@ -78,6 +78,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--deterministic", action="store_true",
                    help="bitwise-reproducible GPU kernels (no split-K / cross-block fp32 atomics; slower)")
     p.add_argument("--timeout-min", type=float, default=10.0, help="process-group timeout (minutes)")
+    p.add_argument("--hip-graph", action="store_true",
+                   help="single GPU: capture the whole training step once and replay it as one HIP graph "
+                        "(host-bound models: Inception-v3, EfficientNet); a batch of another shape runs eagerly")
     return p
 
 

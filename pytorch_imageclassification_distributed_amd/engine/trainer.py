@@ -164,6 +164,7 @@ class Trainer:
                 self.step_stream = torch.cuda.Stream(device=self.dev, priority=hi)
         self.log = JsonlLogger(getattr(a, "metrics_file", None), self.ctx.is_main)
         self._prof = None
+        self._graph = None  # captured whole-step HIP graph (``capture_step``)
 
     # ------------------------------------------------------------------ step
     def compute_loss(self, images, labels):
@@ -195,6 +196,56 @@ class Trainer:
         caller.wait_stream(st)
         loss.record_stream(caller)
         return loss
+
+    # ------------------------------------------------------------------ HIP graph
+    def capture_step(self, images, labels) -> None:
+        """Capture one whole training step (forward, loss, backward, fused Adam) into a HIP graph that
+        ``graph_step`` replays: one launch per step instead of ~1000 host-side op dispatches (Inception-v3
+        and EfficientNet steps are host-bound in eager mode).  Call after enough eager steps that every
+        kernel shape is tuned (the tuner never runs under capture).  Single process (world 1): the
+        graph carries no collectives.  Inputs are copied into static buffers on every replay; the
+        learning rate is a kernel argument of the captured Adam launch, so a scheduler change
+        re-captures (``graph_step`` checks)."""
+        if not self.hip or self.ctx.world_size != 1:
+            raise RuntimeError("capture_step: HIP path on a single process only")
+        self._g_x = images.detach().clone()
+        self._g_y = labels.detach().clone()
+        self._g_lrs = tuple(g["lr"] for g in self.optimizer.param_groups)
+        st = self.step_stream if self.step_stream is not None else torch.cuda.Stream(device=self.dev)
+        torch.cuda.synchronize(self.dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=st):
+            self._g_loss = self._train_step(self._g_x, self._g_y)
+        torch.cuda.synchronize(self.dev)
+        self._graph, self._g_stream = g, st
+
+    def graph_step(self, images, labels):
+        """Replay the captured step on new inputs (same shapes); returns the step's loss tensor, valid
+        until the next replay is enqueued."""
+        if self._graph is None or tuple(g["lr"] for g in self.optimizer.param_groups) != self._g_lrs:
+            self._graph = None
+            self.capture_step(images, labels)
+        st = self._g_stream
+        caller = torch.cuda.current_stream(self.dev)
+        st.wait_stream(caller)
+        with torch.cuda.stream(st):
+            self._g_x.copy_(images, non_blocking=True)
+            self._g_y.copy_(labels, non_blocking=True)
+            self._graph.replay()
+        caller.wait_stream(st)
+        images.record_stream(st)
+        labels.record_stream(st)
+        return self._g_loss
+
+    def _epoch_step(self, images, labels, index: int):
+        """``--hip-graph``: eager for the first two steps of the first epoch (every kernel shape gets tuned),
+        then capture once and replay; a batch of another shape (the epoch's last) runs eagerly."""
+        use = (getattr(self.args, "hip_graph", False) and self.hip and self.ctx.world_size == 1
+               and not self._prof)
+        if use and (self._graph is not None or self.global_step >= 2):
+            if self._graph is None or (self._g_x.shape == images.shape and self._g_y.shape == labels.shape):
+                return self.graph_step(images, labels)
+        return self.train_step(images, labels)
 
     def _train_step(self, images, labels):
         rf = torch.profiler.record_function
@@ -280,7 +331,7 @@ class Trainer:
                 labels = labels.to(self.dev, non_blocking=True)
             self.timer.mark("data")
             self._profile_tick()
-            loss = self.train_step(images, labels)
+            loss = self._epoch_step(images, labels, index)
             meter.update(self.reduce_loss(loss), images.size(0))
             self.global_step += 1
             n_log += images.size(0)

@@ -729,6 +729,10 @@ def _wgrad_config(dy, x, g: ConvGeom, m, ntot):
 # stream waits for the side stream when backward ends (an engine callback), and the reducer issues each
 # bucket's all-reduce behind both streams.  IMGCLS_WGRAD_STREAM=0 keeps everything on one stream.
 WGRAD_STREAM = os.environ.get("IMGCLS_WGRAD_STREAM", "1") == "1"
+# inside a HIP-graph capture the weight gradients stay on the capturing stream: a two-stream capture
+# (event fork / join edges) replays 2x slower than the single-stream one on this ROCm runtime
+# (Inception-v3 b128: 3303 vs 6523 img/s, profiles/r3g_hip_graph_modes.txt); IMGCLS_GRAPH_SIDE=1 forks
+GRAPH_SIDE = os.environ.get("IMGCLS_GRAPH_SIDE", "0") == "1"
 _SIDE: dict = {}  # device index -> _SideStream
 
 
@@ -741,8 +745,9 @@ class _SideStream:
 
 
 def side_stream(dev):
-    """The weight-gradient stream of ``dev``, or None (disabled, CPU, or inside a graph capture)."""
-    if not WGRAD_STREAM or dev.type != "cuda" or torch.cuda.is_current_stream_capturing():
+    """The weight-gradient stream of ``dev``, or None (disabled, CPU, or inside a graph capture with
+    IMGCLS_GRAPH_SIDE=0)."""
+    if not WGRAD_STREAM or dev.type != "cuda" or (not GRAPH_SIDE and torch.cuda.is_current_stream_capturing()):
         return None
     s = _SIDE.get(dev.index)
     if s is None:

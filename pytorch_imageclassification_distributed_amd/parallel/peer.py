@@ -44,6 +44,7 @@ class PeerAllReduce:
 
     def __init__(self, group, device: torch.device, timeout_s: float = 120.0):
         from .. import _ext
+        self.timeout_s = timeout_s
         C = _ext.load()
         self.group = group
         self.rank = dist.get_rank(group)
@@ -81,18 +82,26 @@ class PeerAllReduce:
         """Non-zero once any call timed out waiting for a peer (reads a device word: syncs)."""
         return int(self.comm.error())
 
-    def self_check(self) -> bool:
-        """Three calls (both buffer parities, then a re-use) against the exact sums (collective)."""
+    def self_check(self, timeout_s: float = 15.0, steady_timeout_s: float = 120.0) -> bool:
+        """Three calls (both buffer parities, then a re-use) against the exact sums (collective).
+        The calls wait at most ``timeout_s`` for the peers (a transport whose stores never arrive
+        costs seconds, not 3 x the steady-state bound); later calls get ``steady_timeout_s``."""
         n = min(5000, self.max_elems)
         base = torch.arange(1, n + 1, dtype=torch.float64, device=self.device)
         want = base * (self.world * (self.world + 1) / 2)
         ok = True
-        for k in range(3):
-            t = base * (self.rank + 1) + k
-            self.all_reduce_(t)
-            ok &= bool(torch.equal(t, want + k * self.world))
-        torch.cuda.synchronize(self.device)
-        return ok and self.error() == 0
+        self.comm.set_timeout(float(timeout_s))
+        try:
+            for k in range(3):
+                t = base * (self.rank + 1) + k
+                self.all_reduce_(t)
+                ok &= bool(torch.equal(t, want + k * self.world))  # syncs: a timed-out call ends the check
+                if not ok:
+                    break
+            torch.cuda.synchronize(self.device)
+            return ok and self.error() == 0
+        finally:
+            self.comm.set_timeout(float(steady_timeout_s))
 
     def close(self) -> None:
         if self.comm is not None:
@@ -147,7 +156,8 @@ def setup_peer_syncbn(group, device: torch.device, mode: str = "auto") -> bool:
         chans = []
         for _ in range(2):  # forward (compute stream) and backward (side stream) channels
             chans.append(PeerAllReduce(group, device, tmo))
-        ok = all([c.self_check() for c in chans])
+        check_s = float(os.environ.get("IMGCLS_PEER_CHECK_TIMEOUT_S", "15"))
+        ok = all([c.self_check(check_s, tmo) for c in chans])
         if not _agree(ok, group, device):  # every rank must agree, or ranks would mix transports
             for c in chans:
                 c.close()

@@ -28,6 +28,8 @@ class PhaseTimer:
     def mark(self, name: str) -> None:
         if not self.enabled:
             return
+        if self.gpu and torch.cuda.is_current_stream_capturing():
+            return  # a replayed HIP graph is one opaque phase (the "data" mark brackets it)
         if self.gpu:
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()

@@ -14,13 +14,16 @@ from pytorch_imageclassification_distributed_amd.engine import Trainer, build_pa
 from pytorch_imageclassification_distributed_amd.parallel import init_distributed
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+MODEL = sys.argv[2] if len(sys.argv) > 2 else "resnet50"
+SIZE = int(sys.argv[3]) if len(sys.argv) > 3 else 224
 ctx = init_distributed(device="cuda")
-targs = build_parser().parse_args(["--synthetic", "--model", "resnet50", "--batchsize", str(B), "--num-classes", "7",
+targs = build_parser().parse_args(["--synthetic", "--model", MODEL, "--image-size", str(SIZE), "--batchsize", str(B),
+                                   "--num-classes", "7",
                                    "--num-workers", "0", "--synthetic-train-size", "8", "--synthetic-val-size", "8",
                                    "--no-sync-bn", "--lr", "1e-4"])
 tr = Trainer(targs, ctx)
 tr.net.train()
-batches = list(iter(DeviceSyntheticLoader(B, 7, 224, ctx.device, steps=4, ring=2, seed=1)))
+batches = list(iter(DeviceSyntheticLoader(B, 7, SIZE, ctx.device, steps=4, ring=2, seed=1)))
 for i in range(8):
     tr.train_step(batches[i % 4]["image"], batches[i % 4]["label"])
 torch.cuda.synchronize()
