@@ -294,9 +294,10 @@ def _sync_group(bn):
 # ---------------------------------------------------------------------------
 class ConvGeom:
     __slots__ = ("N", "Ci", "Cx", "H", "W", "Co", "kh", "kw", "sh", "sw", "dil", "pt", "pb", "pl", "pr",
-                 "OH", "OW", "T")
+                 "OH", "OW", "T", "taps", "phases")
 
     def __init__(self, x, conv):
+        self.taps = self.phases = None  # memoised _fwd_taps / _dgrad_phases (host time per launch)
         self.N, self.Cx, self.H, self.W = x.shape
         self.Co, self.Ci, self.kh, self.kw = conv.weight.shape
         self.sh, self.sw = conv.stride
@@ -309,18 +310,35 @@ class ConvGeom:
         self.T = self.kh * self.kw
 
 
+def conv_geom(x, conv) -> ConvGeom:
+    """``ConvGeom(x, conv)`` memoised on the module per input shape: the geometry, its tap table and its
+    dgrad phases are computed once, not on every launch (host time: Inception-v3 runs ~95 convs a step)."""
+    cache = conv.__dict__.get("_imgcls_geom")
+    if cache is None:
+        cache = conv.__dict__["_imgcls_geom"] = {}
+    g = cache.get(x.shape)
+    if g is None:
+        g = cache[x.shape] = ConvGeom(x, conv)
+    return g
+
+
 def _fwd_taps(g: ConvGeom):
+    if g.taps is not None:
+        return g.taps
     dh, dw, tb = [], [], []
     for r in range(g.kh):
         for c in range(g.kw):
             dh.append(r * g.dil - g.pt)
             dw.append(c * g.dil - g.pl)
             tb.append(r * g.kw + c)
-    return dh, dw, tb
+    g.taps = (tuple(dh), tuple(dw), tuple(tb))
+    return g.taps
 
 
 def _dgrad_phases(g: ConvGeom):
     """Sub-pixel decomposition of the transposed convolution (one GEMM per phase)."""
+    if g.phases is not None:
+        return g.phases
     out = []
     for ph in range(g.sh):
         for pw in range(g.sw):
@@ -338,8 +356,9 @@ def _dgrad_phases(g: ConvGeom):
                     tb.append(r * g.kw + c)
             gh = (g.H - ph + g.sh - 1) // g.sh
             gw = (g.W - pw + g.sw - 1) // g.sw
-            out.append((ph, pw, gh, gw, dh, dw, tb))
-    return out
+            out.append((ph, pw, gh, gw, tuple(dh), tuple(dw), tuple(tb)))
+    g.phases = tuple(out)
+    return g.phases
 
 
 def _weight_for_input(w_param, cx):
@@ -657,10 +676,20 @@ def _wgrad_ws(dev, n):
     return buf
 
 
-def _wgrad_launch(dy, x, out, g: ConvGeom, m, ntot, kps, splits, stages=2):
-    wsp = _wgrad_ws(dy.device, splits * g.Co * ntot) if (WGRAD_WS and splits > 1 and ntot % 8 == 0) else None
+def _wgrad_launch(dy, x, out, g: ConvGeom, m, ntot, kps, splits, stages=2, side=None):
+    """One weight-gradient launch on the current stream, or (``side``: a ``_SideStream``) forked onto the
+    side stream inside the launcher (event record / wait and allocator stream records in C++)."""
+    wsp = None
+    if WGRAD_WS and splits > 1 and ntot % 8 == 0:
+        n = splits * g.Co * ntot
+        if side is None:
+            wsp = _wgrad_ws(dy.device, n)
+        else:
+            if side.ws is None or side.ws.numel() < n:
+                side.ws = torch.empty(max(n, 1 << 20), dtype=torch.float32, device=dy.device)
+            wsp = side.ws
     C.conv_wgrad(dy, x, out, m, g.Co, g.Cx, ntot, g.OH, g.OW, g.H, g.W, g.sh, g.sw, g.pt, g.pl,
-                 g.dil, g.dil, g.kw, kps, splits, ws(dy.device).zero, stages, wsp)
+                 g.dil, g.dil, g.kw, kps, splits, ws(dy.device).zero, stages, wsp, side.handle if side else 0)
 
 
 def _wgrad_tiles(co, ntot, stages):
@@ -737,11 +766,13 @@ _SIDE: dict = {}  # device index -> _SideStream
 
 
 class _SideStream:
-    __slots__ = ("stream", "joins")
+    __slots__ = ("stream", "joins", "handle", "ws")
 
     def __init__(self, dev):
         self.stream = torch.cuda.Stream(device=dev)
         self.joins = set()  # compute streams that must wait for this stream when backward ends
+        self.handle = self.stream.cuda_stream  # raw hipStream_t for launchers that fork to it themselves
+        self.ws = None  # split-K workspace of the wgrad launches on this stream
 
 
 def side_stream(dev):
@@ -800,7 +831,14 @@ def conv_wgrad_raw(dy, x, w_param, g: ConvGeom):
     if g.Cx == g.Ci:
         dw = arena_slot(w_param)
         if dw is not None:
-            _on_side(dev, lambda: _wgrad_launch(dy, x, dw, g, m, ntot, kps, splits, stages), dy, x)
+            s = side_stream(dev)
+            if s is None:
+                _wgrad_launch(dy, x, dw, g, m, ntot, kps, splits, stages)
+                return dw
+            if not s.joins:  # first side launch of this backward: join when the engine finishes
+                torch.autograd.Variable._execution_engine.queue_callback(join_side_streams)
+            s.joins.add(torch.cuda.current_stream(dev))
+            _wgrad_launch(dy, x, dw, g, m, ntot, kps, splits, stages, side=s)
             return dw
         dw = grad_buffer(w_param)
         _wgrad_launch(dy, x, dw, g, m, ntot, kps, splits, stages)
@@ -910,7 +948,7 @@ class BwdLink:
 class ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, conv, want_stats, slot=None, fuse_bwd=False):
-        g = ConvGeom(x, conv)
+        g = conv_geom(x, conv)
         stats = ws(x.device).stats_buf(g.Co, stat_groups(g.N * g.OH * g.OW)) if want_stats else None
         y = conv_forward_raw(x, w, g, stats=stats)
         ctx.g = g
@@ -986,6 +1024,7 @@ def _s2d_index(dev):
 
 def _s2d_geom(n, h, w, co) -> ConvGeom:
     g = ConvGeom.__new__(ConvGeom)
+    g.taps = g.phases = None
     g.N, g.Ci, g.Cx, g.H, g.W, g.Co = n, 16, 16, h // 2, w // 2, co
     g.kh = g.kw = 4
     g.sh = g.sw = g.dil = 1
@@ -1048,7 +1087,7 @@ class StemS2dFn(torch.autograd.Function):
 class DwConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, conv, fuse_bwd=False):
-        g = ConvGeom(x, conv)
+        g = conv_geom(x, conv)
         wt = weight_bf16_t(w, g.Co, g.T, 1)
         y = _empty_cl(g.N, g.Co, g.OH, g.OW, x.device)
         C.dw_fwd(x, wt, y, None, g.N, g.H, g.W, g.Co, g.OH, g.OW, g.kh, g.kw, g.sh, g.sw, g.pt, g.pl)
@@ -1400,7 +1439,7 @@ class ConvBiasFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, b, conv):
-        g = ConvGeom(x, conv)
+        g = conv_geom(x, conv)
         y = conv_forward_raw(x, w, g, bias=b)
         ctx.g = g
         ctx.has_b = b is not None
