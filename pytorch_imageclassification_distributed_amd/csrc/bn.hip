@@ -457,6 +457,87 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
 }
 
 
+// U rows of loads in flight per lane, no loads behind runtime selects (as bn_bwd_elemt_u_kernel):
+// FL bit 0 = residual in the activation input, bit 1 = activation, bit 2 = dz written out.  The
+// generic kernel above issues one row of g / y loads per iteration behind the runtime res / act /
+// dz_out branches (3.4 TB/s on the 822 MB stem activation against 5.2 for bn_bwd_elemt).
+template <int FL>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_u_kernel(
+    const bf16_t* __restrict__ g, const bf16_t* __restrict__ y, const float* __restrict__ coef,
+    const bf16_t* __restrict__ res, bf16_t* __restrict__ dz_out, long rows, int C, int act,
+    long rows_per_block, float* __restrict__ part, int G, int ldg, int CHB) {
+  constexpr bool RES = FL & 1, ACT = FL & 2, DZ = FL & 4;
+  __shared__ float red[2][256][9];
+  const int cch = C >> 3;
+  const int RP = 256 / CHB;
+  const int tid = threadIdx.x;
+  const int lc = tid % CHB, lr = tid / CHB;
+  const int chunk = blockIdx.y * CHB + lc;
+  const bool active = lr < RP && chunk < cch;
+  float s[8], q[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { s[k] = 0.f; q[k] = 0.f; }
+  if (active) {
+    const int c0 = chunk * 8;
+    float sc[8], sh[8], mu[8], is[8];
+    load8f(coef + c0, sc);
+    load8f(coef + C + c0, sh);
+    load8f(coef + 2 * C + c0, mu);
+    load8f(coef + 3 * C + c0, is);
+    const long rbeg = blockIdx.x * rows_per_block;
+    const long rend = rbeg + rows_per_block < rows ? rbeg + rows_per_block : rows;
+    for (long row = rbeg + lr; row < rend; row += BN_U * RP) {
+      uint4 gr[BN_U], yr[BN_U], rr[BN_U];
+#pragma unroll
+      for (int u = 0; u < BN_U; ++u) {
+        const long r = row + u * RP < rend ? row + u * RP : row;  // clamped rows load, never count
+        gr[u] = *(const uint4*)(g + r * ldg + c0);
+        yr[u] = *(const uint4*)(y + r * C + c0);
+        if constexpr (RES) rr[u] = *(const uint4*)(res + r * C + c0);
+      }
+#pragma unroll
+      for (int u = 0; u < BN_U; ++u) {
+        if (row + u * RP >= rend) break;
+        float gv[8], yv[8], rv[8];
+        unpack8(gr[u], gv);
+        unpack8(yr[u], yv);
+        if constexpr (RES) unpack8(rr[u], rv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float dz = gv[k];
+          if constexpr (ACT) {
+            float z = yv[k] * sc[k] + sh[k];
+            if constexpr (RES) z += rv[k];
+            dz = act_grad(z, gv[k], act);
+          }
+          gv[k] = dz;
+          s[k] += dz;
+          q[k] += dz * (yv[k] - mu[k]) * is[k];
+        }
+        if constexpr (DZ) *(uint4*)(dz_out + (row + u * RP) * C + c0) = pack8(gv);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { red[0][tid][k] = s[k]; red[1][tid][k] = q[k]; }
+  __syncthreads();
+  if (lr == 0 && chunk < cch) {
+    for (int r = 1; r < RP; ++r) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s[k] += red[0][tid + r * CHB][k];
+        q[k] += red[1][tid + r * CHB][k];
+      }
+    }
+    float* dst = part + (size_t)(blockIdx.x % G) * 2 * C + chunk * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      atomicAdd(dst + k, s[k]);
+      atomicAdd(dst + C + k, q[k]);
+    }
+  }
+}
+
 // ---- standalone statistics pass (outputs not produced by the GEMM epilogue) --
 __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict__ y, long rows, int C,
                                                        long rows_per_block, float* __restrict__ part, int G,
@@ -734,8 +815,25 @@ int bn_apply_launch(const bf16_t* y, const float* coef, const bf16_t* res, bf16_
 int bn_bwd_reduce_launch(const bf16_t* g, const bf16_t* y, const float* coef, const bf16_t* res,
                          bf16_t* dz_out, long rows, int C, int act, float* part, int G, int ldg, hipStream_t s) {
   const RedGrid rg = reduce_grid(rows, C);
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, rg.grid, dim3(256), 0, s, g, y, coef, res, dz_out, rows, C, act,
-                     rg.rpb, part, G, ldg > 0 ? ldg : C, rg.chb);
+  const int ld = ldg > 0 ? ldg : C;
+  if (!g_bn_unroll) {
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel, rg.grid, dim3(256), 0, s, g, y, coef, res, dz_out, rows, C, act,
+                       rg.rpb, part, G, ld, rg.chb);
+    HIP_CHECK_LAUNCH();
+    return 0;
+  }
+  const bool a = act != ACT_NONE;
+  const int fl = (res && a ? 1 : 0) | (a ? 2 : 0) | (dz_out ? 4 : 0);
+#define BWDRED(F)                                                                                        \
+  case F:                                                                                               \
+    hipLaunchKernelGGL(bn_bwd_reduce_u_kernel<F>, rg.grid, dim3(256), 0, s, g, y, coef, res, dz_out, rows, C, \
+                       act, rg.rpb, part, G, ld, rg.chb);                                               \
+    break;
+  switch (fl) {
+    BWDRED(0) BWDRED(2) BWDRED(3) BWDRED(4) BWDRED(6) BWDRED(7)
+    default: return 2;
+  }
+#undef BWDRED
   HIP_CHECK_LAUNCH();
   return 0;
 }

@@ -1171,7 +1171,10 @@ struct WgCfg {
   static constexpr int BLOCKS = (160 * 1024) / MAIN;
   static constexpr int OCC0 = BLOCKS * NW / 4 < 1 ? 1 : (BLOCKS * NW / 4 > 3 ? 3 : BLOCKS * NW / 4);
   static constexpr int ACC = (WBM / WM) * (TN / WN) / 64;
-  static constexpr int OCC = ACC >= 128 ? (OCC0 < 2 ? OCC0 : 2) : OCC0;
+  static constexpr int OCC1 = ACC >= 128 ? (OCC0 < 2 ? OCC0 : 2) : OCC0;
+  // 4-wave 256-column tiles: 64 x 128 per wave needs the whole register file of one wave per SIMD, and
+  // 32 x 128 per wave spilled (216 B / lane) under a 3-waves-per-SIMD bound
+  static constexpr int OCC = (TN == 256 && NW == 4) ? (ACC >= 128 ? 1 : (OCC1 < 2 ? OCC1 : 2)) : OCC1;
 };
 
 // BKP = pixels per k-group per stage: 64, or 32 for a deeper ring of smaller stages (a 4-deep ring of
@@ -1433,22 +1436,52 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
   }
 }
 
-// dW += sum over splits of the workspace slabs ws[s][n] (16 B per lane, 8 slabs in flight)
+// dW += sum over splits of the workspace slabs ws[s][n].  A 256-thread block owns EL = 256 / G
+// consecutive 16-B elements and G split groups: group g sums the slabs s = g, g + G, ... (8 loads in
+// flight per lane) and the G partials are combined in group order through LDS, so the summation order
+// is fixed per (splits, G).  The split dimension is parallel too: one lane per element looping over
+// 200-500 slabs (the 64-channel layers, the stem) was a chain of 25-60 dependent round trips on a
+// 16-150-block grid - ~100 us at the end of every step for the stem.  Blocks stay at 256 threads so the
+// side stream can place them next to the compute stream's kernels (1024-thread blocks of the same
+// split waited for whole free CUs and doubled the in-step reduce time).
+template <int G>
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const f32x4* __restrict__ ws, f32x4* __restrict__ dW,
                                                            long n4, int splits) {
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
-    f32x4 a = dW[i];
-    int s = 0;
-    for (; s + 8 <= splits; s += 8) {
+  constexpr int EL = 256 / G;
+  __shared__ f32x4 part[G > 1 ? G : 1][EL];
+  const int e = threadIdx.x % EL, grp = threadIdx.x / EL;
+  const long i = (long)blockIdx.x * EL + e;
+  f32x4 a = {0.f, 0.f, 0.f, 0.f};
+  if (i < n4) {
+    int s = grp;
+    for (; s + 7 * G < splits; s += 8 * G) {
       f32x4 v[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = ws[(long)(s + k) * n4 + i];
+      for (int k = 0; k < 8; ++k) v[k] = ws[(long)(s + k * G) * n4 + i];
 #pragma unroll
       for (int k = 0; k < 8; ++k) a += v[k];
     }
-    for (; s < splits; ++s) a += ws[(long)s * n4 + i];
-    dW[i] = a;
+    for (; s < splits; s += G) a += ws[(long)s * n4 + i];
   }
+  if constexpr (G > 1) {
+    part[grp][e] = a;
+    __syncthreads();
+    if (grp == 0 && i < n4) {
+      f32x4 r = dW[i];
+#pragma unroll
+      for (int k = 0; k < G; ++k) r += part[k][e];
+      dW[i] = r;
+    }
+  } else {
+    if (i < n4) dW[i] = dW[i] + a;
+  }
+}
+
+template <int G>
+static void launch_wgrad_reduce(const float* ws, float* dW, long n4, int splits, hipStream_t stream) {
+  constexpr int EL = 256 / G;
+  hipLaunchKernelGGL(wgrad_reduce_kernel<G>, dim3((unsigned)((n4 + EL - 1) / EL)), dim3(256), 0, stream,
+                     (const f32x4*)ws, (f32x4*)dW, n4, splits);
 }
 
 }  // namespace
@@ -1571,7 +1604,7 @@ static void launch_wg(const WgradParams& p, int splits, hipStream_t stream) {
                      stream, p);
 }
 
-int conv_wgrad_tile_n(int stages) { return (stages == 4 || stages == 7 || stages == 9) ? 256 : WBN; }
+int conv_wgrad_tile_n(int stages) { return (stages == 4 || stages == 7 || stages >= 9) ? 256 : WBN; }
 
 int conv_wgrad_launch(const WgradParams& p_in, int splits, hipStream_t stream) {
   if (p_in.M <= 0) return 0;
@@ -1581,7 +1614,17 @@ int conv_wgrad_launch(const WgradParams& p_in, int splits, hipStream_t stream) {
   // stages: 1 | 2 (4 waves, 64/128 x 128 tile), 3 = 2-stage ring with the in-block 2-way pixel split
   // (8 waves), 4 = 256 x 256 tile on 8 waves (2-stage ring, one block per CU; Cout >= 256 only),
   // 5 / 6 = 32 x 128 tile with a 1 / 2-stage ring (Cout <= 32 only)
-  if (dma && (p.stages == 7 || p.stages == 9)) {  // 256 x 256, 8 waves, 4- / 3-deep ring of 32-pixel stages
+  if (dma && p.stages >= 10 && p.stages <= 13) {
+    // 64 / 128 x 256 tiles on 4 waves (2 x 2): the narrow-Cout layers (stem, ResNet layer1 / layer2) read
+    // dY once per 256 instead of per 128 columns - dY is the larger operand there (the stem's 822 MB
+    // dY was read twice at 5.4 TB/s, alone on the GPU at the end of every step)
+    if (p.stages <= 11 && p.Cout > 64) return 2;
+    if (p.stages >= 12 && p.Cout > 128) return 2;
+    if (p.stages == 10) launch_wg<64, 256, 2, 2, 1, 1>(p, splits, stream);
+    else if (p.stages == 11) launch_wg<64, 256, 2, 2, 1, 2>(p, splits, stream);
+    else if (p.stages == 12) launch_wg<128, 256, 2, 2, 1, 4, 32>(p, splits, stream);  // 4-deep ring, 32 px
+    else launch_wg<128, 256, 2, 2, 1, 2>(p, splits, stream);
+  } else if (dma && (p.stages == 7 || p.stages == 9)) {  // 256 x 256, 8 waves, 4- / 3-deep ring of 32-pixel stages
     if (p.Cout < 256) return 2;
     if (p.stages == 7) launch_wg<256, 256, 2, 4, 1, 4, 32>(p, splits, stream);
     else launch_wg<256, 256, 2, 4, 1, 3, 32>(p, splits, stream);
@@ -1611,9 +1654,12 @@ int conv_wgrad_launch(const WgradParams& p_in, int splits, hipStream_t stream) {
   HIP_CHECK_LAUNCH();
   if (p.ws != nullptr) {
     const long n4 = (long)p.Cout * p.Ntot / 4;
-    const long blocks = (n4 + 255) / 256;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, stream,
-                       (const f32x4*)p.ws, (f32x4*)p.dW, n4, splits);
+    // split groups ~ splits / 8: one batch of 8 slab loads in flight per lane covers a group
+    if (splits >= 128) launch_wgrad_reduce<16>(p.ws, p.dW, n4, splits, stream);
+    else if (splits >= 64) launch_wgrad_reduce<8>(p.ws, p.dW, n4, splits, stream);
+    else if (splits >= 32) launch_wgrad_reduce<4>(p.ws, p.dW, n4, splits, stream);
+    else if (splits >= 16) launch_wgrad_reduce<2>(p.ws, p.dW, n4, splits, stream);
+    else launch_wgrad_reduce<1>(p.ws, p.dW, n4, splits, stream);
     HIP_CHECK_LAUNCH();
   }
   return 0;
