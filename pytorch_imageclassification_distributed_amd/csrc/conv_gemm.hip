@@ -1171,10 +1171,7 @@ struct WgCfg {
   static constexpr int BLOCKS = (160 * 1024) / MAIN;
   static constexpr int OCC0 = BLOCKS * NW / 4 < 1 ? 1 : (BLOCKS * NW / 4 > 3 ? 3 : BLOCKS * NW / 4);
   static constexpr int ACC = (WBM / WM) * (TN / WN) / 64;
-  static constexpr int OCC1 = ACC >= 128 ? (OCC0 < 2 ? OCC0 : 2) : OCC0;
-  // 4-wave 256-column tiles: 64 x 128 per wave needs the whole register file of one wave per SIMD, and
-  // 32 x 128 per wave spilled (216 B / lane) under a 3-waves-per-SIMD bound
-  static constexpr int OCC = (TN == 256 && NW == 4) ? (ACC >= 128 ? 1 : (OCC1 < 2 ? OCC1 : 2)) : OCC1;
+  static constexpr int OCC = ACC >= 128 ? (OCC0 < 2 ? OCC0 : 2) : OCC0;
 };
 
 // BKP = pixels per k-group per stage: 64, or 32 for a deeper ring of smaller stages (a 4-deep ring of
@@ -1604,7 +1601,7 @@ static void launch_wg(const WgradParams& p, int splits, hipStream_t stream) {
                      stream, p);
 }
 
-int conv_wgrad_tile_n(int stages) { return (stages == 4 || stages == 7 || stages >= 9) ? 256 : WBN; }
+int conv_wgrad_tile_n(int stages) { return (stages == 4 || stages == 7 || stages == 9) ? 256 : WBN; }
 
 int conv_wgrad_launch(const WgradParams& p_in, int splits, hipStream_t stream) {
   if (p_in.M <= 0) return 0;
@@ -1614,17 +1611,7 @@ int conv_wgrad_launch(const WgradParams& p_in, int splits, hipStream_t stream) {
   // stages: 1 | 2 (4 waves, 64/128 x 128 tile), 3 = 2-stage ring with the in-block 2-way pixel split
   // (8 waves), 4 = 256 x 256 tile on 8 waves (2-stage ring, one block per CU; Cout >= 256 only),
   // 5 / 6 = 32 x 128 tile with a 1 / 2-stage ring (Cout <= 32 only)
-  if (dma && p.stages >= 10 && p.stages <= 13) {
-    // 64 / 128 x 256 tiles on 4 waves (2 x 2): the narrow-Cout layers (stem, ResNet layer1 / layer2) read
-    // dY once per 256 instead of per 128 columns - dY is the larger operand there (the stem's 822 MB
-    // dY was read twice at 5.4 TB/s, alone on the GPU at the end of every step)
-    if (p.stages <= 11 && p.Cout > 64) return 2;
-    if (p.stages >= 12 && p.Cout > 128) return 2;
-    if (p.stages == 10) launch_wg<64, 256, 2, 2, 1, 1>(p, splits, stream);
-    else if (p.stages == 11) launch_wg<64, 256, 2, 2, 1, 2>(p, splits, stream);
-    else if (p.stages == 12) launch_wg<128, 256, 2, 2, 1, 4, 32>(p, splits, stream);  // 4-deep ring, 32 px
-    else launch_wg<128, 256, 2, 2, 1, 2>(p, splits, stream);
-  } else if (dma && (p.stages == 7 || p.stages == 9)) {  // 256 x 256, 8 waves, 4- / 3-deep ring of 32-pixel stages
+  if (dma && (p.stages == 7 || p.stages == 9)) {  // 256 x 256, 8 waves, 4- / 3-deep ring of 32-pixel stages
     if (p.Cout < 256) return 2;
     if (p.stages == 7) launch_wg<256, 256, 2, 4, 1, 4, 32>(p, splits, stream);
     else launch_wg<256, 256, 2, 4, 1, 3, 32>(p, splits, stream);

@@ -434,7 +434,7 @@ def load_tuning(path: str) -> int:
             k, v = ast.literal_eval(ks), tuple(int(x) for x in v)
         except (ValueError, SyntaxError, TypeError):
             continue
-        if len(v) == 2 and 1 <= v[1] <= 13 and v[0] > 0 and k not in _WGRAD_TUNED:
+        if len(v) == 2 and 1 <= v[1] <= 9 and v[0] > 0 and k not in _WGRAD_TUNED:
             _WGRAD_TUNED[k] = v
             n += 1
     return n
@@ -694,11 +694,9 @@ def _wgrad_launch(dy, x, out, g: ConvGeom, m, ntot, kps, splits, stages=2, side=
 
 def _wgrad_tiles(co, ntot, stages):
     """Output tiles of one wgrad launch: 256 x 256 for the 8-wave kernels (stages 4, 7, 9), 32 x 128 for
-    stages 5 / 6, 64 x 256 for 10 / 11, 128 x 256 for 12 / 13, else 64|128 x 128."""
+    stages 5 / 6, else 64|128 x 128."""
     if stages in (4, 7, 9):
         return (-(-co // 256)) * (-(-ntot // 256))
-    if stages in (10, 11, 12, 13):
-        return (-(-co // (64 if stages <= 11 else 128))) * (-(-ntot // 256))
     return (-(-co // (32 if stages in (5, 6) else 64 if co <= 64 else 128))) * (-(-ntot // 128))
 
 
@@ -739,8 +737,8 @@ def _wgrad_config(dy, x, g: ConvGeom, m, ntot):
         cands += [(cand, 8) for cand in blocks if cand <= 1024]
         if g.Co <= 32:  # 32-row tiles: a 64-row tile would be half empty
             cands += [(cand, st) for st in (5, 6) for cand in blocks]
-        if g.Co <= 128 and ntot >= 256:  # 64 / 128 x 256 tiles: dY (the larger operand) read half as often
-            cands += [(cand, st) for st in ((10, 11) if g.Co <= 64 else (12, 13)) for cand in blocks]
+        # (64 / 128 x 256 four-wave tiles, reading the narrow layers' dY half as often, were 5-70 % slower
+        # on every ResNet-50 shape: profiles/r4d_wgrad_wide_tiles_probe.txt)
     for cand, st in cands:
         kps, splits = _wgrad_split(m, _wgrad_tiles(g.Co, ntot, st), cand)
         times[(cand, st)] = _time_ms(lambda: _wgrad_launch(dy, x, scratch, g, m, ntot, kps, splits, st))

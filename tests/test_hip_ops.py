@@ -95,10 +95,8 @@ N_FP8_CFG = _table_len("conv_fp8_cfgs", 8)
 
 
 def _wgrad_stage_ok(case, stages):
-    # stages 4 / 7 / 9 = 256x256 8-wave tile (Cout >= 256), 5/6 = 32-row tile (Cout <= 32), 8 = any,
-    # 10 / 11 = 64 x 256 (Cout <= 64), 12 / 13 = 128 x 256 (Cout <= 128)
-    return not ((stages in (4, 7, 9) and case[4] < 256) or (stages in (5, 6) and case[4] > 32)
-                or (stages in (10, 11) and case[4] > 64) or (stages in (12, 13) and case[4] > 128))
+    # stages 4 / 7 / 9 = 256x256 8-wave tile (Cout >= 256), 5/6 = 32-row tile (Cout <= 32), 8 = any
+    return not ((stages in (4, 7, 9) and case[4] < 256) or (stages in (5, 6) and case[4] > 32))
 
 
 @pytest.mark.parametrize("cfg", range(N_CFG))
@@ -118,14 +116,14 @@ def test_conv_tile_configs(case, cfg):
 
 
 @pytest.mark.parametrize("case,stages", [
-    (c, st) for c in [CONV_CASES[i] for i in (0, 1, 3, 4, 5, 6, 7, 8, 12, 13, 14)] for st in (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13)
+    (c, st) for c in [CONV_CASES[i] for i in (0, 1, 3, 4, 5, 6, 7, 8, 12, 13, 14)] for st in (1, 2, 3, 4, 5, 6, 7, 8, 9)
     if _wgrad_stage_ok(c, st)])
 def test_conv_wgrad_ring_variants(case, stages):
     """Weight-gradient kernel variants: 1-stage (occupancy), 2-stage ring, the 8-wave in-block
     2-way pixel split (stages=3), the 256x256 8-wave tile (stages=4, Cout >= 256), the 32-row tile
     (stages=5 / 6, Cout <= 32) and the 4- / 3-deep rings of 32-pixel stages (stages=7 / 9 on the
-    256x256 tile, 8 on the 4-wave tiles) and the 64 / 128 x 256 4-wave tiles (stages=10-13) - each over
-    the tuner's split counts."""
+    256x256 tile, 8 on the 4-wave tiles) - each over the
+    tuner's split counts."""
     hip = _hip()
     keep, hip.WGRAD_STAGES = hip.WGRAD_STAGES, stages
     try:
