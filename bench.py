@@ -40,9 +40,11 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=10)
-    # 512 per GPU: fills 288 GB HBM3E comfortably and halves the share of per-step SyncBN / all-reduce
-    # latency at N>1; the reference stack is measured at the same batch (benchmarks/reference_stack.json)
-    p.add_argument("--batch", type=int, default=512, help="per-GPU batch")
+    # 1024 per GPU (44 GiB of the 288 GB HBM3E): +4-5 % img/s over 512 on one GPU (fuller last waves on the
+    # 14x14 / 7x7 layers, per-step fixed costs amortised; profiles/r4g_b1024_tuning_runs.txt) and half the
+    # share of per-step SyncBN / all-reduce latency at N>1; the reference stack is measured at the same
+    # batch (benchmarks/reference_stack.json)
+    p.add_argument("--batch", type=int, default=1024, help="per-GPU batch")
     p.add_argument("--model", default="resnet50")
     p.add_argument("--image-size", type=int, default=224)
     p.add_argument("--num-classes", type=int, default=7)
@@ -129,6 +131,9 @@ def main():
     barrier(ctx)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    if ctx.device.type == "cuda":
+        print(f"[bench] rank {ctx.rank}: peak memory {torch.cuda.max_memory_allocated(ctx.device) / 2**30:.1f} GiB",
+              file=sys.stderr, flush=True)
     if a.tune_save and ctx.rank == 0:
         from pytorch_imageclassification_distributed_amd.ops import hip
         print(f"[bench] saved {hip.save_tuning(a.tune_save)} kernel choices to {a.tune_save}", file=sys.stderr)
