@@ -132,6 +132,19 @@ def test_conv_wgrad_ring_variants(case, stages):
         hip.WGRAD_STAGES = keep
 
 
+@pytest.mark.parametrize("target", [8, 24, 48, 96, 192])
+def test_wgrad_split_reduce_groups(target):
+    """Split-K workspace reduce at every slab-group count (G = 1, 2, 4, 8, 16 for 8 / 24 / 48 / 96 / 192
+    splits of a one-tile weight gradient): dW against the fp32 reference."""
+    hip = _hip()
+    keep = hip.WGRAD_TARGET_BLOCKS, hip.WGRAD_STAGES
+    hip.WGRAD_TARGET_BLOCKS, hip.WGRAD_STAGES = target, 2
+    try:
+        test_conv_fwd_bwd((32, 64, 56, 56, 64, (1, 1), 1, (0, 0)))
+    finally:
+        hip.WGRAD_TARGET_BLOCKS, hip.WGRAD_STAGES = keep
+
+
 @pytest.mark.parametrize("cfg", range(N_CFG))
 @pytest.mark.parametrize("act,use_res", [("relu", True), ("silu", False)])
 def test_conv_bn_act_tile_configs(act, use_res, cfg):
