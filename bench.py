@@ -79,6 +79,14 @@ def load_baseline(n_gpus: int, batch: int):
         return None
 
 
+def _alloc_counters(dev):
+    if dev.type != "cuda":
+        return {}
+    s = torch.cuda.memory_stats(dev)
+    return {"device_malloc": s.get("num_device_alloc", 0), "device_free": s.get("num_device_free", 0),
+            "alloc_retries": s.get("num_alloc_retries", 0), "ooms": s.get("num_ooms", 0)}
+
+
 def main():
     a = parse()
     ctx = init_distributed(device="cuda", backend=a.dist_backend)
@@ -90,6 +98,10 @@ def main():
         "--compute", a.compute, "--bucket-mb", str(a.bucket_mb), "--comm-dtype", a.comm_dtype,
         "--lr", "1e-4", "--dtype", a.dtype, "--syncbn-comm", a.syncbn_comm,
     ] + ([] if sync_bn else ["--no-sync-bn"]))
+    if ctx.device.type == "cuda":
+        free, total = torch.cuda.mem_get_info(ctx.device)
+        print(f"[bench] rank {ctx.rank}: device memory {free / 2**30:.1f} GiB free of {total / 2**30:.1f} GiB",
+              file=sys.stderr, flush=True)
     tr = Trainer(targs, ctx)
     tr.net.train()
     tune_db = a.tune_db or os.environ.get("IMGCLS_TUNE_DB", "") or os.path.join(HERE, "tuning", "mi355x_find_db.json")
@@ -124,6 +136,7 @@ def main():
         raise FloatingPointError(f"non-finite loss in warmup: {last.item()}")
     barrier(ctx)
     torch.cuda.synchronize()
+    m0 = _alloc_counters(ctx.device)
     t0 = time.perf_counter()
     for i in range(a.steps):
         last = step(a.warmup + i)
@@ -132,7 +145,12 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if ctx.device.type == "cuda":
-        print(f"[bench] rank {ctx.rank}: peak memory {torch.cuda.max_memory_allocated(ctx.device) / 2**30:.1f} GiB",
+        m1 = _alloc_counters(ctx.device)
+        # allocator activity inside the timed steps (diagnostic): device mallocs / frees / OOM retries
+        # there mean the caching allocator is not in steady state (every hipMalloc / hipFree syncs)
+        print(f"[bench] rank {ctx.rank}: peak memory {torch.cuda.max_memory_allocated(ctx.device) / 2**30:.1f} GiB "
+              f"(reserved {torch.cuda.max_memory_reserved(ctx.device) / 2**30:.1f} GiB); "
+              f"timed-region allocator events: " + ", ".join(f"{k} {m1[k] - m0[k]}" for k in m0),
               file=sys.stderr, flush=True)
     if a.tune_save and ctx.rank == 0:
         from pytorch_imageclassification_distributed_amd.ops import hip

@@ -48,6 +48,14 @@ struct ConvParams {
   const uint8_t* b_sc;
   long long a_elems, b_elems;  // A / B extents (bounds of the buffer-resource loads)
   FastDiv fd_ghw, fd_gw;       // multiply-shift division by GH*GW and GW (epilogue pixel remap)
+  // optional fused BatchNorm-backward elementwise on the A operand (data gradient of a 1x1 conv whose
+  // output y fed a BN: ntaps == 1, tap (0, 0), sA == 1, CA % 64 == 0).  A then holds dz (the BN input
+  // gradient's pre-elementwise form) and the kernel multiplies with
+  //   dY = xa_coef[0][c] * dz + xa_coef[1][c] * y + xa_coef[2][c]     (c = channel of the A column)
+  // with y = xa_y at the same index; xa_out (optional) receives dY from the first column tile.
+  const bf16_t* xa_y;
+  const float* xa_coef;  // [3][CA]
+  bf16_t* xa_out;
   int tile_n;  // output-channel tile: 64 or 128; 0 = 64 iff Ncols <= 64 (heuristic / fp8 path)
   int cfg;     // index into the tuned configuration table (conv_cfg_info; MX-FP8: conv_fp8_cfg_info), -1 = stages/tile_n
   int tap_dh[CONV_MAX_TAPS];
@@ -66,6 +74,10 @@ struct WgradParams {
   const bf16_t* zero;  // >= 16 zero bytes (LDS-DMA source of padded chunks)
   int stages;          // 1 | 2: ring depth (4 waves); 3: 8 waves, in-block pixel split; 4: 256x256 tile, 8 waves
   float* ws;           // optional [splits][Cout][Ntot] fp32 partial-tile workspace (plain stores + reduce), else atomics
+  // optional fused BatchNorm-backward elementwise on dY (as ConvParams::xa_*): dY holds dz and the kernel
+  // uses xa_coef[0][co] * dz + xa_coef[1][co] * y + xa_coef[2][co], y = xa_y at the same index
+  const bf16_t* xa_y;
+  const float* xa_coef;  // [3][Cout]
 };
 
 int conv_gemm_launch(const ConvParams& p, hipStream_t stream);

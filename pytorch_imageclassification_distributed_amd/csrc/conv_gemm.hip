@@ -540,10 +540,12 @@ DEVI void glds16(const void* src, char* lds_wave_base) {
 // (1-stage ring: 3-4 blocks/CU hide latency by occupancy; 2-stage: in-block overlap).  256 x {64,128,256}
 // on 8 waves (2 per SIMD, one block per CU) keeps a deeper ring in flight across the barrier (3 stages =
 // 2 tiles ahead at BN <= 128) and halves the LDS-DMA bytes per FLOP of the 128-row tile.
-template <int TM, int BN, int WM, int WN, int STAGES>
+template <int TM, int BN, int WM, int WN, int STAGES, bool XA = false>
 struct GldsCfg {
   static constexpr int NW = WM * WN, NTH = 64 * NW;
-  static constexpr int A_BYTES = TM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  // XA: each wave's private copy of the k-step's fused BN-backward coefficients (3 x 64 floats, DMA'd
+  // with the stage so the wave's own vmcnt covers it) rides behind the B tile
+  static constexpr int A_BYTES = TM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES + (XA ? NW * 1024 : 0);
   static constexpr int CST = BN + 8;
   static constexpr int EPI = TM * CST * 2;
   // the epilogue tile reuses the ring; a short ring is sized by the epilogue instead
@@ -554,7 +556,7 @@ struct GldsCfg {
   static constexpr int BLOCKS = (160 * 1024) / (MAIN + 3 * CONV_MAX_TAPS * 4);
   static constexpr int OCC_LDS = BLOCKS * NW / 4 < 1 ? 1 : (BLOCKS * NW / 4 > 4 ? 4 : BLOCKS * NW / 4);
   static constexpr int EST_VGPR = (TM / WM) * (BN / WN) / 64 + 4 * (TM / WM / 16 + BN / WN / 16) +
-                                  4 * (TM / 8 / NW) + 2 * (BN / 8 / NW) + 48;
+                                  4 * (TM / 8 / NW) + 2 * (BN / 8 / NW) + 48 + (XA ? 5 * (TM / 8 / NW) : 0);
   static constexpr int OCC_REG = 512 / EST_VGPR < 1 ? 1 : 512 / EST_VGPR;
   static constexpr int OCC = OCC_LDS < OCC_REG ? OCC_LDS : OCC_REG;
 };
@@ -581,10 +583,21 @@ DEVI int tap_tb(int pk) { return (int)((unsigned)pk >> 16); }
 
 // PRIO: s_setprio(1) around each k-half's MFMA cluster (guide T5: keeps hipcc from moving MFMAs across
 // the barrier in among the loads); a separate table entry, chosen per shape by the tuner
-template <int TM, int BN, int WM, int WN, int STAGES, bool TAP_UNIFORM, int PRIO = 0>
-__global__ __launch_bounds__((GldsCfg<TM, BN, WM, WN, STAGES>::NTH), (GldsCfg<TM, BN, WM, WN, STAGES>::OCC))
+//
+// XA (fused BatchNorm-backward elementwise): the data gradient of a 1x1 stride-1 conv whose
+// output y fed a BN reads dz (the BN's pre-elementwise gradient, written by the consumer conv's dgrad
+// epilogue) as its A operand and finishes the BN backward on the way into the MFMAs:
+//   dY = c0 * dz + c1 * y + c2   per A column (channel),   instead of a separate bn_bwd_elemt pass that
+// reads dz and y and writes dY (which this kernel and the weight gradient would read again).  Each wave
+// transforms the A pieces it DMA'd itself, right after its own vmcnt wait and before the barrier that
+// publishes the stage: y arrives by a plain buffer load issued with the DMA (same offsets, zeros out of
+// range), the stage's 3 x 64 coefficients by a per-wave LDS-DMA.  1x1 stride-1 only: every valid row's
+// A piece is in bounds, so no padding masks (rows past M never reach the output).  Rings of <= 2 stages
+// (every k-step drains vmcnt to 0 before the barrier, so the register load costs no pipelining).
+template <int TM, int BN, int WM, int WN, int STAGES, bool TAP_UNIFORM, int PRIO = 0, bool XA = false>
+__global__ __launch_bounds__((GldsCfg<TM, BN, WM, WN, STAGES, XA>::NTH), (GldsCfg<TM, BN, WM, WN, STAGES, XA>::OCC))
 void conv_gemm_glds_kernel(const ConvParams p) {
-  using Cfg = GldsCfg<TM, BN, WM, WN, STAGES>;
+  using Cfg = GldsCfg<TM, BN, WM, WN, STAGES, XA>;
   constexpr int NW = Cfg::NW;
   constexpr int A_BYTES = Cfg::A_BYTES;
   constexpr int STAGE = Cfg::STAGE;
@@ -596,6 +609,8 @@ void conv_gemm_glds_kernel(const ConvParams p) {
   constexpr int MAIN = Cfg::MAIN;
   static_assert(AL >= 1 && BL >= 1 && AL * 8 * NW == TM && BL * 8 * NW == BN, "loader mapping");
   static_assert(MAIN + CONV_MAX_TAPS * 4 <= 160 * 1024, "LDS budget");
+  static_assert(!XA || (TAP_UNIFORM && STAGES <= 2 && (TM / NW) % 16 == 0 && AL % 2 == 0),
+                "XA: uniform taps, <= 2 stages, even/odd pieces of a wave share a channel chunk");
   __shared__ __attribute__((aligned(16))) char smem[MAIN + CONV_MAX_TAPS * 4];
   int* s_tap = (int*)(smem + MAIN);
 
@@ -615,6 +630,15 @@ void conv_gemm_glds_kernel(const ConvParams p) {
   const int n_img0 = m0 / ghw;
   const __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.A + (long)n_img0 * img, 2 * (p.a_elems - (long)n_img0 * img));
   const __amdgpu_buffer_rsrc_t rsB = make_rsrc(p.B, 2 * p.b_elems);
+  // XA: y with the same per-block base and extent as A; per-thread state of the pieces in flight
+  __amdgpu_buffer_rsrc_t rsZ, rsK;
+  uint4 xa_y[XA ? AL : 1];
+  unsigned xa_va[XA ? AL : 1];
+  int xa_ci = 0;  // first channel of the k-step in flight
+  if constexpr (XA) {
+    rsZ = make_rsrc(p.xa_y + (long)n_img0 * img, 2 * (p.a_elems - (long)n_img0 * img));
+    rsK = make_rsrc(p.xa_coef, 12L * p.CA);
+  }
   int a_pix[AL], a_ih[AL], a_iw[AL];
 #pragma unroll
   for (int i = 0; i < AL; ++i) {
@@ -709,7 +733,60 @@ void conv_gemm_glds_kernel(const ConvParams p) {
     for (int i = 0; i < AL; ++i) blds16(rsA, va[i], sa + (wid * (TM / NW) + i * 8) * 128);
 #pragma unroll
     for (int i = 0; i < BL; ++i) blds16(rsB, vb[i], sb + (wid * (BN / NW) + i * 8) * 128);
+    if constexpr (XA) {
+      // the k-step's channels [ci, ci + 64): lane l < 48 fetches coefficient array l / 16, floats 4 (l % 16)
+      // .. +4 into this wave's slot (lane-linear); lanes >= 48 land zeros past the used 768 B
+      const int ci = xa_ci;
+      const unsigned ko = lane < 48 ? 4u * (unsigned)((lane >> 4) * p.CA + ci + (lane & 15) * 4) : OOB;
+      blds16(rsK, ko, sb + Cfg::B_BYTES + wid * 1024);
+#pragma unroll
+      for (int i = 0; i < AL; ++i) {
+        xa_va[i] = va[i];
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsZ, va[i], 0, 0);
+        xa_y[i] = *(const uint4*)&v;
+      }
+      xa_ci += BK;
+      if (xa_ci >= p.CA) xa_ci -= p.CA;
+    }
     if constexpr (TAP_UNIFORM) u_pk = s_tap[u_tap < p.ntaps ? u_tap : 0];
+  };
+  // XA: the stage this wave just waited for holds its own dz pieces and coefficient slot; turn the dz
+  // pieces into dY in place (and, for the first column tile, write dY out when xa_out is set)
+  const int xa_ch0 = pch ^ ((lrow >> 1) & 7), xa_ch1 = pch ^ ((4 + (lrow >> 1)) & 7);
+  auto xa_transform = [&](int buf, int ci) {
+    if constexpr (XA) {
+      char* sa = smem + buf * STAGE;
+      const float* kc = (const float*)(sa + Cfg::A_BYTES + Cfg::B_BYTES + wid * 1024);
+      float c0[2][8], c1[2][8], c2[2][8];
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        const int ch = (g ? xa_ch1 : xa_ch0) * 8;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x4 a = *(const f32x4*)(kc + ch + 4 * h);
+          const f32x4 b = *(const f32x4*)(kc + 64 + ch + 4 * h);
+          const f32x4 c = *(const f32x4*)(kc + 128 + ch + 4 * h);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) { c0[g][4 * h + k] = a[k]; c1[g][4 * h + k] = b[k]; c2[g][4 * h + k] = c[k]; }
+        }
+      }
+      const bool wr = p.xa_out != nullptr && n0 == 0;
+#pragma unroll
+      for (int i = 0; i < AL; ++i) {
+        const int g = i & 1;
+        uint4* dst = (uint4*)(sa + (wid * (TM / NW) + i * 8) * 128 + lane * 16);
+        float d[8], y[8];
+        unpack8(*dst, d);
+        unpack8(xa_y[i], y);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) d[k] = fmaf(c0[g][k], d[k], fmaf(c1[g][k], y[k], c2[g][k]));
+        const uint4 v = pack8(d);
+        *dst = v;
+        if (wr && xa_va[i] != OOB) *(uint4*)(p.xa_out + (long)n_img0 * img + (xa_va[i] >> 1)) = v;
+      }
+      (void)ci;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
   };
 
   f32x4 acc[RM][RN];
@@ -732,12 +809,14 @@ void conv_gemm_glds_kernel(const ConvParams p) {
       if (kt > 0) __builtin_amdgcn_s_barrier();
       issue(0);
       wait_vmcnt<0>();
+      xa_transform(0, 0);
       __builtin_amdgcn_s_barrier();
     } else {
       // tile kt landed (the STAGES-2 younger tiles may stay in flight across the barrier); the
       // barrier also retires every wave's reads of the buffer the next issue overwrites
-      if (kt + STAGES - 2 < nk) wait_vmcnt<(STAGES - 2) * LPS>();
+      if (kt + STAGES - 2 < nk) wait_vmcnt<(STAGES - 2) * (LPS + (XA ? 1 + AL : 0))>();
       else wait_vmcnt<0>();
+      xa_transform(kt % STAGES, 0);
       __builtin_amdgcn_s_barrier();
     }
     const char* sa = smem + (kt % STAGES) * STAGE;

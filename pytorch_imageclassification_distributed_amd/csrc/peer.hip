@@ -8,8 +8,9 @@
 //
 //   push:  block g of rank r writes its chunk of the input into slot [parity][r] of EVERY rank's
 //          buffer (system-scope write-through stores straight over the xGMI link to that GPU), waits
-//          for those stores to complete, then raises flag [g][r] = seq on every rank;
-//   wait:  it polls its own flags [g][q] for all q until they reach seq (bounded spin);
+//          for those stores to complete, then (system-scope release) raises flag [g][r] = seq on every
+//          rank;
+//   wait:  it polls its own flags [g][q] for all q until they reach seq (bounded spin), then acquires;
 //   sum:   it adds slot [parity][q] chunk g over q = 0..W-1 in rank order - the same order on every
 //          rank, so all ranks get bitwise identical statistics (as a ring all-reduce does).
 //
@@ -50,6 +51,24 @@ DEVI unsigned long long ld_sys(const unsigned long long* p) {
   return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Hand-off ordering (MI355X_MICROARCH "Workgroup dispatch ... inter-workgroup visibility", system scope):
+// producer = write-through payload stores -> every storing wave s_waitcnt vmcnt(0) -> workgroup barrier ->
+// system-scope RELEASE fence -> s_waitcnt vmcnt(0) (kept explicit: ROCm 7.2 can drop the fence's own
+// wait) -> relaxed flag store; consumer = relaxed polls -> ONE system-scope ACQUIRE fence by the polling
+// wave -> s_waitcnt -> workgroup barrier -> payload loads.  The payload and flags live in uncached memory
+// and are accessed with system-scope (sc0 sc1) operations, so the fences have no dirty lines to write
+// back or stale lines to drop; they make the ordering explicit rather than a property of the memory type.
+DEVI void raise_flag(unsigned long long* flag, unsigned long long seq) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  st_sys(flag, seq);
+}
+
+DEVI void acquire_after_poll() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+}
+
 __global__ __launch_bounds__(kThreads) void peer_allreduce_f64_kernel(
     const double* in, double* out, int n, PeerTable tab, int rank, int world,
     unsigned long long seq, unsigned long long timeout_ticks, int* __restrict__ err) {
@@ -78,10 +97,7 @@ __global__ __launch_bounds__(kThreads) void peer_allreduce_f64_kernel(
   // every storing wave waits for its stores to be acknowledged before the flag may be raised
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (t < world) {
-    unsigned long long* flag = (unsigned long long*)(tab.base[t] + ((size_t)g * kMaxWorld + rank) * 8);
-    st_sys(flag, seq);
-  }
+  if (t < world) raise_flag((unsigned long long*)(tab.base[t] + ((size_t)g * kMaxWorld + rank) * 8), seq);
 
   // 2) wait until every rank's chunk g of this call has arrived (lane q polls flag [g][q])
   if (t < 64) {
@@ -96,6 +112,7 @@ __global__ __launch_bounds__(kThreads) void peer_allreduce_f64_kernel(
       __builtin_amdgcn_s_sleep(1);
     }
     if (t == 0 && timed_out) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    acquire_after_poll();
   }
   __syncthreads();
 
@@ -177,10 +194,7 @@ __global__ __launch_bounds__(256) void peer_bn_kernel(PeerBnArgs a, PeerTable ta
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (t < world) {
-    unsigned long long* flag = (unsigned long long*)(tab.base[t] + ((size_t)g * kMaxWorld + rank) * 8);
-    st_sys(flag, seq);
-  }
+  if (t < world) raise_flag((unsigned long long*)(tab.base[t] + ((size_t)g * kMaxWorld + rank) * 8), seq);
   // 3) wait for every rank's block g of this call
   if (t < 64) {
     const unsigned long long* mine = (const unsigned long long*)(tab.base[rank] + (size_t)g * kMaxWorld * 8);
@@ -194,6 +208,7 @@ __global__ __launch_bounds__(256) void peer_bn_kernel(PeerBnArgs a, PeerTable ta
       __builtin_amdgcn_s_sleep(1);
     }
     if (t == 0 && timed_out) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    acquire_after_poll();
   }
   __syncthreads();
   // 4) rank-ordered sums, then the layer's coefficients for this block's channels

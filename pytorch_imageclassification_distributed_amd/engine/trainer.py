@@ -37,9 +37,9 @@ from ..data import CudaPrefetcher, ImageDataset, NativeFolderLoader, SyntheticIm
 from ..models import DEFAULT_IMAGE_SIZE, Classifier
 from ..ops import functional as Fx
 from ..ops.grad_arena import GradArena
-from ..parallel import GradReducer, convert_sync_batchnorm, setup_peer_syncbn
+from ..parallel import GradReducer, check_peer_errors, convert_sync_batchnorm, setup_peer_syncbn
 from ..utils import (BEST, LATEST, AccuracyCounter, DeviceMeter, JsonlLogger, load_checkpoint,
-                     load_model_state, resolve_resume, save_checkpoint)
+                     load_model_state, resolve_resume, restore_rng_state, save_checkpoint)
 from ..utils.timers import PhaseTimer
 from .config import parse_class_weights
 from .optim import FusedAdam, MultiStepLR
@@ -57,6 +57,11 @@ class Trainer:
         if args.compute != "auto":
             Fx.set_backend(args.compute)
         self.hip = self.dev.type == "cuda" and Fx.get_backend() != "torch"
+        if self.hip and getattr(args, "dtype", "bf16") == "fp32":
+            # the native kernels store activations / weight shadows in bf16 (fp32 accumulation, fp32 master
+            # weights, fp32 BN statistics and head); an fp32 request must not silently run bf16
+            raise SystemExit("--dtype fp32: the HIP kernels compute in bf16 with fp32 accumulation; for the "
+                             "reference's fp32 numerics use --compute torch --dtype fp32 (ATen fp32, no autocast)")
         if self.hip:
             from ..ops import hip as _hipmod
             _hipmod.set_fp8(getattr(args, "dtype", "bf16") == "fp8")
@@ -165,6 +170,7 @@ class Trainer:
         self.log = JsonlLogger(getattr(a, "metrics_file", None), self.ctx.is_main)
         self._prof = None
         self._graph = None  # captured whole-step HIP graph (``capture_step``)
+        self._eager_steps = 0  # eager training steps run by this process (graph capture waits for 2)
 
     # ------------------------------------------------------------------ step
     def compute_loss(self, images, labels):
@@ -238,13 +244,19 @@ class Trainer:
         return self._g_loss
 
     def _epoch_step(self, images, labels, index: int):
-        """``--hip-graph``: eager for the first two steps of the first epoch (every kernel shape gets tuned),
-        then capture once and replay; a batch of another shape (the epoch's last) runs eagerly."""
+        """``--hip-graph``: eager for the first two steps this process runs (every kernel shape gets tuned;
+        counted per process, so a resumed run warms up too), then capture once - on a full batch of the
+        loader's batch size, never on an epoch's short last batch - and replay; a batch of another shape
+        runs eagerly."""
         use = (getattr(self.args, "hip_graph", False) and self.hip and self.ctx.world_size == 1
                and not self._prof)
-        if use and (self._graph is not None or self.global_step >= 2):
-            if self._graph is None or (self._g_x.shape == images.shape and self._g_y.shape == labels.shape):
+        if use:
+            if self._graph is not None:
+                if self._g_x.shape == images.shape and self._g_y.shape == labels.shape:
+                    return self.graph_step(images, labels)
+            elif self._eager_steps >= 2 and images.shape[0] == self.args.batchsize:
                 return self.graph_step(images, labels)
+        self._eager_steps += 1
         return self.train_step(images, labels)
 
     def _train_step(self, images, labels):
@@ -336,6 +348,8 @@ class Trainer:
             self.global_step += 1
             n_log += images.size(0)
             if (index + 1) % max(a.log_interval, 1) == 0:
+                if self.syncbn_peer:  # a timed-out SyncBN peer exchange is fatal (parallel/peer.py)
+                    check_peer_errors(f"epoch {epoch} step {index}")
                 if bar is not None:
                     bar.set_description(f"Epoch: {epoch}; Loss {meter.val:.4f}|({meter.avg:.4f})")
                 if self.timer.enabled:
@@ -352,6 +366,8 @@ class Trainer:
         if bar is not None:
             bar.set_description(f"Epoch: {epoch}; Loss {meter.val:.4f}|({meter.avg:.4f})")
             bar.close()
+        if self.syncbn_peer:
+            check_peer_errors(f"end of epoch {epoch}")
         return meter.avg if meter.count else float("nan")
 
     @torch.no_grad()
@@ -403,6 +419,12 @@ class Trainer:
             self.optimizer.load_state_dict(ck["optimizer"])
         if "scheduler" in ck:
             self.scheduler.load_state_dict(ck["scheduler"])
+        if "rng" in ck:  # full resume: the run continues the saved random streams
+            restore_rng_state(ck["rng"])
+        if "sampler_epoch" in ck:
+            # the next epoch's DistributedSampler shuffle (seed + epoch), as the interrupted run would draw it
+            self.start_epoch = int(ck["sampler_epoch"]) + 1
+        self.train_sampler.set_epoch(self.start_epoch)
         if self.ctx.is_main:
             print(f"Loaded Checkpoint: {which}, with epoch {ck['epoch']} and best score {self.best_score}",
                   flush=True)

@@ -8,9 +8,11 @@ Tensor conventions on this path:
   rewrites after every step (see ``weight_bf16`` / ``engine.optim``);
 * classifier features / logits: fp32 ``[N, C]``;
 * BatchNorm statistics: fp32 partial sums produced by the conv epilogue,
-  reduced in fp64; SyncBN exchanges the fp64 sums with one RCCL all-reduce.
+  reduced in fp64; SyncBN exchanges the fp64 sums (one-shot xGMI peer kernel,
+  ``parallel/peer.py``, or an RCCL all-reduce).
 
-Nothing here falls back to ATen math: a missing extension raises.
+Every GPU op here is an in-tree kernel (``csrc/``): a missing extension raises, there is no
+ATen / library-GEMM fallback on this path (the ATen path is ``--compute torch``).
 """
 from __future__ import annotations
 
@@ -125,12 +127,16 @@ def _krsc_compatible(p: torch.Tensor) -> bool:
 def weight_bf16(p: torch.Tensor) -> torch.Tensor:
     """bf16 copy of ``p`` in KRSC order ([Co][kh][kw][Ci] for conv weights).
 
-    Refreshed when ``p`` changed outside the fused optimizer (version counter or
-    storage moved); the fused Adam kernel keeps registered shadows current.
+    Refreshed when ``p`` changed outside the fused optimizer (version counter or storage moved):
+    ``load_state_dict``, ``--pretrained`` into a live model, an EMA or any in-place edit bumps
+    ``p._version``.  The fused Adam kernel writes the master and its shadows through raw pointers
+    (no version bump), so a registered shadow stays current across steps without a re-cast, and a
+    re-cast (``stamp`` += 1) invalidates the derived dgrad / MX copies even when the optimizer
+    maintains them.
     """
     key = id(p)
     e = _SHADOWS.get(key)
-    if e is not None and e.ref() is p and e.ptr == p.data_ptr() and (e.fused or e.version == p._version):
+    if e is not None and e.ref() is p and e.ptr == p.data_ptr() and e.version == p._version:
         return e.t
     if e is None or e.ref() is not p or e.t.numel() != p.numel():
         e = _Shadow()
@@ -155,10 +161,11 @@ def weight_bf16_t(p: torch.Tensor, co: int, taps: int, ci: int) -> torch.Tensor:
     """bf16 copy of a KRSC conv weight transposed to [Ci][T][Co] (the dgrad B operand).
 
     Cached with the KRSC shadow; once registered with the fused Adam (``shadow_t_for_optimizer``)
-    the optimizer rewrites it in its update pass, so steady-state training never transposes."""
+    the optimizer rewrites it in its update pass (leaving ``stamp`` alone), so steady-state training
+    never transposes; a re-cast of the KRSC shadow after an outside write makes it stale."""
     wb = weight_bf16(p)
     e = _SHADOWS[id(p)]
-    if e.tt is not None and e.tgeom == (co, taps, ci) and (e.tfused or e.tt_stamp == e.stamp):
+    if e.tt is not None and e.tgeom == (co, taps, ci) and e.tt_stamp == e.stamp:
         return e.tt
     if e.tt is None or e.tgeom != (co, taps, ci):
         e.tt = torch.empty(co * taps * ci, dtype=BF16, device=p.device)
@@ -210,7 +217,7 @@ def weight_mx(p: torch.Tensor):
     Kept current by the fused optimizer (one batched launch after Adam) once registered."""
     weight_bf16(p)  # creates / refreshes the shadow entry (version tracking lives there)
     e = _SHADOWS[id(p)]
-    if e.mq is not None and (e.mfused or e.m_stamp == e.stamp):
+    if e.mq is not None and e.m_stamp == e.stamp:
         return e.mq, e.ms
     if e.mq is None:
         if C.mx_wjob_bytes() != _MXW_DT.itemsize:
@@ -893,8 +900,8 @@ class GradSlot:
         return grad
 
 
-PEER_BN_MAX_C = int(getattr(C, "PEER_BN_MAX_C", 0))
-C.bn_set_unroll(os.environ.get("IMGCLS_BN_UNROLL", "1") == "1")  # U-row BN elementwise kernels  # channels the fused SyncBN peer kernels handle
+PEER_BN_MAX_C = int(getattr(C, "PEER_BN_MAX_C", 0))  # channels the fused SyncBN peer kernels handle
+C.bn_set_unroll(os.environ.get("IMGCLS_BN_UNROLL", "1") == "1")  # U-row BN elementwise kernels
 SYNCBN_EARLY_COUNT = [0]  # SyncBN backward all-reduces launched from the consuming conv (tests)
 
 
@@ -1340,38 +1347,59 @@ def dense_conv_eligible(x, conv) -> bool:
             and not getattr(conv, "tf_same", False) and x.shape[1] == conv.in_channels)
 
 
+def _dense_geom(n, k, co) -> ConvGeom:
+    """A dense layer Y[n][co] = X[n][k] . W[co][k] as a 1x1 conv over a 1x1 map with k input channels."""
+    g = ConvGeom.__new__(ConvGeom)
+    g.taps = g.phases = None
+    g.N, g.Ci, g.Cx, g.H, g.W, g.Co = n, k, k, 1, 1, co
+    g.kh = g.kw = g.sh = g.sw = g.dil = 1
+    g.pt = g.pb = g.pl = g.pr = 0
+    g.OH = g.OW = g.T = 1
+    return g
+
+
+def _as_pixel_rows(t, n, k):
+    """[n, c, h, w] channels-last -> [n, k = h*w*c, 1, 1] channels-last: the same memory, one 'pixel' per image."""
+    return _cl(t).permute(0, 2, 3, 1).reshape(n, k).view(n, k, 1, 1)
+
+
 class DenseConvFn(torch.autograd.Function):
     """A convolution whose kernel covers its whole unpadded input is a dense layer:
     Y[n][co] = X[n][(h, w, ci)] . W[co][(h, w, ci)] - NHWC activations and KRSC weights flatten alike
-    (Inception's aux classifier conv1: 5x5 over a 5x5 map).  As an implicit-GEMM transposed conv its
-    data gradient walked all 25 taps per input pixel, 24 of them in the zero padding (279 us of 64
-    blocks at batch 128); as three plain library GEMMs (hipBLASLt; dW accumulated in fp32) it costs
-    microseconds."""
+    (Inception's aux classifier conv1: 5x5 over a 5x5 map, reference nn/classifier.py:20-23 via
+    torchvision's InceptionAux).  As an implicit-GEMM 5x5 conv its data gradient walked all 25 taps per
+    input pixel, 24 of them in the zero padding (279 us of 64 blocks at batch 128).  Here it runs on the
+    same MFMA implicit-GEMM kernels as a 1x1 conv over a 1x1 map with h*w*ci input channels: forward
+    (with the following BN's statistics in the epilogue), data gradient (transposed bf16 shadow) and
+    split-K weight gradient into the gradient arena slot - no library GEMM."""
 
     @staticmethod
-    def forward(ctx, x, w, conv):
+    def forward(ctx, x, w, conv, want_stats=False):
         n, c, h, wd = x.shape
         co = w.shape[0]
-        xf = _cl(x).permute(0, 2, 3, 1).reshape(n, h * wd * c)
-        wf = weight_bf16(w).view(co, h * wd * c)
-        y = torch.mm(xf, wf.t())
-        ctx.save_for_backward(x, w)
-        return y.view(n, 1, 1, co).permute(0, 3, 1, 2)
+        k = h * wd * c
+        g = _dense_geom(n, k, co)
+        xf = _as_pixel_rows(x, n, k)
+        stats = ws(x.device).stats_buf(co, stat_groups(n)) if want_stats else None
+        y = conv_forward_raw(xf, w, g, stats=stats, wb=weight_bf16(w))
+        ctx.g, ctx.xshape = g, (n, c, h, wd)
+        ctx.save_for_backward(xf, w)
+        return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, w = ctx.saved_tensors
-        n, c, h, wd = x.shape
-        co = w.shape[0]
-        dyf = dy.reshape(n, co).to(BF16)
-        xf = _cl(x).permute(0, 2, 3, 1).reshape(n, h * wd * c)
+        xf, w = ctx.saved_tensors
+        g = ctx.g
+        n, c, h, wd = ctx.xshape
+        dy = _cl(dy)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = torch.mm(dyf, weight_bf16(w).view(co, h * wd * c)).view(n, h, wd, c).permute(0, 3, 1, 2)
+            d = conv_dgrad_raw(dy, w, g)  # [n, k, 1, 1] channels-last = [n][h][w][c] in memory
+            dx = torch.empty(0, dtype=d.dtype, device=d.device).set_(
+                d.untyped_storage(), d.storage_offset(), (n, c, h, wd), (h * wd * c, 1, wd * c, c))
         if ctx.needs_input_grad[1]:
-            dw = grad_buffer(w, zero=False)
-            dw.permute(0, 2, 3, 1).copy_(torch.mm(dyf.t().float(), xf.float()).view(co, h, wd, c))
-        return dx, dw, None
+            dw = conv_wgrad_raw(dy, xf, w, g)
+        return dx, dw, None, None
 
 
 POOL_CONV_SWAP = os.environ.get("IMGCLS_POOL_CONV_SWAP", "1") == "1"
@@ -1420,8 +1448,8 @@ def conv_bn_act(x, conv, bn, act, residual, x_slot=None, res_slot=None, exclusiv
         y = DwConvFn.apply(x, conv.weight, conv, exclusive_input and FUSE_BN_BWD and DW_LINK)
         ready = False
     elif dense_conv_eligible(x, conv) and x.shape[2] * x.shape[3] > 1:
-        y = DenseConvFn.apply(x, conv.weight, conv)
-        ready = False
+        y = DenseConvFn.apply(x, conv.weight, conv, bn.training)
+        ready = bn.training
     else:
         if conv.groups != 1:
             raise NotImplementedError("grouped convolution")

@@ -1,6 +1,7 @@
 from .comm import all_gather, all_gather_tensor, all_reduce_sum_, reduce_tensor
 from .dist import DistContext, barrier, destroy, get_rank, get_world_size, init_distributed
-from .peer import PeerAllReduce, peer_active, peer_errors, setup_peer_syncbn, teardown_peer_syncbn
+from .peer import (PeerAllReduce, PeerTimeoutError, check_peer_errors, peer_active, peer_errors, setup_peer_syncbn,
+                   teardown_peer_syncbn)
 from .reducer import GradReducer, broadcast_module_state
 from .syncbn import combine_stats, convert_sync_batchnorm, sync_batch_norm
 
@@ -8,6 +9,7 @@ __all__ = [
     "DistContext", "init_distributed", "barrier", "destroy", "get_rank", "get_world_size",
     "GradReducer", "broadcast_module_state",
     "PeerAllReduce", "setup_peer_syncbn", "teardown_peer_syncbn", "peer_active", "peer_errors",
+    "check_peer_errors", "PeerTimeoutError",
     "convert_sync_batchnorm", "sync_batch_norm", "combine_stats",
     "all_gather", "all_gather_tensor", "all_reduce_sum_", "reduce_tensor",
 ]

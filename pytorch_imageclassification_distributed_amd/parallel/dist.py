@@ -92,6 +92,9 @@ def barrier(ctx: DistContext | None = None) -> None:
 
 
 def destroy() -> None:
+    """Tear down the SyncBN peer channels (IPC mappings, buffers), then the process group."""
+    from .peer import teardown_peer_syncbn
+    teardown_peer_syncbn()
     if dist.is_initialized():
         dist.destroy_process_group()
 

@@ -14,7 +14,11 @@ sums on a side stream (overlapping the consuming conv's weight gradient).
 
 Creation is collective over the group (handles are exchanged with ``all_gather_object``), ends
 with a self-check (three calls against the exact expected sums, both buffer parities), and any
-failure falls back to ``torch.distributed`` (RCCL) with a warning, never to a wrong answer.
+failure falls back to ``torch.distributed`` (RCCL) with a warning, never to a wrong answer.  Once
+training runs, a call that timed out waiting for a peer (``IMGCLS_PEER_TIMEOUT_S``, default 120 s)
+leaves a device error word set: ``check_peer_errors`` (called by the trainer at every log interval
+and epoch end, and by the bench) turns it into an exception, so a run whose statistics may have
+summed stale slots stops instead of training on.
 """
 from __future__ import annotations
 
@@ -87,21 +91,26 @@ class PeerAllReduce:
         The calls wait at most ``timeout_s`` for the peers (a transport whose stores never arrive
         costs seconds, not 3 x the steady-state bound); later calls get ``steady_timeout_s``."""
         n = min(5000, self.max_elems)
-        base = torch.arange(1, n + 1, dtype=torch.float64, device=self.device)
-        want = base * (self.world * (self.world + 1) / 2)
         ok = True
-        self.comm.set_timeout(float(timeout_s))
         try:
-            for k in range(3):
-                t = base * (self.rank + 1) + k
-                self.all_reduce_(t)
-                ok &= bool(torch.equal(t, want + k * self.world))  # syncs: a timed-out call ends the check
-                if not ok:
-                    break
-            torch.cuda.synchronize(self.device)
-            return ok and self.error() == 0
-        finally:
-            self.comm.set_timeout(float(steady_timeout_s))
+            base = torch.arange(1, n + 1, dtype=torch.float64, device=self.device)
+            want = base * (self.world * (self.world + 1) / 2)
+            self.comm.set_timeout(float(timeout_s))
+            try:
+                for k in range(3):
+                    t = base * (self.rank + 1) + k
+                    self.all_reduce_(t)
+                    ok &= bool(torch.equal(t, want + k * self.world))  # syncs: a timed-out call ends the check
+                    if not ok:
+                        break
+                torch.cuda.synchronize(self.device)
+                return ok and self.error() == 0
+            finally:
+                self.comm.set_timeout(float(steady_timeout_s))
+        except Exception as e:  # noqa: BLE001 - a launch / HIP error on this rank is a failed check, so
+            # every rank still reaches the collective agreement that follows (no mismatched collectives)
+            warnings.warn(f"SyncBN peer self-check raised on rank {self.rank}: {e}")
+            return False
 
     def close(self) -> None:
         if self.comm is not None:
@@ -147,22 +156,22 @@ def setup_peer_syncbn(group, device: torch.device, mode: str = "auto") -> bool:
         return False
     world = dist.get_world_size(group)
     tmo = float(os.environ.get("IMGCLS_PEER_TIMEOUT_S", "120"))
+    chans = []
     try:
         from .. import _ext
         if world > int(_ext.load().PEER_MAX_WORLD):  # same answer on every rank
             raise RuntimeError(f"world {world} above the peer kernel's limit")
         if not _same_host(group):
             raise RuntimeError("ranks span several hosts")
-        chans = []
         for _ in range(2):  # forward (compute stream) and backward (side stream) channels
             chans.append(PeerAllReduce(group, device, tmo))
         check_s = float(os.environ.get("IMGCLS_PEER_CHECK_TIMEOUT_S", "15"))
         ok = all([c.self_check(check_s, tmo) for c in chans])
         if not _agree(ok, group, device):  # every rank must agree, or ranks would mix transports
-            for c in chans:
-                c.close()
             raise RuntimeError("self-check failed on some rank")
     except Exception as e:  # noqa: BLE001 - any failure means the torch.distributed path
+        for c in chans:  # channels already mapped (a failure in the second one leaks none)
+            c.close()
         if mode == "peer":
             raise
         warnings.warn(f"SyncBN peer all-reduce disabled, using torch.distributed: {e}")
@@ -185,6 +194,22 @@ def peer_active(group) -> bool:
 def peer_errors() -> int:
     """Sum of the device error words of every channel (timeouts); syncs."""
     return sum(c.error() for chans in _CHANNELS.values() for c in chans)
+
+
+class PeerTimeoutError(RuntimeError):
+    """A SyncBN peer exchange gave up waiting for a peer: its statistics may be wrong."""
+
+
+def check_peer_errors(where: str = "") -> None:
+    """Raise ``PeerTimeoutError`` if any peer call timed out (syncs the device; call it at log
+    intervals, not per step).  The run must stop: the timed-out rank summed whatever the slots held and
+    its call sequence no longer matches its peers'."""
+    if not _CHANNELS:
+        return
+    n = peer_errors()
+    if n:
+        raise PeerTimeoutError(f"SyncBN peer all-reduce timed out waiting for a peer{' (' + where + ')' if where else ''}"
+                               f": {n} channel error word(s) set; the statistics of that step are invalid")
 
 
 def peer_channel(group, which: int):

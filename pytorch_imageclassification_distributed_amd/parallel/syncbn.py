@@ -9,8 +9,11 @@ Here conversion does *not* swap module classes: ``convert_sync_batchnorm``
 tags every ``BatchNorm2d`` with ``sync_group`` so parameter names, state_dict
 keys and ``isinstance`` checks stay those of plain BN.  The tagged module is
 then executed by
-* the HIP path (``ops/hip.py``): fused conv epilogue statistics -> one
-  all-gather of ``[mean, M2, count]`` per layer over RCCL -> fused apply; and
+* the HIP path (``ops/hip.py``): per-channel partial sums from the conv
+  epilogue -> one fp64 exchange of ``[sum, sumsq, count]`` per layer (the
+  one-shot xGMI peer kernel ``csrc/peer.hip`` fused with the finalize, or an
+  RCCL all-reduce) -> coefficients -> apply; backward exchanges ``[sum dz,
+  sum dz*xhat]`` the same way; and
 * the reference path below (ATen ops + ``torch.distributed``), which unlike
   torch's SyncBatchNorm also runs on CPU/gloo (used by the W=2 CPU tests).
 

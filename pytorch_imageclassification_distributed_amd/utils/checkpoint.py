@@ -38,11 +38,34 @@ def ddp_state_dict(model: torch.nn.Module) -> dict:
 
 
 def _rng_state() -> dict:
-    st = {"torch": torch.get_rng_state(), "numpy": np.random.get_state()[1].tolist(),
-          "python": random.getstate()[1]}
+    """Every random stream the trainer draws from, in forms ``torch.load(weights_only=True)`` accepts
+    (tensors, lists, ints, floats): torch CPU / current CUDA device, numpy's MT19937 and Python's."""
+    np_st = np.random.get_state()
+    py_st = random.getstate()
+    st = {"torch": torch.get_rng_state(),
+          "numpy": {"keys": np_st[1].tolist(), "pos": int(np_st[2]), "has_gauss": int(np_st[3]),
+                    "cached_gaussian": float(np_st[4])},
+          "python": {"version": int(py_st[0]), "state": list(py_st[1]),
+                     "gauss_next": None if py_st[2] is None else float(py_st[2])}}
     if torch.cuda.is_available() and torch.cuda.is_initialized():
         st["cuda"] = torch.cuda.get_rng_state()
     return st
+
+
+def restore_rng_state(st: dict) -> None:
+    """Inverse of ``_rng_state`` (resume).  Older checkpoints that stored only the key arrays restore
+    what they have."""
+    if "torch" in st:
+        torch.set_rng_state(st["torch"])
+    if "cuda" in st and torch.cuda.is_available():
+        torch.cuda.set_rng_state(st["cuda"])
+    npst = st.get("numpy")
+    if isinstance(npst, dict):
+        np.random.set_state(("MT19937", np.asarray(npst["keys"], dtype=np.uint32), npst["pos"],
+                             npst["has_gauss"], npst["cached_gaussian"]))
+    pyst = st.get("python")
+    if isinstance(pyst, dict):
+        random.setstate((pyst["version"], tuple(pyst["state"]), pyst["gauss_next"]))
 
 
 def save_checkpoint(path: str, model, epoch: int, best_score: float, optimizer=None,

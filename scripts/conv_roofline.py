@@ -50,8 +50,12 @@ def gemm(A, B_, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(None,
                   2.0 * m * n * k, nb, f"M={m} N={n} K={k} CA={geo[3]}")
 
 
-def wgrad(dy, x, out, g, m, ntot, kps, splits, stages=2):
+def wgrad(dy, x, out, g, m, ntot, kps, splits, stages=2, side=None):
+    # timed on the current stream (the side-stream fork would escape the events); the in-step overlap
+    # is not part of a per-launch roofline
     nb = 2 * (dy.numel() + x.numel()) + 4 * out.numel() * splits
+    if not ON[0]:
+        return _orig_wg(dy, x, out, g, m, ntot, kps, splits, stages, side=side)
     return _timed("wgrad", lambda: _orig_wg(dy, x, out, g, m, ntot, kps, splits, stages), 2.0 * m * g.Co * ntot, nb,
                   f"Co={g.Co} Ntot={ntot} Mpix={m} splits={splits} st={stages}")
 

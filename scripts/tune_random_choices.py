@@ -65,4 +65,4 @@ for t in range(trials):
            "wgrad": [[str(k), str(v)] for k, v in hip._WGRAD_TUNED.items()]}
     out.append(rec)
     print(t, worst, round(cos[worst], 4), "first bad from top:", first_bad, flush=True)
-json.dump(out, open("gpurun_out/dbg_tune_random.json", "w"))
+json.dump(out, open("gpurun_out/tune_random_choices.json", "w"))

@@ -122,3 +122,38 @@ def _model_worker(rank, world, port, out_dir):
 
 def test_peer_syncbn_resnet50_matches_torch_distributed(tmp_path):
     mp.spawn(_model_worker, args=(2, _port(), str(tmp_path)), nprocs=2, join=True)
+
+
+def _timeout_worker(rank, world, port, out_dir):
+    import time
+
+    import torch.distributed as dist
+    from pytorch_imageclassification_distributed_amd.parallel import peer
+    ctx = _init(rank, world, port)
+    os.environ["IMGCLS_PEER_TIMEOUT_S"] = "2"  # steady-state bound for this test: rank 1 arrives late
+    dev = ctx.device
+    grp = dist.group.WORLD
+    assert peer.setup_peer_syncbn(grp, dev, "peer")
+    t = torch.ones(64, dtype=torch.float64, device=dev)
+    if rank == 1:
+        time.sleep(6.0)  # past rank 0's 2 s bound: rank 0's call gives up, sets the error word
+    peer.stats_all_reduce_(t, grp)
+    torch.cuda.synchronize()
+    raised = False
+    try:
+        peer.check_peer_errors("test")
+    except peer.PeerTimeoutError:
+        raised = True
+    with open(os.path.join(out_dir, f"rank{rank}"), "w") as f:
+        f.write("raised" if raised else "clean")
+    peer.teardown_peer_syncbn()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_peer_timeout_is_fatal(tmp_path):
+    """A peer that arrives after the spin bound (IMGCLS_PEER_TIMEOUT_S) makes the waiting rank's call give
+    up with the device error word set; ``check_peer_errors`` (trainer: every log interval and epoch end)
+    must turn that into an exception instead of letting training continue on wrong statistics."""
+    mp.spawn(_timeout_worker, args=(2, _port(), str(tmp_path)), nprocs=2, join=True)
+    assert (tmp_path / "rank0").read_text() == "raised"

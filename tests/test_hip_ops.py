@@ -372,7 +372,15 @@ def test_dense_conv_bn_act():
     x = bf(torch.randn(n, c, hw, hw, device=DEV))
     xb = x.to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
     assert hip.dense_conv_eligible(xb, conv)
-    out = hip.conv_bn_act(xb, conv, bn, "relu", None)
+
+    def no_library_gemm(*a, **k):
+        raise AssertionError("dense conv must run on the in-tree MFMA kernels, not a library GEMM")
+    keep_mm, keep_mat = torch.mm, torch.matmul
+    torch.mm = torch.matmul = no_library_gemm
+    try:
+        out = hip.conv_bn_act(xb, conv, bn, "relu", None)
+    finally:
+        torch.mm, torch.matmul = keep_mm, keep_mat
     xr = x.clone().requires_grad_(True)
     yc = conv_r(xr)
     ref = F.relu(bn_r(yc + (bf(yc) - yc).detach()))
@@ -380,11 +388,56 @@ def test_dense_conv_bn_act():
     assert rel_err(out, ref) < 2e-2
     assert torch.allclose(bn.running_mean, bn_r.running_mean, rtol=1e-2, atol=1e-3)
     g = bf(torch.randn_like(ref))
-    out.backward(g.to(torch.bfloat16).contiguous(memory_format=CL))
+    torch.mm = torch.matmul = no_library_gemm
+    try:
+        out.backward(g.to(torch.bfloat16).contiguous(memory_format=CL))
+    finally:
+        torch.mm, torch.matmul = keep_mm, keep_mat
     ref.backward(g)
     assert rel_err(xb.grad, xr.grad) < 3e-2
     assert rel_err(conv.weight.grad, conv_r.weight.grad) < 3e-2
     assert rel_err(bn.weight.grad, bn_r.weight.grad) < 3e-2
+
+
+def test_weight_shadow_follows_outside_writes():
+    """The conv kernels read bf16 (and transposed / MX) shadows of the fp32 weights that the fused Adam
+    keeps current.  A write to the weights outside the optimizer - load_state_dict between steps, an
+    in-place edit - must reach the next forward and backward (ops/hip.py weight_bf16)."""
+    from pytorch_imageclassification_distributed_amd.engine.optim import FusedAdam
+    hip = _hip()
+    torch.manual_seed(21)
+    conv = nn.Conv2d(64, 64, 3, 1, 1, bias=False).to(DEV).to(memory_format=CL)
+    bn = nn.BatchNorm2d(64).to(DEV)
+    opt = FusedAdam(list(conv.parameters()) + list(bn.parameters()), lr=1e-3)
+    x = bf(torch.randn(4, 64, 14, 14, device=DEV)).to(torch.bfloat16).contiguous(memory_format=CL)
+
+    def step():
+        xb = x.detach().clone().requires_grad_(True)
+        out = hip.conv_bn_act(xb, conv, bn, "relu", None)
+        opt.zero_grad(set_to_none=True)
+        out.float().square().mean().backward()
+        opt.step()
+        return out.detach(), xb.grad.detach()
+
+    step()
+    step()  # the optimizer now owns the shadows (fused refresh)
+    fresh = nn.Conv2d(64, 64, 3, 1, 1, bias=False).to(DEV).to(memory_format=CL)
+    conv.load_state_dict(fresh.state_dict())  # an outside write between steps
+    bn_ref = copy.deepcopy(bn)
+    conv_ref = copy.deepcopy(conv)
+    out, gx = step()
+    xr = x.float().requires_grad_(True)
+    yc = conv_ref(xr)
+    ref = F.relu(bn_ref(yc + (bf(yc) - yc).detach()))
+    ref.square().mean().backward()
+    assert rel_err(out, ref) < 3e-2, "forward used a stale bf16 weight shadow"
+    assert rel_err(gx, xr.grad) < 5e-2, "dgrad used a stale transposed weight shadow"
+    with torch.no_grad():
+        conv.weight.mul_(-1.0)  # in-place edit: bumps the version counter
+    xb = x.detach().clone()
+    out2 = hip.conv_bn_act(xb, conv, copy.deepcopy(bn).eval(), None, None)
+    ref2 = copy.deepcopy(bn).eval()(conv_ref.eval()(x.float()) * -1.0)
+    assert rel_err(out2, ref2) < 3e-2, "in-place weight edit not seen by the next forward"
 
 
 @pytest.mark.parametrize("act,use_res", [("relu", False), ("relu", True), (None, False), ("silu", False)])

@@ -73,3 +73,35 @@ def test_step_timers_metrics_and_profiler(tmp_path):
     trace = json.loads((prof / "trace_rank0.json").read_text())
     names = {e.get("name") for e in trace.get("traceEvents", [])}
     assert {"imgcls::forward", "imgcls::backward", "imgcls::optimizer"} <= names
+
+
+def test_full_resume_continues_the_run(tmp_path):
+    """SURVEY 5.4 full resume: ``latest_model`` carries optimizer, scheduler, RNG and sampler epoch, so
+    'train 1 epoch, stop, resume, train 1 more' reproduces the uninterrupted 2-epoch run."""
+    common = ARGS + ["--latest-every", "1", "--steps-per-epoch", "3", "--val-steps", "1"]
+    full = train.main(common + ["--epochs", "2", "--ckpt-dir", str(tmp_path / "a"), "--resume", "none"])
+    train.main(common + ["--epochs", "1", "--ckpt-dir", str(tmp_path / "b"), "--resume", "none"])
+    lt = load_checkpoint(str(tmp_path / "b" / "resnet18" / "latest_model"))
+    assert lt["sampler_epoch"] == 0 and isinstance(lt["rng"]["numpy"], dict)
+    rest = train.main(common + ["--epochs", "2", "--ckpt-dir", str(tmp_path / "b"), "--resume", "latest"])
+    assert [h["epoch"] for h in rest] == [1]
+    assert rest[0]["train_loss"] == pytest.approx(full[1]["train_loss"], rel=1e-4)
+    assert rest[0]["lr"] == full[1]["lr"]
+
+
+def test_rng_state_roundtrip():
+    import random
+
+    import numpy as np
+
+    from pytorch_imageclassification_distributed_amd.utils import restore_rng_state
+    from pytorch_imageclassification_distributed_amd.utils.checkpoint import _rng_state
+    torch.manual_seed(3)
+    np.random.seed(4)
+    random.seed(5)
+    st = _rng_state()
+    a = (torch.rand(3), np.random.rand(3), random.random(), np.random.randn())
+    torch.rand(7), np.random.rand(5), random.random()
+    restore_rng_state(st)
+    b = (torch.rand(3), np.random.rand(3), random.random(), np.random.randn())
+    assert torch.equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2] and a[3] == b[3]
