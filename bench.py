@@ -27,7 +27,7 @@ import time
 import torch
 import torch.distributed as dist
 
-from pytorch_imageclassification_distributed_amd.data import DeviceSyntheticLoader
+from pytorch_imageclassification_distributed_amd.data import DeviceSyntheticLoader, HostSyntheticLoader
 from pytorch_imageclassification_distributed_amd.engine import Trainer, build_parser
 from pytorch_imageclassification_distributed_amd.parallel import barrier, destroy, init_distributed
 
@@ -64,6 +64,13 @@ def parse():
                    help="replay the whole training step as one captured HIP graph (single process)")
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
                    help="fp8: MX-FP8 forward convolutions (BASELINE config 5); bf16 elsewhere")
+    p.add_argument("--data", default="device", choices=["device", "host"],
+                   help="device: batches generated once in HBM (the step alone); host: pinned uint8 host batches "
+                        "copied by hipMemcpyAsync on a copy stream and normalised on the GPU inside the timed loop "
+                        "(the real-data path minus decode, K24/K25)")
+    p.add_argument("--comm-timing", default="auto", choices=["auto", "on", "off"],
+                   help="per-step device-event timeline of the gradient all-reduce (auto: on when N > 1): "
+                        "overlap window, side-stream tail and exposed collective time in the JSON line")
     return p.parse_args()
 
 
@@ -85,6 +92,32 @@ def _alloc_counters(dev):
     s = torch.cuda.memory_stats(dev)
     return {"device_malloc": s.get("num_device_alloc", 0), "device_free": s.get("num_device_free", 0),
             "alloc_retries": s.get("num_alloc_retries", 0), "ooms": s.get("num_ooms", 0)}
+
+
+def _syncbn_checks(tr, ctx) -> dict:
+    """SyncBN end-of-run checks across the real GPUs: no peer exchange timed out, and every rank holds
+    bitwise the same BN running statistics (each rank sums the same per-rank payloads in rank order, so
+    any transport fault - a stale or torn slot - shows up as a mismatch)."""
+    from pytorch_imageclassification_distributed_amd.parallel import peer_errors
+    out = {"peer_errors": int(peer_errors()) if tr.syncbn_peer else 0}
+    bufs = [b.detach().double().reshape(-1) for n, b in tr.model.named_buffers() if "running_" in n]
+    if bufs:
+        flat = torch.cat(bufs)
+        ref = flat.clone()
+        dist.broadcast(ref, 0)
+        out["syncbn_running_stats_equal_across_ranks"] = bool(torch.equal(ref, flat))
+        ok = torch.tensor([1 if out["syncbn_running_stats_equal_across_ranks"] and not out["peer_errors"] else 0],
+                          dtype=torch.int32, device=flat.device)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        out["syncbn_running_stats_equal_across_ranks"] = bool(ok.item())
+    return out
+
+
+def _from_slowest_rank(extra: dict, dt: float, ctx) -> dict:
+    """The diagnostics of the rank whose timed loop took longest (the one the reported time is from)."""
+    box = [None] * ctx.world_size
+    dist.all_gather_object(box, (dt, extra))
+    return max(box, key=lambda r: r[0])[1]
 
 
 def main():
@@ -109,14 +142,19 @@ def main():
         from pytorch_imageclassification_distributed_amd.ops import hip
         n = hip.load_tuning(tune_db)
         print(f"[bench] rank {ctx.rank}: {n} kernel choices from {tune_db}", file=sys.stderr, flush=True)
-    data = DeviceSyntheticLoader(a.batch, a.num_classes, a.image_size, ctx.device,
-                                 steps=a.warmup + a.steps, ring=2, seed=1234 + ctx.rank)
-    batches = list(iter(data))
+    if a.data == "host":
+        data = HostSyntheticLoader(a.batch, a.num_classes, a.image_size, ctx.device,
+                                   steps=a.warmup + a.steps + 1, ring=2, seed=1234 + ctx.rank)
+        host_it = iter(data)
+    else:
+        data = DeviceSyntheticLoader(a.batch, a.num_classes, a.image_size, ctx.device,
+                                     steps=a.warmup + a.steps, ring=2, seed=1234 + ctx.rank)
+        batches = list(iter(data))
 
     use_graph = a.graph == "on" and a.compute == "hip" and ctx.world_size == 1
 
     def step(i):
-        b = batches[i]
+        b = next(host_it) if a.data == "host" else batches[i]
         if use_graph and i >= 2:  # two eager steps tune every kernel shape, then capture / replay
             loss = tr.graph_step(b["image"], b["label"])
         else:
@@ -134,6 +172,10 @@ def main():
     print(f"[bench] rank {ctx.rank}: host enqueue {t_host * 1e3:.1f} ms/step", file=sys.stderr, flush=True)
     if not torch.isfinite(last).item():
         raise FloatingPointError(f"non-finite loss in warmup: {last.item()}")
+    comm_t = None
+    if a.comm_timing == "on" or (a.comm_timing == "auto" and ctx.world_size > 1):
+        from pytorch_imageclassification_distributed_amd.parallel import comm_timer
+        comm_t = comm_timer.install()
     barrier(ctx)
     torch.cuda.synchronize()
     m0 = _alloc_counters(ctx.device)
@@ -155,9 +197,19 @@ def main():
     if a.tune_save and ctx.rank == 0:
         from pytorch_imageclassification_distributed_amd.ops import hip
         print(f"[bench] saved {hip.save_tuning(a.tune_save)} kernel choices to {a.tune_save}", file=sys.stderr)
+    extra = {}
+    if comm_t is not None:
+        from pytorch_imageclassification_distributed_amd.parallel import comm_timer
+        comm_timer.uninstall()
+        extra.update(comm_t.summary())  # rank-local means; reported for the slowest rank below
+        if tr.reducer is not None:
+            extra["bucket_mb"] = [round(v, 2) for v in tr.reducer.bucket_sizes_mb()]
+    if sync_bn and ctx.world_size > 1:
+        extra.update(_syncbn_checks(tr, ctx))
     t = torch.tensor([dt], dtype=torch.float64, device=ctx.device)
     if ctx.world_size > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        extra = _from_slowest_rank(extra, dt, ctx)
     dt = float(t.item())
     loss_val = float(last.item())
     if ctx.rank == 0:
@@ -171,13 +223,17 @@ def main():
             "n_gpus": ctx.world_size, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": round(value / base, 4) if base else None,
-            "dtype": a.dtype, "data": "synthetic (on-device random images, random-init weights)",
+            "dtype": a.dtype,
+            "data": ("synthetic (on-device random images, random-init weights)" if a.data == "device" else
+                     "synthetic (pinned uint8 host batches, H2D copy + normalisation in the timed loop, "
+                     "random-init weights)"),
             "config": {"model": a.model, "global_batch": a.batch * ctx.world_size,
                        "per_gpu_batch": a.batch, "seq_len": None, "image_size": a.image_size,
                        "num_classes": a.num_classes, "parallelism": f"dp{ctx.world_size}",
                        "sync_bn": sync_bn, "syncbn_comm": ("peer" if tr.syncbn_peer else "rccl") if sync_bn else None,
                        "compute": a.compute, "optimizer": "adam", "hip_graph": use_graph,
                        "final_loss": round(loss_val, 5)},
+            **extra,
         }), flush=True)
     destroy()
     return 0

@@ -22,7 +22,8 @@ using OT = std::optional<Tensor>;
 int bn_partials_launch(float*, int, int, double*, float*, float*, double, hipStream_t);
 int bn_reduce_finalize_launch(float*, int, int, double, const float*, const float*, float*, float*, long long*, float,
                               float, float*, hipStream_t);
-int bn_reduce_bwd_launch(float*, int, int, double, float*, float*, float*, hipStream_t);
+int bn_reduce_bwd_launch(float*, int, int, double, float*, float*, float*, const float*, float*, hipStream_t);
+int bn_xa_coef_launch(const float*, const float*, int, float*, hipStream_t);
 int bn_finalize_launch(const double*, const double*, double, const float*, const float*, float*, float*,
                        long long*, float, float, int, float*, hipStream_t);
 int bn_eval_coef_launch(const float*, const float*, const float*, const float*, float, int, float*, hipStream_t);
@@ -155,7 +156,7 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
                int IH, int IW, int sA, int ldb, int OH, int OW, int so, int oh0, int ow0, int ldc, int c_off,
                std::vector<int> dh, std::vector<int> dw, std::vector<int> tb, int stats_groups, Tensor zero,
                OT addend, OT bwd_y, OT bwd_res, OT bwd_coef, OT bwd_part, int bwd_act, int bwd_groups,
-               int stages, int tile_n, int cfg, OT a_sc, OT b_sc) {
+               int stages, int tile_n, int cfg, OT a_sc, OT b_sc, OT xa_y, OT xa_coef, OT xa_out) {
   const bool fp8 = a_sc.has_value() && a_sc->defined();
   TORCH_CHECK(A.scalar_type() == (fp8 ? at::kFloat8_e4m3fn : BF) && B.scalar_type() == A.scalar_type(),
               "conv_gemm: A and B must both be bf16, or both float8_e4m3fn with scales");
@@ -208,12 +209,22 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
     TORCH_CHECK(!p.bwd_res || bwd_res->numel() == C.numel(), "conv_gemm: bwd_res must match C");
   }
   if (p.addend) TORCH_CHECK(addend->numel() == C.numel() && addend->scalar_type() == BF, "conv_gemm: addend must match C");
+  p.xa_y = optr<bf16_t>(xa_y);
+  p.xa_coef = optr<float>(xa_coef);
+  p.xa_out = optr<bf16_t>(xa_out);
+  if (p.xa_y) {
+    TORCH_CHECK(!fp8 && xa_y->numel() == A.numel() && p.xa_coef && xa_coef->numel() >= 3LL * CA,
+                "conv_gemm: the fused BN-backward A operand needs y matching A and [3][CA] coefficients");
+    TORCH_CHECK(!p.xa_out || (xa_out->numel() == A.numel() && xa_out->scalar_type() == BF),
+                "conv_gemm: xa_out must match A");
+    TORCH_CHECK(cfg < 0 || conv_cfg_has_xa(cfg), "conv_gemm: configuration has no fused BN-backward variant");
+  }
   check(conv_gemm_launch(p, cur()), "conv_gemm");
 }
 
 void conv_wgrad(Tensor dY, Tensor X, Tensor dW, int M, int Cout, int Cin, int Ntot, int OH, int OW, int IH, int IW,
                 int sh, int sw, int pt, int pl, int dh, int dwd, int KW, int k_per_split, int splits, Tensor zero,
-                int stages, OT ws, int64_t side) {
+                int stages, OT ws, int64_t side, OT xa_y, OT xa_coef) {
   req(dY, BF, "dY"); req(X, BF, "X"); req(dW, F32, "dW");
   TORCH_CHECK(Cin % 8 == 0 && Cout % 8 == 0, "conv_wgrad: channels must be multiples of 8");
   TORCH_CHECK(k_per_split % 64 == 0, "conv_wgrad: k_per_split must be a multiple of 64");
@@ -239,6 +250,13 @@ void conv_wgrad(Tensor dY, Tensor X, Tensor dW, int M, int Cout, int Cin, int Nt
                 "conv_wgrad: workspace must be fp32 [>= splits*Cout*Ntot] with a contiguous dW");
     p.ws = ws->data_ptr<float>();
   }
+  p.xa_y = optr<bf16_t>(xa_y);
+  p.xa_coef = optr<float>(xa_coef);
+  if (p.xa_y) {
+    TORCH_CHECK(xa_y->numel() == dY.numel() && p.xa_coef && xa_coef->numel() >= 3LL * Cout && Cout % 8 == 0,
+                "conv_wgrad: the fused BN-backward dY needs y matching dY and [3][Cout] coefficients");
+    TORCH_CHECK(conv_wgrad_has_xa(stages), "conv_wgrad: this ring / tile variant has no fused BN-backward form");
+  }
   if (side == 0) {
     check(conv_wgrad_launch(p, splits, cur()), "conv_wgrad");
     return;
@@ -250,6 +268,10 @@ void conv_wgrad(Tensor dY, Tensor X, Tensor dW, int M, int Cout, int Cin, int Nt
   record_on(dY, s);
   record_on(X, s);
   if (p.ws) record_on(*ws, s);
+  if (p.xa_y) {
+    record_on(*xa_y, s);
+    record_on(*xa_coef, s);
+  }
 }
 
 void bn_partials(Tensor part, int G, int C, Tensor sums, OT dgamma, OT dbeta, double count) {
@@ -279,12 +301,21 @@ void bn_reduce_finalize(Tensor part, int G, int C, double count, OT gamma, OT be
         "bn_reduce_finalize");
 }
 
-void bn_reduce_bwd(Tensor part, int G, int C, double count, OT dgamma, OT dbeta, Tensor k) {
+void bn_reduce_bwd(Tensor part, int G, int C, double count, OT dgamma, OT dbeta, Tensor k, OT coef, OT xa) {
   req(part, F32, "part"); req(k, F32, "k");
   TORCH_CHECK(part.numel() >= (int64_t)G * 2 * C && k.numel() >= 2 * C, "bn_reduce_bwd: buffer sizes");
+  const bool fx = xa.has_value() && xa->defined();
+  TORCH_CHECK(!fx || (coef.has_value() && coef->numel() >= 4LL * C && xa->numel() >= 3LL * C),
+              "bn_reduce_bwd: the fused form needs coef [4][C] and xa [3][C]");
   check(bn_reduce_bwd_launch(ptr<float>(part), G, C, count, optr<float>(dgamma), optr<float>(dbeta), ptr<float>(k),
-                             cur()),
+                             fx ? ptr<float>(*coef) : nullptr, fx ? ptr<float>(*xa) : nullptr, cur()),
         "bn_reduce_bwd");
+}
+
+void bn_xa_coef(Tensor coef, Tensor k, int C, Tensor xa) {
+  req(coef, F32, "coef"); req(k, F32, "k"); req(xa, F32, "xa");
+  TORCH_CHECK(coef.numel() >= 4LL * C && k.numel() >= 2LL * C && xa.numel() >= 3LL * C, "bn_xa_coef: sizes");
+  check(bn_xa_coef_launch(ptr<float>(coef), ptr<float>(k), C, ptr<float>(xa), cur()), "bn_xa_coef");
 }
 
 void bn_eval_coef(OT gamma, OT beta, Tensor rmean, Tensor rvar, double eps, int C, Tensor coef) {
@@ -795,7 +826,8 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("IH"), pybind11::arg("IW"), pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("pt"),
         pybind11::arg("pl"), pybind11::arg("dh"), pybind11::arg("dwd"), pybind11::arg("KW"),
         pybind11::arg("k_per_split"), pybind11::arg("splits"), pybind11::arg("zero"), pybind11::arg("stages"),
-        pybind11::arg("ws") = pybind11::none(), pybind11::arg("side") = 0);
+        pybind11::arg("ws") = pybind11::none(), pybind11::arg("side") = 0, pybind11::arg("xa_y") = pybind11::none(),
+        pybind11::arg("xa_coef") = pybind11::none());
   m.def("conv_set_variant", &conv_set_variant);
   m.def("set_deterministic", [](bool v) { set_deterministic(v ? 1 : 0); });
   m.def("set_force_div64", [](bool v) { set_force_div64(v ? 1 : 0); });
@@ -805,7 +837,10 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("sums"), pybind11::arg("dgamma"), pybind11::arg("dbeta"), pybind11::arg("count") = -1.0);
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_reduce_finalize", &bn_reduce_finalize);
-  m.def("bn_reduce_bwd", &bn_reduce_bwd);
+  m.def("bn_reduce_bwd", &bn_reduce_bwd, pybind11::arg("part"), pybind11::arg("G"), pybind11::arg("C"),
+        pybind11::arg("count"), pybind11::arg("dgamma"), pybind11::arg("dbeta"), pybind11::arg("k"),
+        pybind11::arg("coef") = pybind11::none(), pybind11::arg("xa") = pybind11::none());
+  m.def("bn_xa_coef", &bn_xa_coef);
   m.def("bn_eval_coef", &bn_eval_coef);
   m.def("bn_apply", &bn_apply, pybind11::arg("y"), pybind11::arg("coef"), pybind11::arg("res"), pybind11::arg("out"),
         pybind11::arg("rows"), pybind11::arg("C"), pybind11::arg("ldo"), pybind11::arg("c_off"), pybind11::arg("act"),
@@ -855,6 +890,8 @@ PYBIND11_MODULE(_C, m) {
     }
     return out;
   });
+  m.def("conv_cfg_has_xa", &conv_cfg_has_xa);
+  m.def("conv_wgrad_has_xa", &conv_wgrad_has_xa);
   m.def("conv_cfgs", []() {
     std::vector<std::vector<int>> out;
     for (int i = 0; i < conv_num_cfgs(); ++i) {

@@ -111,10 +111,21 @@ __global__ __launch_bounds__(256) void bn_reduce_finalize_kernel(BnFinalizeArgs 
   }
 }
 
-// backward: (sum dz, sum dz*xhat) -> dbeta, dgamma and k = sums / n for bn_bwd_elemt
+// Fused BN-backward elementwise as an affine map of (dz, y) per channel, for the consumers that apply it
+// on their operand loads (conv_gemm.hip XA): dy = scale * (dz - k1 - (y - mean) * invstd * k2)
+//   = xa[0] * dz + xa[1] * y + xa[2],   xa = [scale | -scale*invstd*k2 | scale*(invstd*k2*mean - k1)]
+DEVI void bn_xa_coef_one(const float* coef, int C, int c, double k1, double k2, float* xa) {
+  const double sc = coef[c], mu = coef[2 * C + c], is = coef[3 * C + c];
+  xa[c] = (float)sc;
+  xa[C + c] = (float)(-sc * is * k2);
+  xa[2 * C + c] = (float)(sc * (is * k2 * mu - k1));
+}
+
+// backward: (sum dz, sum dz*xhat) -> dbeta, dgamma and k = sums / n for bn_bwd_elemt (+ the fused form)
 __global__ __launch_bounds__(256) void bn_reduce_bwd_kernel(float* part, int G, int C, double count,
                                                             float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                            float* __restrict__ kout) {
+                                                            float* __restrict__ kout, const float* __restrict__ coef,
+                                                            float* __restrict__ xa) {
   __shared__ double red[2][4][64];
   const int lc = threadIdx.x & 63, lg = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lc;
@@ -125,6 +136,14 @@ __global__ __launch_bounds__(256) void bn_reduce_bwd_kernel(float* part, int G, 
   if (dgamma) dgamma[c] = (float)q;
   kout[c] = (float)(s / count);
   kout[C + c] = (float)(q / count);
+  if (xa) bn_xa_coef_one(coef, C, c, s / count, q / count, xa);
+}
+
+// the fused form from k (SyncBN paths, where k comes from the exchange)
+__global__ void bn_xa_coef_kernel(const float* __restrict__ coef, const float* __restrict__ k, int C,
+                                  float* __restrict__ xa) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < C) bn_xa_coef_one(coef, C, c, k[c], k[C + c], xa);
 }
 
 // ---- fp64 sums -> coefficients, running stats -----------------------------
@@ -767,8 +786,15 @@ int bn_reduce_finalize_launch(float* part, int G, int C, double count, const flo
 }
 
 int bn_reduce_bwd_launch(float* part, int G, int C, double count, float* dgamma, float* dbeta, float* k,
-                         hipStream_t s) {
-  hipLaunchKernelGGL(bn_reduce_bwd_kernel, dim3(cdiv(C, 64)), dim3(256), 0, s, part, G, C, count, dgamma, dbeta, k);
+                         const float* coef, float* xa, hipStream_t s) {
+  hipLaunchKernelGGL(bn_reduce_bwd_kernel, dim3(cdiv(C, 64)), dim3(256), 0, s, part, G, C, count, dgamma, dbeta, k,
+                     coef, xa);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int bn_xa_coef_launch(const float* coef, const float* k, int C, float* xa, hipStream_t s) {
+  hipLaunchKernelGGL(bn_xa_coef_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, coef, k, C, xa);
   HIP_CHECK_LAUNCH();
   return 0;
 }

@@ -87,5 +87,7 @@ int conv_num_cfgs();
 int conv_num_fp8_cfgs();
 void conv_fp8_cfg_info(int i, int* out5);
 void conv_cfg_info(int i, int* out5);  // {tile rows, tile channels, waves M, waves N, ring depth}
+bool conv_cfg_has_xa(int i);           // configuration i has a fused BN-backward A-operand variant
 int conv_wgrad_launch(const WgradParams& p, int splits, hipStream_t stream);
+bool conv_wgrad_has_xa(int stages);  // the wgrad variant selected by ``stages`` has a fused BN-backward dY form
 void conv_set_wgrad_variant(int v);  // 0 = auto, 1 = register-staged, 2 = LDS-DMA

@@ -556,7 +556,7 @@ struct GldsCfg {
   static constexpr int BLOCKS = (160 * 1024) / (MAIN + 3 * CONV_MAX_TAPS * 4);
   static constexpr int OCC_LDS = BLOCKS * NW / 4 < 1 ? 1 : (BLOCKS * NW / 4 > 4 ? 4 : BLOCKS * NW / 4);
   static constexpr int EST_VGPR = (TM / WM) * (BN / WN) / 64 + 4 * (TM / WM / 16 + BN / WN / 16) +
-                                  4 * (TM / 8 / NW) + 2 * (BN / 8 / NW) + 48 + (XA ? 5 * (TM / 8 / NW) : 0);
+                                  4 * (TM / 8 / NW) + 2 * (BN / 8 / NW) + 48;
   static constexpr int OCC_REG = 512 / EST_VGPR < 1 ? 1 : 512 / EST_VGPR;
   static constexpr int OCC = OCC_LDS < OCC_REG ? OCC_LDS : OCC_REG;
 };
@@ -584,16 +584,17 @@ DEVI int tap_tb(int pk) { return (int)((unsigned)pk >> 16); }
 // PRIO: s_setprio(1) around each k-half's MFMA cluster (guide T5: keeps hipcc from moving MFMAs across
 // the barrier in among the loads); a separate table entry, chosen per shape by the tuner
 //
-// XA (fused BatchNorm-backward elementwise): the data gradient of a 1x1 stride-1 conv whose
-// output y fed a BN reads dz (the BN's pre-elementwise gradient, written by the consumer conv's dgrad
-// epilogue) as its A operand and finishes the BN backward on the way into the MFMAs:
+// XA (fused BatchNorm-backward elementwise): the data gradient of a conv whose output y fed a
+// BN reads dz (the BN's pre-elementwise gradient, written by the consumer conv's dgrad epilogue) as its
+// A operand and finishes the BN backward on the way into the MFMAs:
 //   dY = c0 * dz + c1 * y + c2   per A column (channel),   instead of a separate bn_bwd_elemt pass that
 // reads dz and y and writes dY (which this kernel and the weight gradient would read again).  Each wave
 // transforms the A pieces it DMA'd itself, right after its own vmcnt wait and before the barrier that
 // publishes the stage: y arrives by a plain buffer load issued with the DMA (same offsets, zeros out of
-// range), the stage's 3 x 64 coefficients by a per-wave LDS-DMA.  1x1 stride-1 only: every valid row's
-// A piece is in bounds, so no padding masks (rows past M never reach the output).  Rings of <= 2 stages
-// (every k-step drains vmcnt to 0 before the barrier, so the register load costs no pipelining).
+// range), the stage's 3 x 64 coefficients by a per-wave LDS-DMA.  Pieces whose gather fell into the zero
+// padding (or rows past M) keep the zeros the DMA landed - dY of a padded tap is 0, not c2.  Uniform
+// k-steps (CA % 64 == 0); rings of <= 2 stages (every k-step drains vmcnt to 0 before the barrier, so
+// the register load costs no pipelining).
 template <int TM, int BN, int WM, int WN, int STAGES, bool TAP_UNIFORM, int PRIO = 0, bool XA = false>
 __global__ __launch_bounds__((GldsCfg<TM, BN, WM, WN, STAGES, XA>::NTH), (GldsCfg<TM, BN, WM, WN, STAGES, XA>::OCC))
 void conv_gemm_glds_kernel(const ConvParams p) {
@@ -757,32 +758,31 @@ void conv_gemm_glds_kernel(const ConvParams p) {
     if constexpr (XA) {
       char* sa = smem + buf * STAGE;
       const float* kc = (const float*)(sa + Cfg::A_BYTES + Cfg::B_BYTES + wid * 1024);
-      float c0[2][8], c1[2][8], c2[2][8];
+      const bool wr = p.xa_out != nullptr && n0 == 0;
+      // even pieces share channel chunk xa_ch0, odd ones xa_ch1: one coefficient set live at a time
 #pragma unroll
       for (int g = 0; g < 2; ++g) {
         const int ch = (g ? xa_ch1 : xa_ch0) * 8;
+        float c0[8], c1[8], c2[8];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const f32x4 a = *(const f32x4*)(kc + ch + 4 * h);
-          const f32x4 b = *(const f32x4*)(kc + 64 + ch + 4 * h);
-          const f32x4 c = *(const f32x4*)(kc + 128 + ch + 4 * h);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) { c0[g][4 * h + k] = a[k]; c1[g][4 * h + k] = b[k]; c2[g][4 * h + k] = c[k]; }
+          *(f32x4*)(c0 + 4 * h) = *(const f32x4*)(kc + ch + 4 * h);
+          *(f32x4*)(c1 + 4 * h) = *(const f32x4*)(kc + 64 + ch + 4 * h);
+          *(f32x4*)(c2 + 4 * h) = *(const f32x4*)(kc + 128 + ch + 4 * h);
         }
-      }
-      const bool wr = p.xa_out != nullptr && n0 == 0;
 #pragma unroll
-      for (int i = 0; i < AL; ++i) {
-        const int g = i & 1;
-        uint4* dst = (uint4*)(sa + (wid * (TM / NW) + i * 8) * 128 + lane * 16);
-        float d[8], y[8];
-        unpack8(*dst, d);
-        unpack8(xa_y[i], y);
+        for (int i = g; i < AL; i += 2) {
+          if (xa_va[i] == OOB) continue;  // zero padding / rows past M: the DMA landed zeros, dY is 0 there
+          uint4* dst = (uint4*)(sa + (wid * (TM / NW) + i * 8) * 128 + lane * 16);
+          float d[8], y[8];
+          unpack8(*dst, d);
+          unpack8(xa_y[i], y);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) d[k] = fmaf(c0[g][k], d[k], fmaf(c1[g][k], y[k], c2[g][k]));
-        const uint4 v = pack8(d);
-        *dst = v;
-        if (wr && xa_va[i] != OOB) *(uint4*)(p.xa_out + (long)n_img0 * img + (xa_va[i] >> 1)) = v;
+          for (int k = 0; k < 8; ++k) d[k] = fmaf(c0[k], d[k], fmaf(c1[k], y[k], c2[k]));
+          const uint4 v = pack8(d);
+          *dst = v;
+          if (wr) *(uint4*)(p.xa_out + (long)n_img0 * img + (xa_va[i] >> 1)) = v;
+        }
       }
       (void)ci;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1239,15 +1239,19 @@ DEVI int wswz(int row) {
 // LDS before the atomics).  Split-K partial tiles leave through fp32 atomics (~1.3 TB/s chip-wide):
 // the atomic bytes of a launch are blocks x tile bytes, so the 256 x 256 tile at one block per CU
 // moves fewer of them than many small-tile blocks while running the more efficient 8-wave loop.
-template <int WBM, int TN, int WM, int WN, int KG, int STAGES, int BKP = WBK>
+template <int WBM, int TN, int WM, int WN, int KG, int STAGES, int BKP = WBK, bool XA = false>
 struct WgCfg {
   static constexpr int NW = WM * WN * KG, NTH = 64 * NW;
   static constexpr int AROWB = WBM * 2, BROWB = TN * 2;
-  static constexpr int STAGE = BKP * KG * (AROWB + BROWB);
+  // XA with >= 3 stages: y arrives by LDS-DMA into its own image behind B (a VGPR-destination load beside
+  // DMAs kept in flight across barriers would be waited for with vmcnt(0)); <= 2 stages: by register load
+  static constexpr bool YLDS = XA && STAGES >= 3;
+  static constexpr int STAGE = BKP * KG * (AROWB + BROWB) + (YLDS ? BKP * KG * AROWB : 0);
   static constexpr int LDT = TN + 4;
   static constexpr int EPI = (KG == 2 ? WBM : WBM / WM) * LDT * 4;  // staged fp32 rows
   static constexpr int MAIN = STAGES * STAGE > EPI ? STAGES * STAGE : EPI;
-  static constexpr int BLOCKS = (160 * 1024) / MAIN;
+  static constexpr int XA_BYTES = XA ? 12 * WBM : 0;  // fused BN-backward coefficients [3][WBM] fp32
+  static constexpr int BLOCKS = (160 * 1024) / (MAIN + XA_BYTES);
   static constexpr int OCC0 = BLOCKS * NW / 4 < 1 ? 1 : (BLOCKS * NW / 4 > 3 ? 3 : BLOCKS * NW / 4);
   static constexpr int ACC = (WBM / WM) * (TN / WN) / 64;
   static constexpr int OCC = ACC >= 128 ? (OCC0 < 2 ? OCC0 : 2) : OCC0;
@@ -1255,11 +1259,15 @@ struct WgCfg {
 
 // BKP = pixels per k-group per stage: 64, or 32 for a deeper ring of smaller stages (a 4-deep ring of
 // 32-pixel stages keeps two stages in flight across each barrier at the LDS size of a 2-deep 64 ring).
-template <int WBM, int TN, int WM, int WN, int KG, int STAGES, int BKP = WBK>
-__global__ __launch_bounds__((WgCfg<WBM, TN, WM, WN, KG, STAGES, BKP>::NTH),
-                             (WgCfg<WBM, TN, WM, WN, KG, STAGES, BKP>::OCC))
+// XA: dY holds dz and the fused BN-backward elementwise dY = c0*dz + c1*y + c2 (per output channel co) is
+// applied by each wave to the dz pieces it DMA'd, after its own vmcnt wait and before the barrier that
+// publishes the stage (as conv_gemm_glds_kernel's XA); y comes by a plain buffer load issued with the
+// DMA, the block's [3][WBM] coefficients sit in LDS.  Pixel rows past the split's end stay zero.
+template <int WBM, int TN, int WM, int WN, int KG, int STAGES, int BKP = WBK, bool XA = false>
+__global__ __launch_bounds__((WgCfg<WBM, TN, WM, WN, KG, STAGES, BKP, XA>::NTH),
+                             (WgCfg<WBM, TN, WM, WN, KG, STAGES, BKP, XA>::OCC))
 void conv_wgrad_glds_kernel(const WgradParams p) {
-  using Cfg = WgCfg<WBM, TN, WM, WN, KG, STAGES, BKP>;
+  using Cfg = WgCfg<WBM, TN, WM, WN, KG, STAGES, BKP, XA>;
   constexpr int NW = Cfg::NW;
   constexpr int NTH = Cfg::NTH;
   constexpr int AROWB = Cfg::AROWB;         // A image row bytes (128 / 256 / 512)
@@ -1277,8 +1285,10 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
   constexpr int LDT = Cfg::LDT;             // floats per staged epilogue row
   constexpr int MAIN = Cfg::MAIN;
   static_assert(AL >= 1 && BL >= 1 && AL * ARPI * NW == KPS && BL * BRPI * NW == KPS, "loader mapping");
-  static_assert(MAIN <= 160 * 1024, "LDS budget");
-  __shared__ __attribute__((aligned(16))) char smem[MAIN];
+  static_assert(MAIN + Cfg::XA_BYTES <= 160 * 1024, "LDS budget");
+  constexpr bool YLDS = Cfg::YLDS;
+  constexpr int LPS = AL + BL + (YLDS ? AL : 0);  // LDS-DMA instructions per wave per stage
+  __shared__ __attribute__((aligned(16))) char smem[MAIN + Cfg::XA_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1341,6 +1351,18 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
 #pragma unroll
   for (int i = 0; i < AL; ++i)
     a_off[i] = a_cok[i] ? 2u * (unsigned)(((wid * AL + i) * ARPI + a_lr) * p.Cout + a_col[i]) : OOB;
+  // XA: the block's coefficient table and y's resource (same base / extent as rsY)
+  __amdgpu_buffer_rsrc_t rsZ;
+  uint4 xa_y[XA && !YLDS ? AL : 1];
+  float* const s_xa = (float*)(smem + MAIN);
+  if constexpr (XA) {
+    rsZ = make_rsrc(p.xa_y + (long)kbeg * p.Cout, 2L * (kend - kbeg) * p.Cout);
+    for (int t = tid; t < 3 * WBM; t += NTH) {
+      const int arr = t / WBM, co = co0 + (t - arr * WBM);
+      s_xa[t] = co < p.Cout ? p.xa_coef[arr * p.Cout + co] : 0.f;
+    }
+    __syncthreads();
+  }
   int b_m[BL], b_n[BL], b_oh[BL], b_ow[BL];
 #pragma unroll
   for (int i = 0; i < BL; ++i) {
@@ -1380,6 +1402,44 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
     for (int i = 0; i < AL; ++i) blds16(rsY, va[i], sa + (wid * AL + i) * 1024);
 #pragma unroll
     for (int i = 0; i < BL; ++i) blds16(rsX, vb[i], sb + (wid * BL + i) * 1024);
+    if constexpr (YLDS) {
+#pragma unroll
+      for (int i = 0; i < AL; ++i) blds16(rsZ, va[i], sb + KPS * BROWB + (wid * AL + i) * 1024);
+    } else if constexpr (XA) {
+#pragma unroll
+      for (int i = 0; i < AL; ++i) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsZ, va[i], 0, 0);
+        xa_y[i] = *(const uint4*)&v;
+      }
+    }
+  };
+  // XA: this wave's dz pieces of stage kt (waited for) -> dY in place; rows past kend stay zero
+  auto xa_transform = [&](int buf, int kt) {
+    if constexpr (XA) {
+      char* sa = smem + buf * STAGE;
+#pragma unroll
+      for (int i = 0; i < AL; ++i) {
+        const int pix = kbeg + kt * KPS + (wid * AL + i) * ARPI + a_lr;
+        if (!a_cok[i] || pix >= kend) continue;
+        const int j = a_col[i] - co0;
+        float c0[8], c1[8], c2[8];
+        *(f32x4*)c0 = *(const f32x4*)(s_xa + j);
+        *(f32x4*)(c0 + 4) = *(const f32x4*)(s_xa + j + 4);
+        *(f32x4*)c1 = *(const f32x4*)(s_xa + WBM + j);
+        *(f32x4*)(c1 + 4) = *(const f32x4*)(s_xa + WBM + j + 4);
+        *(f32x4*)c2 = *(const f32x4*)(s_xa + 2 * WBM + j);
+        *(f32x4*)(c2 + 4) = *(const f32x4*)(s_xa + 2 * WBM + j + 4);
+        uint4* dst = (uint4*)(sa + (wid * AL + i) * 1024 + lane * 16);
+        float d[8], y[8];
+        unpack8(*dst, d);
+        if constexpr (YLDS) unpack8(*(const uint4*)(sa + A_BYTES + KPS * BROWB + (wid * AL + i) * 1024 + lane * 16), y);
+        else unpack8(xa_y[i], y);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) d[k] = fmaf(c0[k], d[k], fmaf(c1[k], y[k], c2[k]));
+        *dst = pack8(d);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
   };
 
   f32x4 acc[RM][RN];
@@ -1419,12 +1479,14 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
       if (kt > 0) __builtin_amdgcn_s_barrier();
       issue(0);
       wait_vmcnt<0>();
+      xa_transform(0, kt);
       __builtin_amdgcn_s_barrier();
     } else {
       // stage kt landed; the STAGES-2 younger stages stay in flight across the barrier, which also
       // retires every wave's reads of the slot the next issue overwrites
-      if (kt + STAGES - 2 < nk) wait_vmcnt<(STAGES - 2) * (AL + BL)>();
+      if (kt + STAGES - 2 < nk) wait_vmcnt<(STAGES - 2) * LPS>();
       else wait_vmcnt<0>();
+      xa_transform(kt % STAGES, kt);
       __builtin_amdgcn_s_barrier();
     }
     const char* sa = smem + (STAGES == 1 ? 0 : (kt % STAGES) * STAGE);
@@ -1577,6 +1639,14 @@ static void launch_glds(const ConvParams& p, hipStream_t stream) {
     hipLaunchKernelGGL((conv_gemm_glds_kernel<TM, BN, WM, WN, STAGES, false, PRIO>), dim3(grid), dim3(NTH), 0, stream, p);
 }
 
+// fused BN-backward A-operand variant (XA, host-checked: 1x1 stride-1 geometry, CA % 64 == 0)
+template <int TM, int BN, int WM, int WN, int STAGES, int PRIO = 0>
+static void launch_glds_xa(const ConvParams& p, hipStream_t stream) {
+  const int grid = cdiv(p.M, TM) * cdiv(p.Ncols, BN);
+  hipLaunchKernelGGL((conv_gemm_glds_kernel<TM, BN, WM, WN, STAGES, true, PRIO, true>), dim3(grid),
+                     dim3(64 * WM * WN), 0, stream, p);
+}
+
 template <int BN>
 static void launch_bn(const ConvParams& p, int gm, hipStream_t stream) {
   const int v = g_variant == 0 ? 2 : g_variant;  // measured: 2-stage LDS-DMA wins (benchmarks/conv_bench.py --variants)
@@ -1593,9 +1663,14 @@ static void launch_bn(const ConvParams& p, int gm, hipStream_t stream) {
 
 // Tuned configurations (the per-shape "find" step in ops/hip.py times these on scratch outputs):
 // {tile rows, tile channels, waves along rows, waves along channels, LDS-DMA ring depth}.
-struct ConvCfg { int tm, bn, wm, wn, st; void (*launch)(const ConvParams&, hipStream_t); };
-#define CFG(TM, BN, WM, WN, ST) {TM, BN, WM, WN, ST, &launch_glds<TM, BN, WM, WN, ST>}
-#define CFGP(TM, BN, WM, WN, ST) {TM, BN, WM, WN, ST, &launch_glds<TM, BN, WM, WN, ST, 1>}
+struct ConvCfg {
+  int tm, bn, wm, wn, st;
+  void (*launch)(const ConvParams&, hipStream_t);
+  void (*launch_xa)(const ConvParams&, hipStream_t);  // fused BN-backward A operand, or null
+};
+#define CFG(TM, BN, WM, WN, ST) {TM, BN, WM, WN, ST, &launch_glds<TM, BN, WM, WN, ST>, &launch_glds_xa<TM, BN, WM, WN, ST>}
+#define CFGP(TM, BN, WM, WN, ST) {TM, BN, WM, WN, ST, &launch_glds<TM, BN, WM, WN, ST, 1>, &launch_glds_xa<TM, BN, WM, WN, ST, 1>}
+#define CFGN(TM, BN, WM, WN, ST) {TM, BN, WM, WN, ST, &launch_glds<TM, BN, WM, WN, ST>, nullptr}
 // Measured on the ResNet-50 layers at batch 512 (benchmarks/conv_bench.py --tune-log): the 128-row
 // 4-wave tiles win on 64/128-channel outputs and short K (occupancy hides latency); the 256x256
 // 8-wave tiles (2 waves per SIMD, 64x128 or 128x64 per wave, half the LDS-DMA bytes per FLOP) win
@@ -1604,7 +1679,7 @@ static const ConvCfg g_cfgs[] = {
     CFG(128, 64, 2, 2, 1),  CFG(128, 128, 2, 2, 1), CFG(128, 64, 2, 2, 2), CFG(128, 128, 2, 2, 2),
     CFG(256, 256, 2, 4, 2), CFG(256, 256, 4, 2, 2), CFG(256, 64, 4, 1, 1), CFG(128, 64, 2, 1, 1),
     // 32-channel tiles for 32 / 48 / 96-channel GEMMs (the Inception stem: a 64-wide tile is half empty)
-    CFG(256, 32, 4, 1, 1), CFG(128, 32, 4, 1, 1), CFG(256, 32, 4, 1, 2),
+    CFGN(256, 32, 4, 1, 1), CFGN(128, 32, 4, 1, 1), CFGN(256, 32, 4, 1, 2),
     // s_setprio around the MFMA clusters (T5) on the pipelined tiles
     CFGP(256, 256, 2, 4, 2), CFGP(256, 256, 4, 2, 2), CFGP(128, 128, 2, 2, 2), CFGP(128, 64, 2, 2, 2),
     // (measured and dropped: 256 x 128 / 128 x 256 tiles with a 3-deep ring, 1028-1029 TF at 4096^3 /
@@ -1612,6 +1687,7 @@ static const ConvCfg g_cfgs[] = {
 };
 #undef CFG
 #undef CFGP
+#undef CFGN
 constexpr int kNumCfgs = sizeof(g_cfgs) / sizeof(g_cfgs[0]);
 
 int conv_num_cfgs() { return kNumCfgs; }
@@ -1619,6 +1695,7 @@ void conv_cfg_info(int i, int* out5) {
   const ConvCfg& c = g_cfgs[i];
   out5[0] = c.tm; out5[1] = c.bn; out5[2] = c.wm; out5[3] = c.wn; out5[4] = c.st;
 }
+bool conv_cfg_has_xa(int i) { return i >= 0 && i < kNumCfgs && g_cfgs[i].launch_xa != nullptr; }
 
 template <int TM, int BN, int WM, int WN, int ST>
 static void launch_fp8_cfg(const ConvParams& p, hipStream_t stream) {
@@ -1627,7 +1704,7 @@ static void launch_fp8_cfg(const ConvParams& p, hipStream_t stream) {
 }
 
 // MX-FP8 configurations (same role as g_cfgs for bf16)
-#define FCFG(TM, BN, WM, WN, ST) {TM, BN, WM, WN, ST, &launch_fp8_cfg<TM, BN, WM, WN, ST>}
+#define FCFG(TM, BN, WM, WN, ST) {TM, BN, WM, WN, ST, &launch_fp8_cfg<TM, BN, WM, WN, ST>, nullptr}
 static const ConvCfg g_fp8_cfgs[] = {
     FCFG(128, 64, 2, 2, 1), FCFG(128, 128, 2, 2, 1), FCFG(128, 64, 2, 2, 2), FCFG(128, 128, 2, 2, 2),
     FCFG(256, 256, 2, 4, 2),  // (4 x 2 waves of 64 x 128 spills at 2 waves per SIMD with 8-VGPR fp8 fragments)
@@ -1661,6 +1738,15 @@ int conv_gemm_launch(const ConvParams& p, hipStream_t stream) {
     HIP_CHECK_LAUNCH();
     return 0;
   }
+  if (p.xa_y) {
+    // fused BN-backward A operand: any tap list with uniform k-steps (padded taps / rows stay zero)
+    if (!p.xa_coef || p.CA % BK || p.bias) return 4;
+    const int cfg = p.cfg >= 0 ? p.cfg : (p.Ncols <= 64 || p.tile_n == 64 ? 0 : 1);
+    if (!conv_cfg_has_xa(cfg)) return 4;
+    g_cfgs[cfg].launch_xa(p, stream);
+    HIP_CHECK_LAUNCH();
+    return 0;
+  }
   if (p.cfg >= 0) {
     if (p.cfg >= kNumCfgs) return 3;
     g_cfgs[p.cfg].launch(p, stream);
@@ -1676,14 +1762,27 @@ void conv_set_wgrad_variant(int v) { g_wvariant = v; }
 template <int WBM, int TN, int WM, int WN, int KG, int ST, int BKP = WBK>
 static void launch_wg(const WgradParams& p, int splits, hipStream_t stream) {
   const dim3 grid(cdiv(p.Cout, WBM) * cdiv(p.Ntot, TN), splits);
+  using XCfg = WgCfg<WBM, TN, WM, WN, KG, ST, BKP, true>;
+  if constexpr (XCfg::MAIN + XCfg::XA_BYTES <= 160 * 1024 && !(ST == 2 && WBM == 256)) {
+    if (p.xa_y) {
+      hipLaunchKernelGGL((conv_wgrad_glds_kernel<WBM, TN, WM, WN, KG, ST, BKP, true>), grid,
+                         dim3(64 * WM * WN * KG), 0, stream, p);
+      return;
+    }
+  }
   hipLaunchKernelGGL((conv_wgrad_glds_kernel<WBM, TN, WM, WN, KG, ST, BKP>), grid, dim3(64 * WM * WN * KG), 0,
                      stream, p);
 }
+
+// variants with a fused BN-backward form: all but the 256 x 256 tile with a 2-deep 64-pixel ring (its
+// register y pieces spill at 2 waves per SIMD; LDS y would not fit) and the 4-deep 256 x 256 ring (LDS)
+bool conv_wgrad_has_xa(int stages) { return stages >= 1 && stages <= 9 && stages != 4 && stages != 7; }
 
 int conv_wgrad_tile_n(int stages) { return (stages == 4 || stages == 7 || stages == 9) ? 256 : WBN; }
 
 int conv_wgrad_launch(const WgradParams& p_in, int splits, hipStream_t stream) {
   if (p_in.M <= 0) return 0;
+  if (p_in.xa_y && (g_wvariant == 1 || !conv_wgrad_has_xa(p_in.stages))) return 4;
   const bool dma = g_wvariant != 1;
   WgradParams p = p_in;
   if (!dma || splits <= 1) p.ws = nullptr;  // the register-staged kernel always adds atomically

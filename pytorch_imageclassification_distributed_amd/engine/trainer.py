@@ -37,7 +37,7 @@ from ..data import CudaPrefetcher, ImageDataset, NativeFolderLoader, SyntheticIm
 from ..models import DEFAULT_IMAGE_SIZE, Classifier
 from ..ops import functional as Fx
 from ..ops.grad_arena import GradArena
-from ..parallel import GradReducer, check_peer_errors, convert_sync_batchnorm, setup_peer_syncbn
+from ..parallel import GradReducer, check_peer_errors, comm_timer, convert_sync_batchnorm, setup_peer_syncbn
 from ..utils import (BEST, LATEST, AccuracyCounter, DeviceMeter, JsonlLogger, load_checkpoint,
                      load_model_state, resolve_resume, restore_rng_state, save_checkpoint)
 from ..utils.timers import PhaseTimer
@@ -262,6 +262,9 @@ class Trainer:
     def _train_step(self, images, labels):
         rf = torch.profiler.record_function
         timer = self.timer
+        ct = comm_timer._TIMER if self.dev.type == "cuda" else None
+        if ct is not None:
+            ct.begin()
         if self.reducer is not None and getattr(self.args, "broadcast_buffers", False):
             self.reducer.sync_buffers()
         with rf("imgcls::forward"):
@@ -282,6 +285,8 @@ class Trainer:
         with rf("imgcls::optimizer"):
             self.optimizer.step(grad_scale=scale)
         timer.mark("optimizer")
+        if ct is not None:
+            ct.end()
         return loss.detach()
 
     def reduce_loss(self, loss):

@@ -451,14 +451,18 @@ TUNE_LOG: list = []  # (M, Ncols, K, {cfg: ms}) per tuned geometry (benchmarks/c
 
 
 def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(None, None, None, None, 0, 1),
-               groups=G_STATS, scales=(None, None)):
+               groups=G_STATS, scales=(None, None), xa=None):
     """One implicit-GEMM launch.  The kernel configuration - LDS-DMA ring depth (1 = high occupancy,
     2 / 3 = pipelined) x output-channel tile (64 / 128 / 256: more tiles balance 256 CUs better on
     small layers) x pixel tile (128 rows on 4 waves, or 256 rows on 8 waves) - is chosen once per
-    GEMM geometry by timing the candidates on scratch outputs (a conv-algorithm "find" step)."""
-    if DIRECT_FORCE is not None and _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales) is not None:
+    GEMM geometry by timing the candidates on scratch outputs (a conv-algorithm "find" step).
+    ``xa`` = (y, coef [3][CA]): A holds a BN's pre-elementwise gradient dz and the kernel applies the
+    BN backward's elementwise map on its operand loads (1x1 stride-1 geometry; ``XaLink``)."""
+    xa3 = (xa[0], xa[1], None) if xa is not None else (None, None, None)
+    if DIRECT_FORCE is not None and xa is None and \
+            _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales) is not None:
         cfg = (0, 0, DIRECT_BASE + DIRECT_FORCE)  # (tests) every eligible launch on this direct variant
-    elif CONV_FORCE_CFG is not None and scales[0] is None:
+    elif CONV_FORCE_CFG is not None and scales[0] is None and (xa is None or C.conv_cfg_has_xa(CONV_FORCE_CFG[2])):
         cfg = CONV_FORCE_CFG
     elif CONV_FORCE_FP8_CFG is not None and scales[0] is not None:
         cfg = CONV_FORCE_FP8_CFG
@@ -467,18 +471,18 @@ def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(
     else:
         key = (tuple(geo), out.shape[1], tuple(dh), tuple(dw), stats is not None, bias is not None,
                addend is not None, bwd[0] is not None, bwd[1] is not None, bwd[4], scales[0] is not None,
-               DIRECT_CONV)
+               DIRECT_CONV) + ((True,) if xa is not None else ())
         cfg = _STAGES_TUNED.get(key)
         if cfg is None:
             cfg = (0, 0, -1) if torch.cuda.is_current_stream_capturing() else _tune_conv(
-                A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups, scales)
+                A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups, scales, xa)
             if cfg[0] or cfg[2] >= 0:
                 _STAGES_TUNED[key] = cfg
     if cfg[2] >= DIRECT_BASE:
         _direct_launch(A, B, out, stats, groups, _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales),
                        cfg[2] - DIRECT_BASE, bwd)
         return
-    C.conv_gemm(A, B, out, stats, bias, *geo, dh, dw, tb, groups, zero, addend, *bwd, *cfg, *scales)
+    C.conv_gemm(A, B, out, stats, bias, *geo, dh, dw, tb, groups, zero, addend, *bwd, *cfg, *scales, *xa3)
 
 
 _CFGS = None
@@ -503,10 +507,13 @@ def conv_fp8_cfgs():
     return _FP8_CFGS
 
 
-def _conv_candidates(m, ncols, fp8):
-    """(stages, tile_n, cfg) triples worth timing for an M x Ncols GEMM."""
+def _conv_candidates(m, ncols, fp8, xa=False):
+    """(stages, tile_n, cfg) triples worth timing for an M x Ncols GEMM (``xa``: configurations with a
+    fused BN-backward A-operand variant only)."""
     out = []
     for i, (tm, bn, _wm, _wn, _st) in enumerate(conv_fp8_cfgs() if fp8 else conv_cfgs()):
+        if xa and not C.conv_cfg_has_xa(i):
+            continue
         if bn > 64 and bn >= 2 * ncols:   # tile at least half empty
             continue
         if bn == 64 and ncols >= 512:     # 8+ column tiles re-read the pixel panel too often
@@ -574,18 +581,19 @@ def _direct_launch(A, B, out, stats, groups, dg, variant, bwd):
         C.direct_conv(A, w, out, stats, groups, n, ih, iw, cx, gh, gw, co, pt, pl, variant)
 
 
-def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups, scales=(None, None)):
+def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups, scales=(None, None), xa=None):
     scratch = torch.empty_like(out)
     sst = torch.zeros_like(stats) if stats is not None else None
     bwd = tuple(bwd)
     if bwd[3] is not None:
         bwd = bwd[:3] + (torch.zeros_like(bwd[3]),) + bwd[4:]
-    cands = _conv_candidates(geo[0], geo[1], scales[0] is not None)
+    cands = _conv_candidates(geo[0], geo[1], scales[0] is not None, xa is not None)
+    xa3 = (xa[0], xa[1], None) if xa is not None else (None, None, None)
     times = {}
     for cfg in cands:
         times[cfg] = _time_ms(lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, groups, zero,
-                                                  addend, *bwd, *cfg, *scales))
-    dg = _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales)
+                                                  addend, *bwd, *cfg, *scales, *xa3))
+    dg = _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales) if xa is None else None
     if dg is not None:
         for v, (cip, cot) in DIRECT_CFGS.items():
             if dg[3] <= cip and (cot == 32 or dg[6] > 32):
@@ -629,11 +637,13 @@ def _conv_forward_fp8(x, w_param, g: ConvGeom, stats, bias, out, c_off):
     return y
 
 
-def conv_dgrad_raw(dy, w_param, g: ConvGeom, addend=None, link=None):
+def conv_dgrad_raw(dy, w_param, g: ConvGeom, addend=None, link=None, xa=None):
     """dX = conv_transpose(dY, W) [+ addend], one MFMA GEMM per sub-pixel phase.
 
     With ``link`` (the producer BN of the conv input) the epilogue instead emits
-    dz = act'(z) * dX and the producer's BN-backward partial sums (fused reduce)."""
+    dz = act'(z) * dX and the producer's BN-backward partial sums (fused reduce).
+    With ``xa`` = (y, coef) ``dy`` is the consuming BN's pre-elementwise gradient dz and the kernel
+    forms dY = coef0*dz + coef1*y + coef2 on its A-operand loads (1x1 convs, ``XaLink``)."""
     dev = dy.device
     bwd = (None, None, None, None, 0, 1)
     if link is not None:
@@ -647,7 +657,8 @@ def conv_dgrad_raw(dy, w_param, g: ConvGeom, addend=None, link=None):
             continue
         geo = (g.N * gh * gw, g.Ci, len(tb) * g.Co, g.Co, gh, gw, g.OH, g.OW, 1, g.T * g.Co, g.H, g.W, g.sh,
                ph, pw, g.Ci, 0)
-        _conv_gemm(dy, wt, dx, None, None, geo, dh, dw, tb, ws(dev).zero, addend, bwd)
+        _conv_gemm(dy, wt, dx, None, None, geo, dh, dw, tb, ws(dev).zero, addend, bwd,
+                   xa=xa if len(tb) else None)
     return dx
 
 
@@ -683,9 +694,10 @@ def _wgrad_ws(dev, n):
     return buf
 
 
-def _wgrad_launch(dy, x, out, g: ConvGeom, m, ntot, kps, splits, stages=2, side=None):
+def _wgrad_launch(dy, x, out, g: ConvGeom, m, ntot, kps, splits, stages=2, side=None, xa=None):
     """One weight-gradient launch on the current stream, or (``side``: a ``_SideStream``) forked onto the
-    side stream inside the launcher (event record / wait and allocator stream records in C++)."""
+    side stream inside the launcher (event record / wait and allocator stream records in C++).  ``xa`` =
+    (y, coef): dy is a BN's pre-elementwise gradient, the kernel applies the elementwise map itself."""
     wsp = None
     if WGRAD_WS and splits > 1 and ntot % 8 == 0:
         n = splits * g.Co * ntot
@@ -696,7 +708,8 @@ def _wgrad_launch(dy, x, out, g: ConvGeom, m, ntot, kps, splits, stages=2, side=
                 side.ws = torch.empty(max(n, 1 << 20), dtype=torch.float32, device=dy.device)
             wsp = side.ws
     C.conv_wgrad(dy, x, out, m, g.Co, g.Cx, ntot, g.OH, g.OW, g.H, g.W, g.sh, g.sw, g.pt, g.pl,
-                 g.dil, g.dil, g.kw, kps, splits, ws(dy.device).zero, stages, wsp, side.handle if side else 0)
+                 g.dil, g.dil, g.kw, kps, splits, ws(dy.device).zero, stages, wsp, side.handle if side else 0,
+                 xa_y=xa[0] if xa is not None else None, xa_coef=xa[1] if xa is not None else None)
 
 
 def _wgrad_tiles(co, ntot, stages):
@@ -707,26 +720,28 @@ def _wgrad_tiles(co, ntot, stages):
     return (-(-co // (32 if stages in (5, 6) else 64 if co <= 64 else 128))) * (-(-ntot // 128))
 
 
-def _wgrad_plan(g: ConvGeom, dy, x, m, ntot):
+def _wgrad_plan(g: ConvGeom, dy, x, m, ntot, xa=None):
     """(k_per_split, splits, stages) of the weight-gradient launch for this geometry."""
-    target, stages = _wgrad_config(dy, x, g, m, ntot)
+    target, stages = _wgrad_config(dy, x, g, m, ntot, xa)
     kps, splits = _wgrad_split(m, _wgrad_tiles(g.Co, ntot, stages), target)
     return kps, splits, stages
 
 
-def _wgrad_config(dy, x, g: ConvGeom, m, ntot):
+def _wgrad_config(dy, x, g: ConvGeom, m, ntot, xa=None):
     """(split-K block target, LDS ring depth): fixed by IMGCLS_WGRAD_BLOCKS / IMGCLS_WGRAD_STAGES,
-    else timed jointly once per shape (cached).
+    else timed jointly once per shape (cached).  With ``xa`` (fused BN-backward dY) only the variants
+    that have the fused form are candidates, and they are timed with it.
 
     Tuning runs on a scratch gradient buffer, outside any graph capture, the first time a shape
     is seen (warmup), like a conv-algorithm "find" step."""
+    fx = xa is not None
     if DETERMINISTIC:  # one split: every dW element receives exactly one atomic contribution
-        return 1, (WGRAD_STAGES or 2)
+        return 1, (WGRAD_STAGES if WGRAD_STAGES and (not fx or C.conv_wgrad_has_xa(WGRAD_STAGES)) else 2)
     blocks = (WGRAD_TARGET_BLOCKS,) if WGRAD_TARGET_BLOCKS > 0 else WGRAD_CANDIDATES
-    stages = (WGRAD_STAGES,) if WGRAD_STAGES > 0 else (1, 2)
+    stages = (WGRAD_STAGES,) if WGRAD_STAGES > 0 and (not fx or C.conv_wgrad_has_xa(WGRAD_STAGES)) else (1, 2)
     if len(blocks) == 1 and len(stages) == 1:
         return blocks[0], stages[0]
-    key = (g.N, g.Cx, g.H, g.W, g.Co, g.kh, g.kw, g.sh, g.pt, g.pl, g.dil, blocks, stages)
+    key = (g.N, g.Cx, g.H, g.W, g.Co, g.kh, g.kw, g.sh, g.pt, g.pl, g.dil, blocks, stages) + ((True,) if fx else ())
     best = _WGRAD_TUNED.get(key)
     if best is not None:
         return best
@@ -746,9 +761,11 @@ def _wgrad_config(dy, x, g: ConvGeom, m, ntot):
             cands += [(cand, st) for st in (5, 6) for cand in blocks]
         # (64 / 128 x 256 four-wave tiles, reading the narrow layers' dY half as often, were 5-70 % slower
         # on every ResNet-50 shape: profiles/r4d_wgrad_wide_tiles_probe.txt)
+    if fx:
+        cands = [(cand, st) for cand, st in cands if C.conv_wgrad_has_xa(st)]
     for cand, st in cands:
         kps, splits = _wgrad_split(m, _wgrad_tiles(g.Co, ntot, st), cand)
-        times[(cand, st)] = _time_ms(lambda: _wgrad_launch(dy, x, scratch, g, m, ntot, kps, splits, st))
+        times[(cand, st)] = _time_ms(lambda: _wgrad_launch(dy, x, scratch, g, m, ntot, kps, splits, st, xa=xa))
     best = min(times, key=times.get)
     _WGRAD_TUNED[key] = best
     WGRAD_TUNE_LOG.append((g.Co, ntot, m, times))
@@ -797,9 +814,12 @@ def side_stream(dev):
 
 def join_side_streams() -> None:
     """Make every compute stream that handed work to a side stream wait for it (no host sync)."""
+    from ..parallel import comm_timer
     for s in _SIDE.values():
         for main in s.joins:
+            comm_timer.mark("compute_end", main)
             main.wait_stream(s.stream)
+            comm_timer.mark("side_joined", main)
         s.joins.clear()
 
 
@@ -832,25 +852,27 @@ def comm_stream(dev):
     return s.stream
 
 
-def conv_wgrad_raw(dy, x, w_param, g: ConvGeom):
+def conv_wgrad_raw(dy, x, w_param, g: ConvGeom, xa=None):
     dev = dy.device
     m = g.N * g.OH * g.OW
     ntot = g.T * g.Cx
-    kps, splits, stages = _wgrad_plan(g, dy, x, m, ntot)
+    kps, splits, stages = _wgrad_plan(g, dy, x, m, ntot, xa)
+    if xa is not None and g.Cx != g.Ci:
+        raise RuntimeError("fused BN-backward wgrad: padded input channels")
     if g.Cx == g.Ci:
         dw = arena_slot(w_param)
         if dw is not None:
             s = side_stream(dev)
             if s is None:
-                _wgrad_launch(dy, x, dw, g, m, ntot, kps, splits, stages)
+                _wgrad_launch(dy, x, dw, g, m, ntot, kps, splits, stages, xa=xa)
                 return dw
             if not s.joins:  # first side launch of this backward: join when the engine finishes
                 torch.autograd.Variable._execution_engine.queue_callback(join_side_streams)
             s.joins.add(torch.cuda.current_stream(dev))
-            _wgrad_launch(dy, x, dw, g, m, ntot, kps, splits, stages, side=s)
+            _wgrad_launch(dy, x, dw, g, m, ntot, kps, splits, stages, side=s, xa=xa)
             return dw
         dw = grad_buffer(w_param)
-        _wgrad_launch(dy, x, dw, g, m, ntot, kps, splits, stages)
+        _wgrad_launch(dy, x, dw, g, m, ntot, kps, splits, stages, xa=xa)
         return dw
     full = torch.zeros(g.Co * ntot, dtype=torch.float32, device=dev)
     dw = arena_slot(w_param)
@@ -954,14 +976,55 @@ class BwdLink:
         return self.groups or stat_groups(self.rows)
 
 
+# BN-backward elementwise fused into the producer conv's gradient GEMMs (csrc/conv_gemm.hip XA):
+# for a 1x1 conv followed by BN, the BN backward hands the conv its pre-elementwise gradient dz and the
+# per-channel affine map dY = c0*dz + c1*y + c2 instead of writing dY with bn_bwd_elemt; the conv's dgrad
+# and wgrad kernels form dY on their operand loads.  (Before: elemt read dz and y and wrote dY, then both
+# GEMMs read dY - the BN elementwise passes were 37 % of the ResNet-50 step)
+FUSE_XA = os.environ.get("IMGCLS_BN_XA", "1") == "1"
+XA_COUNT = [0]  # BN backwards handed to their producer conv (tests / diagnostics)
+
+
+class XaLink:
+    """Ties a 1x1 conv to the BN consuming its output y for the fused backward: the BN's backward parks
+    (dz, y, coef [3][C]) here and returns dz as the conv output's gradient; the conv's backward checks
+    that it received exactly that tensor and runs its dgrad / wgrad with the fused operand map."""
+
+    __slots__ = ("dz", "y", "coef")
+
+    def __init__(self):
+        self.dz = self.y = self.coef = None
+
+    def take(self, dy):
+        """(y, coef) when ``dy`` is the parked dz (and clears the link), else None."""
+        if self.dz is None:
+            return None
+        if dy.data_ptr() != self.dz.data_ptr() or dy.shape != self.dz.shape:
+            raise RuntimeError("fused BN backward: the conv received a gradient other than its BN's dz")
+        out = (self.y, self.coef)
+        self.dz = self.y = self.coef = None
+        return out
+
+
+def xa_eligible(x, conv) -> bool:
+    """A dense conv (no bias / groups / dilation, square stride) whose output channels are a multiple of 64
+    (uniform k-steps of the dgrad GEMM, K = taps x Cout) and whose input channels are unpadded: its backward
+    can take the fused BN-backward operand map (padded taps are masked in the kernel)."""
+    return (FUSE_XA and conv.stride[0] == conv.stride[1] and tuple(conv.dilation) == (1, 1)
+            and conv.groups == 1 and conv.bias is None and conv.out_channels % 64 == 0
+            and x.shape[1] == conv.in_channels and conv.in_channels % 8 == 0
+            and conv.kernel_size[0] * conv.kernel_size[1] <= 49)
+
+
 class ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, conv, want_stats, slot=None, fuse_bwd=False):
+    def forward(ctx, x, w, conv, want_stats, slot=None, fuse_bwd=False, xa=None):
         g = conv_geom(x, conv)
         stats = ws(x.device).stats_buf(g.Co, stat_groups(g.N * g.OH * g.OW)) if want_stats else None
         y = conv_forward_raw(x, w, g, stats=stats)
         ctx.g = g
         ctx.slot = slot
+        ctx.xa = xa
         link = getattr(x, "_imgcls_link", None) if (fuse_bwd or slot is not None) else None
         ctx.link = link if (link is not None and link.y is not None and g.Cx == g.Ci) else None
         ctx.save_for_backward(x, w)
@@ -972,6 +1035,7 @@ class ConvFn(torch.autograd.Function):
         x, w = ctx.saved_tensors
         g = ctx.g
         dy = _cl(dy)
+        xa = ctx.xa.take(dy) if ctx.xa is not None else None
         dx = None
         if ctx.needs_input_grad[0]:
             slot, link = ctx.slot, ctx.link
@@ -981,7 +1045,7 @@ class ConvFn(torch.autograd.Function):
                 link = None  # the producer's BN reduce needs the full gradient
             # running sum of the other consumers' contributions rides in as the dgrad addend
             addend = slot.t if (slot is not None and g.Cx == g.Ci) else None
-            dx = conv_dgrad_raw(dy, w, g, addend=addend, link=link)
+            dx = conv_dgrad_raw(dy, w, g, addend=addend, link=link, xa=xa)
             if link is not None:
                 link.done = True
                 if link.group is not None:
@@ -990,8 +1054,8 @@ class ConvFn(torch.autograd.Function):
                     _syncbn_bwd_start(link)
             if slot is not None:
                 dx = slot.deliver(dx, fused=addend is not None)
-        dw = conv_wgrad_raw(dy, x, w, g) if ctx.needs_input_grad[1] else None
-        return dx, dw, None, None, None, None
+        dw = conv_wgrad_raw(dy, x, w, g, xa=xa) if ctx.needs_input_grad[1] else None
+        return dx, dw, None, None, None, None, None
 
 
 # ---------------------------------------------------------------------------
@@ -1177,32 +1241,35 @@ def _bn_coef(y, gamma, beta, bn, stats_ready):
     return coef, group, count_t
 
 
-def _bn_bwd_k(part, grp, c, rows, training, group, count_t, params, dev):
-    """BN-backward partial rows -> (k [2, C] for bn_bwd_elemt, dgamma, dbeta); SyncBN all-reduces the sums."""
+def _bn_bwd_k(part, grp, c, rows, training, group, count_t, params, dev, coef=None, xa=None):
+    """BN-backward partial rows -> (k [2, C] for bn_bwd_elemt, dgamma, dbeta); SyncBN all-reduces the sums.
+    ``xa`` (with ``coef``): also the fused elementwise map [3][C] for ``XaLink`` consumers."""
     k = torch.empty(2 * c, dtype=torch.float32, device=dev)
     dgamma = grad_buffer(params[0], zero=False)
     dbeta = grad_buffer(params[1], zero=False)
-    if training and group is None:  # one launch: partial rows -> dgamma, dbeta, k
-        C.bn_reduce_bwd(part, grp, c, float(rows), dgamma, dbeta, k)
+    if training and group is None:  # one launch: partial rows -> dgamma, dbeta, k (+ the fused map)
+        C.bn_reduce_bwd(part, grp, c, float(rows), dgamma, dbeta, k, coef=coef if xa is not None else None, xa=xa)
         return k, dgamma, dbeta
     pc = peer_channel(group, 0) if (training and group is not None) else None
     if pc is not None and count_t is not None and c <= PEER_BN_MAX_C:  # reduce + exchange + k in one kernel
         pc.comm.bn_bwd(part, grp, c, count_t, dgamma, dbeta, k)
-        return k, dgamma, dbeta
-    sums = torch.empty(2 * c, dtype=torch.float64, device=dev)
-    C.bn_partials(part, grp, c, sums, dgamma, dbeta)
-    if group is not None:
-        stats_all_reduce_(sums, group)
-    if training:
-        C.bn_bwd_k(sums, count_t, float(rows), c, k)
-    else:  # running statistics are constants: dy = scale * dz
-        k.zero_()
+    else:
+        sums = torch.empty(2 * c, dtype=torch.float64, device=dev)
+        C.bn_partials(part, grp, c, sums, dgamma, dbeta)
+        if group is not None:
+            stats_all_reduce_(sums, group)
+        if training:
+            C.bn_bwd_k(sums, count_t, float(rows), c, k)
+        else:  # running statistics are constants: dy = scale * dz
+            k.zero_()
+    if xa is not None:
+        C.bn_xa_coef(coef, k, c, xa)
     return k, dgamma, dbeta
 
 
 class BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, y, gamma, beta, res, bn, act, stats_ready, res_slot=None, link=None, cat=None):
+    def forward(ctx, y, gamma, beta, res, bn, act, stats_ready, res_slot=None, link=None, cat=None, xa=None):
         dev = y.device
         n, c, h, w = y.shape
         rows = n * h * w
@@ -1234,6 +1301,7 @@ class BNActFn(torch.autograd.Function):
             ctx.link = link
         ctx.has_res = res is not None
         ctx.params = (gamma, beta)
+        ctx.xa = xa if bn.training else None
         ctx.save_for_backward(y, coef, res if res is not None else y)
         return out
 
@@ -1248,6 +1316,9 @@ class BNActFn(torch.autograd.Function):
         link = ctx.link
         grp = stat_groups(rows)
         pending = None
+        # fused backward: the producer 1x1 conv applies the elementwise map itself (XaLink); it needs dz
+        # dense (not a concat slice) and the training-mode statistics
+        xa = ctx.xa if (ctx.xa is not None and ctx.training) else None
         if link is not None and link.done:
             # the consuming conv's dgrad epilogue already produced dz and the partial sums
             part, dz = link.part, g
@@ -1255,27 +1326,46 @@ class BNActFn(torch.autograd.Function):
             FUSED_BWD_COUNT[0] += 1
             pending = link.pending
             link.y = link.coef = link.res = link.part = link.pending = link.params = link.count_t = None
+            if ldg:
+                xa = None
         else:
             part = ws(dev).stats_buf(c, grp)
-            dz = torch.empty_like(y, memory_format=CL) if ctx.has_res else None
-            C.bn_bwd_reduce(g, y, coef, res, dz, rows, c, ctx.act, part, grp, ldg)
+            if xa is not None and ldg:
+                xa = None
+            if ctx.has_res or (xa is not None and ctx.act != 0):
+                dz = torch.empty_like(y, memory_format=CL)  # the residual's gradient and / or the fused input
+            elif xa is not None:
+                dz = g  # no activation: the incoming gradient is dz
+            else:
+                dz = None
+            C.bn_bwd_reduce(g, y, coef, res, dz if dz is not g else None, rows, c, ctx.act, part, grp, ldg)
+        xac = torch.empty(3 * c, dtype=torch.float32, device=dev) if xa is not None else None
         if pending is not None:  # SyncBN all-reduce launched early by the consuming conv's backward
             sums, work, dgamma, dbeta, k = pending
             work.wait()
             if k is None:
                 k = torch.empty(2 * c, dtype=torch.float32, device=dev)
                 C.bn_bwd_k(sums, ctx.count_t, float(rows), c, k)
+            if xac is not None:
+                C.bn_xa_coef(coef, k, c, xac)
         else:
-            k, dgamma, dbeta = _bn_bwd_k(part, grp, c, rows, ctx.training, ctx.group, ctx.count_t, ctx.params, dev)
+            k, dgamma, dbeta = _bn_bwd_k(part, grp, c, rows, ctx.training, ctx.group, ctx.count_t, ctx.params, dev,
+                                         coef=coef, xa=xac)
         if link is not None and link.done:
             ws(dev).give_part(part)
-        dy = torch.empty_like(y, memory_format=CL)
-        C.bn_bwd_elemt(None if dz is not None else g, y, coef, k, res, dz, dy, rows, c, ctx.act,
-                       0 if dz is not None else ldg)
+        if xa is not None:
+            # hand dz and the map to the producer conv: no bn_bwd_elemt pass, no dY tensor
+            xa.dz, xa.y, xa.coef = dz, y, xac
+            XA_COUNT[0] += 1
+            dy = dz
+        else:
+            dy = torch.empty_like(y, memory_format=CL)
+            C.bn_bwd_elemt(None if dz is not None else g, y, coef, k, res, dz, dy, rows, c, ctx.act,
+                           0 if dz is not None else ldg)
         dres = dz if ctx.has_res else None
         if dres is not None and ctx.res_slot is not None:
             dres = ctx.res_slot.deliver(dres)
-        return dy, dgamma, dbeta, dres, None, None, None, None, None, None
+        return dy, dgamma, dbeta, dres, None, None, None, None, None, None, None
 
 
 class BNActPoolFn(torch.autograd.Function):
@@ -1442,23 +1532,28 @@ def conv_bn_act(x, conv, bn, act, residual, x_slot=None, res_slot=None, exclusiv
         residual = _cl(residual)
     ensure_channels_last_weight(conv)
     depthwise = conv.groups > 1
+    dense = False
+    xa = None
     if depthwise:
         if not (conv.groups == conv.in_channels == conv.out_channels):
             raise NotImplementedError("grouped (non-depthwise) convolution")
         y = DwConvFn.apply(x, conv.weight, conv, exclusive_input and FUSE_BN_BWD and DW_LINK)
         ready = False
     elif dense_conv_eligible(x, conv) and x.shape[2] * x.shape[3] > 1:
+        dense = True
         y = DenseConvFn.apply(x, conv.weight, conv, bn.training)
         ready = bn.training
     else:
         if conv.groups != 1:
             raise NotImplementedError("grouped convolution")
-        y = ConvFn.apply(x, conv.weight, conv, bn.training, x_slot, exclusive_input and FUSE_BN_BWD)
+        xa = XaLink() if (bn.training and torch.is_grad_enabled() and xa_eligible(x, conv)) else None
+        y = ConvFn.apply(x, conv.weight, conv, bn.training, x_slot, exclusive_input and FUSE_BN_BWD, xa)
         ready = bn.training
     if conv.bias is not None:
         raise NotImplementedError("conv bias before BatchNorm")
     link = BwdLink() if (FUSE_BN_BWD and bn.training and torch.is_grad_enabled()) else None
-    res_out = BNActFn.apply(y, bn.weight, bn.bias, residual, bn, act, ready, res_slot, link, out)
+    res_out = BNActFn.apply(y, bn.weight, bn.bias, residual, bn, act, ready, res_slot, link, out,
+                            xa if not depthwise and not dense else None)
     if link is not None:
         res_out._imgcls_link = link
     return res_out

@@ -1,3 +1,4 @@
+from . import comm_timer
 from .comm import all_gather, all_gather_tensor, all_reduce_sum_, reduce_tensor
 from .dist import DistContext, barrier, destroy, get_rank, get_world_size, init_distributed
 from .peer import (PeerAllReduce, PeerTimeoutError, check_peer_errors, peer_active, peer_errors, setup_peer_syncbn,

@@ -38,6 +38,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops.grad_arena import GradArena
+from . import comm_timer
 
 
 def _comm_stream(dev):
@@ -173,6 +174,8 @@ class GradReducer:
         # stream behind the current one), so it follows the bucket's gradients from both streams
         side = _comm_stream(t.device)
         main = torch.cuda.current_stream(t.device) if side is not None else None
+        if comm_timer.active() and t.is_cuda:
+            comm_timer.mark("first_bucket", side if side is not None else torch.cuda.current_stream(t.device))
         with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
             if self.comm_dtype is not None and self.comm_dtype != torch.float32:
                 c = t.to(self.comm_dtype)
@@ -198,6 +201,10 @@ class GradReducer:
                 self.got[i] = True
                 b = self.bucket_of[i]
                 self.pending[b] -= 1
+        timed = comm_timer.active() and self.flat.is_cuda
+        if timed:  # (no side stream: backward ended on this stream, nothing lags behind it)
+            comm_timer.mark("compute_end")
+            comm_timer.mark("side_joined")
         for b in range(len(self.buckets)):
             if not self.launched[b]:
                 self._launch(b)
@@ -206,6 +213,8 @@ class GradReducer:
             if dst is not None:
                 dst.copy_(comp)
         self.works.clear()
+        if timed:
+            comm_timer.mark("comm_end")
         self._reset_counts()
         if self._rebuild_pending:
             self._rebuild_pending = False

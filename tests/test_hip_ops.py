@@ -433,10 +433,11 @@ def test_weight_shadow_follows_outside_writes():
     assert rel_err(out, ref) < 3e-2, "forward used a stale bf16 weight shadow"
     assert rel_err(gx, xr.grad) < 5e-2, "dgrad used a stale transposed weight shadow"
     with torch.no_grad():
-        conv.weight.mul_(-1.0)  # in-place edit: bumps the version counter
+        conv.weight.mul_(-1.0)  # in-place edit (after the optimizer step above): bumps the version counter
+    conv_ref2 = copy.deepcopy(conv)
     xb = x.detach().clone()
     out2 = hip.conv_bn_act(xb, conv, copy.deepcopy(bn).eval(), None, None)
-    ref2 = copy.deepcopy(bn).eval()(conv_ref.eval()(x.float()) * -1.0)
+    ref2 = copy.deepcopy(bn).eval()(conv_ref2(x.float()))
     assert rel_err(out2, ref2) < 3e-2, "in-place weight edit not seen by the next forward"
 
 
@@ -1016,3 +1017,88 @@ def test_se_gate_fused_bn_backward(n, c, hw):
     mine = [p_.grad for m in (conv, bn, red, exp) for p_ in m.parameters()]
     for i, (m_, r_) in enumerate(zip(mine, ps)):
         assert rel_err(m_.reshape(r_.grad.shape), r_.grad) < 3e-2, i
+
+
+# ---------------------------------------------------------------------------------------------------------
+# BN-backward elementwise fused into the producer 1x1 conv's dgrad / wgrad (ops/hip.py XaLink, csrc XA)
+# ---------------------------------------------------------------------------------------------------------
+def _xa_block(hip, n, cin, hw, cmid, stride, act, use_res, xa_on, cfg=None, wstages=None, k=1):
+    """x -> kxk conv (stride) -> BN -> act [+ res] -> 1x1 conv -> BN: the first BN's backward is linked to
+    the second conv's dgrad (dz arrives fused), then handed to the first conv (XA).  Returns outputs and
+    gradients, and how many BN backwards took the fused path."""
+    torch.manual_seed(31)
+    c1 = nn.Conv2d(cin, cmid, k, stride, k // 2, bias=False).to(DEV).to(memory_format=CL)
+    b1 = nn.BatchNorm2d(cmid).to(DEV)
+    c2 = nn.Conv2d(cmid, 256, 1, 1, 0, bias=False).to(DEV).to(memory_format=CL)
+    b2 = nn.BatchNorm2d(256).to(DEV)
+    with torch.no_grad():
+        for m in (c1, c2):
+            m.weight.copy_(bf(m.weight))
+        b1.weight.uniform_(0.5, 1.5)
+        b1.bias.uniform_(-0.5, 0.5)
+    x = bf(torch.randn(n, cin, hw, hw, device=DEV)).to(torch.bfloat16).contiguous(memory_format=CL)
+    oh = (hw + 2 * (k // 2) - k) // stride + 1
+    res = bf(torch.randn(n, cmid, oh, oh, device=DEV)).to(torch.bfloat16).contiguous(memory_format=CL)
+    keep = hip.FUSE_XA, hip.CONV_FORCE_CFG, hip.WGRAD_STAGES
+    hip.FUSE_XA = xa_on
+    if cfg is not None:
+        hip.CONV_FORCE_CFG = (0, 0, cfg)
+    if wstages is not None:
+        hip.WGRAD_STAGES = wstages
+    n0 = hip.XA_COUNT[0]
+    try:
+        xb = x.detach().clone().requires_grad_(True)
+        rb = res.detach().clone().requires_grad_(True) if use_res else None
+        h = hip.conv_bn_act(xb, c1, b1, act, rb)
+        out = hip.conv_bn_act(h, c2, b2, "relu", None, exclusive_input=True)
+        g = torch.linspace(-1, 1, out.numel(), device=DEV).view_as(out).to(torch.bfloat16)
+        out.backward(g.contiguous(memory_format=CL))
+        torch.cuda.synchronize()
+        grads = [xb.grad.float(), c1.weight.grad.float(), b1.weight.grad.float(), b1.bias.grad.float(),
+                 c2.weight.grad.float()] + ([rb.grad.float()] if use_res else [])
+        return out.float(), grads, hip.XA_COUNT[0] - n0
+    finally:
+        hip.FUSE_XA, hip.CONV_FORCE_CFG, hip.WGRAD_STAGES = keep
+
+
+@pytest.mark.parametrize("case", [
+    # n, cin, hw, cmid, stride, act, residual, kernel
+    (4, 64, 28, 256, 1, "relu", True, 1),    # bn3-like: wide output, residual + ReLU
+    (4, 256, 28, 64, 1, "relu", False, 1),   # bn1-like: narrow output
+    (4, 128, 28, 128, 2, None, False, 1),    # downsample-like: stride 2, no activation
+    (2, 512, 7, 512, 1, "relu", True, 1),    # 7x7 map, partial row tiles
+    (3, 64, 15, 192, 1, "silu", False, 1),   # odd pixel count, SiLU
+    (4, 64, 14, 64, 1, "relu", False, 3),    # bn2-like: 3x3 dgrad, padded taps masked
+    (4, 128, 15, 128, 2, "relu", False, 3),  # 3x3 stride 2: sub-pixel phases, odd input
+])
+def test_bn_backward_fused_into_producer_conv(case):
+    """dgrad / wgrad with the fused BN-backward operand map against the unfused path (bn_bwd_elemt + plain
+    GEMMs): same outputs, same gradients to bf16 accuracy, and the fused path really taken."""
+    hip = _hip()
+    n, cin, hw, cmid, stride, act, use_res, k = case
+    o0, g0, k0 = _xa_block(hip, n, cin, hw, cmid, stride, act, use_res, False, k=k)
+    o1, g1, k1 = _xa_block(hip, n, cin, hw, cmid, stride, act, use_res, True, k=k)
+    assert k0 == 0 and k1 >= 1, (k0, k1)
+    assert torch.equal(o0, o1)
+    for a_, b_ in zip(g1, g0):
+        assert rel_err(a_, b_) < 2e-2, rel_err(a_, b_)
+        assert mean_err(a_, b_) < 5e-3, mean_err(a_, b_)
+
+
+def test_bn_backward_fused_every_kernel_variant():
+    """Every conv configuration with a fused A-operand variant and every wgrad ring / tile variant with a
+    fused dY form, on one bn3-like block, against the unfused path."""
+    hip = _hip()
+    case = (2, 64, 20, 256, 1, "relu", True)
+    _o, g0, _ = _xa_block(hip, *case, xa_on=False)
+    ran = 0
+    for i in range(len(hip.conv_cfgs())):
+        if not hip.C.conv_cfg_has_xa(i):
+            continue
+        for wst in (1, 2, 3, 4):
+            _o, g1, k1 = _xa_block(hip, *case, xa_on=True, cfg=i, wstages=wst)
+            assert k1 >= 1
+            for a_, b_ in zip(g1, g0):
+                assert rel_err(a_, b_) < 2e-2, (i, wst, rel_err(a_, b_))
+            ran += 1
+    assert ran >= 8
