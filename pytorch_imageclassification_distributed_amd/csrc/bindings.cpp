@@ -21,11 +21,11 @@ using OT = std::optional<Tensor>;
 // ---- launcher prototypes (defined in *.hip) ----
 int bn_partials_launch(float*, int, int, double*, float*, float*, double, hipStream_t);
 int bn_reduce_finalize_launch(float*, int, int, double, const float*, const float*, float*, float*, long long*, float,
-                              float, float*, hipStream_t);
+                              float, float*, const float*, hipStream_t);
 int bn_reduce_bwd_launch(float*, int, int, double, float*, float*, float*, const float*, float*, hipStream_t);
 int bn_xa_coef_launch(const float*, const float*, int, float*, hipStream_t);
 int bn_finalize_launch(const double*, const double*, double, const float*, const float*, float*, float*,
-                       long long*, float, float, int, float*, hipStream_t);
+                       long long*, float, float, int, float*, const float*, hipStream_t);
 int bn_eval_coef_launch(const float*, const float*, const float*, const float*, float, int, float*, hipStream_t);
 int bn_apply_launch(const bf16_t*, const float*, const bf16_t*, bf16_t*, long, int, int, int, int, uint8_t*, uint8_t*,
                     hipStream_t);
@@ -36,8 +36,8 @@ int bn_bwd_elemt_launch(const bf16_t*, const bf16_t*, const float*, const float*
                         bf16_t*, long, int, int, int, hipStream_t);
 int bn_act_maxpool_launch(const bf16_t*, const float*, bf16_t*, uint8_t*, int, int, const int*, int, hipStream_t);
 int direct_conv_launch(const bf16_t*, const bf16_t*, bf16_t*, float*, int, int, int, int, int, int, int, int, int,
-                       int, int, const bf16_t*, const float*, int, hipStream_t);
-int stem_s2d_conv_launch(const bf16_t*, const bf16_t*, bf16_t*, float*, int, int, int, int, hipStream_t);
+                       int, int, const bf16_t*, const float*, int, const float*, hipStream_t);
+int stem_s2d_conv_launch(const bf16_t*, const bf16_t*, bf16_t*, float*, int, int, int, int, const float*, hipStream_t);
 int maxpool_fwd_launch(const bf16_t*, bf16_t*, uint8_t*, int, int, int, int, int, int, int, int, int, int, int,
                        int, hipStream_t);
 int maxpool_bwd_launch(const bf16_t*, const uint8_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int,
@@ -92,7 +92,7 @@ int se_dx_launch(const bf16_t*, const float*, const float*, bf16_t*, int, int, i
                  int, int, hipStream_t);
 int act32_fwd_launch(const float*, float*, long, int, hipStream_t);
 int act32_bwd_launch(const float*, const float*, float*, long, int, hipStream_t);
-int bn_stats_launch(const bf16_t*, long, int, float*, int, hipStream_t);
+int bn_stats_launch(const bf16_t*, long, int, float*, int, const float*, hipStream_t);
 int se_mlp_fwd_launch(const float*, const float*, const float*, const float*, const float*, float*, float*, int, int,
                       int, hipStream_t);
 int se_mlp_bwd_launch(const float*, const float*, const float*, const float*, const float*, const float*, float*,
@@ -109,8 +109,8 @@ int peer_allreduce_f64_launch(const double*, double*, int, const unsigned long l
                               unsigned long long, int*, hipStream_t);
 int peer_bn_max_channels();
 int peer_bn_launch(bool, float*, int, int, double, const float*, const float*, float*, float*, long long*, float, float,
-                   float*, float*, float*, double*, const unsigned long long*, int, int, unsigned long long,
-                   unsigned long long, int*, hipStream_t);
+                   float*, float*, float*, double*, const float*, const unsigned long long*, int, int,
+                   unsigned long long, unsigned long long, int*, hipStream_t);
 
 namespace {
 
@@ -156,7 +156,7 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
                int IH, int IW, int sA, int ldb, int OH, int OW, int so, int oh0, int ow0, int ldc, int c_off,
                std::vector<int> dh, std::vector<int> dw, std::vector<int> tb, int stats_groups, Tensor zero,
                OT addend, OT bwd_y, OT bwd_res, OT bwd_coef, OT bwd_part, int bwd_act, int bwd_groups,
-               int stages, int tile_n, int cfg, OT a_sc, OT b_sc, OT xa_y, OT xa_coef, OT xa_out) {
+               int stages, int tile_n, int cfg, OT a_sc, OT b_sc, OT xa_y, OT xa_coef, OT xa_out, OT stats_shift) {
   const bool fp8 = a_sc.has_value() && a_sc->defined();
   TORCH_CHECK(A.scalar_type() == (fp8 ? at::kFloat8_e4m3fn : BF) && B.scalar_type() == A.scalar_type(),
               "conv_gemm: A and B must both be bf16, or both float8_e4m3fn with scales");
@@ -175,6 +175,8 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
   TORCH_CHECK(2LL * IH * IW * CA < (1LL << 31) && 2LL * B.numel() < (1LL << 31),
               "conv_gemm: an input image or the weight matrix exceeds 2 GiB (32-bit buffer offsets)");
   p.stats = optr<float>(stats); p.bias = optr<float>(bias);
+  p.stats_shift = p.stats ? optr<float>(stats_shift) : nullptr;
+  TORCH_CHECK(!p.stats_shift || stats_shift->numel() >= Ncols, "conv_gemm: stats_shift [Ncols]");
   p.M = M; p.Ncols = Ncols; p.K = K; p.CA = CA; p.GH = GH; p.GW = GW; p.IH = IH; p.IW = IW; p.sA = sA;
   p.ldb = ldb; p.OH = OH; p.OW = OW; p.so = so; p.oh0 = oh0; p.ow0 = ow0; p.ldc = ldc; p.c_off = c_off;
   p.ntaps = (int)dh.size(); p.stats_groups = stats_groups > 0 ? stats_groups : 1;
@@ -283,21 +285,21 @@ void bn_partials(Tensor part, int G, int C, Tensor sums, OT dgamma, OT dbeta, do
 }
 
 void bn_finalize(Tensor sums, OT count_t, double count, OT gamma, OT beta, OT rmean, OT rvar, OT nbt,
-                 double momentum, double eps, int C, Tensor coef) {
+                 double momentum, double eps, int C, Tensor coef, OT shift) {
   req(sums, at::kDouble, "sums"); req(coef, F32, "coef");
   check(bn_finalize_launch(ptr<double>(sums), optr<double>(count_t), count, optr<float>(gamma), optr<float>(beta),
                            optr<float>(rmean), optr<float>(rvar), optr<long long>(nbt), (float)momentum, (float)eps,
-                           C, ptr<float>(coef), cur()),
+                           C, ptr<float>(coef), optr<float>(shift), cur()),
         "bn_finalize");
 }
 
 void bn_reduce_finalize(Tensor part, int G, int C, double count, OT gamma, OT beta, OT rmean, OT rvar, OT nbt,
-                        double momentum, double eps, Tensor coef) {
+                        double momentum, double eps, Tensor coef, OT shift) {
   req(part, F32, "part"); req(coef, F32, "coef");
   TORCH_CHECK(part.numel() >= (int64_t)G * 2 * C && coef.numel() >= 4 * C, "bn_reduce_finalize: buffer sizes");
   check(bn_reduce_finalize_launch(ptr<float>(part), G, C, count, optr<float>(gamma), optr<float>(beta),
                                   optr<float>(rmean), optr<float>(rvar), optr<long long>(nbt), (float)momentum,
-                                  (float)eps, ptr<float>(coef), cur()),
+                                  (float)eps, ptr<float>(coef), optr<float>(shift), cur()),
         "bn_reduce_finalize");
 }
 
@@ -396,7 +398,7 @@ void bn_act_maxpool(Tensor y, Tensor coef, Tensor out, Tensor idx, int64_t N, in
 
 // ResNet stem on the space-to-depth input: x [N, H, W, 16] bf16, w [64, 256] bf16, y [N, H, W, 64] bf16,
 // part: BN statistics rows [G, 2, 64] (or None)
-void stem_conv(Tensor x, Tensor w, Tensor y, OT part, int G, int64_t N, int64_t H, int64_t W) {
+void stem_conv(Tensor x, Tensor w, Tensor y, OT part, int G, int64_t N, int64_t H, int64_t W, OT shift) {
   req(x, BF, "x"); req(w, BF, "w"); req(y, BF, "y");
   TORCH_CHECK(N > 0 && H > 0 && W > 0 && N * H * W < (1LL << 31), "stem_conv: bad geometry");
   TORCH_CHECK(x.numel() == N * H * W * 16 && w.numel() == 64 * 256 && y.numel() == N * H * W * 64,
@@ -409,13 +411,14 @@ void stem_conv(Tensor x, Tensor w, Tensor y, OT part, int G, int64_t N, int64_t 
     TORCH_CHECK(G > 0 && part->numel() >= (int64_t)G * 2 * 64, "stem_conv: part [G, 2, 64]");
     pp = part->data_ptr<float>();
   }
-  check(stem_s2d_conv_launch(ptr<bf16_t>(x), ptr<bf16_t>(w), ptr<bf16_t>(y), pp, G, (int)N, (int)H, (int)W, cur()),
+  check(stem_s2d_conv_launch(ptr<bf16_t>(x), ptr<bf16_t>(w), ptr<bf16_t>(y), pp, G, (int)N, (int)H, (int)W,
+                             optr<float>(shift), cur()),
         "stem_conv");
 }
 
 // stride-1 3x3 conv as a halo-tile direct kernel: x [N,H,W,Cin], w [Cout,3,3,Cin] (KRSC), y [N,OH,OW,Cout]
 void direct_conv(Tensor x, Tensor w, Tensor y, OT part, int G, int64_t N, int64_t H, int64_t W, int64_t Cin,
-                 int64_t OH, int64_t OW, int64_t Cout, int pt, int pl, int cfg, OT y_bn, OT coef, int act) {
+                 int64_t OH, int64_t OW, int64_t Cout, int pt, int pl, int cfg, OT y_bn, OT coef, int act, OT shift) {
   req(x, BF, "x"); req(w, BF, "w"); req(y, BF, "y");
   TORCH_CHECK(N > 0 && H > 0 && W > 0 && OH > 0 && OW > 0 && Cin > 0 && Cout > 0 && Cin % 8 == 0 && Cout % 8 == 0 &&
                   Cin <= 96 && pt >= 0 && pl >= 0 && pt <= 2 && pl <= 2 && OH <= H + 2 * pt && OW <= W + 2 * pl,
@@ -438,7 +441,7 @@ void direct_conv(Tensor x, Tensor w, Tensor y, OT part, int G, int64_t N, int64_
   }
   check(direct_conv_launch(ptr<bf16_t>(x), ptr<bf16_t>(w), ptr<bf16_t>(y), pp, G, (int)N, (int)H, (int)W, (int)Cin,
                            (int)OH, (int)OW, (int)Cout, pt, pl, cfg, bwd ? ptr<bf16_t>(*y_bn) : nullptr,
-                           bwd ? ptr<float>(*coef) : nullptr, act, cur()),
+                           bwd ? ptr<float>(*coef) : nullptr, act, optr<float>(shift), cur()),
         "direct_conv");
 }
 
@@ -671,10 +674,10 @@ void act32_bwd(Tensor x, Tensor dy, Tensor dx, int kind) {
   check(act32_bwd_launch(ptr<float>(x), ptr<float>(dy), ptr<float>(dx), x.numel(), kind, cur()), "act32_bwd");
 }
 
-void bn_stats(Tensor y, long rows, int C, Tensor part, int G) {
+void bn_stats(Tensor y, long rows, int C, Tensor part, int G, OT shift) {
   req(y, BF, "y");
   TORCH_CHECK(C % 8 == 0, "bn_stats: C % 8");
-  check(bn_stats_launch(ptr<bf16_t>(y), rows, C, ptr<float>(part), G, cur()), "bn_stats");
+  check(bn_stats_launch(ptr<bf16_t>(y), rows, C, ptr<float>(part), G, optr<float>(shift), cur()), "bn_stats");
 }
 
 void f32(const Tensor& t, long n, const char* name) {
@@ -755,14 +758,14 @@ class PeerComm {
 
   // SyncBN forward, exchange fused: partial rows -> coef [4][C], running stats, total count (count_out)
   void bn_fwd(Tensor part, int G, int C, double count, OT gamma, OT beta, OT rmean, OT rvar, OT nbt, double momentum,
-              double eps, Tensor coef, Tensor count_out) {
+              double eps, Tensor coef, Tensor count_out, OT shift) {
     req(part, F32, "part");
     req(coef, F32, "coef");
     req(count_out, at::kDouble, "count_out");
     TORCH_CHECK(part.numel() >= 2L * G * C && coef.numel() >= 4L * C, "PeerComm.bn_fwd: sizes");
     launch_bn(true, part, G, C, count, optr<float>(gamma), optr<float>(beta), optr<float>(rmean), optr<float>(rvar),
               optr<long long>(nbt), (float)momentum, (float)eps, ptr<float>(coef), nullptr, nullptr,
-              ptr<double>(count_out));
+              ptr<double>(count_out), optr<float>(shift));
   }
 
   // SyncBN backward, exchange fused: partial rows -> k [2][C] (global sums / total count), local dgamma / dbeta
@@ -772,7 +775,7 @@ class PeerComm {
     req(count_total, at::kDouble, "count_total");
     TORCH_CHECK(part.numel() >= 2L * G * C && k.numel() >= 2L * C, "PeerComm.bn_bwd: sizes");
     launch_bn(false, part, G, C, 0.0, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, ptr<float>(k),
-              optr<float>(dgamma), optr<float>(dbeta), ptr<double>(count_total));
+              optr<float>(dgamma), optr<float>(dbeta), ptr<double>(count_total), nullptr);
   }
 
   int error() {
@@ -794,12 +797,12 @@ class PeerComm {
  private:
   void launch_bn(bool fwd, Tensor& part, int G, int C, double count, const float* gamma, const float* beta,
                  float* rmean, float* rvar, long long* nbt, float momentum, float eps, float* out, float* dgamma,
-                 float* dbeta, double* count_io) {
+                 float* dbeta, double* count_io, const float* shift) {
     TORCH_CHECK(C <= peer_bn_max_channels(), "PeerComm: at most ", peer_bn_max_channels(), " BN channels");
     for (int q = 0; q < world_; ++q) TORCH_CHECK(bases_[q] != 0ull, "PeerComm: peers not opened");
     ++seq_;
     check(peer_bn_launch(fwd, ptr<float>(part), G, C, count, gamma, beta, rmean, rvar, nbt, momentum, eps, out, dgamma,
-                         dbeta, count_io, bases_.data(), rank_, world_, seq_, timeout_ticks_, err_, cur()),
+                         dbeta, count_io, shift, bases_.data(), rank_, world_, seq_, timeout_ticks_, err_, cur()),
           "peer_bn");
   }
 
@@ -835,8 +838,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_set_wgrad_variant", &conv_set_wgrad_variant);
   m.def("bn_partials", &bn_partials, pybind11::arg("part"), pybind11::arg("G"), pybind11::arg("C"),
         pybind11::arg("sums"), pybind11::arg("dgamma"), pybind11::arg("dbeta"), pybind11::arg("count") = -1.0);
-  m.def("bn_finalize", &bn_finalize);
-  m.def("bn_reduce_finalize", &bn_reduce_finalize);
+  m.def("bn_finalize", &bn_finalize, pybind11::arg("sums"), pybind11::arg("count_t"), pybind11::arg("count"),
+        pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("rmean"), pybind11::arg("rvar"),
+        pybind11::arg("nbt"), pybind11::arg("momentum"), pybind11::arg("eps"), pybind11::arg("C"),
+        pybind11::arg("coef"), pybind11::arg("shift") = pybind11::none());
+  m.def("bn_reduce_finalize", &bn_reduce_finalize, pybind11::arg("part"), pybind11::arg("G"), pybind11::arg("C"),
+        pybind11::arg("count"), pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("rmean"),
+        pybind11::arg("rvar"), pybind11::arg("nbt"), pybind11::arg("momentum"), pybind11::arg("eps"),
+        pybind11::arg("coef"), pybind11::arg("shift") = pybind11::none());
   m.def("bn_reduce_bwd", &bn_reduce_bwd, pybind11::arg("part"), pybind11::arg("G"), pybind11::arg("C"),
         pybind11::arg("count"), pybind11::arg("dgamma"), pybind11::arg("dbeta"), pybind11::arg("k"),
         pybind11::arg("coef") = pybind11::none(), pybind11::arg("xa") = pybind11::none());
@@ -875,12 +884,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_set_reduce_blocks", &bn_set_reduce_blocks, pybind11::arg("n"), pybind11::arg("chb") = 0);
   m.def("bn_act_maxpool", &bn_act_maxpool);
   m.def("bn_set_unroll", [](bool v) { bn_set_unroll(v ? 1 : 0); });
-  m.def("stem_conv", &stem_conv);
+  m.def("stem_conv", &stem_conv, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"), pybind11::arg("part"),
+        pybind11::arg("G"), pybind11::arg("N"), pybind11::arg("H"), pybind11::arg("W"),
+        pybind11::arg("shift") = pybind11::none());
   m.def("direct_conv", &direct_conv, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"),
         pybind11::arg("part"), pybind11::arg("G"), pybind11::arg("N"), pybind11::arg("H"), pybind11::arg("W"),
         pybind11::arg("Cin"), pybind11::arg("OH"), pybind11::arg("OW"), pybind11::arg("Cout"), pybind11::arg("pt"),
         pybind11::arg("pl"), pybind11::arg("cfg"), pybind11::arg("y_bn") = pybind11::none(),
-        pybind11::arg("coef") = pybind11::none(), pybind11::arg("act") = 0);
+        pybind11::arg("coef") = pybind11::none(), pybind11::arg("act") = 0, pybind11::arg("shift") = pybind11::none());
   m.def("conv_fp8_cfgs", []() {
     std::vector<std::vector<int>> out;
     for (int i = 0; i < conv_num_fp8_cfgs(); ++i) {
@@ -929,7 +940,8 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("G") = 1, pybind11::arg("act") = 0);
   m.def("act32_fwd", &act32_fwd);
   m.def("act32_bwd", &act32_bwd);
-  m.def("bn_stats", &bn_stats);
+  m.def("bn_stats", &bn_stats, pybind11::arg("y"), pybind11::arg("rows"), pybind11::arg("C"), pybind11::arg("part"),
+        pybind11::arg("G"), pybind11::arg("shift") = pybind11::none());
   m.def("se_mlp_fwd", &se_mlp_fwd);
   m.def("se_mlp_bwd", &se_mlp_bwd);
   pybind11::class_<PeerComm>(m, "PeerComm")
@@ -938,7 +950,10 @@ PYBIND11_MODULE(_C, m) {
       .def("handle", &PeerComm::handle)
       .def("open", &PeerComm::open)
       .def("all_reduce_", &PeerComm::all_reduce_)
-      .def("bn_fwd", &PeerComm::bn_fwd)
+      .def("bn_fwd", &PeerComm::bn_fwd, pybind11::arg("part"), pybind11::arg("G"), pybind11::arg("C"),
+           pybind11::arg("count"), pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("rmean"),
+           pybind11::arg("rvar"), pybind11::arg("nbt"), pybind11::arg("momentum"), pybind11::arg("eps"),
+           pybind11::arg("coef"), pybind11::arg("count_out"), pybind11::arg("shift") = pybind11::none())
       .def("bn_bwd", &PeerComm::bn_bwd)
       .def("error", &PeerComm::error)
       .def("set_timeout", &PeerComm::set_timeout)

@@ -1,7 +1,10 @@
 // BatchNorm (training + eval) for NHWC bf16 activations, fp32 statistics.
 //
 // Forward (K5, K8, K9):
-//   conv epilogue -> per-channel (sum, sumsq) fp32 partials in G rotating rows
+//   conv epilogue -> per-channel (sum, sumsq) fp32 partials in G rotating rows, taken about a per-channel
+//                    pivot K (the BN's running mean; 0 without one): sums of (x - K) and (x - K)^2, so the
+//                    variance S2/n - (S1/n)^2 never cancels at large |mean| / std once K tracks the mean
+//                    (the shifted-data form of Chan's parallel combine; K is identical on every rank)
 //   bn_partials   -> fp64 per-channel sums, partial rows re-zeroed for the next layer
 //   [SyncBN: RCCL all-reduce of the fp64 sums + count]
 //   bn_finalize   -> scale = gamma*invstd, shift = beta - mean*scale (+ mean, invstd),
@@ -61,7 +64,16 @@ struct BnFinalizeArgs {
   float* part; int G, C; double count;
   const float* gamma; const float* beta; float* rmean; float* rvar; long long* nbt;
   float momentum, eps; float* coef;
+  const float* shift;  // pivot the partial sums were taken about (or null = 0)
 };
+
+// mean / biased variance from sums of (x - K) and (x - K)^2 over n elements
+DEVI void shifted_moments(double s, double q, double n, double K, double& mean, double& var) {
+  const double m1 = s / n;
+  mean = K + m1;
+  var = q / n - m1 * m1;
+  var = var < 0.0 ? 0.0 : var;
+}
 
 DEVI void reduce_partials_64(float* part, int G, int C, int c, int lc, int lg, double (*red)[4][64],
                              double& s, double& q) {
@@ -93,9 +105,8 @@ __global__ __launch_bounds__(256) void bn_reduce_finalize_kernel(BnFinalizeArgs 
   if (blockIdx.x == 0 && threadIdx.x == 0 && a.nbt) *a.nbt += 1;
   if (lg != 0 || c >= a.C) return;
   const double n = a.count;
-  const double mean = s / n;
-  double var = q / n - mean * mean;
-  var = var < 0.0 ? 0.0 : var;
+  double mean, var;
+  shifted_moments(s, q, n, a.shift ? (double)a.shift[c] : 0.0, mean, var);
   const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
   const float g = a.gamma ? a.gamma[c] : 1.f, b = a.beta ? a.beta[c] : 0.f;
   const float scale = g * invstd;
@@ -150,16 +161,15 @@ __global__ void bn_xa_coef_kernel(const float* __restrict__ coef, const float* _
 // coef layout [4][C]: scale, shift, mean, invstd
 __global__ void bn_finalize_kernel(const double* __restrict__ sums, const double* __restrict__ count_p,
                                    double count_host, const float* __restrict__ gamma,
-                                   const float* __restrict__ beta, float* __restrict__ rmean,
+                                   const float* __restrict__ beta, float* rmean,
                                    float* __restrict__ rvar, long long* __restrict__ nbt, float momentum,
-                                   float eps, int C, float* __restrict__ coef) {
+                                   float eps, int C, float* __restrict__ coef, const float* shift) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   const double n = count_p ? *count_p : count_host;
   if (c == 0 && nbt) *nbt += 1;
   if (c >= C) return;
-  const double mean = sums[c] / n;
-  double var = sums[C + c] / n - mean * mean;
-  var = var < 0.0 ? 0.0 : var;
+  double mean, var;
+  shifted_moments(sums[c], sums[C + c], n, shift ? (double)shift[c] : 0.0, mean, var);
   const float invstd = (float)(1.0 / sqrt(var + (double)eps));
   const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
   const float scale = g * invstd;
@@ -560,7 +570,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_u_kernel(
 // ---- standalone statistics pass (outputs not produced by the GEMM epilogue) --
 __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict__ y, long rows, int C,
                                                        long rows_per_block, float* __restrict__ part, int G,
-                                                       int CHB) {
+                                                       int CHB, const float* __restrict__ shift) {
   __shared__ float red[2][256][9];
   const int cch = C >> 3;
   const int RP = 256 / CHB;
@@ -573,12 +583,15 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict_
   if (lr < RP && chunk < cch) {
     const long rbeg = blockIdx.x * rows_per_block;
     const long rend = rbeg + rows_per_block < rows ? rbeg + rows_per_block : rows;
+    float K[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) K[k] = shift ? shift[chunk * 8 + k] : 0.f;
 #pragma unroll 4
     for (long row = rbeg + lr; row < rend; row += RP) {
       float v[8];
       unpack8(*(const uint4*)(y + row * C + chunk * 8), v);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) { s[k] += v[k]; q[k] += v[k] * v[k]; }
+      for (int k = 0; k < 8; ++k) { const float d = v[k] - K[k]; s[k] += d; q[k] += d * d; }
     }
   }
 #pragma unroll
@@ -778,8 +791,8 @@ int bn_partials_launch(float* part, int G, int C, double* sums, float* dgamma, f
 
 int bn_reduce_finalize_launch(float* part, int G, int C, double count, const float* gamma, const float* beta,
                               float* rmean, float* rvar, long long* nbt, float momentum, float eps, float* coef,
-                              hipStream_t s) {
-  BnFinalizeArgs a{part, G, C, count, gamma, beta, rmean, rvar, nbt, momentum, eps, coef};
+                              const float* shift, hipStream_t s) {
+  BnFinalizeArgs a{part, G, C, count, gamma, beta, rmean, rvar, nbt, momentum, eps, coef, shift};
   hipLaunchKernelGGL(bn_reduce_finalize_kernel, dim3(cdiv(C, 64)), dim3(256), 0, s, a);
   HIP_CHECK_LAUNCH();
   return 0;
@@ -801,9 +814,9 @@ int bn_xa_coef_launch(const float* coef, const float* k, int C, float* xa, hipSt
 
 int bn_finalize_launch(const double* sums, const double* count_p, double count, const float* gamma,
                        const float* beta, float* rmean, float* rvar, long long* nbt, float momentum,
-                       float eps, int C, float* coef, hipStream_t s) {
+                       float eps, int C, float* coef, const float* shift, hipStream_t s) {
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, sums, count_p, count, gamma,
-                     beta, rmean, rvar, nbt, momentum, eps, C, coef);
+                     beta, rmean, rvar, nbt, momentum, eps, C, coef, shift);
   HIP_CHECK_LAUNCH();
   return 0;
 }
@@ -888,9 +901,9 @@ int bn_bwd_elemt_launch(const bf16_t* g, const bf16_t* y, const float* coef, con
   return 0;
 }
 
-int bn_stats_launch(const bf16_t* y, long rows, int C, float* part, int G, hipStream_t s) {
+int bn_stats_launch(const bf16_t* y, long rows, int C, float* part, int G, const float* shift, hipStream_t s) {
   const RedGrid rg = reduce_grid(rows, C);
-  hipLaunchKernelGGL(bn_stats_kernel, rg.grid, dim3(256), 0, s, y, rows, C, rg.rpb, part, G, rg.chb);
+  hipLaunchKernelGGL(bn_stats_kernel, rg.grid, dim3(256), 0, s, y, rows, C, rg.rpb, part, G, rg.chb, shift);
   HIP_CHECK_LAUNCH();
   return 0;
 }

@@ -24,7 +24,8 @@ struct ConvParams {
   const bf16_t* A;
   const bf16_t* B;
   bf16_t* C;
-  float* stats;        // optional BN partials [G][2][Ncols] fp32 (sum, sum of squares)
+  float* stats;        // optional BN partials [G][2][Ncols] fp32 (sum, sum of squares) of (y - stats_shift)
+  const float* stats_shift;  // optional per-channel pivot of those sums (the BN's running mean), else 0
   const float* bias;   // optional [Ncols]
   int M, Ncols, K, CA;
   int GH, GW, IH, IW, sA;

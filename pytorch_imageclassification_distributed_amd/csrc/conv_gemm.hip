@@ -89,9 +89,9 @@ DEVI void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN 
   const int col = n0 + sch * 8;
   const bool col_ok = col < p.Ncols;
   const bool direct = (p.so == 1 && p.oh0 == 0 && p.ow0 == 0 && p.GH == p.OH && p.GW == p.OW);
-  float s8[8], q8[8];
+  float s8[8], q8[8], k8[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) { s8[k] = 0.f; q8[k] = 0.f; }
+  for (int k = 0; k < 8; ++k) { s8[k] = 0.f; q8[k] = 0.f; k8[k] = (p.stats_shift && col_ok) ? p.stats_shift[col + k] : 0.f; }
   const bool bwd = p.bwd_y != nullptr;
   float bsc[8], bsh[8], bmu[8], bis[8];
   if (bwd && col_ok) {
@@ -149,7 +149,7 @@ DEVI void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN 
         float f[8];
         unpack8(v, f);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) { s8[k] += f[k]; q8[k] += f[k] * f[k]; }
+        for (int k = 0; k < 8; ++k) { const float d = f[k] - k8[k]; s8[k] += d; q8[k] += d * d; }
       }
     }
   }
@@ -247,9 +247,16 @@ DEVI void conv_epi(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16]
   const int col = n0 + sch * 8;
   const bool col_ok = col < p.Ncols;
   const int col_l = col_ok ? col : 0;
-  float s8[8], q8[8];
+  float s8[8], q8[8], k8[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) { s8[k] = 0.f; q8[k] = 0.f; }
+  for (int k = 0; k < 8; ++k) { s8[k] = 0.f; q8[k] = 0.f; k8[k] = 0.f; }
+  if constexpr (STATS) {
+    if (p.stats_shift != nullptr) {  // pivot of the statistics (the BN's running mean)
+      const f32x4 a = *(const f32x4*)(p.stats_shift + col_l), b = *(const f32x4*)(p.stats_shift + col_l + 4);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { k8[k] = a[k]; k8[4 + k] = b[k]; }
+    }
+  }
   __syncthreads();
   float bsc[8], bsh[8], bmu[8], bis[8];
   if constexpr (BWD) {
@@ -324,7 +331,7 @@ DEVI void conv_epi(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16]
       if constexpr (STATS) {
         if (ok[u]) {
 #pragma unroll
-          for (int k = 0; k < 8; ++k) { s8[k] += f[k]; q8[k] += f[k] * f[k]; }
+          for (int k = 0; k < 8; ++k) { const float d = f[k] - k8[k]; s8[k] += d; q8[k] += d * d; }
         }
       }
     }

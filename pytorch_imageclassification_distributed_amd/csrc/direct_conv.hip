@@ -30,6 +30,7 @@ struct DirectArgs {
   int act;
   int N, H, W, Cin, OH, OW, Cout, pt, pl, G;
   int tiles_w, tiles_hw, ntiles, nco;
+  const float* shift;  // forward statistics: sums of (y - shift[c]) (the BN's running mean), or null = 0
 };
 
 template <int CIP, int KH, int KW, int COT>
@@ -123,11 +124,16 @@ __global__ __launch_bounds__(256, (DC<CIP, KH, KW, COT>::OCC)) void direct_conv_
   if (t + tstride < a.ntiles) dload<CIP, KH, KW, COT>(a, t + tstride, tid, regA);
   __syncthreads();
 
-  float s[D::CB][4], q[D::CB][4];  // forward statistics: channel cb*16 + 4*lg + i
+  float s[D::CB][4], q[D::CB][4], kpiv[D::CB][4];  // forward statistics: channel cb*16 + 4*lg + i
 #pragma unroll
   for (int cb = 0; cb < D::CB; ++cb)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) { s[cb][i] = 0.f; q[cb][i] = 0.f; }
+    for (int i = 0; i < 4; ++i) {
+      s[cb][i] = 0.f;
+      q[cb][i] = 0.f;
+      const int co = co0 + cb * 16 + 4 * lg + i;
+      kpiv[cb][i] = (!BWD && a.shift && co < a.Cout) ? a.shift[co] : 0.f;
+    }
   // BWD: each lane's read-back chunk c = lane % CH is fixed, so it owns 8 channels for the whole kernel
   const int rc = lane % D::CH, rco = co0 + rc * 8;
   float bs[8], bq[8], bsc[8], bsh[8], bmu[8], bis[8];
@@ -190,7 +196,7 @@ __global__ __launch_bounds__(256, (DC<CIP, KH, KW, COT>::OCC)) void direct_conv_
         *(uint2*)(stg + p * (COT * 2) + ((c ^ (p & (D::CH - 1))) * 16) + (lg & 1) * 8) = pk;
         if (!BWD && live) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) { s[cb][i] += v[i]; q[cb][i] += v[i] * v[i]; }
+          for (int i = 0; i < 4; ++i) { const float d = v[i] - kpiv[cb][i]; s[cb][i] += d; q[cb][i] += d * d; }
         }
       }
     }
@@ -322,8 +328,8 @@ int direct_conv_num_cfgs() { return 5; }
 
 int direct_conv_launch(const bf16_t* x, const bf16_t* w, bf16_t* y, float* part, int G, int N, int H, int W,
                        int Cin, int OH, int OW, int Cout, int pt, int pl, int cfg, const bf16_t* y_bn,
-                       const float* coef, int act, hipStream_t s) {
-  DirectArgs a{x, w, y, part, y_bn, coef, act, N, H, W, Cin, OH, OW, Cout, pt, pl, G > 0 ? G : 1, 0, 0, 0, 1};
+                       const float* coef, int act, const float* shift, hipStream_t s) {
+  DirectArgs a{x, w, y, part, y_bn, coef, act, N, H, W, Cin, OH, OW, Cout, pt, pl, G > 0 ? G : 1, 0, 0, 0, 1, shift};
   const bool bwd = y_bn != nullptr;
   a.tiles_w = cdiv(OW, 16);
   a.tiles_hw = cdiv(OH, 8) * a.tiles_w;

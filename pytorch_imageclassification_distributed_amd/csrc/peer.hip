@@ -158,6 +158,7 @@ struct PeerBnArgs {
   float* dgamma;             // backward: local sum dz * xhat
   float* dbeta;              // backward: local sum dz
   double* count_io;          // forward: total count (out); backward: total count (in)
+  const float* shift;        // forward: pivot of the partial sums (the running mean, equal on every rank)
 };
 
 template <bool FWD>
@@ -227,8 +228,9 @@ __global__ __launch_bounds__(256) void peer_bn_kernel(PeerBnArgs a, PeerTable ta
       if (a.count_io) *a.count_io = n;
     }
     if (c >= C) return;
-    const double mean = S / n;
-    double var = Q / n - mean * mean;
+    const double m1 = S / n;  // sums are of (x - K): the shifted-data form of Chan's combine
+    const double mean = (a.shift ? (double)a.shift[c] : 0.0) + m1;
+    double var = Q / n - m1 * m1;
     var = var < 0.0 ? 0.0 : var;
     const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
     const float gm = a.gamma ? a.gamma[c] : 1.f, bt = a.beta ? a.beta[c] : 0.f;
@@ -300,14 +302,15 @@ int peer_bn_max_channels() { return kBnCB * kBnMaxBlocks; }
 
 int peer_bn_launch(bool fwd, float* part, int G, int C, double count, const float* gamma, const float* beta,
                    float* rmean, float* rvar, long long* nbt, float momentum, float eps, float* out, float* dgamma,
-                   float* dbeta, double* count_io, const unsigned long long* bases, int rank, int world,
-                   unsigned long long seq, unsigned long long timeout_ticks, int* err, hipStream_t st) {
+                   float* dbeta, double* count_io, const float* shift, const unsigned long long* bases, int rank,
+                   int world, unsigned long long seq, unsigned long long timeout_ticks, int* err, hipStream_t st) {
   if (C <= 0) return 0;
   if (world < 1 || world > kMaxWorld || rank < 0 || rank >= world || C > kBnCB * kBnMaxBlocks || G < 1)
     return (int)hipErrorInvalidValue;
   PeerTable tab;
   for (int i = 0; i < kMaxWorld; ++i) tab.base[i] = i < world ? bases[i] : 0ull;
-  const PeerBnArgs a{part, G, C, count, gamma, beta, rmean, rvar, nbt, momentum, eps, out, dgamma, dbeta, count_io};
+  const PeerBnArgs a{part, G, C, count, gamma, beta, rmean, rvar, nbt, momentum, eps, out, dgamma, dbeta, count_io,
+                     shift};
   const int blocks = (C + kBnCB - 1) / kBnCB;
   if (fwd)
     hipLaunchKernelGGL(peer_bn_kernel<true>, dim3(blocks), dim3(256), 0, st, a, tab, rank, world, seq, timeout_ticks,

@@ -42,8 +42,9 @@ struct StemArgs {
   const bf16_t* x;  // [N, H, W, 16]
   const bf16_t* w;  // [64, 256]
   bf16_t* y;        // [N, H, W, 64]   (stride 1, pad 2 top/left, 1 bottom/right: same spatial size)
-  float* part;      // [G, 2, 64] or null
+  float* part;      // [G, 2, 64] or null: statistics of (y - shift[c]) (the BN's running mean; null = 0)
   int N, H, W, G, tiles_w, tiles_hw, ntiles;
+  const float* shift;
 };
 
 DEVI void tile_origin(const StemArgs& a, int t, int& n, int& oh0, int& ow0) {
@@ -104,11 +105,15 @@ __global__ __launch_bounds__(256, 2) void stem_s2d_conv_kernel(const StemArgs a)
   if (t + (int)gridDim.x < a.ntiles) load_patch(a, t + gridDim.x, tid, regA);
   __syncthreads();
 
-  float s[4][4], q[4][4];  // [channel block][i]: channel cb*16 + 4*lg + i
+  float s[4][4], q[4][4], kpiv[4][4];  // [channel block][i]: channel cb*16 + 4*lg + i
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) { s[cb][i] = 0.f; q[cb][i] = 0.f; }
+    for (int i = 0; i < 4; ++i) {
+      s[cb][i] = 0.f;
+      q[cb][i] = 0.f;
+      kpiv[cb][i] = a.shift ? a.shift[cb * 16 + 4 * lg + i] : 0.f;
+    }
 
   int buf = 0;
   // one tile; `rl` receives the patch of tile t + 2 grid, `rs` holds that of t + grid.  The loop below
@@ -166,7 +171,7 @@ __global__ __launch_bounds__(256, 2) void stem_s2d_conv_kernel(const StemArgs a)
         *(uint2*)(stg + p * 128 + ((c ^ (p & 7)) * 16) + (lg & 1) * 8) = pk;
         if (live) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) { s[cb][i] += v[i]; q[cb][i] += v[i] * v[i]; }
+          for (int i = 0; i < 4; ++i) { const float d = v[i] - kpiv[cb][i]; s[cb][i] += d; q[cb][i] += d * d; }
         }
       }
     }
@@ -226,8 +231,8 @@ __global__ __launch_bounds__(256, 2) void stem_s2d_conv_kernel(const StemArgs a)
 
 // y = conv4x4/s1/p(2,1)(x) over the s2d input, 64 output channels; part: BN statistics rows (or null)
 int stem_s2d_conv_launch(const bf16_t* x, const bf16_t* w, bf16_t* y, float* part, int G, int N, int H, int W,
-                         hipStream_t s) {
-  StemArgs a{x, w, y, part, N, H, W, G > 0 ? G : 1, 0, 0, 0};
+                         const float* shift, hipStream_t s) {
+  StemArgs a{x, w, y, part, N, H, W, G > 0 ? G : 1, 0, 0, 0, shift};
   a.tiles_w = cdiv(W, TW);
   a.tiles_hw = cdiv(H, TH) * a.tiles_w;
   a.ntiles = N * a.tiles_hw;

@@ -59,6 +59,22 @@ def stat_groups(rows: int) -> int:
     """Partial-sum rows for BN statistics over ``rows`` pixels: 64 rotating rows normally; in
     deterministic mode at least one per producing block (128-row conv tiles, <=1024 reduce blocks)."""
     return max(-(-rows // 128), 1024) if DETERMINISTIC else G_STATS
+# BN statistics are summed about a per-channel pivot K = the BN's running mean (identical on every rank under
+# SyncBN): sums of (x - K) and (x - K)^2, so var = S2/n - (S1/n)^2 cannot cancel at large |mean| / std once K
+# tracks the batch mean (the shifted-data form of Chan's parallel combine; csrc/bn.hip).  The producer (conv
+# epilogue, direct / stem kernels, bn_stats) and the finalize must use the same K: callers pass one tensor.
+SHIFT_STATS = os.environ.get("IMGCLS_BN_SHIFT", "1") == "1"
+
+
+def stat_shift(bn):
+    """The pivot of ``bn``'s training statistics (its running mean), or None (pivot 0)."""
+    rm = getattr(bn, "running_mean", None)
+    if not (SHIFT_STATS and bn.training and getattr(bn, "track_running_stats", False) and rm is not None
+            and rm.is_cuda and rm.dtype == torch.float32):
+        return None
+    return rm
+
+
 FUSE_BN_BWD = os.environ.get("IMGCLS_FUSE_BN_BWD", "1") == "1"  # BN-backward reduce in the consumer's dgrad
 FUSED_BWD_COUNT = [0]  # number of BN-backward reduces served by a conv epilogue (tests / diagnostics)
 
@@ -451,7 +467,7 @@ TUNE_LOG: list = []  # (M, Ncols, K, {cfg: ms}) per tuned geometry (benchmarks/c
 
 
 def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(None, None, None, None, 0, 1),
-               groups=G_STATS, scales=(None, None), xa=None):
+               groups=G_STATS, scales=(None, None), xa=None, shift=None):
     """One implicit-GEMM launch.  The kernel configuration - LDS-DMA ring depth (1 = high occupancy,
     2 / 3 = pipelined) x output-channel tile (64 / 128 / 256: more tiles balance 256 CUs better on
     small layers) x pixel tile (128 rows on 4 waves, or 256 rows on 8 waves) - is chosen once per
@@ -480,9 +496,9 @@ def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(
                 _STAGES_TUNED[key] = cfg
     if cfg[2] >= DIRECT_BASE:
         _direct_launch(A, B, out, stats, groups, _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales),
-                       cfg[2] - DIRECT_BASE, bwd)
+                       cfg[2] - DIRECT_BASE, bwd, shift)
         return
-    C.conv_gemm(A, B, out, stats, bias, *geo, dh, dw, tb, groups, zero, addend, *bwd, *cfg, *scales, *xa3)
+    C.conv_gemm(A, B, out, stats, bias, *geo, dh, dw, tb, groups, zero, addend, *bwd, *cfg, *scales, *xa3, shift)
 
 
 _CFGS = None
@@ -564,7 +580,7 @@ def _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales):
 _ORDER_IDX: dict = {}
 
 
-def _direct_launch(A, B, out, stats, groups, dg, variant, bwd):
+def _direct_launch(A, B, out, stats, groups, dg, variant, bwd, shift=None):
     n, ih, iw, cx, gh, gw, co, pt, pl, order = dg
     if order == tuple(range(9)):
         w = B
@@ -578,7 +594,7 @@ def _direct_launch(A, B, out, stats, groups, dg, variant, bwd):
         C.direct_conv(A, w, out, bwd[3], bwd[5], n, ih, iw, cx, gh, gw, co, pt, pl, variant,
                       y_bn=bwd[0], coef=bwd[2], act=bwd[4])
     else:
-        C.direct_conv(A, w, out, stats, groups, n, ih, iw, cx, gh, gw, co, pt, pl, variant)
+        C.direct_conv(A, w, out, stats, groups, n, ih, iw, cx, gh, gw, co, pt, pl, variant, shift=shift)
 
 
 def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups, scales=(None, None), xa=None):
@@ -592,7 +608,7 @@ def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, group
     times = {}
     for cfg in cands:
         times[cfg] = _time_ms(lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, groups, zero,
-                                                  addend, *bwd, *cfg, *scales, *xa3))
+                                                  addend, *bwd, *cfg, *scales, *xa3, None))
     dg = _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales) if xa is None else None
     if dg is not None:
         for v, (cip, cot) in DIRECT_CFGS.items():
@@ -607,10 +623,10 @@ def fp8_eligible(g: "ConvGeom") -> bool:
     return FP8_FWD and g.Cx == g.Ci and g.Cx % 128 == 0 and g.Co % 8 == 0
 
 
-def conv_forward_raw(x, w_param, g: ConvGeom, stats=None, bias=None, out=None, c_off=0, wb=None):
+def conv_forward_raw(x, w_param, g: ConvGeom, stats=None, bias=None, out=None, c_off=0, wb=None, shift=None):
     dev = x.device
     if wb is None and fp8_eligible(g):
-        return _conv_forward_fp8(x, w_param, g, stats, bias, out, c_off)
+        return _conv_forward_fp8(x, w_param, g, stats, bias, out, c_off, shift)
     if wb is None:
         wb = _weight_for_input(w_param, g.Cx)
     y = out if out is not None else _empty_cl(g.N, g.Co, g.OH, g.OW, dev)
@@ -620,11 +636,11 @@ def conv_forward_raw(x, w_param, g: ConvGeom, stats=None, bias=None, out=None, c
         raise NotImplementedError("anisotropic stride")
     geo = (g.N * g.OH * g.OW, g.Co, g.T * g.Cx, g.Cx, g.OH, g.OW, g.H, g.W, g.sh, g.T * g.Cx, g.OH, g.OW,
            1, 0, 0, ldc, c_off)
-    _conv_gemm(x, wb, y, stats, bias, geo, dh, dw, tb, ws(dev).zero, groups=stat_groups(geo[0]))
+    _conv_gemm(x, wb, y, stats, bias, geo, dh, dw, tb, ws(dev).zero, groups=stat_groups(geo[0]), shift=shift)
     return y
 
 
-def _conv_forward_fp8(x, w_param, g: ConvGeom, stats, bias, out, c_off):
+def _conv_forward_fp8(x, w_param, g: ConvGeom, stats, bias, out, c_off, shift=None):
     dev = x.device
     xq, xs = act_mx(x)
     wq, wsc = weight_mx(w_param)
@@ -633,7 +649,7 @@ def _conv_forward_fp8(x, w_param, g: ConvGeom, stats, bias, out, c_off):
     geo = (g.N * g.OH * g.OW, g.Co, g.T * g.Cx, g.Cx, g.OH, g.OW, g.H, g.W, g.sh, g.T * g.Cx, g.OH, g.OW,
            1, 0, 0, y.shape[1], c_off)
     _conv_gemm(xq, wq, y, stats, bias, geo, dh, dw, tb, ws(dev).zero, groups=stat_groups(geo[0]),
-               scales=(xs, wsc))
+               scales=(xs, wsc), shift=shift)
     return y
 
 
@@ -1018,10 +1034,10 @@ def xa_eligible(x, conv) -> bool:
 
 class ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, conv, want_stats, slot=None, fuse_bwd=False, xa=None):
+    def forward(ctx, x, w, conv, want_stats, slot=None, fuse_bwd=False, xa=None, shift=None):
         g = conv_geom(x, conv)
         stats = ws(x.device).stats_buf(g.Co, stat_groups(g.N * g.OH * g.OW)) if want_stats else None
-        y = conv_forward_raw(x, w, g, stats=stats)
+        y = conv_forward_raw(x, w, g, stats=stats, shift=shift if want_stats else None)
         ctx.g = g
         ctx.slot = slot
         ctx.xa = xa
@@ -1055,7 +1071,7 @@ class ConvFn(torch.autograd.Function):
             if slot is not None:
                 dx = slot.deliver(dx, fused=addend is not None)
         dw = conv_wgrad_raw(dy, x, w, g, xa=xa) if ctx.needs_input_grad[1] else None
-        return dx, dw, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None
 
 
 # ---------------------------------------------------------------------------
@@ -1110,7 +1126,7 @@ class StemS2dFn(torch.autograd.Function):
     """The ResNet stem conv on the space-to-depth input (the image itself needs no gradient)."""
 
     @staticmethod
-    def forward(ctx, x, w, conv, want_stats):
+    def forward(ctx, x, w, conv, want_stats, shift=None):
         n, _, h, wd = x.shape
         co = w.shape[0]
         xs = _empty_cl(n, 16, h // 2, wd // 2, x.device)
@@ -1123,9 +1139,9 @@ class StemS2dFn(torch.autograd.Function):
         stats = ws(x.device).stats_buf(co, grp) if want_stats else None
         if STEM_DIRECT and co == 64:  # halo-tile direct kernel (csrc/stem.hip)
             y = _empty_cl(g.N, co, g.OH, g.OW, x.device)
-            C.stem_conv(xs, wq, y, stats, grp, g.N, g.OH, g.OW)
+            C.stem_conv(xs, wq, y, stats, grp, g.N, g.OH, g.OW, shift=shift if want_stats else None)
         else:
-            y = conv_forward_raw(xs, None, g, stats=stats, wb=wq.view(-1))
+            y = conv_forward_raw(xs, None, g, stats=stats, wb=wq.view(-1), shift=shift if want_stats else None)
         ctx.g = g
         ctx.save_for_backward(xs, w)
         return y
@@ -1151,7 +1167,7 @@ class StemS2dFn(torch.autograd.Function):
                 _on_side(dy.device, launch, dy, xs, full)
             else:
                 launch()
-        return None, dw, None, None
+        return None, dw, None, None, None
 
 
 # ---------------------------------------------------------------------------
@@ -1204,8 +1220,9 @@ class DwConvFn(torch.autograd.Function):
 # ---------------------------------------------------------------------------
 # BatchNorm (+ residual) (+ activation)
 # ---------------------------------------------------------------------------
-def _bn_coef(y, gamma, beta, bn, stats_ready):
+def _bn_coef(y, gamma, beta, bn, stats_ready, shift=None):
     """Batch (training) or running (eval) statistics of ``y`` -> coef [4, C] = scale, shift, mean, invstd.
+    ``shift``: the pivot the partial sums are taken about (``stat_shift``; the producer used the same).
     Returns (coef, SyncBN group or None, all-reduced count tensor or None)."""
     dev = y.device
     n, c, h, w = y.shape
@@ -1216,24 +1233,24 @@ def _bn_coef(y, gamma, beta, bn, stats_ready):
         grp = stat_groups(rows)
         part = ws(dev).stats_buf(c, grp)
         if not stats_ready:
-            C.bn_stats(y, rows, c, part, grp)
+            C.bn_stats(y, rows, c, part, grp, shift=shift)
         group = _sync_group(bn)
         mom = bn.momentum if bn.momentum is not None else 0.1
         track = bn.track_running_stats and bn.running_mean is not None
         rs = (bn.running_mean, bn.running_var, bn.num_batches_tracked) if track else (None, None, None)
         if group is None:  # one launch: partial rows -> coefficients + running stats
-            C.bn_reduce_finalize(part, grp, c, float(rows), gamma, beta, *rs, mom, bn.eps, coef)
+            C.bn_reduce_finalize(part, grp, c, float(rows), gamma, beta, *rs, mom, bn.eps, coef, shift=shift)
         else:
             pc = peer_channel(group, 0)
             if pc is not None and c <= PEER_BN_MAX_C:  # one kernel: reduce + xGMI exchange + finalize
                 count_t = torch.empty(1, dtype=torch.float64, device=dev)
-                pc.comm.bn_fwd(part, grp, c, float(rows), gamma, beta, *rs, mom, bn.eps, coef, count_t)
+                pc.comm.bn_fwd(part, grp, c, float(rows), gamma, beta, *rs, mom, bn.eps, coef, count_t, shift=shift)
             else:
                 sums = torch.empty(2 * c + 1, dtype=torch.float64, device=dev)
                 C.bn_partials(part, grp, c, sums, None, None, float(rows))  # + local count in the tail
                 stats_all_reduce_(sums, group)
                 count_t = sums[2 * c:]
-                C.bn_finalize(sums, count_t, float(rows), gamma, beta, *rs, mom, bn.eps, c, coef)
+                C.bn_finalize(sums, count_t, float(rows), gamma, beta, *rs, mom, bn.eps, c, coef, shift=shift)
     else:
         if stats_ready:
             raise RuntimeError("eval-mode BN received fused statistics")
@@ -1269,12 +1286,13 @@ def _bn_bwd_k(part, grp, c, rows, training, group, count_t, params, dev, coef=No
 
 class BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, y, gamma, beta, res, bn, act, stats_ready, res_slot=None, link=None, cat=None, xa=None):
+    def forward(ctx, y, gamma, beta, res, bn, act, stats_ready, res_slot=None, link=None, cat=None, xa=None,
+                shift=None):
         dev = y.device
         n, c, h, w = y.shape
         rows = n * h * w
         a = ACT[act]
-        coef, group, count_t = _bn_coef(y, gamma, beta, bn, stats_ready)
+        coef, group, count_t = _bn_coef(y, gamma, beta, bn, stats_ready, shift)
         if cat is not None:  # write straight into this branch's channel slice of the concat output
             cbuf, idx = cat
             base = cbuf.ensure(n, h, w, dev)
@@ -1365,7 +1383,7 @@ class BNActFn(torch.autograd.Function):
         dres = dz if ctx.has_res else None
         if dres is not None and ctx.res_slot is not None:
             dres = ctx.res_slot.deliver(dres)
-        return dy, dgamma, dbeta, dres, None, None, None, None, None, None, None
+        return dy, dgamma, dbeta, dres, None, None, None, None, None, None, None, None
 
 
 class BNActPoolFn(torch.autograd.Function):
@@ -1375,14 +1393,14 @@ class BNActPoolFn(torch.autograd.Function):
     gathering the pooled gradient inside both BN-backward passes measured slower (docs/DESIGN.md)."""
 
     @staticmethod
-    def forward(ctx, y, gamma, beta, bn, act, stats_ready, pool):
+    def forward(ctx, y, gamma, beta, bn, act, stats_ready, pool, shift=None):
         dev = y.device
         n, c, h, w = y.shape
         (kh, kw), (sh, sw), (ph, pw) = pool
         oh = (h + 2 * ph - kh) // sh + 1
         ow = (w + 2 * pw - kw) // sw + 1
         a = ACT[act]
-        coef, group, count_t = _bn_coef(y, gamma, beta, bn, stats_ready)
+        coef, group, count_t = _bn_coef(y, gamma, beta, bn, stats_ready, shift)
         out = _empty_cl(n, c, oh, ow, dev)
         idx = torch.empty((n, oh, ow, c), dtype=torch.uint8, device=dev)
         geo = [h, w, oh, ow, kh, kw, sh, sw, ph, pw]
@@ -1408,7 +1426,7 @@ class BNActPoolFn(torch.autograd.Function):
         k, dgamma, dbeta = _bn_bwd_k(part, grp, c, rows, ctx.training, ctx.group, ctx.count_t, ctx.params, dev)
         dy = torch.empty_like(y, memory_format=CL)
         C.bn_bwd_elemt(g, y, coef, k, None, None, dy, rows, c, ctx.act)
-        return dy, dgamma, dbeta, None, None, None, None
+        return dy, dgamma, dbeta, None, None, None, None, None
 
 
 STEM_POOL_FUSE = os.environ.get("IMGCLS_STEM_POOL_FUSE", "1") == "1"
@@ -1421,13 +1439,14 @@ def conv_bn_act_pool(x, conv, bn, act, pool, exclusive_input=False):
     if not STEM_POOL_FUSE or k[0] * k[1] > 255 or 2 * p[0] > k[0] or 2 * p[1] > k[1]:
         return max_pool2d(conv_bn_act(x, conv, bn, act, None, exclusive_input=exclusive_input), *pool)
     ensure_channels_last_weight(conv)
+    shift = stat_shift(bn)
     if stem_s2d_eligible(x, conv) and not x.requires_grad:
-        y = StemS2dFn.apply(x, conv.weight, conv, bn.training)
+        y = StemS2dFn.apply(x, conv.weight, conv, bn.training, shift)
     else:
         if conv.groups != 1 or conv.bias is not None:
             raise NotImplementedError("conv_bn_act_pool: grouped conv / conv bias")
-        y = ConvFn.apply(_cl(x), conv.weight, conv, bn.training, None, exclusive_input and FUSE_BN_BWD)
-    return BNActPoolFn.apply(y, bn.weight, bn.bias, bn, act, bn.training, (k, s, p))
+        y = ConvFn.apply(_cl(x), conv.weight, conv, bn.training, None, exclusive_input and FUSE_BN_BWD, None, shift)
+    return BNActPoolFn.apply(y, bn.weight, bn.bias, bn, act, bn.training, (k, s, p), shift)
 
 
 def dense_conv_eligible(x, conv) -> bool:
@@ -1464,14 +1483,14 @@ class DenseConvFn(torch.autograd.Function):
     split-K weight gradient into the gradient arena slot - no library GEMM."""
 
     @staticmethod
-    def forward(ctx, x, w, conv, want_stats=False):
+    def forward(ctx, x, w, conv, want_stats=False, shift=None):
         n, c, h, wd = x.shape
         co = w.shape[0]
         k = h * wd * c
         g = _dense_geom(n, k, co)
         xf = _as_pixel_rows(x, n, k)
         stats = ws(x.device).stats_buf(co, stat_groups(n)) if want_stats else None
-        y = conv_forward_raw(xf, w, g, stats=stats, wb=weight_bf16(w))
+        y = conv_forward_raw(xf, w, g, stats=stats, wb=weight_bf16(w), shift=shift if want_stats else None)
         ctx.g, ctx.xshape = g, (n, c, h, wd)
         ctx.save_for_backward(xf, w)
         return y
@@ -1489,7 +1508,7 @@ class DenseConvFn(torch.autograd.Function):
                 d.untyped_storage(), d.storage_offset(), (n, c, h, wd), (h * wd * c, 1, wd * c, c))
         if ctx.needs_input_grad[1]:
             dw = conv_wgrad_raw(dy, xf, w, g)
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
 POOL_CONV_SWAP = os.environ.get("IMGCLS_POOL_CONV_SWAP", "1") == "1"
@@ -1512,18 +1531,19 @@ def pool_conv_bn_act(x, conv, bn, act, prepool, x_slot=None, out=None, out_plan=
     ensure_channels_last_weight(conv)
     y = ConvFn.apply(x, conv.weight, conv, False, x_slot, False)
     yp = AvgPoolFn.apply(y, k, s, p, None)
-    return BNActFn.apply(yp, bn.weight, bn.bias, None, bn, act, False, None, None, out)
+    return BNActFn.apply(yp, bn.weight, bn.bias, None, bn, act, False, None, None, out, None, stat_shift(bn))
 
 
 def conv_bn_act(x, conv, bn, act, residual, x_slot=None, res_slot=None, exclusive_input=False, out=None):
     """``exclusive_input``: this conv is the only consumer of ``x`` (lets its dgrad fuse the BN-backward
     reduce of x's producer); a slot-paired consumer qualifies automatically.  ``out`` = (ConcatBuffer,
     branch index): the result is written into that branch's channel slice of the concat output."""
+    shift = stat_shift(bn)
     if stem_s2d_eligible(x, conv) and residual is None and not x.requires_grad:
         ensure_channels_last_weight(conv)
-        y = StemS2dFn.apply(x, conv.weight, conv, bn.training)
+        y = StemS2dFn.apply(x, conv.weight, conv, bn.training, shift)
         link = BwdLink() if (FUSE_BN_BWD and bn.training and torch.is_grad_enabled()) else None
-        out = BNActFn.apply(y, bn.weight, bn.bias, None, bn, act, bn.training, None, link)
+        out = BNActFn.apply(y, bn.weight, bn.bias, None, bn, act, bn.training, None, link, None, None, shift)
         if link is not None:
             out._imgcls_link = link
         return out
@@ -1541,19 +1561,19 @@ def conv_bn_act(x, conv, bn, act, residual, x_slot=None, res_slot=None, exclusiv
         ready = False
     elif dense_conv_eligible(x, conv) and x.shape[2] * x.shape[3] > 1:
         dense = True
-        y = DenseConvFn.apply(x, conv.weight, conv, bn.training)
+        y = DenseConvFn.apply(x, conv.weight, conv, bn.training, shift)
         ready = bn.training
     else:
         if conv.groups != 1:
             raise NotImplementedError("grouped convolution")
         xa = XaLink() if (bn.training and torch.is_grad_enabled() and xa_eligible(x, conv)) else None
-        y = ConvFn.apply(x, conv.weight, conv, bn.training, x_slot, exclusive_input and FUSE_BN_BWD, xa)
+        y = ConvFn.apply(x, conv.weight, conv, bn.training, x_slot, exclusive_input and FUSE_BN_BWD, xa, shift)
         ready = bn.training
     if conv.bias is not None:
         raise NotImplementedError("conv bias before BatchNorm")
     link = BwdLink() if (FUSE_BN_BWD and bn.training and torch.is_grad_enabled()) else None
     res_out = BNActFn.apply(y, bn.weight, bn.bias, residual, bn, act, ready, res_slot, link, out,
-                            xa if not depthwise and not dense else None)
+                            xa if not depthwise and not dense else None, shift)
     if link is not None:
         res_out._imgcls_link = link
     return res_out

@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 ( while true; do sleep 30; date +%s >> gpurun_out/r5d_ticks.txt; done ) & TICK=$!
 trap 'kill $TICK' EXIT
 timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_hip_ops.py \
-  -k "fused or shadow or dense" > gpurun_out/r5d_pytest_xa.log 2>&1 || { tail -40 gpurun_out/r5d_pytest_xa.log; exit 1; }
+  -k "fused or shadow or dense or large_mean or conv_bn_act or stem" > gpurun_out/r5d_pytest_xa.log 2>&1 || { tail -40 gpurun_out/r5d_pytest_xa.log; exit 1; }
 tail -2 gpurun_out/r5d_pytest_xa.log
 b() { local tag=$1; shift; timeout -k 10 400 python bench.py "$@" > gpurun_out/r5d_$tag.log 2>&1 || { tail -5 gpurun_out/r5d_$tag.log; return 1; }
       echo "$tag $(grep -h '^{"metric' gpurun_out/r5d_$tag.log | cut -c80-170)"; }

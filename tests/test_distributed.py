@@ -237,6 +237,8 @@ def _w_order(rank, world, port):
     layouts = [None] * world
     dist.all_gather_object(layouts, [(s, e, list(i)) for s, e, i in red.buckets])
     assert layouts[0] == layouts[1]  # rank 0's observed order is the one every rank rebuilt with
+    dist.barrier()
+    dist.destroy_process_group()  # clean gloo teardown before exit (an exit with live gloo threads can abort)
 
 
 def test_bucket_rebuild_uses_rank0_order():

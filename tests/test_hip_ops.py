@@ -1102,3 +1102,51 @@ def test_bn_backward_fused_every_kernel_variant():
                 assert rel_err(a_, b_) < 2e-2, (i, wst, rel_err(a_, b_))
             ran += 1
     assert ran >= 8
+
+
+@pytest.mark.parametrize("path", ["bn_stats", "conv_epilogue"])
+def test_bn_statistics_large_mean(path):
+    """BN training statistics at |mean| / std ~ 20 (about as large as bf16 activations can carry the
+    spread): the partial sums are taken about the running mean (ops/hip.py stat_shift), so the variance
+    does not cancel.  The batch mean / variance (read back from the running-statistics update) against
+    fp64 statistics of the same bf16 values, for the standalone statistics pass and the conv epilogue."""
+    hip = _hip()
+    torch.manual_seed(41)
+    n, c, hw = 16, 128, 28
+
+    def run(shift_on):
+        keep = hip.SHIFT_STATS
+        hip.SHIFT_STATS = shift_on
+        try:
+            bn = nn.BatchNorm2d(c, momentum=1.0).to(DEV)  # running stats = this batch's statistics
+            with torch.no_grad():
+                bn.running_mean.fill_(60.0)  # steady state: the pivot tracks the batch mean
+            if path == "bn_stats":
+                y = (60.0 + 3.0 * torch.randn(n, c, hw, hw, device=DEV)).to(torch.bfloat16)
+                y = y.contiguous(memory_format=CL)
+                hip.BNActFn.apply(y, bn.weight, bn.bias, None, bn, None, False, None, None, None, None,
+                                  hip.stat_shift(bn))
+                yref = y
+            else:
+                conv = nn.Conv2d(64, c, 1, bias=False).to(DEV).to(memory_format=CL)
+                with torch.no_grad():
+                    conv.weight.copy_(bf(1.0 / 64 + 0.05 * torch.randn_like(conv.weight)))
+                x = bf(60.0 + 8.0 * torch.randn(n, 64, hw, hw, device=DEV)).to(torch.bfloat16)
+                x = x.contiguous(memory_format=CL)
+                hip.conv_bn_act(x, conv, bn, None, None)
+                yref = conv(x.float()).to(torch.bfloat16)  # the conv output as the HIP path stores it
+            torch.cuda.synchronize()
+            yd = yref.double()
+            mu = yd.mean((0, 2, 3))
+            var = yd.var((0, 2, 3), unbiased=True)
+            assert (mu.abs() / var.sqrt()).median() > 8, "the case must have a large mean / std"
+            e_mu = ((bn.running_mean.double() - mu).abs() / var.sqrt()).max().item()
+            e_var = ((bn.running_var.double() - var).abs() / var).max().item()
+            return e_mu, e_var
+        finally:
+            hip.SHIFT_STATS = keep
+
+    (m1, v1), (m0, v0) = run(True), run(False)
+    print(f"{path}: mean err/std {m1:.2e} (unshifted {m0:.2e}), var rel err {v1:.2e} (unshifted {v0:.2e})")
+    assert m1 < 1e-3 and v1 < 2e-3, (m1, v1)  # bf16 rounding of y differs from the reference's
+    assert v1 <= v0 * 1.5 + 1e-6
