@@ -156,7 +156,8 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
                int IH, int IW, int sA, int ldb, int OH, int OW, int so, int oh0, int ow0, int ldc, int c_off,
                std::vector<int> dh, std::vector<int> dw, std::vector<int> tb, int stats_groups, Tensor zero,
                OT addend, OT bwd_y, OT bwd_res, OT bwd_coef, OT bwd_part, int bwd_act, int bwd_groups,
-               int stages, int tile_n, int cfg, OT a_sc, OT b_sc, OT xa_y, OT xa_coef, OT xa_out, OT stats_shift) {
+               int stages, int tile_n, int cfg, OT a_sc, OT b_sc, OT xa_y, OT xa_coef, OT xa_out, OT stats_shift,
+               OT xf_coef, int xf_act) {
   const bool fp8 = a_sc.has_value() && a_sc->defined();
   TORCH_CHECK(A.scalar_type() == (fp8 ? at::kFloat8_e4m3fn : BF) && B.scalar_type() == A.scalar_type(),
               "conv_gemm: A and B must both be bf16, or both float8_e4m3fn with scales");
@@ -221,12 +222,20 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
                 "conv_gemm: xa_out must match A");
     TORCH_CHECK(cfg < 0 || conv_cfg_has_xa(cfg), "conv_gemm: configuration has no fused BN-backward variant");
   }
+  p.xf_coef = optr<float>(xf_coef);
+  p.xf_act = xf_act;
+  if (p.xf_coef) {
+    TORCH_CHECK(!fp8 && !p.xa_y && xf_coef->numel() >= 2LL * CA && CA % 64 == 0 && !p.bias && (xf_act == 0 || xf_act == 1),
+                "conv_gemm: the fused BN-apply A operand needs bf16, [2][CA] coefficients, CA % 64 == 0, no bias, "
+                "identity or ReLU");
+    TORCH_CHECK(cfg < 0 || conv_cfg_has_xa(cfg), "conv_gemm: configuration has no fused BN-apply variant");
+  }
   check(conv_gemm_launch(p, cur()), "conv_gemm");
 }
 
 void conv_wgrad(Tensor dY, Tensor X, Tensor dW, int M, int Cout, int Cin, int Ntot, int OH, int OW, int IH, int IW,
                 int sh, int sw, int pt, int pl, int dh, int dwd, int KW, int k_per_split, int splits, Tensor zero,
-                int stages, OT ws, int64_t side, OT xa_y, OT xa_coef) {
+                int stages, OT ws, int64_t side, OT xa_y, OT xa_coef, OT xf_coef, int xf_act) {
   req(dY, BF, "dY"); req(X, BF, "X"); req(dW, F32, "dW");
   TORCH_CHECK(Cin % 8 == 0 && Cout % 8 == 0, "conv_wgrad: channels must be multiples of 8");
   TORCH_CHECK(k_per_split % 64 == 0, "conv_wgrad: k_per_split must be a multiple of 64");
@@ -259,6 +268,13 @@ void conv_wgrad(Tensor dY, Tensor X, Tensor dW, int M, int Cout, int Cin, int Nt
                 "conv_wgrad: the fused BN-backward dY needs y matching dY and [3][Cout] coefficients");
     TORCH_CHECK(conv_wgrad_has_xa(stages), "conv_wgrad: this ring / tile variant has no fused BN-backward form");
   }
+  p.xf_coef = optr<float>(xf_coef);
+  p.xf_act = xf_act;
+  if (p.xf_coef) {
+    TORCH_CHECK(xf_coef->numel() >= 2LL * Cin && (xf_act == 0 || xf_act == 1),
+                "conv_wgrad: the fused BN-apply X needs [2][Cin] coefficients and identity / ReLU");
+    TORCH_CHECK(conv_wgrad_has_xf(stages), "conv_wgrad: this ring / tile variant has no fused BN-apply form");
+  }
   if (side == 0) {
     check(conv_wgrad_launch(p, splits, cur()), "conv_wgrad");
     return;
@@ -274,6 +290,7 @@ void conv_wgrad(Tensor dY, Tensor X, Tensor dW, int M, int Cout, int Cin, int Nt
     record_on(*xa_y, s);
     record_on(*xa_coef, s);
   }
+  if (p.xf_coef) record_on(*xf_coef, s);
 }
 
 void bn_partials(Tensor part, int G, int C, Tensor sums, OT dgamma, OT dbeta, double count) {
@@ -830,7 +847,8 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("pl"), pybind11::arg("dh"), pybind11::arg("dwd"), pybind11::arg("KW"),
         pybind11::arg("k_per_split"), pybind11::arg("splits"), pybind11::arg("zero"), pybind11::arg("stages"),
         pybind11::arg("ws") = pybind11::none(), pybind11::arg("side") = 0, pybind11::arg("xa_y") = pybind11::none(),
-        pybind11::arg("xa_coef") = pybind11::none());
+        pybind11::arg("xa_coef") = pybind11::none(), pybind11::arg("xf_coef") = pybind11::none(),
+        pybind11::arg("xf_act") = 0);
   m.def("conv_set_variant", &conv_set_variant);
   m.def("set_deterministic", [](bool v) { set_deterministic(v ? 1 : 0); });
   m.def("set_force_div64", [](bool v) { set_force_div64(v ? 1 : 0); });
@@ -903,6 +921,7 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("conv_cfg_has_xa", &conv_cfg_has_xa);
   m.def("conv_wgrad_has_xa", &conv_wgrad_has_xa);
+  m.def("conv_wgrad_has_xf", &conv_wgrad_has_xf);
   m.def("conv_cfgs", []() {
     std::vector<std::vector<int>> out;
     for (int i = 0; i < conv_num_cfgs(); ++i) {

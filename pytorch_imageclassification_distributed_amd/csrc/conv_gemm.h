@@ -57,6 +57,12 @@ struct ConvParams {
   const bf16_t* xa_y;
   const float* xa_coef;  // [3][CA]
   bf16_t* xa_out;
+  // optional fused BatchNorm-apply on the A operand (forward of a conv whose input is act(bn(y)) and the
+  // BN's only reader; CA % 64 == 0): A holds y (the BN input) and the kernel multiplies with
+  //   a = act(xf_coef[0][c] * y + xf_coef[1][c])     (act: xf_act 0 = identity, 1 = ReLU)
+  // padded taps / rows past M stay 0 (the padding of a, not act(shift)).  xf_coef = the BN's [scale|shift|..].
+  const float* xf_coef;
+  int xf_act;
   int tile_n;  // output-channel tile: 64 or 128; 0 = 64 iff Ncols <= 64 (heuristic / fp8 path)
   int cfg;     // index into the tuned configuration table (conv_cfg_info; MX-FP8: conv_fp8_cfg_info), -1 = stages/tile_n
   int tap_dh[CONV_MAX_TAPS];
@@ -79,6 +85,10 @@ struct WgradParams {
   // uses xa_coef[0][co] * dz + xa_coef[1][co] * y + xa_coef[2][co], y = xa_y at the same index
   const bf16_t* xa_y;
   const float* xa_coef;  // [3][Cout]
+  // optional fused BatchNorm-apply on X (as ConvParams::xf_*): X holds y, the kernel uses
+  // act(xf_coef[0][ci] * y + xf_coef[1][ci]) with the zero padding kept
+  const float* xf_coef;  // [2][Cin] (the BN's scale, shift)
+  int xf_act;
 };
 
 int conv_gemm_launch(const ConvParams& p, hipStream_t stream);
@@ -88,7 +98,8 @@ int conv_num_cfgs();
 int conv_num_fp8_cfgs();
 void conv_fp8_cfg_info(int i, int* out5);
 void conv_cfg_info(int i, int* out5);  // {tile rows, tile channels, waves M, waves N, ring depth}
-bool conv_cfg_has_xa(int i);           // configuration i has a fused BN-backward A-operand variant
+bool conv_cfg_has_xa(int i);           // configuration i has fused BN-backward / BN-apply A-operand variants
 int conv_wgrad_launch(const WgradParams& p, int splits, hipStream_t stream);
 bool conv_wgrad_has_xa(int stages);  // the wgrad variant selected by ``stages`` has a fused BN-backward dY form
+bool conv_wgrad_has_xf(int stages);  // ... a fused BN-apply X form (alone or together with the dY form)
 void conv_set_wgrad_variant(int v);  // 0 = auto, 1 = register-staged, 2 = LDS-DMA

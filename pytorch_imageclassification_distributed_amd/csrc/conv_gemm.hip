@@ -547,12 +547,12 @@ DEVI void glds16(const void* src, char* lds_wave_base) {
 // (1-stage ring: 3-4 blocks/CU hide latency by occupancy; 2-stage: in-block overlap).  256 x {64,128,256}
 // on 8 waves (2 per SIMD, one block per CU) keeps a deeper ring in flight across the barrier (3 stages =
 // 2 tiles ahead at BN <= 128) and halves the LDS-DMA bytes per FLOP of the 128-row tile.
-template <int TM, int BN, int WM, int WN, int STAGES, bool XA = false>
+template <int TM, int BN, int WM, int WN, int STAGES, int XM = 0>
 struct GldsCfg {
   static constexpr int NW = WM * WN, NTH = 64 * NW;
-  // XA: each wave's private copy of the k-step's fused BN-backward coefficients (3 x 64 floats, DMA'd
-  // with the stage so the wave's own vmcnt covers it) rides behind the B tile
-  static constexpr int A_BYTES = TM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES + (XA ? NW * 1024 : 0);
+  // XA / XF (XM 1 / 2): each wave's private copy of the k-step's fused BN coefficients (3 resp. 2 x 64
+  // floats, DMA'd with the stage so the wave's own vmcnt covers it) rides behind the B tile
+  static constexpr int A_BYTES = TM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES + (XM ? NW * 1024 : 0);
   static constexpr int CST = BN + 8;
   static constexpr int EPI = TM * CST * 2;
   // the epilogue tile reuses the ring; a short ring is sized by the epilogue instead
@@ -602,10 +602,16 @@ DEVI int tap_tb(int pk) { return (int)((unsigned)pk >> 16); }
 // padding (or rows past M) keep the zeros the DMA landed - dY of a padded tap is 0, not c2.  Uniform
 // k-steps (CA % 64 == 0); rings of <= 2 stages (every k-step drains vmcnt to 0 before the barrier, so
 // the register load costs no pipelining).
-template <int TM, int BN, int WM, int WN, int STAGES, bool TAP_UNIFORM, int PRIO = 0, bool XA = false>
-__global__ __launch_bounds__((GldsCfg<TM, BN, WM, WN, STAGES, XA>::NTH), (GldsCfg<TM, BN, WM, WN, STAGES, XA>::OCC))
+//
+// XF (XM == 2, fused BatchNorm apply, forward): the A operand is the BN input y of a conv whose input is
+// act(bn(y)) and the BN's only reader; each wave turns its own A pieces into a = act(c0 * y + c1) the same
+// way (no extra operand: c0 / c1 are the BN's scale / shift), so the activated tensor is never written.
+// Pieces in the zero padding stay 0 (the padding of a).
+template <int TM, int BN, int WM, int WN, int STAGES, bool TAP_UNIFORM, int PRIO = 0, int XM = 0>
+__global__ __launch_bounds__((GldsCfg<TM, BN, WM, WN, STAGES, XM>::NTH), (GldsCfg<TM, BN, WM, WN, STAGES, XM>::OCC))
 void conv_gemm_glds_kernel(const ConvParams p) {
-  using Cfg = GldsCfg<TM, BN, WM, WN, STAGES, XA>;
+  using Cfg = GldsCfg<TM, BN, WM, WN, STAGES, XM>;
+  constexpr bool XA = XM == 1, XF = XM == 2;
   constexpr int NW = Cfg::NW;
   constexpr int A_BYTES = Cfg::A_BYTES;
   constexpr int STAGE = Cfg::STAGE;
@@ -617,8 +623,8 @@ void conv_gemm_glds_kernel(const ConvParams p) {
   constexpr int MAIN = Cfg::MAIN;
   static_assert(AL >= 1 && BL >= 1 && AL * 8 * NW == TM && BL * 8 * NW == BN, "loader mapping");
   static_assert(MAIN + CONV_MAX_TAPS * 4 <= 160 * 1024, "LDS budget");
-  static_assert(!XA || (TAP_UNIFORM && STAGES <= 2 && (TM / NW) % 16 == 0 && AL % 2 == 0),
-                "XA: uniform taps, <= 2 stages, even/odd pieces of a wave share a channel chunk");
+  static_assert(!XM || (TAP_UNIFORM && STAGES <= 2 && (TM / NW) % 16 == 0 && AL % 2 == 0),
+                "XA / XF: uniform taps, <= 2 stages, even/odd pieces of a wave share a channel chunk");
   __shared__ __attribute__((aligned(16))) char smem[MAIN + CONV_MAX_TAPS * 4];
   int* s_tap = (int*)(smem + MAIN);
 
@@ -641,11 +647,13 @@ void conv_gemm_glds_kernel(const ConvParams p) {
   // XA: y with the same per-block base and extent as A; per-thread state of the pieces in flight
   __amdgpu_buffer_rsrc_t rsZ, rsK;
   uint4 xa_y[XA ? AL : 1];
-  unsigned xa_va[XA ? AL : 1];
+  unsigned xa_va[XM ? AL : 1];
   int xa_ci = 0;  // first channel of the k-step in flight
   if constexpr (XA) {
     rsZ = make_rsrc(p.xa_y + (long)n_img0 * img, 2 * (p.a_elems - (long)n_img0 * img));
     rsK = make_rsrc(p.xa_coef, 12L * p.CA);
+  } else if constexpr (XF) {
+    rsK = make_rsrc(p.xf_coef, 8L * p.CA);
   }
   int a_pix[AL], a_ih[AL], a_iw[AL];
 #pragma unroll
@@ -741,17 +749,19 @@ void conv_gemm_glds_kernel(const ConvParams p) {
     for (int i = 0; i < AL; ++i) blds16(rsA, va[i], sa + (wid * (TM / NW) + i * 8) * 128);
 #pragma unroll
     for (int i = 0; i < BL; ++i) blds16(rsB, vb[i], sb + (wid * (BN / NW) + i * 8) * 128);
-    if constexpr (XA) {
-      // the k-step's channels [ci, ci + 64): lane l < 48 fetches coefficient array l / 16, floats 4 (l % 16)
-      // .. +4 into this wave's slot (lane-linear); lanes >= 48 land zeros past the used 768 B
+    if constexpr (XM) {
+      // the k-step's channels [ci, ci + 64): lane l < 48 (XF: 32) fetches coefficient array l / 16, floats
+      // 4 (l % 16) .. +4 into this wave's slot (lane-linear); the other lanes land zeros past the used bytes
       const int ci = xa_ci;
-      const unsigned ko = lane < 48 ? 4u * (unsigned)((lane >> 4) * p.CA + ci + (lane & 15) * 4) : OOB;
+      const unsigned ko = lane < (XA ? 48 : 32) ? 4u * (unsigned)((lane >> 4) * p.CA + ci + (lane & 15) * 4) : OOB;
       blds16(rsK, ko, sb + Cfg::B_BYTES + wid * 1024);
 #pragma unroll
       for (int i = 0; i < AL; ++i) {
         xa_va[i] = va[i];
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsZ, va[i], 0, 0);
-        xa_y[i] = *(const uint4*)&v;
+        if constexpr (XA) {
+          const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsZ, va[i], 0, 0);
+          xa_y[i] = *(const uint4*)&v;
+        }
       }
       xa_ci += BK;
       if (xa_ci >= p.CA) xa_ci -= p.CA;
@@ -762,6 +772,36 @@ void conv_gemm_glds_kernel(const ConvParams p) {
   // pieces into dY in place (and, for the first column tile, write dY out when xa_out is set)
   const int xa_ch0 = pch ^ ((lrow >> 1) & 7), xa_ch1 = pch ^ ((4 + (lrow >> 1)) & 7);
   auto xa_transform = [&](int buf, int ci) {
+    if constexpr (XF) {
+      char* sa = smem + buf * STAGE;
+      const float* kc = (const float*)(sa + Cfg::A_BYTES + Cfg::B_BYTES + wid * 1024);
+      const bool relu = p.xf_act == 1;
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        const int ch = (g ? xa_ch1 : xa_ch0) * 8;
+        float c0[8], c1[8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          *(f32x4*)(c0 + 4 * h) = *(const f32x4*)(kc + ch + 4 * h);
+          *(f32x4*)(c1 + 4 * h) = *(const f32x4*)(kc + 64 + ch + 4 * h);
+        }
+#pragma unroll
+        for (int i = g; i < AL; i += 2) {
+          if (xa_va[i] == OOB) continue;  // zero padding / rows past M: a is 0 there
+          uint4* dst = (uint4*)(sa + (wid * (TM / NW) + i * 8) * 128 + lane * 16);
+          float d[8];
+          unpack8(*dst, d);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            d[k] = fmaf(c0[k], d[k], c1[k]);
+            if (relu) d[k] = fmaxf(d[k], 0.f);
+          }
+          *dst = pack8(d);
+        }
+      }
+      (void)ci;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
     if constexpr (XA) {
       char* sa = smem + buf * STAGE;
       const float* kc = (const float*)(sa + Cfg::A_BYTES + Cfg::B_BYTES + wid * 1024);
@@ -821,7 +861,7 @@ void conv_gemm_glds_kernel(const ConvParams p) {
     } else {
       // tile kt landed (the STAGES-2 younger tiles may stay in flight across the barrier); the
       // barrier also retires every wave's reads of the buffer the next issue overwrites
-      if (kt + STAGES - 2 < nk) wait_vmcnt<(STAGES - 2) * (LPS + (XA ? 1 + AL : 0))>();
+      if (kt + STAGES - 2 < nk) wait_vmcnt<(STAGES - 2) * (LPS + (XA ? 1 + AL : XF ? 1 : 0))>();
       else wait_vmcnt<0>();
       xa_transform(kt % STAGES, 0);
       __builtin_amdgcn_s_barrier();
@@ -1246,7 +1286,7 @@ DEVI int wswz(int row) {
 // LDS before the atomics).  Split-K partial tiles leave through fp32 atomics (~1.3 TB/s chip-wide):
 // the atomic bytes of a launch are blocks x tile bytes, so the 256 x 256 tile at one block per CU
 // moves fewer of them than many small-tile blocks while running the more efficient 8-wave loop.
-template <int WBM, int TN, int WM, int WN, int KG, int STAGES, int BKP = WBK, bool XA = false>
+template <int WBM, int TN, int WM, int WN, int KG, int STAGES, int BKP = WBK, bool XA = false, bool XF = false>
 struct WgCfg {
   static constexpr int NW = WM * WN * KG, NTH = 64 * NW;
   static constexpr int AROWB = WBM * 2, BROWB = TN * 2;
@@ -1258,7 +1298,8 @@ struct WgCfg {
   static constexpr int EPI = (KG == 2 ? WBM : WBM / WM) * LDT * 4;  // staged fp32 rows
   static constexpr int MAIN = STAGES * STAGE > EPI ? STAGES * STAGE : EPI;
   static constexpr int XA_BYTES = XA ? 12 * WBM : 0;  // fused BN-backward coefficients [3][WBM] fp32
-  static constexpr int BLOCKS = (160 * 1024) / (MAIN + XA_BYTES);
+  static constexpr int XF_BYTES = XF ? 8 * TN : 0;    // fused BN-apply coefficients [2][TN] fp32 (per column)
+  static constexpr int BLOCKS = (160 * 1024) / (MAIN + XA_BYTES + XF_BYTES);
   static constexpr int OCC0 = BLOCKS * NW / 4 < 1 ? 1 : (BLOCKS * NW / 4 > 3 ? 3 : BLOCKS * NW / 4);
   static constexpr int ACC = (WBM / WM) * (TN / WN) / 64;
   static constexpr int OCC = ACC >= 128 ? (OCC0 < 2 ? OCC0 : 2) : OCC0;
@@ -1270,11 +1311,14 @@ struct WgCfg {
 // applied by each wave to the dz pieces it DMA'd, after its own vmcnt wait and before the barrier that
 // publishes the stage (as conv_gemm_glds_kernel's XA); y comes by a plain buffer load issued with the
 // DMA, the block's [3][WBM] coefficients sit in LDS.  Pixel rows past the split's end stay zero.
-template <int WBM, int TN, int WM, int WN, int KG, int STAGES, int BKP = WBK, bool XA = false>
-__global__ __launch_bounds__((WgCfg<WBM, TN, WM, WN, KG, STAGES, BKP, XA>::NTH),
-                             (WgCfg<WBM, TN, WM, WN, KG, STAGES, BKP, XA>::OCC))
+// XF: X holds the BN input y of a conv whose input is act(bn(y)); each wave turns its own X pieces into
+// act(c0 * y + c1) (per input channel, [2][TN] per-column table in LDS) the same way.  Pieces that fell
+// into the zero padding stay 0: their validity rides in a per-lane shift register, BL bits per stage.
+template <int WBM, int TN, int WM, int WN, int KG, int STAGES, int BKP = WBK, bool XA = false, bool XF = false>
+__global__ __launch_bounds__((WgCfg<WBM, TN, WM, WN, KG, STAGES, BKP, XA, XF>::NTH),
+                             (WgCfg<WBM, TN, WM, WN, KG, STAGES, BKP, XA, XF>::OCC))
 void conv_wgrad_glds_kernel(const WgradParams p) {
-  using Cfg = WgCfg<WBM, TN, WM, WN, KG, STAGES, BKP, XA>;
+  using Cfg = WgCfg<WBM, TN, WM, WN, KG, STAGES, BKP, XA, XF>;
   constexpr int NW = Cfg::NW;
   constexpr int NTH = Cfg::NTH;
   constexpr int AROWB = Cfg::AROWB;         // A image row bytes (128 / 256 / 512)
@@ -1292,10 +1336,11 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
   constexpr int LDT = Cfg::LDT;             // floats per staged epilogue row
   constexpr int MAIN = Cfg::MAIN;
   static_assert(AL >= 1 && BL >= 1 && AL * ARPI * NW == KPS && BL * BRPI * NW == KPS, "loader mapping");
-  static_assert(MAIN + Cfg::XA_BYTES <= 160 * 1024, "LDS budget");
+  static_assert(MAIN + Cfg::XA_BYTES + Cfg::XF_BYTES <= 160 * 1024, "LDS budget");
+  static_assert(!XF || BL * STAGES <= 64, "XF: validity bits of the stages in flight fit 64 bits");
   constexpr bool YLDS = Cfg::YLDS;
   constexpr int LPS = AL + BL + (YLDS ? AL : 0);  // LDS-DMA instructions per wave per stage
-  __shared__ __attribute__((aligned(16))) char smem[MAIN + Cfg::XA_BYTES];
+  __shared__ __attribute__((aligned(16))) char smem[MAIN + Cfg::XA_BYTES + Cfg::XF_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1327,13 +1372,14 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
   }
   // B (X gather): per instruction the logical column -> (tap, ci) is fixed over k-steps
   const int b_lr = lane / (BROWB / 16), b_pc = lane % (BROWB / 16);
-  int b_ci[BL], b_dh[BL], b_dw[BL];
+  int b_ci[BL], b_dh[BL], b_dw[BL], b_jl[BL];
   bool b_cok[BL];
 #pragma unroll
   for (int i = 0; i < BL; ++i) {
     const int row = (wid * BL + i) * BRPI + b_lr;
     const int lchunk = (((b_pc >> 1) ^ wswz<BROWB>(row)) << 1) | (b_pc & 1);
     const int j = j0 + lchunk * 8;
+    b_jl[i] = lchunk * 8;
     b_cok[i] = j < p.Ntot;
     const int tap = b_cok[i] ? j / p.Cin : 0;
     b_ci[i] = j - tap * p.Cin;
@@ -1370,6 +1416,17 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
     }
     __syncthreads();
   }
+  // XF: per-column (tap, ci) scale / shift table; validity of this lane's X pieces per stage in flight
+  float* const s_xf = (float*)(smem + MAIN + Cfg::XA_BYTES);
+  unsigned long long xf_bits = 0;
+  int xf_issued = -1;  // index of the last stage issued
+  if constexpr (XF) {
+    for (int t = tid; t < 2 * TN; t += NTH) {
+      const int arr = t / TN, j = j0 + (t - arr * TN);
+      s_xf[t] = j < p.Ntot ? p.xf_coef[arr * p.Cin + (j % p.Cin)] : 0.f;
+    }
+    __syncthreads();
+  }
   int b_m[BL], b_n[BL], b_oh[BL], b_ow[BL];
 #pragma unroll
   for (int i = 0; i < BL; ++i) {
@@ -1393,6 +1450,7 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
       const int ih = b_oh[i] * p.stride_h + b_dh[i], iw = b_ow[i] * p.stride_w + b_dw[i];
       const bool ok = b_cok[i] && b_m[i] < kend && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW;
       vb[i] = ok ? 2u * (unsigned)(((b_n[i] * p.IH + ih) * p.IW + iw) * p.Cin + b_ci[i]) : OOB;
+      if constexpr (XF) xf_bits = (xf_bits << 1) | (ok ? 1ull : 0ull);
       // advance by KPS pixels: adv_q output rows + adv_r columns, carrying into rows and images (the
       // image carry by one float-reciprocal division, not a data-dependent loop)
       b_m[i] += KPS;
@@ -1405,6 +1463,7 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
         b_oh[i] = r;
       }
     }
+    if constexpr (XF) ++xf_issued;
 #pragma unroll
     for (int i = 0; i < AL; ++i) blds16(rsY, va[i], sa + (wid * AL + i) * 1024);
 #pragma unroll
@@ -1421,7 +1480,34 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
     }
   };
   // XA: this wave's dz pieces of stage kt (waited for) -> dY in place; rows past kend stay zero
+  // XF: this wave's y pieces of stage kt -> act(c0 * y + c1) in place; padded / out-of-range pieces stay 0
   auto xa_transform = [&](int buf, int kt) {
+    if constexpr (XF) {
+      char* sb = smem + buf * STAGE + A_BYTES;
+      // stage kt's bits: issue i of a stage shifted its bit in as bit 0, BL per stage, newest stage lowest
+      const int sh = (xf_issued - kt) * BL;
+      const bool relu = p.xf_act == 1;
+#pragma unroll
+      for (int i = 0; i < BL; ++i) {
+        if (!((xf_bits >> (sh + BL - 1 - i)) & 1ull)) continue;
+        const int j = b_jl[i];
+        float c0[8], c1[8];
+        *(f32x4*)c0 = *(const f32x4*)(s_xf + j);
+        *(f32x4*)(c0 + 4) = *(const f32x4*)(s_xf + j + 4);
+        *(f32x4*)c1 = *(const f32x4*)(s_xf + TN + j);
+        *(f32x4*)(c1 + 4) = *(const f32x4*)(s_xf + TN + j + 4);
+        uint4* dst = (uint4*)(sb + (wid * BL + i) * 1024 + lane * 16);
+        float d[8];
+        unpack8(*dst, d);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          d[k] = fmaf(c0[k], d[k], c1[k]);
+          if (relu) d[k] = fmaxf(d[k], 0.f);
+        }
+        *dst = pack8(d);
+      }
+      if constexpr (!XA) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
     if constexpr (XA) {
       char* sa = smem + buf * STAGE;
 #pragma unroll
@@ -1641,16 +1727,24 @@ static void launch_glds(const ConvParams& p, hipStream_t stream) {
   const int grid = cdiv(p.M, TM) * cdiv(p.Ncols, BN);
   constexpr int NTH = 64 * WM * WN;
   if ((p.CA % BK) == 0)
-    hipLaunchKernelGGL((conv_gemm_glds_kernel<TM, BN, WM, WN, STAGES, true, PRIO>), dim3(grid), dim3(NTH), 0, stream, p);
+    hipLaunchKernelGGL((conv_gemm_glds_kernel<TM, BN, WM, WN, STAGES, true, PRIO, 0>), dim3(grid), dim3(NTH), 0, stream, p);
   else
-    hipLaunchKernelGGL((conv_gemm_glds_kernel<TM, BN, WM, WN, STAGES, false, PRIO>), dim3(grid), dim3(NTH), 0, stream, p);
+    hipLaunchKernelGGL((conv_gemm_glds_kernel<TM, BN, WM, WN, STAGES, false, PRIO, 0>), dim3(grid), dim3(NTH), 0, stream, p);
 }
 
 // fused BN-backward A-operand variant (XA, host-checked: 1x1 stride-1 geometry, CA % 64 == 0)
 template <int TM, int BN, int WM, int WN, int STAGES, int PRIO = 0>
 static void launch_glds_xa(const ConvParams& p, hipStream_t stream) {
   const int grid = cdiv(p.M, TM) * cdiv(p.Ncols, BN);
-  hipLaunchKernelGGL((conv_gemm_glds_kernel<TM, BN, WM, WN, STAGES, true, PRIO, true>), dim3(grid),
+  hipLaunchKernelGGL((conv_gemm_glds_kernel<TM, BN, WM, WN, STAGES, true, PRIO, 1>), dim3(grid),
+                     dim3(64 * WM * WN), 0, stream, p);
+}
+
+// fused BN-apply A-operand variant (XF, host-checked: CA % 64 == 0, no bias)
+template <int TM, int BN, int WM, int WN, int STAGES, int PRIO = 0>
+static void launch_glds_xf(const ConvParams& p, hipStream_t stream) {
+  const int grid = cdiv(p.M, TM) * cdiv(p.Ncols, BN);
+  hipLaunchKernelGGL((conv_gemm_glds_kernel<TM, BN, WM, WN, STAGES, true, PRIO, 2>), dim3(grid),
                      dim3(64 * WM * WN), 0, stream, p);
 }
 
@@ -1674,10 +1768,15 @@ struct ConvCfg {
   int tm, bn, wm, wn, st;
   void (*launch)(const ConvParams&, hipStream_t);
   void (*launch_xa)(const ConvParams&, hipStream_t);  // fused BN-backward A operand, or null
+  void (*launch_xf)(const ConvParams&, hipStream_t);  // fused BN-apply A operand, or null
 };
-#define CFG(TM, BN, WM, WN, ST) {TM, BN, WM, WN, ST, &launch_glds<TM, BN, WM, WN, ST>, &launch_glds_xa<TM, BN, WM, WN, ST>}
-#define CFGP(TM, BN, WM, WN, ST) {TM, BN, WM, WN, ST, &launch_glds<TM, BN, WM, WN, ST, 1>, &launch_glds_xa<TM, BN, WM, WN, ST, 1>}
-#define CFGN(TM, BN, WM, WN, ST) {TM, BN, WM, WN, ST, &launch_glds<TM, BN, WM, WN, ST>, nullptr}
+#define CFG(TM, BN, WM, WN, ST)                                                                           \
+  {TM, BN, WM, WN, ST, &launch_glds<TM, BN, WM, WN, ST>, &launch_glds_xa<TM, BN, WM, WN, ST>,            \
+   &launch_glds_xf<TM, BN, WM, WN, ST>}
+#define CFGP(TM, BN, WM, WN, ST)                                                                          \
+  {TM, BN, WM, WN, ST, &launch_glds<TM, BN, WM, WN, ST, 1>, &launch_glds_xa<TM, BN, WM, WN, ST, 1>,      \
+   &launch_glds_xf<TM, BN, WM, WN, ST, 1>}
+#define CFGN(TM, BN, WM, WN, ST) {TM, BN, WM, WN, ST, &launch_glds<TM, BN, WM, WN, ST>, nullptr, nullptr}
 // Measured on the ResNet-50 layers at batch 512 (benchmarks/conv_bench.py --tune-log): the 128-row
 // 4-wave tiles win on 64/128-channel outputs and short K (occupancy hides latency); the 256x256
 // 8-wave tiles (2 waves per SIMD, 64x128 or 128x64 per wave, half the LDS-DMA bytes per FLOP) win
@@ -1711,7 +1810,7 @@ static void launch_fp8_cfg(const ConvParams& p, hipStream_t stream) {
 }
 
 // MX-FP8 configurations (same role as g_cfgs for bf16)
-#define FCFG(TM, BN, WM, WN, ST) {TM, BN, WM, WN, ST, &launch_fp8_cfg<TM, BN, WM, WN, ST>, nullptr}
+#define FCFG(TM, BN, WM, WN, ST) {TM, BN, WM, WN, ST, &launch_fp8_cfg<TM, BN, WM, WN, ST>, nullptr, nullptr}
 static const ConvCfg g_fp8_cfgs[] = {
     FCFG(128, 64, 2, 2, 1), FCFG(128, 128, 2, 2, 1), FCFG(128, 64, 2, 2, 2), FCFG(128, 128, 2, 2, 2),
     FCFG(256, 256, 2, 4, 2),  // (4 x 2 waves of 64 x 128 spills at 2 waves per SIMD with 8-VGPR fp8 fragments)
@@ -1754,6 +1853,15 @@ int conv_gemm_launch(const ConvParams& p, hipStream_t stream) {
     HIP_CHECK_LAUNCH();
     return 0;
   }
+  if (p.xf_coef) {
+    // fused BN-apply A operand: uniform k-steps (padded taps / rows stay zero)
+    if (p.CA % BK || p.bias) return 4;
+    const int cfg = p.cfg >= 0 ? p.cfg : (p.Ncols <= 64 || p.tile_n == 64 ? 0 : 1);
+    if (cfg >= kNumCfgs || !g_cfgs[cfg].launch_xf) return 4;
+    g_cfgs[cfg].launch_xf(p, stream);
+    HIP_CHECK_LAUNCH();
+    return 0;
+  }
   if (p.cfg >= 0) {
     if (p.cfg >= kNumCfgs) return 3;
     g_cfgs[p.cfg].launch(p, stream);
@@ -1766,30 +1874,41 @@ int conv_gemm_launch(const ConvParams& p, hipStream_t stream) {
 static int g_wvariant = 0;
 void conv_set_wgrad_variant(int v) { g_wvariant = v; }
 
-template <int WBM, int TN, int WM, int WN, int KG, int ST, int BKP = WBK>
-static void launch_wg(const WgradParams& p, int splits, hipStream_t stream) {
-  const dim3 grid(cdiv(p.Cout, WBM) * cdiv(p.Ntot, TN), splits);
-  using XCfg = WgCfg<WBM, TN, WM, WN, KG, ST, BKP, true>;
-  if constexpr (XCfg::MAIN + XCfg::XA_BYTES <= 160 * 1024 && !(ST == 2 && WBM == 256)) {
-    if (p.xa_y) {
-      hipLaunchKernelGGL((conv_wgrad_glds_kernel<WBM, TN, WM, WN, KG, ST, BKP, true>), grid,
-                         dim3(64 * WM * WN * KG), 0, stream, p);
-      return;
-    }
+template <int WBM, int TN, int WM, int WN, int KG, int ST, int BKP, bool XA, bool XF>
+static bool launch_wg_x(const WgradParams& p, const dim3& grid, hipStream_t stream) {
+  using XCfg = WgCfg<WBM, TN, WM, WN, KG, ST, BKP, XA, XF>;
+  if constexpr (XCfg::MAIN + XCfg::XA_BYTES + XCfg::XF_BYTES <= 160 * 1024 && !(XA && ST == 2 && WBM == 256)) {
+    hipLaunchKernelGGL((conv_wgrad_glds_kernel<WBM, TN, WM, WN, KG, ST, BKP, XA, XF>), grid,
+                       dim3(64 * WM * WN * KG), 0, stream, p);
+    return true;
   }
-  hipLaunchKernelGGL((conv_wgrad_glds_kernel<WBM, TN, WM, WN, KG, ST, BKP>), grid, dim3(64 * WM * WN * KG), 0,
-                     stream, p);
+  return false;
+}
+
+// false: no fused form of the requested kind for this tile / ring (the caller reports it)
+template <int WBM, int TN, int WM, int WN, int KG, int ST, int BKP = WBK>
+static bool launch_wg(const WgradParams& p, int splits, hipStream_t stream) {
+  const dim3 grid(cdiv(p.Cout, WBM) * cdiv(p.Ntot, TN), splits);
+  const bool xa = p.xa_y != nullptr, xf = p.xf_coef != nullptr;
+  if (xa && xf) return launch_wg_x<WBM, TN, WM, WN, KG, ST, BKP, true, true>(p, grid, stream);
+  if (xa) return launch_wg_x<WBM, TN, WM, WN, KG, ST, BKP, true, false>(p, grid, stream);
+  if (xf) return launch_wg_x<WBM, TN, WM, WN, KG, ST, BKP, false, true>(p, grid, stream);
+  return launch_wg_x<WBM, TN, WM, WN, KG, ST, BKP, false, false>(p, grid, stream);
 }
 
 // variants with a fused BN-backward form: all but the 256 x 256 tile with a 2-deep 64-pixel ring (its
 // register y pieces spill at 2 waves per SIMD; LDS y would not fit) and the 4-deep 256 x 256 ring (LDS)
 bool conv_wgrad_has_xa(int stages) { return stages >= 1 && stages <= 9 && stages != 4 && stages != 7; }
+// the fused BN-apply X form needs no register operand: every LDS-DMA variant has it
+bool conv_wgrad_has_xf(int stages) { return stages >= 1 && stages <= 9; }
 
 int conv_wgrad_tile_n(int stages) { return (stages == 4 || stages == 7 || stages == 9) ? 256 : WBN; }
 
 int conv_wgrad_launch(const WgradParams& p_in, int splits, hipStream_t stream) {
   if (p_in.M <= 0) return 0;
   if (p_in.xa_y && (g_wvariant == 1 || !conv_wgrad_has_xa(p_in.stages))) return 4;
+  if (p_in.xf_coef && (g_wvariant == 1 || !conv_wgrad_has_xf(p_in.stages))) return 4;
+  bool ok = true;
   const bool dma = g_wvariant != 1;
   WgradParams p = p_in;
   if (!dma || splits <= 1) p.ws = nullptr;  // the register-staged kernel always adds atomically
@@ -1798,31 +1917,32 @@ int conv_wgrad_launch(const WgradParams& p_in, int splits, hipStream_t stream) {
   // 5 / 6 = 32 x 128 tile with a 1 / 2-stage ring (Cout <= 32 only)
   if (dma && (p.stages == 7 || p.stages == 9)) {  // 256 x 256, 8 waves, 4- / 3-deep ring of 32-pixel stages
     if (p.Cout < 256) return 2;
-    if (p.stages == 7) launch_wg<256, 256, 2, 4, 1, 4, 32>(p, splits, stream);
-    else launch_wg<256, 256, 2, 4, 1, 3, 32>(p, splits, stream);
+    if (p.stages == 7) ok = launch_wg<256, 256, 2, 4, 1, 4, 32>(p, splits, stream);
+    else ok = launch_wg<256, 256, 2, 4, 1, 3, 32>(p, splits, stream);
   } else if (dma && p.stages == 8) {  // 64 / 128 x 128, 4 waves, 4-deep ring of 32-pixel stages
-    if (p.Cout <= 64) launch_wg<64, 128, 2, 2, 1, 4, 32>(p, splits, stream);
-    else launch_wg<128, 128, 2, 2, 1, 4, 32>(p, splits, stream);
+    if (p.Cout <= 64) ok = launch_wg<64, 128, 2, 2, 1, 4, 32>(p, splits, stream);
+    else ok = launch_wg<128, 128, 2, 2, 1, 4, 32>(p, splits, stream);
   } else if (dma && p.stages == 4) {
     if (p.Cout < 256) return 2;
-    launch_wg<256, 256, 2, 4, 1, 2>(p, splits, stream);
+    ok = launch_wg<256, 256, 2, 4, 1, 2>(p, splits, stream);
   } else if (dma && (p.stages == 5 || p.stages == 6)) {  // 32-row tile (Cout <= 32: no empty half tile)
     if (p.Cout > 32) return 2;
-    if (p.stages == 5) launch_wg<32, 128, 2, 2, 1, 1>(p, splits, stream);
-    else launch_wg<32, 128, 2, 2, 1, 2>(p, splits, stream);
+    if (p.stages == 5) ok = launch_wg<32, 128, 2, 2, 1, 1>(p, splits, stream);
+    else ok = launch_wg<32, 128, 2, 2, 1, 2>(p, splits, stream);
   } else if (p.Cout <= 64) {
-    if (dma && p.stages == 1) launch_wg<64, 128, 2, 2, 1, 1>(p, splits, stream);
-    else if (dma && p.stages == 3) launch_wg<64, 128, 2, 2, 2, 2>(p, splits, stream);
-    else if (dma) launch_wg<64, 128, 2, 2, 1, 2>(p, splits, stream);
+    if (dma && p.stages == 1) ok = launch_wg<64, 128, 2, 2, 1, 1>(p, splits, stream);
+    else if (dma && p.stages == 3) ok = launch_wg<64, 128, 2, 2, 2, 2>(p, splits, stream);
+    else if (dma) ok = launch_wg<64, 128, 2, 2, 1, 2>(p, splits, stream);
     else hipLaunchKernelGGL(conv_wgrad_kernel<64>, dim3(cdiv(p.Cout, 64) * cdiv(p.Ntot, WBN), splits), dim3(NT), 0,
                             stream, p);
   } else {
-    if (dma && p.stages == 1) launch_wg<128, 128, 2, 2, 1, 1>(p, splits, stream);
-    else if (dma && p.stages == 3) launch_wg<128, 128, 2, 2, 2, 2>(p, splits, stream);
-    else if (dma) launch_wg<128, 128, 2, 2, 1, 2>(p, splits, stream);
+    if (dma && p.stages == 1) ok = launch_wg<128, 128, 2, 2, 1, 1>(p, splits, stream);
+    else if (dma && p.stages == 3) ok = launch_wg<128, 128, 2, 2, 2, 2>(p, splits, stream);
+    else if (dma) ok = launch_wg<128, 128, 2, 2, 1, 2>(p, splits, stream);
     else hipLaunchKernelGGL(conv_wgrad_kernel<128>, dim3(cdiv(p.Cout, 128) * cdiv(p.Ntot, WBN), splits), dim3(NT),
                             0, stream, p);
   }
+  if (!ok) return 4;
   HIP_CHECK_LAUNCH();
   if (p.ws != nullptr) {
     const long n4 = (long)p.Cout * p.Ntot / 4;

@@ -43,7 +43,7 @@ class BasicBlock(nn.Module):
             identity = Fx.conv_bn_act(x, self.downsample[0], self.downsample[1], None, x_slot=slot)
         else:
             identity = x
-        out = Fx.conv_bn_act(x, self.conv1, self.bn1, "relu", x_slot=slot)
+        out = Fx.conv_bn_act(x, self.conv1, self.bn1, "relu", x_slot=slot, defer_act=True)
         return Fx.conv_bn_act(out, self.conv2, self.bn2, "relu", residual=identity,
                               res_slot=None if self.downsample is not None else slot, exclusive_input=True)
 
@@ -70,8 +70,9 @@ class Bottleneck(nn.Module):
             identity = Fx.conv_bn_act(x, self.downsample[0], self.downsample[1], None, x_slot=slot)
         else:
             identity = x
-        out = Fx.conv_bn_act(x, self.conv1, self.bn1, "relu", x_slot=slot)
-        out = Fx.conv_bn_act(out, self.conv2, self.bn2, "relu", exclusive_input=True)
+        # bn1 / bn2 outputs feed only the next conv: the HIP path fuses their apply into that conv's loads
+        out = Fx.conv_bn_act(x, self.conv1, self.bn1, "relu", x_slot=slot, defer_act=True)
+        out = Fx.conv_bn_act(out, self.conv2, self.bn2, "relu", exclusive_input=True, defer_act=True)
         return Fx.conv_bn_act(out, self.conv3, self.bn3, "relu", residual=identity,
                               res_slot=None if self.downsample is not None else slot, exclusive_input=True)
 

@@ -112,7 +112,7 @@ def grad_slot(x, n: int = 2):
 
 
 def conv_bn_act(x, conv, bn, act="relu", residual=None, x_slot=None, res_slot=None, exclusive_input=False,
-                out=None, pool=None, prepool=None):
+                out=None, pool=None, prepool=None, defer_act=False):
     """act(bn(conv(x)) [+ residual]).
 
     Reference equivalents: torchvision ``BasicConv2d`` (conv -> BN -> ReLU),
@@ -123,6 +123,8 @@ def conv_bn_act(x, conv, bn, act="relu", residual=None, x_slot=None, res_slot=No
     ``prepool`` = (kernel, stride, padding): an average pool (count_include_pad) precedes the conv (the
     Inception ``branch_pool``); for a 1x1 conv the HIP path runs the conv first and pools its narrower
     output - both are linear, so conv1x1(avgpool(x)) == avgpool(conv1x1(x)).
+    ``defer_act``: the caller feeds the result only to the next ``conv_bn_act`` (as its exclusive input);
+    the HIP path may then skip writing act(bn(y)) and let that conv apply the BN on its operand loads.
     """
     if prepool is not None:
         if residual is not None or pool is not None:
@@ -140,7 +142,8 @@ def conv_bn_act(x, conv, bn, act="relu", residual=None, x_slot=None, res_slot=No
         return F.max_pool2d(_act(_torch_bn(_torch_conv(x, conv), bn), act), *pool)
     if use_hip(x):
         hout = (out[0].hip(), out[1]) if (out is not None and _hip().CONCAT_INPLACE) else None
-        return _hip().conv_bn_act(x, conv, bn, act, residual, x_slot, res_slot, exclusive_input, hout)
+        return _hip().conv_bn_act(x, conv, bn, act, residual, x_slot, res_slot, exclusive_input, hout,
+                                  defer_act=defer_act)
     y = _torch_bn(_torch_conv(x, conv), bn)
     if residual is not None:
         y = y + residual

@@ -467,18 +467,22 @@ TUNE_LOG: list = []  # (M, Ncols, K, {cfg: ms}) per tuned geometry (benchmarks/c
 
 
 def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(None, None, None, None, 0, 1),
-               groups=G_STATS, scales=(None, None), xa=None, shift=None):
+               groups=G_STATS, scales=(None, None), xa=None, shift=None, xf=None):
     """One implicit-GEMM launch.  The kernel configuration - LDS-DMA ring depth (1 = high occupancy,
     2 / 3 = pipelined) x output-channel tile (64 / 128 / 256: more tiles balance 256 CUs better on
     small layers) x pixel tile (128 rows on 4 waves, or 256 rows on 8 waves) - is chosen once per
     GEMM geometry by timing the candidates on scratch outputs (a conv-algorithm "find" step).
     ``xa`` = (y, coef [3][CA]): A holds a BN's pre-elementwise gradient dz and the kernel applies the
-    BN backward's elementwise map on its operand loads (1x1 stride-1 geometry; ``XaLink``)."""
+    BN backward's elementwise map on its operand loads (1x1 stride-1 geometry; ``XaLink``).
+    ``xf`` = (coef, act): A holds a BN's input y and the kernel applies act(bn(y)) on its operand loads
+    (``XfHold``)."""
     xa3 = (xa[0], xa[1], None) if xa is not None else (None, None, None)
-    if DIRECT_FORCE is not None and xa is None and \
+    xf2 = (xf[0], xf[1]) if xf is not None else (None, 0)
+    fused = xa is not None or xf is not None
+    if DIRECT_FORCE is not None and not fused and \
             _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales) is not None:
         cfg = (0, 0, DIRECT_BASE + DIRECT_FORCE)  # (tests) every eligible launch on this direct variant
-    elif CONV_FORCE_CFG is not None and scales[0] is None and (xa is None or C.conv_cfg_has_xa(CONV_FORCE_CFG[2])):
+    elif CONV_FORCE_CFG is not None and scales[0] is None and (not fused or C.conv_cfg_has_xa(CONV_FORCE_CFG[2])):
         cfg = CONV_FORCE_CFG
     elif CONV_FORCE_FP8_CFG is not None and scales[0] is not None:
         cfg = CONV_FORCE_FP8_CFG
@@ -487,18 +491,19 @@ def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(
     else:
         key = (tuple(geo), out.shape[1], tuple(dh), tuple(dw), stats is not None, bias is not None,
                addend is not None, bwd[0] is not None, bwd[1] is not None, bwd[4], scales[0] is not None,
-               DIRECT_CONV) + ((True,) if xa is not None else ())
+               DIRECT_CONV) + ((True,) if xa is not None else ()) + (("xf",) if xf is not None else ())
         cfg = _STAGES_TUNED.get(key)
         if cfg is None:
             cfg = (0, 0, -1) if torch.cuda.is_current_stream_capturing() else _tune_conv(
-                A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups, scales, xa)
+                A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups, scales, xa, xf)
             if cfg[0] or cfg[2] >= 0:
                 _STAGES_TUNED[key] = cfg
     if cfg[2] >= DIRECT_BASE:
         _direct_launch(A, B, out, stats, groups, _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales),
                        cfg[2] - DIRECT_BASE, bwd, shift)
         return
-    C.conv_gemm(A, B, out, stats, bias, *geo, dh, dw, tb, groups, zero, addend, *bwd, *cfg, *scales, *xa3, shift)
+    C.conv_gemm(A, B, out, stats, bias, *geo, dh, dw, tb, groups, zero, addend, *bwd, *cfg, *scales, *xa3, shift,
+                *xf2)
 
 
 _CFGS = None
@@ -524,8 +529,8 @@ def conv_fp8_cfgs():
 
 
 def _conv_candidates(m, ncols, fp8, xa=False):
-    """(stages, tile_n, cfg) triples worth timing for an M x Ncols GEMM (``xa``: configurations with a
-    fused BN-backward A-operand variant only)."""
+    """(stages, tile_n, cfg) triples worth timing for an M x Ncols GEMM (``xa``: configurations with
+    fused BN-backward / BN-apply A-operand variants only)."""
     out = []
     for i, (tm, bn, _wm, _wn, _st) in enumerate(conv_fp8_cfgs() if fp8 else conv_cfgs()):
         if xa and not C.conv_cfg_has_xa(i):
@@ -597,19 +602,22 @@ def _direct_launch(A, B, out, stats, groups, dg, variant, bwd, shift=None):
         C.direct_conv(A, w, out, stats, groups, n, ih, iw, cx, gh, gw, co, pt, pl, variant, shift=shift)
 
 
-def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups, scales=(None, None), xa=None):
+def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups, scales=(None, None), xa=None,
+               xf=None):
     scratch = torch.empty_like(out)
     sst = torch.zeros_like(stats) if stats is not None else None
     bwd = tuple(bwd)
     if bwd[3] is not None:
         bwd = bwd[:3] + (torch.zeros_like(bwd[3]),) + bwd[4:]
-    cands = _conv_candidates(geo[0], geo[1], scales[0] is not None, xa is not None)
+    fused = xa is not None or xf is not None
+    cands = _conv_candidates(geo[0], geo[1], scales[0] is not None, fused)
     xa3 = (xa[0], xa[1], None) if xa is not None else (None, None, None)
+    xf2 = (xf[0], xf[1]) if xf is not None else (None, 0)
     times = {}
     for cfg in cands:
         times[cfg] = _time_ms(lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, groups, zero,
-                                                  addend, *bwd, *cfg, *scales, *xa3, None))
-    dg = _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales) if xa is None else None
+                                                  addend, *bwd, *cfg, *scales, *xa3, None, *xf2))
+    dg = _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales) if not fused else None
     if dg is not None:
         for v, (cip, cot) in DIRECT_CFGS.items():
             if dg[3] <= cip and (cot == 32 or dg[6] > 32):
@@ -623,9 +631,11 @@ def fp8_eligible(g: "ConvGeom") -> bool:
     return FP8_FWD and g.Cx == g.Ci and g.Cx % 128 == 0 and g.Co % 8 == 0
 
 
-def conv_forward_raw(x, w_param, g: ConvGeom, stats=None, bias=None, out=None, c_off=0, wb=None, shift=None):
+def conv_forward_raw(x, w_param, g: ConvGeom, stats=None, bias=None, out=None, c_off=0, wb=None, shift=None,
+                     xf=None):
+    """``xf`` = (coef, act): x holds a BN's input y; the conv reads act(bn(y)) (``XfHold``)."""
     dev = x.device
-    if wb is None and fp8_eligible(g):
+    if wb is None and xf is None and fp8_eligible(g):
         return _conv_forward_fp8(x, w_param, g, stats, bias, out, c_off, shift)
     if wb is None:
         wb = _weight_for_input(w_param, g.Cx)
@@ -636,7 +646,8 @@ def conv_forward_raw(x, w_param, g: ConvGeom, stats=None, bias=None, out=None, c
         raise NotImplementedError("anisotropic stride")
     geo = (g.N * g.OH * g.OW, g.Co, g.T * g.Cx, g.Cx, g.OH, g.OW, g.H, g.W, g.sh, g.T * g.Cx, g.OH, g.OW,
            1, 0, 0, ldc, c_off)
-    _conv_gemm(x, wb, y, stats, bias, geo, dh, dw, tb, ws(dev).zero, groups=stat_groups(geo[0]), shift=shift)
+    _conv_gemm(x, wb, y, stats, bias, geo, dh, dw, tb, ws(dev).zero, groups=stat_groups(geo[0]), shift=shift,
+               xf=xf)
     return y
 
 
@@ -710,10 +721,11 @@ def _wgrad_ws(dev, n):
     return buf
 
 
-def _wgrad_launch(dy, x, out, g: ConvGeom, m, ntot, kps, splits, stages=2, side=None, xa=None):
+def _wgrad_launch(dy, x, out, g: ConvGeom, m, ntot, kps, splits, stages=2, side=None, xa=None, xf=None):
     """One weight-gradient launch on the current stream, or (``side``: a ``_SideStream``) forked onto the
     side stream inside the launcher (event record / wait and allocator stream records in C++).  ``xa`` =
-    (y, coef): dy is a BN's pre-elementwise gradient, the kernel applies the elementwise map itself."""
+    (y, coef): dy is a BN's pre-elementwise gradient, the kernel applies the elementwise map itself.
+    ``xf`` = (coef, act): x is a BN's input y, the kernel reads act(bn(y))."""
     wsp = None
     if WGRAD_WS and splits > 1 and ntot % 8 == 0:
         n = splits * g.Co * ntot
@@ -725,7 +737,8 @@ def _wgrad_launch(dy, x, out, g: ConvGeom, m, ntot, kps, splits, stages=2, side=
             wsp = side.ws
     C.conv_wgrad(dy, x, out, m, g.Co, g.Cx, ntot, g.OH, g.OW, g.H, g.W, g.sh, g.sw, g.pt, g.pl,
                  g.dil, g.dil, g.kw, kps, splits, ws(dy.device).zero, stages, wsp, side.handle if side else 0,
-                 xa_y=xa[0] if xa is not None else None, xa_coef=xa[1] if xa is not None else None)
+                 xa_y=xa[0] if xa is not None else None, xa_coef=xa[1] if xa is not None else None,
+                 xf_coef=xf[0] if xf is not None else None, xf_act=xf[1] if xf is not None else 0)
 
 
 def _wgrad_tiles(co, ntot, stages):
@@ -736,28 +749,33 @@ def _wgrad_tiles(co, ntot, stages):
     return (-(-co // (32 if stages in (5, 6) else 64 if co <= 64 else 128))) * (-(-ntot // 128))
 
 
-def _wgrad_plan(g: ConvGeom, dy, x, m, ntot, xa=None):
+def _wgrad_plan(g: ConvGeom, dy, x, m, ntot, xa=None, xf=None):
     """(k_per_split, splits, stages) of the weight-gradient launch for this geometry."""
-    target, stages = _wgrad_config(dy, x, g, m, ntot, xa)
+    target, stages = _wgrad_config(dy, x, g, m, ntot, xa, xf)
     kps, splits = _wgrad_split(m, _wgrad_tiles(g.Co, ntot, stages), target)
     return kps, splits, stages
 
 
-def _wgrad_config(dy, x, g: ConvGeom, m, ntot, xa=None):
+def _wgrad_has(st, fx, ff):
+    return (not fx or C.conv_wgrad_has_xa(st)) and (not ff or C.conv_wgrad_has_xf(st))
+
+
+def _wgrad_config(dy, x, g: ConvGeom, m, ntot, xa=None, xf=None):
     """(split-K block target, LDS ring depth): fixed by IMGCLS_WGRAD_BLOCKS / IMGCLS_WGRAD_STAGES,
     else timed jointly once per shape (cached).  With ``xa`` (fused BN-backward dY) only the variants
     that have the fused form are candidates, and they are timed with it.
 
     Tuning runs on a scratch gradient buffer, outside any graph capture, the first time a shape
     is seen (warmup), like a conv-algorithm "find" step."""
-    fx = xa is not None
+    fx, ff = xa is not None, xf is not None
     if DETERMINISTIC:  # one split: every dW element receives exactly one atomic contribution
-        return 1, (WGRAD_STAGES if WGRAD_STAGES and (not fx or C.conv_wgrad_has_xa(WGRAD_STAGES)) else 2)
+        return 1, (WGRAD_STAGES if WGRAD_STAGES and _wgrad_has(WGRAD_STAGES, fx, ff) else 2)
     blocks = (WGRAD_TARGET_BLOCKS,) if WGRAD_TARGET_BLOCKS > 0 else WGRAD_CANDIDATES
-    stages = (WGRAD_STAGES,) if WGRAD_STAGES > 0 and (not fx or C.conv_wgrad_has_xa(WGRAD_STAGES)) else (1, 2)
+    stages = (WGRAD_STAGES,) if WGRAD_STAGES > 0 and _wgrad_has(WGRAD_STAGES, fx, ff) else (1, 2)
     if len(blocks) == 1 and len(stages) == 1:
         return blocks[0], stages[0]
-    key = (g.N, g.Cx, g.H, g.W, g.Co, g.kh, g.kw, g.sh, g.pt, g.pl, g.dil, blocks, stages) + ((True,) if fx else ())
+    key = ((g.N, g.Cx, g.H, g.W, g.Co, g.kh, g.kw, g.sh, g.pt, g.pl, g.dil, blocks, stages) + ((True,) if fx else ())
+           + (("xf",) if ff else ()))
     best = _WGRAD_TUNED.get(key)
     if best is not None:
         return best
@@ -777,11 +795,12 @@ def _wgrad_config(dy, x, g: ConvGeom, m, ntot, xa=None):
             cands += [(cand, st) for st in (5, 6) for cand in blocks]
         # (64 / 128 x 256 four-wave tiles, reading the narrow layers' dY half as often, were 5-70 % slower
         # on every ResNet-50 shape: profiles/r4d_wgrad_wide_tiles_probe.txt)
-    if fx:
-        cands = [(cand, st) for cand, st in cands if C.conv_wgrad_has_xa(st)]
+    if fx or ff:
+        cands = [(cand, st) for cand, st in cands if _wgrad_has(st, fx, ff)]
     for cand, st in cands:
         kps, splits = _wgrad_split(m, _wgrad_tiles(g.Co, ntot, st), cand)
-        times[(cand, st)] = _time_ms(lambda: _wgrad_launch(dy, x, scratch, g, m, ntot, kps, splits, st, xa=xa))
+        times[(cand, st)] = _time_ms(lambda: _wgrad_launch(dy, x, scratch, g, m, ntot, kps, splits, st, xa=xa,
+                                                           xf=xf))
     best = min(times, key=times.get)
     _WGRAD_TUNED[key] = best
     WGRAD_TUNE_LOG.append((g.Co, ntot, m, times))
@@ -868,27 +887,27 @@ def comm_stream(dev):
     return s.stream
 
 
-def conv_wgrad_raw(dy, x, w_param, g: ConvGeom, xa=None):
+def conv_wgrad_raw(dy, x, w_param, g: ConvGeom, xa=None, xf=None):
     dev = dy.device
     m = g.N * g.OH * g.OW
     ntot = g.T * g.Cx
-    kps, splits, stages = _wgrad_plan(g, dy, x, m, ntot, xa)
-    if xa is not None and g.Cx != g.Ci:
-        raise RuntimeError("fused BN-backward wgrad: padded input channels")
+    kps, splits, stages = _wgrad_plan(g, dy, x, m, ntot, xa, xf)
+    if (xa is not None or xf is not None) and g.Cx != g.Ci:
+        raise RuntimeError("fused BN wgrad: padded input channels")
     if g.Cx == g.Ci:
         dw = arena_slot(w_param)
         if dw is not None:
             s = side_stream(dev)
             if s is None:
-                _wgrad_launch(dy, x, dw, g, m, ntot, kps, splits, stages, xa=xa)
+                _wgrad_launch(dy, x, dw, g, m, ntot, kps, splits, stages, xa=xa, xf=xf)
                 return dw
             if not s.joins:  # first side launch of this backward: join when the engine finishes
                 torch.autograd.Variable._execution_engine.queue_callback(join_side_streams)
             s.joins.add(torch.cuda.current_stream(dev))
-            _wgrad_launch(dy, x, dw, g, m, ntot, kps, splits, stages, side=s, xa=xa)
+            _wgrad_launch(dy, x, dw, g, m, ntot, kps, splits, stages, side=s, xa=xa, xf=xf)
             return dw
         dw = grad_buffer(w_param)
-        _wgrad_launch(dy, x, dw, g, m, ntot, kps, splits, stages, xa=xa)
+        _wgrad_launch(dy, x, dw, g, m, ntot, kps, splits, stages, xa=xa, xf=xf)
         return dw
     full = torch.zeros(g.Co * ntot, dtype=torch.float32, device=dev)
     dw = arena_slot(w_param)
@@ -1032,15 +1051,73 @@ def xa_eligible(x, conv) -> bool:
             and conv.kernel_size[0] * conv.kernel_size[1] <= 49)
 
 
+# BN apply (+ReLU) fused into the consuming conv (csrc/conv_gemm.hip XF): a BN whose output only
+# feeds one conv hands that conv its input y and its [scale | shift] instead of writing act(bn(y)); the
+# conv's forward and weight-gradient kernels form act(scale * y + shift) on their operand loads, padded taps
+# kept at zero.  The activated tensor is never written or re-read (VERDICT round 2, item 1 "forward").
+FUSE_XF = os.environ.get("IMGCLS_BN_XF", "1") == "1"
+XF_COUNT = [0]  # convs that read a deferred BN output (tests / diagnostics)
+
+
+class XfHold:
+    """The deferred BN output's map: ``coef`` = the BN's [scale | shift | mean | invstd] (written by its
+    forward), ``act`` = 0 (identity) or 1 (ReLU).  Rides on the BN's output tensor as ``_imgcls_xf``; that
+    tensor holds y (the BN input), so only a conv taking the map (``ConvFn``) or ``XfMaterializeFn`` may
+    read it."""
+
+    __slots__ = ("coef", "act")
+
+    def __init__(self):
+        self.coef = None
+        self.act = 0
+
+
+def xf_eligible(x, conv) -> bool:
+    """The conv can read a deferred BN output: dense (no bias / groups / dilation, square stride), input
+    channels a multiple of 64 (uniform k-steps of the forward GEMM, K = taps x Cin), not a dense layer
+    (``DenseConvFn``)."""
+    return (conv.stride[0] == conv.stride[1] and tuple(conv.dilation) == (1, 1) and conv.groups == 1
+            and conv.bias is None and x.shape[1] == conv.in_channels and conv.in_channels % 64 == 0
+            and conv.kernel_size[0] * conv.kernel_size[1] <= 49 and not getattr(conv, "tf_same", False)
+            and not FP8_FWD and not dense_conv_eligible(x, conv))
+
+
+class XfMaterializeFn(torch.autograd.Function):
+    """act(bn(y)) of a deferred BN output for a consumer that cannot take the map (one bn_apply pass -
+    what the BN would have written).  The gradient passes through: it is the gradient w.r.t. act(bn(y)),
+    which is what the deferred output stands for."""
+
+    @staticmethod
+    def forward(ctx, y, hold):
+        n, c, h, w = y.shape
+        out = _empty_cl(n, c, h, w, y.device)
+        C.bn_apply(y, hold.coef, None, out, n * h * w, c, c, 0, hold.act)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None
+
+
+def materialize_deferred(x):
+    """x itself, or act(bn(y)) when x is a deferred BN output (``XfHold``)."""
+    hold = getattr(x, "_imgcls_xf", None)
+    return x if hold is None else XfMaterializeFn.apply(x, hold)
+
+
 class ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, conv, want_stats, slot=None, fuse_bwd=False, xa=None, shift=None):
+    def forward(ctx, x, w, conv, want_stats, slot=None, fuse_bwd=False, xa=None, shift=None, xf=None):
         g = conv_geom(x, conv)
         stats = ws(x.device).stats_buf(g.Co, stat_groups(g.N * g.OH * g.OW)) if want_stats else None
-        y = conv_forward_raw(x, w, g, stats=stats, shift=shift if want_stats else None)
+        xfm = (xf.coef, xf.act) if xf is not None else None
+        y = conv_forward_raw(x, w, g, stats=stats, shift=shift if want_stats else None, xf=xfm)
+        if xf is not None:
+            XF_COUNT[0] += 1
         ctx.g = g
         ctx.slot = slot
         ctx.xa = xa
+        ctx.xf = xfm
         link = getattr(x, "_imgcls_link", None) if (fuse_bwd or slot is not None) else None
         ctx.link = link if (link is not None and link.y is not None and g.Cx == g.Ci) else None
         ctx.save_for_backward(x, w)
@@ -1070,8 +1147,8 @@ class ConvFn(torch.autograd.Function):
                     _syncbn_bwd_start(link)
             if slot is not None:
                 dx = slot.deliver(dx, fused=addend is not None)
-        dw = conv_wgrad_raw(dy, x, w, g, xa=xa) if ctx.needs_input_grad[1] else None
-        return dx, dw, None, None, None, None, None, None
+        dw = conv_wgrad_raw(dy, x, w, g, xa=xa, xf=ctx.xf) if ctx.needs_input_grad[1] else None
+        return dx, dw, None, None, None, None, None, None, None
 
 
 # ---------------------------------------------------------------------------
@@ -1287,13 +1364,20 @@ def _bn_bwd_k(part, grp, c, rows, training, group, count_t, params, dev, coef=No
 class BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, y, gamma, beta, res, bn, act, stats_ready, res_slot=None, link=None, cat=None, xa=None,
-                shift=None):
+                shift=None, defer=None):
         dev = y.device
         n, c, h, w = y.shape
         rows = n * h * w
         a = ACT[act]
         coef, group, count_t = _bn_coef(y, gamma, beta, bn, stats_ready, shift)
-        if cat is not None:  # write straight into this branch's channel slice of the concat output
+        if defer is not None:
+            # deferred (XfHold): the consuming conv applies act(bn(y)) itself; the output stands for
+            # act(bn(y)) but holds y (autograd returns a view of the input)
+            if res is not None or cat is not None or a > 1:
+                raise RuntimeError("deferred BN output: no residual / concat slice, identity or ReLU only")
+            defer.coef, defer.act = coef, a
+            out = y
+        elif cat is not None:  # write straight into this branch's channel slice of the concat output
             cbuf, idx = cat
             base = cbuf.ensure(n, h, w, dev)
             C.bn_apply(y, coef, res, base, rows, c, cbuf.total, cbuf.offs[idx], a)
@@ -1324,7 +1408,7 @@ class BNActFn(torch.autograd.Function):
         return out
 
     @staticmethod
-    def backward(ctx, gout):
+    def backward(ctx, gout):  # (with ``defer`` too: gout is the gradient w.r.t. act(bn(y)))
         y, coef, res = ctx.saved_tensors
         res = res if ctx.has_res else None
         dev = y.device
@@ -1383,7 +1467,7 @@ class BNActFn(torch.autograd.Function):
         dres = dz if ctx.has_res else None
         if dres is not None and ctx.res_slot is not None:
             dres = ctx.res_slot.deliver(dres)
-        return dy, dgamma, dbeta, dres, None, None, None, None, None, None, None, None
+        return dy, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None
 
 
 class BNActPoolFn(torch.autograd.Function):
@@ -1534,11 +1618,17 @@ def pool_conv_bn_act(x, conv, bn, act, prepool, x_slot=None, out=None, out_plan=
     return BNActFn.apply(yp, bn.weight, bn.bias, None, bn, act, False, None, None, out, None, stat_shift(bn))
 
 
-def conv_bn_act(x, conv, bn, act, residual, x_slot=None, res_slot=None, exclusive_input=False, out=None):
+def conv_bn_act(x, conv, bn, act, residual, x_slot=None, res_slot=None, exclusive_input=False, out=None,
+                defer_act=False):
     """``exclusive_input``: this conv is the only consumer of ``x`` (lets its dgrad fuse the BN-backward
     reduce of x's producer); a slot-paired consumer qualifies automatically.  ``out`` = (ConcatBuffer,
-    branch index): the result is written into that branch's channel slice of the concat output."""
+    branch index): the result is written into that branch's channel slice of the concat output.
+    ``defer_act``: the result only feeds the next ``conv_bn_act`` (as its exclusive input); in training the
+    BN then hands that conv y and its map instead of writing act(bn(y)) (``XfHold``)."""
     shift = stat_shift(bn)
+    xf = getattr(x, "_imgcls_xf", None)
+    if xf is not None and not xf_eligible(x, conv):
+        x, xf = XfMaterializeFn.apply(x, xf), None
     if stem_s2d_eligible(x, conv) and residual is None and not x.requires_grad:
         ensure_channels_last_weight(conv)
         y = StemS2dFn.apply(x, conv.weight, conv, bn.training, shift)
@@ -1567,15 +1657,22 @@ def conv_bn_act(x, conv, bn, act, residual, x_slot=None, res_slot=None, exclusiv
         if conv.groups != 1:
             raise NotImplementedError("grouped convolution")
         xa = XaLink() if (bn.training and torch.is_grad_enabled() and xa_eligible(x, conv)) else None
-        y = ConvFn.apply(x, conv.weight, conv, bn.training, x_slot, exclusive_input and FUSE_BN_BWD, xa, shift)
+        y = ConvFn.apply(x, conv.weight, conv, bn.training, x_slot, exclusive_input and FUSE_BN_BWD, xa, shift, xf)
+        xf = None
         ready = bn.training
+    if xf is not None:
+        raise RuntimeError("deferred BN output reached a consumer without the fused map")
     if conv.bias is not None:
         raise NotImplementedError("conv bias before BatchNorm")
     link = BwdLink() if (FUSE_BN_BWD and bn.training and torch.is_grad_enabled()) else None
+    hold = XfHold() if (defer_act and FUSE_XF and bn.training and torch.is_grad_enabled() and residual is None
+                        and out is None and ACT[act] <= 1 and not FP8_FWD) else None
     res_out = BNActFn.apply(y, bn.weight, bn.bias, residual, bn, act, ready, res_slot, link, out,
-                            xa if not depthwise and not dense else None, shift)
+                            xa if not depthwise and not dense else None, shift, hold)
     if link is not None:
         res_out._imgcls_link = link
+    if hold is not None:
+        res_out._imgcls_xf = hold
     return res_out
 
 

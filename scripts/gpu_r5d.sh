@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 3 call d: fused BN-backward (XA; 1x1, padded 3x3, strided dgrads) tests, headline A/B + kernel-trace
+# Round 3 call d: fused BN-backward (XA) and BN-apply (XF) tests, headline A/B + kernel-trace
 # breakdown, learning-parity tests, b1536 memory diagnosis, SyncBN peer tests (incl. fatal timeout), host
 # data path, Inception small batch (eager / graph / reference stack), and a 2-rank one-GPU rehearsal of the
 # N>1 bench fields (gloo: functional, not a scaling number).
@@ -9,11 +9,14 @@ export TMPDIR=/tmp
 ( while true; do sleep 30; date +%s >> gpurun_out/r5d_ticks.txt; done ) & TICK=$!
 trap 'kill $TICK' EXIT
 timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_hip_ops.py \
-  -k "fused or shadow or dense or large_mean or conv_bn_act or stem" > gpurun_out/r5d_pytest_xa.log 2>&1 || { tail -40 gpurun_out/r5d_pytest_xa.log; exit 1; }
+  -k "fused or shadow or dense or large_mean or conv_bn_act or stem or defers" > gpurun_out/r5d_pytest_xa.log 2>&1 || { tail -40 gpurun_out/r5d_pytest_xa.log; exit 1; }
 tail -2 gpurun_out/r5d_pytest_xa.log
 b() { local tag=$1; shift; timeout -k 10 400 python bench.py "$@" > gpurun_out/r5d_$tag.log 2>&1 || { tail -5 gpurun_out/r5d_$tag.log; return 1; }
       echo "$tag $(grep -h '^{"metric' gpurun_out/r5d_$tag.log | cut -c80-170)"; }
-for xa in 0 1; do IMGCLS_BN_XA=$xa b xa$xa --warmup 8 --steps 20 || exit 1; done
+# round-2 path (no fusion) / BN-backward fused (XA) / + BN-apply fused (XF, the default)
+IMGCLS_BN_XA=0 IMGCLS_BN_XF=0 b xa0 --warmup 8 --steps 20 || exit 1
+IMGCLS_BN_XF=0 b xa1 --warmup 8 --steps 20 || exit 1
+b xaxf --warmup 8 --steps 20 || exit 1
 timeout -k 10 500 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r5d_prof -o hip -- \
   python3 bench.py --warmup 6 --steps 3 > gpurun_out/r5d_prof.log 2>&1 || { tail -5 gpurun_out/r5d_prof.log; exit 1; }
 python scripts/step_breakdown.py gpurun_out/r5d_prof/hip_kernel_trace.csv > gpurun_out/r5d_step_breakdown.txt
