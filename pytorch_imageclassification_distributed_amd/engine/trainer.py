@@ -22,6 +22,7 @@ all-reduces two integers (A14) instead of per-sample ``.cpu()`` + pickle.
 """
 from __future__ import annotations
 
+import collections
 import math
 import os
 import sys
@@ -43,6 +44,9 @@ from ..utils import (BEST, LATEST, AccuracyCounter, DeviceMeter, JsonlLogger, lo
 from ..utils.timers import PhaseTimer
 from .config import parse_class_weights
 from .optim import FusedAdam, MultiStepLR
+
+# training steps the host may have enqueued ahead of the GPU (Trainer._throttle; 0 = unbounded)
+MAX_INFLIGHT_STEPS = int(os.environ.get("IMGCLS_MAX_INFLIGHT_STEPS", "2"))
 
 
 def _is_inception(name: str) -> bool:
@@ -171,6 +175,7 @@ class Trainer:
         self._prof = None
         self._graph = None  # captured whole-step HIP graph (``capture_step``)
         self._eager_steps = 0  # eager training steps run by this process (graph capture waits for 2)
+        self._inflight = collections.deque()  # end-of-step events of the steps the GPU has not finished
 
     # ------------------------------------------------------------------ step
     def compute_loss(self, images, labels):
@@ -192,16 +197,40 @@ class Trainer:
         dispatcher hands free CUs to the critical dgrad -> BN-backward chain first and the weight
         GEMMs fill the rest (ResNet-50 b512: +1.5 % over one stream; the side stream at equal priority
         was 1.8 % slower than one stream)."""
+        self._throttle()
         st = self.step_stream
         if st is None:
-            return self._train_step(images, labels)
+            loss = self._train_step(images, labels)
+            self._step_enqueued()
+            return loss
         caller = torch.cuda.current_stream(self.dev)
         st.wait_stream(caller)
         with torch.cuda.stream(st):
             loss = self._train_step(images, labels)
         caller.wait_stream(st)
         loss.record_stream(caller)
+        self._step_enqueued()
         return loss
+
+    def _throttle(self) -> None:
+        """Keep at most MAX_INFLIGHT_STEPS steps enqueued ahead of the GPU (a host wait on the oldest step's
+        end event).  The host enqueues a ResNet-50 b1024 step in ~10 ms and the GPU runs it in ~75 ms, so an
+        unthrottled host runs many steps ahead.  Every tensor handed to the weight-gradient side stream
+        (``record_stream``) then stays unusable until the GPU reaches its event, so the caching allocator
+        keeps mapping new blocks for the steps in flight.  Round 3 measured ResNet-50 b1024 at 44 GiB
+        allocated but 286 GiB reserved; at the 288 GB limit the allocator frees its whole cache with
+        device syncs and re-maps each block: 1.6 s steps, the b1536 / b2048 slowdown of round 2
+        (docs/DESIGN.md).  Two steps in flight keep the GPU fed and bound the cache."""
+        if self.dev.type != "cuda" or MAX_INFLIGHT_STEPS <= 0:
+            return
+        while len(self._inflight) >= MAX_INFLIGHT_STEPS:
+            self._inflight.popleft().synchronize()
+
+    def _step_enqueued(self) -> None:
+        if self.dev.type == "cuda" and MAX_INFLIGHT_STEPS > 0:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.dev))
+            self._inflight.append(ev)
 
     # ------------------------------------------------------------------ HIP graph
     def capture_step(self, images, labels) -> None:
@@ -231,6 +260,7 @@ class Trainer:
         if self._graph is None or tuple(g["lr"] for g in self.optimizer.param_groups) != self._g_lrs:
             self._graph = None
             self.capture_step(images, labels)
+        self._throttle()
         st = self._g_stream
         caller = torch.cuda.current_stream(self.dev)
         st.wait_stream(caller)
@@ -241,6 +271,7 @@ class Trainer:
         caller.wait_stream(st)
         images.record_stream(st)
         labels.record_stream(st)
+        self._step_enqueued()
         return self._g_loss
 
     def _epoch_step(self, images, labels, index: int):

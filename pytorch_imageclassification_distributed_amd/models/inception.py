@@ -28,14 +28,15 @@ class BasicConv2d(nn.Module):
         self.conv = nn.Conv2d(cin, cout, bias=False, **kw)
         self.bn = nn.BatchNorm2d(cout, eps=0.001)
 
-    def forward(self, x, exclusive=False, slot=None, out=None, pool=None, prepool=None):
+    def forward(self, x, exclusive=False, slot=None, out=None, pool=None, prepool=None, defer=False):
         """``exclusive``: this conv is the only consumer of ``x`` (a chain-internal conv), which lets its
         dgrad epilogue run the producer's BN-backward reduce; ``slot``: x feeds exactly two convs;
         ``out``: (concat plan, branch) - write the result into the block's concat output in place;
         ``pool``: (kernel, stride, padding) of a max pool applied to the result (stem); ``prepool``: of an
-        average pool applied to ``x`` first (``branch_pool``)."""
+        average pool applied to ``x`` first (``branch_pool``); ``defer``: the result feeds only the next
+        conv of the chain (the HIP path lets that conv apply this BN + ReLU on its operand loads)."""
         return Fx.conv_bn_act(x, self.conv, self.bn, "relu", x_slot=slot, exclusive_input=exclusive, out=out,
-                              pool=pool, prepool=prepool)
+                              pool=pool, prepool=prepool, defer_act=defer)
 
 
 class InceptionA(nn.Module):
@@ -54,7 +55,8 @@ class InceptionA(nn.Module):
         cat = Fx.concat_buffer([64, 64, 96, self.branch_pool.conv.out_channels])  # branches write in place
         b1 = self.branch1x1(x, slot=s, out=(cat, 0))
         b5 = self.branch5x5_2(self.branch5x5_1(x, slot=s), True, out=(cat, 1))
-        b3 = self.branch3x3dbl_3(self.branch3x3dbl_2(self.branch3x3dbl_1(x, slot=s), True), True, out=(cat, 2))
+        b3 = self.branch3x3dbl_3(self.branch3x3dbl_2(self.branch3x3dbl_1(x, slot=s, defer=True), True), True,
+                                 out=(cat, 2))
         bp = self.branch_pool(x, slot=s, prepool=(3, 1, 1), out=(cat, 3))
         return Fx.cat_channels([b1, b5, b3, bp], cat)
 
@@ -71,7 +73,8 @@ class InceptionB(nn.Module):
         s = Fx.grad_slot(x, 3)
         cat = Fx.concat_buffer([384, 96, x.shape[1]])  # the pool branch is copied in
         b3 = self.branch3x3(x, slot=s, out=(cat, 0))
-        bd = self.branch3x3dbl_3(self.branch3x3dbl_2(self.branch3x3dbl_1(x, slot=s), True), True, out=(cat, 1))
+        bd = self.branch3x3dbl_3(self.branch3x3dbl_2(self.branch3x3dbl_1(x, slot=s, defer=True), True), True,
+                                 out=(cat, 1))
         bp = Fx.max_pool2d(x, 3, 2, 0, slot=s)
         return Fx.cat_channels([b3, bd, bp], cat)
 
@@ -95,10 +98,12 @@ class InceptionC(nn.Module):
         s = Fx.grad_slot(x, 4)
         cat = Fx.concat_buffer([192, 192, 192, 192])
         b1 = self.branch1x1(x, slot=s, out=(cat, 0))
-        b7 = self.branch7x7_3(self.branch7x7_2(self.branch7x7_1(x, slot=s), True), True, out=(cat, 1))
-        bd = self.branch7x7dbl_1(x, slot=s)
-        bd = self.branch7x7dbl_3(self.branch7x7dbl_2(bd, True), True)
-        bd = self.branch7x7dbl_5(self.branch7x7dbl_4(bd, True), True, out=(cat, 2))
+        # chain-internal outputs are deferred (their consumer applies BN + ReLU; c7 = 160 materialises them)
+        b7 = self.branch7x7_1(x, slot=s, defer=True)
+        b7 = self.branch7x7_3(self.branch7x7_2(b7, True, defer=True), True, out=(cat, 1))
+        bd = self.branch7x7dbl_1(x, slot=s, defer=True)
+        bd = self.branch7x7dbl_3(self.branch7x7dbl_2(bd, True, defer=True), True, defer=True)
+        bd = self.branch7x7dbl_5(self.branch7x7dbl_4(bd, True, defer=True), True, out=(cat, 2))
         bp = self.branch_pool(x, slot=s, prepool=(3, 1, 1), out=(cat, 3))
         return Fx.cat_channels([b1, b7, bd, bp], cat)
 
@@ -116,9 +121,9 @@ class InceptionD(nn.Module):
     def forward(self, x):
         s = Fx.grad_slot(x, 3)
         cat = Fx.concat_buffer([320, 192, x.shape[1]])
-        b3 = self.branch3x3_2(self.branch3x3_1(x, slot=s), True, out=(cat, 0))
-        b7 = self.branch7x7x3_2(self.branch7x7x3_1(x, slot=s), True)
-        b7 = self.branch7x7x3_4(self.branch7x7x3_3(b7, True), True, out=(cat, 1))
+        b3 = self.branch3x3_2(self.branch3x3_1(x, slot=s, defer=True), True, out=(cat, 0))
+        b7 = self.branch7x7x3_2(self.branch7x7x3_1(x, slot=s, defer=True), True, defer=True)
+        b7 = self.branch7x7x3_4(self.branch7x7x3_3(b7, True, defer=True), True, out=(cat, 1))
         bp = Fx.max_pool2d(x, 3, 2, 0, slot=s)
         return Fx.cat_channels([b3, b7, bp], cat)
 
@@ -143,7 +148,7 @@ class InceptionE(nn.Module):
         b3 = self.branch3x3_1(x, slot=s)
         s3 = Fx.grad_slot(b3)  # b3 and bd each feed exactly two convs: paired gradient slots
         b3a, b3b = self.branch3x3_2a(b3, slot=s3, out=(cat, 1)), self.branch3x3_2b(b3, slot=s3, out=(cat, 2))
-        bd = self.branch3x3dbl_2(self.branch3x3dbl_1(x, slot=s), True)
+        bd = self.branch3x3dbl_2(self.branch3x3dbl_1(x, slot=s, defer=True), True)
         sd = Fx.grad_slot(bd)
         bda, bdb = self.branch3x3dbl_3a(bd, slot=sd, out=(cat, 3)), self.branch3x3dbl_3b(bd, slot=sd, out=(cat, 4))
         bp = self.branch_pool(x, slot=s, prepool=(3, 1, 1), out=(cat, 5))

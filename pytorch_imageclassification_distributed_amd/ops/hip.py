@@ -1519,6 +1519,7 @@ STEM_POOL_FUSE = os.environ.get("IMGCLS_STEM_POOL_FUSE", "1") == "1"
 def conv_bn_act_pool(x, conv, bn, act, pool, exclusive_input=False):
     """max_pool2d(act(bn(conv(x))), *pool) with the pool fused into the BN passes (stems).
     ``exclusive_input`` as for ``conv_bn_act`` (the conv's dgrad may run x's producer BN reduce)."""
+    x = materialize_deferred(x)
     k, s, p = _pool_args(*pool)
     if not STEM_POOL_FUSE or k[0] * k[1] > 255 or 2 * p[0] > k[0] or 2 * p[1] > k[1]:
         return max_pool2d(conv_bn_act(x, conv, bn, act, None, exclusive_input=exclusive_input), *pool)
@@ -1604,6 +1605,7 @@ def pool_conv_bn_act(x, conv, bn, act, prepool, x_slot=None, out=None, out_plan=
     ``branch_pool`` convs narrow 192-2048 channels to 32-192, so the pool's forward and backward passes
     move 4-11x fewer bytes, and the conv's dgrad (not an avgpool backward) delivers into the block
     input's gradient slot.  BN statistics are taken after the pool."""
+    x = materialize_deferred(x)
     k, s, p = _pool_args(*prepool)
     pointwise = (tuple(conv.kernel_size) == (1, 1) and tuple(conv.stride) == (1, 1)
                  and tuple(conv.padding) == (0, 0) and conv.groups == 1 and conv.bias is None

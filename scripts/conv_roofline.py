@@ -43,20 +43,22 @@ def _timed(kind, fn, flop, nbytes, desc):
 
 def gemm(A, B_, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(None,) * 4 + (0, 1), **kw):
     m, n, k = geo[0], geo[1], geo[2]
-    kind = "dgrad" if (bwd[0] is not None or addend is not None or geo[12] > 1 or geo[13] or geo[14]) else "fwd"
+    xa = kw.get("xa")
+    kind = "dgrad" if (bwd[0] is not None or addend is not None or xa is not None or geo[12] > 1 or geo[13]
+                       or geo[14]) else "fwd"
     nb = 2 * (A.numel() + B_.numel() + m * n) + (2 * m * n if addend is not None else 0) + \
-        (4 * m * n if bwd[0] is not None else 0)
+        (4 * m * n if bwd[0] is not None else 0) + (2 * A.numel() if xa is not None else 0)
     return _timed(kind, lambda: _orig_gemm(A, B_, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, **kw),
                   2.0 * m * n * k, nb, f"M={m} N={n} K={k} CA={geo[3]}")
 
 
-def wgrad(dy, x, out, g, m, ntot, kps, splits, stages=2, side=None):
+def wgrad(dy, x, out, g, m, ntot, kps, splits, stages=2, side=None, **kw):
     # timed on the current stream (the side-stream fork would escape the events); the in-step overlap
     # is not part of a per-launch roofline
-    nb = 2 * (dy.numel() + x.numel()) + 4 * out.numel() * splits
+    nb = 2 * (dy.numel() + x.numel()) + 4 * out.numel() * splits + (2 * dy.numel() if kw.get("xa") is not None else 0)
     if not ON[0]:
-        return _orig_wg(dy, x, out, g, m, ntot, kps, splits, stages, side=side)
-    return _timed("wgrad", lambda: _orig_wg(dy, x, out, g, m, ntot, kps, splits, stages), 2.0 * m * g.Co * ntot, nb,
+        return _orig_wg(dy, x, out, g, m, ntot, kps, splits, stages, side=side, **kw)
+    return _timed("wgrad", lambda: _orig_wg(dy, x, out, g, m, ntot, kps, splits, stages, **kw), 2.0 * m * g.Co * ntot, nb,
                   f"Co={g.Co} Ntot={ntot} Mpix={m} splits={splits} st={stages}")
 
 

@@ -1167,9 +1167,9 @@ def test_bn_apply_fused_into_consumer_conv(case):
 
 def test_bn_apply_fused_every_kernel_variant():
     """Every conv configuration with a fused A-operand variant and every wgrad ring / tile variant with a
-    fused X form (256 output channels: the 256 x 256 wgrad tiles qualify), against the unfused path."""
+    fused X form (256 channels on both convs: the 256 x 256 wgrad tiles qualify), against the unfused path."""
     hip = _hip()
-    case = (2, 128, 20, 64, 3, 1, "relu")
+    case = (2, 128, 12, 256, 3, 1, "relu")
     _o, g0, _ = _xf_block(hip, *case, xf_on=False, cout=256)
     ran = 0
     for i in range(len(hip.conv_cfgs())):
@@ -1213,6 +1213,41 @@ def test_resnet_bottleneck_defers_bn_apply():
     assert res[0][-1] == 0 and res[1][-1] == 2, (res[0][-1], res[1][-1])
     for a_, b_ in zip(res[1][:-1], res[0][:-1]):
         assert rel_err(a_, b_) < 2e-2, rel_err(a_, b_)
+
+
+@pytest.mark.parametrize("block,expect", [("A", 1), ("C128", 6), ("C160", 0), ("D", 4), ("E", 1)])
+def test_inception_defers_chain_bn_apply(block, expect):
+    """Inception blocks: every chain-internal BN output is deferred; consumers with 64-multiple input
+    channels read it through the fused map, the others (48 / 96 / 160 channels) materialise it.  Output and
+    gradients against the unfused run."""
+    hip = _hip()
+    from pytorch_imageclassification_distributed_amd.models import inception as inc
+    torch.manual_seed(5)
+    mk = {"A": (lambda: inc.InceptionA(192, 32), 192, 35), "C128": (lambda: inc.InceptionC(768, 128), 768, 17),
+          "C160": (lambda: inc.InceptionC(768, 160), 768, 17), "D": (lambda: inc.InceptionD(768), 768, 17),
+          "E": (lambda: inc.InceptionE(1280), 1280, 8)}[block]
+    blk = mk[0]().to(DEV).to(memory_format=CL)
+    x = torch.randn(4, mk[1], mk[2], mk[2], device=DEV).to(torch.bfloat16).contiguous(memory_format=CL)
+    res = []
+    for on in (False, True):
+        keep = hip.FUSE_XF
+        hip.FUSE_XF = on
+        try:
+            b = copy.deepcopy(blk)
+            xb = x.clone().requires_grad_(True)
+            n0 = hip.XF_COUNT[0]
+            out = b(xb)
+            out.float().square().mean().backward()
+            torch.cuda.synchronize()
+            wg = [m.weight.grad.float() for m in b.modules() if isinstance(m, nn.Conv2d)]
+            res.append((out.float(), xb.grad.float(), wg, hip.XF_COUNT[0] - n0))
+        finally:
+            hip.FUSE_XF = keep
+    assert res[0][3] == 0 and res[1][3] == expect, (res[0][3], res[1][3])
+    assert rel_err(res[1][0], res[0][0]) < 2e-2
+    assert rel_err(res[1][1], res[0][1]) < 3e-2, rel_err(res[1][1], res[0][1])
+    for a_, b_ in zip(res[1][2], res[0][2]):
+        assert rel_err(a_, b_) < 3e-2, rel_err(a_, b_)
 
 
 @pytest.mark.parametrize("path", ["bn_stats", "conv_epilogue"])
