@@ -63,7 +63,8 @@ def parse():
     p.add_argument("--graph", default="off", choices=["on", "off"],
                    help="replay the whole training step as one captured HIP graph (single process)")
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
-                   help="fp8: MX-FP8 forward convolutions (BASELINE config 5); bf16 elsewhere")
+                   help="fp8 (experimental): MX-FP8 forward convolutions only, bf16 backward - measured "
+                        "+0.3 %% over bf16 at b1024, not a speed-up (README)")
     p.add_argument("--data", default="device", choices=["device", "host"],
                    help="device: batches generated once in HBM (the step alone); host: pinned uint8 host batches "
                         "copied by hipMemcpyAsync on a copy stream and normalised on the GPU inside the timed loop "

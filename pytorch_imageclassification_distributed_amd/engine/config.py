@@ -48,8 +48,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--compute", default="auto", choices=["auto", "hip", "torch"],
                    help="hip = native kernels (GPU default); torch = ATen reference stack")
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp8"],
-                   help="GPU compute dtype: bf16 (fp32 master weights); fp8 = MX-FP8 forward convolutions "
-                        "(e4m3 + E8M0 per 32 channels) where Cin % 128 == 0, bf16 elsewhere and in backward")
+                   help="GPU compute dtype: bf16 (fp32 master weights); fp8 = experimental MX-FP8 forward "
+                        "convolutions (e4m3 + E8M0 per 32 channels) where Cin %% 128 == 0, bf16 elsewhere and in "
+                        "backward (no measurable speed-up: README); fp32 = the ATen path only (--compute torch)")
     p.add_argument("--sync-bn", dest="sync_bn", action="store_true", default=True)
     p.add_argument("--no-sync-bn", dest="sync_bn", action="store_false")
     p.add_argument("--syncbn-comm", default="auto", choices=["auto", "peer", "rccl"],

@@ -1018,6 +1018,16 @@ class BwdLink:
 # GEMMs read dY - the BN elementwise passes were 37 % of the ResNet-50 step)
 FUSE_XA = os.environ.get("IMGCLS_BN_XA", "1") == "1"
 XA_COUNT = [0]  # BN backwards handed to their producer conv (tests / diagnostics)
+# A fused operand map is applied every time the GEMM loads the element: once per tap that gathers it and
+# once per tile along the GEMM's other dimension.  The unfused pass touches each element once (memory-
+# bound), so fusing pays only while that replication stays small (docs/DESIGN.md, "what fusion costs").
+XA_MAX_REP = int(os.environ.get("IMGCLS_XA_MAX_REP", "2"))
+XF_MAX_REP = int(os.environ.get("IMGCLS_XF_MAX_REP", "2"))
+
+
+def _rep(taps: int, other: int) -> int:
+    """Times a fused operand map runs per element: taps x tiles of (up to) 256 along the other dimension."""
+    return taps * max(1, -(-other // 256))
 
 
 class XaLink:
@@ -1045,17 +1055,22 @@ def xa_eligible(x, conv) -> bool:
     """A dense conv (no bias / groups / dilation, square stride) whose output channels are a multiple of 64
     (uniform k-steps of the dgrad GEMM, K = taps x Cout) and whose input channels are unpadded: its backward
     can take the fused BN-backward operand map (padded taps are masked in the kernel)."""
+    taps = conv.kernel_size[0] * conv.kernel_size[1]
     return (FUSE_XA and conv.stride[0] == conv.stride[1] and tuple(conv.dilation) == (1, 1)
             and conv.groups == 1 and conv.bias is None and conv.out_channels % 64 == 0
-            and x.shape[1] == conv.in_channels and conv.in_channels % 8 == 0
-            and conv.kernel_size[0] * conv.kernel_size[1] <= 49)
+            and x.shape[1] == conv.in_channels and conv.in_channels % 8 == 0 and taps <= 49
+            # dgrad: dz gathered by every tap, per tile of the input channels; wgrad: per column tile
+            and max(_rep(taps, conv.in_channels), _rep(1, taps * conv.in_channels)) <= XA_MAX_REP)
 
 
 # BN apply (+ReLU) fused into the consuming conv (SURVEY K6, csrc/conv_gemm.hip XF): a BN whose output only
 # feeds one conv hands that conv its input y and its [scale | shift] instead of writing act(bn(y)); the
 # conv's forward and weight-gradient kernels form act(scale * y + shift) on their operand loads, padded taps
 # kept at zero.  The activated tensor is never written or re-read (VERDICT round 2, item 1 "forward").
-FUSE_XF = os.environ.get("IMGCLS_BN_XF", "1") == "1"
+# Off by default: measured on ResNet-50 b1024 (profiles/r5f_fusion_ab.txt) it does not pay - the bn_apply passes
+# it removes are small (the non-residual ones were 3.5 ms of the 77 ms step) and a 3x3 consumer re-applies the
+# map once per tap
+FUSE_XF = os.environ.get("IMGCLS_BN_XF", "0") == "1"
 XF_COUNT = [0]  # convs that read a deferred BN output (tests / diagnostics)
 
 
@@ -1076,9 +1091,12 @@ def xf_eligible(x, conv) -> bool:
     """The conv can read a deferred BN output: dense (no bias / groups / dilation, square stride), input
     channels a multiple of 64 (uniform k-steps of the forward GEMM, K = taps x Cin), not a dense layer
     (``DenseConvFn``)."""
+    taps = conv.kernel_size[0] * conv.kernel_size[1]
     return (conv.stride[0] == conv.stride[1] and tuple(conv.dilation) == (1, 1) and conv.groups == 1
             and conv.bias is None and x.shape[1] == conv.in_channels and conv.in_channels % 64 == 0
-            and conv.kernel_size[0] * conv.kernel_size[1] <= 49 and not getattr(conv, "tf_same", False)
+            and taps <= 49 and not getattr(conv, "tf_same", False)
+            # forward and wgrad: y gathered by every tap, per tile of the output channels
+            and _rep(taps, conv.out_channels) <= XF_MAX_REP
             and not FP8_FWD and not dense_conv_eligible(x, conv))
 
 

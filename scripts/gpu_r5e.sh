@@ -6,9 +6,12 @@ cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out
 export TMPDIR=/tmp
 ( while true; do sleep 30; date +%s >> gpurun_out/r5e_ticks.txt; done ) & TICK=$!
 trap 'kill $TICK' EXIT
-timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_hip_ops.py -k "defers or apply_fused" \
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_hip_ops.py -k "defers or apply_fused or large_mean" \
   > gpurun_out/r5e_pytest_xf.log 2>&1 || { tail -30 gpurun_out/r5e_pytest_xf.log; exit 1; }
 tail -1 gpurun_out/r5e_pytest_xf.log
+timeout -k 10 900 python -u -m pytest -x -v -s --timeout 400 --timeout-method thread tests/test_gpu_learning.py \
+  > gpurun_out/r5e_pytest_learning.log 2>&1 || { grep -h "hip loss" gpurun_out/r5e_pytest_learning.log; tail -30 gpurun_out/r5e_pytest_learning.log; exit 1; }
+grep -h "hip loss" gpurun_out/r5e_pytest_learning.log; tail -1 gpurun_out/r5e_pytest_learning.log
 timeout -k 10 600 python scripts/conv_roofline.py 1024 2300 6.0 > gpurun_out/r5e_conv_roofline_b1024.txt 2>&1 || { tail -20 gpurun_out/r5e_conv_roofline_b1024.txt; exit 1; }
 sed -n '8,40p' gpurun_out/r5e_conv_roofline_b1024.txt
 P="python3 scripts/conv_probe.py --batch 1024 --iters 10"

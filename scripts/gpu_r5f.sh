@@ -12,6 +12,9 @@ b() { local tag=$1; shift; timeout -k 10 400 python bench.py "$@" > gpurun_out/r
 IMGCLS_BN_XA=0 IMGCLS_BN_XF=0 b plain --warmup 8 --steps 20 || exit 1
 IMGCLS_BN_XF=0 b xa --warmup 8 --steps 20 || exit 1
 b xaxf --warmup 8 --steps 20 || exit 1
+IMGCLS_XA_MAX_REP=1000000 IMGCLS_XF_MAX_REP=1000000 b xaxf_ungated --warmup 8 --steps 20 || exit 1
+IMGCLS_XA_MAX_REP=1 IMGCLS_XF_MAX_REP=1 b xaxf_rep1 --warmup 8 --steps 20 || exit 1
+IMGCLS_XA_MAX_REP=4 IMGCLS_XF_MAX_REP=4 b xaxf_rep4 --warmup 8 --steps 20 || exit 1
 IMGCLS_MAX_INFLIGHT_STEPS=0 b xaxf_unthrottled --warmup 8 --steps 20 || exit 1
 b xaxf_b1536 --batch 1536 --warmup 8 --steps 15 || exit 1
 b xaxf_b2048 --batch 2048 --warmup 8 --steps 10 || exit 1

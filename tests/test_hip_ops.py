@@ -1039,8 +1039,8 @@ def _xa_block(hip, n, cin, hw, cmid, stride, act, use_res, xa_on, cfg=None, wsta
     x = bf(torch.randn(n, cin, hw, hw, device=DEV)).to(torch.bfloat16).contiguous(memory_format=CL)
     oh = (hw + 2 * (k // 2) - k) // stride + 1
     res = bf(torch.randn(n, cmid, oh, oh, device=DEV)).to(torch.bfloat16).contiguous(memory_format=CL)
-    keep = hip.FUSE_XA, hip.CONV_FORCE_CFG, hip.WGRAD_STAGES
-    hip.FUSE_XA = xa_on
+    keep = hip.FUSE_XA, hip.CONV_FORCE_CFG, hip.WGRAD_STAGES, hip.XA_MAX_REP
+    hip.FUSE_XA, hip.XA_MAX_REP = xa_on, 10 ** 6  # every eligible geometry, whatever the cost gate says
     if cfg is not None:
         hip.CONV_FORCE_CFG = (0, 0, cfg)
     if wstages is not None:
@@ -1058,7 +1058,7 @@ def _xa_block(hip, n, cin, hw, cmid, stride, act, use_res, xa_on, cfg=None, wsta
                  c2.weight.grad.float()] + ([rb.grad.float()] if use_res else [])
         return out.float(), grads, hip.XA_COUNT[0] - n0
     finally:
-        hip.FUSE_XA, hip.CONV_FORCE_CFG, hip.WGRAD_STAGES = keep
+        hip.FUSE_XA, hip.CONV_FORCE_CFG, hip.WGRAD_STAGES, hip.XA_MAX_REP = keep
 
 
 @pytest.mark.parametrize("case", [
@@ -1119,8 +1119,8 @@ def _xf_block(hip, n, cin, hw, cmid, k, stride, act, xf_on, cout=128, cfg=None, 
         b1.weight.uniform_(0.5, 1.5)
         b1.bias.uniform_(-0.5, 0.5)
     x = bf(torch.randn(n, cin, hw, hw, device=DEV)).to(torch.bfloat16).contiguous(memory_format=CL)
-    keep = hip.FUSE_XF, hip.CONV_FORCE_CFG, hip.WGRAD_STAGES
-    hip.FUSE_XF = xf_on
+    keep = hip.FUSE_XF, hip.CONV_FORCE_CFG, hip.WGRAD_STAGES, hip.XF_MAX_REP
+    hip.FUSE_XF, hip.XF_MAX_REP = xf_on, 10 ** 6
     if cfg is not None:
         hip.CONV_FORCE_CFG = (0, 0, cfg)
     if wstages is not None:
@@ -1138,7 +1138,7 @@ def _xf_block(hip, n, cin, hw, cmid, k, stride, act, xf_on, cout=128, cfg=None, 
                  c2.weight.grad.float(), b2.weight.grad.float()]
         return out.float(), grads, hip.XF_COUNT[0] - n0
     finally:
-        hip.FUSE_XF, hip.CONV_FORCE_CFG, hip.WGRAD_STAGES = keep
+        hip.FUSE_XF, hip.CONV_FORCE_CFG, hip.WGRAD_STAGES, hip.XF_MAX_REP = keep
 
 
 @pytest.mark.parametrize("case", [
@@ -1197,8 +1197,8 @@ def test_resnet_bottleneck_defers_bn_apply():
     x = torch.randn(4, 256, 28, 28, device=DEV).to(torch.bfloat16).contiguous(memory_format=CL)
     res = []
     for on in (False, True):
-        keep = hip.FUSE_XF
-        hip.FUSE_XF = on
+        keep = hip.FUSE_XF, hip.XF_MAX_REP
+        hip.FUSE_XF, hip.XF_MAX_REP = on, 10 ** 6
         try:
             b = copy.deepcopy(blk)
             xb = x.clone().requires_grad_(True)
@@ -1209,7 +1209,7 @@ def test_resnet_bottleneck_defers_bn_apply():
             res.append((out.float(), xb.grad.float(), b.conv2.weight.grad.float(), b.conv3.weight.grad.float(),
                         hip.XF_COUNT[0] - n0))
         finally:
-            hip.FUSE_XF = keep
+            hip.FUSE_XF, hip.XF_MAX_REP = keep
     assert res[0][-1] == 0 and res[1][-1] == 2, (res[0][-1], res[1][-1])
     for a_, b_ in zip(res[1][:-1], res[0][:-1]):
         assert rel_err(a_, b_) < 2e-2, rel_err(a_, b_)
@@ -1230,8 +1230,8 @@ def test_inception_defers_chain_bn_apply(block, expect):
     x = torch.randn(4, mk[1], mk[2], mk[2], device=DEV).to(torch.bfloat16).contiguous(memory_format=CL)
     res = []
     for on in (False, True):
-        keep = hip.FUSE_XF
-        hip.FUSE_XF = on
+        keep = hip.FUSE_XF, hip.XF_MAX_REP
+        hip.FUSE_XF, hip.XF_MAX_REP = on, 10 ** 6
         try:
             b = copy.deepcopy(blk)
             xb = x.clone().requires_grad_(True)
@@ -1242,7 +1242,7 @@ def test_inception_defers_chain_bn_apply(block, expect):
             wg = [m.weight.grad.float() for m in b.modules() if isinstance(m, nn.Conv2d)]
             res.append((out.float(), xb.grad.float(), wg, hip.XF_COUNT[0] - n0))
         finally:
-            hip.FUSE_XF = keep
+            hip.FUSE_XF, hip.XF_MAX_REP = keep
     assert res[0][3] == 0 and res[1][3] == expect, (res[0][3], res[1][3])
     assert rel_err(res[1][0], res[0][0]) < 2e-2
     assert rel_err(res[1][1], res[0][1]) < 3e-2, rel_err(res[1][1], res[0][1])
