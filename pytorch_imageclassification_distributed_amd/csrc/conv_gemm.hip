@@ -1788,6 +1788,9 @@ static const ConvCfg g_cfgs[] = {
     CFGN(256, 32, 4, 1, 1), CFGN(128, 32, 4, 1, 1), CFGN(256, 32, 4, 1, 2),
     // s_setprio around the MFMA clusters (T5) on the pipelined tiles
     CFGP(256, 256, 2, 4, 2), CFGP(256, 256, 4, 2, 2), CFGP(128, 128, 2, 2, 2), CFGP(128, 64, 2, 2, 2),
+    // 256 x 128 on 8 waves for 128-channel outputs (the 3x3 convs of the second stage): 25 % fewer LDS-DMA
+    // pieces per MFMA than 128 x 128 without the half-empty 256 x 256 tile (appended: find-db indices stay)
+    CFG(256, 128, 4, 2, 1), CFG(256, 128, 4, 2, 2), CFGP(256, 128, 4, 2, 2),
     // (measured and dropped: 256 x 128 / 128 x 256 tiles with a 3-deep ring, 1028-1029 TF at 4096^3 /
     // 8192^3 against 1245 / 1151 for 256 x 256 with 2 stages - profiles/r2r_gemm_ref_3stage.txt)
 };

@@ -25,4 +25,9 @@ for spec in "fwd 128,128,3,1,1,28 1" "fwd 64,64,3,1,1,56 0" "fwd 256,256,3,1,1,1
   timeout -s KILL 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE FETCH_SIZE \
     --output-format csv -d gpurun_out/${tag}_b -o p -- $P --op $1 --shape $2 --cfg $3 > gpurun_out/${tag}_b.log 2>&1 || { tail -5 gpurun_out/${tag}_b.log; exit 1; }
 done
-echo done
+
+# re-tune every shape (the 256 x 128 configurations are new) and bench the fresh choices
+timeout -k 10 600 python bench.py --tune-db none --tune-save gpurun_out/r5e_find_db.json --warmup 8 --steps 20 > gpurun_out/r5e_retune.log 2>&1 || { tail -5 gpurun_out/r5e_retune.log; exit 1; }
+grep -h '^{"metric' gpurun_out/r5e_retune.log | cut -c80-150
+timeout -k 10 400 python bench.py --tune-db gpurun_out/r5e_find_db.json --warmup 8 --steps 20 > gpurun_out/r5e_retuned_bench.log 2>&1 || { tail -5 gpurun_out/r5e_retuned_bench.log; exit 1; }
+grep -h '^{"metric' gpurun_out/r5e_retuned_bench.log | cut -c80-150
