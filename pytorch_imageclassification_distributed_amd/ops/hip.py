@@ -976,8 +976,10 @@ def _syncbn_bwd_start(link):
         cur = torch.cuda.current_stream(dev)
         side = peer_side_stream(dev)
         side.wait_stream(cur)
+        from ..parallel import comm_timer
         with torch.cuda.stream(side):
-            pc.comm.bn_bwd(link.part, link.part_rows(), c, link.count_t, dgamma, dbeta, k)
+            with comm_timer.span("syncbn_bwd", side):
+                pc.comm.bn_bwd(link.part, link.part_rows(), c, link.count_t, dgamma, dbeta, k)
             ev = torch.cuda.Event()
             ev.record(side)
         for t in (k, link.count_t, dgamma, dbeta):
@@ -1337,15 +1339,18 @@ def _bn_coef(y, gamma, beta, bn, stats_ready, shift=None):
             C.bn_reduce_finalize(part, grp, c, float(rows), gamma, beta, *rs, mom, bn.eps, coef, shift=shift)
         else:
             pc = peer_channel(group, 0)
-            if pc is not None and c <= PEER_BN_MAX_C:  # one kernel: reduce + xGMI exchange + finalize
-                count_t = torch.empty(1, dtype=torch.float64, device=dev)
-                pc.comm.bn_fwd(part, grp, c, float(rows), gamma, beta, *rs, mom, bn.eps, coef, count_t, shift=shift)
-            else:
-                sums = torch.empty(2 * c + 1, dtype=torch.float64, device=dev)
-                C.bn_partials(part, grp, c, sums, None, None, float(rows))  # + local count in the tail
-                stats_all_reduce_(sums, group)
-                count_t = sums[2 * c:]
-                C.bn_finalize(sums, count_t, float(rows), gamma, beta, *rs, mom, bn.eps, c, coef, shift=shift)
+            from ..parallel import comm_timer
+            with comm_timer.span("syncbn_fwd"):
+                if pc is not None and c <= PEER_BN_MAX_C:  # one kernel: reduce + xGMI exchange + finalize
+                    count_t = torch.empty(1, dtype=torch.float64, device=dev)
+                    pc.comm.bn_fwd(part, grp, c, float(rows), gamma, beta, *rs, mom, bn.eps, coef, count_t,
+                                   shift=shift)
+                else:
+                    sums = torch.empty(2 * c + 1, dtype=torch.float64, device=dev)
+                    C.bn_partials(part, grp, c, sums, None, None, float(rows))  # + local count in the tail
+                    stats_all_reduce_(sums, group)
+                    count_t = sums[2 * c:]
+                    C.bn_finalize(sums, count_t, float(rows), gamma, beta, *rs, mom, bn.eps, c, coef, shift=shift)
     else:
         if stats_ready:
             raise RuntimeError("eval-mode BN received fused statistics")
@@ -1363,13 +1368,16 @@ def _bn_bwd_k(part, grp, c, rows, training, group, count_t, params, dev, coef=No
         C.bn_reduce_bwd(part, grp, c, float(rows), dgamma, dbeta, k, coef=coef if xa is not None else None, xa=xa)
         return k, dgamma, dbeta
     pc = peer_channel(group, 0) if (training and group is not None) else None
+    from ..parallel import comm_timer
     if pc is not None and count_t is not None and c <= PEER_BN_MAX_C:  # reduce + exchange + k in one kernel
-        pc.comm.bn_bwd(part, grp, c, count_t, dgamma, dbeta, k)
+        with comm_timer.span("syncbn_bwd"):
+            pc.comm.bn_bwd(part, grp, c, count_t, dgamma, dbeta, k)
     else:
         sums = torch.empty(2 * c, dtype=torch.float64, device=dev)
         C.bn_partials(part, grp, c, sums, dgamma, dbeta)
         if group is not None:
-            stats_all_reduce_(sums, group)
+            with comm_timer.span("syncbn_bwd"):
+                stats_all_reduce_(sums, group)
         if training:
             C.bn_bwd_k(sums, count_t, float(rows), c, k)
         else:  # running statistics are constants: dy = scale * dz

