@@ -126,8 +126,11 @@ class Trainer:
         self.arena = None
         self.autocast = False
         if self.dev.type == "cuda" and not self.hip:
-            # reference stack: torch DDP + SyncBatchNorm (+ bf16 autocast)
-            model = model.to(memory_format=torch.channels_last)
+            # reference stack: torch DDP + SyncBatchNorm (+ bf16 autocast).  bf16: channels-last (MIOpen's fast
+            # layout); fp32 keeps the reference's own NCHW layout - MIOpen's fp32 channels-last backward faulted
+            # the GPU on EfficientNet-B0 (illegal memory access, gpurun_out/r5e_pytest_learning.log)
+            if a.dtype != "fp32":
+                model = model.to(memory_format=torch.channels_last)
             if a.sync_bn and ctx.world_size > 1:
                 model = nn.SyncBatchNorm.convert_sync_batchnorm(model)
             self.autocast = a.dtype == "bf16"

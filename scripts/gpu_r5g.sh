@@ -9,6 +9,12 @@ export TMPDIR=/tmp
 trap 'kill $TICK' EXIT
 b() { local tag=$1; shift; timeout -k 10 400 python bench.py "$@" > gpurun_out/r5g_$tag.log 2>&1 || { tail -5 gpurun_out/r5g_$tag.log; return 1; }
       echo "$tag $(grep -h '^{"metric' gpurun_out/r5g_$tag.log | cut -c80-150)"; }
+# the full GPU suite and the driver's smoke step first (assertion failures are recorded; a timeout / crash ends it)
+timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 400 --timeout-method thread > gpurun_out/r5g_pytest_gpu.log 2>&1; rc=$?
+tail -5 gpurun_out/r5g_pytest_gpu.log
+case $rc in 0|1) ;; *) echo "gpu suite rc=$rc"; exit 1;; esac
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r5g_smoke.log 2>&1 || { tail -5 gpurun_out/r5g_smoke.log; exit 1; }
+tail -2 gpurun_out/r5g_smoke.log
 # kernel-trace breakdown of the default headline step (XA on, run-ahead throttle, retuned find-db if present)
 DB=""; [ -f tuning/mi355x_find_db_r5e.json ] && DB="--tune-db tuning/mi355x_find_db_r5e.json"
 timeout -k 10 500 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r5g_prof -o hip -- \

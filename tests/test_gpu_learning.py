@@ -44,6 +44,17 @@ def _run(model, size, compute, dtype, steps, batch, lr, train, val):
             j = (i * batch) % n
             losses.append(tr.train_step(xs[j:j + batch], ys[j:j + batch]).float())
         losses = torch.stack(losses).cpu()
+        # precise BN: the running statistics of a 100-step run lag the fast-moving weights (momentum 0.1), so
+        # validation accuracy swung 0.41-0.82 between identical runs.  One train-mode pass over 256 training
+        # images with momentum 1 sets them to those images' batch statistics, on both stacks alike.
+        bns = [m for m in tr.net.modules() if isinstance(m, torch.nn.modules.batchnorm._BatchNorm)]
+        keep = [m.momentum for m in bns]
+        for m in bns:
+            m.momentum = 1.0
+        with torch.no_grad():
+            tr.net(xs[:256])
+        for m, mom in zip(bns, keep):
+            m.momentum = mom
         tr.net.eval()
         correct = 0
         with torch.no_grad():
