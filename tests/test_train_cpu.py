@@ -105,3 +105,32 @@ def test_rng_state_roundtrip():
     restore_rng_state(st)
     b = (torch.rand(3), np.random.rand(3), random.random(), np.random.randn())
     assert torch.equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2] and a[3] == b[3]
+
+
+def test_step_throttle_bounds_steps_in_flight(monkeypatch):
+    """Trainer._throttle waits on the oldest step's end event once MAX_INFLIGHT_STEPS are enqueued (the guard
+    against the allocator growth of an unbounded host run-ahead, docs/DESIGN.md)."""
+    import collections
+    import types
+
+    from pytorch_imageclassification_distributed_amd.engine import trainer as tm
+
+    waited = []
+
+    class Ev:
+        def __init__(self, i):
+            self.i = i
+
+        def synchronize(self):
+            waited.append(self.i)
+
+    monkeypatch.setattr(tm, "MAX_INFLIGHT_STEPS", 2)
+    fake = types.SimpleNamespace(dev=types.SimpleNamespace(type="cuda"), _inflight=collections.deque())
+    for i in range(5):
+        tm.Trainer._throttle(fake)
+        assert len(fake._inflight) < 2
+        fake._inflight.append(Ev(i))  # what _step_enqueued records after the step
+    assert waited == [0, 1, 2]
+    monkeypatch.setattr(tm, "MAX_INFLIGHT_STEPS", 0)  # 0: unbounded, never waits
+    tm.Trainer._throttle(fake)
+    assert waited == [0, 1, 2]
