@@ -1,0 +1,42 @@
+"""Summarise rocprofv3 --pmc CSV passes of scripts/conv_probe.py runs (one directory per counter pass).
+
+    python scripts/pmc_summary.py gpurun_out/r5e_pmc_*_a gpurun_out/r5e_pmc_*_b
+
+Per conv kernel: MFMA utilisation (SQ_VALU_MFMA_BUSY_CYCLES over SIMD-cycles = GRBM_GUI_ACTIVE / 8 XCDs x 1024
+SIMDs), the wave-cycle split (parked on waitcnt / barrier, issue-stalled, issuing), VALU and LDS instructions
+per wave, LDS bank-conflict share.  Means over the dispatches of the kernel.
+"""
+import collections
+import csv
+import os
+import sys
+
+runs = collections.defaultdict(dict)  # probe tag -> counter -> mean
+for d in sys.argv[1:]:
+    f = os.path.join(d, "p_counter_collection.csv")
+    if not os.path.exists(f):
+        continue
+    tag = os.path.basename(d)[:-2]
+    acc = collections.defaultdict(list)
+    name = None
+    for r in csv.DictReader(open(f)):
+        k = r["Kernel_Name"]
+        if "glds_kernel" not in k and "direct_conv" not in k:
+            continue
+        name = k
+        acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    runs[tag].update({c: sum(v) / len(v) for c, v in acc.items()})
+    if name:
+        runs[tag]["kernel"] = name.replace("void (anonymous namespace)::", "").split("(")[0]
+for tag, c in sorted(runs.items()):
+    simd_cycles = c.get("GRBM_GUI_ACTIVE", 0) / 8 * 1024
+    wc = c.get("SQ_WAVE_CYCLES", 0) or 1
+    waves = c.get("SQ_WAVES", 0) or 1
+    print(f"{tag}: {c.get('kernel', '?')}")
+    if simd_cycles:
+        print(f"  MFMA busy {100 * c.get('SQ_VALU_MFMA_BUSY_CYCLES', 0) / simd_cycles:5.1f} % of SIMD-cycles")
+    print(f"  wave-cycles: parked (waitcnt / barrier) {100 * c.get('SQ_WAIT_ANY', 0) / wc:4.1f} %, issue-stalled "
+          f"{100 * c.get('SQ_WAIT_INST_ANY', 0) / wc:4.1f} % (LDS issue {100 * c.get('SQ_WAIT_INST_LDS', 0) / wc:4.1f} %), "
+          f"issuing {100 * c.get('SQ_ACTIVE_INST_ANY', 0) / wc:4.1f} %")
+    print(f"  per wave: {c.get('SQ_INSTS_VALU', 0) / waves:7.0f} VALU, {c.get('SQ_INSTS_LDS', 0) / waves:6.0f} LDS instructions; "
+          f"LDS bank-conflict cycles {100 * c.get('SQ_LDS_BANK_CONFLICT', 0) / max(c.get('SQ_LDS_IDX_ACTIVE', 1), 1):4.1f} % of LDS-active")
