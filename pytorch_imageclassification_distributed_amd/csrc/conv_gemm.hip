@@ -547,7 +547,7 @@ DEVI void glds16(const void* src, char* lds_wave_base) {
 // (1-stage ring: 3-4 blocks/CU hide latency by occupancy; 2-stage: in-block overlap).  256 x {64,128,256}
 // on 8 waves (2 per SIMD, one block per CU) keeps a deeper ring in flight across the barrier (3 stages =
 // 2 tiles ahead at BN <= 128) and halves the LDS-DMA bytes per FLOP of the 128-row tile.
-template <int TM, int BN, int WM, int WN, int STAGES, int XM = 0>
+template <int TM, int BN, int WM, int WN, int STAGES, int XM = 0, int PR = 0>
 struct GldsCfg {
   static constexpr int NW = WM * WN, NTH = 64 * NW;
   // XA / XF (XM 1 / 2): each wave's private copy of the k-step's fused BN coefficients (3 resp. 2 x 64
@@ -565,7 +565,9 @@ struct GldsCfg {
   static constexpr int EST_VGPR = (TM / WM) * (BN / WN) / 64 + 4 * (TM / WM / 16 + BN / WN / 16) +
                                   4 * (TM / 8 / NW) + 2 * (BN / 8 / NW) + 48;
   static constexpr int OCC_REG = 512 / EST_VGPR < 1 ? 1 : 512 / EST_VGPR;
-  static constexpr int OCC = OCC_LDS < OCC_REG ? OCC_LDS : OCC_REG;
+  // PR & 2 (lean): one fragment buffer instead of two, register budget of 4 waves per SIMD - more
+  // co-resident blocks to cover the 1-stage ring's load round trip (profiles/r5e_conv_pmc_b1024.txt)
+  static constexpr int OCC = (PR & 2) ? (OCC_LDS < 4 ? OCC_LDS : 4) : (OCC_LDS < OCC_REG ? OCC_LDS : OCC_REG);
 };
 
 // Buffer-resource LDS-DMA (buffer_load_dwordx4 ... lds): 32-bit byte offsets against a per-block base,
@@ -608,9 +610,11 @@ DEVI int tap_tb(int pk) { return (int)((unsigned)pk >> 16); }
 // way (no extra operand: c0 / c1 are the BN's scale / shift), so the activated tensor is never written.
 // Pieces in the zero padding stay 0 (the padding of a).
 template <int TM, int BN, int WM, int WN, int STAGES, bool TAP_UNIFORM, int PRIO = 0, int XM = 0>
-__global__ __launch_bounds__((GldsCfg<TM, BN, WM, WN, STAGES, XM>::NTH), (GldsCfg<TM, BN, WM, WN, STAGES, XM>::OCC))
+__global__ __launch_bounds__((GldsCfg<TM, BN, WM, WN, STAGES, XM, PRIO>::NTH),
+                             (GldsCfg<TM, BN, WM, WN, STAGES, XM, PRIO>::OCC))
 void conv_gemm_glds_kernel(const ConvParams p) {
-  using Cfg = GldsCfg<TM, BN, WM, WN, STAGES, XM>;
+  using Cfg = GldsCfg<TM, BN, WM, WN, STAGES, XM, PRIO>;
+  constexpr bool SETPRIO = PRIO & 1, LEAN = PRIO & 2;
   constexpr bool XA = XM == 1, XF = XM == 2;
   constexpr int NW = Cfg::NW;
   constexpr int A_BYTES = Cfg::A_BYTES;
@@ -868,6 +872,26 @@ void conv_gemm_glds_kernel(const ConvParams p) {
     }
     const char* sa = smem + (kt % STAGES) * STAGE;
     const char* sb = sa + A_BYTES;
+    if constexpr (LEAN) {
+      // one fragment set live: each k-half loads its fragments, then its MFMAs (the co-resident waves cover
+      // the LDS latency)
+      if constexpr (STAGES > 1)
+        if (kt + STAGES - 1 < nk) issue((kt + STAGES - 1) % STAGES);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 af[RM];
+#pragma unroll
+        for (int i = 0; i < RM; ++i) af[i] = *(const bf16x8*)(sa + swz(wm * WTM + i * 16 + fr, 4 * kk + fq));
+#pragma unroll
+        for (int j = 0; j < RN; ++j) {
+          const bf16x8 bfg = *(const bf16x8*)(sb + swz(wn * WTN + j * 16 + fr, 4 * kk + fq));
+#pragma unroll
+          for (int i = 0; i < RM; ++i)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg, af[i], acc[i][j], 0, 0, 0);
+        }
+      }
+      continue;
+    }
     bf16x8 af[RM], bfg[RN];
 #pragma unroll
     for (int i = 0; i < RM; ++i) af[i] = *(const bf16x8*)(sa + swz(wm * WTM + i * 16 + fr, fq));
@@ -883,7 +907,7 @@ void conv_gemm_glds_kernel(const ConvParams p) {
 #pragma unroll
         for (int i = 0; i < RM; ++i) af2[i] = *(const bf16x8*)(sa + swz(wm * WTM + i * 16 + fr, 4 + fq));
       }
-      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+      if constexpr (SETPRIO) __builtin_amdgcn_s_setprio(1);
       if constexpr (JOUT) {
 #pragma unroll
         for (int j = 0; j < RN; ++j) {
@@ -903,7 +927,7 @@ void conv_gemm_glds_kernel(const ConvParams p) {
         for (int j = 0; j < RN; ++j)
           if (kk == 0) bf2[j] = *(const bf16x8*)(sb + swz(wn * WTN + j * 16 + fr, 4 + fq));
       }
-      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+      if constexpr (SETPRIO) __builtin_amdgcn_s_setprio(0);
       if (kk == 0) {
 #pragma unroll
         for (int i = 0; i < RM; ++i) af[i] = af2[i];
@@ -1777,6 +1801,9 @@ struct ConvCfg {
   {TM, BN, WM, WN, ST, &launch_glds<TM, BN, WM, WN, ST, 1>, &launch_glds_xa<TM, BN, WM, WN, ST, 1>,      \
    &launch_glds_xf<TM, BN, WM, WN, ST, 1>}
 #define CFGN(TM, BN, WM, WN, ST) {TM, BN, WM, WN, ST, &launch_glds<TM, BN, WM, WN, ST>, nullptr, nullptr}
+#define CFGL(TM, BN, WM, WN, ST)                                                                          \
+  {TM, BN, WM, WN, ST, &launch_glds<TM, BN, WM, WN, ST, 2>, &launch_glds_xa<TM, BN, WM, WN, ST, 2>,      \
+   &launch_glds_xf<TM, BN, WM, WN, ST, 2>}
 // Measured on the ResNet-50 layers at batch 512 (benchmarks/conv_bench.py --tune-log): the 128-row
 // 4-wave tiles win on 64/128-channel outputs and short K (occupancy hides latency); the 256x256
 // 8-wave tiles (2 waves per SIMD, 64x128 or 128x64 per wave, half the LDS-DMA bytes per FLOP) win
@@ -1791,12 +1818,16 @@ static const ConvCfg g_cfgs[] = {
     // 256 x 128 on 8 waves for 128-channel outputs (the 3x3 convs of the second stage): 25 % fewer LDS-DMA
     // pieces per MFMA than 128 x 128 without the half-empty 256 x 256 tile (appended: find-db indices stay)
     CFG(256, 128, 4, 2, 1), CFG(256, 128, 4, 2, 2), CFGP(256, 128, 4, 2, 2),
+    // 1-stage 128 x 128 on 8 waves (64 x 32 per wave): 4 waves per SIMD instead of the 4-wave tile's 3, more
+    // loads in flight per CU for the same LDS-DMA bytes per block (profiles/r5e_conv_pmc_b1024.txt)
+    CFG(128, 128, 4, 2, 1), CFG(128, 128, 2, 4, 1), CFGL(128, 128, 2, 2, 1),
     // (measured and dropped: 256 x 128 / 128 x 256 tiles with a 3-deep ring, 1028-1029 TF at 4096^3 /
     // 8192^3 against 1245 / 1151 for 256 x 256 with 2 stages - profiles/r2r_gemm_ref_3stage.txt)
 };
 #undef CFG
 #undef CFGP
 #undef CFGN
+#undef CFGL
 constexpr int kNumCfgs = sizeof(g_cfgs) / sizeof(g_cfgs[0]);
 
 int conv_num_cfgs() { return kNumCfgs; }

@@ -15,6 +15,15 @@ tail -5 gpurun_out/r5g_pytest_gpu.log
 case $rc in 0|1) ;; *) echo "gpu suite rc=$rc"; exit 1;; esac
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r5g_smoke.log 2>&1 || { tail -5 gpurun_out/r5g_smoke.log; exit 1; }
 tail -2 gpurun_out/r5g_smoke.log
+# the new 1-stage 128 x 128 variants (8 waves: cfg 18 / 19; lean 4-wave at occupancy 4: cfg 20) against cfg 1
+for shape in 128,128,3,1,1,28 256,256,3,1,1,14 64,64,3,1,1,56 512,512,3,1,1,7; do
+  for c in 1 18 19 20; do
+    timeout -k 10 120 python3 scripts/conv_probe.py --batch 1024 --iters 10 --op fwd --shape $shape --cfg $c 2>&1 | grep -h " us " || exit 1
+  done
+  for c in 1 18 20; do
+    timeout -k 10 120 python3 scripts/conv_probe.py --batch 1024 --iters 10 --op dgrad --shape $shape --cfg $c 2>&1 | grep -h " us " || exit 1
+  done
+done | tee gpurun_out/r5g_cfg_probe.txt
 # kernel-trace breakdown of the default headline step (XA on, run-ahead throttle, retuned find-db if present)
 DB=""; [ -f tuning/mi355x_find_db_r5e.json ] && DB="--tune-db tuning/mi355x_find_db_r5e.json"
 timeout -k 10 500 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r5g_prof -o hip -- \
