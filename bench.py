@@ -29,6 +29,7 @@ import torch.distributed as dist
 
 from pytorch_imageclassification_distributed_amd.data import DeviceSyntheticLoader, HostSyntheticLoader
 from pytorch_imageclassification_distributed_amd.engine import Trainer, build_parser
+from pytorch_imageclassification_distributed_amd.engine.config import GRAPH_AUTO_MAX_BATCH
 from pytorch_imageclassification_distributed_amd.parallel import barrier, destroy, init_distributed
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -60,8 +61,9 @@ def parse():
                    "(default: $IMGCLS_TUNE_DB, else tuning/mi355x_find_db.json; 'none' disables); shapes it "
                    "does not list are still timed")
     p.add_argument("--tune-save", default="", help="write the kernel choices of this run to this file")
-    p.add_argument("--graph", default="off", choices=["on", "off"],
-                   help="replay the whole training step as one captured HIP graph (single process)")
+    p.add_argument("--graph", default="auto", choices=["on", "off", "auto"],
+                   help="replay the whole training step as one captured HIP graph (single process); auto = on "
+                        "at per-GPU batch <= 64 (host-bound steps, train.py --hip-graph auto)")
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
                    help="fp8 (experimental): MX-FP8 forward convolutions only, bf16 backward - measured "
                         "+0.3 %% over bf16 at b1024, not a speed-up (README)")
@@ -152,7 +154,8 @@ def main():
                                      steps=a.warmup + a.steps, ring=2, seed=1234 + ctx.rank)
         batches = list(iter(data))
 
-    use_graph = a.graph == "on" and a.compute == "hip" and ctx.world_size == 1
+    use_graph = a.compute == "hip" and ctx.world_size == 1 and (
+        a.graph == "on" or (a.graph == "auto" and a.batch <= GRAPH_AUTO_MAX_BATCH))
 
     def step(i):
         b = next(host_it) if a.data == "host" else batches[i]

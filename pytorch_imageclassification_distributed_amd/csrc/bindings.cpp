@@ -193,7 +193,9 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
   TORCH_CHECK(stages >= 0 && stages <= 3, "conv_gemm: stages must be 0 (auto), 1, 2 or 3");
   p.stages = stages;
   TORCH_CHECK(tile_n == 0 || tile_n == 64 || tile_n == 128, "conv_gemm: tile_n must be 0, 64 or 128");
-  TORCH_CHECK(cfg >= -1 && cfg < (fp8 ? conv_num_fp8_cfgs() : conv_num_cfgs()), "conv_gemm: cfg out of range");
+  TORCH_CHECK((cfg >= -1 && cfg < (fp8 ? conv_num_fp8_cfgs() : conv_num_cfgs())) ||
+                  (!fp8 && cfg >= CONV_HALO_BASE && cfg < CONV_HALO_BASE + conv_halo_num()),
+              "conv_gemm: cfg out of range");
   p.tile_n = tile_n;
   p.cfg = cfg;
   if (fp8) {
@@ -922,6 +924,15 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_cfg_has_xa", &conv_cfg_has_xa);
   m.def("conv_wgrad_has_xa", &conv_wgrad_has_xa);
   m.def("conv_wgrad_has_xf", &conv_wgrad_has_xf);
+  m.def("conv_halo_cfgs", []() {
+    std::vector<std::vector<int>> out;
+    for (int i = 0; i < conv_halo_num(); ++i) {
+      std::vector<int> c(6);
+      conv_halo_info(i, c.data());
+      out.push_back(c);
+    }
+    return out;
+  });
   m.def("conv_cfgs", []() {
     std::vector<std::vector<int>> out;
     for (int i = 0; i < conv_num_cfgs(); ++i) {

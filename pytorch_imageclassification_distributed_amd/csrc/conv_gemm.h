@@ -99,6 +99,11 @@ int conv_num_fp8_cfgs();
 void conv_fp8_cfg_info(int i, int* out5);
 void conv_cfg_info(int i, int* out5);  // {tile rows, tile channels, waves M, waves N, ring depth}
 bool conv_cfg_has_xa(int i);           // configuration i has fused BN-backward / BN-apply A-operand variants
+// halo-patch kernel (conv_halo.hip): ConvParams::cfg >= CONV_HALO_BASE selects entry cfg - CONV_HALO_BASE
+#define CONV_HALO_BASE 1000
+int conv_halo_num();
+void conv_halo_info(int i, int* out6);  // {tile rows, tile channels, waves M, waves N, weight ring depth, patch rows}
+int conv_halo_launch(int i, const ConvParams& p, hipStream_t stream);  // 3: geometry not handled
 int conv_wgrad_launch(const WgradParams& p, int splits, hipStream_t stream);
 bool conv_wgrad_has_xa(int stages);  // the wgrad variant selected by ``stages`` has a fused BN-backward dY form
 bool conv_wgrad_has_xf(int stages);  // ... a fused BN-apply X form (alone or together with the dY form)

@@ -14,6 +14,7 @@ from __future__ import annotations
 import argparse
 
 REF_CLASS_WEIGHTS = (3.0, 3.0, 10.0, 1.0, 4.0, 4.0, 5.0)
+GRAPH_AUTO_MAX_BATCH = 64  # --hip-graph auto: largest per-GPU batch that replays the step as a graph
 
 
 def build_parser() -> argparse.ArgumentParser:
@@ -79,10 +80,22 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--deterministic", action="store_true",
                    help="bitwise-reproducible GPU kernels (no split-K / cross-block fp32 atomics; slower)")
     p.add_argument("--timeout-min", type=float, default=10.0, help="process-group timeout (minutes)")
-    p.add_argument("--hip-graph", action="store_true",
+    p.add_argument("--hip-graph", nargs="?", const="on", default="auto", choices=["on", "off", "auto"],
                    help="single GPU: capture the whole training step once and replay it as one HIP graph "
-                        "(host-bound models: Inception-v3, EfficientNet); a batch of another shape runs eagerly")
+                        "(host-bound steps); a batch of another shape runs eagerly.  auto = on at per-GPU "
+                        f"batch <= {GRAPH_AUTO_MAX_BATCH} (Inception-v3 @299: b4 466 vs 164 img/s eager, b32 "
+                        "2943 vs 1978; at b128 eager wins, profiles/r6_bench_host_data_and_inception_small_batch.jsonl)")
     return p
+
+
+def hip_graph_enabled(args, world_size: int) -> bool:
+    """Whether ``--hip-graph`` (on / off / auto) replays the training step as a HIP graph."""
+    mode = getattr(args, "hip_graph", "off")
+    if mode is True:
+        mode = "on"
+    if mode in (False, None, "off") or world_size != 1:
+        return False
+    return mode == "on" or args.batchsize <= GRAPH_AUTO_MAX_BATCH
 
 
 def parse_class_weights(spec: str, num_classes: int):

@@ -42,7 +42,7 @@ from ..parallel import GradReducer, check_peer_errors, comm_timer, convert_sync_
 from ..utils import (BEST, LATEST, AccuracyCounter, DeviceMeter, JsonlLogger, load_checkpoint,
                      load_model_state, resolve_resume, restore_rng_state, save_checkpoint)
 from ..utils.timers import PhaseTimer
-from .config import parse_class_weights
+from .config import hip_graph_enabled, parse_class_weights
 from .optim import FusedAdam, MultiStepLR
 
 # training steps the host may have enqueued ahead of the GPU (Trainer._throttle; 0 = unbounded)
@@ -282,8 +282,7 @@ class Trainer:
         counted per process, so a resumed run warms up too), then capture once - on a full batch of the
         loader's batch size, never on an epoch's short last batch - and replay; a batch of another shape
         runs eagerly."""
-        use = (getattr(self.args, "hip_graph", False) and self.hip and self.ctx.world_size == 1
-               and not self._prof)
+        use = hip_graph_enabled(self.args, self.ctx.world_size) and self.hip and not self._prof
         if use:
             if self._graph is not None:
                 if self._g_x.shape == images.shape and self._g_y.shape == labels.shape:

@@ -447,8 +447,11 @@ def load_tuning(path: str) -> int:
         except (ValueError, SyntaxError, TypeError):
             continue
         fp8 = bool(k[10]) if len(k) > 10 else False
-        ok = (v[2] - DIRECT_BASE in DIRECT_CFGS if v[2] >= DIRECT_BASE else
-              v[2] < (nfp8 if fp8 else ncfg)) and len(v) == 3
+        if v[2] >= HALO_BASE:
+            ok = not fp8 and v[2] - HALO_BASE < len(conv_halo_cfgs()) and len(v) == 3
+        else:
+            ok = (v[2] - DIRECT_BASE in DIRECT_CFGS if v[2] >= DIRECT_BASE else
+                  v[2] < (nfp8 if fp8 else ncfg)) and len(v) == 3
         if ok and k not in _STAGES_TUNED:
             _STAGES_TUNED[k] = v
             n += 1
@@ -482,6 +485,9 @@ def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(
     if DIRECT_FORCE is not None and not fused and \
             _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales) is not None:
         cfg = (0, 0, DIRECT_BASE + DIRECT_FORCE)  # (tests) every eligible launch on this direct variant
+    elif HALO_FORCE is not None and not fused and scales[0] is None and \
+            _halo_ok(geo, dh, dw, *conv_halo_cfgs()[HALO_FORCE][::5]):
+        cfg = (0, 0, HALO_BASE + HALO_FORCE)  # (tests) every eligible launch on this halo variant
     elif CONV_FORCE_CFG is not None and scales[0] is None and (not fused or C.conv_cfg_has_xa(CONV_FORCE_CFG[2])):
         cfg = CONV_FORCE_CFG
     elif CONV_FORCE_FP8_CFG is not None and scales[0] is not None:
@@ -498,7 +504,9 @@ def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(
                 A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups, scales, xa, xf)
             if cfg[0] or cfg[2] >= 0:
                 _STAGES_TUNED[key] = cfg
-    if cfg[2] >= DIRECT_BASE:
+    if cfg[2] >= HALO_BASE:
+        HALO_COUNT[0] += 1
+    elif cfg[2] >= DIRECT_BASE:
         _direct_launch(A, B, out, stats, groups, _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales),
                        cfg[2] - DIRECT_BASE, bwd, shift)
         return
@@ -515,6 +523,36 @@ def conv_cfgs():
     if _CFGS is None:
         _CFGS = [tuple(c) for c in C.conv_cfgs()]
     return _CFGS
+
+
+_HALO_CFGS = None
+HALO_CONV = os.environ.get("IMGCLS_HALO", "1") == "1"  # halo-patch 3x3 kernels as tuner candidates
+# entries the tuner times: only the 256 x 256 tile beat the LDS-DMA implicit GEMM on a ResNet-50 b1024 shape
+# (512-channel 7x7: 266 vs 279 us); the others lost 1.3-2x (profiles/r6b_halo_probe_b1024.txt)
+HALO_TUNE = tuple(int(v) for v in os.environ.get("IMGCLS_HALO_TUNE", "6").split(",") if v)
+HALO_FORCE = None  # tests: force a halo variant on every eligible launch
+HALO_COUNT = [0]   # halo-kernel launches (tests)
+HALO_BASE = 1000   # cfg[2] >= HALO_BASE: the halo-patch kernel (csrc/conv_halo.hip), entry cfg - base
+
+
+def conv_halo_cfgs():
+    """The halo-patch kernel's table: (tile rows, tile channels, waves M, waves N, weight ring, patch rows)."""
+    global _HALO_CFGS
+    if _HALO_CFGS is None:
+        _HALO_CFGS = [tuple(c) for c in C.conv_halo_cfgs()]
+    return _HALO_CFGS
+
+
+def _halo_ok(geo, dh, dw, tm, pmax):
+    """The launch is a stride-1 GEMM whose taps lie in a 3x3 window over an input grid of the output's size
+    (3x3 same-padded forward convs, stride-1 data gradients) and the tile's patch fits ``pmax`` rows - the
+    same test as csrc/conv_halo.hip::halo_geometry."""
+    m, _co, k, ca, gh, gw, ih, iw, sa = geo[:9]
+    if ca % 64 or sa != 1 or gh != ih or gw != iw or not 2 <= len(dh) <= 9 or k != len(dh) * ca:
+        return False
+    if m % (ih * iw) or any(abs(v) > 1 for v in dh) or any(abs(v) > 1 for v in dw):
+        return False
+    return tm + 2 * iw + 2 <= pmax and pmax * ca * 2 < (1 << 30)
 
 
 _FP8_CFGS = None
@@ -617,6 +655,14 @@ def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, group
     for cfg in cands:
         times[cfg] = _time_ms(lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, groups, zero,
                                                   addend, *bwd, *cfg, *scales, *xa3, None, *xf2))
+    if HALO_CONV and not fused and scales[0] is None:
+        for v, (tm, bn, _wm, _wn, _bst, pmax) in enumerate(conv_halo_cfgs()):
+            if v not in HALO_TUNE or not _halo_ok(geo, dh, dw, tm, pmax) or (bn > 64 and bn >= 2 * geo[1]) or \
+                    (bn == 64 and geo[1] >= 256) or geo[0] < tm * 16:
+                continue
+            cfg = (0, 0, HALO_BASE + v)
+            times[cfg] = _time_ms(lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, groups, zero,
+                                                      addend, *bwd, *cfg, *scales, *xa3, None, *xf2))
     dg = _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales) if not fused else None
     if dg is not None:
         for v, (cip, cot) in DIRECT_CFGS.items():

@@ -3,6 +3,7 @@
     python scripts/conv_probe.py --shape 128,128,3,1,1,28 --batch 1024 --op fwd --cfg 1 --iters 20
 
 ``--cfg``: index into ``ops.hip.conv_cfgs()`` (fwd / dgrad), forced for every launch (-1: tuned choice);
+``--halo``: index into ``ops.hip.conv_halo_cfgs()`` instead (the halo-patch kernel; stride-1 3x3 window);
 ``--op``: fwd | dgrad | wgrad (wgrad: ``--wstages`` forces the ring / tile variant).  Prints the mean
 time per launch and the TF/s of the GEMM.  Synthetic bf16 data, random weights.
 """
@@ -24,6 +25,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--op", default="fwd", choices=["fwd", "dgrad", "wgrad"])
     ap.add_argument("--cfg", type=int, default=-1)
+    ap.add_argument("--halo", type=int, default=-1)
     ap.add_argument("--wstages", type=int, default=0)
     ap.add_argument("--iters", type=int, default=20)
     a = ap.parse_args()
@@ -35,6 +37,8 @@ def main():
     x = torch.randn(a.batch, cin, h, h, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     if a.cfg >= 0:
         hip.CONV_FORCE_CFG = (0, 0, a.cfg)
+    if a.halo >= 0:
+        hip.HALO_FORCE = a.halo
     if a.wstages:
         hip.WGRAD_STAGES = a.wstages
     hip.ensure_channels_last_weight(conv)
@@ -61,7 +65,8 @@ def main():
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.iters
     flops = 2.0 * g.N * g.OH * g.OW * cout * g.T * cin
-    print(f"{a.op} shape {a.shape} b{a.batch} cfg {a.cfg}: {ms * 1e3:.1f} us  {flops / ms / 1e9:.0f} TF/s", flush=True)
+    tag = f"halo {a.halo}" if a.halo >= 0 else f"cfg {a.cfg}"
+    print(f"{a.op} shape {a.shape} b{a.batch} {tag}: {ms * 1e3:.1f} us  {flops / ms / 1e9:.0f} TF/s", flush=True)
 
 
 if __name__ == "__main__":

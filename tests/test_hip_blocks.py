@@ -9,12 +9,30 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
+class _SameState:
+    """Restores a module's buffers (BN running statistics, batch counters) before every run.  Train-mode
+    passes update the running mean, and the HIP BN kernels sum their statistics about it (the shifted-data
+    pivot), so two passes compared against each other must start from the same buffers - otherwise they
+    differ by the pivot's rounding, which random-init BatchNorm stacks amplify."""
+
+    def __init__(self, module):
+        self.m = module
+        self.saved = [b.detach().clone() for b in module.buffers()]
+
+    def __call__(self):
+        with torch.no_grad():
+            for b, s in zip(self.m.buffers(), self.saved):
+                b.copy_(s)
+
+
 def _grads(block, x, use_slots):
     """use_slots=False: no paired slots and no BN-backward fusion (plain autograd accumulation +
     standalone BN reduce kernel) - the reference the fused path must match."""
     from pytorch_imageclassification_distributed_amd.ops import functional as Fx
     from pytorch_imageclassification_distributed_amd.ops import hip
     orig, orig_fuse = Fx.grad_slot, hip.FUSE_BN_BWD
+    block._imgcls_same_state = getattr(block, "_imgcls_same_state", None) or _SameState(block)
+    block._imgcls_same_state()
     if not use_slots:
         Fx.grad_slot = lambda t, n=2: None
         hip.FUSE_BN_BWD = False
@@ -87,7 +105,10 @@ def test_grad_arena(model_name):
     params = [p for p in m.parameters() if p.requires_grad]
     names = [n for n, p in m.named_parameters() if p.requires_grad]
 
+    same = _SameState(m)
+
     def loss_fn():
+        same()
         torch.manual_seed(1)  # same dropout / drop-connect masks every call
         return m(x).float().square().mean()
 
@@ -133,8 +154,10 @@ def test_deterministic_mode(model_name):
     torch.manual_seed(0)
     m = Classifier(model_name, 5).to(DEV).to(memory_format=torch.channels_last).train()
     x = torch.randn(4, 3, 96, 96, device=DEV)
+    same = _SameState(m)
 
     def run():
+        same()
         for p in m.parameters():
             p.grad = None
         torch.manual_seed(1)
@@ -237,8 +260,10 @@ def test_inception_concat_in_place(kind):
                     "E": (I.InceptionE(1280), 1280, 5)}[kind]
     blk = blk.to(DEV).to(memory_format=torch.channels_last)
     x = torch.randn(4, cin, hw, hw, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    same = _SameState(blk)
 
     def run(inplace):
+        same()
         keep, hip.CONCAT_INPLACE = hip.CONCAT_INPLACE, inplace
         try:
             for p in blk.parameters():

@@ -115,6 +115,53 @@ def test_conv_tile_configs(case, cfg):
         hip.CONV_FORCE_CFG = keep
 
 
+N_HALO = _table_len("conv_halo_cfgs", 12)
+HALO_CASES = [
+    CONV_CASES[1],                             # 64 ch, 56 x 56 (W = 56: the 384-row patches only)
+    CONV_CASES[6],                             # 512 ch, 7 x 7: a tile spans many images
+    (2, 128, 15, 13, 128, (3, 3), 1, (1, 1)),  # odd map: rows wrap mid-tile, partial last tile
+    (2, 128, 28, 28, 96, (3, 3), 1, (1, 1)),   # partial output-channel tile
+    (2, 64, 8, 8, 64, (1, 3), 1, (0, 1)),      # Inception 1x3 (3 taps in a row)
+    (2, 64, 8, 8, 64, (3, 1), 1, (1, 0)),      # ... and 3x1
+]
+
+
+@pytest.mark.parametrize("cfg", range(N_HALO))
+@pytest.mark.parametrize("case", HALO_CASES)
+def test_conv_halo_configs(case, cfg):
+    """Every halo-patch configuration (csrc/conv_halo.hip) forced on the stride-1 3x3-window convs it
+    accepts: forward and the stride-1 data gradient against the fp32 reference, and the kernel ran."""
+    hip = _hip()
+    if cfg >= len(hip.conv_halo_cfgs()):
+        pytest.skip("past the configuration table")
+    keep, hip.HALO_FORCE = hip.HALO_FORCE, cfg
+    before = hip.HALO_COUNT[0]
+    try:
+        test_conv_fwd_bwd(case)
+    finally:
+        hip.HALO_FORCE = keep
+    tm, pmax, w = hip.conv_halo_cfgs()[cfg][0], hip.conv_halo_cfgs()[cfg][5], case[3]
+    if tm + 2 * w + 2 <= pmax:  # the data gradient (K = taps x Cout) qualifies when Cout % 64 == 0
+        expect = 1 + (case[4] % 64 == 0)
+        assert hip.HALO_COUNT[0] - before >= expect, "halo kernel not launched"
+
+
+@pytest.mark.parametrize("cfg", range(N_HALO))
+@pytest.mark.parametrize("act,use_res", [("relu", True), ("silu", False)])
+def test_conv_bn_act_halo(act, use_res, cfg):
+    """Fused epilogues (BN statistics, residual, BN-backward link) on every halo configuration."""
+    hip = _hip()
+    if cfg >= len(hip.conv_halo_cfgs()):
+        pytest.skip("past the configuration table")
+    keep, hip.HALO_FORCE = hip.HALO_FORCE, cfg
+    before = hip.HALO_COUNT[0]
+    try:
+        test_conv_bn_act(act, use_res)
+    finally:
+        hip.HALO_FORCE = keep
+    assert hip.HALO_COUNT[0] > before
+
+
 @pytest.mark.parametrize("case,stages", [
     (c, st) for c in [CONV_CASES[i] for i in (0, 1, 3, 4, 5, 6, 7, 8, 12, 13, 14)] for st in (1, 2, 3, 4, 5, 6, 7, 8, 9)
     if _wgrad_stage_ok(c, st)])
