@@ -958,10 +958,11 @@ def conv_wgrad_raw(dy, x, w_param, g: ConvGeom, xa=None, xf=None):
     full = torch.zeros(g.Co * ntot, dtype=torch.float32, device=dev)
     dw = arena_slot(w_param)
     if dw is not None:
-        def launch():
-            _wgrad_launch(dy, x, full, g, m, ntot, kps, splits, stages)
-            C.grad_unpad(full, dw, g.Co * g.T, g.Cx, g.Ci)
-        _on_side(dev, launch, dy, x, full)
+        # padded input channels = the network's input layer, the last weight gradient of backward: on the
+        # compute stream (idle by then) it runs beside the side stream's backlog instead of behind it - the
+        # ResNet-50 b1024 stem wgrad is ~0.7 ms of the step tail (profiles/r5e_conv_roofline_b1024.txt)
+        _wgrad_launch(dy, x, full, g, m, ntot, kps, splits, stages)
+        C.grad_unpad(full, dw, g.Co * g.T, g.Cx, g.Ci)
         return dw
     _wgrad_launch(dy, x, full, g, m, ntot, kps, splits, stages)
     dw = grad_buffer(w_param, zero=False)

@@ -166,8 +166,15 @@ def setup_peer_syncbn(group, device: torch.device, mode: str = "auto") -> bool:
         for _ in range(2):  # forward (compute stream) and backward (side stream) channels
             chans.append(PeerAllReduce(group, device, tmo))
         check_s = float(os.environ.get("IMGCLS_PEER_CHECK_TIMEOUT_S", "15"))
-        ok = all([c.self_check(check_s, tmo) for c in chans])
+        ok, err = True, None
+        for c in chans:
+            try:  # a local exception (launch error, ...) is a failed check: this rank still reaches _agree
+                ok = c.self_check(check_s, tmo) and ok
+            except Exception as e:  # noqa: BLE001
+                ok, err = False, e
         if not _agree(ok, group, device):  # every rank must agree, or ranks would mix transports
+            if err is not None:
+                raise RuntimeError(f"self-check raised on this rank: {err}") from err
             raise RuntimeError("self-check failed on some rank")
     except Exception as e:  # noqa: BLE001 - any failure means the torch.distributed path
         for c in chans:  # channels already mapped (a failure in the second one leaks none)
