@@ -1304,13 +1304,10 @@ class StemS2dFn(torch.autograd.Function):
             slot = arena_slot(w)
             dw = slot if slot is not None else grad_buffer(w, zero=False)
 
-            def launch():
-                _wgrad_launch(dy, xs, full, g, m, ntot, kps, splits, stages)
-                dw.permute(0, 2, 3, 1).reshape(g.Co, 147).copy_(full.view(g.Co, ntot)[:, idx])
-            if slot is not None:
-                _on_side(dy.device, launch, dy, xs, full)
-            else:
-                launch()
+            # the last weight gradient of backward: on the compute stream (idle by then) it runs beside the
+            # side stream's backlog instead of behind it (conv_wgrad_raw, padded-channel path)
+            _wgrad_launch(dy, xs, full, g, m, ntot, kps, splits, stages)
+            dw.permute(0, 2, 3, 1).reshape(g.Co, 147).copy_(full.view(g.Co, ntot)[:, idx])
         return None, dw, None, None, None
 
 
