@@ -55,6 +55,8 @@ def parse():
     p.add_argument("--syncbn-comm", default="auto", choices=["auto", "peer", "rccl"],
                    help="SyncBN statistics transport (parallel/peer.py): one-shot xGMI peer kernel or RCCL")
     p.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
+    p.add_argument("--comm-backend", default="pg", choices=["pg", "rccl"],
+                   help="gradient all-reduce through ProcessGroupNCCL (pg) or the native C++ RCCL communicator")
     p.add_argument("--dist-backend", default="auto", help="auto (RCCL) | gloo (functional multi-rank runs on one GPU)")
     p.add_argument("--profile-steps", type=int, default=0)
     p.add_argument("--tune-db", default="", help="kernel-choice find-db to seed the per-shape tuner with "
@@ -131,7 +133,7 @@ def main():
         "--synthetic", "--model", a.model, "--image-size", str(a.image_size),
         "--batchsize", str(a.batch), "--num-classes", str(a.num_classes),
         "--num-workers", "0", "--synthetic-train-size", "8", "--synthetic-val-size", "8",
-        "--compute", a.compute, "--bucket-mb", str(a.bucket_mb), "--comm-dtype", a.comm_dtype,
+        "--compute", a.compute, "--bucket-mb", str(a.bucket_mb), "--comm-dtype", a.comm_dtype, "--comm-backend", a.comm_backend,
         "--lr", "1e-4", "--dtype", a.dtype, "--syncbn-comm", a.syncbn_comm,
     ] + ([] if sync_bn else ["--no-sync-bn"]))
     if ctx.device.type == "cuda":
@@ -236,6 +238,7 @@ def main():
                        "num_classes": a.num_classes, "parallelism": f"dp{ctx.world_size}",
                        "sync_bn": sync_bn, "syncbn_comm": ("peer" if tr.syncbn_peer else "rccl") if sync_bn else None,
                        "compute": a.compute, "optimizer": "adam", "hip_graph": use_graph,
+                       "grad_comm": (a.comm_backend if ctx.world_size > 1 else None),
                        "final_loss": round(loss_val, 5)},
             **extra,
         }), flush=True)

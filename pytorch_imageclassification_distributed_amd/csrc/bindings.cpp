@@ -18,6 +18,18 @@ extern int g_imgcls_det;  // misc.hip: deterministic mode
 using at::Tensor;
 using OT = std::optional<Tensor>;
 
+// ---- native RCCL communicator (rccl_comm.cpp) ----
+int rccl_load(const char*);
+const char* rccl_last_error();
+int rccl_version();
+int rccl_unique_id(char*, int);
+int rccl_comm_init(const char*, int, int, int, int, int64_t*);
+int rccl_all_reduce(int64_t, void*, size_t, int, int, hipStream_t);
+int rccl_broadcast(int64_t, void*, size_t, int, int, hipStream_t);
+int rccl_group(bool);
+int rccl_async_error(int64_t);
+int rccl_comm_close(int64_t, bool);
+
 // ---- launcher prototypes (defined in *.hip) ----
 int bn_partials_launch(float*, int, int, double*, float*, float*, double, hipStream_t);
 int bn_reduce_finalize_launch(float*, int, int, double, const float*, const float*, float*, float*, long long*, float,
@@ -840,7 +852,61 @@ void register_loader(pybind11::module& m);  // loader.cpp: native image-folder l
 void bn_set_reduce_blocks(int n, int chb);
 void bn_set_unroll(int v);  // bn.hip: target blocks / channel lanes of the row reductions
 
+static void rccl_check(int r, const char* what) {
+  TORCH_CHECK(r == 0, what, ": ", rccl_last_error(), " (code ", r, ")");
+}
+
+static int rccl_dtype(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return 0;
+    case at::kBFloat16: return 1;
+    case at::kDouble: return 2;
+    case at::kInt: return 3;
+    case at::kLong: return 4;
+    case at::kHalf: return 5;
+    default: TORCH_CHECK(false, "rccl: unsupported dtype ", t.scalar_type());
+  }
+  return -1;
+}
+
+static hipStream_t rccl_stream(int64_t stream, const Tensor& t) {
+  return stream ? (hipStream_t)stream : c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+static void rccl_bind(pybind11::module_& m) {
+  m.def("rccl_load", [](const std::string& path) { rccl_check(rccl_load(path.c_str()), "rccl_load"); });
+  m.def("rccl_version", &rccl_version);
+  m.def("rccl_unique_id", []() {
+    char id[128];
+    rccl_check(rccl_unique_id(id, 128), "ncclGetUniqueId");
+    return pybind11::bytes(id, 128);
+  });
+  m.def("rccl_comm_init", [](const std::string& uid, int nranks, int rank, int device) {
+    TORCH_CHECK(uid.size() == 128, "rccl_comm_init: the unique id is 128 bytes");
+    int64_t h = 0;
+    rccl_check(rccl_comm_init(uid.data(), 128, nranks, rank, device, &h), "ncclCommInitRank");
+    return h;
+  });
+  // in-place all-reduce / broadcast of a contiguous CUDA tensor on ``stream`` (raw hipStream_t; 0 = current)
+  m.def("rccl_all_reduce", [](int64_t h, Tensor t, int op, int64_t stream) {
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "rccl_all_reduce: contiguous device tensor");
+    rccl_check(rccl_all_reduce(h, t.data_ptr(), (size_t)t.numel(), rccl_dtype(t), op, rccl_stream(stream, t)),
+               "ncclAllReduce");
+  });
+  m.def("rccl_broadcast", [](int64_t h, Tensor t, int root, int64_t stream) {
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "rccl_broadcast: contiguous device tensor");
+    rccl_check(rccl_broadcast(h, t.data_ptr(), (size_t)t.numel(), rccl_dtype(t), root, rccl_stream(stream, t)),
+               "ncclBroadcast");
+  });
+  m.def("rccl_group_start", []() { rccl_check(rccl_group(true), "ncclGroupStart"); });
+  m.def("rccl_group_end", []() { rccl_check(rccl_group(false), "ncclGroupEnd"); });
+  m.def("rccl_async_error", &rccl_async_error);
+  m.def("rccl_last_error", []() { return std::string(rccl_last_error()); });
+  m.def("rccl_comm_close", [](int64_t h, bool abort) { rccl_check(rccl_comm_close(h, abort), "ncclCommDestroy"); });
+}
+
 PYBIND11_MODULE(_C, m) {
+  rccl_bind(m);
   m.doc() = "gfx950 (MI355X) HIP kernels for pytorch_imageclassification_distributed_amd";
   m.def("conv_gemm", &conv_gemm);
   m.def("conv_wgrad", &conv_wgrad, pybind11::arg("dY"), pybind11::arg("X"), pybind11::arg("dW"), pybind11::arg("M"),

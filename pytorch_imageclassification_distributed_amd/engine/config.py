@@ -59,6 +59,9 @@ def build_parser() -> argparse.ArgumentParser:
                         "torch.distributed / RCCL (rccl), or peer when all ranks share a host and it self-checks (auto)")
     p.add_argument("--bucket-mb", type=float, default=32.0)
     p.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
+    p.add_argument("--comm-backend", default="pg", choices=["pg", "rccl"],
+                   help="gradient buckets: torch.distributed's ProcessGroupNCCL (pg) or our C++ RCCL communicator "
+                        "(rccl: one comm stream behind the weight-gradient stream, parallel/rccl.py)")
     p.add_argument("--steps-per-epoch", type=int, default=None, help="cap on train steps per epoch")
     p.add_argument("--val-steps", type=int, default=None, help="cap on validation steps")
     p.add_argument("--resume", default="best",

@@ -154,7 +154,8 @@ class Trainer:
                     grp, self.dev, getattr(a, "syncbn_comm", "auto"))
             if ctx.world_size > 1:
                 comm = torch.bfloat16 if a.comm_dtype == "bf16" else None
-                self.reducer = GradReducer(model, bucket_cap_mb=a.bucket_mb, comm_dtype=comm)
+                self.reducer = GradReducer(model, bucket_cap_mb=a.bucket_mb, comm_dtype=comm,
+                                           comm=getattr(a, "comm_backend", "pg") if self.dev.type == "cuda" else "pg")
                 self.arena = self.reducer.arena
             elif self.hip:
                 params = [p for p in model.parameters() if p.requires_grad]

@@ -28,6 +28,11 @@ MI355X design:
   bucket is kept small (1 MiB) so communication starts early in backward.
 * optional bf16 gradient transport (``comm_dtype=torch.bfloat16``) halves the
   xGMI bytes.
+* ``comm="rccl"``: the buckets go through our own C++ RCCL communicator
+  (``parallel/rccl.py``) instead of ProcessGroupNCCL - each collective is enqueued
+  on one dedicated high-priority comm stream straight behind the weight-gradient
+  side stream (no Work objects, no per-collective event bookkeeping), and
+  ``finish()`` is a single stream wait.
 """
 from __future__ import annotations
 
@@ -71,7 +76,8 @@ def broadcast_module_state(module: nn.Module, src: int = 0, group=None) -> None:
 class GradReducer:
     def __init__(self, module: nn.Module, group=None, bucket_cap_mb: float = 32.0,
                  first_bucket_mb: float = 1.0, broadcast: bool = True,
-                 rebuild_buckets: bool = True, comm_dtype: torch.dtype | None = None):
+                 rebuild_buckets: bool = True, comm_dtype: torch.dtype | None = None, comm: str = "pg",
+                 force_collectives: bool = False):
         self.module = module
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -84,6 +90,15 @@ class GradReducer:
         self._ready_order: list[int] = []
         self.works: list = []
         self.arena: GradArena | None = None
+        # force_collectives (tests): run the bucket collectives even in a world of one
+        self._collect = self.world > 1 or force_collectives
+        self.rccl = None
+        if comm == "rccl" and self._collect:
+            from .rccl import RcclComm
+            dev = next(iter(self.params)).device
+            self.rccl = RcclComm(group, dev)
+        elif comm not in ("pg", "rccl"):
+            raise ValueError(f"GradReducer: comm must be 'pg' or 'rccl', not {comm!r}")
         self._verify_param_shapes()
         if broadcast:
             broadcast_module_state(module, 0, group)
@@ -165,7 +180,7 @@ class GradReducer:
 
     def _launch(self, b: int) -> None:
         self.launched[b] = True
-        if self.world == 1:
+        if not self._collect:
             return
         s, e, _ = self.buckets[b]
         t = self.flat[s:e]
@@ -176,6 +191,13 @@ class GradReducer:
         main = torch.cuda.current_stream(t.device) if side is not None else None
         if comm_timer.active() and t.is_cuda:
             comm_timer.mark("first_bucket", side if side is not None else torch.cuda.current_stream(t.device))
+        if self.rccl is not None:
+            after = side if side is not None else torch.cuda.current_stream(t.device)
+            with torch.cuda.stream(after):
+                c = t.to(self.comm_dtype) if self.comm_dtype not in (None, torch.float32) else t
+            self.rccl.all_reduce_(c, after=after)
+            self.works.append((None, t, c) if c is not t else (None, None, None))
+            return
         with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
             if self.comm_dtype is not None and self.comm_dtype != torch.float32:
                 c = t.to(self.comm_dtype)
@@ -208,8 +230,11 @@ class GradReducer:
         for b in range(len(self.buckets)):
             if not self.launched[b]:
                 self._launch(b)
+        if self.rccl is not None and self.works:
+            self.rccl.join()  # the compute stream waits for every bucket's collective
         for work, dst, comp in self.works:
-            work.wait()
+            if work is not None:
+                work.wait()
             if dst is not None:
                 dst.copy_(comp)
         self.works.clear()
