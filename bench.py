@@ -224,6 +224,8 @@ def main():
         base = load_baseline(ctx.world_size, a.batch) if a.dtype == "bf16" else None
         metric = METRIC if (a.model, a.image_size, a.dtype) == ("resnet50", 224, "bf16") else \
             f"images/sec (whole node) {a.model} {a.image_size}x{a.image_size} {a.dtype} MI355X"
+        if os.environ.get("IMGCLS_DIAG_SKIP_WGRAD", "0") == "1":  # a diagnostic, never a benchmark number
+            metric, base = "DIAGNOSTIC (weight gradients skipped, invalid as a benchmark): " + metric, None
         print(json.dumps({
             "metric": metric, "value": round(value, 2), "unit": "images/sec",
             "n_gpus": ctx.world_size, "steps": a.steps, "warmup": a.warmup,

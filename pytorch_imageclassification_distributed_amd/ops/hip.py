@@ -767,11 +767,18 @@ def _wgrad_ws(dev, n):
     return buf
 
 
+# diagnostic only (scripts/gpu_*.sh contention studies; never a benchmark number): skip the weight-gradient
+# GEMMs to time the compute stream without the side stream's load.  bench.py refuses to report with it set.
+SKIP_WGRAD = os.environ.get("IMGCLS_DIAG_SKIP_WGRAD", "0") == "1"
+
+
 def _wgrad_launch(dy, x, out, g: ConvGeom, m, ntot, kps, splits, stages=2, side=None, xa=None, xf=None):
     """One weight-gradient launch on the current stream, or (``side``: a ``_SideStream``) forked onto the
     side stream inside the launcher (event record / wait and allocator stream records in C++).  ``xa`` =
     (y, coef): dy is a BN's pre-elementwise gradient, the kernel applies the elementwise map itself.
     ``xf`` = (coef, act): x is a BN's input y, the kernel reads act(bn(y))."""
+    if SKIP_WGRAD:
+        return
     wsp = None
     if WGRAD_WS and splits > 1 and ntot % 8 == 0:
         n = splits * g.Co * ntot
