@@ -40,7 +40,7 @@ int bn_finalize_launch(const double*, const double*, double, const float*, const
                        long long*, float, float, int, float*, const float*, hipStream_t);
 int bn_eval_coef_launch(const float*, const float*, const float*, const float*, float, int, float*, hipStream_t);
 int bn_apply_launch(const bf16_t*, const float*, const bf16_t*, bf16_t*, long, int, int, int, int, uint8_t*, uint8_t*,
-                    hipStream_t);
+                    uint8_t*, hipStream_t);
 int bn_bwd_reduce_launch(const bf16_t*, const bf16_t*, const float*, const bf16_t*, bf16_t*, long, int, int,
                          float*, int, int, hipStream_t);
 int bn_bwd_k_launch(const double*, const double*, double, int, float*, hipStream_t);
@@ -169,7 +169,7 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
                std::vector<int> dh, std::vector<int> dw, std::vector<int> tb, int stats_groups, Tensor zero,
                OT addend, OT bwd_y, OT bwd_res, OT bwd_coef, OT bwd_part, int bwd_act, int bwd_groups,
                int stages, int tile_n, int cfg, OT a_sc, OT b_sc, OT xa_y, OT xa_coef, OT xa_out, OT stats_shift,
-               OT xf_coef, int xf_act) {
+               OT xf_coef, int xf_act, OT bwd_mask) {
   const bool fp8 = a_sc.has_value() && a_sc->defined();
   TORCH_CHECK(A.scalar_type() == (fp8 ? at::kFloat8_e4m3fn : BF) && B.scalar_type() == A.scalar_type(),
               "conv_gemm: A and B must both be bf16, or both float8_e4m3fn with scales");
@@ -224,6 +224,12 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
     TORCH_CHECK(bwd_y->numel() == C.numel() && p.bwd_coef && p.bwd_part && c_off == 0,
                 "conv_gemm: fused BN-backward needs y matching C, coefficients and a partial buffer");
     TORCH_CHECK(!p.bwd_res || bwd_res->numel() == C.numel(), "conv_gemm: bwd_res must match C");
+    if (bwd_mask.has_value() && bwd_mask->defined()) {
+      TORCH_CHECK(bwd_mask->is_cuda() && bwd_mask->scalar_type() == at::kByte &&
+                      bwd_mask->numel() * 8 >= C.numel() && bwd_act == 1 && ldc == Ncols,
+                  "conv_gemm: bwd_mask needs uint8 [C.numel()/8], ReLU and a dense output");
+      p.bwd_mask = bwd_mask->data_ptr<uint8_t>();
+    }
   }
   if (p.addend) TORCH_CHECK(addend->numel() == C.numel() && addend->scalar_type() == BF, "conv_gemm: addend must match C");
   p.xa_y = optr<bf16_t>(xa_y);
@@ -358,7 +364,7 @@ void bn_eval_coef(OT gamma, OT beta, Tensor rmean, Tensor rvar, double eps, int 
 }
 
 void bn_apply(Tensor y, Tensor coef, OT res, Tensor out, long rows, int C, int ldo, int c_off, int act, OT q,
-              OT qs) {
+              OT qs, OT mask) {
   req(y, BF, "y"); req(out, BF, "out"); req(coef, F32, "coef");
   TORCH_CHECK(C % 8 == 0, "bn_apply: C % 8");
   uint8_t* qp = nullptr;
@@ -370,8 +376,15 @@ void bn_apply(Tensor y, Tensor coef, OT res, Tensor out, long rows, int C, int l
     qp = (uint8_t*)q->data_ptr();
     qsp = qs->data_ptr<uint8_t>();
   }
+  uint8_t* mp = nullptr;
+  if (mask.has_value() && mask->defined()) {  // + the ReLU mask of a residual BN (1 bit per element)
+    TORCH_CHECK(mask->is_cuda() && mask->scalar_type() == at::kByte && mask->numel() >= rows * C / 8 &&
+                    res.has_value() && res->defined() && act == 1 && ldo == C && c_off == 0 && !qp,
+                "bn_apply: mask needs uint8 [rows*C/8], a residual, ReLU and a dense bf16 output");
+    mp = mask->data_ptr<uint8_t>();
+  }
   check(bn_apply_launch(ptr<bf16_t>(y), ptr<float>(coef), optr<bf16_t>(res), ptr<bf16_t>(out), rows, C, ldo, c_off,
-                        act, qp, qsp, cur()),
+                        act, qp, qsp, mp, cur()),
         "bn_apply");
 }
 
@@ -939,7 +952,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_eval_coef", &bn_eval_coef);
   m.def("bn_apply", &bn_apply, pybind11::arg("y"), pybind11::arg("coef"), pybind11::arg("res"), pybind11::arg("out"),
         pybind11::arg("rows"), pybind11::arg("C"), pybind11::arg("ldo"), pybind11::arg("c_off"), pybind11::arg("act"),
-        pybind11::arg("q") = pybind11::none(), pybind11::arg("qs") = pybind11::none());
+        pybind11::arg("q") = pybind11::none(), pybind11::arg("qs") = pybind11::none(),
+        pybind11::arg("mask") = pybind11::none());
   m.def("bn_bwd_reduce", &bn_bwd_reduce, pybind11::arg("g"), pybind11::arg("y"), pybind11::arg("coef"), pybind11::arg("res"),
         pybind11::arg("dz_out"), pybind11::arg("rows"), pybind11::arg("C"), pybind11::arg("act"), pybind11::arg("part"), pybind11::arg("G"),
         pybind11::arg("ldg") = 0);

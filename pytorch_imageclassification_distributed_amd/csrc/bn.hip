@@ -246,7 +246,7 @@ constexpr int BN_U = 4;
 template <bool RES>
 __global__ void bn_apply_u_kernel(const bf16_t* __restrict__ y, const float* __restrict__ coef,
                                   const bf16_t* __restrict__ res, bf16_t* __restrict__ out, long rows, int C,
-                                  int ldo, int c_off, int act) {
+                                  int ldo, int c_off, int act, uint8_t* __restrict__ mask) {
   const int cch = C >> 3;
   const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
   if (cch == 0) return;
@@ -274,13 +274,17 @@ __global__ void bn_apply_u_kernel(const bf16_t* __restrict__ y, const float* __r
       float v[8], rr[8];
       unpack8(yv[u], v);
       if constexpr (RES) unpack8(rv[u], rr);
+      unsigned mk = 0;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         float z = v[k] * sc[k] + sh[k];
         if constexpr (RES) z += rr[k];
+        mk |= (z > 0.f ? 1u : 0u) << k;
         v[k] = apply_act(z, act);
       }
       *(uint4*)(out + r * ldo + c_off + c0) = pack8(v);
+      // ReLU mask for the backward (residual BNs): bit k of byte r * C/8 + c0/8 = channel c0 + k positive
+      if (mask) mask[r * (C >> 3) + (c0 >> 3)] = (uint8_t)mk;
     }
   }
 }
@@ -830,7 +834,8 @@ int bn_eval_coef_launch(const float* gamma, const float* beta, const float* rmea
 }
 
 int bn_apply_launch(const bf16_t* y, const float* coef, const bf16_t* res, bf16_t* out, long rows, int C,
-                    int ldo, int c_off, int act, uint8_t* q, uint8_t* qs, hipStream_t s) {
+                    int ldo, int c_off, int act, uint8_t* q, uint8_t* qs, uint8_t* mask, hipStream_t s) {
+  if (mask && (q || !res || act != ACT_RELU || ldo != C || c_off)) return 2;
   if (q) {
     if (C % 32 || ldo != C || c_off) return 2;
     hipLaunchKernelGGL(bn_apply_mx_kernel, dim3(grid_chan(rows, C)), dim3(256), 0, s, y, coef, res, out, q,
@@ -838,11 +843,11 @@ int bn_apply_launch(const bf16_t* y, const float* coef, const bf16_t* res, bf16_
     HIP_CHECK_LAUNCH();
     return 0;
   }
-  if (g_bn_unroll) {
+  if (g_bn_unroll || mask) {
     if (res) hipLaunchKernelGGL(bn_apply_u_kernel<true>, dim3(grid_chan(rows, C)), dim3(256), 0, s, y, coef, res, out,
-                                rows, C, ldo, c_off, act);
+                                rows, C, ldo, c_off, act, mask);
     else hipLaunchKernelGGL(bn_apply_u_kernel<false>, dim3(grid_chan(rows, C)), dim3(256), 0, s, y, coef, res, out,
-                            rows, C, ldo, c_off, act);
+                            rows, C, ldo, c_off, act, mask);
   } else {
     hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_chan(rows, C)), dim3(256), 0, s, y, coef, res, out,
                        rows, C, ldo, c_off, act);

@@ -100,11 +100,14 @@ DEVI void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN 
         float gv[8], yv[8], rv[8];
         unpack8(v, gv);
         unpack8(*(const uint4*)(p.bwd_y + pix * p.ldc + col), yv);
-        if (p.bwd_res) unpack8(*(const uint4*)(p.bwd_res + pix * p.ldc + col), rv);
+        const unsigned mk = p.bwd_mask ? (unsigned)p.bwd_mask[pix * (p.ldc >> 3) + (col >> 3)] : 0u;
+        if (p.bwd_res && !p.bwd_mask) unpack8(*(const uint4*)(p.bwd_res + pix * p.ldc + col), rv);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           float dz = gv[k];
-          if (p.bwd_act != ACT_NONE) {
+          if (p.bwd_mask) {
+            dz = ((mk >> k) & 1u) ? dz : 0.f;
+          } else if (p.bwd_act != ACT_NONE) {
             float z = yv[k] * bsc[k] + bsh[k];
             if (p.bwd_res) z += rv[k];
             dz = act_grad(z, gv[k], p.bwd_act);
@@ -168,7 +171,8 @@ DEVI void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN 
 // once per block): U rows' loads are issued together (out-of-range rows read row 0 and are masked at
 // the store), coefficients arrive as 16-B vectors.
 // ---------------------------------------------------------------------------
-enum : int { EP_STATS = 1, EP_ADD = 2, EP_BWD = 4, EP_RES = 8, EP_DIRECT = 16, EP_RELU = 32, EP_GENERIC = -1 };
+enum : int { EP_STATS = 1, EP_ADD = 2, EP_BWD = 4, EP_RES = 8, EP_DIRECT = 16, EP_RELU = 32, EP_MASK = 64,
+             EP_GENERIC = -1 };
 
 DEVI int epi_mode(const ConvParams& p) {
   if (p.bias != nullptr) return EP_GENERIC;
@@ -181,7 +185,7 @@ DEVI int epi_mode(const ConvParams& p) {
   if (p.addend != nullptr) m |= EP_ADD;
   if (p.bwd_y != nullptr) {
     if (p.bwd_act != ACT_RELU) return EP_GENERIC;
-    m |= EP_BWD | EP_RELU | (p.bwd_res != nullptr ? EP_RES : 0);
+    m |= EP_BWD | EP_RELU | (p.bwd_mask != nullptr ? EP_MASK : p.bwd_res != nullptr ? EP_RES : 0);
   }
   return m;
 }
@@ -190,7 +194,7 @@ template <int TM, int BN, int WM, int WN, int MODE, int UR>
 DEVI void conv_epi(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16], char* smem, int tid,
                    int lane, int wid, int wm, int wn, int m0, int n0, int bm) {
   constexpr bool STATS = MODE & EP_STATS, ADD = MODE & EP_ADD, BWD = MODE & EP_BWD, RES = MODE & EP_RES;
-  constexpr bool DIRECT = MODE & EP_DIRECT, RELU = MODE & EP_RELU;
+  constexpr bool DIRECT = MODE & EP_DIRECT, RELU = MODE & EP_RELU, MASK = MODE & EP_MASK;
   constexpr int NTH = 64 * WM * WN;
   constexpr int WTM = TM / WM, WTN = BN / WN;
   constexpr int RM = WTM / 16, RN = WTN / 16;
@@ -246,6 +250,7 @@ DEVI void conv_epi(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16]
 #pragma unroll 1
   for (int it0 = 0; it0 < IT; it0 += U) {  // not unrolled: the scheduler would hoist every row's loads
     uint4 v[U], ad[U], yv[U], rv[U];
+    unsigned mk[U];
     long pix[U];
     bool ok[U];
 #pragma unroll
@@ -265,6 +270,7 @@ DEVI void conv_epi(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16]
       if constexpr (ADD) ad[u] = *(const uint4*)(p.addend + pix[u] * p.ldc + p.c_off + col_l);
       if constexpr (BWD) yv[u] = *(const uint4*)(p.bwd_y + pix[u] * p.ldc + col_l);
       if constexpr (RES) rv[u] = *(const uint4*)(p.bwd_res + pix[u] * p.ldc + col_l);
+      if constexpr (MASK) mk[u] = p.bwd_mask[pix[u] * (p.ldc >> 3) + (col_l >> 3)];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -285,7 +291,9 @@ DEVI void conv_epi(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16]
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           float dz = f[k];
-          if constexpr (RELU) {
+          if constexpr (MASK) {
+            dz = ((mk[u] >> k) & 1u) ? dz : 0.f;
+          } else if constexpr (RELU) {
             float z = yf[k] * bsc[k] + bsh[k];
             if constexpr (RES) z += rf[k];
             dz = z > 0.f ? dz : 0.f;
@@ -358,12 +366,16 @@ DEVI void conv_epilogue_dispatch(const ConvParams& p, f32x4 (&acc)[TM / WM / 16]
     EPI_CASE(EP_BWD | EP_RELU | EP_RES | EP_DIRECT)
     EPI_CASE(EP_BWD | EP_RELU | EP_ADD | EP_DIRECT)
     EPI_CASE(EP_BWD | EP_RELU | EP_RES | EP_ADD | EP_DIRECT)
+    EPI_CASE(EP_BWD | EP_RELU | EP_MASK | EP_DIRECT)
+    EPI_CASE(EP_BWD | EP_RELU | EP_MASK | EP_ADD | EP_DIRECT)
     // stride-2 data gradients (sub-pixel phases, remapped pixels)
     EPI_CASE(EP_ADD)
     EPI_CASE(EP_BWD | EP_RELU)
     EPI_CASE(EP_BWD | EP_RELU | EP_RES)
     EPI_CASE(EP_BWD | EP_RELU | EP_ADD)
     EPI_CASE(EP_BWD | EP_RELU | EP_RES | EP_ADD)
+    EPI_CASE(EP_BWD | EP_RELU | EP_MASK)
+    EPI_CASE(EP_BWD | EP_RELU | EP_MASK | EP_ADD)
     default: conv_epilogue<TM, BN, WM, WN>(p, acc, smem, tid, lane, wid, wm, wn, m0, n0, bm, ghw);
   }
 #undef EPI_CASE

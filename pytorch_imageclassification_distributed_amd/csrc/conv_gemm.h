@@ -39,6 +39,9 @@ struct ConvParams {
   // accumulates per-channel (sum dz, sum dz*xhat) into bwd_part rows.  bwd_coef = [scale|shift|mean|invstd].
   const bf16_t* bwd_y;
   const bf16_t* bwd_res;
+  // optional: the consumer BN's ReLU mask from its forward (bit k of byte pix*ldc/8 + c/8 = channel c + k
+  // was positive), written by bn_apply for a residual BN - read instead of bwd_res (1/16 of its bytes)
+  const uint8_t* bwd_mask;
   const float* bwd_coef;
   float* bwd_part;
   int bwd_act, bwd_groups;

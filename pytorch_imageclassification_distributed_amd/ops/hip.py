@@ -470,7 +470,7 @@ TUNE_LOG: list = []  # (M, Ncols, K, {cfg: ms}) per tuned geometry (benchmarks/c
 
 
 def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(None, None, None, None, 0, 1),
-               groups=G_STATS, scales=(None, None), xa=None, shift=None, xf=None):
+               groups=G_STATS, scales=(None, None), xa=None, shift=None, xf=None, mask=None):
     """One implicit-GEMM launch.  The kernel configuration - LDS-DMA ring depth (1 = high occupancy,
     2 / 3 = pipelined) x output-channel tile (64 / 128 / 256: more tiles balance 256 CUs better on
     small layers) x pixel tile (128 rows on 4 waves, or 256 rows on 8 waves) - is chosen once per
@@ -501,7 +501,7 @@ def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(
         cfg = _STAGES_TUNED.get(key)
         if cfg is None:
             cfg = (0, 0, -1) if torch.cuda.is_current_stream_capturing() else _tune_conv(
-                A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups, scales, xa, xf)
+                A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups, scales, xa, xf, mask)
             if cfg[0] or cfg[2] >= 0:
                 _STAGES_TUNED[key] = cfg
     if cfg[2] >= HALO_BASE:
@@ -511,7 +511,7 @@ def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(
                        cfg[2] - DIRECT_BASE, bwd, shift)
         return
     C.conv_gemm(A, B, out, stats, bias, *geo, dh, dw, tb, groups, zero, addend, *bwd, *cfg, *scales, *xa3, shift,
-                *xf2)
+                *xf2, mask)
 
 
 _CFGS = None
@@ -641,7 +641,7 @@ def _direct_launch(A, B, out, stats, groups, dg, variant, bwd, shift=None):
 
 
 def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups, scales=(None, None), xa=None,
-               xf=None):
+               xf=None, mask=None):
     scratch = torch.empty_like(out)
     sst = torch.zeros_like(stats) if stats is not None else None
     bwd = tuple(bwd)
@@ -654,7 +654,7 @@ def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, group
     times = {}
     for cfg in cands:
         times[cfg] = _time_ms(lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, groups, zero,
-                                                  addend, *bwd, *cfg, *scales, *xa3, None, *xf2))
+                                                  addend, *bwd, *cfg, *scales, *xa3, None, *xf2, mask))
     if HALO_CONV and not fused and scales[0] is None:
         for v, (tm, bn, _wm, _wn, _bst, pmax) in enumerate(conv_halo_cfgs()):
             if v not in HALO_TUNE or not _halo_ok(geo, dh, dw, tm, pmax) or (bn > 64 and bn >= 2 * geo[1]) or \
@@ -662,7 +662,7 @@ def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, group
                 continue
             cfg = (0, 0, HALO_BASE + v)
             times[cfg] = _time_ms(lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, groups, zero,
-                                                      addend, *bwd, *cfg, *scales, *xa3, None, *xf2))
+                                                      addend, *bwd, *cfg, *scales, *xa3, None, *xf2, mask))
     dg = _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales) if not fused else None
     if dg is not None:
         for v, (cip, cot) in DIRECT_CFGS.items():
@@ -719,10 +719,12 @@ def conv_dgrad_raw(dy, w_param, g: ConvGeom, addend=None, link=None, xa=None):
     forms dY = coef0*dz + coef1*y + coef2 on its A-operand loads (1x1 convs, ``XaLink``)."""
     dev = dy.device
     bwd = (None, None, None, None, 0, 1)
+    mask = None
     if link is not None:
         grp = stat_groups(g.N * g.H * g.W)
         link.part = ws(dev).take_part(g.Ci, grp)
         bwd = (link.y, link.res, link.coef, link.part, link.act, grp)
+        mask = link.mask
     wt = weight_bf16_t(w_param, g.Co, g.T, g.Ci)
     dx = _empty_cl(g.N, g.Ci, g.H, g.W, dev)
     for ph, pw, gh, gw, dh, dw, tb in _dgrad_phases(g):
@@ -731,7 +733,7 @@ def conv_dgrad_raw(dy, w_param, g: ConvGeom, addend=None, link=None, xa=None):
         geo = (g.N * gh * gw, g.Ci, len(tb) * g.Co, g.Co, gh, gw, g.OH, g.OW, 1, g.T * g.Co, g.H, g.W, g.sh,
                ph, pw, g.Ci, 0)
         _conv_gemm(dy, wt, dx, None, None, geo, dh, dw, tb, ws(dev).zero, addend, bwd,
-                   xa=xa if len(tb) else None)
+                   xa=xa if len(tb) else None, mask=mask)
     return dx
 
 
@@ -1051,11 +1053,11 @@ class BwdLink:
     """Ties a BN(+act) output to the conv that consumes it, so the consumer's dgrad epilogue can run
     the producer's BN-backward reduce (``done`` tells the producer its gradient arrives as dz)."""
 
-    __slots__ = ("y", "coef", "res", "act", "part", "done", "group", "params", "pending", "c", "rows", "groups",
-                 "count_t")
+    __slots__ = ("y", "coef", "res", "mask", "act", "part", "done", "group", "params", "pending", "c", "rows",
+                 "groups", "count_t")
 
     def __init__(self):
-        self.y = self.coef = self.res = self.part = None
+        self.y = self.coef = self.res = self.mask = self.part = None
         self.act = 0
         self.done = False
         self.group = self.params = self.pending = None  # SyncBN: early backward all-reduce
@@ -1438,6 +1440,11 @@ def _bn_bwd_k(part, grp, c, rows, training, group, count_t, params, dev, coef=No
     return k, dgamma, dbeta
 
 
+# The residual BN's ReLU mask (1 bit per element, written by bn_apply) replaces the consumer dgrad epilogue's
+# re-read of the residual when it recomputes z = bn(y) + res > 0: ~11 GB less per ResNet-50 b1024 step.
+RELU_MASK = os.environ.get("IMGCLS_RELU_MASK", "1") == "1"
+
+
 class BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, y, gamma, beta, res, bn, act, stats_ready, res_slot=None, link=None, cat=None, xa=None,
@@ -1467,7 +1474,13 @@ class BNActFn(torch.autograd.Function):
             out._imgcls_mx = (q, qs, out._version)
         else:
             out = _empty_cl(n, c, h, w, dev)
-            C.bn_apply(y, coef, res, out, rows, c, c, 0, a)
+            # residual + ReLU in training: also the 1-bit ReLU mask, which the consuming conv's dgrad epilogue
+            # reads instead of re-reading the residual (1/16 of its bytes, RELU_MASK)
+            mask = (torch.empty(rows * c // 8, dtype=torch.uint8, device=dev)
+                    if RELU_MASK and res is not None and a == 1 and bn.training and link is not None else None)
+            C.bn_apply(y, coef, res, out, rows, c, c, 0, a, mask=mask)
+            if link is not None:
+                link.mask = mask
         ctx.act, ctx.group, ctx.rows, ctx.c = a, group, rows, c
         ctx.training = bn.training
         ctx.count_t = count_t
@@ -1504,7 +1517,7 @@ class BNActFn(torch.autograd.Function):
             grp = link.part_rows()
             FUSED_BWD_COUNT[0] += 1
             pending = link.pending
-            link.y = link.coef = link.res = link.part = link.pending = link.params = link.count_t = None
+            link.y = link.coef = link.res = link.mask = link.part = link.pending = link.params = link.count_t = None
             if ldg:
                 xa = None
         else:

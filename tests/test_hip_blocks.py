@@ -330,3 +330,32 @@ def test_inception_pool_conv_swap(kind):
     for n in gp_r:
         if "branch_pool" in n:
             assert merr(gp_s[n], gp_r[n]) < max(3e-2, 1.3 * merr(gp_p[n], gp_r[n])), n
+
+
+@pytest.mark.parametrize("kind", ["bottle_id", "chain"])
+def test_relu_mask_matches_residual_recompute(kind):
+    """The residual BN's forward ReLU mask (bn_apply writes 1 bit per element; the consuming conv's dgrad
+    epilogue reads it instead of re-reading the residual) gives the gradients of the recompute path."""
+    import torch.nn as nn
+    from pytorch_imageclassification_distributed_amd.models.resnet import Bottleneck, _conv1x1
+    from pytorch_imageclassification_distributed_amd.ops import hip
+    torch.manual_seed(0)
+    if kind == "bottle_id":
+        blk = nn.Sequential(Bottleneck(256, 64), Bottleneck(256, 64))
+    else:
+        blk = nn.Sequential(Bottleneck(256, 128, 2, nn.Sequential(_conv1x1(256, 512, 2), nn.BatchNorm2d(512))),
+                            Bottleneck(512, 128))
+    blk = blk.to(DEV).to(memory_format=torch.channels_last)
+    x = torch.randn(4, 256, 16, 16, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    keep = hip.RELU_MASK
+    try:
+        hip.RELU_MASK = False
+        gx0, gp0 = _grads(blk, x, True)
+        hip.RELU_MASK = True
+        gx1, gp1 = _grads(blk, x, True)
+    finally:
+        hip.RELU_MASK = keep
+    err = lambda a, b: ((a - b).abs().max() / b.abs().max().clamp(min=1e-6)).item()  # noqa: E731
+    assert err(gx1, gx0) < 1e-2, err(gx1, gx0)
+    for n in gp0:
+        assert err(gp1[n], gp0[n]) < 1e-2, (n, err(gp1[n], gp0[n]))
