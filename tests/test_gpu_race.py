@@ -2,6 +2,7 @@
 serialised (AMD_SERIALIZE_KERNEL=3) as with the side / comm / copy streams running concurrently
 (scripts/race_check.py).  A missing stream wait would make the concurrent digest differ."""
 import os
+import socket
 import subprocess
 import sys
 
@@ -16,7 +17,10 @@ def _digest(serialize: bool, model: str) -> str:
     env.pop("AMD_SERIALIZE_KERNEL", None)
     if serialize:
         env["AMD_SERIALIZE_KERNEL"] = "3"
-    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    env["MASTER_ADDR"] = "127.0.0.1"
+    with socket.socket() as s:  # the pytest process may already hold its own rendezvous port
+        s.bind(("127.0.0.1", 0))
+        env["MASTER_PORT"] = str(s.getsockname()[1])
     # fixed kernel choices in both processes (the per-shape tuner times candidates, and serialised timings
     # could pick other kernels - another fp32 summation order, not a race)
     env.update(IMGCLS_CONV_STAGES="1", IMGCLS_WGRAD_STAGES="2", IMGCLS_WGRAD_BLOCKS="256", IMGCLS_DIRECT_CONV="0")
