@@ -942,6 +942,10 @@ def comm_stream(dev):
     return s.stream
 
 
+# 1: the input layer's weight gradient joins the side stream like every other (the round-2 placement)
+STEM_WGRAD_SIDE = os.environ.get("IMGCLS_STEM_WGRAD_SIDE", "0") == "1"
+
+
 def conv_wgrad_raw(dy, x, w_param, g: ConvGeom, xa=None, xf=None):
     dev = dy.device
     m = g.N * g.OH * g.OW
@@ -970,6 +974,12 @@ def conv_wgrad_raw(dy, x, w_param, g: ConvGeom, xa=None, xf=None):
         # padded input channels = the network's input layer, the last weight gradient of backward: on the
         # compute stream (idle by then) it runs beside the side stream's backlog instead of behind it - the
         # ResNet-50 b1024 stem wgrad is ~0.7 ms of the step tail (profiles/r5e_conv_roofline_b1024.txt)
+        if STEM_WGRAD_SIDE:
+            def launch():
+                _wgrad_launch(dy, x, full, g, m, ntot, kps, splits, stages)
+                C.grad_unpad(full, dw, g.Co * g.T, g.Cx, g.Ci)
+            _on_side(dev, launch, dy, x, full)
+            return dw
         _wgrad_launch(dy, x, full, g, m, ntot, kps, splits, stages)
         C.grad_unpad(full, dw, g.Co * g.T, g.Cx, g.Ci)
         return dw
