@@ -6,5 +6,5 @@ for r in 1 2; do
   b def$r --model inceptionv3 --image-size 299 --batch 256 --warmup 8 --steps 20 || exit 1
   IMGCLS_HALO=0 b nohalo$r --model inceptionv3 --image-size 299 --batch 256 --warmup 8 --steps 20 || exit 1
   IMGCLS_STEM_WGRAD_SIDE=1 b stemside$r --model inceptionv3 --image-size 299 --batch 256 --warmup 8 --steps 20 || exit 1
-  IMGCLS_RELU_MASK=0 b nomask$r --model inceptionv3 --image-size 299 --batch 256 --warmup 8 --steps 20 || exit 1
+  IMGCLS_MAX_INFLIGHT_STEPS=4 b inflight4$r --model inceptionv3 --image-size 299 --batch 256 --warmup 8 --steps 20 || exit 1
 done
