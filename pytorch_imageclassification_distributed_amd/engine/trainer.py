@@ -38,7 +38,8 @@ from ..data import CudaPrefetcher, ImageDataset, NativeFolderLoader, SyntheticIm
 from ..models import DEFAULT_IMAGE_SIZE, Classifier
 from ..ops import functional as Fx
 from ..ops.grad_arena import GradArena
-from ..parallel import GradReducer, check_peer_errors, comm_timer, convert_sync_batchnorm, setup_peer_syncbn
+from ..parallel import (GradReducer, check_peer_errors, check_syncbn_consistency, comm_timer, convert_sync_batchnorm,
+                        setup_peer_syncbn)
 from ..utils import (BEST, LATEST, AccuracyCounter, DeviceMeter, JsonlLogger, load_checkpoint,
                      load_model_state, resolve_resume, restore_rng_state, save_checkpoint)
 from ..utils.timers import PhaseTimer
@@ -389,6 +390,7 @@ class Trainer:
             if (index + 1) % max(a.log_interval, 1) == 0:
                 if self.syncbn_peer:  # a timed-out SyncBN peer exchange is fatal (parallel/peer.py)
                     check_peer_errors(f"epoch {epoch} step {index}")
+                    check_syncbn_consistency(self.model, None, f"epoch {epoch} step {index}")
                 if bar is not None:
                     bar.set_description(f"Epoch: {epoch}; Loss {meter.val:.4f}|({meter.avg:.4f})")
                 if self.timer.enabled:
@@ -407,6 +409,7 @@ class Trainer:
             bar.close()
         if self.syncbn_peer:
             check_peer_errors(f"end of epoch {epoch}")
+            check_syncbn_consistency(self.model, None, f"end of epoch {epoch}")
         return meter.avg if meter.count else float("nan")
 
     @torch.no_grad()

@@ -219,6 +219,34 @@ def check_peer_errors(where: str = "") -> None:
                                f": {n} channel error word(s) set; the statistics of that step are invalid")
 
 
+class SyncBNMismatchError(RuntimeError):
+    pass
+
+
+def check_syncbn_consistency(module, group=None, where: str = "") -> None:
+    """Steady-state guard for SyncBN (collective; call at log intervals): every rank must hold bitwise the
+    same BN running statistics, because each rank sums the same per-rank payloads in rank order (peer path) or
+    receives the same all-reduce result (RCCL).  A transport fault - a stale or torn slot - shows up here as a
+    mismatch, and the run stops instead of training on diverged statistics."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return
+    bufs = [b for n, b in module.named_buffers() if "running_" in n]
+    if not bufs:
+        return
+    dev = bufs[0].device
+    s = torch.zeros(2, dtype=torch.float64, device=dev)
+    for i, b in enumerate(bufs):  # position-weighted sums: a swapped or shifted buffer changes them too
+        v = b.detach().double().reshape(-1)
+        w = torch.arange(1, v.numel() + 1, dtype=torch.float64, device=dev) * (1.0 + 1e-3 * i)
+        s[0] += v.sum()
+        s[1] += (v * w).sum()
+    both = torch.cat([s, -s])
+    dist.all_reduce(both, op=dist.ReduceOp.MAX, group=group)
+    if not torch.equal(both[:2], -both[2:]):
+        raise SyncBNMismatchError(f"SyncBN running statistics differ between ranks{' (' + where + ')' if where else ''}:"
+                                  f" checksum max {both[:2].tolist()} vs min {(-both[2:]).tolist()}")
+
+
 def peer_channel(group, which: int):
     """The group's forward (0, compute stream) or backward (1, side stream) channel, or None."""
     chans = _CHANNELS.get(id(group)) if group is not None else None

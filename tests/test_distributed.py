@@ -243,3 +243,26 @@ def _w_order(rank, world, port):
 
 def test_bucket_rebuild_uses_rank0_order():
     _run(_w_order)
+
+
+def _w_syncbn_guard(rank, world, port):
+    _setup(rank, world, port)
+    import torch.distributed as dist
+    import torch.nn as nn
+    from pytorch_imageclassification_distributed_amd.parallel import SyncBNMismatchError, check_syncbn_consistency
+    torch.manual_seed(0)
+    m = nn.Sequential(nn.Conv2d(3, 8, 3), nn.BatchNorm2d(8), nn.ReLU(), nn.Conv2d(8, 8, 1), nn.BatchNorm2d(8))
+    check_syncbn_consistency(m, None, "identical")  # same buffers on both ranks: passes
+    if rank == 1:
+        with torch.no_grad():
+            m[4].running_var[3] += 1e-6  # one element on one rank
+    with pytest.raises(SyncBNMismatchError, match="differ between ranks"):
+        check_syncbn_consistency(m, None, "perturbed")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_syncbn_consistency_guard():
+    """Steady-state SyncBN guard: diverged running statistics on any rank stop the run on
+    every rank (the check is collective, so all ranks raise together)."""
+    _run(_w_syncbn_guard)
