@@ -46,8 +46,12 @@ from ..utils.timers import PhaseTimer
 from .config import hip_graph_enabled, parse_class_weights
 from .optim import FusedAdam, MultiStepLR
 
-# training steps the host may have enqueued ahead of the GPU (Trainer._throttle; 0 = unbounded)
-MAX_INFLIGHT_STEPS = int(os.environ.get("IMGCLS_MAX_INFLIGHT_STEPS", "2"))
+# training steps the host may have enqueued ahead of the GPU (Trainer._throttle; 0 = unbounded).  Unset: 2, or
+# 4 when a step's peak allocation is under SMALL_STEP_FRACTION of the device (the host-bound small-memory
+# steps gain from the deeper queue - Inception-v3 b256 8323 -> 8400 img/s, profiles/r7d_* - and their cache
+# stays small; ResNet-50 b1024 at 44 GiB keeps 2)
+MAX_INFLIGHT_STEPS = int(os.environ.get("IMGCLS_MAX_INFLIGHT_STEPS", "-1"))
+SMALL_STEP_FRACTION = 0.1
 
 
 def _is_inception(name: str) -> bool:
@@ -180,6 +184,8 @@ class Trainer:
         self._prof = None
         self._graph = None  # captured whole-step HIP graph (``capture_step``)
         self._eager_steps = 0  # eager training steps run by this process (graph capture waits for 2)
+        self._steps_enqueued = 0
+        self._auto_inflight = None  # MAX_INFLIGHT_STEPS unset: chosen from the steady-state peak allocation
         self._inflight = collections.deque()  # end-of-step events of the steps the GPU has not finished
 
     # ------------------------------------------------------------------ step
@@ -226,13 +232,28 @@ class Trainer:
         allocated but 286 GiB reserved; at the 288 GB limit the allocator frees its whole cache with
         device syncs and re-maps each block: 1.6 s steps, the b1536 / b2048 slowdown of round 2
         (docs/DESIGN.md).  Two steps in flight keep the GPU fed and bound the cache."""
-        if self.dev.type != "cuda" or MAX_INFLIGHT_STEPS <= 0:
+        limit = self._inflight_limit()
+        if limit <= 0:
             return
-        while len(self._inflight) >= MAX_INFLIGHT_STEPS:
+        while len(self._inflight) >= limit:
             self._inflight.popleft().synchronize()
 
+    def _inflight_limit(self) -> int:
+        if self.dev.type != "cuda" or MAX_INFLIGHT_STEPS == 0:
+            return 0
+        if MAX_INFLIGHT_STEPS > 0:
+            return MAX_INFLIGHT_STEPS
+        if self._auto_inflight is None:
+            if self._steps_enqueued < 2:  # the first steps tune kernels: their peak is not the steady one
+                return 2
+            total = torch.cuda.get_device_properties(self.dev).total_memory
+            small = torch.cuda.max_memory_allocated(self.dev) < SMALL_STEP_FRACTION * total
+            self._auto_inflight = 4 if small else 2
+        return self._auto_inflight
+
     def _step_enqueued(self) -> None:
-        if self.dev.type == "cuda" and MAX_INFLIGHT_STEPS > 0:
+        self._steps_enqueued += 1
+        if self._inflight_limit() > 0:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.dev))
             self._inflight.append(ev)

@@ -125,7 +125,9 @@ def test_step_throttle_bounds_steps_in_flight(monkeypatch):
             waited.append(self.i)
 
     monkeypatch.setattr(tm, "MAX_INFLIGHT_STEPS", 2)
-    fake = types.SimpleNamespace(dev=types.SimpleNamespace(type="cuda"), _inflight=collections.deque())
+    fake = types.SimpleNamespace(dev=types.SimpleNamespace(type="cuda"), _inflight=collections.deque(),
+                                 _auto_inflight=None, _steps_enqueued=0)
+    fake._inflight_limit = lambda: tm.Trainer._inflight_limit(fake)
     for i in range(5):
         tm.Trainer._throttle(fake)
         assert len(fake._inflight) < 2
@@ -134,6 +136,11 @@ def test_step_throttle_bounds_steps_in_flight(monkeypatch):
     monkeypatch.setattr(tm, "MAX_INFLIGHT_STEPS", 0)  # 0: unbounded, never waits
     tm.Trainer._throttle(fake)
     assert waited == [0, 1, 2]
+    # unset (-1): 2 while the first steps tune, then the memory-based choice (4 for a small step)
+    monkeypatch.setattr(tm, "MAX_INFLIGHT_STEPS", -1)
+    assert tm.Trainer._inflight_limit(fake) == 2
+    fake._steps_enqueued, fake._auto_inflight = 5, 4
+    assert tm.Trainer._inflight_limit(fake) == 4
 
 
 def test_hip_graph_auto_mode():
