@@ -379,7 +379,7 @@ void bn_apply(Tensor y, Tensor coef, OT res, Tensor out, long rows, int C, int l
   uint8_t* mp = nullptr;
   if (mask.has_value() && mask->defined()) {  // + the ReLU mask of a residual BN (1 bit per element)
     TORCH_CHECK(mask->is_cuda() && mask->scalar_type() == at::kByte && mask->numel() >= rows * C / 8 &&
-                    res.has_value() && res->defined() && act == 1 && ldo == C && c_off == 0 && !qp,
+                    res.has_value() && res->defined() && act == 1 && ldo == C && c_off == 0,
                 "bn_apply: mask needs uint8 [rows*C/8], a residual, ReLU and a dense bf16 output");
     mp = mask->data_ptr<uint8_t>();
   }

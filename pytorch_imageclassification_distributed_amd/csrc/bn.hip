@@ -292,11 +292,13 @@ __global__ void bn_apply_u_kernel(const bf16_t* __restrict__ y, const float* __r
 // apply + MX-FP8 copy of the output for the fp8 forward convolution that consumes it (no separate
 // quantisation pass): the 4 lanes of a 32-channel block are consecutive lanes (C % 32 == 0), the
 // grid stride is a multiple of 4, so the block max is two xor-shuffles away.
+template <bool RES>
 __global__ void bn_apply_mx_kernel(const bf16_t* __restrict__ y, const float* __restrict__ coef,
                                    const bf16_t* __restrict__ res, bf16_t* __restrict__ out, uint8_t* __restrict__ q,
-                                   uint8_t* __restrict__ qs, long rows, int C, int act) {
-  // channel-fixed mapping (grid_chan) as bn_apply_kernel; C % 32 == 0 makes every 4-lane MX block share
-  // its row, so whole groups leave the loop together and the xor-shuffles below stay within live lanes
+                                   uint8_t* __restrict__ qs, long rows, int C, int act, uint8_t* __restrict__ mask) {
+  // channel-fixed mapping (grid_chan) as bn_apply_u_kernel, BN_U rows' loads in flight; C % 32 == 0 makes every
+  // 4-lane MX block share its row, so whole groups leave the loop together and the xor-shuffles below stay
+  // within live lanes
   const int cch = C >> 3;
   if (cch == 0) return;
   const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
@@ -307,28 +309,43 @@ __global__ void bn_apply_mx_kernel(const bf16_t* __restrict__ y, const float* __
   float sc[8], sh[8];
   load8f(coef + c0, sc);
   load8f(coef + C + c0, sh);
-  for (; row < rows; row += rstride) {
-    float v[8], r[8];
-    unpack8(*(const uint4*)(y + row * C + c0), v);
-    if (res) unpack8(*(const uint4*)(res + row * C + c0), r);
+  for (; row < rows; row += BN_U * rstride) {
+    uint4 yv[BN_U], rv[BN_U];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float z = v[k] * sc[k] + sh[k];
-      if (res) z += r[k];
-      v[k] = apply_act(z, act);
+    for (int u = 0; u < BN_U; ++u) {
+      const long r = row + u * rstride < rows ? row + u * rstride : row;
+      yv[u] = *(const uint4*)(y + r * C + c0);
+      if constexpr (RES) rv[u] = *(const uint4*)(res + r * C + c0);
     }
-    const uint4 o = pack8(v);
-    *(uint4*)(out + row * C + c0) = o;
-    unpack8(o, v);  // quantise the bf16 value the backward pass will see
-    float amax = 0.f;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) amax = fmaxf(amax, fabsf(v[k]));
-    amax = fmaxf(amax, __shfl_xor(amax, 1));
-    amax = fmaxf(amax, __shfl_xor(amax, 2));
-    const int e = mx_exponent(amax);
-    const long i = row * cch + ch;
-    *(uint2*)(q + i * 8) = to_fp8x8(v, ldexpf(1.f, -e));
-    if ((i & 3) == 0) qs[i >> 2] = (uint8_t)(e + 127);
+    for (int u = 0; u < BN_U; ++u) {
+      const long r = row + u * rstride;
+      if (r >= rows) break;  // the 4 lanes of an MX block share r: they leave together
+      float v[8], rr[8];
+      unpack8(yv[u], v);
+      if constexpr (RES) unpack8(rv[u], rr);
+      unsigned mk = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float z = v[k] * sc[k] + sh[k];
+        if constexpr (RES) z += rr[k];
+        mk |= (z > 0.f ? 1u : 0u) << k;
+        v[k] = apply_act(z, act);
+      }
+      const uint4 o = pack8(v);
+      *(uint4*)(out + r * C + c0) = o;
+      if (mask) mask[r * cch + ch] = (uint8_t)mk;
+      unpack8(o, v);  // quantise the bf16 value the backward pass will see
+      float amax = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) amax = fmaxf(amax, fabsf(v[k]));
+      amax = fmaxf(amax, __shfl_xor(amax, 1));
+      amax = fmaxf(amax, __shfl_xor(amax, 2));
+      const int e = mx_exponent(amax);
+      const long i = r * cch + ch;
+      *(uint2*)(q + i * 8) = to_fp8x8(v, ldexpf(1.f, -e));
+      if ((i & 3) == 0) qs[i >> 2] = (uint8_t)(e + 127);
+    }
   }
 }
 
@@ -835,11 +852,13 @@ int bn_eval_coef_launch(const float* gamma, const float* beta, const float* rmea
 
 int bn_apply_launch(const bf16_t* y, const float* coef, const bf16_t* res, bf16_t* out, long rows, int C,
                     int ldo, int c_off, int act, uint8_t* q, uint8_t* qs, uint8_t* mask, hipStream_t s) {
-  if (mask && (q || !res || act != ACT_RELU || ldo != C || c_off)) return 2;
+  if (mask && (!res || act != ACT_RELU || ldo != C || c_off)) return 2;
   if (q) {
     if (C % 32 || ldo != C || c_off) return 2;
-    hipLaunchKernelGGL(bn_apply_mx_kernel, dim3(grid_chan(rows, C)), dim3(256), 0, s, y, coef, res, out, q,
-                       qs, rows, C, act);
+    if (res) hipLaunchKernelGGL(bn_apply_mx_kernel<true>, dim3(grid_chan(rows, C)), dim3(256), 0, s, y, coef, res, out, q,
+                                qs, rows, C, act, mask);
+    else hipLaunchKernelGGL(bn_apply_mx_kernel<false>, dim3(grid_chan(rows, C)), dim3(256), 0, s, y, coef, res, out, q,
+                            qs, rows, C, act, mask);
     HIP_CHECK_LAUNCH();
     return 0;
   }

@@ -1480,8 +1480,12 @@ class BNActFn(torch.autograd.Function):
             out = _empty_cl(n, c, h, w, dev)
             q = torch.empty(rows * c, dtype=FP8, device=dev)
             qs = torch.empty(rows * c // 32, dtype=torch.uint8, device=dev)
-            C.bn_apply(y, coef, res, out, rows, c, c, 0, a, q, qs)
+            mask = (torch.empty(rows * c // 8, dtype=torch.uint8, device=dev)
+                    if RELU_MASK and res is not None and a == 1 and bn.training and link is not None else None)
+            C.bn_apply(y, coef, res, out, rows, c, c, 0, a, q, qs, mask=mask)
             out._imgcls_mx = (q, qs, out._version)
+            if link is not None:
+                link.mask = mask
         else:
             out = _empty_cl(n, c, h, w, dev)
             # residual + ReLU in training: also the 1-bit ReLU mask, which the consuming conv's dgrad epilogue

@@ -332,8 +332,8 @@ def test_inception_pool_conv_swap(kind):
             assert merr(gp_s[n], gp_r[n]) < max(3e-2, 1.3 * merr(gp_p[n], gp_r[n])), n
 
 
-@pytest.mark.parametrize("kind", ["bottle_id", "chain"])
-def test_relu_mask_matches_residual_recompute(kind):
+@pytest.mark.parametrize("kind,fp8", [("bottle_id", False), ("chain", False), ("chain", True)])
+def test_relu_mask_matches_residual_recompute(kind, fp8):
     """The residual BN's forward ReLU mask (bn_apply writes 1 bit per element; the consuming conv's dgrad
     epilogue reads it instead of re-reading the residual) gives the gradients of the recompute path."""
     import torch.nn as nn
@@ -348,6 +348,7 @@ def test_relu_mask_matches_residual_recompute(kind):
     blk = blk.to(DEV).to(memory_format=torch.channels_last)
     x = torch.randn(4, 256, 16, 16, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
     keep = hip.RELU_MASK
+    hip.set_fp8(fp8)  # fp8: the residual BN writes its mask from the MX-FP8 apply kernel
     try:
         hip.RELU_MASK = False
         gx0, gp0 = _grads(blk, x, True)
@@ -355,6 +356,7 @@ def test_relu_mask_matches_residual_recompute(kind):
         gx1, gp1 = _grads(blk, x, True)
     finally:
         hip.RELU_MASK = keep
+        hip.set_fp8(False)
     err = lambda a, b: ((a - b).abs().max() / b.abs().max().clamp(min=1e-6)).item()  # noqa: E731
     assert err(gx1, gx0) < 1e-2, err(gx1, gx0)
     for n in gp0:
