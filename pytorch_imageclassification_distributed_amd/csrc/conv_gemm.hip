@@ -1516,11 +1516,13 @@ static bool launch_wg(const WgradParams& p, int splits, hipStream_t stream) {
 
 // variants with a fused BN-backward form: all but the 256 x 256 tile with a 2-deep 64-pixel ring (its
 // register y pieces spill at 2 waves per SIMD; LDS y would not fit) and the 4-deep 256 x 256 ring (LDS)
-bool conv_wgrad_has_xa(int stages) { return stages >= 1 && stages <= 9 && stages != 4 && stages != 7; }
+bool conv_wgrad_has_xa(int stages) { return stages >= 1 && stages <= 12 && stages != 4 && stages != 7; }
 // the fused BN-apply X form needs no register operand: every LDS-DMA variant has it
-bool conv_wgrad_has_xf(int stages) { return stages >= 1 && stages <= 9; }
+bool conv_wgrad_has_xf(int stages) { return stages >= 1 && stages <= 12; }
 
-int conv_wgrad_tile_n(int stages) { return (stages == 4 || stages == 7 || stages == 9) ? 256 : WBN; }
+int conv_wgrad_tile_n(int stages) {
+  return (stages == 4 || stages == 7 || stages == 9) ? 256 : stages >= 10 ? 64 : WBN;
+}
 
 int conv_wgrad_launch(const WgradParams& p_in, int splits, hipStream_t stream) {
   if (p_in.M <= 0) return 0;
@@ -1533,7 +1535,19 @@ int conv_wgrad_launch(const WgradParams& p_in, int splits, hipStream_t stream) {
   // stages: 1 | 2 (4 waves, 64/128 x 128 tile), 3 = 2-stage ring with the in-block 2-way pixel split
   // (8 waves), 4 = 256 x 256 tile on 8 waves (2-stage ring, one block per CU; Cout >= 256 only),
   // 5 / 6 = 32 x 128 tile with a 1 / 2-stage ring (Cout <= 32 only)
-  if (dma && (p.stages == 7 || p.stages == 9)) {  // 256 x 256, 8 waves, 4- / 3-deep ring of 32-pixel stages
+  if (dma && p.stages >= 10 && p.stages <= 12) {
+    // 64-column tiles for Ntot <= 64 (ResNet layer1 conv3: Cin 64), where a 128-column tile is half empty:
+    // 10 / 11 = 64|128 x 64 on 4 waves with a 1- / 2-stage ring, 12 = 256 x 64 on 8 waves (Cout >= 256)
+    if (p.stages == 12) {
+      if (p.Cout < 256) return 2;
+      ok = launch_wg<256, 64, 4, 2, 1, 2>(p, splits, stream);
+    } else if (p.Cout <= 64) {
+      ok = p.stages == 10 ? launch_wg<64, 64, 2, 2, 1, 1>(p, splits, stream) : launch_wg<64, 64, 2, 2, 1, 2>(p, splits, stream);
+    } else {
+      ok = p.stages == 10 ? launch_wg<128, 64, 2, 2, 1, 1>(p, splits, stream)
+                          : launch_wg<128, 64, 2, 2, 1, 2>(p, splits, stream);
+    }
+  } else if (dma && (p.stages == 7 || p.stages == 9)) {  // 256 x 256, 8 waves, 4- / 3-deep ring of 32-pixel stages
     if (p.Cout < 256) return 2;
     if (p.stages == 7) ok = launch_wg<256, 256, 2, 4, 1, 4, 32>(p, splits, stream);
     else ok = launch_wg<256, 256, 2, 4, 1, 3, 32>(p, splits, stream);

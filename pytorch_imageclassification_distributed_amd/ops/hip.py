@@ -460,7 +460,7 @@ def load_tuning(path: str) -> int:
             k, v = ast.literal_eval(ks), tuple(int(x) for x in v)
         except (ValueError, SyntaxError, TypeError):
             continue
-        if len(v) == 2 and 1 <= v[1] <= 9 and v[0] > 0 and k not in _WGRAD_TUNED:
+        if len(v) == 2 and 1 <= v[1] <= 12 and v[0] > 0 and k not in _WGRAD_TUNED:
             _WGRAD_TUNED[k] = v
             n += 1
     return n
@@ -798,9 +798,11 @@ def _wgrad_launch(dy, x, out, g: ConvGeom, m, ntot, kps, splits, stages=2, side=
 
 def _wgrad_tiles(co, ntot, stages):
     """Output tiles of one wgrad launch: 256 x 256 for the 8-wave kernels (stages 4, 7, 9), 32 x 128 for
-    stages 5 / 6, else 64|128 x 128."""
+    stages 5 / 6, 64-column tiles for stages 10 / 11 (64|128 rows) and 12 (256 rows), else 64|128 x 128."""
     if stages in (4, 7, 9):
         return (-(-co // 256)) * (-(-ntot // 256))
+    if stages >= 10:
+        return (-(-co // (256 if stages == 12 else 64 if co <= 64 else 128))) * (-(-ntot // 64))
     return (-(-co // (32 if stages in (5, 6) else 64 if co <= 64 else 128))) * (-(-ntot // 128))
 
 
@@ -848,6 +850,10 @@ def _wgrad_config(dy, x, g: ConvGeom, m, ntot, xa=None, xf=None):
         cands += [(cand, 8) for cand in blocks if cand <= 1024]
         if g.Co <= 32:  # 32-row tiles: a 64-row tile would be half empty
             cands += [(cand, st) for st in (5, 6) for cand in blocks]
+        if ntot <= 64:  # 64-column tiles: a 128-column tile would be half empty (ResNet layer1 conv3)
+            cands += [(cand, st) for st in (10, 11) for cand in blocks]
+            if g.Co >= 256:
+                cands += [(cand, 12) for cand in blocks if cand <= 1024]
         # (64 / 128 x 256 four-wave tiles, reading the narrow layers' dY half as often, were 5-70 % slower
         # on every ResNet-50 shape: profiles/r4d_wgrad_wide_tiles_probe.txt)
     if fx or ff:

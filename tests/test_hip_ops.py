@@ -95,8 +95,9 @@ N_FP8_CFG = _table_len("conv_fp8_cfgs", 8)
 
 
 def _wgrad_stage_ok(case, stages):
-    # stages 4 / 7 / 9 = 256x256 8-wave tile (Cout >= 256), 5/6 = 32-row tile (Cout <= 32), 8 = any
-    return not ((stages in (4, 7, 9) and case[4] < 256) or (stages in (5, 6) and case[4] > 32))
+    # stages 4 / 7 / 9 = 256x256 8-wave tile (Cout >= 256), 5/6 = 32-row tile (Cout <= 32), 8 = any,
+    # 10 / 11 = 64-column tiles (any), 12 = 256 x 64 (Cout >= 256)
+    return not ((stages in (4, 7, 9, 12) and case[4] < 256) or (stages in (5, 6) and case[4] > 32))
 
 
 @pytest.mark.parametrize("cfg", range(N_CFG))
@@ -163,7 +164,8 @@ def test_conv_bn_act_halo(act, use_res, cfg):
 
 
 @pytest.mark.parametrize("case,stages", [
-    (c, st) for c in [CONV_CASES[i] for i in (0, 1, 3, 4, 5, 6, 7, 8, 12, 13, 14)] for st in (1, 2, 3, 4, 5, 6, 7, 8, 9)
+    (c, st) for c in [CONV_CASES[i] for i in (0, 1, 3, 4, 5, 6, 7, 8, 12, 13, 14)]
+    for st in (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12)
     if _wgrad_stage_ok(c, st)])
 def test_conv_wgrad_ring_variants(case, stages):
     """Weight-gradient kernel variants: 1-stage (occupancy), 2-stage ring, the 8-wave in-block
