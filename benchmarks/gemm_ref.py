@@ -64,7 +64,7 @@ def main():
                 continue
             res[f"{tm}x{bn}/{wm}x{wn}/s{st}#{i}"] = timeit(
                 lambda: hip.C.conv_gemm(A, B.view(-1), out, None, None, *geo, [0], [0], [0], hip.G_STATS, zero,
-                                        None, None, None, None, None, 0, 1, 0, 0, i, None, None, None, None, None, None, None, 0, None))
+                                        None, None, None, None, None, 0, 1, 0, 0, i, None, None, None, None, None, None, None, 0, None, None, None, None, 0))
         ref = torch.mm(A, B.t())
         err = ((out.float() - ref.float()).abs().max() / ref.float().abs().max()).item()
         best = min(res, key=res.get)

@@ -53,7 +53,7 @@ def main():
             continue
         for st in (None, stats):
             t = timeit(lambda: C.conv_gemm(xs, wq, y, st, None, *geo, dh, dw, tb, grp, zero, None,
-                                           None, None, None, None, 0, 1, 0, 0, i, None, None, None, None, None, None, None, 0, None))
+                                           None, None, None, None, 0, 1, 0, 0, i, None, None, None, None, None, None, None, 0, None, None, None, None, 0))
             print(f"  cfg {cfg}: {'stats' if st is not None else 'plain'} {t:7.1f} us  "
                   f"{(m * 64 * 2 + xs.numel() * 2) / t / 1e6:5.2f} TB/s")
     for st in (None, stats):

@@ -169,7 +169,7 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
                std::vector<int> dh, std::vector<int> dw, std::vector<int> tb, int stats_groups, Tensor zero,
                OT addend, OT bwd_y, OT bwd_res, OT bwd_coef, OT bwd_part, int bwd_act, int bwd_groups,
                int stages, int tile_n, int cfg, OT a_sc, OT b_sc, OT xa_y, OT xa_coef, OT xa_out, OT stats_shift,
-               OT xf_coef, int xf_act, OT bwd_mask) {
+               OT xf_coef, int xf_act, OT bwd_mask, OT fw_x, OT fw_ws, OT fw_dw, int fw_blocks) {
   const bool fp8 = a_sc.has_value() && a_sc->defined();
   TORCH_CHECK(A.scalar_type() == (fp8 ? at::kFloat8_e4m3fn : BF) && B.scalar_type() == A.scalar_type(),
               "conv_gemm: A and B must both be bf16, or both float8_e4m3fn with scales");
@@ -249,6 +249,19 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
                 "conv_gemm: the fused BN-apply A operand needs bf16, [2][CA] coefficients, CA % 64 == 0, no bias, "
                 "identity or ReLU");
     TORCH_CHECK(cfg < 0 || conv_cfg_has_xa(cfg), "conv_gemm: configuration has no fused BN-apply variant");
+  }
+  if (fw_x.has_value() && fw_x->defined()) {
+    // fused XA 1x1 backward: this data-gradient launch also produces the weight gradient (fw_dw += ...)
+    req(*fw_x, BF, "fw_x");
+    TORCH_CHECK(fw_ws.has_value() && fw_dw.has_value() && fw_ws->scalar_type() == F32 && fw_dw->scalar_type() == F32 &&
+                    fw_x->numel() == (long long)M * Ncols && fw_dw->numel() == (long long)CA * Ncols &&
+                    fw_blocks > 0 && fw_ws->numel() >= (long long)fw_blocks * CA * Ncols && p.xa_y,
+                "conv_gemm: fused backward needs X [M][Ncols], dW [CA*Ncols] fp32, a workspace of blocks*CA*Ncols "
+                "floats and the XA operand");
+    check(conv_fused_bwd_launch(p, ptr<bf16_t>(*fw_x), fw_ws->data_ptr<float>(), fw_dw->data_ptr<float>(), fw_blocks,
+                                cur()),
+          "conv_fused_bwd");
+    return;
   }
   check(conv_gemm_launch(p, cur()), "conv_gemm");
 }

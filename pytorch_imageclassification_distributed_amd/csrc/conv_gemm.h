@@ -108,6 +108,7 @@ int conv_halo_num();
 void conv_halo_info(int i, int* out6);  // {tile rows, tile channels, waves M, waves N, weight ring depth, patch rows}
 int conv_halo_launch(int i, const ConvParams& p, hipStream_t stream);  // 3: geometry not handled
 int conv_wgrad_launch(const WgradParams& p, int splits, hipStream_t stream);
+int conv_fused_bwd_launch(const ConvParams& p, const bf16_t* X, float* ws, float* dW, int blocks, hipStream_t stream);
 bool conv_wgrad_has_xa(int stages);  // the wgrad variant selected by ``stages`` has a fused BN-backward dY form
 bool conv_wgrad_has_xf(int stages);  // ... a fused BN-apply X form (alone or together with the dY form)
 void conv_set_wgrad_variant(int v);  // 0 = auto, 1 = register-staged, 2 = LDS-DMA

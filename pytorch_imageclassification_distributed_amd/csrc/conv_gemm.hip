@@ -1322,6 +1322,218 @@ static void launch_wgrad_reduce(const float* ws, float* dW, long n4, int splits,
                      (const f32x4*)ws, (f32x4*)dW, n4, splits);
 }
 
+
+// ---------------------------------------------------------------------------
+// Fused backward of a 1x1 stride-1 conv whose output fed a BN (XA) and whose input has CIN = 64 channels
+// (ResNet layer1 conv3: 64 -> 256): ONE pass over dz and y forms dY = c0*dz + c1*y + c2 in LDS and feeds
+// both GEMMs from it - the data gradient dX = dY * W (+ the producer BN's fused backward epilogue) and the
+// weight gradient dW += dY^T X.  Separately, the XA dgrad and the XA wgrad each read dz and y (4 tensor
+// passes of the conv's widest tensors); here they are read once.  Persistent blocks walk 128-pixel tiles;
+// the dW partial (CO x 64 fp32, 16-64 VGPRs per lane) stays in registers across a block's tiles and goes to
+// the split-K workspace once at the end (wgrad_reduce_kernel sums the blocks' slabs in a fixed order).
+//
+// Per tile: the X tile [128 px][64 ch] lands once by LDS-DMA; each 64-channel k-step of dz (A), y (register
+// load), the k-step's coefficients and the transposed weight rows (B) land by LDS-DMA into the 1-stage ring,
+// every wave rewrites its own dz pieces to dY, and then the dgrad MFMAs read A row-wise (ds_read_b128) while
+// the wgrad MFMAs read A and X column-wise (ds_read_b64_tr_b16) - the same LDS image serves both.
+// ---------------------------------------------------------------------------
+struct FusedW {
+  const bf16_t* X;  // [M][64] conv input (the dgrad's output layout)
+  float* ws;        // [gridDim.x][CO][64] fp32 partial dW slabs
+};
+
+// 8 waves (2 per SIMD, one block per CU): each wave holds a 32 x 32 dgrad tile and a 16 x 32 slice of every
+// k-step's 64 x 64 dW block (CO / 2 fp32 accumulators per lane), which keeps CO = 256 within 256 VGPRs
+template <int CO, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN, 2) void conv_fused_bwd_kernel(const ConvParams p, const FusedW f) {
+  constexpr int TM = 128, BNc = 64, NW = WM * WN;
+  constexpr int WTM = TM / WM, WTN = BNc / WN;       // dgrad wave tile
+  constexpr int RM = WTM / 16, RN = WTN / 16;
+  constexpr int AL = TM / 8 / NW, BL = BNc / 8 / NW; // LDS-DMA pieces per wave per k-step
+  constexpr int QM = 64 / WM / 16, QN = 64 / WN / 16; // wgrad: 16-blocks of each k-step's 64 x 64 dW per wave
+  static_assert(AL >= 1 && BL >= 1 && QM >= 1 && QN >= 1 && (TM / NW) % 16 == 0, "fused backward mapping");
+  constexpr int A_BYTES = TM * BK * 2, B_BYTES = BNc * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES + NW * 1024;
+  constexpr int X_BYTES = TM * 128;
+  constexpr int NKC = CO / BK;                       // k-steps (64-channel chunks of dz)
+  constexpr int EPI = TM * (BNc + 8) * 2;
+  constexpr int MAIN = STAGE + X_BYTES > EPI ? STAGE + X_BYTES : EPI;
+  static_assert(CO % BK == 0 && CO <= 256, "fused backward: CO in {64, 128, 192, 256}");
+  __shared__ __attribute__((aligned(16))) char smem[MAIN];
+  char* const sa = smem;
+  char* const sb = smem + A_BYTES;
+  char* const sk = smem + A_BYTES + B_BYTES;
+  char* const sx = smem + STAGE;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int lrow = lane >> 3, pch = lane & 7;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int g4 = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
+  const int CA = p.CA;  // == CO (the dz row stride)
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.A, 2 * p.a_elems);
+  const __amdgpu_buffer_rsrc_t rsZ = make_rsrc(p.xa_y, 2 * p.a_elems);
+  const __amdgpu_buffer_rsrc_t rsK = make_rsrc(p.xa_coef, 12L * CA);
+  const __amdgpu_buffer_rsrc_t rsB = make_rsrc(p.B, 2 * p.b_elems);
+  const __amdgpu_buffer_rsrc_t rsX = make_rsrc(f.X, 2L * p.M * BNc);
+  // weight rows (n = input channel) of the transposed weight, per-lane chunk swizzle as conv_gemm_glds_kernel
+  unsigned b_row[BL];
+#pragma unroll
+  for (int i = 0; i < BL; ++i) {
+    const int row = wid * (BNc / NW) + i * 8 + lrow;
+    b_row[i] = 2u * (unsigned)(row * p.ldb + (pch ^ ((row >> 1) & 7)) * 8);
+  }
+  // dY-image address of (pixel row r, channel c), c a multiple of 4 (the glds swizzle)
+  auto a_addr = [](int r, int c) { return r * 128 + ((((c >> 3) ^ ((r >> 1) & 7))) << 4) + (c & 7) * 2; };
+
+  f32x4 accw[NKC][QM][QN];  // dW[kc*64 + wm*16*QM + i*16 + fr][wn*16*QN + j*16 + fq*4 + r]
+#pragma unroll
+  for (int c = 0; c < NKC; ++c)
+#pragma unroll
+    for (int i = 0; i < QM; ++i)
+#pragma unroll
+      for (int j = 0; j < QN; ++j) accw[c][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int ntiles = (p.M + TM - 1) / TM;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int m0 = tile * TM;
+    // X tile: 128 pixel rows x 128 B, rows past M land zeros (they add nothing to dW)
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      const int row = wid * (TM / NW) + i * 8 + lrow;
+      const int m = m0 + row;
+      const unsigned off = m < p.M ? 2u * (unsigned)(m * BNc + (pch ^ ((row >> 1) & 7)) * 8) : OOB;
+      blds16(rsX, off, sx + (wid * (TM / NW) + i * 8) * 128);
+    }
+    f32x4 acc[RM][RN];
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kc = 0; kc < NKC; ++kc) {
+      if (kc > 0) __builtin_amdgcn_s_barrier();  // every wave is done reading the previous k-step
+      // issue: dz pieces (A), y pieces (registers), the k-step's coefficients, weight rows (B)
+      unsigned va[AL];
+      uint4 yv[AL];
+#pragma unroll
+      for (int i = 0; i < AL; ++i) {
+        const int row = wid * (TM / NW) + i * 8 + lrow;
+        const int m = m0 + row;
+        va[i] = m < p.M ? 2u * (unsigned)(m * CA + kc * BK + (pch ^ ((row >> 1) & 7)) * 8) : OOB;
+        blds16(rsA, va[i], sa + (wid * (TM / NW) + i * 8) * 128);
+      }
+#pragma unroll
+      for (int i = 0; i < BL; ++i) blds16(rsB, b_row[i] + 2u * (unsigned)(kc * BK), sb + (wid * (BNc / NW) + i * 8) * 128);
+      {
+        const unsigned ko = lane < 48 ? 4u * (unsigned)((lane >> 4) * CA + kc * BK + (lane & 15) * 4) : OOB;
+        blds16(rsK, ko, sk + wid * 1024);
+      }
+#pragma unroll
+      for (int i = 0; i < AL; ++i) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsZ, va[i], 0, 0);
+        yv[i] = *(const uint4*)&v;
+      }
+      wait_vmcnt<0>();
+      // this wave's dz pieces -> dY in place (rows past M stay zero)
+      {
+        const float* kcf = (const float*)(sk + wid * 1024);
+#pragma unroll
+        for (int gg = 0; gg < 2; ++gg) {
+          const int ch = (pch ^ (((gg * 4 + (lrow >> 1)) & 7))) * 8;
+          float c0[8], c1[8], c2[8];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            *(f32x4*)(c0 + 4 * h) = *(const f32x4*)(kcf + ch + 4 * h);
+            *(f32x4*)(c1 + 4 * h) = *(const f32x4*)(kcf + 64 + ch + 4 * h);
+            *(f32x4*)(c2 + 4 * h) = *(const f32x4*)(kcf + 128 + ch + 4 * h);
+          }
+#pragma unroll
+          for (int i = gg; i < AL; i += 2) {
+            if (va[i] == OOB) continue;
+            uint4* dst = (uint4*)(sa + (wid * (TM / NW) + i * 8) * 128 + lane * 16);
+            float d[8], y[8];
+            unpack8(*dst, d);
+            unpack8(yv[i], y);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) d[k] = fmaf(c0[k], d[k], fmaf(c1[k], y[k], c2[k]));
+            *dst = pack8(d);
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      // data gradient: dX[px][ci] += dY[px][k] W^T[ci][k]   (row-wise fragments)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 af[RM], bfg[RN];
+#pragma unroll
+        for (int i = 0; i < RM; ++i) af[i] = *(const bf16x8*)(sa + swz(wm * WTM + i * 16 + fr, 4 * kk + fq));
+#pragma unroll
+        for (int j = 0; j < RN; ++j) bfg[j] = *(const bf16x8*)(sb + swz(wn * WTN + j * 16 + fr, 4 * kk + fq));
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+#pragma unroll
+          for (int i = 0; i < RM; ++i)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[j], af[i], acc[i][j], 0, 0, 0);
+      }
+      // weight gradient of this k-step's 64 output channels: dW[co][ci] += sum_px dY[px][co] X[px][ci]
+      // (column-wise fragments by transposed reads; k order permuted identically for both operands)
+#pragma unroll
+      for (int kk = 0; kk < TM / 32; ++kk) {
+        const int r0 = kk * 32 + 4 * g4 + tq, r1 = r0 + 16;
+        bf16x8 ad[QM], bx[QN];
+#pragma unroll
+        for (int i = 0; i < QM; ++i) {
+          const int c = wm * 16 * QM + i * 16 + tp * 4;
+          const bf16x4 lo = tr_read(sa + a_addr(r0, c)), hi = tr_read(sa + a_addr(r1, c));
+          ad[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+#pragma unroll
+        for (int j = 0; j < QN; ++j) {
+          const int c = wn * 16 * QN + j * 16 + tp * 4;
+          const bf16x4 lo = tr_read(sx + a_addr(r0, c)), hi = tr_read(sx + a_addr(r1, c));
+          bx[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+#pragma unroll
+        for (int i = 0; i < QM; ++i)
+#pragma unroll
+          for (int j = 0; j < QN; ++j)
+            accw[kc][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx[j], ad[i], accw[kc][i][j], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+    conv_epilogue_dispatch<TM, BNc, WM, WN, 1>(p, acc, smem, tid, lane, wid, wm, wn, m0, 0, tile, p.GH * p.GW);
+    __syncthreads();  // the epilogue's LDS is the next tile's X image / ring
+  }
+  // this block's dW partial -> its workspace slab (plain 16-B stores; the reduce adds the slabs in order)
+  float* slab = f.ws + (long)blockIdx.x * CO * BNc;
+#pragma unroll
+  for (int c = 0; c < NKC; ++c)
+#pragma unroll
+    for (int i = 0; i < QM; ++i)
+#pragma unroll
+      for (int j = 0; j < QN; ++j) {
+        const int co = c * 64 + wm * 16 * QM + i * 16 + fr, ci = wn * 16 * QN + j * 16 + fq * 4;
+        *(f32x4*)(slab + (long)co * BNc + ci) = accw[c][i][j];
+      }
+}
+
+template <int CO>
+static int launch_fused_bwd(const ConvParams& p, const FusedW& f, float* dW, int blocks, hipStream_t stream) {
+  hipLaunchKernelGGL((conv_fused_bwd_kernel<CO, 4, 2>), dim3(blocks), dim3(512), 0, stream, p, f);
+  HIP_CHECK_LAUNCH();
+  const long n4 = (long)CO * 64 / 4;
+  if (blocks >= 128) launch_wgrad_reduce<16>(f.ws, dW, n4, blocks, stream);
+  else if (blocks >= 64) launch_wgrad_reduce<8>(f.ws, dW, n4, blocks, stream);
+  else if (blocks >= 32) launch_wgrad_reduce<4>(f.ws, dW, n4, blocks, stream);
+  else if (blocks >= 16) launch_wgrad_reduce<2>(f.ws, dW, n4, blocks, stream);
+  else launch_wgrad_reduce<1>(f.ws, dW, n4, blocks, stream);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
 }  // namespace
 
 static int g_variant = 0;
@@ -1587,4 +1799,22 @@ int conv_wgrad_launch(const WgradParams& p_in, int splits, hipStream_t stream) {
     HIP_CHECK_LAUNCH();
   }
   return 0;
+}
+
+// fused XA 1x1 backward (conv_fused_bwd_kernel): p = the XA data-gradient launch (1x1, stride 1, Ncols 64,
+// CA = CO in {64, 128, 192, 256}), X = the conv input [M][64], ws >= blocks * CO * 64 floats, dW [CO][64]
+// += sum of the blocks' partials.  3 = geometry not handled.
+int conv_fused_bwd_launch(const ConvParams& p, const bf16_t* X, float* ws, float* dW, int blocks, hipStream_t stream) {
+  if (!p.xa_y || !p.xa_coef || p.Ncols != 64 || p.CA % BK || p.CA > 256 || p.K != p.CA || p.ntaps != 1 ||
+      p.tap_dh[0] || p.tap_dw[0] || p.sA != 1 || p.GH != p.IH || p.GW != p.IW || p.so != 1 || p.ldc != 64 ||
+      p.c_off || p.stats || p.bias || p.a_sc || p.xf_coef || blocks <= 0)
+    return 3;
+  const FusedW f{X, ws};
+  switch (p.CA) {
+    case 64: return launch_fused_bwd<64>(p, f, dW, blocks, stream);
+    case 128: return launch_fused_bwd<128>(p, f, dW, blocks, stream);
+    case 192: return launch_fused_bwd<192>(p, f, dW, blocks, stream);
+    case 256: return launch_fused_bwd<256>(p, f, dW, blocks, stream);
+    default: return 3;
+  }
 }

@@ -511,7 +511,7 @@ def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(
                        cfg[2] - DIRECT_BASE, bwd, shift)
         return
     C.conv_gemm(A, B, out, stats, bias, *geo, dh, dw, tb, groups, zero, addend, *bwd, *cfg, *scales, *xa3, shift,
-                *xf2, mask)
+                *xf2, mask, None, None, None, 0)
 
 
 _CFGS = None
@@ -654,7 +654,7 @@ def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, group
     times = {}
     for cfg in cands:
         times[cfg] = _time_ms(lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, groups, zero,
-                                                  addend, *bwd, *cfg, *scales, *xa3, None, *xf2, mask))
+                                                  addend, *bwd, *cfg, *scales, *xa3, None, *xf2, mask, None, None, None, 0))
     if HALO_CONV and not fused and scales[0] is None:
         for v, (tm, bn, _wm, _wn, _bst, pmax) in enumerate(conv_halo_cfgs()):
             if v not in HALO_TUNE or not _halo_ok(geo, dh, dw, tm, pmax) or (bn > 64 and bn >= 2 * geo[1]) or \
@@ -662,7 +662,7 @@ def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, group
                 continue
             cfg = (0, 0, HALO_BASE + v)
             times[cfg] = _time_ms(lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, groups, zero,
-                                                      addend, *bwd, *cfg, *scales, *xa3, None, *xf2, mask))
+                                                      addend, *bwd, *cfg, *scales, *xa3, None, *xf2, mask, None, None, None, 0))
     dg = _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales) if not fused else None
     if dg is not None:
         for v, (cip, cot) in DIRECT_CFGS.items():
@@ -708,6 +708,48 @@ def _conv_forward_fp8(x, w_param, g: ConvGeom, stats, bias, out, c_off, shift=No
     _conv_gemm(xq, wq, y, stats, bias, geo, dh, dw, tb, ws(dev).zero, groups=stat_groups(geo[0]),
                scales=(xs, wsc), shift=shift)
     return y
+
+
+# Fused XA backward of a 1x1 stride-1 conv with 64 input channels (ResNet layer1 conv3, csrc/conv_gemm.hip
+# conv_fused_bwd_kernel): one pass over dz and y feeds both the data gradient (+ its BN-backward epilogue) and
+# the weight gradient, instead of each GEMM reading dz and y (IMGCLS_FUSED_BWD=0: separate launches).
+FUSED_BWD = os.environ.get("IMGCLS_FUSED_BWD", "1") == "1"
+FUSED_BWD_COUNT = [0]
+_CU_COUNT: dict = {}
+
+
+def fused_bwd_eligible(g: ConvGeom, xa) -> bool:
+    return (FUSED_BWD and xa is not None and g.kh == 1 and g.kw == 1 and g.sh == 1 and g.sw == 1
+            and g.pt == 0 and g.pl == 0 and g.Cx == g.Ci == 64 and g.Co % 64 == 0 and g.Co <= 256
+            and g.OH == g.H and g.OW == g.W)
+
+
+def conv_fused_bwd_raw(dz, x, w_param, g: ConvGeom, xa, addend=None, link=None):
+    """dX (as ``conv_dgrad_raw`` with ``xa``) and dW (into the parameter's arena slot or a fresh gradient
+    buffer) of a ``fused_bwd_eligible`` conv from one launch; returns (dx, dw)."""
+    dev = dz.device
+    bwd = (None, None, None, None, 0, 1)
+    mask = None
+    if link is not None:
+        grp = stat_groups(g.N * g.H * g.W)
+        link.part = ws(dev).take_part(g.Ci, grp)
+        bwd = (link.y, link.res, link.coef, link.part, link.act, grp)
+        mask = link.mask
+    wt = weight_bf16_t(w_param, g.Co, g.T, g.Ci)
+    dx = _empty_cl(g.N, g.Ci, g.H, g.W, dev)
+    dw = arena_slot(w_param)
+    if dw is None:
+        dw = grad_buffer(w_param)
+    blocks = _CU_COUNT.get(dev.index)
+    if blocks is None:
+        blocks = _CU_COUNT[dev.index] = torch.cuda.get_device_properties(dev).multi_processor_count
+    wsp = _wgrad_ws(dev, blocks * g.Co * g.Ci)
+    m = g.N * g.H * g.W
+    geo = (m, g.Ci, g.Co, g.Co, g.H, g.W, g.OH, g.OW, 1, g.Co, g.H, g.W, 1, 0, 0, g.Ci, 0)
+    C.conv_gemm(dz, wt, dx, None, None, *geo, [0], [0], [0], G_STATS, ws(dev).zero, addend, *bwd, 0, 0, -1, None, None,
+                xa[0], xa[1], None, None, None, 0, mask, x, wsp, dw.view(-1), blocks)
+    FUSED_BWD_COUNT[0] += 1
+    return dx, dw
 
 
 def conv_dgrad_raw(dy, w_param, g: ConvGeom, addend=None, link=None, xa=None):
@@ -1230,7 +1272,11 @@ class ConvFn(torch.autograd.Function):
                 link = None  # the producer's BN reduce needs the full gradient
             # running sum of the other consumers' contributions rides in as the dgrad addend
             addend = slot.t if (slot is not None and g.Cx == g.Ci) else None
-            dx = conv_dgrad_raw(dy, w, g, addend=addend, link=link, xa=xa)
+            if ctx.needs_input_grad[1] and fused_bwd_eligible(g, xa):
+                dx, dw_fused = conv_fused_bwd_raw(dy, x, w, g, xa, addend=addend, link=link)
+            else:
+                dw_fused = None
+                dx = conv_dgrad_raw(dy, w, g, addend=addend, link=link, xa=xa)
             if link is not None:
                 link.done = True
                 if link.group is not None:
@@ -1239,7 +1285,12 @@ class ConvFn(torch.autograd.Function):
                     _syncbn_bwd_start(link)
             if slot is not None:
                 dx = slot.deliver(dx, fused=addend is not None)
-        dw = conv_wgrad_raw(dy, x, w, g, xa=xa, xf=ctx.xf) if ctx.needs_input_grad[1] else None
+        else:
+            dw_fused = None
+        if dw_fused is not None:
+            dw = dw_fused
+        else:
+            dw = conv_wgrad_raw(dy, x, w, g, xa=xa, xf=ctx.xf) if ctx.needs_input_grad[1] else None
         return dx, dw, None, None, None, None, None, None, None
 
 

@@ -361,3 +361,30 @@ def test_relu_mask_matches_residual_recompute(kind, fp8):
     assert err(gx1, gx0) < 1e-2, err(gx1, gx0)
     for n in gp0:
         assert err(gp1[n], gp0[n]) < 1e-2, (n, err(gp1[n], gp0[n]))
+
+
+@pytest.mark.parametrize("n_blocks,hw", [(2, 16), (1, 15)])
+def test_fused_xa_backward_matches_separate(n_blocks, hw):
+    """conv_fused_bwd_kernel (ResNet layer1 conv3: 64 -> 256, XA): one pass over dz and y gives the data
+    gradient with its BN-backward epilogue and the weight gradient - the same values as the separate XA dgrad
+    and XA wgrad launches (odd map: partial last pixel tile)."""
+    import torch.nn as nn
+    from pytorch_imageclassification_distributed_amd.models.resnet import Bottleneck
+    from pytorch_imageclassification_distributed_amd.ops import hip
+    torch.manual_seed(0)
+    blk = nn.Sequential(*[Bottleneck(256, 64) for _ in range(n_blocks)]).to(DEV).to(memory_format=torch.channels_last)
+    x = torch.randn(4, 256, hw, hw, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    keep = hip.FUSED_BWD
+    try:
+        hip.FUSED_BWD = False
+        gx0, gp0 = _grads(blk, x, True)
+        hip.FUSED_BWD = True
+        before = hip.FUSED_BWD_COUNT[0]
+        gx1, gp1 = _grads(blk, x, True)
+        assert hip.FUSED_BWD_COUNT[0] - before == n_blocks
+    finally:
+        hip.FUSED_BWD = keep
+    err = lambda a, b: ((a - b).abs().max() / b.abs().max().clamp(min=1e-6)).item()  # noqa: E731
+    assert err(gx1, gx0) < 1e-2, err(gx1, gx0)
+    for n in gp0:
+        assert err(gp1[n], gp0[n]) < 1e-2, (n, err(gp1[n], gp0[n]))
