@@ -1728,7 +1728,9 @@ static bool launch_wg(const WgradParams& p, int splits, hipStream_t stream) {
 
 // variants with a fused BN-backward form: all but the 256 x 256 tile with a 2-deep 64-pixel ring (its
 // register y pieces spill at 2 waves per SIMD; LDS y would not fit) and the 4-deep 256 x 256 ring (LDS)
-bool conv_wgrad_has_xa(int stages) { return stages >= 1 && stages <= 12 && stages != 4 && stages != 7; }
+bool conv_wgrad_has_xa(int stages) {
+  return stages >= 1 && stages <= 12 && stages != 4 && stages != 7 && stages != 12;
+}
 // the fused BN-apply X form needs no register operand: every LDS-DMA variant has it
 bool conv_wgrad_has_xf(int stages) { return stages >= 1 && stages <= 12; }
 

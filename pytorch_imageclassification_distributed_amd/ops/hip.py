@@ -713,13 +713,13 @@ def _conv_forward_fp8(x, w_param, g: ConvGeom, stats, bias, out, c_off, shift=No
 # Fused XA backward of a 1x1 stride-1 conv with 64 input channels (ResNet layer1 conv3, csrc/conv_gemm.hip
 # conv_fused_bwd_kernel): one pass over dz and y feeds both the data gradient (+ its BN-backward epilogue) and
 # the weight gradient, instead of each GEMM reading dz and y (IMGCLS_FUSED_BWD=0: separate launches).
-FUSED_BWD = os.environ.get("IMGCLS_FUSED_BWD", "1") == "1"
-FUSED_BWD_COUNT = [0]
+FUSED_XA_BWD = os.environ.get("IMGCLS_FUSED_BWD", "1") == "1"
+FUSED_XA_BWD_COUNT = [0]  # fused dgrad + wgrad launches (tests / diagnostics)
 _CU_COUNT: dict = {}
 
 
 def fused_bwd_eligible(g: ConvGeom, xa) -> bool:
-    return (FUSED_BWD and xa is not None and g.kh == 1 and g.kw == 1 and g.sh == 1 and g.sw == 1
+    return (FUSED_XA_BWD and xa is not None and g.kh == 1 and g.kw == 1 and g.sh == 1 and g.sw == 1
             and g.pt == 0 and g.pl == 0 and g.Cx == g.Ci == 64 and g.Co % 64 == 0 and g.Co <= 256
             and g.OH == g.H and g.OW == g.W)
 
@@ -748,7 +748,7 @@ def conv_fused_bwd_raw(dz, x, w_param, g: ConvGeom, xa, addend=None, link=None):
     geo = (m, g.Ci, g.Co, g.Co, g.H, g.W, g.OH, g.OW, 1, g.Co, g.H, g.W, 1, 0, 0, g.Ci, 0)
     C.conv_gemm(dz, wt, dx, None, None, *geo, [0], [0], [0], G_STATS, ws(dev).zero, addend, *bwd, 0, 0, -1, None, None,
                 xa[0], xa[1], None, None, None, 0, mask, x, wsp, dw.view(-1), blocks)
-    FUSED_BWD_COUNT[0] += 1
+    FUSED_XA_BWD_COUNT[0] += 1
     return dx, dw
 
 

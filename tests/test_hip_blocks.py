@@ -374,16 +374,16 @@ def test_fused_xa_backward_matches_separate(n_blocks, hw):
     torch.manual_seed(0)
     blk = nn.Sequential(*[Bottleneck(256, 64) for _ in range(n_blocks)]).to(DEV).to(memory_format=torch.channels_last)
     x = torch.randn(4, 256, hw, hw, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    keep = hip.FUSED_BWD
+    keep = hip.FUSED_XA_BWD
     try:
-        hip.FUSED_BWD = False
+        hip.FUSED_XA_BWD = False
         gx0, gp0 = _grads(blk, x, True)
-        hip.FUSED_BWD = True
-        before = hip.FUSED_BWD_COUNT[0]
+        hip.FUSED_XA_BWD = True
+        before = hip.FUSED_XA_BWD_COUNT[0]
         gx1, gp1 = _grads(blk, x, True)
-        assert hip.FUSED_BWD_COUNT[0] - before == n_blocks
+        assert hip.FUSED_XA_BWD_COUNT[0] - before == n_blocks
     finally:
-        hip.FUSED_BWD = keep
+        hip.FUSED_XA_BWD = keep
     err = lambda a, b: ((a - b).abs().max() / b.abs().max().clamp(min=1e-6)).item()  # noqa: E731
     assert err(gx1, gx0) < 1e-2, err(gx1, gx0)
     for n in gp0:
