@@ -1272,7 +1272,7 @@ class ConvFn(torch.autograd.Function):
                 link = None  # the producer's BN reduce needs the full gradient
             # running sum of the other consumers' contributions rides in as the dgrad addend
             addend = slot.t if (slot is not None and g.Cx == g.Ci) else None
-            if ctx.needs_input_grad[1] and fused_bwd_eligible(g, xa):
+            if ctx.needs_input_grad[1] and ctx.xf is None and fused_bwd_eligible(g, xa):  # (XF: X is y, not act(bn(y)))
                 dx, dw_fused = conv_fused_bwd_raw(dy, x, w, g, xa, addend=addend, link=link)
             else:
                 dw_fused = None
