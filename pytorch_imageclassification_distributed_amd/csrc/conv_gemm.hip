@@ -1343,7 +1343,11 @@ struct FusedW {
 };
 
 // 8 waves (2 per SIMD, one block per CU): each wave holds a 32 x 32 dgrad tile and a 16 x 32 slice of every
-// k-step's 64 x 64 dW block (CO / 2 fp32 accumulators per lane), which keeps CO = 256 within 256 VGPRs
+// k-step's 64 x 64 dW block (CO / 2 fp32 accumulators per lane), which keeps CO = 256 within 256 VGPRs.
+// The (tile, k-step) sequence of a block is one flat stream on a 2-deep ring: step s + 1's dz / weight /
+// coefficient DMAs and y loads (and, on a tile's first k-step, its X tile into the other X buffer) are issued
+// right after step s's barrier, so they land during step s's MFMAs and the previous tile's epilogue; the
+// epilogue stages through its own LDS region.
 template <int CO, int WM, int WN>
 __global__ __launch_bounds__(64 * WM * WN, 2) void conv_fused_bwd_kernel(const ConvParams p, const FusedW f) {
   constexpr int TM = 128, BNc = 64, NW = WM * WN;
@@ -1356,14 +1360,10 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_fused_bwd_kernel(const C
   constexpr int STAGE = A_BYTES + B_BYTES + NW * 1024;
   constexpr int X_BYTES = TM * 128;
   constexpr int NKC = CO / BK;                       // k-steps (64-channel chunks of dz)
-  constexpr int EPI = TM * (BNc + 8) * 2;
-  constexpr int MAIN = STAGE + X_BYTES > EPI ? STAGE + X_BYTES : EPI;
-  static_assert(CO % BK == 0 && CO <= 256, "fused backward: CO in {64, 128, 192, 256}");
+  constexpr int EPI = TM * (BNc + 8) * 2 > NW * 2 * BNc * 4 ? TM * (BNc + 8) * 2 : NW * 2 * BNc * 4;
+  constexpr int RING = 2 * STAGE, XOFF = RING, EOFF = RING + 2 * X_BYTES, MAIN = EOFF + EPI;
+  static_assert(CO % BK == 0 && CO <= 256 && MAIN <= 160 * 1024, "fused backward: CO in {64, 128, 192, 256}");
   __shared__ __attribute__((aligned(16))) char smem[MAIN];
-  char* const sa = smem;
-  char* const sb = smem + A_BYTES;
-  char* const sk = smem + A_BYTES + B_BYTES;
-  char* const sx = smem + STAGE;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1377,14 +1377,13 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_fused_bwd_kernel(const C
   const __amdgpu_buffer_rsrc_t rsK = make_rsrc(p.xa_coef, 12L * CA);
   const __amdgpu_buffer_rsrc_t rsB = make_rsrc(p.B, 2 * p.b_elems);
   const __amdgpu_buffer_rsrc_t rsX = make_rsrc(f.X, 2L * p.M * BNc);
-  // weight rows (n = input channel) of the transposed weight, per-lane chunk swizzle as conv_gemm_glds_kernel
   unsigned b_row[BL];
 #pragma unroll
   for (int i = 0; i < BL; ++i) {
     const int row = wid * (BNc / NW) + i * 8 + lrow;
     b_row[i] = 2u * (unsigned)(row * p.ldb + (pch ^ ((row >> 1) & 7)) * 8);
   }
-  // dY-image address of (pixel row r, channel c), c a multiple of 4 (the glds swizzle)
+  // dY / X image address of (pixel row r, channel c), c a multiple of 4 (the glds swizzle)
   auto a_addr = [](int r, int c) { return r * 128 + ((((c >> 3) ^ ((r >> 1) & 7))) << 4) + (c & 7) * 2; };
 
   f32x4 accw[NKC][QM][QN];  // dW[kc*64 + wm*16*QM + i*16 + fr][wn*16*QN + j*16 + fq*4 + r]
@@ -1396,116 +1395,139 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_fused_bwd_kernel(const C
       for (int j = 0; j < QN; ++j) accw[c][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int ntiles = (p.M + TM - 1) / TM;
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int m0 = tile * TM;
-    // X tile: 128 pixel rows x 128 B, rows past M land zeros (they add nothing to dW)
-#pragma unroll
-    for (int i = 0; i < AL; ++i) {
-      const int row = wid * (TM / NW) + i * 8 + lrow;
-      const int m = m0 + row;
-      const unsigned off = m < p.M ? 2u * (unsigned)(m * BNc + (pch ^ ((row >> 1) & 7)) * 8) : OOB;
-      blds16(rsX, off, sx + (wid * (TM / NW) + i * 8) * 128);
-    }
-    f32x4 acc[RM][RN];
-#pragma unroll
-    for (int i = 0; i < RM; ++i)
-#pragma unroll
-      for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kc = 0; kc < NKC; ++kc) {
-      if (kc > 0) __builtin_amdgcn_s_barrier();  // every wave is done reading the previous k-step
-      // issue: dz pieces (A), y pieces (registers), the k-step's coefficients, weight rows (B)
-      unsigned va[AL];
-      uint4 yv[AL];
+  const int my_tiles = blockIdx.x < ntiles ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int nsteps = my_tiles * NKC;
+  unsigned va[AL];
+  uint4 yv[AL];
+  // issue flat step s = (tile t, k-step kc) into ring slot s & 1 (and the tile's X image into slot t & 1)
+  auto issue = [&](int s) {
+    const int t = s / NKC, kc = s - t * NKC;
+    const int m0 = ((int)blockIdx.x + t * (int)gridDim.x) * TM;
+    char* sa = smem + (s & 1) * STAGE;
+    if (kc == 0) {
+      char* sx = smem + XOFF + (t & 1) * X_BYTES;
 #pragma unroll
       for (int i = 0; i < AL; ++i) {
         const int row = wid * (TM / NW) + i * 8 + lrow;
         const int m = m0 + row;
-        va[i] = m < p.M ? 2u * (unsigned)(m * CA + kc * BK + (pch ^ ((row >> 1) & 7)) * 8) : OOB;
-        blds16(rsA, va[i], sa + (wid * (TM / NW) + i * 8) * 128);
+        const unsigned off = m < p.M ? 2u * (unsigned)(m * BNc + (pch ^ ((row >> 1) & 7)) * 8) : OOB;
+        blds16(rsX, off, sx + (wid * (TM / NW) + i * 8) * 128);
       }
+    }
 #pragma unroll
-      for (int i = 0; i < BL; ++i) blds16(rsB, b_row[i] + 2u * (unsigned)(kc * BK), sb + (wid * (BNc / NW) + i * 8) * 128);
-      {
-        const unsigned ko = lane < 48 ? 4u * (unsigned)((lane >> 4) * CA + kc * BK + (lane & 15) * 4) : OOB;
-        blds16(rsK, ko, sk + wid * 1024);
-      }
+    for (int i = 0; i < AL; ++i) {
+      const int row = wid * (TM / NW) + i * 8 + lrow;
+      const int m = m0 + row;
+      va[i] = m < p.M ? 2u * (unsigned)(m * CA + kc * BK + (pch ^ ((row >> 1) & 7)) * 8) : OOB;
+      blds16(rsA, va[i], sa + (wid * (TM / NW) + i * 8) * 128);
+    }
 #pragma unroll
-      for (int i = 0; i < AL; ++i) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsZ, va[i], 0, 0);
-        yv[i] = *(const uint4*)&v;
-      }
-      wait_vmcnt<0>();
-      // this wave's dz pieces -> dY in place (rows past M stay zero)
-      {
-        const float* kcf = (const float*)(sk + wid * 1024);
+    for (int i = 0; i < BL; ++i)
+      blds16(rsB, b_row[i] + 2u * (unsigned)(kc * BK), sa + A_BYTES + (wid * (BNc / NW) + i * 8) * 128);
+    {
+      const unsigned ko = lane < 48 ? 4u * (unsigned)((lane >> 4) * CA + kc * BK + (lane & 15) * 4) : OOB;
+      blds16(rsK, ko, sa + A_BYTES + B_BYTES + wid * 1024);
+    }
 #pragma unroll
-        for (int gg = 0; gg < 2; ++gg) {
-          const int ch = (pch ^ (((gg * 4 + (lrow >> 1)) & 7))) * 8;
-          float c0[8], c1[8], c2[8];
+    for (int i = 0; i < AL; ++i) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsZ, va[i], 0, 0);
+      yv[i] = *(const uint4*)&v;
+    }
+  };
+
+  f32x4 acc[RM][RN];
+  if (nsteps > 0) issue(0);
+  for (int s = 0; s < nsteps; ++s) {
+    const int t = s / NKC, kc = s - t * NKC;
+    const int tile = (int)blockIdx.x + t * (int)gridDim.x, m0 = tile * TM;
+    char* sa = smem + (s & 1) * STAGE;
+    char* sb = sa + A_BYTES;
+    const char* sx = smem + XOFF + (t & 1) * X_BYTES;
+    wait_vmcnt<0>();
+    // this wave's dz pieces of step s -> dY in place (rows past M stay zero)
+    {
+      const float* kcf = (const float*)(sb + B_BYTES + wid * 1024);
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            *(f32x4*)(c0 + 4 * h) = *(const f32x4*)(kcf + ch + 4 * h);
-            *(f32x4*)(c1 + 4 * h) = *(const f32x4*)(kcf + 64 + ch + 4 * h);
-            *(f32x4*)(c2 + 4 * h) = *(const f32x4*)(kcf + 128 + ch + 4 * h);
-          }
+      for (int gg = 0; gg < 2; ++gg) {
+        const int ch = (pch ^ (((gg * 4 + (lrow >> 1)) & 7))) * 8;
+        float c0[8], c1[8], c2[8];
 #pragma unroll
-          for (int i = gg; i < AL; i += 2) {
-            if (va[i] == OOB) continue;
-            uint4* dst = (uint4*)(sa + (wid * (TM / NW) + i * 8) * 128 + lane * 16);
-            float d[8], y[8];
-            unpack8(*dst, d);
-            unpack8(yv[i], y);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) d[k] = fmaf(c0[k], d[k], fmaf(c1[k], y[k], c2[k]));
-            *dst = pack8(d);
-          }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      }
-      __builtin_amdgcn_s_barrier();
-      // data gradient: dX[px][ci] += dY[px][k] W^T[ci][k]   (row-wise fragments)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        bf16x8 af[RM], bfg[RN];
-#pragma unroll
-        for (int i = 0; i < RM; ++i) af[i] = *(const bf16x8*)(sa + swz(wm * WTM + i * 16 + fr, 4 * kk + fq));
-#pragma unroll
-        for (int j = 0; j < RN; ++j) bfg[j] = *(const bf16x8*)(sb + swz(wn * WTN + j * 16 + fr, 4 * kk + fq));
-#pragma unroll
-        for (int j = 0; j < RN; ++j)
-#pragma unroll
-          for (int i = 0; i < RM; ++i)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[j], af[i], acc[i][j], 0, 0, 0);
-      }
-      // weight gradient of this k-step's 64 output channels: dW[co][ci] += sum_px dY[px][co] X[px][ci]
-      // (column-wise fragments by transposed reads; k order permuted identically for both operands)
-#pragma unroll
-      for (int kk = 0; kk < TM / 32; ++kk) {
-        const int r0 = kk * 32 + 4 * g4 + tq, r1 = r0 + 16;
-        bf16x8 ad[QM], bx[QN];
-#pragma unroll
-        for (int i = 0; i < QM; ++i) {
-          const int c = wm * 16 * QM + i * 16 + tp * 4;
-          const bf16x4 lo = tr_read(sa + a_addr(r0, c)), hi = tr_read(sa + a_addr(r1, c));
-          ad[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        for (int h = 0; h < 2; ++h) {
+          *(f32x4*)(c0 + 4 * h) = *(const f32x4*)(kcf + ch + 4 * h);
+          *(f32x4*)(c1 + 4 * h) = *(const f32x4*)(kcf + 64 + ch + 4 * h);
+          *(f32x4*)(c2 + 4 * h) = *(const f32x4*)(kcf + 128 + ch + 4 * h);
         }
 #pragma unroll
-        for (int j = 0; j < QN; ++j) {
-          const int c = wn * 16 * QN + j * 16 + tp * 4;
-          const bf16x4 lo = tr_read(sx + a_addr(r0, c)), hi = tr_read(sx + a_addr(r1, c));
-          bx[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        for (int i = gg; i < AL; i += 2) {
+          if (va[i] == OOB) continue;
+          uint4* dst = (uint4*)(sa + (wid * (TM / NW) + i * 8) * 128 + lane * 16);
+          float d[8], y[8];
+          unpack8(*dst, d);
+          unpack8(yv[i], y);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) d[k] = fmaf(c0[k], d[k], fmaf(c1[k], y[k], c2[k]));
+          *dst = pack8(d);
         }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    // step s published; every wave is also done with slot (s + 1) & 1 (step s - 1) and X slot of tile t - 1
+    __builtin_amdgcn_s_barrier();
+    if (s + 1 < nsteps) issue(s + 1);
+    if (kc == 0) {
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+    // data gradient: dX[px][ci] += dY[px][k] W^T[ci][k]   (row-wise fragments)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[RM], bfg[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i) af[i] = *(const bf16x8*)(sa + swz(wm * WTM + i * 16 + fr, 4 * kk + fq));
+#pragma unroll
+      for (int j = 0; j < RN; ++j) bfg[j] = *(const bf16x8*)(sb + swz(wn * WTN + j * 16 + fr, 4 * kk + fq));
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    // weight gradient of this k-step's 64 output channels: dW[co][ci] += sum_px dY[px][co] X[px][ci]
+    // (column-wise fragments by transposed reads; k order permuted identically for both operands)
+#pragma unroll
+    for (int kk = 0; kk < TM / 32; ++kk) {
+      const int r0 = kk * 32 + 4 * g4 + tq, r1 = r0 + 16;
+      bf16x8 ad[QM], bx[QN];
+#pragma unroll
+      for (int i = 0; i < QM; ++i) {
+        const int c = wm * 16 * QM + i * 16 + tp * 4;
+        const bf16x4 lo = tr_read(sa + a_addr(r0, c)), hi = tr_read(sa + a_addr(r1, c));
+        ad[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int j = 0; j < QN; ++j) {
+        const int c = wn * 16 * QN + j * 16 + tp * 4;
+        const bf16x4 lo = tr_read(sx + a_addr(r0, c)), hi = tr_read(sx + a_addr(r1, c));
+        bx[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int c = 0; c < NKC; ++c) {  // (a constant-index select: accw stays in registers)
+        if (c != kc) continue;
 #pragma unroll
         for (int i = 0; i < QM; ++i)
 #pragma unroll
           for (int j = 0; j < QN; ++j)
-            accw[kc][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx[j], ad[i], accw[kc][i][j], 0, 0, 0);
+            accw[c][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx[j], ad[i], accw[c][i][j], 0, 0, 0);
       }
     }
-    __syncthreads();
-    conv_epilogue_dispatch<TM, BNc, WM, WN, 1>(p, acc, smem, tid, lane, wid, wm, wn, m0, 0, tile, p.GH * p.GW);
-    __syncthreads();  // the epilogue's LDS is the next tile's X image / ring
+    if (kc == NKC - 1) {
+      // the tile's epilogue in its own LDS region (the ring and X buffers keep the prefetch in flight)
+      conv_epilogue_dispatch<TM, BNc, WM, WN, 1>(p, acc, smem + EOFF, tid, lane, wid, wm, wn, m0, 0, tile,
+                                                  p.GH * p.GW);
+      __syncthreads();  // epilogue LDS reused by the next tile
+    }
   }
   // this block's dW partial -> its workspace slab (plain 16-B stores; the reduce adds the slabs in order)
   float* slab = f.ws + (long)blockIdx.x * CO * BNc;
