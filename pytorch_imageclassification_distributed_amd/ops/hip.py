@@ -1138,6 +1138,7 @@ XA_COUNT = [0]  # BN backwards handed to their producer conv (tests / diagnostic
 # once per tile along the GEMM's other dimension.  The unfused pass touches each element once (memory-
 # bound), so fusing pays only while that replication stays small (docs/DESIGN.md, "what fusion costs").
 XA_MAX_REP = int(os.environ.get("IMGCLS_XA_MAX_REP", "2"))
+XA_NARROW_OFF = os.environ.get("IMGCLS_XA_NARROW_OFF", "0") == "1"
 XF_MAX_REP = int(os.environ.get("IMGCLS_XF_MAX_REP", "2"))
 
 
@@ -1172,6 +1173,8 @@ def xa_eligible(x, conv) -> bool:
     (uniform k-steps of the dgrad GEMM, K = taps x Cout) and whose input channels are unpadded: its backward
     can take the fused BN-backward operand map (padded taps are masked in the kernel)."""
     taps = conv.kernel_size[0] * conv.kernel_size[1]
+    if XA_NARROW_OFF and conv.out_channels <= 64 and conv.in_channels > 64:
+        return False  # (diagnostic knob) the narrow-output XA weight gradient
     return (FUSE_XA and conv.stride[0] == conv.stride[1] and tuple(conv.dilation) == (1, 1)
             and conv.groups == 1 and conv.bias is None and conv.out_channels % 64 == 0
             and x.shape[1] == conv.in_channels and conv.in_channels % 8 == 0 and taps <= 49

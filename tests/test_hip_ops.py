@@ -54,6 +54,7 @@ CONV_CASES = [
     (1, 32, 15, 13, 40, (3, 3), 1, (0, 0)),
     (2, 32, 37, 37, 32, (3, 3), 1, (0, 0)),   # 32-row wgrad tile (Inception Conv2d_2a)
     (2, 24, 20, 20, 24, (3, 3), 1, (1, 1)),   # ... with a partial 24-of-32 channel tile (EfficientNet widths)
+    (2, 24, 20, 20, 144, (1, 1), 1, (0, 0)),  # EfficientNet expand 1x1: Ntot 24 (a partial 64-column wgrad tile)
 ]
 
 
@@ -164,7 +165,7 @@ def test_conv_bn_act_halo(act, use_res, cfg):
 
 
 @pytest.mark.parametrize("case,stages", [
-    (c, st) for c in [CONV_CASES[i] for i in (0, 1, 3, 4, 5, 6, 7, 8, 12, 13, 14)]
+    (c, st) for c in [CONV_CASES[i] for i in (0, 1, 3, 4, 5, 6, 7, 8, 12, 13, 14, 15)]
     for st in (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12)
     if _wgrad_stage_ok(c, st)])
 def test_conv_wgrad_ring_variants(case, stages):
