@@ -1542,6 +1542,198 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_fused_bwd_kernel(const C
       }
 }
 
+// The same fusion for 64 output channels and CI = 128 / 256 input channels (ResNet layer1 conv1: 256 -> 64):
+// K = 64 is one k-step, so a tile's dY (dz + y -> dY in LDS, double-buffered by tile) is formed once and the
+// data gradient's CI columns are walked in 64-column chunks; each (tile, chunk) step streams its weight rows
+// and X columns through a 2-deep ring, runs the dgrad MFMAs + epilogue for that column chunk and adds
+// dY^T X_chunk into the chunk's dW block (64 x 64 per chunk, CI / 8 fp32 accumulators per lane).
+template <int CI, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN, 2) void conv_fused_bwd_n_kernel(const ConvParams p, const FusedW f) {
+  constexpr int TM = 128, CO = 64, NW = WM * WN, NNC = CI / 64;
+  constexpr int WTM = TM / WM, WTN = 64 / WN;
+  constexpr int RM = WTM / 16, RN = WTN / 16;
+  constexpr int AL = TM / 8 / NW, BL = 64 / 8 / NW;
+  constexpr int QM = 64 / WM / 16, QN = 64 / WN / 16;
+  static_assert(AL >= 1 && BL >= 1 && QM >= 1 && QN >= 1 && (TM / NW) % 16 == 0 && CI % 64 == 0, "mapping");
+  constexpr int A_SLOT = TM * 128 + NW * 1024;       // dY image + per-wave coefficient slots
+  constexpr int R_SLOT = 64 * 128 + TM * 128;        // weight rows + X column chunk
+  constexpr int EPI = TM * (64 + 8) * 2 > NW * 2 * 64 * 4 ? TM * (64 + 8) * 2 : NW * 2 * 64 * 4;
+  constexpr int ROFF = 2 * A_SLOT, EOFF = ROFF + 2 * R_SLOT, MAIN = EOFF + EPI;
+  static_assert(MAIN <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(16))) char smem[MAIN];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int lrow = lane >> 3, pch = lane & 7;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int g4 = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.A, 2 * p.a_elems);
+  const __amdgpu_buffer_rsrc_t rsZ = make_rsrc(p.xa_y, 2 * p.a_elems);
+  const __amdgpu_buffer_rsrc_t rsK = make_rsrc(p.xa_coef, 12L * CO);
+  const __amdgpu_buffer_rsrc_t rsB = make_rsrc(p.B, 2 * p.b_elems);
+  const __amdgpu_buffer_rsrc_t rsX = make_rsrc(f.X, 2L * p.M * CI);
+  auto a_addr = [](int r, int c) { return r * 128 + ((((c >> 3) ^ ((r >> 1) & 7))) << 4) + (c & 7) * 2; };
+
+  f32x4 accw[NNC][QM][QN];  // dW[wm*16*QM + i*16 + fr][nc*64 + wn*16*QN + j*16 + fq*4 + r]
+#pragma unroll
+  for (int c = 0; c < NNC; ++c)
+#pragma unroll
+    for (int i = 0; i < QM; ++i)
+#pragma unroll
+      for (int j = 0; j < QN; ++j) accw[c][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int ntiles = (p.M + TM - 1) / TM;
+  const int my_tiles = blockIdx.x < ntiles ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int nsteps = my_tiles * NNC;
+  unsigned va[AL];
+  uint4 yv[AL];
+  auto issue = [&](int s) {
+    const int t = s / NNC, nc = s - t * NNC;
+    const int m0 = ((int)blockIdx.x + t * (int)gridDim.x) * TM;
+    if (nc == 0) {  // the tile's dz pieces, y pieces and coefficients
+      char* sa = smem + (t & 1) * A_SLOT;
+#pragma unroll
+      for (int i = 0; i < AL; ++i) {
+        const int row = wid * (TM / NW) + i * 8 + lrow;
+        const int m = m0 + row;
+        va[i] = m < p.M ? 2u * (unsigned)(m * CO + (pch ^ ((row >> 1) & 7)) * 8) : OOB;
+        blds16(rsA, va[i], sa + (wid * (TM / NW) + i * 8) * 128);
+      }
+      const unsigned ko = lane < 48 ? 4u * (unsigned)((lane >> 4) * CO + (lane & 15) * 4) : OOB;
+      blds16(rsK, ko, sa + TM * 128 + wid * 1024);
+#pragma unroll
+      for (int i = 0; i < AL; ++i) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsZ, va[i], 0, 0);
+        yv[i] = *(const uint4*)&v;
+      }
+    }
+    char* sr = smem + ROFF + (s & 1) * R_SLOT;
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {  // weight rows nc*64 .. +64 of the transposed [CI][CO] weight
+      const int row = wid * (64 / NW) + i * 8 + lrow;
+      blds16(rsB, 2u * (unsigned)((nc * 64 + row) * p.ldb + (pch ^ ((row >> 1) & 7)) * 8),
+             sr + (wid * (64 / NW) + i * 8) * 128);
+    }
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {  // X columns nc*64 .. +64 of the tile's pixels
+      const int row = wid * (TM / NW) + i * 8 + lrow;
+      const int m = m0 + row;
+      const unsigned off = m < p.M ? 2u * (unsigned)(m * CI + nc * 64 + (pch ^ ((row >> 1) & 7)) * 8) : OOB;
+      blds16(rsX, off, sr + 64 * 128 + (wid * (TM / NW) + i * 8) * 128);
+    }
+  };
+
+  f32x4 acc[RM][RN];
+  if (nsteps > 0) issue(0);
+  for (int s = 0; s < nsteps; ++s) {
+    const int t = s / NNC, nc = s - t * NNC;
+    const int tile = (int)blockIdx.x + t * (int)gridDim.x, m0 = tile * TM;
+    char* sa = smem + (t & 1) * A_SLOT;
+    const char* sb = smem + ROFF + (s & 1) * R_SLOT;
+    const char* sx = sb + 64 * 128;
+    wait_vmcnt<0>();
+    if (nc == 0) {  // this wave's dz pieces -> dY in place
+      const float* kcf = (const float*)(sa + TM * 128 + wid * 1024);
+#pragma unroll
+      for (int gg = 0; gg < 2; ++gg) {
+        const int ch = (pch ^ (((gg * 4 + (lrow >> 1)) & 7))) * 8;
+        float c0[8], c1[8], c2[8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          *(f32x4*)(c0 + 4 * h) = *(const f32x4*)(kcf + ch + 4 * h);
+          *(f32x4*)(c1 + 4 * h) = *(const f32x4*)(kcf + 64 + ch + 4 * h);
+          *(f32x4*)(c2 + 4 * h) = *(const f32x4*)(kcf + 128 + ch + 4 * h);
+        }
+#pragma unroll
+        for (int i = gg; i < AL; i += 2) {
+          if (va[i] == OOB) continue;
+          uint4* dst = (uint4*)(sa + (wid * (TM / NW) + i * 8) * 128 + lane * 16);
+          float d[8], y[8];
+          unpack8(*dst, d);
+          unpack8(yv[i], y);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) d[k] = fmaf(c0[k], d[k], fmaf(c1[k], y[k], c2[k]));
+          *dst = pack8(d);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (s + 1 < nsteps) issue(s + 1);
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[RM], bfg[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i) af[i] = *(const bf16x8*)(sa + swz(wm * WTM + i * 16 + fr, 4 * kk + fq));
+#pragma unroll
+      for (int j = 0; j < RN; ++j) bfg[j] = *(const bf16x8*)(sb + swz(wn * WTN + j * 16 + fr, 4 * kk + fq));
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[j], af[i], acc[i][j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int kk = 0; kk < TM / 32; ++kk) {
+      const int r0 = kk * 32 + 4 * g4 + tq, r1 = r0 + 16;
+      bf16x8 ad[QM], bx[QN];
+#pragma unroll
+      for (int i = 0; i < QM; ++i) {
+        const int c = wm * 16 * QM + i * 16 + tp * 4;
+        const bf16x4 lo = tr_read(sa + a_addr(r0, c)), hi = tr_read(sa + a_addr(r1, c));
+        ad[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int j = 0; j < QN; ++j) {
+        const int c = wn * 16 * QN + j * 16 + tp * 4;
+        const bf16x4 lo = tr_read(sx + a_addr(r0, c)), hi = tr_read(sx + a_addr(r1, c));
+        bx[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int c = 0; c < NNC; ++c) {
+        if (c != nc) continue;
+#pragma unroll
+        for (int i = 0; i < QM; ++i)
+#pragma unroll
+          for (int j = 0; j < QN; ++j)
+            accw[c][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx[j], ad[i], accw[c][i][j], 0, 0, 0);
+      }
+    }
+    conv_epilogue_dispatch<TM, 64, WM, WN, 1>(p, acc, smem + EOFF, tid, lane, wid, wm, wn, m0, nc * 64, tile,
+                                               p.GH * p.GW);
+    __syncthreads();
+  }
+  float* slab = f.ws + (long)blockIdx.x * CO * CI;
+#pragma unroll
+  for (int c = 0; c < NNC; ++c)
+#pragma unroll
+    for (int i = 0; i < QM; ++i)
+#pragma unroll
+      for (int j = 0; j < QN; ++j) {
+        const int co = wm * 16 * QM + i * 16 + fr, ci = c * 64 + wn * 16 * QN + j * 16 + fq * 4;
+        *(f32x4*)(slab + (long)co * CI + ci) = accw[c][i][j];
+      }
+}
+
+template <int CI>
+static int launch_fused_bwd_n(const ConvParams& p, const FusedW& f, float* dW, int blocks, hipStream_t stream) {
+  hipLaunchKernelGGL((conv_fused_bwd_n_kernel<CI, 4, 2>), dim3(blocks), dim3(512), 0, stream, p, f);
+  HIP_CHECK_LAUNCH();
+  const long n4 = 64L * CI / 4;
+  if (blocks >= 128) launch_wgrad_reduce<16>(f.ws, dW, n4, blocks, stream);
+  else if (blocks >= 64) launch_wgrad_reduce<8>(f.ws, dW, n4, blocks, stream);
+  else if (blocks >= 32) launch_wgrad_reduce<4>(f.ws, dW, n4, blocks, stream);
+  else if (blocks >= 16) launch_wgrad_reduce<2>(f.ws, dW, n4, blocks, stream);
+  else launch_wgrad_reduce<1>(f.ws, dW, n4, blocks, stream);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
 template <int CO>
 static int launch_fused_bwd(const ConvParams& p, const FusedW& f, float* dW, int blocks, hipStream_t stream) {
   hipLaunchKernelGGL((conv_fused_bwd_kernel<CO, 4, 2>), dim3(blocks), dim3(512), 0, stream, p, f);
@@ -1829,11 +2021,17 @@ int conv_wgrad_launch(const WgradParams& p_in, int splits, hipStream_t stream) {
 // CA = CO in {64, 128, 192, 256}), X = the conv input [M][64], ws >= blocks * CO * 64 floats, dW [CO][64]
 // += sum of the blocks' partials.  3 = geometry not handled.
 int conv_fused_bwd_launch(const ConvParams& p, const bf16_t* X, float* ws, float* dW, int blocks, hipStream_t stream) {
-  if (!p.xa_y || !p.xa_coef || p.Ncols != 64 || p.CA % BK || p.CA > 256 || p.K != p.CA || p.ntaps != 1 ||
-      p.tap_dh[0] || p.tap_dw[0] || p.sA != 1 || p.GH != p.IH || p.GW != p.IW || p.so != 1 || p.ldc != 64 ||
-      p.c_off || p.stats || p.bias || p.a_sc || p.xf_coef || blocks <= 0)
+  if (!p.xa_y || !p.xa_coef || p.CA % BK || p.CA > 256 || p.K != p.CA || p.ntaps != 1 || p.tap_dh[0] ||
+      p.tap_dw[0] || p.sA != 1 || p.GH != p.IH || p.GW != p.IW || p.so != 1 || p.ldc != p.Ncols || p.c_off ||
+      p.stats || p.bias || p.a_sc || p.xf_coef || blocks <= 0)
     return 3;
   const FusedW f{X, ws};
+  if (p.Ncols != 64) {  // 64 output channels (K), 128 / 256 input channels (N)
+    if (p.CA != 64) return 3;
+    if (p.Ncols == 128) return launch_fused_bwd_n<128>(p, f, dW, blocks, stream);
+    if (p.Ncols == 256) return launch_fused_bwd_n<256>(p, f, dW, blocks, stream);
+    return 3;
+  }
   switch (p.CA) {
     case 64: return launch_fused_bwd<64>(p, f, dW, blocks, stream);
     case 128: return launch_fused_bwd<128>(p, f, dW, blocks, stream);

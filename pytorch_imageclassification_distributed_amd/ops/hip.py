@@ -719,9 +719,11 @@ _CU_COUNT: dict = {}
 
 
 def fused_bwd_eligible(g: ConvGeom, xa) -> bool:
-    return (FUSED_XA_BWD and xa is not None and g.kh == 1 and g.kw == 1 and g.sh == 1 and g.sw == 1
-            and g.pt == 0 and g.pl == 0 and g.Cx == g.Ci == 64 and g.Co % 64 == 0 and g.Co <= 256
-            and g.OH == g.H and g.OW == g.W)
+    if not (FUSED_XA_BWD and xa is not None and g.kh == 1 and g.kw == 1 and g.sh == 1 and g.sw == 1
+            and g.pt == 0 and g.pl == 0 and g.Cx == g.Ci and g.OH == g.H and g.OW == g.W):
+        return False
+    # 64 input channels and up to 256 outputs (layer1 conv3), or 64 outputs and 128 / 256 inputs (layer1 conv1)
+    return (g.Ci == 64 and g.Co % 64 == 0 and g.Co <= 256) or (g.Co == 64 and g.Ci in (128, 256))
 
 
 def conv_fused_bwd_raw(dz, x, w_param, g: ConvGeom, xa, addend=None, link=None):

@@ -365,9 +365,10 @@ def test_relu_mask_matches_residual_recompute(kind, fp8):
 
 @pytest.mark.parametrize("n_blocks,hw", [(2, 16), (1, 15)])
 def test_fused_xa_backward_matches_separate(n_blocks, hw):
-    """conv_fused_bwd_kernel (ResNet layer1 conv3: 64 -> 256, XA): one pass over dz and y gives the data
-    gradient with its BN-backward epilogue and the weight gradient - the same values as the separate XA dgrad
-    and XA wgrad launches (odd map: partial last pixel tile)."""
+    """conv_fused_bwd_kernel (ResNet layer1 conv3: 64 -> 256) and conv_fused_bwd_n_kernel (conv1: 256 -> 64, the
+    residual gradient as the dgrad addend), XA: one pass over dz and y gives the data gradient with its
+    BN-backward epilogue and the weight gradient - the same values as the separate XA dgrad and XA wgrad
+    launches (odd map: partial last pixel tile)."""
     import torch.nn as nn
     from pytorch_imageclassification_distributed_amd.models.resnet import Bottleneck
     from pytorch_imageclassification_distributed_amd.ops import hip
@@ -381,7 +382,7 @@ def test_fused_xa_backward_matches_separate(n_blocks, hw):
         hip.FUSED_XA_BWD = True
         before = hip.FUSED_XA_BWD_COUNT[0]
         gx1, gp1 = _grads(blk, x, True)
-        assert hip.FUSED_XA_BWD_COUNT[0] - before == n_blocks
+        assert hip.FUSED_XA_BWD_COUNT[0] - before == 2 * n_blocks  # conv1 (256 -> 64) and conv3 (64 -> 256)
     finally:
         hip.FUSED_XA_BWD = keep
     err = lambda a, b: ((a - b).abs().max() / b.abs().max().clamp(min=1e-6)).item()  # noqa: E731
