@@ -715,6 +715,9 @@ def _conv_forward_fp8(x, w_param, g: ConvGeom, stats, bias, out, c_off, shift=No
 # the weight gradient, instead of each GEMM reading dz and y (IMGCLS_FUSED_BWD=0: separate launches).
 FUSED_XA_BWD = os.environ.get("IMGCLS_FUSED_BWD", "1") == "1"
 FUSED_XA_BWD_COUNT = [0]  # fused dgrad + wgrad launches (tests / diagnostics)
+# the 64-output form (layer1 conv1: dgrad columns walked in 64-channel chunks) measured slower than the separate
+# launches (ResNet-50 b1024 13344-13358 vs 13589-13626 img/s with only the 64-input form, profiles/r7n_*): off
+FUSED_XA_BWD_N = os.environ.get("IMGCLS_FUSED_BWD_N", "0") == "1"
 _CU_COUNT: dict = {}
 
 
@@ -723,7 +726,7 @@ def fused_bwd_eligible(g: ConvGeom, xa) -> bool:
             and g.pt == 0 and g.pl == 0 and g.Cx == g.Ci and g.OH == g.H and g.OW == g.W):
         return False
     # 64 input channels and up to 256 outputs (layer1 conv3), or 64 outputs and 128 / 256 inputs (layer1 conv1)
-    return (g.Ci == 64 and g.Co % 64 == 0 and g.Co <= 256) or (g.Co == 64 and g.Ci in (128, 256))
+    return (g.Ci == 64 and g.Co % 64 == 0 and g.Co <= 256) or (FUSED_XA_BWD_N and g.Co == 64 and g.Ci in (128, 256))
 
 
 def conv_fused_bwd_raw(dz, x, w_param, g: ConvGeom, xa, addend=None, link=None):

@@ -375,7 +375,8 @@ def test_fused_xa_backward_matches_separate(n_blocks, hw):
     torch.manual_seed(0)
     blk = nn.Sequential(*[Bottleneck(256, 64) for _ in range(n_blocks)]).to(DEV).to(memory_format=torch.channels_last)
     x = torch.randn(4, 256, hw, hw, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    keep = hip.FUSED_XA_BWD
+    keep, keep_n = hip.FUSED_XA_BWD, hip.FUSED_XA_BWD_N
+    hip.FUSED_XA_BWD_N = True  # both fused forms (the 64-output one is off by default)
     try:
         hip.FUSED_XA_BWD = False
         gx0, gp0 = _grads(blk, x, True)
@@ -384,7 +385,7 @@ def test_fused_xa_backward_matches_separate(n_blocks, hw):
         gx1, gp1 = _grads(blk, x, True)
         assert hip.FUSED_XA_BWD_COUNT[0] - before == 2 * n_blocks  # conv1 (256 -> 64) and conv3 (64 -> 256)
     finally:
-        hip.FUSED_XA_BWD = keep
+        hip.FUSED_XA_BWD, hip.FUSED_XA_BWD_N = keep, keep_n
     err = lambda a, b: ((a - b).abs().max() / b.abs().max().clamp(min=1e-6)).item()  # noqa: E731
     assert err(gx1, gx0) < 1e-2, err(gx1, gx0)
     for n in gp0:
