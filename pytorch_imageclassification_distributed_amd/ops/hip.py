@@ -799,6 +799,7 @@ def _wgrad_split(m, tiles, target):
     return kps, splits
 
 
+WGRAD_NARROW_TILES = os.environ.get("IMGCLS_WGRAD_NARROW_TILES", "1") == "1"  # stages 10-12 as tuner candidates
 WGRAD_STAGES = int(os.environ.get("IMGCLS_WGRAD_STAGES", "0"))  # 0 = tuned with the split count; 1 | 2 | 3
 
 
@@ -897,7 +898,7 @@ def _wgrad_config(dy, x, g: ConvGeom, m, ntot, xa=None, xf=None):
         cands += [(cand, 8) for cand in blocks if cand <= 1024]
         if g.Co <= 32:  # 32-row tiles: a 64-row tile would be half empty
             cands += [(cand, st) for st in (5, 6) for cand in blocks]
-        if ntot <= 64:  # 64-column tiles: a 128-column tile would be half empty (ResNet layer1 conv3)
+        if ntot <= 64 and WGRAD_NARROW_TILES:  # 64-column tiles: a 128-column tile is half empty (layer1 conv3)
             cands += [(cand, st) for st in (10, 11) for cand in blocks]
             if g.Co >= 256:
                 cands += [(cand, 12) for cand in blocks if cand <= 1024]
