@@ -86,7 +86,9 @@ def _run(model, size, compute, dtype, steps, batch, lr, train, val):
     ("resnet18", 64, 150, 64, 1e-3),
     ("resnet50", 96, 120, 32, 1e-3),
     ("inceptionv3", 299, 80, 16, 1e-3),     # aux head + 0.4-weighted aux loss (reference train.py:48-52)
-    ("efficientnet-b0", 128, 120, 32, 2e-3),
+    # lr 1e-3: at 2e-3 the HIP run's tail loss spread 0.76-1.34 over 9 runs (bf16 + chaotic random-init
+    # EfficientNet); at 1e-3 four runs ended 0.53-0.67 against the fp32 reference's 0.73 (r7x)
+    ("efficientnet-b0", 128, 120, 32, 1e-3),
 ])
 def test_hip_bf16_learns_like_torch_fp32(model, size, steps, batch, lr):
     train = _data(max(steps * batch // 3, 4 * batch), size, seed=11)
