@@ -21,6 +21,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -73,6 +75,8 @@ def parse():
                    help="device: batches generated once in HBM (the step alone); host: pinned uint8 host batches "
                         "copied by hipMemcpyAsync on a copy stream and normalised on the GPU inside the timed loop "
                         "(the real-data path minus decode, K24/K25)")
+    p.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                   help="cpu: functional rehearsal of the multi-rank path over gloo (no GPU; never a benchmark)")
     p.add_argument("--comm-timing", default="auto", choices=["auto", "on", "off"],
                    help="per-step device-event timeline of the gradient all-reduce (auto: on when N > 1): "
                         "overlap window, side-stream tail and exposed collective time in the JSON line")
@@ -125,9 +129,36 @@ def _from_slowest_rank(extra: dict, dt: float, ctx) -> dict:
     return max(box, key=lambda r: r[0])[1]
 
 
+def _spawn_ranks(a) -> int:
+    """``--gpus N`` without a launcher: start N ranks under torch.distributed.run (one per GPU, rendezvous on
+    127.0.0.1) as a child process and return its exit code.  Runs before this process touches the GPU."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"[bench] launching {a.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.run(cmd).returncode
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+
+
 def main():
     a = parse()
-    ctx = init_distributed(device="cuda", backend=a.dist_backend)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return _spawn_ranks(a)
+    if a.device == "cpu":
+        a.compute = "torch"  # the HIP kernels need the GPU; the rehearsal checks launch, rendezvous, reporting
+    backend = a.dist_backend if a.device == "cuda" else "gloo"
+    ctx = init_distributed(device=a.device, backend=backend)
+    if ctx.world_size != a.gpus:
+        print(f"[bench] world size {ctx.world_size} != --gpus {a.gpus}: refusing to report a mislabelled number",
+              file=sys.stderr, flush=True)
+        destroy()
+        return 2
     sync_bn = (a.sync_bn == "on") or (a.sync_bn == "auto" and ctx.world_size > 1)
     targs = build_parser().parse_args([
         "--synthetic", "--model", a.model, "--image-size", str(a.image_size),
@@ -169,28 +200,28 @@ def main():
 
     for i in range(a.warmup):
         last = step(i)
-    torch.cuda.synchronize()
+    _sync(ctx.device)
     # host enqueue cost of one step (diagnostic, stderr): > ms_per_step would mean CPU-bound
     t_host = time.perf_counter()
     last = step(max(a.warmup - 1, 0))
     t_host = time.perf_counter() - t_host
-    torch.cuda.synchronize()
+    _sync(ctx.device)
     print(f"[bench] rank {ctx.rank}: host enqueue {t_host * 1e3:.1f} ms/step", file=sys.stderr, flush=True)
     if not torch.isfinite(last).item():
         raise FloatingPointError(f"non-finite loss in warmup: {last.item()}")
     comm_t = None
-    if a.comm_timing == "on" or (a.comm_timing == "auto" and ctx.world_size > 1):
+    if ctx.device.type == "cuda" and (a.comm_timing == "on" or (a.comm_timing == "auto" and ctx.world_size > 1)):
         from pytorch_imageclassification_distributed_amd.parallel import comm_timer
         comm_t = comm_timer.install()
     barrier(ctx)
-    torch.cuda.synchronize()
+    _sync(ctx.device)
     m0 = _alloc_counters(ctx.device)
     t0 = time.perf_counter()
     for i in range(a.steps):
         last = step(a.warmup + i)
-    torch.cuda.synchronize()
+    _sync(ctx.device)
     barrier(ctx)
-    torch.cuda.synchronize()
+    _sync(ctx.device)
     dt = time.perf_counter() - t0
     if ctx.device.type == "cuda":
         m1 = _alloc_counters(ctx.device)
@@ -221,9 +252,11 @@ def main():
     if ctx.rank == 0:
         imgs = a.batch * ctx.world_size * a.steps
         value = imgs / dt
-        base = load_baseline(ctx.world_size, a.batch) if a.dtype == "bf16" else None
-        metric = METRIC if (a.model, a.image_size, a.dtype) == ("resnet50", 224, "bf16") else \
+        base = load_baseline(ctx.world_size, a.batch) if a.dtype == "bf16" and a.device == "cuda" else None
+        metric = METRIC if (a.model, a.image_size, a.dtype, a.device) == ("resnet50", 224, "bf16", "cuda") else \
             f"images/sec (whole node) {a.model} {a.image_size}x{a.image_size} {a.dtype} MI355X"
+        if a.device == "cpu":
+            metric = "CPU REHEARSAL of the multi-rank path (gloo, fp32, not a benchmark): " + metric
         if os.environ.get("IMGCLS_DIAG_SKIP_WGRAD", "0") == "1":  # a diagnostic, never a benchmark number
             metric, base = "DIAGNOSTIC (weight gradients skipped, invalid as a benchmark): " + metric, None
         print(json.dumps({
@@ -231,7 +264,7 @@ def main():
             "n_gpus": ctx.world_size, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": round(value / base, 4) if base else None,
-            "dtype": a.dtype,
+            "dtype": a.dtype if a.device == "cuda" else "fp32 (cpu rehearsal, not a benchmark)",
             "data": ("synthetic (on-device random images, random-init weights)" if a.data == "device" else
                      "synthetic (pinned uint8 host batches, H2D copy + normalisation in the timed loop, "
                      "random-init weights)"),
@@ -240,7 +273,7 @@ def main():
                        "num_classes": a.num_classes, "parallelism": f"dp{ctx.world_size}",
                        "sync_bn": sync_bn, "syncbn_comm": ("peer" if tr.syncbn_peer else "rccl") if sync_bn else None,
                        "compute": a.compute, "optimizer": "adam", "hip_graph": use_graph,
-                       "grad_comm": (a.comm_backend if ctx.world_size > 1 else None),
+                       "grad_comm": (getattr(tr, "comm_backend", a.comm_backend) if ctx.world_size > 1 else None),
                        "final_loss": round(loss_val, 5)},
             **extra,
         }), flush=True)

@@ -65,8 +65,14 @@ def main():
             res[f"{tm}x{bn}/{wm}x{wn}/s{st}#{i}"] = timeit(
                 lambda: hip.C.conv_gemm(A, B.view(-1), out, None, None, *geo, [0], [0], [0], hip.G_STATS, zero,
                                         None, None, None, None, None, 0, 1, 0, 0, i, None, None, None, None, None, None, None, 0, None, None, None, None, 0))
+        for v, (tm, bn, wm, wn, var) in enumerate(hip.conv_deep_cfgs()):
+            if (bn > 64 and bn >= 2 * N) or var & 6:
+                continue
+            res[f"{tm}x{bn}/{wm}x{wn}/deep#{v}"] = timeit(
+                lambda: hip.C.conv_gemm(A, B.view(-1), out, None, None, *geo, [0], [0], [0], hip.G_STATS, zero,
+                                        None, None, None, None, None, 0, 1, 0, 0, hip.DEEP_BASE + v, None, None, None, None, None, None, None, 0, None, None, None, None, 0))
         ref = torch.mm(A, B.t())
-        err = ((out.float() - ref.float()).abs().max() / ref.float().abs().max()).item()
+        err = ((out.float() - ref.float()).abs().max() / ref.float().abs().max()).item()  # (last config run)
         best = min(res, key=res.get)
         line = (f"M={M:8d} N={N:5d} K={K:5d}: hipBLASLt {t_ref * 1e3:8.1f}us {flop / t_ref / 1e9:6.0f}TF | "
                 f"ours {best:>16} {res[best] * 1e3:8.1f}us {flop / res[best] / 1e9:6.0f}TF (err {err:.1e})")

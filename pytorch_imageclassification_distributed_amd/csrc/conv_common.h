@@ -19,7 +19,7 @@ DEVI int xcd_remap(int bid, int nwg) {
 }
 
 // Epilogue of a TM x BN tile computed by WM x WN waves (each wave a (TM/WM) x (BN/WN) sub-tile).
-template <int TM, int BN, int WM, int WN>
+template <int TM, int BN, int WM, int WN, bool STAGED = false>
 DEVI void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16], char* smem, int tid,
                         int lane, int wid, int wm, int wn, int m0, int n0, int bm, int ghw) {
   constexpr int NTH = 64 * WM * WN;
@@ -31,7 +31,7 @@ DEVI void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN 
   // 1) 4 consecutive channels -> one 8-B ds_write into the bf16 tile [BM][CST]
   bf16_t* ct = (bf16_t*)smem;
 #pragma unroll
-  for (int i = 0; i < RM; ++i) {
+  for (int i = 0; i < (STAGED ? 0 : RM); ++i) {
     const int row = wm * WTM + i * 16 + fr;
 #pragma unroll
     for (int j = 0; j < RN; ++j) {
@@ -190,7 +190,7 @@ DEVI int epi_mode(const ConvParams& p) {
   return m;
 }
 
-template <int TM, int BN, int WM, int WN, int MODE, int UR>
+template <int TM, int BN, int WM, int WN, int MODE, int UR, bool STAGED = false>
 DEVI void conv_epi(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16], char* smem, int tid,
                    int lane, int wid, int wm, int wn, int m0, int n0, int bm) {
   constexpr bool STATS = MODE & EP_STATS, ADD = MODE & EP_ADD, BWD = MODE & EP_BWD, RES = MODE & EP_RES;
@@ -202,7 +202,7 @@ DEVI void conv_epi(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16]
   const int fr = lane & 15, fq = lane >> 4;
   bf16_t* ct = (bf16_t*)smem;
 #pragma unroll
-  for (int i = 0; i < RM; ++i) {
+  for (int i = 0; i < (STAGED ? 0 : RM); ++i) {  // STAGED: the caller wrote the bf16 tile already
     const int row = wm * WTM + i * 16 + fr;
 #pragma unroll
     for (int j = 0; j < RN; ++j) {
@@ -352,10 +352,10 @@ DEVI void conv_epi(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16]
 
 // UR: rows of operands in flight per thread - 2 where the launch bound leaves >= 200 VGPRs, else 1 (two
 // rows of four 16-B operands plus the BN-backward coefficients cost ~150 VGPRs)
-template <int TM, int BN, int WM, int WN, int UR>
+template <int TM, int BN, int WM, int WN, int UR, bool STAGED = false>
 DEVI void conv_epilogue_dispatch(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16], char* smem, int tid,
                                  int lane, int wid, int wm, int wn, int m0, int n0, int bm, int ghw) {
-#define EPI_CASE(M_) case (M_): conv_epi<TM, BN, WM, WN, (M_), UR>(p, acc, smem, tid, lane, wid, wm, wn, m0, n0, bm); break;
+#define EPI_CASE(M_) case (M_): conv_epi<TM, BN, WM, WN, (M_), UR, STAGED>(p, acc, smem, tid, lane, wid, wm, wn, m0, n0, bm); break;
   switch (epi_mode(p)) {
     EPI_CASE(EP_STATS | EP_DIRECT)
     EPI_CASE(EP_STATS)
@@ -376,7 +376,7 @@ DEVI void conv_epilogue_dispatch(const ConvParams& p, f32x4 (&acc)[TM / WM / 16]
     EPI_CASE(EP_BWD | EP_RELU | EP_RES | EP_ADD)
     EPI_CASE(EP_BWD | EP_RELU | EP_MASK)
     EPI_CASE(EP_BWD | EP_RELU | EP_MASK | EP_ADD)
-    default: conv_epilogue<TM, BN, WM, WN>(p, acc, smem, tid, lane, wid, wm, wn, m0, n0, bm, ghw);
+    default: conv_epilogue<TM, BN, WM, WN, STAGED>(p, acc, smem, tid, lane, wid, wm, wn, m0, n0, bm, ghw);
   }
 #undef EPI_CASE
 }

@@ -107,6 +107,11 @@ bool conv_cfg_has_xa(int i);           // configuration i has fused BN-backward 
 int conv_halo_num();
 void conv_halo_info(int i, int* out6);  // {tile rows, tile channels, waves M, waves N, weight ring depth, patch rows}
 int conv_halo_launch(int i, const ConvParams& p, hipStream_t stream);  // 3: geometry not handled
+// prefetch-depth-2 kernel (conv_deep.hip): ConvParams::cfg >= CONV_DEEP_BASE selects entry cfg - CONV_DEEP_BASE
+#define CONV_DEEP_BASE 2000
+int conv_deep_num();
+void conv_deep_info(int i, int* out5);  // {tile rows, tile channels, waves M, waves N, schedule variant}
+int conv_deep_launch(int i, const ConvParams& p, hipStream_t stream);  // 3: geometry not handled
 int conv_wgrad_launch(const WgradParams& p, int splits, hipStream_t stream);
 int conv_fused_bwd_launch(const ConvParams& p, const bf16_t* X, float* ws, float* dW, int blocks, hipStream_t stream);
 bool conv_wgrad_has_xa(int stages);  // the wgrad variant selected by ``stages`` has a fused BN-backward dY form

@@ -106,14 +106,17 @@ int rccl_unique_id(char* out, int n) {
 
 int rccl_comm_init(const char* uid, int n, int nranks, int rank, int device, int64_t* handle) {
   if (!g_api.lib || n != NCCL_UNIQUE_ID_BYTES) return -1;
-  if (hipSetDevice(device) != hipSuccess) {
-    g_err = "hipSetDevice failed";
+  // ncclCommInitRank binds to the current device: select `device` for the call and restore the caller's
+  int prev = 0;
+  if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) {
+    g_err = "hipGetDevice / hipSetDevice failed";
     return -1;
   }
   ncclUniqueId id;
   std::memcpy(id.internal, uid, NCCL_UNIQUE_ID_BYTES);
   ncclComm_t c = nullptr;
   const ncclResult_t r = g_api.comm_init_rank(&c, nranks, id, rank);
+  (void)hipSetDevice(prev);
   if (r != ncclSuccess) return fail(r);
   std::lock_guard<std::mutex> lk(g_mu);
   g_comms.push_back(c);

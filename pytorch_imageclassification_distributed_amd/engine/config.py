@@ -57,11 +57,17 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--syncbn-comm", default="auto", choices=["auto", "peer", "rccl"],
                    help="SyncBN statistics transport: one-shot peer all-reduce over xGMI IPC buffers (peer), "
                         "torch.distributed / RCCL (rccl), or peer when all ranks share a host and it self-checks (auto)")
+    p.add_argument("--syncbn-check-every", type=int, default=100,
+                   help="every N train steps (and at each epoch end) check that all ranks hold bitwise-equal BN "
+                        "running statistics and that no SyncBN peer exchange timed out (0: epoch end only)")
     p.add_argument("--bucket-mb", type=float, default=32.0)
     p.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--comm-backend", default="pg", choices=["pg", "rccl"],
                    help="gradient buckets: torch.distributed's ProcessGroupNCCL (pg) or our C++ RCCL communicator "
-                        "(rccl: one comm stream behind the weight-gradient stream, parallel/rccl.py)")
+                        "(rccl: one comm stream behind the weight-gradient stream, parallel/rccl.py; a host "
+                        "watchdog ends the run if its collectives stall past --timeout-min).  rccl needs SyncBN "
+                        "off or on the peer transport: with SyncBN on RCCL the run falls back to pg (two "
+                        "communicators' collectives in flight on the same GPUs have no progress guarantee)")
     p.add_argument("--steps-per-epoch", type=int, default=None, help="cap on train steps per epoch")
     p.add_argument("--val-steps", type=int, default=None, help="cap on validation steps")
     p.add_argument("--resume", default="best",

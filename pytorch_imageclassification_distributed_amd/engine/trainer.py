@@ -41,7 +41,8 @@ from ..ops.grad_arena import GradArena
 from ..parallel import (GradReducer, check_peer_errors, check_syncbn_consistency, comm_timer, convert_sync_batchnorm,
                         setup_peer_syncbn)
 from ..utils import (BEST, LATEST, AccuracyCounter, DeviceMeter, JsonlLogger, load_checkpoint,
-                     load_model_state, resolve_resume, restore_rng_state, save_checkpoint)
+                     load_model_state, resolve_resume, save_checkpoint)
+from ..utils.checkpoint import gather_rng_states, restore_rank_rng
 from ..utils.timers import PhaseTimer
 from .config import hip_graph_enabled, parse_class_weights
 from .optim import FusedAdam, MultiStepLR
@@ -84,6 +85,10 @@ class Trainer:
         self.image_size = args.image_size or DEFAULT_IMAGE_SIZE.get(args.model, 224)
         self._build_data()
         self._build_model()
+        if ctx.world_size > 1:
+            # the weights are rank 0's (broadcast at construction); from here each rank draws its own dropout /
+            # drop-connect masks, as unseeded DDP ranks do (a checkpoint keeps every rank's streams: rng_ranks)
+            torch.manual_seed(args.seed + 1_000_003 * ctx.rank)
 
     # ------------------------------------------------------------------ data
     def _build_data(self):
@@ -159,8 +164,18 @@ class Trainer:
                     grp, self.dev, getattr(a, "syncbn_comm", "auto"))
             if ctx.world_size > 1:
                 comm = torch.bfloat16 if a.comm_dtype == "bf16" else None
-                self.reducer = GradReducer(model, bucket_cap_mb=a.bucket_mb, comm_dtype=comm,
-                                           comm=getattr(a, "comm_backend", "pg") if self.dev.type == "cuda" else "pg")
+                backend = getattr(a, "comm_backend", "pg") if self.dev.type == "cuda" else "pg"
+                if backend == "rccl" and a.sync_bn and not self.syncbn_peer:
+                    # SyncBN's statistics would go through ProcessGroupNCCL while the buckets ride our own
+                    # communicator: two communicators' collectives in flight on the same GPUs, in no common
+                    # order, have no progress guarantee - keep every collective on the process group
+                    if ctx.is_main:
+                        print("[imgcls] --comm-backend rccl needs SyncBN off or on the peer transport; "
+                              "gradient buckets use the process group (pg)", file=sys.stderr, flush=True)
+                    backend = "pg"
+                self.comm_backend = backend
+                self.reducer = GradReducer(model, bucket_cap_mb=a.bucket_mb, comm_dtype=comm, comm=backend,
+                                           timeout_s=60.0 * getattr(a, "timeout_min", 10.0))
                 self.arena = self.reducer.arena
             elif self.hip:
                 params = [p for p in model.parameters() if p.requires_grad]
@@ -245,6 +260,9 @@ class Trainer:
             return MAX_INFLIGHT_STEPS
         if self._auto_inflight is None:
             if self._steps_enqueued < 2:  # the first steps tune kernels: their peak is not the steady one
+                return 2
+            if self._steps_enqueued == 2:  # drop the tuning steps' peak; decide from the next step's
+                torch.cuda.reset_peak_memory_stats(self.dev)
                 return 2
             total = torch.cuda.get_device_properties(self.dev).total_memory
             small = torch.cuda.max_memory_allocated(self.dev) < SMALL_STEP_FRACTION * total
@@ -408,10 +426,15 @@ class Trainer:
             meter.update(self.reduce_loss(loss), images.size(0))
             self.global_step += 1
             n_log += images.size(0)
+            every = getattr(a, "syncbn_check_every", 100)
+            if self.syncbn_peer and every > 0 and self.global_step % every == 0:
+                # a timed-out SyncBN peer exchange is fatal; ranks must agree bitwise (parallel/peer.py) -
+                # its own interval: the guard is a collective plus a host sync, not a per-step cost
+                check_peer_errors(f"epoch {epoch} step {index}")
+                check_syncbn_consistency(self.model, None, f"epoch {epoch} step {index}")
             if (index + 1) % max(a.log_interval, 1) == 0:
-                if self.syncbn_peer:  # a timed-out SyncBN peer exchange is fatal (parallel/peer.py)
-                    check_peer_errors(f"epoch {epoch} step {index}")
-                    check_syncbn_consistency(self.model, None, f"epoch {epoch} step {index}")
+                if self.reducer is not None:
+                    self.reducer.check()  # native communicator async error (no-op on the process group)
                 if bar is not None:
                     bar.set_description(f"Epoch: {epoch}; Loss {meter.val:.4f}|({meter.avg:.4f})")
                 if self.timer.enabled:
@@ -482,8 +505,8 @@ class Trainer:
             self.optimizer.load_state_dict(ck["optimizer"])
         if "scheduler" in ck:
             self.scheduler.load_state_dict(ck["scheduler"])
-        if "rng" in ck:  # full resume: the run continues the saved random streams
-            restore_rng_state(ck["rng"])
+        # full resume: each rank continues its own saved random streams
+        self.rng_restored = restore_rank_rng(ck, self.ctx.rank, self.ctx.world_size)
         if "sampler_epoch" in ck:
             # the next epoch's DistributedSampler shuffle (seed + epoch), as the interrupted run would draw it
             self.start_epoch = int(ck["sampler_epoch"]) + 1
@@ -507,13 +530,15 @@ class Trainer:
             improved = val_acc > self.best_score
             if improved:
                 self.best_score = val_acc
+            save_latest = bool(a.latest_every) and epoch % a.latest_every == 0
+            rng_ranks = gather_rng_states() if save_latest else None  # collective: every rank's streams
             if self.ctx.is_main:
                 if improved:
                     print(f"Model improved to {val_acc} so storing checkpoint", flush=True)
                     save_checkpoint(self.ckpt_path(BEST), self.model, epoch, val_acc)
-                if a.latest_every and epoch % a.latest_every == 0:
+                if save_latest:
                     save_checkpoint(self.ckpt_path(LATEST), self.model, epoch, self.best_score,
-                                    self.optimizer, self.scheduler)
+                                    self.optimizer, self.scheduler, rng_ranks=rng_ranks)
             rec = dict(epoch=epoch, train_loss=train_loss, val_acc=val_acc, best=self.best_score,
                        lr=self.optimizer.param_groups[0]["lr"])
             history.append(rec)

@@ -447,7 +447,9 @@ def load_tuning(path: str) -> int:
         except (ValueError, SyntaxError, TypeError):
             continue
         fp8 = bool(k[10]) if len(k) > 10 else False
-        if v[2] >= HALO_BASE:
+        if v[2] >= DEEP_BASE:
+            ok = not fp8 and v[2] - DEEP_BASE < len(conv_deep_cfgs()) and len(v) == 3
+        elif v[2] >= HALO_BASE:
             ok = not fp8 and v[2] - HALO_BASE < len(conv_halo_cfgs()) and len(v) == 3
         else:
             ok = (v[2] - DIRECT_BASE in DIRECT_CFGS if v[2] >= DIRECT_BASE else
@@ -485,6 +487,8 @@ def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(
     if DIRECT_FORCE is not None and not fused and \
             _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales) is not None:
         cfg = (0, 0, DIRECT_BASE + DIRECT_FORCE)  # (tests) every eligible launch on this direct variant
+    elif DEEP_FORCE is not None and not fused and scales[0] is None and _deep_ok(geo, dh, dw):
+        cfg = (0, 0, DEEP_BASE + DEEP_FORCE)  # (tests) every eligible launch on this prefetch-depth-2 variant
     elif HALO_FORCE is not None and not fused and scales[0] is None and \
             _halo_ok(geo, dh, dw, *conv_halo_cfgs()[HALO_FORCE][::5]):
         cfg = (0, 0, HALO_BASE + HALO_FORCE)  # (tests) every eligible launch on this halo variant
@@ -504,7 +508,9 @@ def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(
                 A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups, scales, xa, xf, mask)
             if cfg[0] or cfg[2] >= 0:
                 _STAGES_TUNED[key] = cfg
-    if cfg[2] >= HALO_BASE:
+    if cfg[2] >= DEEP_BASE:
+        DEEP_COUNT[0] += 1
+    elif cfg[2] >= HALO_BASE:
         HALO_COUNT[0] += 1
     elif cfg[2] >= DIRECT_BASE:
         _direct_launch(A, B, out, stats, groups, _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales),
@@ -553,6 +559,29 @@ def _halo_ok(geo, dh, dw, tm, pmax):
     if m % (ih * iw) or any(abs(v) > 1 for v in dh) or any(abs(v) > 1 for v in dw):
         return False
     return tm + 2 * iw + 2 <= pmax and pmax * ca * 2 < (1 << 30)
+
+
+_DEEP_CFGS = None
+DEEP_CONV = os.environ.get("IMGCLS_DEEP", "1") == "1"  # prefetch-depth-2 kernels (csrc/conv_deep.hip) as tuner candidates
+DEEP_FORCE = None  # tests: force a deep variant on every eligible launch
+DEEP_COUNT = [0]   # deep-kernel launches (tests)
+DEEP_BASE = 2000   # cfg[2] >= DEEP_BASE: the prefetch-depth-2 kernel, entry cfg - base
+
+
+def conv_deep_cfgs():
+    """The prefetch-depth-2 kernel's table: (tile rows, tile channels, waves M, waves N, schedule variant);
+    variants with bit 2 or 4 set are diagnostics (wrong results) the tuner never times."""
+    global _DEEP_CFGS
+    if _DEEP_CFGS is None:
+        _DEEP_CFGS = [tuple(c) for c in C.conv_deep_cfgs()]
+    return _DEEP_CFGS
+
+
+def _deep_ok(geo, dh, dw):
+    """Uniform 64-channel k-steps and 16-bit input coordinates (csrc/conv_deep.hip::conv_deep_launch)."""
+    if geo[3] % 64:
+        return False
+    return (geo[6] <= 16383 and geo[7] <= 16383) or not any(dh) and not any(dw)
 
 
 _FP8_CFGS = None
@@ -661,6 +690,13 @@ def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, group
                     (bn == 64 and geo[1] >= 256) or geo[0] < tm * 16:
                 continue
             cfg = (0, 0, HALO_BASE + v)
+            times[cfg] = _time_ms(lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, groups, zero,
+                                                      addend, *bwd, *cfg, *scales, *xa3, None, *xf2, mask, None, None, None, 0))
+    if DEEP_CONV and not fused and scales[0] is None and _deep_ok(geo, dh, dw):
+        for v, (tm, bn, _wm, _wn, var) in enumerate(conv_deep_cfgs()):
+            if var & 6 or (bn > 64 and bn >= 2 * geo[1]) or (bn == 64 and geo[1] >= 256) or geo[0] < tm * 8:
+                continue
+            cfg = (0, 0, DEEP_BASE + v)
             times[cfg] = _time_ms(lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, groups, zero,
                                                       addend, *bwd, *cfg, *scales, *xa3, None, *xf2, mask, None, None, None, 0))
     dg = _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales) if not fused else None

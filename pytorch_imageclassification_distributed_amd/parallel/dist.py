@@ -92,8 +92,11 @@ def barrier(ctx: DistContext | None = None) -> None:
 
 
 def destroy() -> None:
-    """Tear down the SyncBN peer channels (IPC mappings, buffers), then the process group."""
+    """Tear down the native RCCL communicators, the SyncBN peer channels (IPC mappings, buffers), then the
+    process group."""
     from .peer import teardown_peer_syncbn
+    from .rccl import close_all
+    close_all()
     teardown_peer_syncbn()
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -224,27 +224,31 @@ class SyncBNMismatchError(RuntimeError):
 
 
 def check_syncbn_consistency(module, group=None, where: str = "") -> None:
-    """Steady-state guard for SyncBN (collective; call at log intervals): every rank must hold bitwise the
-    same BN running statistics, because each rank sums the same per-rank payloads in rank order (peer path) or
-    receives the same all-reduce result (RCCL).  A transport fault - a stale or torn slot - shows up here as a
-    mismatch, and the run stops instead of training on diverged statistics."""
+    """Steady-state guard for SyncBN (collective; call every ``--syncbn-check-every`` steps and at epoch end):
+    every rank must hold bitwise the same BN running statistics, because each rank sums the same per-rank
+    payloads in rank order (peer path) or receives the same all-reduce result (RCCL).  A transport fault - a
+    stale or torn slot - shows up here as a mismatch, and the run stops instead of training on diverged
+    statistics.  One flat pass: the running buffers are concatenated once and reduced to a position-weighted
+    checksum pair (a swapped or shifted buffer changes it too), then one 4-value all-reduce.  Non-finite
+    running statistics (a diverged run) are reported as such, not as a transport fault."""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return
     bufs = [b for n, b in module.named_buffers() if "running_" in n]
     if not bufs:
         return
-    dev = bufs[0].device
-    s = torch.zeros(2, dtype=torch.float64, device=dev)
-    for i, b in enumerate(bufs):  # position-weighted sums: a swapped or shifted buffer changes them too
-        v = b.detach().double().reshape(-1)
-        w = torch.arange(1, v.numel() + 1, dtype=torch.float64, device=dev) * (1.0 + 1e-3 * i)
-        s[0] += v.sum()
-        s[1] += (v * w).sum()
-    both = torch.cat([s, -s])
+    flat = torch.cat([b.detach().reshape(-1) for b in bufs]).double()
+    w = torch.arange(1, flat.numel() + 1, dtype=torch.float64, device=flat.device)
+    s = torch.stack([flat.sum(), (flat * w).sum()])
+    fin = torch.isfinite(s).all()
+    s = torch.where(fin, s, torch.zeros_like(s))
+    both = torch.cat([s, -s, (~fin).double().reshape(1)])
     dist.all_reduce(both, op=dist.ReduceOp.MAX, group=group)
-    if not torch.equal(both[:2], -both[2:]):
+    if both[4].item() > 0:
+        raise SyncBNMismatchError(f"SyncBN running statistics are not finite on some rank{' (' + where + ')' if where else ''}"
+                                  ": the run diverged (not a transport fault)")
+    if not torch.equal(both[:2], -both[2:4]):
         raise SyncBNMismatchError(f"SyncBN running statistics differ between ranks{' (' + where + ')' if where else ''}:"
-                                  f" checksum max {both[:2].tolist()} vs min {(-both[2:]).tolist()}")
+                                  f" checksum max {both[:2].tolist()} vs min {(-both[2:4]).tolist()}")
 
 
 def peer_channel(group, which: int):

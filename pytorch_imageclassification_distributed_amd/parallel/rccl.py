@@ -12,11 +12,20 @@ Rendezvous reuses the process group's TCPStore (env:// / torchrun compatible): r
 ``librccl.so``), so the process holds one RCCL whichever side calls it.
 
 Failure detection: ``check()`` polls ``ncclCommGetAsyncError`` (a dead peer / link error) and raises;
-``close(abort=True)`` tears the communicator down without waiting for peers.
+``close(abort=True)`` tears the communicator down without waiting for peers.  ProcessGroupNCCL's watchdog
+(``TORCH_NCCL_ASYNC_ERROR_HANDLING``, the PG timeout) does not cover this communicator, so ``CommWatchdog``
+does its job: a host thread polls the async error and the age of every step's "collectives done" event,
+and when either goes bad it aborts the communicator and ends the process non-zero - a dead peer cannot
+leave the compute stream waiting on a comm stream that never finishes (reference: the NCCL PG timeout,
+/root/reference/train.py:102).
 """
 from __future__ import annotations
 
+import collections
 import os
+import sys
+import threading
+import time
 
 import torch
 import torch.distributed as dist
@@ -31,6 +40,9 @@ def _lib():
     path = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
     C.rccl_load(path if os.path.exists(path) else "librccl.so")
     return C
+
+
+_LIVE: "list[RcclComm]" = []  # communicators not yet closed (parallel.dist.destroy() closes them)
 
 
 class RcclComm:
@@ -54,6 +66,7 @@ class RcclComm:
             self.handle = self.C.rccl_comm_init(bytes(uid), self.world, self.rank, self.device.index)
             # collectives run on their own stream, above the compute streams' priority
             self.stream = torch.cuda.Stream(device=self.device, priority=-1)
+        _LIVE.append(self)
 
     # ------------------------------------------------------------------ collectives
     def all_reduce_(self, t: torch.Tensor, op: str = "sum", after: torch.cuda.Stream | None = None) -> torch.Tensor:
@@ -81,10 +94,80 @@ class RcclComm:
         if e != 0:
             raise RuntimeError(f"RCCL communicator error {e}: {self.C.rccl_last_error()}")
 
+    def async_error(self) -> int:
+        return int(self.C.rccl_async_error(self.handle)) if getattr(self, "handle", 0) else 0
+
     def close(self, abort: bool = False) -> None:
         if getattr(self, "handle", 0):
             self.C.rccl_comm_close(self.handle, abort)
             self.handle = 0
+        if self in _LIVE:
+            _LIVE.remove(self)
+
+
+def close_all(abort: bool = False) -> None:
+    for c in list(_LIVE):
+        c.close(abort)
+
+
+class CommWatchdog:
+    """Host-side deadline for collectives on a communicator the process group does not watch.
+
+    ``arm(done)`` registers a completion probe (a HIP event recorded on the comm stream after a step's
+    collectives; anything with ``query() -> bool``).  A daemon thread polls every ``interval`` s: if
+    ``poll_error()`` is non-zero, or the oldest unfinished probe is older than ``timeout`` s, it calls
+    ``abort()`` (RcclComm.close(abort=True)) and ``on_fatal(message)`` - by default a message on stderr and
+    ``os._exit(exit_code)``, the process-level equivalent of ProcessGroupNCCL's async error handling (the
+    main thread may be blocked inside a device synchronisation that would never return)."""
+
+    def __init__(self, poll_error, abort, timeout: float = 600.0, interval: float = 0.5, exit_code: int = 13,
+                 on_fatal=None):
+        self.poll_error, self.abort, self.timeout, self.interval = poll_error, abort, timeout, interval
+        self.exit_code = exit_code
+        self.on_fatal = on_fatal if on_fatal is not None else self._die
+        self._pending = collections.deque()
+        self._lock = threading.Lock()
+        self._stop = threading.Event()
+        self.fired = None
+        self._t = threading.Thread(target=self._run, name="imgcls-comm-watchdog", daemon=True)
+        self._t.start()
+
+    def arm(self, done) -> None:
+        with self._lock:
+            self._pending.append((time.monotonic(), done))
+
+    def _die(self, msg: str) -> None:
+        print(f"[imgcls] FATAL: {msg}; aborting the communicator and exiting ({self.exit_code})", file=sys.stderr,
+              flush=True)
+        os._exit(self.exit_code)
+
+    def check_once(self) -> str | None:
+        e = self.poll_error()
+        if e:
+            return f"RCCL communicator reported asynchronous error {e}"
+        now = time.monotonic()
+        with self._lock:
+            while self._pending and self._pending[0][1].query():
+                self._pending.popleft()
+            if self._pending and now - self._pending[0][0] > self.timeout:
+                return f"collectives enqueued {now - self._pending[0][0]:.0f} s ago have not completed (timeout " \
+                       f"{self.timeout:.0f} s): a peer is dead or hung"
+        return None
+
+    def _run(self) -> None:
+        while not self._stop.wait(self.interval):
+            msg = self.check_once()
+            if msg is not None:
+                self.fired = msg
+                try:
+                    self.abort()
+                finally:
+                    self.on_fatal(msg)
+                return
+
+    def stop(self) -> None:
+        self._stop.set()
+        self._t.join(timeout=5)
 
 
 def rccl_version() -> int:

@@ -77,7 +77,7 @@ class GradReducer:
     def __init__(self, module: nn.Module, group=None, bucket_cap_mb: float = 32.0,
                  first_bucket_mb: float = 1.0, broadcast: bool = True,
                  rebuild_buckets: bool = True, comm_dtype: torch.dtype | None = None, comm: str = "pg",
-                 force_collectives: bool = False):
+                 force_collectives: bool = False, timeout_s: float = 600.0):
         self.module = module
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -93,10 +93,13 @@ class GradReducer:
         # force_collectives (tests): run the bucket collectives even in a world of one
         self._collect = self.world > 1 or force_collectives
         self.rccl = None
+        self.watchdog = None
         if comm == "rccl" and self._collect:
-            from .rccl import RcclComm
+            from .rccl import CommWatchdog, RcclComm
             dev = next(iter(self.params)).device
             self.rccl = RcclComm(group, dev)
+            # the process group's timeout / async error handling do not watch this communicator
+            self.watchdog = CommWatchdog(self.rccl.async_error, lambda: self.rccl.close(abort=True), timeout_s)
         elif comm not in ("pg", "rccl"):
             raise ValueError(f"GradReducer: comm must be 'pg' or 'rccl', not {comm!r}")
         self._verify_param_shapes()
@@ -232,6 +235,9 @@ class GradReducer:
                 self._launch(b)
         if self.rccl is not None and self.works:
             self.rccl.join()  # the compute stream waits for every bucket's collective
+            done = torch.cuda.Event()
+            done.record(self.rccl.stream)
+            self.watchdog.arm(done)  # a step whose collectives never finish ends the process (CommWatchdog)
         for work, dst, comp in self.works:
             if work is not None:
                 work.wait()
@@ -267,6 +273,20 @@ class GradReducer:
             return
         for b in self.module.buffers():
             dist.broadcast(b, src, group=self.group)
+
+    def check(self) -> None:
+        """Raise if the native communicator reported an asynchronous error (log-interval health check)."""
+        if self.rccl is not None:
+            self.rccl.check()
+
+    def close(self) -> None:
+        """Stop the watchdog and free the native communicator (no-op on the process-group path)."""
+        if self.watchdog is not None:
+            self.watchdog.stop()
+            self.watchdog = None
+        if self.rccl is not None:
+            self.rccl.close()
+            self.rccl = None
 
     def remove_hooks(self) -> None:
         for h in self._hooks:

@@ -9,7 +9,9 @@ Kept: paths, file names, the three keys, the ``module.`` prefix, best-on-
 improvement and latest-every-5-epochs cadence.  Fixed:
 * the directory is created (A10);
 * ``latest_model`` additionally stores ``optimizer``, ``scheduler``, ``rng`` and
-  ``sampler_epoch`` as *extra* keys (A9);
+  ``sampler_epoch`` as *extra* keys (A9), and ``rng_ranks`` - every rank's random
+  streams (gathered to rank 0), so a resumed multi-rank run draws per-rank dropout /
+  drop-connect masks as the uninterrupted one would;
 * resume honours the stored epoch, can pick ``latest`` or ``best`` (A11), and
   accepts keys with or without the ``module.`` prefix (partial key match as the
   reference does, train.py:143-147);
@@ -52,6 +54,31 @@ def _rng_state() -> dict:
     return st
 
 
+def gather_rng_states() -> list:
+    """Every rank's ``_rng_state()`` on every rank (collective when a process group with > 1 rank exists)."""
+    import torch.distributed as dist
+    mine = _rng_state()
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return [mine]
+    box = [None] * dist.get_world_size()
+    dist.all_gather_object(box, mine)
+    return box
+
+
+def restore_rank_rng(ck: dict, rank: int, world: int) -> str:
+    """Restore this rank's random streams from a checkpoint: its own entry of ``rng_ranks`` when the run has
+    the same world size, else the single ``rng`` entry (rank 0's - every rank then draws the same masks).
+    Returns which one was used."""
+    ranks = ck.get("rng_ranks")
+    if isinstance(ranks, list) and len(ranks) == world:
+        restore_rng_state(ranks[rank])
+        return "rank"
+    if "rng" in ck:
+        restore_rng_state(ck["rng"])
+        return "shared"
+    return "none"
+
+
 def restore_rng_state(st: dict) -> None:
     """Inverse of ``_rng_state`` (resume).  Older checkpoints that stored only the key arrays restore
     what they have."""
@@ -69,7 +96,7 @@ def restore_rng_state(st: dict) -> None:
 
 
 def save_checkpoint(path: str, model, epoch: int, best_score: float, optimizer=None,
-                    scheduler=None, extra: dict | None = None) -> None:
+                    scheduler=None, extra: dict | None = None, rng_ranks: list | None = None) -> None:
     os.makedirs(os.path.dirname(path), exist_ok=True)
     payload = {"epoch": epoch, "best_score": float(best_score), "state_dict": ddp_state_dict(model)}
     if optimizer is not None:
@@ -77,6 +104,8 @@ def save_checkpoint(path: str, model, epoch: int, best_score: float, optimizer=N
     if scheduler is not None:
         payload["scheduler"] = scheduler.state_dict()
     payload["rng"] = _rng_state()
+    if rng_ranks is not None:
+        payload["rng_ranks"] = rng_ranks
     payload["sampler_epoch"] = epoch
     if extra:
         payload.update(extra)

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--op", default="fwd", choices=["fwd", "dgrad", "wgrad"])
     ap.add_argument("--cfg", type=int, default=-1)
     ap.add_argument("--halo", type=int, default=-1)
+    ap.add_argument("--deep", type=int, default=-1, help="index into ops.hip.conv_deep_cfgs() (prefetch-depth-2 kernel)")
     ap.add_argument("--wstages", type=int, default=0)
     ap.add_argument("--iters", type=int, default=20)
     a = ap.parse_args()
@@ -39,6 +40,8 @@ def main():
         hip.CONV_FORCE_CFG = (0, 0, a.cfg)
     if a.halo >= 0:
         hip.HALO_FORCE = a.halo
+    if a.deep >= 0:
+        hip.DEEP_FORCE = a.deep
     if a.wstages:
         hip.WGRAD_STAGES = a.wstages
     hip.ensure_channels_last_weight(conv)

@@ -11,28 +11,27 @@ import csv
 import os
 import sys
 
-runs = collections.defaultdict(dict)  # probe tag -> counter -> mean
+runs = collections.defaultdict(dict)  # (probe tag, kernel) -> counter -> mean
 for d in sys.argv[1:]:
     f = os.path.join(d, "p_counter_collection.csv")
     if not os.path.exists(f):
         continue
     tag = os.path.basename(d)[:-2]
-    acc = collections.defaultdict(list)
-    name = None
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        if "glds_kernel" not in k and "direct_conv" not in k:
+        if not any(t in k for t in ("glds_kernel", "direct_conv", "deep_kernel", "Cijk")):
             continue
-        name = k
-        acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    runs[tag].update({c: sum(v) / len(v) for c, v in acc.items()})
-    if name:
-        runs[tag]["kernel"] = name.replace("void (anonymous namespace)::", "").split("(")[0]
-for tag, c in sorted(runs.items()):
+        kn = k.replace("void (anonymous namespace)::", "").split("(")[0]
+        acc[kn][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    for kn, cs in acc.items():
+        runs[(tag, kn)].update({c: sum(v) / len(v) for c, v in cs.items()})
+        runs[(tag, kn)]["kernel"] = kn
+for (tag, _kn), c in sorted(runs.items()):
     simd_cycles = c.get("GRBM_GUI_ACTIVE", 0) / 8 * 1024
     wc = c.get("SQ_WAVE_CYCLES", 0) or 1
     waves = c.get("SQ_WAVES", 0) or 1
-    print(f"{tag}: {c.get('kernel', '?')}")
+    print(f"{tag}: {c.get('kernel', '?')[:90]}")
     if simd_cycles:
         print(f"  MFMA busy {100 * c.get('SQ_VALU_MFMA_BUSY_CYCLES', 0) / simd_cycles:5.1f} % of SIMD-cycles")
     print(f"  wave-cycles: parked (waitcnt / barrier) {100 * c.get('SQ_WAIT_ANY', 0) / wc:4.1f} %, issue-stalled "

@@ -302,3 +302,217 @@ def test_syncbn_consistency_guard():
     """Steady-state SyncBN guard: diverged running statistics on any rank stop the run on
     every rank (the check is collective, so all ranks raise together)."""
     _run(_w_syncbn_guard)
+
+
+# ---------------------------------------------------------------------------
+def _bench(args, env_extra=None, timeout=300):
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=timeout, env=env, cwd=root)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r.returncode, (json.loads(lines[-1]) if lines else None), r.stderr
+
+
+def test_bench_gpus_flag_launches_the_ranks():
+    """``bench.py --gpus 2`` with no launcher starts 2 ranks itself (torch.distributed.run, 127.0.0.1) and the
+    JSON line reports the whole job: n_gpus 2, dp2, global batch = 2 x per-GPU batch (gloo CPU rehearsal)."""
+    rc, out, err = _bench(["--gpus", "2", "--device", "cpu", "--model", "resnet18", "--image-size", "32",
+                           "--batch", "4", "--steps", "2", "--warmup", "1"])
+    assert rc == 0, err[-2000:]
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 8
+    assert out["steps"] == 2 and out["value"] > 0 and "not a benchmark" in out["metric"]
+
+
+def test_bench_refuses_a_world_size_mismatch():
+    """A single rank asked for ``--gpus 2`` under a launcher-provided WORLD_SIZE=1 exits non-zero without a
+    (mislabelled) JSON line."""
+    rc, out, _ = _bench(["--gpus", "2", "--device", "cpu", "--model", "resnet18", "--image-size", "32",
+                         "--batch", "2", "--steps", "1", "--warmup", "1"],
+                        env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                                   "MASTER_PORT": str(_port())})
+    assert rc == 2 and out is None
+
+
+# ---------------------------------------------------------------------------
+def _w_resume(rank, world, port, ck, port2):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import train
+    from pytorch_imageclassification_distributed_amd.utils import load_checkpoint
+    args = ["--synthetic", "--model", "resnet18", "--image-size", "32", "--device", "cpu", "--batchsize", "8",
+            "--num-workers", "0", "--synthetic-train-size", "64", "--synthetic-val-size", "16", "--no-progress",
+            "--val-batchsize", "8", "--steps-per-epoch", "2", "--val-steps", "1", "--latest-every", "1",
+            "--ckpt-dir", ck]
+    train.main(args + ["--epochs", "1", "--resume", "none"])
+    import time
+    path = os.path.join(ck, "resnet18", "latest_model")
+    for _ in range(600):  # rank 0 writes it (temp file + rename): wait until it exists
+        if os.path.exists(path):
+            break
+        time.sleep(0.1)
+    lt = load_checkpoint(path)
+    assert len(lt["rng_ranks"]) == world
+    # the ranks' streams differ (per-rank seeding), and each entry is that rank's own
+    assert not torch.equal(lt["rng_ranks"][0]["torch"], lt["rng_ranks"][1]["torch"])
+    assert torch.equal(lt["rng"]["torch"], lt["rng_ranks"][0]["torch"])
+    mine = lt["rng_ranks"][rank]["torch"]
+    from pytorch_imageclassification_distributed_amd.engine import trainer as tm
+    seen = {}
+    orig = tm.Trainer.maybe_resume
+
+    def spy(self):
+        orig(self)
+        seen["how"] = getattr(self, "rng_restored", None)
+        seen["state"] = torch.get_rng_state().clone()
+    tm.Trainer.maybe_resume = spy
+    os.environ["MASTER_PORT"] = str(port2)  # a fresh rendezvous for the second process group
+    try:
+        hist = train.main(args + ["--epochs", "2", "--resume", "latest"])
+    finally:
+        tm.Trainer.maybe_resume = orig
+    assert [h["epoch"] for h in hist] == [1]
+    assert seen["how"] == "rank" and torch.equal(seen["state"], mine)
+
+
+def test_resume_restores_each_ranks_rng(tmp_path):
+    """2-rank gloo: latest_model stores every rank's random streams (rng_ranks), and --resume latest gives
+    each rank back its own - not rank 0's (reference train.py:183-188 saves from rank 0 only)."""
+    port, port2 = _port(), _port()
+    mp.spawn(_w_resume, args=(2, port, str(tmp_path), port2), nprocs=2, join=True)
+
+
+# ---------------------------------------------------------------------------
+class _Probe:
+    def __init__(self, done=False):
+        self.done = done
+
+    def query(self):
+        return self.done
+
+
+def test_comm_watchdog_aborts_on_async_error():
+    """The native communicator's watchdog (parallel/rccl.py CommWatchdog): an asynchronous RCCL error aborts
+    the communicator and ends the process (os._exit by default; a recorder here)."""
+    import time
+
+    from pytorch_imageclassification_distributed_amd.parallel.rccl import CommWatchdog
+    err, calls = [0], []
+    wd = CommWatchdog(lambda: err[0], lambda: calls.append("abort"), timeout=60, interval=0.01,
+                      on_fatal=lambda m: calls.append(m))
+    wd.arm(_Probe(True))
+    time.sleep(0.1)
+    assert calls == [] and wd.fired is None
+    err[0] = 6  # ncclRemoteError
+    for _ in range(200):
+        if len(calls) == 2:
+            break
+        time.sleep(0.01)
+    assert calls[0] == "abort" and "asynchronous error 6" in calls[1]
+    wd.stop()
+
+
+def test_comm_watchdog_ends_a_hung_collective():
+    """Collectives whose completion event never fires within the deadline abort the communicator and end the
+    process - a dead peer cannot leave a rank waiting forever (the PG timeout does not watch this comm)."""
+    import subprocess
+    import sys
+    code = ("import time\n"
+            "from pytorch_imageclassification_distributed_amd.parallel.rccl import CommWatchdog\n"
+            "class P:\n    def query(self): return False\n"
+            "wd = CommWatchdog(lambda: 0, lambda: print('aborted', flush=True), timeout=0.3, interval=0.05)\n"
+            "wd.arm(P())\n"
+            "time.sleep(30)\n"
+            "print('not reached', flush=True)\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60, cwd=root)
+    assert r.returncode == 13, (r.returncode, r.stdout, r.stderr)
+    assert "aborted" in r.stdout and "not reached" not in r.stdout and "have not completed" in r.stderr
+
+
+def test_grad_reducer_wires_the_watchdog(monkeypatch):
+    """GradReducer(comm='rccl') arms the watchdog with one completion event per step and check() raises on
+    an async error (a stub communicator stands in for RcclComm: RCCL needs GPUs)."""
+    import types
+
+    from pytorch_imageclassification_distributed_amd.parallel import rccl as R
+    from pytorch_imageclassification_distributed_amd.parallel.reducer import GradReducer
+
+    class FakeComm:
+        def __init__(self, group=None, device=None):
+            self.err = 0
+            self.closed = None
+
+        def async_error(self):
+            return self.err
+
+        def check(self):
+            if self.err:
+                raise RuntimeError(f"RCCL communicator error {self.err}")
+
+        def close(self, abort=False):
+            self.closed = abort
+
+    monkeypatch.setattr(R, "RcclComm", FakeComm)
+    m = torch.nn.Linear(4, 2)
+    red = GradReducer(m, comm="rccl", force_collectives=True, broadcast=False)
+    assert isinstance(red.watchdog, R.CommWatchdog) and red.watchdog.timeout == 600.0
+    red.check()
+    red.rccl.err = 2
+    with pytest.raises(RuntimeError, match="error 2"):
+        red.check()
+    red.rccl.err = 0
+    comm = red.rccl
+    red.close()
+    assert red.watchdog is None and red.rccl is None and comm.closed is False
+
+
+# ---------------------------------------------------------------------------
+def _w_syncbn_guard(rank, world, port):
+    _setup(rank, world, port)
+    from pytorch_imageclassification_distributed_amd.parallel.peer import SyncBNMismatchError, check_syncbn_consistency
+    m = torch.nn.Sequential(torch.nn.BatchNorm2d(4), torch.nn.BatchNorm2d(3))
+    check_syncbn_consistency(m)  # equal on both ranks
+    if rank == 1:
+        m[1].running_mean[2] += 1e-6
+    with pytest.raises(SyncBNMismatchError, match="differ between ranks"):
+        check_syncbn_consistency(m)
+    if rank == 1:
+        m[1].running_mean[2] -= 1e-6
+        m[0].running_var[1] = float("nan")
+    with pytest.raises(SyncBNMismatchError, match="not finite"):
+        check_syncbn_consistency(m)
+
+
+def test_syncbn_guard_flat_checksum_and_nonfinite():
+    """The SyncBN guard (one flat checksum + one all-reduce): a one-ulp difference on one rank is a mismatch;
+    a NaN running statistic is reported as divergence, consistently on every rank, not as a transport fault."""
+    _run(_w_syncbn_guard)
+
+
+def test_syncbn_guard_runs_on_its_own_interval(monkeypatch, tmp_path):
+    """The guard (a collective + host sync) runs every --syncbn-check-every steps and at epoch end, not at
+    every log interval (--log-interval defaults to 1)."""
+    import train
+    from pytorch_imageclassification_distributed_amd.engine import trainer as tm
+    calls = []
+    monkeypatch.setattr(tm, "check_syncbn_consistency", lambda *a, **k: calls.append("sum"))
+    monkeypatch.setattr(tm, "check_peer_errors", lambda *a, **k: calls.append("err"))
+    orig = tm.Trainer._build_model
+
+    def build(self):
+        orig(self)
+        self.syncbn_peer = True  # pretend the peer transport is up (CPU: it never is)
+    monkeypatch.setattr(tm.Trainer, "_build_model", build)
+    args = ["--synthetic", "--model", "resnet18", "--image-size", "32", "--device", "cpu", "--batchsize", "8",
+            "--num-workers", "0", "--synthetic-train-size", "48", "--synthetic-val-size", "8", "--no-progress",
+            "--epochs", "1", "--resume", "none", "--ckpt-dir", str(tmp_path)]
+    train.main(args + ["--syncbn-check-every", "2"])  # 6 steps: after steps 2, 4, 6 and at epoch end
+    assert calls.count("sum") == 4
+    calls.clear()
+    train.main(args)  # default interval 100: epoch end only
+    assert calls.count("sum") == 1

@@ -148,6 +148,69 @@ def test_conv_halo_configs(case, cfg):
         assert hip.HALO_COUNT[0] - before >= expect, "halo kernel not launched"
 
 
+N_DEEP = _table_len("conv_deep_cfgs", 12)
+DEEP_CASES = [CONV_CASES[i] for i in (0, 1, 2, 3, 4, 5, 6)] + [
+    (2, 128, 15, 13, 128, (3, 3), 1, (1, 1)),  # odd map: partial last row tile
+    (2, 128, 28, 28, 96, (3, 3), 1, (1, 1)),   # partial output-channel tile
+    (1, 64, 9, 9, 320, (3, 3), 2, (1, 1)),     # stride 2, partial column tile of a 256-wide tile
+]
+
+
+@pytest.mark.parametrize("cfg", range(N_DEEP))
+@pytest.mark.parametrize("case", DEEP_CASES)
+def test_conv_deep_configs(case, cfg):
+    """Every prefetch-depth-2 configuration (csrc/conv_deep.hip) forced on each launch it accepts (64-channel
+    k-steps): forward and data-gradient phases against the fp32 reference, and the kernel ran."""
+    hip = _hip()
+    if cfg >= len(hip.conv_deep_cfgs()) or hip.conv_deep_cfgs()[cfg][4] & 6:
+        pytest.skip("past the configuration table / a diagnostic variant")
+    keep, hip.DEEP_FORCE = hip.DEEP_FORCE, cfg
+    before = hip.DEEP_COUNT[0]
+    try:
+        test_conv_fwd_bwd(case)
+    finally:
+        hip.DEEP_FORCE = keep
+    assert hip.DEEP_COUNT[0] - before >= 1 + (case[4] % 64 == 0), "deep kernel not launched"
+
+
+@pytest.mark.parametrize("cfg", range(N_DEEP))
+@pytest.mark.parametrize("act,use_res", [("relu", True), ("silu", False)])
+def test_conv_bn_act_deep(act, use_res, cfg):
+    """Fused epilogues (BN statistics, residual, BN-backward link) on every prefetch-depth-2 configuration."""
+    hip = _hip()
+    if cfg >= len(hip.conv_deep_cfgs()) or hip.conv_deep_cfgs()[cfg][4] & 6:
+        pytest.skip("past the configuration table / a diagnostic variant")
+    keep, hip.DEEP_FORCE = hip.DEEP_FORCE, cfg
+    before = hip.DEEP_COUNT[0]
+    try:
+        test_conv_bn_act(act, use_res)
+    finally:
+        hip.DEEP_FORCE = keep
+    assert hip.DEEP_COUNT[0] > before
+
+
+@pytest.mark.parametrize("cfg", range(N_DEEP))
+@pytest.mark.parametrize("mnk", [(4096 + 40, 512, 1024), (700, 200, 192), (20000, 2048, 64)])
+def test_conv_deep_plain_gemm(mnk, cfg):
+    """The GEMM view (benchmarks/gemm_ref.py: a 1x1 conv over an M x 1 'image', so the input height exceeds
+    the kernel's 16-bit coordinates) against torch.mm in fp32: partial row / column tiles, K of 1..16 steps."""
+    hip = _hip()
+    if cfg >= len(hip.conv_deep_cfgs()) or hip.conv_deep_cfgs()[cfg][4] & 6:
+        pytest.skip("past the configuration table / a diagnostic variant")
+    M, N, K = mnk
+    torch.manual_seed(0)
+    A = (torch.rand(M, K, device=DEV) * 2 - 1).to(torch.bfloat16)
+    B = (torch.rand(N, K, device=DEV) * 2 - 1).to(torch.bfloat16)
+    out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+    geo = (M, N, K, K, M, 1, M, 1, 1, K, M, 1, 1, 0, 0, N, 0)
+    hip.C.conv_gemm(A, B.view(-1), out, None, None, *geo, [0], [0], [0], hip.G_STATS, hip.ws(torch.device(DEV)).zero,
+                    None, None, None, None, None, 0, 1, 0, 0, hip.DEEP_BASE + cfg, None, None, None, None, None, None,
+                    None, 0, None, None, None, None, 0)
+    ref = A.float() @ B.float().t()
+    assert torch.isfinite(out.float()).all()
+    assert rel_err(out, ref) < 1e-2
+
+
 @pytest.mark.parametrize("cfg", range(N_HALO))
 @pytest.mark.parametrize("act,use_res", [("relu", True), ("silu", False)])
 def test_conv_bn_act_halo(act, use_res, cfg):
