@@ -75,6 +75,9 @@ def parse():
                    help="device: batches generated once in HBM (the step alone); host: pinned uint8 host batches "
                         "copied by hipMemcpyAsync on a copy stream and normalised on the GPU inside the timed loop "
                         "(the real-data path minus decode, K24/K25)")
+    p.add_argument("--host-input", default="fused", choices=["fused", "fp32"],
+                   help="--data host: fused = uint8 -> model input (bf16, s2d stem layout) in one kernel on the copy "
+                        "stream; fp32 = the older normalize_u8 to fp32 NCHW, converted again inside the step")
     p.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                    help="cpu: functional rehearsal of the multi-rank path over gloo (no GPU; never a benchmark)")
     p.add_argument("--comm-timing", default="auto", choices=["auto", "on", "off"],
@@ -181,6 +184,8 @@ def main():
     if a.data == "host":
         data = HostSyntheticLoader(a.batch, a.num_classes, a.image_size, ctx.device,
                                    steps=a.warmup + a.steps + 1, ring=2, seed=1234 + ctx.rank)
+        if a.host_input == "fused":
+            data.input_fn = tr.input_fn  # uint8 -> the model's bf16 input in one kernel on the copy stream
         host_it = iter(data)
     else:
         data = DeviceSyntheticLoader(a.batch, a.num_classes, a.image_size, ctx.device,

@@ -71,6 +71,7 @@ int adam_tick_launch(float*, float, hipStream_t);
 int prepare_input_launch(const float*, bf16_t*, int, int, int, int, const float*, const float*, hipStream_t);
 int prepare_input_s2d_launch(const float*, bf16_t*, int, int, int, hipStream_t);
 int normalize_u8_launch(const uint8_t*, float*, long, int, const float*, const float*, hipStream_t);
+int input_u8_launch(const uint8_t*, bf16_t*, int, int, int, int, const float*, hipStream_t);
 int cast_bf16_launch(const float*, bf16_t*, long, hipStream_t);
 int weight_pad_launch(const bf16_t*, bf16_t*, long, int, int, hipStream_t);
 int weight_t_launch(const bf16_t*, bf16_t*, int, int, int, hipStream_t);
@@ -577,6 +578,27 @@ void adam(Tensor table, Tensor chunks, int nchunks, Tensor lr_step, double b1, d
 
 void adam_tick(Tensor lr_step, double lr) { check(adam_tick_launch(ptr<float>(lr_step), (float)lr, cur()), "adam_tick"); }
 
+// uint8 NHWC RGB batch -> the model's bf16 input in one pass: y = u * a[c] + b[c] (normalisation and any
+// transform_input folded by the caller); s2d = 1: the space-to-depth stem layout [N][H/2][W/2][16],
+// else NHWC padded to 8 channels
+void input_u8(Tensor x, Tensor y, std::vector<double> a, std::vector<double> b, int s2d) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kByte && x.dim() == 4 && x.size(3) == 3 && x.is_contiguous(),
+              "input_u8: x is contiguous uint8 [N,H,W,3] on the GPU");
+  req(y, BF, "y");
+  TORCH_CHECK(a.size() == 3 && b.size() == 3, "input_u8: 3 scales and 3 offsets");
+  const int N = (int)x.size(0), H = (int)x.size(1), W = (int)x.size(2);
+  if (s2d) {
+    TORCH_CHECK(H % 2 == 0 && W % 2 == 0 && y.numel() == (long long)N * (H / 2) * (W / 2) * 16,
+                "input_u8: the s2d layout needs even H, W and y of N*H/2*W/2*16 elements");
+  } else {
+    TORCH_CHECK(((long long)N * H * W) % 4 == 0 && y.numel() == (long long)N * H * W * 8,
+                "input_u8: NHWC8 needs N*H*W % 4 == 0 and y of N*H*W*8 elements");
+  }
+  TORCH_CHECK(y.is_contiguous() || y.is_contiguous(at::MemoryFormat::ChannelsLast), "input_u8: dense y");
+  const float f[6] = {(float)a[0], (float)a[1], (float)a[2], (float)b[0], (float)b[1], (float)b[2]};
+  check(input_u8_launch(x.data_ptr<uint8_t>(), ptr<bf16_t>(y), N, H, W, s2d, f, cur()), "input_u8");
+}
+
 void normalize_u8(Tensor x, Tensor y, std::vector<double> mean, std::vector<double> std_) {
   req(x, at::kByte, "x"); req(y, F32, "y");
   TORCH_CHECK(x.dim() == 4 && x.size(3) == 3 && x.is_contiguous(), "normalize_u8: x is contiguous uint8 [N,H,W,3]");
@@ -994,6 +1016,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("prepare_input", &prepare_input);
   m.def("prepare_input_s2d", &prepare_input_s2d);
   m.def("normalize_u8", &normalize_u8);
+  m.def("input_u8", &input_u8);
   register_loader(m);
   m.def("bn_set_reduce_blocks", &bn_set_reduce_blocks, pybind11::arg("n"), pybind11::arg("chb") = 0);
   m.def("bn_act_maxpool", &bn_act_maxpool);

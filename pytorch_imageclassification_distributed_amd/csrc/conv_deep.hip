@@ -45,6 +45,11 @@ DEVI void mfma_acc(f32x4& acc, const bf16x8& a, const bf16x8& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b) : "memory");
 }
 
+// LDS-DMA of 16 B per lane with a per-lane offset and a wave-uniform (SGPR) offset
+DEVI void blds16s(__amdgpu_buffer_rsrc_t r, unsigned voff, int soff, char* lds_wave_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, soff, 0, 0);
+}
+
 // lgkmcnt(0) through the builtin, so hipcc's wait-count pass knows the fragments have landed
 DEVI void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }
 
@@ -76,7 +81,20 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_deep_kernel(const ConvPa
   const int wm = wid / WN, wn = wid % WN;
   const int gm = (p.M + TM - 1) / TM, gn = (p.Ncols + BN - 1) / BN;
   const int lin = xcd_remap(blockIdx.x, gm * gn);
-  const int bm = lin / gn, bn = lin - bm * gn;
+  // GROUP (variant 64 / 128): consecutive tiles of an XCD walk a GROUP-row band column by column, so the
+  // XCD's L2 holds GROUP row panels + (tiles / GROUP) column panels instead of ~2 + tiles (row-major order)
+  constexpr int GROUP = (PRIO & 64) ? 4 : (PRIO & 128) ? 8 : 1;
+  int bm, bn;
+  if constexpr (GROUP > 1) {
+    const int band = lin / (GROUP * gn), first = band * GROUP;
+    const int rows = gm - first < GROUP ? gm - first : GROUP;
+    const int r = lin - band * GROUP * gn;
+    bm = first + r % rows;
+    bn = r / rows;
+  } else {
+    bm = lin / gn;
+    bn = lin - bm * gn;
+  }
   const int m0 = bm * TM, n0 = bn * BN;
   if (tid < p.ntaps) s_tap[tid] = tap_pack(p.tap_dh[tid], p.tap_dw[tid], p.tap_b[tid]);
   const int lrow = lane >> 3, pch = lane & 7;
@@ -98,7 +116,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_deep_kernel(const ConvPa
       a_hw[i] = hw_pack(ih, iw);
       a_pix[i] = (n - n_img0) * img + (ih * p.IW + iw) * p.CA + ch * 8;
     } else {
-      a_hw[i] = (-16384) << 16;
+      a_hw[i] = (int)0xC0000000;  // row -16384: no tap is in bounds
       a_pix[i] = 0;
     }
   }
@@ -115,29 +133,38 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_deep_kernel(const ConvPa
   // Every k-step issues its LPS pieces - the ones past the last tile go to a zero-extent resource (they land
   // zeros into the buffer just released), so the loop below has no branches and its vmcnt waits are constant.
   const __amdgpu_buffer_rsrc_t rsZ = make_rsrc(p.A, 0);
-  int u_tap = 0, u_ci = 0, u_k = 0;
+  // The per-lane source offsets change only at a tap boundary (per-row validity and the tap's pixel shift);
+  // the channel slice of a k-step is a wave-uniform byte offset passed as the load's SGPR offset, so a
+  // k-step inside a tap costs no VALU at all (the library GEMM's loop has ~7 VALU per k-step; a per-piece
+  // address recompute cost this kernel ~30 points of MFMA busy: profiles/r9d_*).
+  int u_tap = 0, u_ci = 0;
   int u_pk = s_tap[0];
-  unsigned voff[LPS];
-  auto plan = [&]() {  // source offsets of the next k-step's pieces
-    const int pk = __builtin_amdgcn_readfirstlane(u_pk);
-    const int dh = tap_dh(pk), dw = tap_dw(pk);
-    const int a_t = (dh * p.IW + dw) * p.CA + u_ci;
-    const unsigned b_t = 2u * (unsigned)(tap_tb(pk) * p.CA + u_ci);
+  unsigned a_vb[AL];
+  int s_tb = 0, s_off_a = 0, s_off_b = 0;
 #pragma unroll
-    for (int i = 0; i < AL; ++i) {
-      const int ih = a_hw[i] >> 16, iw = (a_hw[i] << 16) >> 16;
-      const bool ok = (unsigned)(ih + dh) < (unsigned)p.IH && (unsigned)(iw + dw) < (unsigned)p.IW;
-      voff[i] = ok ? 2u * (unsigned)(a_pix[i] + a_t) : OOB;
+  for (int i = 0; i < AL; ++i) a_vb[i] = OOB;
+  auto plan = [&]() {  // offsets of the next k-step's pieces
+    if (u_ci == 0) {
+      const int pk = __builtin_amdgcn_readfirstlane(u_pk);
+      const int dh = tap_dh(pk), dw = tap_dw(pk);
+      const int a_t = (dh * p.IW + dw) * p.CA;
+#pragma unroll
+      for (int i = 0; i < AL; ++i) {
+        const int ih = a_hw[i] >> 16, iw = (a_hw[i] << 16) >> 16;
+        const bool ok = (unsigned)(ih + dh) < (unsigned)p.IH && (unsigned)(iw + dw) < (unsigned)p.IW;
+        a_vb[i] = ok ? 2u * (unsigned)(a_pix[i] + a_t) : OOB;
+      }
+      s_tb = 2 * tap_tb(pk) * p.CA;
     }
-#pragma unroll
-    for (int i = 0; i < BL; ++i) voff[AL + i] = b_row[i] + b_t;
+    s_off_a = 2 * u_ci;
+    s_off_b = s_tb + 2 * u_ci;
     u_ci += BK;
     if (u_ci >= p.CA) { u_ci -= p.CA; ++u_tap; }
     u_pk = s_tap[u_tap < p.ntaps ? u_tap : 0];
   };
   auto piece = [&](int buf, int q, bool live) {  // LDS-DMA piece q of the planned k-step into buffer buf
     char* dst = smem + buf * STAGE + (q < AL ? (wid * (TM / NW) + q * 8) * 128 : A_BYTES + (wid * (BN / NW) + (q - AL) * 8) * 128);
-    blds16(live ? (q < AL ? rsA : rsB) : rsZ, voff[q], dst);
+    blds16s(live ? (q < AL ? rsA : rsB) : rsZ, q < AL ? a_vb[q] : b_row[q - AL], q < AL ? s_off_a : s_off_b, dst);
   };
 
   f32x4 acc[RM][RN];
@@ -221,9 +248,11 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_deep_kernel(const ConvPa
 #pragma unroll
       for (int q = 0; q < NF; ++q)
         if (!D_NOFRAG && (q * MB) / NF == t - MB) frag(a0, b0, cur ^ 1, 0, q);
+      if constexpr (SPREAD && !D_NOLOAD) {
 #pragma unroll
-      for (int q = PB; q < LPS; ++q)
-        if (SPREAD && !D_NOLOAD && ((q - PB) * MB) / (LPS - PB) == t - MB) piece(cur, q, live);
+        for (int q = PB; q < LPS; ++q)
+          if (((q - PB) * MB) / (LPS - PB) == t - MB) piece(cur, q, live);
+      }
     }
     if constexpr (SETPRIO) __builtin_amdgcn_s_setprio(0);
   }
@@ -271,6 +300,8 @@ const DeepEntry g_deep[] = {
     // schedule variants of the 256 x 256 tile, and two diagnostics (variant & 6: wrong results, never tuned)
     DEEP(256, 256, 2, 2, 8), DEEP(256, 256, 2, 2, 16), DEEP(256, 256, 2, 2, 32), DEEP(256, 256, 2, 2, 2),
     DEEP(256, 256, 2, 2, 4),
+    // spread pieces + grouped tile order (4- / 8-row bands per XCD)
+    DEEP(256, 256, 2, 2, 16 | 64), DEEP(256, 256, 2, 2, 16 | 128), DEEP(256, 128, 2, 2, 16 | 64),
 };
 #undef DEEP
 

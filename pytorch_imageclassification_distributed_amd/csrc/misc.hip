@@ -2,6 +2,9 @@
 //
 //  prepare_input   fp32 NCHW (loader output) -> bf16 NHWC padded to Cp channels,
 //                  optional per-channel affine (Inception transform_input) - one pass
+//  input_u8        uint8 NHWC RGB (native / host loaders) -> the model's input in ONE pass: bf16 NHWC
+//                  padded to 8 channels, or the 16-channel space-to-depth stem layout, with the ImageNet
+//                  normalisation and any transform_input folded into one per-channel affine (K24-K26)
 //  cast_bf16       fp32 -> bf16 (weight shadow initialisation)
 //  weight_pad      [Co][T][Ci] -> [Co][T][Cp] zero-padded (stem conv, Cin 3 -> 8)
 //  weight_t        [Co][T][Ci] -> [Ci][T'][Co] with optional tap flip, for dgrad
@@ -78,6 +81,63 @@ __global__ void normalize_u8_kernel(const uint8_t* __restrict__ x, float* __rest
     o[0] = ((float)px[0] / 255.f - m0) / s0;
     o[hw] = ((float)px[1] / 255.f - m1) / s1;
     o[2 * (long)hw] = ((float)px[2] / 255.f - m2) / s2;
+  }
+}
+
+// y = u * a[c] + b[c] per channel: (u / 255 - mean) / std, then the model's own affine, folded on the host
+struct Affine3 {
+  float a0, a1, a2, b0, b1, b2;
+};
+
+// 4 pixels per lane: 12 input bytes as three dword loads (pixel 4q starts at byte 12q), 4 x 16-B stores
+__global__ void input_u8_nhwc8_kernel(const uint8_t* __restrict__ x, bf16_t* __restrict__ y, long nquad,
+                                      Affine3 f) {
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < nquad; q += (long)gridDim.x * blockDim.x) {
+    const uint32_t* src = (const uint32_t*)(x + q * 12);
+    const uint32_t w0 = src[0], w1 = src[1], w2 = src[2];
+    const uint32_t bytes[3] = {w0, w1, w2};
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      float v[8];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int b = p * 3 + c;
+        const float u = (float)((bytes[b >> 2] >> (8 * (b & 3))) & 0xffu);
+        v[c] = c == 0 ? u * f.a0 + f.b0 : c == 1 ? u * f.a1 + f.b1 : u * f.a2 + f.b2;
+      }
+#pragma unroll
+      for (int k = 3; k < 8; ++k) v[k] = 0.f;
+      *(uint4*)(y + (q * 4 + p) * 8) = pack8(v);
+    }
+  }
+}
+
+// space-to-depth stem layout (prepare_input_s2d_kernel's) straight from uint8 NHWC: one lane per output
+// pixel (a 2x2 input block = two 6-byte runs), two 16-B stores
+__global__ void input_u8_s2d_kernel(const uint8_t* __restrict__ x, bf16_t* __restrict__ y, int N, int H, int W,
+                                    Affine3 f) {
+  const int Ho = H >> 1, Wo = W >> 1;
+  const long total = (long)N * Ho * Wo;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long n = i / ((long)Ho * Wo);
+    const int r = (int)(i - n * Ho * Wo);
+    const int oh = r / Wo, ow = r - oh * Wo;
+    float v[16];
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy) {
+      const uint16_t* row = (const uint16_t*)(x + ((n * H + 2 * oh + dy) * (long)W + 2 * ow) * 3);  // 6 bytes
+      const uint32_t lo = row[0] | ((uint32_t)row[1] << 16), hi = row[2];
+#pragma unroll
+      for (int b = 0; b < 6; ++b) {  // byte b = pixel dx = b / 3, channel c = b % 3
+        const float u = (float)(((b < 4 ? lo >> (8 * b) : hi >> (8 * (b - 4)))) & 0xffu);
+        const int c = b % 3, dx = b / 3;
+        v[(dy * 2 + dx) * 3 + c] = c == 0 ? u * f.a0 + f.b0 : c == 1 ? u * f.a1 + f.b1 : u * f.a2 + f.b2;
+      }
+    }
+#pragma unroll
+    for (int k = 12; k < 16; ++k) v[k] = 0.f;
+    *(uint4*)(y + i * 16) = pack8(v);
+    *(uint4*)(y + i * 16 + 8) = pack8(v + 8);
   }
 }
 
@@ -217,6 +277,19 @@ int normalize_u8_launch(const uint8_t* x, float* y, long npix, int hw, const flo
                      mean[2], std_[0], std_[1], std_[2]);
   HIP_CHECK_LAUNCH();
   return 0;
+}
+
+// s2d: 1 = space-to-depth stem layout (H, W even), 0 = NHWC padded to 8 channels; aff = a[3], b[3]
+int input_u8_launch(const uint8_t* x, bf16_t* y, int N, int H, int W, int s2d, const float* aff, hipStream_t s) {
+  const Affine3 f{aff[0], aff[1], aff[2], aff[3], aff[4], aff[5]};
+  if (s2d) {
+    hipLaunchKernelGGL(input_u8_s2d_kernel, dim3(grid_for((long)N * (H / 2) * (W / 2))), dim3(256), 0, s, x, y, N, H,
+                       W, f);
+  } else {
+    const long nquad = (long)N * H * W / 4;  // host-checked: N * H * W % 4 == 0
+    hipLaunchKernelGGL(input_u8_nhwc8_kernel, dim3(grid_for(nquad)), dim3(256), 0, s, x, y, nquad, f);
+  }
+  return (int)hipGetLastError();
 }
 
 int prepare_input_s2d_launch(const float* x, bf16_t* y, int N, int H, int W, hipStream_t s) {

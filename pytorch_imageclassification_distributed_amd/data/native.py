@@ -59,6 +59,9 @@ class NativeFolderLoader:
         self.epoch = 0
         self.ring = max(int(ring), 2)
         self._pending: deque = deque()
+        # optional uint8 NHWC (device) -> model input conversion run on the copy stream (the trainer sets it
+        # on the HIP path: normalisation + layout + transform_input in one kernel); None = fp32 NCHW batches
+        self.input_fn = None
 
     def set_epoch(self, epoch: int) -> None:
         self.epoch = epoch
@@ -91,9 +94,12 @@ class NativeFolderLoader:
             lab = labels.to(self.device, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(self.stream)
-            n, s = img_u8.shape[0], img_u8.shape[1]
-            x = torch.empty((n, 3, s, s), dtype=torch.float32, device=self.device)
-            self.C.normalize_u8(u8, x, list(IMAGENET_MEAN), list(IMAGENET_STD))
+            if self.input_fn is not None:  # the model's first-layer input in one pass (ops/hip.py input_from_u8)
+                x = self.input_fn(u8)
+            else:
+                n, s = img_u8.shape[0], img_u8.shape[1]
+                x = torch.empty((n, 3, s, s), dtype=torch.float32, device=self.device)
+                self.C.normalize_u8(u8, x, list(IMAGENET_MEAN), list(IMAGENET_STD))
         cur.wait_stream(self.stream)
         for t in (u8, lab, x):
             t.record_stream(cur)

@@ -13,7 +13,9 @@
 * ``HostSyntheticLoader`` - the host data path of a real run (K24/K25) with the
   decode left out: a ring of *pinned* uint8 NHWC batches (what the native
   loader's C++ workers produce, data/native.py) is copied to the GPU with
-  ``hipMemcpyAsync`` on a copy stream, one batch ahead, and normalised there
+  ``hipMemcpyAsync`` on a copy stream, one batch ahead, and converted there -
+  with ``input_fn`` set (the trainer's, HIP path) straight to the model's bf16
+  input in one kernel (``input_from_u8``), else normalised to fp32 NCHW
   (``normalize_u8``); the compute stream waits on an event.  ``bench.py --data
   host`` times the training step with it, so the H2D copy and normalisation the
   on-device loader skips are inside the measurement.
@@ -79,6 +81,7 @@ class HostSyntheticLoader:
         self.device = torch.device(device)
         self.stream = torch.cuda.Stream(device=self.device)
         self.steps = steps
+        self.input_fn = None  # as NativeFolderLoader.input_fn: uint8 -> model input in one pass, on the copy stream
 
     def __len__(self):
         return self.steps
@@ -90,8 +93,11 @@ class HostSyntheticLoader:
         with torch.cuda.stream(self.stream):
             u8 = img.to(self.device, non_blocking=True)
             y = lab.to(self.device, non_blocking=True)
-            x = torch.empty((n, 3, s, s), dtype=torch.float32, device=self.device)
-            self.C.normalize_u8(u8, x, list(IMAGENET_MEAN), list(IMAGENET_STD))
+            if self.input_fn is not None:
+                x = self.input_fn(u8)
+            else:
+                x = torch.empty((n, 3, s, s), dtype=torch.float32, device=self.device)
+                self.C.normalize_u8(u8, x, list(IMAGENET_MEAN), list(IMAGENET_STD))
         return {"image": x, "label": y, "_u8": u8}
 
     def __iter__(self):

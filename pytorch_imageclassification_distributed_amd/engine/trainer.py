@@ -85,6 +85,19 @@ class Trainer:
         self.image_size = args.image_size or DEFAULT_IMAGE_SIZE.get(args.model, 224)
         self._build_data()
         self._build_model()
+        self.input_fn = None
+        spec = getattr(self.model.encoder, "input_spec", None) if hasattr(self.model, "encoder") else None
+        if self.hip and spec is not None:
+            # loaders that deliver uint8 batches convert them to the model's input in one kernel on their copy
+            # stream (normalisation, layout / space-to-depth, transform_input)
+            import functools
+            from ..data.folder import IMAGENET_MEAN, IMAGENET_STD
+            from ..ops import hip as _hipops
+            self.input_fn = functools.partial(_hipops.input_from_u8, spec=spec(), mean=IMAGENET_MEAN,
+                                              std=IMAGENET_STD)
+            for ld in (getattr(self, "train_loader", None), getattr(self, "val_loader", None)):
+                if ld is not None and hasattr(ld, "input_fn"):
+                    ld.input_fn = self.input_fn
         if ctx.world_size > 1:
             # the weights are rank 0's (broadcast at construction); from here each rank draws its own dropout /
             # drop-connect masks, as unseeded DDP ranks do (a checkpoint keeps every rank's streams: rng_ranks)
@@ -288,6 +301,9 @@ class Trainer:
         if not self.hip or self.ctx.world_size != 1:
             raise RuntimeError("capture_step: HIP path on a single process only")
         self._g_x = images.detach().clone()
+        for attr in ("_imgcls_s2d", "_imgcls_prepared"):  # loader-converted input (input_from_u8) stays marked
+            if hasattr(images, attr):
+                setattr(self._g_x, attr, getattr(images, attr))
         self._g_y = labels.detach().clone()
         self._g_lrs = tuple(g["lr"] for g in self.optimizer.param_groups)
         st = self.step_stream if self.step_stream is not None else torch.cuda.Stream(device=self.dev)
@@ -524,7 +540,7 @@ class Trainer:
             self.train_sampler.set_epoch(epoch)
             train_loss = self.train_epoch(epoch)
             self.scheduler.step()
-            if self.dev.type == "cuda":
+            if self.dev.type == "cuda" and os.environ.get("IMGCLS_DIAG_NO_EMPTY_CACHE", "0") != "1":
                 torch.cuda.empty_cache()
             val_acc = self.val_epoch(epoch)
             improved = val_acc > self.best_score

@@ -151,6 +151,10 @@ class EfficientNet(nn.Module):
             x = block(x, drop_connect_rate=dcr)
         return Fx.conv_bn_act(x, self._conv_head, self._bn1, "silu")
 
+    def input_spec(self):
+        """(space-to-depth stem input, per-channel scale, shift) (ops/hip.py input_from_u8)."""
+        return (False, None, None)
+
     def forward(self, x):
         x = Fx.prepare_input(x)
         x = Fx.global_avg_pool(self.extract_features(x))

@@ -210,6 +210,13 @@ class Inception3(nn.Module):
     TRANSFORM_SCALE = (0.229 / 0.5, 0.224 / 0.5, 0.225 / 0.5)
     TRANSFORM_SHIFT = ((0.485 - 0.5) / 0.5, (0.456 - 0.5) / 0.5, (0.406 - 0.5) / 0.5)
 
+    def input_spec(self):
+        """(space-to-depth stem input, per-channel scale, shift): transform_input folded into the loaders'
+        one-pass uint8 conversion (ops/hip.py input_from_u8)."""
+        if self.transform_input:
+            return (False, self.TRANSFORM_SCALE, self.TRANSFORM_SHIFT)
+        return (False, None, None)
+
     def _transform_input(self, x):
         if not self.transform_input:
             return Fx.prepare_input(x)

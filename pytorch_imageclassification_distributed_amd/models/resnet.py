@@ -119,6 +119,11 @@ class ResNet(nn.Module):
         x = self.layer4(x)
         return Fx.global_avg_pool(x)
 
+    def input_spec(self):
+        """(space-to-depth stem input, per-channel scale, shift) of the model's first layer (the loaders'
+        one-pass uint8 conversion, ops/hip.py input_from_u8)."""
+        return (Fx._hip().stem_s2d_conv(self.conv1), None, None)
+
     def forward(self, x):
         x = Fx.prepare_input(x, stem=self.conv1)
         x = self.forward_features(x)

@@ -1353,12 +1353,46 @@ STEM_DIRECT = os.environ.get("IMGCLS_STEM_DIRECT", "1") == "1"  # stem.hip inste
 _S2D_INDEX: dict = {}
 
 
-def stem_s2d_eligible(x, conv) -> bool:
-    return (STEM_S2D and x.dim() == 4 and x.shape[1] == 3 and x.dtype == torch.float32
-            and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0 and conv.groups == 1 and conv.bias is None
+def stem_s2d_conv(conv) -> bool:
+    """The 7x7 stride-2 3-channel stem conv the space-to-depth form serves."""
+    return (STEM_S2D and conv.groups == 1 and conv.bias is None and conv.in_channels == 3
             and tuple(conv.kernel_size) == (7, 7) and tuple(conv.stride) == (2, 2)
             and tuple(conv.padding) == (3, 3) and tuple(conv.dilation) == (1, 1)
             and not getattr(conv, "tf_same", False))
+
+
+def stem_s2d_eligible(x, conv) -> bool:
+    """fp32 NCHW images of even size (the stem converts them), or a batch the loader already converted to
+    the space-to-depth layout (``input_from_u8``)."""
+    if getattr(x, "_imgcls_s2d", None) is not None:
+        return stem_s2d_conv(conv)
+    return (x.dim() == 4 and x.shape[1] == 3 and x.dtype == torch.float32
+            and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0 and stem_s2d_conv(conv))
+
+
+def input_from_u8(u8, spec, mean, std):
+    """uint8 NHWC RGB batch on the GPU -> the model's first-layer input in ONE kernel:
+    ``(u / 255 - mean) / std`` (reference dp/loader.py:86-91) and the model's own per-channel affine
+    (Inception transform_input) folded into ``u * a + b``, written as bf16 either in the 16-channel
+    space-to-depth stem layout (``spec[0]``, ResNet) or NHWC padded to 8 channels.  Replaces
+    normalize_u8 (fp32 NCHW) + prepare_input / prepare_input_s2d (a second pass over that fp32 tensor).
+    The result carries a marker so prepare_input / the stem pass it through unchanged."""
+    s2d, sc, sh = spec
+    n, h, w, _ = u8.shape
+    a = [1.0 / (255.0 * std[c]) for c in range(3)]
+    b = [-mean[c] / std[c] for c in range(3)]
+    if sc is not None:
+        a = [a[c] * sc[c] for c in range(3)]
+        b = [b[c] * sc[c] + sh[c] for c in range(3)]
+    if s2d:
+        y = _empty_cl(n, 16, h // 2, w // 2, u8.device)
+        C.input_u8(u8, y, a, b, 1)
+        y._imgcls_s2d = (h, w)
+    else:
+        y = _empty_cl(n, 8, h, w, u8.device)
+        C.input_u8(u8, y, a, b, 0)
+        y._imgcls_prepared = True
+    return y
 
 
 def _s2d_index(dev):
@@ -1391,11 +1425,14 @@ class StemS2dFn(torch.autograd.Function):
     """The ResNet stem conv on the space-to-depth input (the image itself needs no gradient)."""
 
     @staticmethod
-    def forward(ctx, x, w, conv, want_stats, shift=None):
-        n, _, h, wd = x.shape
+    def forward(ctx, x, w, conv, want_stats, shift=None, s2d_hw=None):
         co = w.shape[0]
-        xs = _empty_cl(n, 16, h // 2, wd // 2, x.device)
-        C.prepare_input_s2d(x.contiguous(), xs, n, h, wd)
+        if s2d_hw is not None:  # the loader converted the batch already (input_from_u8)
+            n, (h, wd), xs = x.shape[0], s2d_hw, x
+        else:
+            n, _, h, wd = x.shape
+            xs = _empty_cl(n, 16, h // 2, wd // 2, x.device)
+            C.prepare_input_s2d(x.contiguous(), xs, n, h, wd)
         g = _s2d_geom(n, h, wd, co)
         idx = _s2d_index(x.device)
         wq = torch.zeros(co, 256, dtype=BF16, device=x.device)
@@ -1429,7 +1466,7 @@ class StemS2dFn(torch.autograd.Function):
             # side stream's backlog instead of behind it (conv_wgrad_raw, padded-channel path)
             _wgrad_launch(dy, xs, full, g, m, ntot, kps, splits, stages)
             dw.permute(0, 2, 3, 1).reshape(g.Co, 147).copy_(full.view(g.Co, ntot)[:, idx])
-        return None, dw, None, None, None
+        return None, dw, None, None, None, None
 
 
 # ---------------------------------------------------------------------------
@@ -1732,7 +1769,7 @@ def conv_bn_act_pool(x, conv, bn, act, pool, exclusive_input=False):
     ensure_channels_last_weight(conv)
     shift = stat_shift(bn)
     if stem_s2d_eligible(x, conv) and not x.requires_grad:
-        y = StemS2dFn.apply(x, conv.weight, conv, bn.training, shift)
+        y = StemS2dFn.apply(x, conv.weight, conv, bn.training, shift, getattr(x, "_imgcls_s2d", None))
     else:
         if conv.groups != 1 or conv.bias is not None:
             raise NotImplementedError("conv_bn_act_pool: grouped conv / conv bias")
@@ -1839,7 +1876,7 @@ def conv_bn_act(x, conv, bn, act, residual, x_slot=None, res_slot=None, exclusiv
         x, xf = XfMaterializeFn.apply(x, xf), None
     if stem_s2d_eligible(x, conv) and residual is None and not x.requires_grad:
         ensure_channels_last_weight(conv)
-        y = StemS2dFn.apply(x, conv.weight, conv, bn.training, shift)
+        y = StemS2dFn.apply(x, conv.weight, conv, bn.training, shift, getattr(x, "_imgcls_s2d", None))
         link = BwdLink() if (FUSE_BN_BWD and bn.training and torch.is_grad_enabled()) else None
         out = BNActFn.apply(y, bn.weight, bn.bias, None, bn, act, bn.training, None, link, None, None, shift)
         if link is not None:
@@ -2128,6 +2165,12 @@ def prepare_input(x, scale=None, shift=None, stem=None):
     """fp32 NCHW batch -> bf16 NHWC padded to a multiple of 8 channels (one kernel).  With ``stem``
     (the first conv) eligible for the space-to-depth form, the fp32 batch is returned unchanged: the
     stem converts it itself (``StemS2dFn``)."""
+    if getattr(x, "_imgcls_s2d", None) is not None:
+        if stem is None or scale is not None or not stem_s2d_eligible(x, stem):
+            raise ValueError("a space-to-depth input batch (input_from_u8) reached a model without the s2d stem")
+        return x
+    if getattr(x, "_imgcls_prepared", False):
+        return x  # converted by the loader, the model's affine included (input_from_u8)
     if stem is not None and scale is None and stem_s2d_eligible(x, stem):
         return x
     if x.dtype == BF16 and x.is_contiguous(memory_format=CL) and x.shape[1] % 8 == 0:

@@ -1412,3 +1412,55 @@ def test_bn_statistics_large_mean(path):
         assert v1 <= v0 * 1.5 + 1e-6
     # (the conv epilogue sums the fp32 accumulators before their bf16 rounding, the reference the rounded
     # output: ~1e-5 either way, which is that rounding, not the summation)
+
+
+@pytest.mark.parametrize("s2d,affine", [(False, None), (False, "inception"), (True, None)])
+def test_input_u8_one_pass(s2d, affine):
+    """input_from_u8 (one kernel: uint8 NHWC -> bf16 model input) against the reference normalisation
+    (data/folder.py normalize = reference dp/loader.py:86-91) in fp32, then the model's affine (Inception
+    transform_input) and the layout the old two-pass path produced (prepare_input / prepare_input_s2d)."""
+    import numpy as np
+
+    from pytorch_imageclassification_distributed_amd.data.folder import IMAGENET_MEAN, IMAGENET_STD, normalize
+    from pytorch_imageclassification_distributed_amd.models.inception import Inception3
+    hip = _hip()
+    torch.manual_seed(0)
+    n, h, w = 3, 38, 22
+    u8 = torch.randint(0, 256, (n, h, w, 3), dtype=torch.uint8)
+    ref = torch.from_numpy(np.stack([normalize(u8[i].numpy().astype(np.float32)) for i in range(n)]))  # NHWC fp32
+    ref = ref.permute(0, 3, 1, 2).contiguous()  # NCHW
+    sc = sh = None
+    if affine == "inception":
+        sc, sh = Inception3.TRANSFORM_SCALE, Inception3.TRANSFORM_SHIFT
+        ref = ref * torch.tensor(sc).view(1, 3, 1, 1) + torch.tensor(sh).view(1, 3, 1, 1)
+    y = hip.input_from_u8(u8.to(DEV), (s2d, sc, sh), IMAGENET_MEAN, IMAGENET_STD)
+    if s2d:
+        assert y._imgcls_s2d == (h, w) and tuple(y.shape) == (n, 16, h // 2, w // 2)
+        want = torch.empty_like(y)
+        hip.C.prepare_input_s2d(ref.to(DEV), want, n, h, w)
+    else:
+        assert y._imgcls_prepared and tuple(y.shape) == (n, 8, h, w) and y.is_contiguous(memory_format=CL)
+        want = torch.zeros(n, 8, h, w, device=DEV)
+        want[:, :3] = ref.to(DEV)
+    # one bf16 rounding of the same fp32 value (the affine's operation order differs): <= 1 ulp apart
+    d = (y.float() - want.float()).abs()
+    assert (d <= want.float().abs() * 2 ** -7 + 1e-6).all(), d.max()
+
+
+def test_input_u8_resnet_forward_matches_fp32_input():
+    """A ResNet fed the loader-converted (space-to-depth) batch computes what it computes from the fp32 NCHW
+    batch of the same images (eval mode, same weights): the s2d marker routes around prepare_input_s2d."""
+    from pytorch_imageclassification_distributed_amd.data.folder import IMAGENET_MEAN, IMAGENET_STD
+    from pytorch_imageclassification_distributed_amd.models import Classifier
+    hip = _hip()
+    torch.manual_seed(0)
+    m = Classifier("resnet18", 7).to(DEV).eval()
+    u8 = torch.randint(0, 256, (4, 64, 64, 3), dtype=torch.uint8, device=DEV)
+    x32 = torch.empty(4, 3, 64, 64, device=DEV)
+    hip.C.normalize_u8(u8, x32, list(IMAGENET_MEAN), list(IMAGENET_STD))
+    spec = m.encoder.input_spec()
+    assert spec[0] is True
+    with torch.no_grad():
+        a = m(hip.input_from_u8(u8, spec, IMAGENET_MEAN, IMAGENET_STD)).float()
+        b = m(x32).float()
+    assert rel_err(a, b) < 2e-2
