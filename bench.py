@@ -68,9 +68,9 @@ def parse():
     p.add_argument("--graph", default="auto", choices=["on", "off", "auto"],
                    help="replay the whole training step as one captured HIP graph (single process); auto = on "
                         "at per-GPU batch <= 64 (host-bound steps, train.py --hip-graph auto)")
-    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
-                   help="fp8 (experimental): MX-FP8 forward convolutions only, bf16 backward - measured "
-                        "+0.3 %% over bf16 at b1024, not a speed-up (README)")
+    p.add_argument("--dtype", default="bf16", choices=["bf16"],
+                   help="compute dtype (bf16).  MX-FP8 is not a benchmark configuration: forward-only fp8 "
+                        "measured no speed-up over bf16 (README, BASELINE.md config 5)")
     p.add_argument("--data", default="device", choices=["device", "host"],
                    help="device: batches generated once in HBM (the step alone); host: pinned uint8 host batches "
                         "copied by hipMemcpyAsync on a copy stream and normalised on the GPU inside the timed loop "

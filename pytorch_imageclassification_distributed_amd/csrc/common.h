@@ -95,6 +95,12 @@ DEVI float act_grad(float z, float g, int act) {
 
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
+// Zero n floats with a kernel (csrc/head.hip).  Launchers that must start from a zeroed output use this, not
+// hipMemsetAsync: on ROCm 7 a memset node of a captured HIP graph is clobbered by later eager hipMemsetAsync
+// calls, so the first replay after an eager pass (Trainer.fit's validation) accumulated into garbage
+// (tests/test_gpu_graph_zeroing.py).  Kernel nodes replay faithfully.
+int zero_f32_launch(float* p, long n, hipStream_t s);
+
 // x / d for 32-bit x by a runtime divisor: one mul_hi + add + shift (Granlund-Montgomery round-up
 // method with a 33-bit sum; exact for every 32-bit x - tests/test_native_math.py checks the formula)
 struct FastDiv {
@@ -204,7 +210,7 @@ inline int spatial_reduce_launch(const bf16_t* a, const bf16_t* b, float* out, i
     while ((long)N * slices * splits < 1024 && HW / (splits * 2) >= 8 * RP) splits *= 2;
   const int rps = (HW + splits - 1) / splits;
   splits = (HW + rps - 1) / rps;
-  if (splits > 1 && hipMemsetAsync(out, 0, sizeof(float) * (size_t)N * C, s) != hipSuccess) return 1;
+  if (splits > 1 && zero_f32_launch(out, (long)N * C, s) != 0) return 1;
   hipLaunchKernelGGL(spatial_reduce_kernel<PROD>, dim3(N, slices, splits), dim3(256), 0, s, a, b, out, HW, C, rps,
                      scale, splits > 1 ? 1 : 0);
   return hipGetLastError() == hipSuccess ? 0 : 2;

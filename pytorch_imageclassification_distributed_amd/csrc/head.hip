@@ -158,7 +158,19 @@ __global__ void ce_bwd_kernel(const float* __restrict__ prob, const long long* _
   dx[i] = gout[0] * wi * (prob[i] - (c == t ? 1.f : 0.f)) / stats[1];
 }
 
+__global__ __launch_bounds__(256) void zero_f32_kernel(float* __restrict__ p, long n) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) p[i] = 0.f;
+}
+
 }  // namespace
+
+int zero_f32_launch(float* p, long n, hipStream_t s) {
+  if (n <= 0) return 0;
+  const long blocks = (n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048;
+  hipLaunchKernelGGL(zero_f32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, n);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
 
 int sgemm_launch(const float* A, const float* B, float* C, const float* bias, const float* mask, int M, int N,
                  int K, long sam, long sak, long sbk, long sbn, long ldc, long smm, long smk, int relu,
@@ -172,7 +184,7 @@ int sgemm_launch(const float* A, const float* B, float* C, const float* bias, co
   SgemmArgs a{A, B, C, bias, mask, M, N, K, sam, sak, sbk, sbn, ldc, smm, smk, relu, accumulate, kchunk, splits > 1};
   if (splits > 1 && !accumulate) {
     if (ldc == N) {
-      if (hipMemsetAsync(C, 0, sizeof(float) * (size_t)M * N, s) != hipSuccess) return 1;
+      if (zero_f32_launch(C, (long)M * N, s) != 0) return 1;
     } else {
       return 2;  // strided split-K output without accumulate: not needed by the callers
     }
@@ -188,7 +200,7 @@ int sgemm_launch(const float* A, const float* B, float* C, const float* bias, co
 
 int colsum_launch(const float* X, const float* mask, float* out, int M, int N, long ld, int accumulate,
                   hipStream_t s) {
-  if (!accumulate && hipMemsetAsync(out, 0, sizeof(float) * (size_t)N, s) != hipSuccess) return 1;
+  if (!accumulate && zero_f32_launch(out, N, s) != 0) return 1;
   const int rpb = g_imgcls_det ? (M > 0 ? M : 1) : CS_ROWS;  // deterministic: one ordered pass per column
   hipLaunchKernelGGL(colsum_kernel, dim3(cdiv(N, 64), cdiv(M, rpb)), dim3(256), 0, s, X, mask, out, M, N, ld, rpb);
   HIP_CHECK_LAUNCH();

@@ -540,7 +540,7 @@ class Trainer:
             self.train_sampler.set_epoch(epoch)
             train_loss = self.train_epoch(epoch)
             self.scheduler.step()
-            if self.dev.type == "cuda" and os.environ.get("IMGCLS_DIAG_NO_EMPTY_CACHE", "0") != "1":
+            if self.dev.type == "cuda":
                 torch.cuda.empty_cache()
             val_acc = self.val_epoch(epoch)
             improved = val_acc > self.best_score

@@ -94,6 +94,21 @@ def main():
         out["n_wgrad_ws"] = len(hip._WGRAD_WS)
         return out
 
+    def bad_grads(tag):
+        torch.cuda.synchronize()
+        rows = []
+        for n, p in tr.model.named_parameters():
+            g = p.grad
+            if g is None:
+                continue
+            mx = float(g.detach().float().abs().max())
+            rows.append((n, mx, tuple(p.shape)))
+        bad = [r for r in rows if not (r[1] < 1e3)]
+        print(f"  {tag}: {len(bad)}/{len(rows)} grads with |g|max >= 1e3 or non-finite; "
+              f"max finite {max((r[1] for r in rows if r[1] < 1e3), default=0):.3g}", flush=True)
+        for n, mx, shp in bad[:12]:
+            print(f"    {n} {shp} {mx:.3g}", flush=True)
+
     def diff(tag, a_, b_):
         ch = [k for k in a_ if a_[k] != b_[k]]
         print(f"  {tag}: changed {ch}" + "".join(f" {k} {a_[k]:.6g}->{b_[k]:.6g}" for k in ch), flush=True)
@@ -111,6 +126,9 @@ def main():
             losses.append(float(loss.item()))
             if i == 0 and epoch > 0:
                 diff("first step", sa, sums())
+                bad_grads("first step grads")
+            if i == 15 and epoch == 0:
+                bad_grads("last step grads (epoch 0)")
         print(f"epoch {epoch} graph={tr._graph is not None}: " + " ".join(f"{v:.3g}" for v in losses), flush=True)
         s0 = sums()
         tr.scheduler.step()
