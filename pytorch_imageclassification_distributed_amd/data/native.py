@@ -25,6 +25,7 @@ from collections import deque
 import torch
 
 from .folder import IMAGENET_MEAN, IMAGENET_STD, ImageDataset
+from .prefetch import copy_stream
 
 
 def available() -> bool:
@@ -55,7 +56,7 @@ class NativeFolderLoader:
                                    max(int(workers), 1), bool(aug), int(seed), int(ring), cuda, not cuda,
                                    list(IMAGENET_MEAN), list(IMAGENET_STD))
         self.C = C
-        self.stream = torch.cuda.Stream(device=self.device) if cuda else None
+        self.stream = copy_stream(self.device) if cuda else None
         self.epoch = 0
         self.ring = max(int(ring), 2)
         self._pending: deque = deque()

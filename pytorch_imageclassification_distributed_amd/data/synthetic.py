@@ -25,6 +25,8 @@ from __future__ import annotations
 import torch
 from torch.utils.data import Dataset
 
+from .prefetch import copy_stream
+
 
 class SyntheticImageDataset(Dataset):
     def __init__(self, length: int, num_classes: int, image_size: int, seed: int = 0):
@@ -79,7 +81,7 @@ class HostSyntheticLoader:
             lab = torch.randint(0, num_classes, (batch_size,), generator=g).pin_memory()
             self.host.append((img, lab))
         self.device = torch.device(device)
-        self.stream = torch.cuda.Stream(device=self.device)
+        self.stream = copy_stream(self.device)
         self.steps = steps
         self.input_fn = None  # as NativeFolderLoader.input_fn: uint8 -> model input in one pass, on the copy stream
 
