@@ -109,7 +109,8 @@ int bn_stats_launch(const bf16_t*, long, int, float*, int, const float*, hipStre
 int se_mlp_fwd_launch(const float*, const float*, const float*, const float*, const float*, float*, float*, int, int,
                       int, hipStream_t);
 int se_mlp_bwd_launch(const float*, const float*, const float*, const float*, const float*, const float*, float*,
-                      float*, float*, float*, float*, float*, float*, int, int, int, hipStream_t);
+                      float*, float*, float*, float*, float*, float*, float*, int, int, int, hipStream_t);
+long se_bwd_w_slices(int, int, int);
 size_t peer_buffer_bytes();
 int peer_max_world();
 int peer_max_elems();
@@ -778,9 +779,11 @@ void se_mlp_bwd(Tensor ds, Tensor s, Tensor h, Tensor p, Tensor wr, Tensor we, T
   f32(ds, nc, "ds"); f32(s, nc, "s"); f32(h, nh, "h"); f32(p, nc, "p"); f32(wr, w, "wr"); f32(we, w, "we");
   f32(de, nc, "de"); f32(dh, nh, "dh"); f32(dp, nc, "dp"); f32(dwr, w, "dwr"); f32(dbr, nsq, "dbr");
   f32(dwe, w, "dwe"); f32(dbe, C, "dbe");
+  // per-slice partial weight / bias gradients (se.hip se_bwd_w), summed in order by the reduce launch
+  Tensor part = at::empty({se_bwd_w_slices(N, C, nsq) * (2 * w + C + nsq)}, ds.options());
   check(se_mlp_bwd_launch(ptr<float>(ds), ptr<float>(s), ptr<float>(h), ptr<float>(p), ptr<float>(wr), ptr<float>(we),
                           ptr<float>(de), ptr<float>(dh), ptr<float>(dp), ptr<float>(dwr), ptr<float>(dbr),
-                          ptr<float>(dwe), ptr<float>(dbe), N, C, nsq, cur()), "se_mlp_bwd");
+                          ptr<float>(dwe), ptr<float>(dbe), ptr<float>(part), N, C, nsq, cur()), "se_mlp_bwd");
 }
 
 // One rank's end of the one-shot peer all-reduce (peer.hip): its IPC-exported buffer, the peers'

@@ -69,6 +69,10 @@ targs = build_parser().parse_args(["--synthetic", "--model", "resnet50", "--batc
                                    "--num-workers", "0", "--synthetic-train-size", "8", "--synthetic-val-size", "8",
                                    "--no-sync-bn", "--lr", "1e-4"])
 tr = Trainer(targs, ctx)
+_db = os.environ.get("IMGCLS_TUNE_DB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                   "tuning", "mi355x_find_db.json"))
+if _db != "none" and os.path.exists(_db):
+    print(f"{hip.load_tuning(_db)} kernel choices from {_db}")
 tr.net.train()
 batches = list(iter(DeviceSyntheticLoader(B, 7, 224, ctx.device, steps=2, ring=2, seed=1)))
 for i in range(4):

@@ -1,6 +1,6 @@
 """Per-kernel breakdown of ONE steady-state training step from a rocprofv3 kernel trace.
 
-usage: python scripts/step_breakdown.py gpurun_out/prof_q/hip_kernel_trace.csv [marker=adam_kernel]
+usage: python scripts/step_breakdown.py gpurun_out/prof_q/hip_kernel_trace.csv|run_results.db [marker=adam_kernel]
 The step is the span between the last two launches of the marker kernel (one per optimizer step)."""
 import collections
 import csv
@@ -9,7 +9,13 @@ import sys
 
 path = sys.argv[1]
 marker = sys.argv[2] if len(sys.argv) > 2 else "adam_kernel"
-rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+if path.endswith(".db"):  # the rocpd SQLite database (rocprofv3's default output)
+    import sqlite3
+    keys = ("Kernel_Name", "Start_Timestamp", "End_Timestamp")
+    rows = [dict(zip(keys, map(str, r))) for r in sqlite3.connect(path).execute("select name, start, end from kernels")]
+else:
+    rows = list(csv.DictReader(open(path)))
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 idx = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
 a, b = idx[-2], idx[-1]
 step = rows[a + 1:b + 1]

@@ -1059,11 +1059,11 @@ def test_bn_apply_emits_mx_copy():
 
 @pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("n,c,nsq,hw", [(2, 96, 4, 9), (40, 144, 6, 7), (3, 1152, 48, 5), (33, 240, 10, 4),
-                                        (5, 2560, 160, 2)])
+                                        (5, 2560, 160, 2), (300, 96, 4, 3), (1024, 240, 10, 2)])
 def test_se_gate_fused_grads(n, c, nsq, hw, fused):
     """SE MLP (csrc/se.hip fused kernels and the GEMM/activation fallback) against fp32 autograd: output,
     input gradient and all four weight / bias gradients; batches above the 32-image LDS chunk and hidden
-    sizes that are not multiples of 4."""
+    sizes that are not multiples of 4; batches of 300 / 1024 split the weight gradients into 3 / 8 slices."""
     hip = _hip()
     torch.manual_seed(n * 7 + c)
     red = nn.Conv2d(c, nsq, 1).to(DEV)
