@@ -326,6 +326,10 @@ int launch_direct(DirectArgs a, bool bwd, hipStream_t s) {
 // 4 = CIP 96 / COT 32 (Inception Conv2d_4a: 80 channels) - 3x3 only
 int direct_conv_num_cfgs() { return 5; }
 
+int direct64_launch(const bf16_t* x, const bf16_t* w, bf16_t* y, float* part, int G, int N, int H, int W, int Cin,
+                    int OH, int OW, int Cout, int pt, int pl, const bf16_t* y_bn, const float* coef, int act,
+                    const float* shift, hipStream_t s);
+
 int direct_conv_launch(const bf16_t* x, const bf16_t* w, bf16_t* y, float* part, int G, int N, int H, int W,
                        int Cin, int OH, int OW, int Cout, int pt, int pl, int cfg, const bf16_t* y_bn,
                        const float* coef, int act, const float* shift, hipStream_t s) {
@@ -341,6 +345,7 @@ int direct_conv_launch(const bf16_t* x, const bf16_t* w, bf16_t* y, float* part,
     case 2: return Cin <= 64 ? launch_direct<64, 3, 3, 32>(a, bwd, s) : 3;
     case 3: return Cin <= 64 ? launch_direct<64, 3, 3, 64>(a, bwd, s) : 3;
     case 4: return Cin <= 96 ? launch_direct<96, 3, 3, 32>(a, bwd, s) : 3;
+    case 5: return direct64_launch(x, w, y, part, G, N, H, W, Cin, OH, OW, Cout, pt, pl, y_bn, coef, act, shift, s);
     default: return 3;
   }
 }

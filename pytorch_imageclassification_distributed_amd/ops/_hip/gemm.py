@@ -189,7 +189,8 @@ def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(
     xf2 = (xf[0], xf[1]) if xf is not None else (None, 0)
     fused = xa is not None or xf is not None
     if DIRECT_FORCE is not None and not fused and \
-            _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales) is not None:
+            _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales) is not None and \
+            _direct_variant_ok(DIRECT_FORCE, _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales)):
         cfg = (0, 0, DIRECT_BASE + DIRECT_FORCE)  # (tests) every eligible launch on this direct variant
     elif DEEP_FORCE is not None and not fused and scales[0] is None and _deep_ok(geo, dh, dw):
         cfg = (0, 0, DEEP_BASE + DEEP_FORCE)  # (tests) every eligible launch on this prefetch-depth-2 variant
@@ -323,7 +324,16 @@ DIRECT_FORCE = None  # tests: force a direct-kernel variant on every eligible la
 DIRECT_DGRAD = os.environ.get("IMGCLS_DIRECT_DGRAD", "1") == "1"  # data gradients (+ BN-backward epilogue)
 DIRECT_BASE = 100  # cfg[2] >= DIRECT_BASE: the halo-tile direct kernel (csrc/direct_conv.hip), variant cfg - base
 # variant -> (padded input channels, output-channel tile)
-DIRECT_CFGS = {0: (32, 32), 1: (32, 64), 2: (64, 32), 3: (64, 64), 4: (96, 32)}
+DIRECT_CFGS = {0: (32, 32), 1: (32, 64), 2: (64, 32), 3: (64, 64), 4: (96, 32), 5: (64, 64)}
+# variant 5: csrc/direct64.hip (weights resident in LDS, LDS-DMA double-buffered 8 x 32 patches) - exactly 64
+# input channels and a 'same' 3x3 window (OH == H, OW == W): ResNet layer1 conv2 forward and data gradient
+
+
+def _direct_variant_ok(v, dg) -> bool:
+    cip, cot = DIRECT_CFGS[v]
+    if dg[3] > cip or not (cot == 32 or dg[6] > 32):
+        return False
+    return v != 5 or (dg[3] == 64 and dg[4] == dg[1] and dg[5] == dg[2] and dg[6] % 8 == 0)
 
 
 def _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales):
@@ -405,8 +415,8 @@ def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, group
                                                       addend, *bwd, *cfg, *scales, *xa3, None, *xf2, mask, None, None, None, 0))
     dg = _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales) if not fused else None
     if dg is not None:
-        for v, (cip, cot) in DIRECT_CFGS.items():
-            if dg[3] <= cip and (cot == 32 or dg[6] > 32):
+        for v in DIRECT_CFGS:
+            if _direct_variant_ok(v, dg):
                 times[(0, 0, DIRECT_BASE + v)] = _time_ms(
                     lambda: _direct_launch(A, B, scratch, sst, groups, dg, v, bwd))
     TUNE_LOG.append((geo[0], geo[1], geo[2], times))
@@ -664,7 +674,7 @@ _OWNED = (
     'SKIP_WGRAD', 'TUNE_LOG', 'WGRAD_CANDIDATES', 'WGRAD_MIN_K', 'WGRAD_NARROW_TILES', 'WGRAD_STAGES',
     'WGRAD_TARGET_BLOCKS', 'WGRAD_TUNE_LOG', 'WGRAD_WS', '_CFGS', '_CU_COUNT', '_DEEP_CFGS', '_FP8_CFGS',
     '_HALO_CFGS', '_ORDER_IDX', '_STAGES_TUNED', '_WGRAD_TUNED', '_WGRAD_WS', '_conv_candidates',
-    '_conv_forward_fp8', '_conv_gemm', '_deep_ok', '_dgrad_phases', '_direct_geom', '_direct_launch',
+    '_conv_forward_fp8', '_conv_gemm', '_deep_ok', '_dgrad_phases', '_direct_geom', '_direct_launch', '_direct_variant_ok',
     '_fwd_taps', '_halo_ok', '_time_ms', '_tune_conv', '_weight_for_input', '_wgrad_config', '_wgrad_has',
     '_wgrad_launch', '_wgrad_plan', '_wgrad_split', '_wgrad_tiles', '_wgrad_ws', 'conv_cfgs', 'conv_deep_cfgs',
     'conv_dgrad_raw', 'conv_forward_raw', 'conv_fp8_cfgs', 'conv_fused_bwd_raw', 'conv_geom', 'conv_halo_cfgs',
