@@ -1301,7 +1301,17 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const f32x4* __restri
     }
     for (; s < splits; s += G) a += ws[(long)s * n4 + i];
   }
-  if constexpr (G > 1) {
+  if constexpr (G > 16) {
+    // many split groups per element (a small dW with hundreds of splits: the stem, layer1 3x3): tree-fold
+    part[grp][e] = a;
+    __syncthreads();
+#pragma unroll
+    for (int off = G / 2; off >= 1; off >>= 1) {
+      if (grp < off) part[grp][e] += part[grp + off][e];
+      __syncthreads();
+    }
+    if (grp == 0 && i < n4) dW[i] = dW[i] + part[0][e];
+  } else if constexpr (G > 1) {
     part[grp][e] = a;
     __syncthreads();
     if (grp == 0 && i < n4) {
@@ -1320,6 +1330,26 @@ static void launch_wgrad_reduce(const float* ws, float* dW, long n4, int splits,
   constexpr int EL = 256 / G;
   hipLaunchKernelGGL(wgrad_reduce_kernel<G>, dim3((unsigned)((n4 + EL - 1) / EL)), dim3(256), 0, stream,
                      (const f32x4*)ws, (f32x4*)dW, n4, splits);
+}
+
+// Split groups per element G = the power of two that leaves <= 8 slab loads per lane (one batch in flight).
+// Capping G at 16 made the small-dW / many-split reduces (layer1 3x3: 9216 float4 x 408 splits; the stem:
+// 4096 x 512) a few hundred blocks each walking 25-32 slabs serially: 1.08 ms and 0.39 ms at the end of
+// backward (profiles/r9w_wgrad_reduce.txt); with G up to 256 they spread over >= 1000 blocks.
+static void wgrad_reduce_auto(const float* ws, float* dW, long n4, int splits, hipStream_t stream) {
+  int g = 1;
+  while (g < 256 && g * 8 < splits) g *= 2;
+  switch (g) {
+    case 1: launch_wgrad_reduce<1>(ws, dW, n4, splits, stream); break;
+    case 2: launch_wgrad_reduce<2>(ws, dW, n4, splits, stream); break;
+    case 4: launch_wgrad_reduce<4>(ws, dW, n4, splits, stream); break;
+    case 8: launch_wgrad_reduce<8>(ws, dW, n4, splits, stream); break;
+    case 16: launch_wgrad_reduce<16>(ws, dW, n4, splits, stream); break;
+    case 32: launch_wgrad_reduce<32>(ws, dW, n4, splits, stream); break;
+    case 64: launch_wgrad_reduce<64>(ws, dW, n4, splits, stream); break;
+    case 128: launch_wgrad_reduce<128>(ws, dW, n4, splits, stream); break;
+    default: launch_wgrad_reduce<256>(ws, dW, n4, splits, stream); break;
+  }
 }
 
 
@@ -1725,11 +1755,7 @@ static int launch_fused_bwd_n(const ConvParams& p, const FusedW& f, float* dW, i
   hipLaunchKernelGGL((conv_fused_bwd_n_kernel<CI, 4, 2>), dim3(blocks), dim3(512), 0, stream, p, f);
   HIP_CHECK_LAUNCH();
   const long n4 = 64L * CI / 4;
-  if (blocks >= 128) launch_wgrad_reduce<16>(f.ws, dW, n4, blocks, stream);
-  else if (blocks >= 64) launch_wgrad_reduce<8>(f.ws, dW, n4, blocks, stream);
-  else if (blocks >= 32) launch_wgrad_reduce<4>(f.ws, dW, n4, blocks, stream);
-  else if (blocks >= 16) launch_wgrad_reduce<2>(f.ws, dW, n4, blocks, stream);
-  else launch_wgrad_reduce<1>(f.ws, dW, n4, blocks, stream);
+  wgrad_reduce_auto(f.ws, dW, n4, blocks, stream);
   HIP_CHECK_LAUNCH();
   return 0;
 }
@@ -1739,11 +1765,7 @@ static int launch_fused_bwd(const ConvParams& p, const FusedW& f, float* dW, int
   hipLaunchKernelGGL((conv_fused_bwd_kernel<CO, 4, 2>), dim3(blocks), dim3(512), 0, stream, p, f);
   HIP_CHECK_LAUNCH();
   const long n4 = (long)CO * 64 / 4;
-  if (blocks >= 128) launch_wgrad_reduce<16>(f.ws, dW, n4, blocks, stream);
-  else if (blocks >= 64) launch_wgrad_reduce<8>(f.ws, dW, n4, blocks, stream);
-  else if (blocks >= 32) launch_wgrad_reduce<4>(f.ws, dW, n4, blocks, stream);
-  else if (blocks >= 16) launch_wgrad_reduce<2>(f.ws, dW, n4, blocks, stream);
-  else launch_wgrad_reduce<1>(f.ws, dW, n4, blocks, stream);
+  wgrad_reduce_auto(f.ws, dW, n4, blocks, stream);
   HIP_CHECK_LAUNCH();
   return 0;
 }
@@ -2012,11 +2034,7 @@ int conv_wgrad_launch(const WgradParams& p_in, int splits, hipStream_t stream) {
   if (p.ws != nullptr) {
     const long n4 = (long)p.Cout * p.Ntot / 4;
     // split groups ~ splits / 8: one batch of 8 slab loads in flight per lane covers a group
-    if (splits >= 128) launch_wgrad_reduce<16>(p.ws, p.dW, n4, splits, stream);
-    else if (splits >= 64) launch_wgrad_reduce<8>(p.ws, p.dW, n4, splits, stream);
-    else if (splits >= 32) launch_wgrad_reduce<4>(p.ws, p.dW, n4, splits, stream);
-    else if (splits >= 16) launch_wgrad_reduce<2>(p.ws, p.dW, n4, splits, stream);
-    else launch_wgrad_reduce<1>(p.ws, p.dW, n4, splits, stream);
+    wgrad_reduce_auto(p.ws, p.dW, n4, splits, stream);
     HIP_CHECK_LAUNCH();
   }
   return 0;

@@ -35,6 +35,12 @@ struct HaloCfg {
   static constexpr int OCC = OCC_LDS < OCC_REG ? OCC_LDS : OCC_REG;
 };
 
+// Patch rows are read at every tap offset (dh * W + dw), i.e. 16-row fragments starting at arbitrary rows; the
+// GEMM swizzle's (row >> 1) & 7 key is conflict-free only for starts that are multiples of 4 (2-way conflicts
+// otherwise, tests/test_lds_swizzle.py).  The patch uses the shift-invariant table of csrc/direct64.hip.
+DEVI int pswz(int row, int chunk) { return row * 128 + ((chunk ^ ((0x05775220 >> ((row & 7) * 4)) & 7)) << 4); }
+DEVI int pkey(int row) { return (0x05775220 >> ((row & 7) * 4)) & 7; }
+
 DEVI bf16x8 mask8(const bf16x8& v, bool ok) {
   return __builtin_bit_cast(bf16x8, sel4(ok, __builtin_bit_cast(uint4, v)));
 }
@@ -80,7 +86,7 @@ void conv_halo_kernel(const ConvParams p) {
 #pragma unroll
   for (int i = 0; i < PL; ++i) {
     const int row = wid * (PMAX / NW) + i * 8 + lrow;
-    const int ch = pch ^ ((row >> 1) & 7);
+    const int ch = pch ^ pkey(row);
     const long g = (long)pstart + row;
     p_off[i] = (row < P && g >= 0 && g < tot_pix) ? 2u * ((unsigned)(g - pbase) * (unsigned)CA + ch * 8) : OOB;
   }
@@ -155,7 +161,7 @@ void conv_halo_kernel(const ConvParams p) {
     for (int i = 0; i < RM; ++i) ok[i] = (vmask[i] >> ct) & 1u;
     bf16x8 af[RM], bfg[RN];
 #pragma unroll
-    for (int i = 0; i < RM; ++i) af[i] = mask8(*(const bf16x8*)(sp + swz(wm * WTM + i * 16 + fr + off, fq)), ok[i]);
+    for (int i = 0; i < RM; ++i) af[i] = mask8(*(const bf16x8*)(sp + pswz(wm * WTM + i * 16 + fr + off, fq)), ok[i]);
 #pragma unroll
     for (int j = 0; j < RN; ++j) bfg[j] = *(const bf16x8*)(sb + swz(wn * WTN + j * 16 + fr, fq));
     if (g + BST - 1 < nk) issue(g + BST - 1);
@@ -165,7 +171,7 @@ void conv_halo_kernel(const ConvParams p) {
       if (kk == 0) {
 #pragma unroll
         for (int i = 0; i < RM; ++i)
-          af2[i] = mask8(*(const bf16x8*)(sp + swz(wm * WTM + i * 16 + fr + off, 4 + fq)), ok[i]);
+          af2[i] = mask8(*(const bf16x8*)(sp + pswz(wm * WTM + i * 16 + fr + off, 4 + fq)), ok[i]);
       }
       if constexpr (JOUT) {
 #pragma unroll
