@@ -209,7 +209,8 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
   TORCH_CHECK(tile_n == 0 || tile_n == 64 || tile_n == 128, "conv_gemm: tile_n must be 0, 64 or 128");
   TORCH_CHECK((cfg >= -1 && cfg < (fp8 ? conv_num_fp8_cfgs() : conv_num_cfgs())) ||
                   (!fp8 && cfg >= CONV_HALO_BASE && cfg < CONV_HALO_BASE + conv_halo_num()) ||
-                  (!fp8 && cfg >= CONV_DEEP_BASE && cfg < CONV_DEEP_BASE + conv_deep_num()),
+                  (!fp8 && cfg >= CONV_DEEP_BASE && cfg < CONV_DEEP_BASE + conv_deep_num()) ||
+                  (!fp8 && cfg >= CONV_PW_BASE && cfg < CONV_PW_BASE + conv_pw_num()),
               "conv_gemm: cfg out of range");
   p.tile_n = tile_n;
   p.cfg = cfg;
@@ -1049,6 +1050,15 @@ PYBIND11_MODULE(_C, m) {
     for (int i = 0; i < conv_halo_num(); ++i) {
       std::vector<int> c(6);
       conv_halo_info(i, c.data());
+      out.push_back(c);
+    }
+    return out;
+  });
+  m.def("conv_pw_cfgs", []() {
+    std::vector<std::vector<int>> out;
+    for (int i = 0; i < conv_pw_num(); ++i) {
+      std::vector<int> c(2);
+      conv_pw_info(i, c.data());
       out.push_back(c);
     }
     return out;

@@ -112,6 +112,11 @@ int conv_halo_launch(int i, const ConvParams& p, hipStream_t stream);  // 3: geo
 int conv_deep_num();
 void conv_deep_info(int i, int* out5);  // {tile rows, tile channels, waves M, waves N, schedule variant}
 int conv_deep_launch(int i, const ConvParams& p, hipStream_t stream);  // 3: geometry not handled
+// pointwise kernel with register-resident weights (conv_pw.hip): cfg >= CONV_PW_BASE selects entry cfg - base
+#define CONV_PW_BASE 3000
+int conv_pw_num();
+void conv_pw_info(int i, int* out2);  // {output channels per block, k capacity}
+int conv_pw_launch(int i, const ConvParams& p, hipStream_t stream);  // 3: not a plain 1x1 stride-1 forward
 int conv_wgrad_launch(const WgradParams& p, int splits, hipStream_t stream);
 int conv_fused_bwd_launch(const ConvParams& p, const bf16_t* X, float* ws, float* dW, int blocks, hipStream_t stream);
 bool conv_wgrad_has_xa(int stages);  // the wgrad variant selected by ``stages`` has a fused BN-backward dY form

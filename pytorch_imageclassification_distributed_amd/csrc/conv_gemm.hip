@@ -1898,6 +1898,11 @@ static void launch_fp8(const ConvParams& p, int gm, hipStream_t stream) {
 
 int conv_gemm_launch(const ConvParams& p, hipStream_t stream) {
   if (p.M <= 0 || p.Ncols <= 0) return 0;
+  if (p.cfg >= CONV_PW_BASE) {
+    const int r = conv_pw_launch(p.cfg - CONV_PW_BASE, p, stream);
+    if (r == 0) HIP_CHECK_LAUNCH();
+    return r;
+  }
   if (p.cfg >= CONV_DEEP_BASE) {
     const int r = conv_deep_launch(p.cfg - CONV_DEEP_BASE, p, stream);
     if (r == 0) HIP_CHECK_LAUNCH();

@@ -192,6 +192,10 @@ def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(
             _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales) is not None and \
             _direct_variant_ok(DIRECT_FORCE, _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales)):
         cfg = (0, 0, DIRECT_BASE + DIRECT_FORCE)  # (tests) every eligible launch on this direct variant
+    elif PW_FORCE is not None and not fused and scales[0] is None and bias is None and addend is None and \
+            bwd[0] is None and bwd[1] is None and mask is None and _pw_ok(geo, dh, dw, tb) and \
+            geo[2] <= conv_pw_cfgs()[PW_FORCE][1]:
+        cfg = (0, 0, PW_BASE + PW_FORCE)  # (tests) every eligible launch on this pointwise variant
     elif DEEP_FORCE is not None and not fused and scales[0] is None and _deep_ok(geo, dh, dw):
         cfg = (0, 0, DEEP_BASE + DEEP_FORCE)  # (tests) every eligible launch on this prefetch-depth-2 variant
     elif HALO_FORCE is not None and not fused and scales[0] is None and \
@@ -213,7 +217,9 @@ def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(
                 A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups, scales, xa, xf, mask)
             if cfg[0] or cfg[2] >= 0:
                 _STAGES_TUNED[key] = cfg
-    if cfg[2] >= DEEP_BASE:
+    if cfg[2] >= PW_BASE:
+        PW_COUNT[0] += 1
+    elif cfg[2] >= DEEP_BASE:
         DEEP_COUNT[0] += 1
     elif cfg[2] >= HALO_BASE:
         HALO_COUNT[0] += 1
@@ -287,6 +293,35 @@ def _deep_ok(geo, dh, dw):
     if geo[3] % 64:
         return False
     return (geo[6] <= 16383 and geo[7] <= 16383) or not any(dh) and not any(dw)
+
+
+_PW_CFGS = None
+PW_CONV = os.environ.get("IMGCLS_PW", "1") == "1"  # register-resident-weight 1x1 kernels (csrc/conv_pw.hip) as candidates
+PW_FORCE = None  # tests: force a pointwise variant on every eligible launch
+PW_COUNT = [0]   # pointwise-kernel launches (tests)
+PW_BASE = 3000   # cfg[2] >= PW_BASE: the pointwise kernel, entry cfg - base
+
+
+def conv_pw_cfgs():
+    """The pointwise kernel's table: (output channels per block, k capacity)."""
+    global _PW_CFGS
+    if _PW_CFGS is None:
+        _PW_CFGS = [tuple(c) for c in C.conv_pw_cfgs()]
+    return _PW_CFGS
+
+
+def _pw_ok(geo, dh, dw, tb, v=None):
+    """A plain 1x1 stride-1 forward launch (csrc/conv_pw.hip::conv_pw_launch) that entry ``v`` covers: K fits
+    its k capacity without a whole spare 32-wide chunk, and its channel tile is not wider than the layer."""
+    m, co, k, ca, gh, gw, ih, iw, sa = geo[:9]
+    if len(dh) != 1 or dh[0] or dw[0] or tb[0] or sa != 1 or (gh, gw) != (ih, iw) or k != ca or ca % 8 or co % 8:
+        return False
+    if geo[12] != 1 or geo[13] or geo[14] or (geo[10], geo[11]) != (gh, gw) or geo[15] % 4 or geo[16] % 4:
+        return False
+    if v is None:
+        return True
+    n_blk, k_cap = conv_pw_cfgs()[v]
+    return k <= k_cap < k + 32 and n_blk < co + 16
 
 
 _FP8_CFGS = None
@@ -413,6 +448,14 @@ def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, group
             cfg = (0, 0, DEEP_BASE + v)
             times[cfg] = _time_ms(lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, groups, zero,
                                                       addend, *bwd, *cfg, *scales, *xa3, None, *xf2, mask, None, None, None, 0))
+    if PW_CONV and not fused and scales[0] is None and bias is None and addend is None and bwd[0] is None and \
+            bwd[1] is None and mask is None and _pw_ok(geo, dh, dw, tb):
+        for v in range(len(conv_pw_cfgs())):
+            if _pw_ok(geo, dh, dw, tb, v):
+                cfg = (0, 0, PW_BASE + v)
+                times[cfg] = _time_ms(lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, groups, zero,
+                                                          addend, *bwd, *cfg, *scales, *xa3, None, *xf2, mask, None,
+                                                          None, None, 0))
     dg = _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales) if not fused else None
     if dg is not None:
         for v in DIRECT_CFGS:
@@ -669,12 +712,12 @@ def _wgrad_config(dy, x, g: ConvGeom, m, ntot, xa=None, xf=None):
 # names this part owns (ops/hip.py re-exports them)
 _OWNED = (
     'CONV_FORCE_CFG', 'CONV_FORCE_FP8_CFG', 'CONV_STAGES', 'ConvGeom', 'DEEP_BASE', 'DEEP_CONV', 'DEEP_COUNT',
-    'DEEP_FORCE', 'DIRECT_BASE', 'DIRECT_CFGS', 'DIRECT_CONV', 'DIRECT_DGRAD', 'DIRECT_FORCE', 'FUSED_XA_BWD',
+    'DEEP_FORCE', 'DIRECT_BASE', 'PW_BASE', 'PW_CONV', 'PW_COUNT', 'PW_FORCE', '_PW_CFGS', 'DIRECT_CFGS', 'DIRECT_CONV', 'DIRECT_DGRAD', 'DIRECT_FORCE', 'FUSED_XA_BWD',
     'FUSED_XA_BWD_COUNT', 'FUSED_XA_BWD_N', 'HALO_BASE', 'HALO_CONV', 'HALO_COUNT', 'HALO_FORCE', 'HALO_TUNE',
     'SKIP_WGRAD', 'TUNE_LOG', 'WGRAD_CANDIDATES', 'WGRAD_MIN_K', 'WGRAD_NARROW_TILES', 'WGRAD_STAGES',
     'WGRAD_TARGET_BLOCKS', 'WGRAD_TUNE_LOG', 'WGRAD_WS', '_CFGS', '_CU_COUNT', '_DEEP_CFGS', '_FP8_CFGS',
     '_HALO_CFGS', '_ORDER_IDX', '_STAGES_TUNED', '_WGRAD_TUNED', '_WGRAD_WS', '_conv_candidates',
-    '_conv_forward_fp8', '_conv_gemm', '_deep_ok', '_dgrad_phases', '_direct_geom', '_direct_launch', '_direct_variant_ok',
+    '_conv_forward_fp8', '_conv_gemm', '_deep_ok', '_dgrad_phases', '_direct_geom', '_direct_launch', '_direct_variant_ok', '_pw_ok', 'conv_pw_cfgs',
     '_fwd_taps', '_halo_ok', '_time_ms', '_tune_conv', '_weight_for_input', '_wgrad_config', '_wgrad_has',
     '_wgrad_launch', '_wgrad_plan', '_wgrad_split', '_wgrad_tiles', '_wgrad_ws', 'conv_cfgs', 'conv_deep_cfgs',
     'conv_dgrad_raw', 'conv_forward_raw', 'conv_fp8_cfgs', 'conv_fused_bwd_raw', 'conv_geom', 'conv_halo_cfgs',

@@ -28,24 +28,17 @@ _OWNER = {}
 for _m in _PARTS.values():
     for _k in _m.__dict__.get("_OWNED", ()):
         _OWNER[_k] = _m
-# flags the tests / set_* functions rebind and functions scripts monkeypatch: read live from the owner
-_LATE = frozenset((
-    'CONCAT_INPLACE', 'CONV_FORCE_CFG', 'CONV_FORCE_FP8_CFG', 'CONV_STAGES', 'DEEP_BASE', 'DEEP_CONV',
-    'DEEP_COUNT', 'DEEP_FORCE', 'DETERMINISTIC', 'DIRECT_BASE', 'DIRECT_CFGS', 'DIRECT_CONV', 'DIRECT_DGRAD',
-    'DIRECT_FORCE', 'DW_LINK', 'FP8_FWD', 'FUSED_BWD_COUNT', 'FUSED_XA_BWD', 'FUSED_XA_BWD_COUNT',
-    'FUSED_XA_BWD_N', 'FUSE_BN_BWD', 'FUSE_XA', 'FUSE_XF', 'GRAPH_SIDE', 'HALO_BASE', 'HALO_CONV', 'HALO_COUNT',
-    'HALO_FORCE', 'HALO_TUNE', 'PEER_BN_MAX_C', 'POOL_CONV_SWAP', 'RELU_MASK', 'SE_FUSED', 'SE_LINK',
-    'SHIFT_STATS', 'SKIP_WGRAD', 'STEM_DIRECT', 'STEM_POOL_FUSE', 'STEM_S2D', 'STEM_WGRAD_SIDE',
-    'SYNCBN_EARLY_COUNT', 'TUNE_LOG', 'WGRAD_CANDIDATES', 'WGRAD_MIN_K', 'WGRAD_NARROW_TILES', 'WGRAD_STAGES',
-    'WGRAD_STREAM', 'WGRAD_TARGET_BLOCKS', 'WGRAD_TUNE_LOG', 'WGRAD_WS', 'XA_COUNT', 'XA_MAX_REP',
-    'XA_NARROW_OFF', 'XF_COUNT', 'XF_MAX_REP', '_ADAM_CHUNK', '_AFFINE_CACHE', '_CFGS', '_CU_COUNT',
-    '_DEEP_CFGS', '_FP8_CFGS', '_HALO_CFGS', '_MXW_DT', '_ORDER_IDX', '_S2D_INDEX', '_SHADOWS', '_SHADOW_GEN',
-    '_SIDE', '_STAGES_TUNED', '_TENSOR_DT', '_WGRAD_TUNED', '_WGRAD_WS', '_WS', '_WTJOB_DT', '_conv_gemm',
-    '_time_ms', '_wgrad_launch',
-))
+# Data (flags, counters, caches, tables) is read live from the owning part on every ``hip.X`` (tests and
+# set_* functions rebind flags); functions and classes are copied here for plain attribute speed, except the
+# ones scripts monkeypatch (scripts/conv_roofline.py, scripts/tune_random_choices.py).
+_PATCHED = frozenset(("_conv_gemm", "_wgrad_launch", "_time_ms"))
+_LATE = set(_PATCHED)
 for _k, _m in _OWNER.items():
-    if _k not in _LATE:
-        globals()[_k] = getattr(_m, _k)
+    _v = getattr(_m, _k)
+    if isinstance(_v, (types.FunctionType, type)) and _k not in _PATCHED:
+        globals()[_k] = _v
+    else:
+        _LATE.add(_k)
 
 
 class _HipFacade(types.ModuleType):

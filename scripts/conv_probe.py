@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--halo", type=int, default=-1)
     ap.add_argument("--deep", type=int, default=-1, help="index into ops.hip.conv_deep_cfgs() (prefetch-depth-2 kernel)")
     ap.add_argument("--direct", type=int, default=-1, help="index into ops.hip.DIRECT_CFGS (halo-tile direct kernels)")
+    ap.add_argument("--pw", type=int, default=-1, help="index into ops.hip.conv_pw_cfgs() (1x1 resident-weight kernel)")
     ap.add_argument("--wstages", type=int, default=0)
     ap.add_argument("--iters", type=int, default=20)
     a = ap.parse_args()
@@ -45,6 +46,8 @@ def main():
         hip.DEEP_FORCE = a.deep
     if a.direct >= 0:
         hip.DIRECT_FORCE = a.direct
+    if a.pw >= 0:
+        hip.PW_FORCE = a.pw
     if a.wstages:
         hip.WGRAD_STAGES = a.wstages
     hip.ensure_channels_last_weight(conv)
@@ -71,7 +74,8 @@ def main():
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.iters
     flops = 2.0 * g.N * g.OH * g.OW * cout * g.T * cin
-    tag = f"halo {a.halo}" if a.halo >= 0 else f"direct {a.direct}" if a.direct >= 0 else f"cfg {a.cfg}"
+    tag = f"halo {a.halo}" if a.halo >= 0 else f"direct {a.direct}" if a.direct >= 0 else \
+        f"pw {a.pw}" if a.pw >= 0 else f"cfg {a.cfg}"
     print(f"{a.op} shape {a.shape} b{a.batch} {tag}: {ms * 1e3:.1f} us  {flops / ms / 1e9:.0f} TF/s", flush=True)
 
 

@@ -5,7 +5,7 @@ timed with HIP events around it (synchronising, so the numbers are per-launch, n
 compared with its roofline time max(FLOP / PEAK_TF, bytes / PEAK_BW).  Sorted by time lost to the
 roofline: the top rows are where kernel work pays most.
 
-    python scripts/conv_roofline.py [batch=256] [peak_tf=2300] [peak_tbps=6.0]
+    python scripts/conv_roofline.py [batch=256] [peak_tf=2300] [peak_tbps=6.0] [model=resnet50] [image_size]
 """
 import collections
 import os
@@ -22,6 +22,8 @@ from pytorch_imageclassification_distributed_amd.parallel import init_distribute
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 PEAK_TF = float(sys.argv[2]) if len(sys.argv) > 2 else 2300.0
 PEAK_BW = float(sys.argv[3]) if len(sys.argv) > 3 else 6.0
+MODEL = sys.argv[4] if len(sys.argv) > 4 else "resnet50"
+SIZE = int(sys.argv[5]) if len(sys.argv) > 5 else 224
 REC = []
 ON = [False]
 
@@ -65,7 +67,7 @@ def wgrad(dy, x, out, g, m, ntot, kps, splits, stages=2, side=None, **kw):
 hip._conv_gemm, hip._wgrad_launch = gemm, wgrad
 
 ctx = init_distributed(device="cuda")
-targs = build_parser().parse_args(["--synthetic", "--model", "resnet50", "--batchsize", str(B), "--num-classes", "7",
+targs = build_parser().parse_args(["--synthetic", "--model", MODEL, "--image-size", str(SIZE), "--batchsize", str(B), "--num-classes", "7",
                                    "--num-workers", "0", "--synthetic-train-size", "8", "--synthetic-val-size", "8",
                                    "--no-sync-bn", "--lr", "1e-4"])
 tr = Trainer(targs, ctx)
@@ -74,7 +76,7 @@ _db = os.environ.get("IMGCLS_TUNE_DB", os.path.join(os.path.dirname(os.path.dirn
 if _db != "none" and os.path.exists(_db):
     print(f"{hip.load_tuning(_db)} kernel choices from {_db}")
 tr.net.train()
-batches = list(iter(DeviceSyntheticLoader(B, 7, 224, ctx.device, steps=2, ring=2, seed=1)))
+batches = list(iter(DeviceSyntheticLoader(B, 7, SIZE, ctx.device, steps=2, ring=2, seed=1)))
 for i in range(4):
     tr.train_step(batches[i % 2]["image"], batches[i % 2]["label"])
 torch.cuda.synchronize()

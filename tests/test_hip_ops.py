@@ -211,6 +211,59 @@ def test_conv_deep_plain_gemm(mnk, cfg):
     assert rel_err(out, ref) < 1e-2
 
 
+N_PW = _table_len("conv_pw_cfgs", 12)
+PW_CASES = [  # N, Cin, H, W, Cout: EfficientNet expand / project 1x1 shapes, partial fragments and channel tiles
+    (2, 16, 40, 40, 96), (2, 24, 28, 28, 144), (3, 144, 20, 20, 24), (2, 32, 33, 31, 16), (2, 40, 14, 14, 240),
+    (2, 96, 15, 15, 24), (1, 80, 9, 7, 48)]
+
+
+@pytest.mark.parametrize("cfg", range(N_PW))
+@pytest.mark.parametrize("case", PW_CASES)
+def test_conv_pw_configs(case, cfg):
+    """Every register-resident-weight pointwise configuration (csrc/conv_pw.hip) forced on the 1x1 forward it
+    covers, inside conv -> BN (train) -> SiLU: output (through the epilogue's BN statistics), running
+    statistics and the backward against fp32 torch, and the kernel ran."""
+    hip = _hip()
+    if cfg >= len(hip.conv_pw_cfgs()):
+        pytest.skip("past the configuration table")
+    n, c, h, w, co = case
+    if c > hip.conv_pw_cfgs()[cfg][1]:
+        pytest.skip("K exceeds the entry's k capacity")
+    torch.manual_seed(3)
+    conv = nn.Conv2d(c, co, 1, bias=False).to(DEV).to(memory_format=CL)
+    bn = nn.BatchNorm2d(co).to(DEV)
+    with torch.no_grad():
+        conv.weight.copy_(bf(conv.weight))
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+        bn.running_mean.uniform_(-0.2, 0.2)  # a non-zero statistics pivot (the BN's running mean)
+    conv_r = nn.Conv2d(c, co, 1, bias=False).to(DEV)
+    bn_r = nn.BatchNorm2d(co).to(DEV)
+    conv_r.load_state_dict(conv.state_dict())
+    bn_r.load_state_dict(bn.state_dict())
+    x = bf(torch.randn(n, c, h, w, device=DEV))
+    xb = x.to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
+    keep, hip.PW_FORCE = hip.PW_FORCE, cfg
+    before = hip.PW_COUNT[0]
+    try:
+        out = hip.conv_bn_act(xb, conv, bn, "silu", None)
+    finally:
+        hip.PW_FORCE = keep
+    assert hip.PW_COUNT[0] > before, "pointwise kernel not launched"
+    xr = x.clone().requires_grad_(True)
+    yc = conv_r(xr)
+    yc = yc + (bf(yc) - yc).detach()
+    ref = F.silu(bn_r(yc))
+    assert rel_err(out, ref) < 2e-2
+    assert torch.allclose(bn.running_mean, bn_r.running_mean, rtol=1e-2, atol=1e-3)
+    assert torch.allclose(bn.running_var, bn_r.running_var, rtol=1e-2, atol=1e-3)
+    g = bf(torch.randn_like(ref))
+    out.backward(g.to(torch.bfloat16).contiguous(memory_format=CL))
+    ref.backward(g)
+    assert rel_err(xb.grad, xr.grad) < 3e-2
+    assert rel_err(conv.weight.grad, conv_r.weight.grad) < 3e-2
+
+
 @pytest.mark.parametrize("cfg", range(N_HALO))
 @pytest.mark.parametrize("act,use_res", [("relu", True), ("silu", False)])
 def test_conv_bn_act_halo(act, use_res, cfg):
