@@ -22,6 +22,8 @@
 #include <numeric>
 #include "common.h"
 
+#include <cstdlib>
+
 namespace {
 
 // ---- partial rows [G][2][C] -> fp64 sums [2][C]; zero the rows -------------
@@ -243,34 +245,64 @@ __global__ void bn_apply_kernel(const bf16_t* __restrict__ y, const float* __res
 // sits behind a runtime select (which makes hipcc branch around and wait for each load).
 constexpr int BN_U = 4;
 
+// Rows of a channel-fixed elementwise pass (the grid's thread count is a multiple of C/8, grid_chan): when
+// 256 % (C/8) == 0 each block streams its own contiguous run of rows (256 / (C/8) rows per step), otherwise
+// the grid-wide stride.  The grid-wide stride had every wave's U loads land in U regions tens of MB apart;
+// block-contiguous runs took the residual BN apply from 4.46 to 5.03 TB/s (torch's add: 6.07) on ResNet-50
+// layer1 at b1024 and 4.52 -> 5.12 at C = 512 (scripts/bn_probe.py, profiles/r10e_bn_apply_layouts.txt).
+struct RowWalk {
+  long row, rend, step;
+  int c0;
+};
+DEVI RowWalk row_walk(long rows, int cch, int contiguous) {
+  RowWalk w;
+  if (contiguous && 256 % cch == 0) {
+    const int rpb = 256 / cch;
+    const long per = (rows + gridDim.x - 1) / gridDim.x;
+    const long per_r = (per + rpb - 1) / rpb * rpb;
+    w.row = (long)blockIdx.x * per_r + threadIdx.x / cch;
+    w.rend = (long)(blockIdx.x + 1) * per_r < rows ? (long)(blockIdx.x + 1) * per_r : rows;
+    w.step = rpb;
+    w.c0 = (int)(threadIdx.x % cch) * 8;
+  } else {
+    const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    w.step = ((long)gridDim.x * blockDim.x) / cch;
+    w.row = t / cch;
+    w.rend = rows;
+    w.c0 = (int)(t - w.row * cch) * 8;
+  }
+  return w;
+}
+
 template <bool RES>
 __global__ void bn_apply_u_kernel(const bf16_t* __restrict__ y, const float* __restrict__ coef,
                                   const bf16_t* __restrict__ res, bf16_t* __restrict__ out, long rows, int C,
-                                  int ldo, int c_off, int act, uint8_t* __restrict__ mask) {
+                                  int ldo, int c_off, int act, uint8_t* __restrict__ mask, int walk) {
+  constexpr int U = 2 * BN_U;  // 8 rows in flight measured best with the block-contiguous walk
   const int cch = C >> 3;
-  const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
   if (cch == 0) return;
-  const long rstride = ((long)gridDim.x * blockDim.x) / cch;
-  long row = t / cch;
-  if (row >= rows) return;
-  const int c0 = (int)(t - row * cch) * 8;
+  const RowWalk w = row_walk(rows, cch, walk);
+  long row = w.row;
+  const long rend = w.rend, rstride = w.step;
+  const int c0 = w.c0;
+  if (row >= rend) return;
   float sc[8], sh[8];
   *(float4*)sc = *(const float4*)(coef + c0);
   *(float4*)(sc + 4) = *(const float4*)(coef + c0 + 4);
   *(float4*)sh = *(const float4*)(coef + C + c0);
   *(float4*)(sh + 4) = *(const float4*)(coef + C + c0 + 4);
-  for (; row < rows; row += BN_U * rstride) {
-    uint4 yv[BN_U], rv[BN_U];
+  for (; row < rend; row += U * rstride) {
+    uint4 yv[U], rv[U];
 #pragma unroll
-    for (int u = 0; u < BN_U; ++u) {
-      const long r = row + u * rstride < rows ? row + u * rstride : row;
+    for (int u = 0; u < U; ++u) {
+      const long r = row + u * rstride < rend ? row + u * rstride : row;
       yv[u] = *(const uint4*)(y + r * C + c0);
       if constexpr (RES) rv[u] = *(const uint4*)(res + r * C + c0);
     }
 #pragma unroll
-    for (int u = 0; u < BN_U; ++u) {
+    for (int u = 0; u < U; ++u) {
       const long r = row + u * rstride;
-      if (r >= rows) break;
+      if (r >= rend) break;
       float v[8], rr[8];
       unpack8(yv[u], v);
       if constexpr (RES) unpack8(rv[u], rr);
@@ -694,14 +726,14 @@ template <int MODE>
 __global__ void bn_bwd_elemt_u_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ y,
                                       const float* __restrict__ coef, const float* __restrict__ kk,
                                       const bf16_t* __restrict__ res, const bf16_t* __restrict__ dz_in,
-                                      bf16_t* __restrict__ dy, long rows, int C, int act, int ldg) {
+                                      bf16_t* __restrict__ dy, long rows, int C, int act, int ldg, int walk) {
   const int cch = C >> 3;
-  const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
   if (cch == 0) return;
-  const long rstride = ((long)gridDim.x * blockDim.x) / cch;
-  long row = t / cch;
-  if (row >= rows) return;
-  const int c0 = (int)(t - row * cch) * 8;
+  const RowWalk w = row_walk(rows, cch, walk);
+  long row = w.row;
+  const long rend = w.rend, rstride = w.step;
+  const int c0 = w.c0;
+  if (row >= rend) return;
   float sc[8], sh[8], mu[8], is[8], k1[8], k2[8];
   load8f(coef + c0, sc);
   load8f(coef + 2 * C + c0, mu);
@@ -709,11 +741,11 @@ __global__ void bn_bwd_elemt_u_kernel(const bf16_t* __restrict__ g, const bf16_t
   load8f(kk + c0, k1);
   load8f(kk + C + c0, k2);
   if constexpr (MODE == 1 || MODE == 2) load8f(coef + C + c0, sh);
-  for (; row < rows; row += BN_U * rstride) {
+  for (; row < rend; row += BN_U * rstride) {
     uint4 yr[BN_U], gr[BN_U], rr[BN_U];
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
-      const long r = row + u * rstride < rows ? row + u * rstride : row;
+      const long r = row + u * rstride < rend ? row + u * rstride : row;
       yr[u] = *(const uint4*)(y + r * C + c0);
       if constexpr (MODE == 0) gr[u] = *(const uint4*)(dz_in + r * C + c0);
       else gr[u] = *(const uint4*)(g + r * ldg + c0);
@@ -722,7 +754,7 @@ __global__ void bn_bwd_elemt_u_kernel(const bf16_t* __restrict__ g, const bf16_t
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
       const long r = row + u * rstride;
-      if (r >= rows) break;
+      if (r >= rend) break;
       float gv[8], yv[8];
       unpack8(yr[u], yv);
       unpack8(gr[u], gv);
@@ -791,6 +823,9 @@ int grid_for(long work, int per_block = 256, int cap = 4096) {
 // grid for the channel-fixed elementwise kernels: grid_for's block count rounded up so that
 // blocks * 256 is a multiple of C/8 (threads past the last row return at once)
 int g_bn_unroll = 1;  // U-row elementwise kernels (bn_set_unroll; A/B and tests)
+// row walk of the U-row apply / backward-elementwise kernels: 1 = block-contiguous runs (row_walk), 0 = the
+// grid-wide stride (IMGCLS_BN_WALK=0, same-box A/B)
+int g_bn_walk = getenv("IMGCLS_BN_WALK") ? atoi(getenv("IMGCLS_BN_WALK")) : 1;
 
 int grid_chan(long rows, int C) {
   const int cch = C / 8;
@@ -864,9 +899,9 @@ int bn_apply_launch(const bf16_t* y, const float* coef, const bf16_t* res, bf16_
   }
   if (g_bn_unroll || mask) {
     if (res) hipLaunchKernelGGL(bn_apply_u_kernel<true>, dim3(grid_chan(rows, C)), dim3(256), 0, s, y, coef, res, out,
-                                rows, C, ldo, c_off, act, mask);
+                                rows, C, ldo, c_off, act, mask, g_bn_walk);
     else hipLaunchKernelGGL(bn_apply_u_kernel<false>, dim3(grid_chan(rows, C)), dim3(256), 0, s, y, coef, res, out,
-                            rows, C, ldo, c_off, act, mask);
+                            rows, C, ldo, c_off, act, mask, g_bn_walk);
   } else {
     hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_chan(rows, C)), dim3(256), 0, s, y, coef, res, out,
                        rows, C, ldo, c_off, act);
@@ -913,10 +948,14 @@ int bn_bwd_elemt_launch(const bf16_t* g, const bf16_t* y, const float* coef, con
   const int lg = ldg > 0 ? ldg : C;
   if (g_bn_unroll) {
     const dim3 gr(grid_chan(rows, C));
-    if (dz_in) hipLaunchKernelGGL(bn_bwd_elemt_u_kernel<0>, gr, dim3(256), 0, s, g, y, coef, k, res, dz_in, dy, rows, C, act, lg);
-    else if (act == ACT_NONE) hipLaunchKernelGGL(bn_bwd_elemt_u_kernel<3>, gr, dim3(256), 0, s, g, y, coef, k, res, dz_in, dy, rows, C, act, lg);
-    else if (res) hipLaunchKernelGGL(bn_bwd_elemt_u_kernel<2>, gr, dim3(256), 0, s, g, y, coef, k, res, dz_in, dy, rows, C, act, lg);
-    else hipLaunchKernelGGL(bn_bwd_elemt_u_kernel<1>, gr, dim3(256), 0, s, g, y, coef, k, res, dz_in, dy, rows, C, act, lg);
+    if (dz_in) hipLaunchKernelGGL(bn_bwd_elemt_u_kernel<0>, gr, dim3(256), 0, s, g, y, coef, k, res, dz_in, dy, rows, C, act, lg,
+                                       g_bn_walk);
+    else if (act == ACT_NONE) hipLaunchKernelGGL(bn_bwd_elemt_u_kernel<3>, gr, dim3(256), 0, s, g, y, coef, k, res, dz_in, dy, rows, C, act, lg,
+                                       g_bn_walk);
+    else if (res) hipLaunchKernelGGL(bn_bwd_elemt_u_kernel<2>, gr, dim3(256), 0, s, g, y, coef, k, res, dz_in, dy, rows, C, act, lg,
+                                       g_bn_walk);
+    else hipLaunchKernelGGL(bn_bwd_elemt_u_kernel<1>, gr, dim3(256), 0, s, g, y, coef, k, res, dz_in, dy, rows, C, act, lg,
+                                       g_bn_walk);
   } else {
     hipLaunchKernelGGL(bn_bwd_elemt_kernel, dim3(grid_chan(rows, C)), dim3(256), 0, s, g, y, coef, k,
                        res, dz_in, dy, rows, C, act, lg);
