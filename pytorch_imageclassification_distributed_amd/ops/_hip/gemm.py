@@ -151,7 +151,9 @@ def load_tuning(path: str) -> int:
         except (ValueError, SyntaxError, TypeError):
             continue
         fp8 = bool(k[10]) if len(k) > 10 else False
-        if v[2] >= DEEP_BASE:
+        if v[2] >= PW_BASE:
+            ok = not fp8 and v[2] - PW_BASE < len(conv_pw_cfgs()) and len(v) == 3
+        elif v[2] >= DEEP_BASE:
             ok = not fp8 and v[2] - DEEP_BASE < len(conv_deep_cfgs()) and len(v) == 3
         elif v[2] >= HALO_BASE:
             ok = not fp8 and v[2] - HALO_BASE < len(conv_halo_cfgs()) and len(v) == 3

@@ -55,5 +55,23 @@ def test_invalid_and_existing_entries(hip, tmp_path):
 
 
 def test_committed_db_parses(hip):
+    # every committed entry names a configuration this build has: none is dropped on load (pointwise entries,
+    # cfg >= PW_BASE, used to fall into the deep-kernel range check and were skipped)
     path = os.path.join(ROOT, "tuning", "mi355x_find_db.json")
-    assert hip.load_tuning(path) > 100
+    with open(path) as f:
+        db = json.load(f)
+    assert hip.load_tuning(path) == len(db["conv"]) + len(db["wgrad"]) > 100
+
+
+def test_round_trip_every_kernel_family(hip, tmp_path):
+    base = ((1024, 64, 64, 64, 8, 8, 8, 8, 1, 64, 8, 8, 1, 0, 0, 64, 0), 64, (0,), (0,), False, False, False,
+            False, False, 0, False, True)
+    cfgs = [(0, 0, 0), (0, 0, hip.DIRECT_BASE + 5), (3, 128, hip.HALO_BASE), (0, 0, hip.DEEP_BASE),
+            (0, 0, hip.PW_BASE + len(hip.conv_pw_cfgs()) - 1)]
+    for i, v in enumerate(cfgs):
+        hip._STAGES_TUNED[base[:1] + (16 * (i + 1),) + base[2:]] = v
+    path = str(tmp_path / "db.json")
+    assert hip.save_tuning(path) == len(cfgs)
+    hip._STAGES_TUNED.clear()
+    assert hip.load_tuning(path) == len(cfgs)
+    assert sorted(hip._STAGES_TUNED.values()) == sorted(cfgs)
