@@ -23,6 +23,8 @@
 // Scope: uniform k-steps (CA % 64 == 0), no fused A-operand map (XA / XF keep conv_gemm_glds_kernel).
 // Per-row gather state is packed (pixel offset + 16-bit row / column) to leave registers for the
 // fragments; a launch whose input map is wider than 16383 pixels with a non-centre tap falls back.
+#include <type_traits>
+
 #include "conv_common.h"
 
 namespace {
@@ -44,6 +46,11 @@ struct DeepCfg {
 DEVI void mfma_acc(f32x4& acc, const bf16x8& a, const bf16x8& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b) : "memory");
 }
+// 32 x 32 x 16 (variant bit 256): lane l supplies row l & 31 of each operand at k 8 (l >> 5) .. + 7 and holds
+// D[row 8 (r >> 2) + 4 (l >> 5) + (r & 3)][col l & 31] (scripts/probes/mfma_shape_rate.hip checks the map)
+DEVI void mfma_acc(f32x16& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b) : "memory");
+}
 
 // LDS-DMA of 16 B per lane with a per-lane offset and a wave-uniform (SGPR) offset
 DEVI void blds16s(__amdgpu_buffer_rsrc_t r, unsigned voff, int soff, char* lds_wave_base) {
@@ -63,6 +70,10 @@ template <int TM, int BN, int WM, int WN, int PRIO>
 __global__ __launch_bounds__(64 * WM * WN, 1) void conv_deep_kernel(const ConvParams p) {
   using Cfg = DeepCfg<TM, BN, WM, WN>;
   constexpr bool SETPRIO = PRIO & 1;
+  // BIG (variant bit 256): v_mfma_f32_32x32x16_bf16 on 32 x 32 accumulator blocks.  Same LDS bytes per k-step
+  // (the fragments are register-reused across the sub-tile either way), half the MFMA instructions, and each
+  // 32-deep k-half splits into two 16-deep sub-steps s, so a half's MFMAs divide into phases B / C by s.
+  constexpr bool BIG = PRIO & 256;
   constexpr int NW = Cfg::NW;
   constexpr int A_BYTES = Cfg::A_BYTES, STAGE = Cfg::STAGE;
   constexpr int WTM = TM / WM, WTN = BN / WN;
@@ -167,21 +178,39 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_deep_kernel(const ConvPa
     blds16s(live ? (q < AL ? rsA : rsB) : rsZ, q < AL ? a_vb[q] : b_row[q - AL], q < AL ? s_off_a : s_off_b, dst);
   };
 
-  f32x4 acc[RM][RN];
+  using AccT = typename std::conditional<BIG, f32x16, f32x4>::type;
+  constexpr int AR = BIG ? RM / 2 : RM, AC = BIG ? RN / 2 : RN;  // accumulator blocks of the wave's sub-tile
+  AccT acc[AR][AC];
 #pragma unroll
-  for (int i = 0; i < RM; ++i)
+  for (int i = 0; i < AR; ++i)
 #pragma unroll
-    for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < AC; ++j) acc[i][j] = AccT{};
   asm volatile("s_nop 7");
 
   const int nk = (p.K + BK - 1) / BK;
   const int fr = lane & 15, fq = lane >> 4;
   bf16x8 a0[RM], b0[RN], a1[RM], b1[RN];
   // fragment q of a half (A rows first, then B rows) from buffer buf, k-half h
+  // BIG: fragment q of a half is sub-step s = q / AR (A) of 32 rows x 16 k - row l & 31, chunk 4h + 2s + (l >> 5)
   auto frag = [&](bf16x8 (&fa)[RM], bf16x8 (&fb)[RN], int buf, int h, int q) {
     const char* sa = smem + buf * STAGE;
-    if (q < RM) fa[q] = *(const bf16x8*)(sa + swz(wm * WTM + q * 16 + fr, 4 * h + fq));
-    else fb[q - RM] = *(const bf16x8*)(sa + A_BYTES + swz(wn * WTN + (q - RM) * 16 + fr, 4 * h + fq));
+    if constexpr (BIG) {
+      const int r32 = lane & 31, c32 = 4 * h + (lane >> 5);
+      if (q < RM) fa[q] = *(const bf16x8*)(sa + swz(wm * WTM + (q % AR) * 32 + r32, c32 + 2 * (q / AR)));
+      else fb[q - RM] = *(const bf16x8*)(sa + A_BYTES + swz(wn * WTN + ((q - RM) % AC) * 32 + r32, c32 + 2 * ((q - RM) / AC)));
+    } else {
+      if (q < RM) fa[q] = *(const bf16x8*)(sa + swz(wm * WTM + q * 16 + fr, 4 * h + fq));
+      else fb[q - RM] = *(const bf16x8*)(sa + A_BYTES + swz(wn * WTN + (q - RM) * 16 + fr, 4 * h + fq));
+    }
+  };
+  // MFMA t of a half: 16x16 - block (t / RN, t % RN); BIG - sub-step s = t / (AR AC), block (t / AC % AR, t % AC)
+  auto mm = [&](int t, const bf16x8 (&fa)[RM], const bf16x8 (&fb)[RN]) {
+    if constexpr (BIG) {
+      const int s = t / (AR * AC), i = (t / AC) % AR, j = t % AC;
+      mfma_acc(acc[i][j], fb[s * AC + j], fa[s * AR + i]);
+    } else {
+      mfma_acc(acc[t / RN][t % RN], fb[t % RN], fa[t / RN]);
+    }
   };
   plan();
 #pragma unroll
@@ -202,8 +231,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_deep_kernel(const ConvPa
   //     vmcnt(LPS) + barrier: tile kt+1 has landed everywhere (tile kt+2 stays in flight)
   //  C: rest of the half-1 MFMAs | tile kt+1's half-0 fragment reads (a0 / b0)
   constexpr int NF = RM + RN;        // fragment reads per half
-  constexpr int MA = RM * RN;        // MFMAs of phase A
-  constexpr int MB = RM * RN / 2;    // ... of phase B and of phase C
+  constexpr int MA = BIG ? RM * RN / 2 : RM * RN;  // MFMAs of phase A
+  constexpr int MB = MA / 2;                        // ... of phase B and of phase C
   // variant bits (PRIO): 1 s_setprio around the MFMA runs; 8 tile kt+2's pieces in one burst after the
   // barrier; 16 pieces spread over phases B and C; 32 phase-A fragment reads spread over all of phase A.
   // Diagnostics (wrong results, never tuned): 2 no pieces in the loop, 4 no fragment reads in the loop.
@@ -215,7 +244,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_deep_kernel(const ConvPa
     if constexpr (SETPRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int t = 0; t < MA; ++t) {
-      mfma_acc(acc[t / RN][t % RN], b0[t % RN], a0[t / RN]);
+      mm(t, a0, b0);
 #pragma unroll
       for (int q = 0; q < NF; ++q)
         if (!D_NOFRAG && (q * MA) / (FRAGALL ? NF : 2 * NF) == t) frag(a1, b1, cur, 1, q);
@@ -232,7 +261,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_deep_kernel(const ConvPa
     if constexpr (SETPRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int t = 0; t < MB; ++t) {
-      mfma_acc(acc[t / RN][t % RN], b1[t % RN], a1[t / RN]);
+      mm(t, a1, b1);
 #pragma unroll
       for (int q = 0; q < PB; ++q)
         if (!BURST && !D_NOLOAD && (q * MB) / PB == t) piece(cur, q, live);
@@ -244,7 +273,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_deep_kernel(const ConvPa
     if constexpr (SETPRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int t = MB; t < 2 * MB; ++t) {
-      mfma_acc(acc[t / RN][t % RN], b1[t % RN], a1[t / RN]);
+      mm(t, a1, b1);
 #pragma unroll
       for (int q = 0; q < NF; ++q)
         if (!D_NOFRAG && (q * MB) / NF == t - MB) frag(a0, b0, cur ^ 1, 0, q);
@@ -263,25 +292,36 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_deep_kernel(const ConvPa
   // the scheduler reads every AGPR out before the first store and spills
   bf16_t* ct = (bf16_t*)smem;
   constexpr int CST = BN + 8;
+  auto stage4 = [&](int row, int col, float v0, float v1, float v2, float v3) {
+    float v[4] = {v0, v1, v2, v3};
+    if (p.bias != nullptr) {
 #pragma unroll
-  for (int i = 0; i < RM; ++i) {
-    const int row = wm * WTM + i * 16 + fr;
+      for (int r = 0; r < 4; ++r) v[r] += n0 + col + r < p.Ncols ? p.bias[n0 + col + r] : 0.f;
+    }
+    uint2 pk;
+    pk.x = pack2(v[0], v[1]);
+    pk.y = pack2(v[2], v[3]);
+    *(uint2*)(ct + row * CST + col) = pk;
+  };
 #pragma unroll
-    for (int j = 0; j < RN; ++j) {
-      const int col = wn * WTN + j * 16 + fq * 4;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (p.bias != nullptr) {
+  for (int i = 0; i < AR; ++i) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += n0 + col + r < p.Ncols ? p.bias[n0 + col + r] : 0.f;
+    for (int j = 0; j < AC; ++j) {
+      if constexpr (BIG) {  // pixel l & 31, channels 8g + 4 (l >> 5) + r
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          stage4(wm * WTM + i * 32 + (lane & 31), wn * WTN + j * 32 + 8 * g + 4 * (lane >> 5), acc[i][j][4 * g],
+                 acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
+      } else {
+        stage4(wm * WTM + i * 16 + fr, wn * WTN + j * 16 + fq * 4, acc[i][j][0], acc[i][j][1], acc[i][j][2],
+               acc[i][j][3]);
       }
-      uint2 pk;
-      pk.x = pack2(v[0], v[1]);
-      pk.y = pack2(v[2], v[3]);
-      *(uint2*)(ct + row * CST + col) = pk;
     }
     __builtin_amdgcn_sched_barrier(0);
   }
-  conv_epilogue_dispatch<TM, BN, WM, WN, 2, true>(p, acc, smem, tid, lane, wid, wm, wn, m0, n0, bm, ghw);
+  // the staged epilogue reads the tile from LDS only (its accumulator argument is unused)
+  conv_epilogue_dispatch<TM, BN, WM, WN, 2, true>(p, *reinterpret_cast<f32x4(*)[RM][RN]>(&acc), smem, tid, lane, wid,
+                                                  wm, wn, m0, n0, bm, ghw);
 }
 
 template <int TM, int BN, int WM, int WN, int PRIO>
@@ -302,6 +342,9 @@ const DeepEntry g_deep[] = {
     DEEP(256, 256, 2, 2, 4),
     // spread pieces + grouped tile order (4- / 8-row bands per XCD)
     DEEP(256, 256, 2, 2, 16 | 64), DEEP(256, 256, 2, 2, 16 | 128), DEEP(256, 128, 2, 2, 16 | 64),
+    // 32 x 32 x 16 MFMA blocks
+    DEEP(256, 256, 2, 2, 256), DEEP(256, 256, 2, 2, 16 | 64 | 256), DEEP(256, 128, 2, 2, 16 | 64 | 256),
+    DEEP(256, 256, 2, 2, 1 | 256),
 };
 #undef DEEP
 

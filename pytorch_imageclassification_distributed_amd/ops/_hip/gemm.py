@@ -445,7 +445,9 @@ def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, group
                                                       addend, *bwd, *cfg, *scales, *xa3, None, *xf2, mask, None, None, None, 0))
     if DEEP_CONV and not fused and scales[0] is None and _deep_ok(geo, dh, dw):
         for v, (tm, bn, _wm, _wn, var) in enumerate(conv_deep_cfgs()):
-            if var & 6 or (bn > 64 and bn >= 2 * geo[1]) or (bn == 64 and geo[1] >= 256) or geo[0] < tm * 8:
+            # var & 256 (32x32x16 MFMA blocks) is measured but not tuned: 5-10% slower than the same schedule on
+            # 16x16x32 on every ResNet-50 shape (profiles/r10n_deep_mfma32_ab.txt)
+            if var & (6 | 256) or (bn > 64 and bn >= 2 * geo[1]) or (bn == 64 and geo[1] >= 256) or geo[0] < tm * 8:
                 continue
             cfg = (0, 0, DEEP_BASE + v)
             times[cfg] = _time_ms(lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, groups, zero,
