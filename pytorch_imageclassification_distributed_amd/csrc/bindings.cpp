@@ -287,7 +287,7 @@ void conv_wgrad(Tensor dY, Tensor X, Tensor dW, int M, int Cout, int Cin, int Nt
   p.stride_h = sh; p.stride_w = sw; p.pad_t = pt; p.pad_l = pl; p.dil_h = dh; p.dil_w = dwd; p.KW = KW;
   p.k_per_split = k_per_split;
   p.zero = ptr<bf16_t>(zero);
-  TORCH_CHECK(stages >= 0 && stages <= 12, "conv_wgrad: stages must be 0..12");
+  TORCH_CHECK(stages >= 0 && stages <= 15, "conv_wgrad: stages must be 0..15");
   TORCH_CHECK((stages != 5 && stages != 6) || Cout <= 32, "conv_wgrad: stages 5 / 6 (32-row tile) need Cout <= 32");
   TORCH_CHECK((stages != 4 && stages != 7 && stages != 9) || Cout >= 256, "conv_wgrad: the 256x256 tile needs Cout >= 256");
   p.stages = stages;

@@ -117,6 +117,9 @@ int conv_deep_launch(int i, const ConvParams& p, hipStream_t stream);  // 3: geo
 int conv_pw_num();
 void conv_pw_info(int i, int* out2);  // {output channels per block, k capacity}
 int conv_pw_launch(int i, const ConvParams& p, hipStream_t stream);  // 3: not a plain 1x1 stride-1 forward
+// prefetch-depth-2 weight gradient (wgrad_deep.hip): WgradParams::stages 13 / 14 / 15 = 256 x 256 /
+// 128 x 256 / 256 x 128 tiles, plain operands only; 3 = not this kernel's variant or geometry
+int wgrad_deep_launch(const WgradParams& p, int splits, hipStream_t stream);
 int conv_wgrad_launch(const WgradParams& p, int splits, hipStream_t stream);
 int conv_fused_bwd_launch(const ConvParams& p, const bf16_t* X, float* ws, float* dW, int blocks, hipStream_t stream);
 bool conv_wgrad_has_xa(int stages);  // the wgrad variant selected by ``stages`` has a fused BN-backward dY form

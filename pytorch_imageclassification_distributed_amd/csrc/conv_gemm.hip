@@ -1987,6 +1987,19 @@ int conv_wgrad_tile_n(int stages) {
 int conv_wgrad_launch(const WgradParams& p_in, int splits, hipStream_t stream) {
   if (p_in.M <= 0) return 0;
   if (p_in.xa_y && (g_wvariant == 1 || !conv_wgrad_has_xa(p_in.stages))) return 4;
+  if (p_in.stages >= 13) {
+    if (p_in.xf_coef) return 4;
+    WgradParams p = p_in;
+    if (splits <= 1) p.ws = nullptr;
+    const int r = wgrad_deep_launch(p, splits, stream);
+    if (r) return r;
+    HIP_CHECK_LAUNCH();
+    if (p.ws != nullptr) {
+      wgrad_reduce_auto(p.ws, p.dW, (long)p.Cout * p.Ntot / 4, splits, stream);
+      HIP_CHECK_LAUNCH();
+    }
+    return 0;
+  }
   if (p_in.xf_coef && (g_wvariant == 1 || !conv_wgrad_has_xf(p_in.stages))) return 4;
   bool ok = true;
   const bool dma = g_wvariant != 1;

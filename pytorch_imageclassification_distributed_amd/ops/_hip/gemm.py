@@ -168,7 +168,7 @@ def load_tuning(path: str) -> int:
             k, v = ast.literal_eval(ks), tuple(int(x) for x in v)
         except (ValueError, SyntaxError, TypeError):
             continue
-        if len(v) == 2 and 1 <= v[1] <= 12 and v[0] > 0 and k not in _WGRAD_TUNED:
+        if len(v) == 2 and 1 <= v[1] <= 15 and v[0] > 0 and k not in _WGRAD_TUNED:
             _WGRAD_TUNED[k] = v
             n += 1
     return n
@@ -596,6 +596,7 @@ def _wgrad_split(m, tiles, target):
     return kps, splits
 
 
+WGRAD_DEEP = os.environ.get("IMGCLS_WGRAD_DEEP", "1") == "1"  # stages 13-15 (csrc/wgrad_deep.hip) as candidates
 WGRAD_NARROW_TILES = os.environ.get("IMGCLS_WGRAD_NARROW_TILES", "1") == "1"  # stages 10-12 as tuner candidates
 WGRAD_STAGES = int(os.environ.get("IMGCLS_WGRAD_STAGES", "0"))  # 0 = tuned with the split count; 1 | 2 | 3
 
@@ -644,8 +645,10 @@ def _wgrad_launch(dy, x, out, g: ConvGeom, m, ntot, kps, splits, stages=2, side=
 def _wgrad_tiles(co, ntot, stages):
     """Output tiles of one wgrad launch: 256 x 256 for the 8-wave kernels (stages 4, 7, 9), 32 x 128 for
     stages 5 / 6, 64-column tiles for stages 10 / 11 (64|128 rows) and 12 (256 rows), else 64|128 x 128."""
-    if stages in (4, 7, 9):
+    if stages in (4, 7, 9, 13):
         return (-(-co // 256)) * (-(-ntot // 256))
+    if stages in (14, 15):  # prefetch-depth-2 kernel (csrc/wgrad_deep.hip): 128 x 256 / 256 x 128
+        return (-(-co // (128 if stages == 14 else 256))) * (-(-ntot // (256 if stages == 14 else 128)))
     if stages >= 10:
         return (-(-co // (256 if stages == 12 else 64 if co <= 64 else 128))) * (-(-ntot // 64))
     return (-(-co // (32 if stages in (5, 6) else 64 if co <= 64 else 128))) * (-(-ntot // 128))
@@ -693,6 +696,13 @@ def _wgrad_config(dy, x, g: ConvGeom, m, ntot, xa=None, xf=None):
             cands += [(cand, st) for st in (4, 7, 9) for cand in (256, 512)]
         # 4-deep ring of 32-pixel stages (two stages in flight across every barrier), 4 waves
         cands += [(cand, 8) for cand in blocks if cand <= 1024]
+        if WGRAD_DEEP and not (fx or ff):  # prefetch-depth-2 kernel, 4 waves of 128 x 128 / 64 x 128 / 128 x 64
+            if g.Co >= 256 and ntot >= 256:
+                cands += [(cand, 13) for cand in (256, 512, 768)]
+            if g.Co >= 128 and ntot >= 256:
+                cands += [(cand, 14) for cand in (256, 512, 768, 1024)]
+            if g.Co >= 256 and ntot >= 128:
+                cands += [(cand, 15) for cand in (256, 512, 768, 1024)]
         if g.Co <= 32:  # 32-row tiles: a 64-row tile would be half empty
             cands += [(cand, st) for st in (5, 6) for cand in blocks]
         if ntot <= 64 and WGRAD_NARROW_TILES:  # 64-column tiles: a 128-column tile is half empty (layer1 conv3)
@@ -718,7 +728,7 @@ _OWNED = (
     'CONV_FORCE_CFG', 'CONV_FORCE_FP8_CFG', 'CONV_STAGES', 'ConvGeom', 'DEEP_BASE', 'DEEP_CONV', 'DEEP_COUNT',
     'DEEP_FORCE', 'DIRECT_BASE', 'PW_BASE', 'PW_CONV', 'PW_COUNT', 'PW_FORCE', '_PW_CFGS', 'DIRECT_CFGS', 'DIRECT_CONV', 'DIRECT_DGRAD', 'DIRECT_FORCE', 'FUSED_XA_BWD',
     'FUSED_XA_BWD_COUNT', 'FUSED_XA_BWD_N', 'HALO_BASE', 'HALO_CONV', 'HALO_COUNT', 'HALO_FORCE', 'HALO_TUNE',
-    'SKIP_WGRAD', 'TUNE_LOG', 'WGRAD_CANDIDATES', 'WGRAD_MIN_K', 'WGRAD_NARROW_TILES', 'WGRAD_STAGES',
+    'SKIP_WGRAD', 'TUNE_LOG', 'WGRAD_CANDIDATES', 'WGRAD_DEEP', 'WGRAD_MIN_K', 'WGRAD_NARROW_TILES', 'WGRAD_STAGES',
     'WGRAD_TARGET_BLOCKS', 'WGRAD_TUNE_LOG', 'WGRAD_WS', '_CFGS', '_CU_COUNT', '_DEEP_CFGS', '_FP8_CFGS',
     '_HALO_CFGS', '_ORDER_IDX', '_STAGES_TUNED', '_WGRAD_TUNED', '_WGRAD_WS', '_conv_candidates',
     '_conv_forward_fp8', '_conv_gemm', '_deep_ok', '_dgrad_phases', '_direct_geom', '_direct_launch', '_direct_variant_ok', '_pw_ok', 'conv_pw_cfgs',

@@ -282,13 +282,14 @@ def test_conv_bn_act_halo(act, use_res, cfg):
 
 @pytest.mark.parametrize("case,stages", [
     (c, st) for c in [CONV_CASES[i] for i in (0, 1, 3, 4, 5, 6, 7, 8, 12, 13, 14, 15)]
-    for st in (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12)
+    for st in (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
     if _wgrad_stage_ok(c, st)])
 def test_conv_wgrad_ring_variants(case, stages):
     """Weight-gradient kernel variants: 1-stage (occupancy), 2-stage ring, the 8-wave in-block
     2-way pixel split (stages=3), the 256x256 8-wave tile (stages=4, Cout >= 256), the 32-row tile
-    (stages=5 / 6, Cout <= 32) and the 4- / 3-deep rings of 32-pixel stages (stages=7 / 9 on the
-    256x256 tile, 8 on the 4-wave tiles) - each over the
+    (stages=5 / 6, Cout <= 32), the 4- / 3-deep rings of 32-pixel stages (stages=7 / 9 on the
+    256x256 tile, 8 on the 4-wave tiles) and the prefetch-depth-2 kernel (csrc/wgrad_deep.hip, stages
+    13 / 14 / 15: 256 x 256, 128 x 256, 256 x 128 on 4 waves, partial tiles included) - each over the
     tuner's split counts."""
     hip = _hip()
     keep, hip.WGRAD_STAGES = hip.WGRAD_STAGES, stages
