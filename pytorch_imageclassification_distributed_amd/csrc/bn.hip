@@ -780,7 +780,7 @@ __global__ void bn_bwd_elemt_u_kernel(const bf16_t* __restrict__ g, const bf16_t
 
 // target block count of the row-reduction kernels (bn_stats, bn_bwd_reduce); 0 = measured default:
 // 2048 for C <= 256 (~10 % faster than 1024), 1024 above (more blocks only add partial-row atomics)
-static int g_reduce_blocks = 0;
+static int g_reduce_blocks = getenv("IMGCLS_BN_REDUCE_BLOCKS") ? atoi(getenv("IMGCLS_BN_REDUCE_BLOCKS")) : 0;
 // channel-chunk lanes per block (8 channels each); 0 = auto: the smallest divisor of C/8 in [8, 32]
 // (C/8 itself below 8; 32 when none divides), so a block ends in 2 x 64 .. 2 x 256 partial-row atomics
 // whatever C is.  With all C/8 chunks in one block (the former layout) a C = 2048 layer issued 4096
