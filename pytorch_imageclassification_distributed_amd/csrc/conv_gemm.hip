@@ -31,6 +31,8 @@
 //    of the bf16-rounded outputs) with one fp32 atomic per channel per block
 //    into G rotating partial rows (low contention) - so the BN statistics pass
 //    never re-reads the conv output.
+#include <cstdlib>
+
 #include "conv_gemm.h"
 #include "conv_common.h"
 
@@ -1378,7 +1380,11 @@ struct FusedW {
 // coefficient DMAs and y loads (and, on a tile's first k-step, its X tile into the other X buffer) are issued
 // right after step s's barrier, so they land during step s's MFMAs and the previous tile's epilogue; the
 // epilogue stages through its own LDS region.
-template <int CO, int WM, int WN>
+//
+// DEPTH 3 (CO >= 128): a 3-deep ring, two steps of loads in flight across each barrier (the 2-deep ring had one,
+// and at one 8-wave block per CU the kernel streamed dz / y at ~3.4 TB/s); the y register pieces alternate
+// between two sets, so the step loop is unrolled by two.
+template <int CO, int WM, int WN, int DEPTH = 2>
 __global__ __launch_bounds__(64 * WM * WN, 2) void conv_fused_bwd_kernel(const ConvParams p, const FusedW f) {
   constexpr int TM = 128, BNc = 64, NW = WM * WN;
   constexpr int WTM = TM / WM, WTN = BNc / WN;       // dgrad wave tile
@@ -1391,8 +1397,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_fused_bwd_kernel(const C
   constexpr int X_BYTES = TM * 128;
   constexpr int NKC = CO / BK;                       // k-steps (64-channel chunks of dz)
   constexpr int EPI = TM * (BNc + 8) * 2 > NW * 2 * BNc * 4 ? TM * (BNc + 8) * 2 : NW * 2 * BNc * 4;
-  constexpr int RING = 2 * STAGE, XOFF = RING, EOFF = RING + 2 * X_BYTES, MAIN = EOFF + EPI;
+  constexpr int RING = DEPTH * STAGE, XOFF = RING, EOFF = RING + 2 * X_BYTES, MAIN = EOFF + EPI;
   static_assert(CO % BK == 0 && CO <= 256 && MAIN <= 160 * 1024, "fused backward: CO in {64, 128, 192, 256}");
+  static_assert(DEPTH == 2 || (DEPTH == 3 && NKC >= 2), "3-deep ring: a tile's X slot is reused two tiles later");
   __shared__ __attribute__((aligned(16))) char smem[MAIN];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1427,13 +1434,13 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_fused_bwd_kernel(const C
   const int ntiles = (p.M + TM - 1) / TM;
   const int my_tiles = blockIdx.x < ntiles ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
   const int nsteps = my_tiles * NKC;
-  unsigned va[AL];
-  uint4 yv[AL];
-  // issue flat step s = (tile t, k-step kc) into ring slot s & 1 (and the tile's X image into slot t & 1)
-  auto issue = [&](int s) {
+  uint4 yv0[AL], yv1[AL];
+  // issue flat step s = (tile t, k-step kc) into ring slot s % DEPTH (and the tile's X image into slot t & 1)
+  auto issue = [&](int s, uint4 (&yv)[AL]) __attribute__((always_inline)) {
     const int t = s / NKC, kc = s - t * NKC;
     const int m0 = ((int)blockIdx.x + t * (int)gridDim.x) * TM;
-    char* sa = smem + (s & 1) * STAGE;
+    char* sa = smem + (s % DEPTH) * STAGE;
+    unsigned va[AL];
     if (kc == 0) {
       char* sx = smem + XOFF + (t & 1) * X_BYTES;
 #pragma unroll
@@ -1466,14 +1473,20 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_fused_bwd_kernel(const C
   };
 
   f32x4 acc[RM][RN];
-  if (nsteps > 0) issue(0);
-  for (int s = 0; s < nsteps; ++s) {
+  auto step = [&](int s, uint4 (&yv)[AL]) __attribute__((always_inline)) {
     const int t = s / NKC, kc = s - t * NKC;
     const int tile = (int)blockIdx.x + t * (int)gridDim.x, m0 = tile * TM;
-    char* sa = smem + (s & 1) * STAGE;
+    char* sa = smem + (s % DEPTH) * STAGE;
     char* sb = sa + A_BYTES;
     const char* sx = smem + XOFF + (t & 1) * X_BYTES;
-    wait_vmcnt<0>();
+    if constexpr (DEPTH == 2) {
+      wait_vmcnt<0>();
+    } else {  // step s has landed; step s + 1's loads (its X tile too on a k-step 0) stay in flight
+      constexpr int N0 = 2 * AL + BL + 1, N1 = N0 + AL;
+      if (s + 1 >= nsteps) wait_vmcnt<0>();
+      else if ((s + 1) % NKC == 0) wait_vmcnt<N1>();
+      else wait_vmcnt<N0>();
+    }
     // this wave's dz pieces of step s -> dY in place (rows past M stay zero)
     {
       const float* kcf = (const float*)(sb + B_BYTES + wid * 1024);
@@ -1489,7 +1502,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_fused_bwd_kernel(const C
         }
 #pragma unroll
         for (int i = gg; i < AL; i += 2) {
-          if (va[i] == OOB) continue;
+          if (m0 + wid * (TM / NW) + i * 8 + lrow >= p.M) continue;
           uint4* dst = (uint4*)(sa + (wid * (TM / NW) + i * 8) * 128 + lane * 16);
           float d[8], y[8];
           unpack8(*dst, d);
@@ -1501,9 +1514,10 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_fused_bwd_kernel(const C
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
-    // step s published; every wave is also done with slot (s + 1) & 1 (step s - 1) and X slot of tile t - 1
+    // step s published; every wave is also done with slot (s + DEPTH - 1) % DEPTH (step s - 1) and the X slot
+    // of tile t - 1; the y set just consumed takes step s + DEPTH - 1's pieces (same parity for DEPTH 3)
     __builtin_amdgcn_s_barrier();
-    if (s + 1 < nsteps) issue(s + 1);
+    if (s + DEPTH - 1 < nsteps) issue(s + DEPTH - 1, yv);
     if (kc == 0) {
 #pragma unroll
       for (int i = 0; i < RM; ++i)
@@ -1557,6 +1571,16 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_fused_bwd_kernel(const C
       conv_epilogue_dispatch<TM, BNc, WM, WN, 1>(p, acc, smem + EOFF, tid, lane, wid, wm, wn, m0, 0, tile,
                                                   p.GH * p.GW);
       __syncthreads();  // epilogue LDS reused by the next tile
+    }
+  };
+  if (nsteps > 0) issue(0, yv0);
+  if constexpr (DEPTH == 2) {
+    for (int s = 0; s < nsteps; ++s) step(s, yv0);
+  } else {
+    if (nsteps > 1) issue(1, yv1);
+    for (int s = 0; s < nsteps; s += 2) {
+      step(s, yv0);
+      if (s + 1 < nsteps) step(s + 1, yv1);
     }
   }
   // this block's dW partial -> its workspace slab (plain 16-B stores; the reduce adds the slabs in order)
@@ -1760,9 +1784,18 @@ static int launch_fused_bwd_n(const ConvParams& p, const FusedW& f, float* dW, i
   return 0;
 }
 
+static const int g_fused_depth = getenv("IMGCLS_FUSED_DEPTH") ? atoi(getenv("IMGCLS_FUSED_DEPTH")) : 3;
+
 template <int CO>
 static int launch_fused_bwd(const ConvParams& p, const FusedW& f, float* dW, int blocks, hipStream_t stream) {
-  hipLaunchKernelGGL((conv_fused_bwd_kernel<CO, 4, 2>), dim3(blocks), dim3(512), 0, stream, p, f);
+  if constexpr (CO >= 128) {
+    if (g_fused_depth == 3)
+      hipLaunchKernelGGL((conv_fused_bwd_kernel<CO, 4, 2, 3>), dim3(blocks), dim3(512), 0, stream, p, f);
+    else
+      hipLaunchKernelGGL((conv_fused_bwd_kernel<CO, 4, 2>), dim3(blocks), dim3(512), 0, stream, p, f);
+  } else {
+    hipLaunchKernelGGL((conv_fused_bwd_kernel<CO, 4, 2>), dim3(blocks), dim3(512), 0, stream, p, f);
+  }
   HIP_CHECK_LAUNCH();
   const long n4 = (long)CO * 64 / 4;
   wgrad_reduce_auto(f.ws, dW, n4, blocks, stream);
