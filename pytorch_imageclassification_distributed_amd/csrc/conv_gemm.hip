@@ -1381,9 +1381,10 @@ struct FusedW {
 // right after step s's barrier, so they land during step s's MFMAs and the previous tile's epilogue; the
 // epilogue stages through its own LDS region.
 //
-// DEPTH 3 (CO >= 128): a 3-deep ring, two steps of loads in flight across each barrier (the 2-deep ring had one,
-// and at one 8-wave block per CU the kernel streamed dz / y at ~3.4 TB/s); the y register pieces alternate
-// between two sets, so the step loop is unrolled by two.
+// DEPTH 3 (CO >= 128, IMGCLS_FUSED_DEPTH=3): a 3-deep ring, two steps of loads in flight across each barrier
+// (the 2-deep ring has one; the kernel streams dz / y at ~3.4 TB/s at one 8-wave block per CU).  The y register
+// pieces alternate between two sets, so the step loop is unrolled by two.  Measured no faster, so not the
+// default: load latency is not what bounds this kernel.
 template <int CO, int WM, int WN, int DEPTH = 2>
 __global__ __launch_bounds__(64 * WM * WN, 2) void conv_fused_bwd_kernel(const ConvParams p, const FusedW f) {
   constexpr int TM = 128, BNc = 64, NW = WM * WN;
@@ -1784,7 +1785,9 @@ static int launch_fused_bwd_n(const ConvParams& p, const FusedW& f, float* dW, i
   return 0;
 }
 
-static const int g_fused_depth = getenv("IMGCLS_FUSED_DEPTH") ? atoi(getenv("IMGCLS_FUSED_DEPTH")) : 3;
+// 3-deep ring: measured no faster at the kernel level (4.865 vs 4.825 ms for the 4 launches, profiles/r10t_*), so
+// the 2-deep ring stays the default; IMGCLS_FUSED_DEPTH=3 selects the other
+static const int g_fused_depth = getenv("IMGCLS_FUSED_DEPTH") ? atoi(getenv("IMGCLS_FUSED_DEPTH")) : 2;
 
 template <int CO>
 static int launch_fused_bwd(const ConvParams& p, const FusedW& f, float* dW, int blocks, hipStream_t stream) {
