@@ -92,6 +92,9 @@ struct WgradParams {
   // act(xf_coef[0][ci] * y + xf_coef[1][ci]) with the zero padding kept
   const float* xf_coef;  // [2][Cin] (the BN's scale, shift)
   int xf_act;
+  // fused (XA / XF) forms with a >= 2-deep ring: stage kt+1's in-place transform runs after stage kt's MFMAs
+  // are issued (overlapping them) instead of between the wait and the barrier of stage kt (set by the launcher)
+  int xa_pipe;
 };
 
 int conv_gemm_launch(const ConvParams& p, hipStream_t stream);

@@ -1155,6 +1155,18 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
 #pragma unroll
   for (int s0 = 0; s0 < STAGES - 1; ++s0)
     if (s0 < nk) issue(s0);
+  // PIPE (IMGCLS_WGRAD_XA_PIPE=1, off by default - measured slower): the fused operand transform of stage kt+1
+  // is done after stage kt's MFMAs are issued, to overlap its VALU / LDS work with the matrix pipe; in the plain
+  // order every wave transforms between its wait and the barrier (the XA / XF weight gradients run 10-20 % MFMA
+  // busy against 38 % without a transform: profiles/r10v_*).  Stage kt+1 is published by iteration kt+1's barrier.
+  const bool PIPE = (XA || XF) && STAGES >= 2 && p.xa_pipe;
+  if constexpr ((XA || XF) && STAGES >= 2) {
+    if (PIPE) {
+      if (STAGES - 2 < nk) wait_vmcnt<(STAGES - 2) * LPS>();
+      else wait_vmcnt<0>();
+      xa_transform(0, 0);
+    }
+  }
   const int g = lane >> 4, li = lane & 15;
   const int tq = li >> 2, tp = li & 3;
   // fragments of k-half kk: permuted k order (identical for A and B): elements 0-3 <- rows 4g+q,
@@ -1186,9 +1198,11 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
     } else {
       // stage kt landed; the STAGES-2 younger stages stay in flight across the barrier, which also
       // retires every wave's reads of the slot the next issue overwrites
-      if (kt + STAGES - 2 < nk) wait_vmcnt<(STAGES - 2) * LPS>();
-      else wait_vmcnt<0>();
-      xa_transform(kt % STAGES, kt);
+      if (!PIPE) {
+        if (kt + STAGES - 2 < nk) wait_vmcnt<(STAGES - 2) * LPS>();
+        else wait_vmcnt<0>();
+        xa_transform(kt % STAGES, kt);
+      }
       __builtin_amdgcn_s_barrier();
     }
     const char* sa = smem + (STAGES == 1 ? 0 : (kt % STAGES) * STAGE);
@@ -1206,6 +1220,13 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
 #pragma unroll
         for (int j = 0; j < RN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    if constexpr ((XA || XF) && STAGES >= 2) {
+      if (PIPE && kt + 1 < nk) {  // stage kt+1 landed (the younger stages stay in flight): transform it
+        if (kt + STAGES - 1 < nk) wait_vmcnt<(STAGES - 2) * LPS>();
+        else wait_vmcnt<0>();
+        xa_transform((kt + 1) % STAGES, kt + 1);
+      }
     }
   }
   const int fr = lane & 15, fq = lane >> 4;
@@ -1985,6 +2006,10 @@ int conv_gemm_launch(const ConvParams& p, hipStream_t stream) {
 
 static int g_wvariant = 0;
 void conv_set_wgrad_variant(int v) { g_wvariant = v; }
+// IMGCLS_WGRAD_XA_PIPE=1: the fused weight-gradient transforms pipelined behind the MFMAs.  Measured slower per
+// kernel (the 12 XA 256 x 256 launches 6.47 vs 6.33 ms, the 2-deep 128 x 128 ones 2.22 vs 1.81 ms) and on the
+// step (-0.3 %, profiles/r10w_wgrad_xa_pipe_ab.txt), so the plain order is the default.
+static const int g_xa_pipe = getenv("IMGCLS_WGRAD_XA_PIPE") ? atoi(getenv("IMGCLS_WGRAD_XA_PIPE")) : 0;
 
 template <int WBM, int TN, int WM, int WN, int KG, int ST, int BKP, bool XA, bool XF>
 static bool launch_wg_x(const WgradParams& p, const dim3& grid, hipStream_t stream) {
@@ -2040,6 +2065,7 @@ int conv_wgrad_launch(const WgradParams& p_in, int splits, hipStream_t stream) {
   bool ok = true;
   const bool dma = g_wvariant != 1;
   WgradParams p = p_in;
+  p.xa_pipe = g_xa_pipe;
   if (!dma || splits <= 1) p.ws = nullptr;  // the register-staged kernel always adds atomically
   // stages: 1 | 2 (4 waves, 64/128 x 128 tile), 3 = 2-stage ring with the in-block 2-way pixel split
   // (8 waves), 4 = 256 x 256 tile on 8 waves (2-stage ring, one block per CU; Cout >= 256 only),
