@@ -36,14 +36,19 @@ struct DirectArgs {
 template <int CIP, int KH, int KW, int COT>
 struct DC {
   static constexpr int TH = 8, TW = 16, PH = TH + KH - 1, PW = TW + KW - 1;
-  static constexpr int PIX_B = CIP * 2 + 16;   // +16 B: conflict-free 16-lane operand reads
+  // Row pads: a fragment read has lane l fetch 16 B at row (l & 15) * S + chunk (l >> 4) (S = row bytes / 16), and
+  // a ds_read_b128 is conflict-free when every 16-lane group hits 16 distinct 16-B slots of the bank row - true
+  // for S = 2 mod 4 only.  +16 B (S = 9 at CIP 64) cost 2-way conflicts on 7 of 16 lanes (46 % of LDS-active
+  // cycles, profiles/r10v_resnet50_b1024_pmc_summary.txt); +32 B gives S = CIP / 8 + 2 = 2 mod 4 for every CIP
+  // (a multiple of 32), and the same for the weight rows (KP / 8 + 2).
+  static constexpr int PIX_B = CIP * 2 + 32;
   static constexpr int PATCH_B = PH * PW * PIX_B;
   static constexpr int CPP = CIP / 8;          // 16-byte pieces per patch pixel
   static constexpr int PIECES = PH * PW * CPP;
   static constexpr int PPT = (PIECES + 255) / 256;
   static constexpr int KP = KH * KW * CIP;
   static constexpr int NKC = KP / 32;
-  static constexpr int W_ROW = KP * 2 + 16;
+  static constexpr int W_ROW = KP * 2 + 32;
   static constexpr int W_B = COT * W_ROW;
   static constexpr int CB = COT / 16;
   static constexpr int CH = COT / 8;           // 16-byte output chunks per pixel
