@@ -60,3 +60,21 @@ def test_direct64_swizzle_conflict_free_at_every_row():
 def test_direct64_swizzle_is_a_chunk_permutation():
     for row in range(8):
         assert sorted(c ^ d64_key(row) for c in range(8)) == list(range(8))
+
+
+def stride_conflicts(S):
+    """Padded-row layout (csrc/direct_conv.hip patch / weight rows): lane l reads the 16-B slot
+    (l & 15) * S + (l >> 4) of the bank row, S = row bytes / 16."""
+    bad = 0
+    for g in GROUPS:
+        slots = [((l & 15) * S + (l >> 4)) % 16 for l in g]
+        bad += len(slots) - len(set(slots))
+    return bad
+
+
+def test_direct_conv_row_pad_conflict_free():
+    # rows of CIP * 2 + 32 bytes (patch pixels) and KH * KW * CIP * 2 + 32 (weights), CIP a multiple of 32
+    for cip in (32, 64, 96, 128):
+        assert stride_conflicts((cip * 2 + 32) // 16) == 0, cip
+        assert stride_conflicts((9 * cip * 2 + 32) // 16) == 0, cip
+    assert stride_conflicts((64 * 2 + 16) // 16) > 0  # the former 16-byte pad (S = 9) conflicts
