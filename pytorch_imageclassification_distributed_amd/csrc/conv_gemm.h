@@ -95,6 +95,7 @@ struct WgradParams {
   // fused (XA / XF) forms with a >= 2-deep ring: stage kt+1's in-place transform runs after stage kt's MFMAs
   // are issued (overlapping them) instead of between the wait and the barrier of stage kt (set by the launcher)
   int xa_pipe;
+  int xa_tab;  // floats per 8-channel chunk of the XA coefficient table in LDS: 12 (conflict-free) or 8 (packed)
 };
 
 int conv_gemm_launch(const ConvParams& p, hipStream_t stream);

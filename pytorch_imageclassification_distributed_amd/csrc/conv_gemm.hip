@@ -906,7 +906,11 @@ struct WgCfg {
   static constexpr int LDT = TN + 4;
   static constexpr int EPI = (KG == 2 ? WBM : WBM / WM) * LDT * 4;  // staged fp32 rows
   static constexpr int MAIN = STAGES * STAGE > EPI ? STAGES * STAGE : EPI;
-  static constexpr int XA_BYTES = XA ? 12 * WBM : 0;  // fused BN-backward coefficients [3][WBM] fp32
+  // fused BN-backward coefficients [3][WBM / 8 chunks][12] fp32: 8 per 8-channel chunk at a 48-B chunk stride, so
+  // the per-piece 16-B reads of a 16-lane group (16 distinct chunks, distinct mod 16) hit 16 distinct bank slots
+  // (a 32-B stride put them on 8: the XA weight gradients showed 27-31 % LDS bank-conflict cycles, r10v)
+  static constexpr int XA_ROW = WBM / 8 * 12;
+  static constexpr int XA_BYTES = XA ? 3 * XA_ROW * 4 : 0;
   static constexpr int XF_BYTES = XF ? 8 * TN : 0;    // fused BN-apply coefficients [2][TN] fp32 (per column)
   static constexpr int BLOCKS = (160 * 1024) / (MAIN + XA_BYTES + XF_BYTES);
   static constexpr int OCC0 = BLOCKS * NW / 4 < 1 ? 1 : (BLOCKS * NW / 4 > 3 ? 3 : BLOCKS * NW / 4);
@@ -1021,7 +1025,8 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
     rsZ = make_rsrc(p.xa_y + (long)kbeg * p.Cout, 2L * (kend - kbeg) * p.Cout);
     for (int t = tid; t < 3 * WBM; t += NTH) {
       const int arr = t / WBM, co = co0 + (t - arr * WBM);
-      s_xa[t] = co < p.Cout ? p.xa_coef[arr * p.Cout + co] : 0.f;
+      const int c = t - arr * WBM;
+      s_xa[arr * Cfg::XA_ROW + (c >> 3) * p.xa_tab + (c & 7)] = co < p.Cout ? p.xa_coef[arr * p.Cout + co] : 0.f;
     }
     __syncthreads();
   }
@@ -1125,12 +1130,14 @@ void conv_wgrad_glds_kernel(const WgradParams p) {
         if (!a_cok[i] || pix >= kend) continue;
         const int j = a_col[i] - co0;
         float c0[8], c1[8], c2[8];
-        *(f32x4*)c0 = *(const f32x4*)(s_xa + j);
-        *(f32x4*)(c0 + 4) = *(const f32x4*)(s_xa + j + 4);
-        *(f32x4*)c1 = *(const f32x4*)(s_xa + WBM + j);
-        *(f32x4*)(c1 + 4) = *(const f32x4*)(s_xa + WBM + j + 4);
-        *(f32x4*)c2 = *(const f32x4*)(s_xa + 2 * WBM + j);
-        *(f32x4*)(c2 + 4) = *(const f32x4*)(s_xa + 2 * WBM + j + 4);
+        const float* xc = s_xa + (j >> 3) * p.xa_tab;  // j = the piece's first column, a multiple of 8
+        constexpr int XR = Cfg::XA_ROW;
+        *(f32x4*)c0 = *(const f32x4*)(xc);
+        *(f32x4*)(c0 + 4) = *(const f32x4*)(xc + 4);
+        *(f32x4*)c1 = *(const f32x4*)(xc + XR);
+        *(f32x4*)(c1 + 4) = *(const f32x4*)(xc + XR + 4);
+        *(f32x4*)c2 = *(const f32x4*)(xc + 2 * XR);
+        *(f32x4*)(c2 + 4) = *(const f32x4*)(xc + 2 * XR + 4);
         uint4* dst = (uint4*)(sa + (wid * AL + i) * 1024 + lane * 16);
         float d[8], y[8];
         unpack8(*dst, d);
@@ -2010,6 +2017,8 @@ void conv_set_wgrad_variant(int v) { g_wvariant = v; }
 // kernel (the 12 XA 256 x 256 launches 6.47 vs 6.33 ms, the 2-deep 128 x 128 ones 2.22 vs 1.81 ms) and on the
 // step (-0.3 %, profiles/r10w_wgrad_xa_pipe_ab.txt), so the plain order is the default.
 static const int g_xa_pipe = getenv("IMGCLS_WGRAD_XA_PIPE") ? atoi(getenv("IMGCLS_WGRAD_XA_PIPE")) : 0;
+// IMGCLS_WGRAD_XA_TAB=8: the packed (bank-conflicting) XA coefficient table, for A/B
+static const int g_xa_tab = getenv("IMGCLS_WGRAD_XA_TAB") && atoi(getenv("IMGCLS_WGRAD_XA_TAB")) == 8 ? 8 : 12;
 
 template <int WBM, int TN, int WM, int WN, int KG, int ST, int BKP, bool XA, bool XF>
 static bool launch_wg_x(const WgradParams& p, const dim3& grid, hipStream_t stream) {
@@ -2066,6 +2075,7 @@ int conv_wgrad_launch(const WgradParams& p_in, int splits, hipStream_t stream) {
   const bool dma = g_wvariant != 1;
   WgradParams p = p_in;
   p.xa_pipe = g_xa_pipe;
+  p.xa_tab = g_xa_tab;
   if (!dma || splits <= 1) p.ws = nullptr;  // the register-staged kernel always adds atomically
   // stages: 1 | 2 (4 waves, 64/128 x 128 tile), 3 = 2-stage ring with the in-block 2-way pixel split
   // (8 waves), 4 = 256 x 256 tile on 8 waves (2-stage ring, one block per CU; Cout >= 256 only),
