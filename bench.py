@@ -54,6 +54,8 @@ def parse():
     p.add_argument("--compute", default="hip", choices=["hip", "torch"])
     p.add_argument("--sync-bn", default="auto", choices=["auto", "on", "off"])
     p.add_argument("--bucket-mb", type=float, default=32.0)
+    p.add_argument("--tail-bucket-mb", type=float, default=4.0,
+                   help="pieces of the last gradient bucket (stem + layer1, produced last), MiB; 0 = one bucket")
     p.add_argument("--syncbn-comm", default="auto", choices=["auto", "peer", "rccl"],
                    help="SyncBN statistics transport (parallel/peer.py): one-shot xGMI peer kernel or RCCL")
     p.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
@@ -125,11 +127,14 @@ def _syncbn_checks(tr, ctx) -> dict:
     return out
 
 
-def _from_slowest_rank(extra: dict, dt: float, ctx) -> dict:
-    """The diagnostics of the rank whose timed loop took longest (the one the reported time is from)."""
+def _from_slowest_rank(extra: dict, dt: float, ctx, steps: int) -> dict:
+    """The diagnostics of the rank whose timed loop took longest (the one the reported time is from), plus
+    which rank that was and every rank's own ms/step (a straggler GPU or link shows up here)."""
     box = [None] * ctx.world_size
     dist.all_gather_object(box, (dt, extra))
-    return max(box, key=lambda r: r[0])[1]
+    slow = max(range(ctx.world_size), key=lambda r: box[r][0])
+    return {**box[slow][1], "slowest_rank": slow,
+            "rank_ms_per_step": [round(b[0] / steps * 1e3, 3) for b in box]}
 
 
 def _spawn_ranks(a) -> int:
@@ -155,6 +160,10 @@ def main():
         return _spawn_ranks(a)
     if a.device == "cpu":
         a.compute = "torch"  # the HIP kernels need the GPU; the rehearsal checks launch, rendezvous, reporting
+        if a.data == "host":  # the host loader's copy stream and u8 conversion kernel are GPU-only
+            print("[bench] --device cpu: --data host needs a GPU copy stream; rehearsing with --data device",
+                  file=sys.stderr, flush=True)
+            a.data = "device"
     backend = a.dist_backend if a.device == "cuda" else "gloo"
     ctx = init_distributed(device=a.device, backend=backend)
     if ctx.world_size != a.gpus:
@@ -167,7 +176,7 @@ def main():
         "--synthetic", "--model", a.model, "--image-size", str(a.image_size),
         "--batchsize", str(a.batch), "--num-classes", str(a.num_classes),
         "--num-workers", "0", "--synthetic-train-size", "8", "--synthetic-val-size", "8",
-        "--compute", a.compute, "--bucket-mb", str(a.bucket_mb), "--comm-dtype", a.comm_dtype, "--comm-backend", a.comm_backend,
+        "--compute", a.compute, "--bucket-mb", str(a.bucket_mb), "--tail-bucket-mb", str(a.tail_bucket_mb), "--comm-dtype", a.comm_dtype, "--comm-backend", a.comm_backend,
         "--lr", "1e-4", "--dtype", a.dtype, "--syncbn-comm", a.syncbn_comm,
     ] + ([] if sync_bn else ["--no-sync-bn"]))
     if ctx.device.type == "cuda":
@@ -251,7 +260,7 @@ def main():
     t = torch.tensor([dt], dtype=torch.float64, device=ctx.device)
     if ctx.world_size > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        extra = _from_slowest_rank(extra, dt, ctx)
+        extra = _from_slowest_rank(extra, dt, ctx, a.steps)
     dt = float(t.item())
     loss_val = float(last.item())
     if ctx.rank == 0:

@@ -593,8 +593,7 @@ void input_u8(Tensor x, Tensor y, std::vector<double> a, std::vector<double> b, 
     TORCH_CHECK(H % 2 == 0 && W % 2 == 0 && y.numel() == (long long)N * (H / 2) * (W / 2) * 16,
                 "input_u8: the s2d layout needs even H, W and y of N*H/2*W/2*16 elements");
   } else {
-    TORCH_CHECK(((long long)N * H * W) % 4 == 0 && y.numel() == (long long)N * H * W * 8,
-                "input_u8: NHWC8 needs N*H*W % 4 == 0 and y of N*H*W*8 elements");
+    TORCH_CHECK(y.numel() == (long long)N * H * W * 8, "input_u8: NHWC8 needs y of N*H*W*8 elements");
   }
   TORCH_CHECK(y.is_contiguous() || y.is_contiguous(at::MemoryFormat::ChannelsLast), "input_u8: dense y");
   const float f[6] = {(float)a[0], (float)a[1], (float)a[2], (float)b[0], (float)b[1], (float)b[2]};

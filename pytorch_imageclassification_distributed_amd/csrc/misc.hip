@@ -89,10 +89,23 @@ struct Affine3 {
   float a0, a1, a2, b0, b1, b2;
 };
 
-// 4 pixels per lane: 12 input bytes as three dword loads (pixel 4q starts at byte 12q), 4 x 16-B stores
-__global__ void input_u8_nhwc8_kernel(const uint8_t* __restrict__ x, bf16_t* __restrict__ y, long nquad,
+// 4 pixels per lane: 12 input bytes as three dword loads (pixel 4q starts at byte 12q), 4 x 16-B stores;
+// the last npix % 4 pixels (odd 299 x 299 maps, partial batches) by byte loads, one pixel per lane
+__global__ void input_u8_nhwc8_kernel(const uint8_t* __restrict__ x, bf16_t* __restrict__ y, long npix,
                                       Affine3 f) {
-  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < nquad; q += (long)gridDim.x * blockDim.x) {
+  const long nquad = npix >> 2;
+  const long t0 = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (t0 < (npix & 3)) {
+    const long p = nquad * 4 + t0;
+    float v[8];
+    v[0] = x[p * 3] * f.a0 + f.b0;
+    v[1] = x[p * 3 + 1] * f.a1 + f.b1;
+    v[2] = x[p * 3 + 2] * f.a2 + f.b2;
+#pragma unroll
+    for (int k = 3; k < 8; ++k) v[k] = 0.f;
+    *(uint4*)(y + p * 8) = pack8(v);
+  }
+  for (long q = t0; q < nquad; q += (long)gridDim.x * blockDim.x) {
     const uint32_t* src = (const uint32_t*)(x + q * 12);
     const uint32_t w0 = src[0], w1 = src[1], w2 = src[2];
     const uint32_t bytes[3] = {w0, w1, w2};
@@ -286,8 +299,8 @@ int input_u8_launch(const uint8_t* x, bf16_t* y, int N, int H, int W, int s2d, c
     hipLaunchKernelGGL(input_u8_s2d_kernel, dim3(grid_for((long)N * (H / 2) * (W / 2))), dim3(256), 0, s, x, y, N, H,
                        W, f);
   } else {
-    const long nquad = (long)N * H * W / 4;  // host-checked: N * H * W % 4 == 0
-    hipLaunchKernelGGL(input_u8_nhwc8_kernel, dim3(grid_for(nquad)), dim3(256), 0, s, x, y, nquad, f);
+    const long npix = (long)N * H * W;
+    hipLaunchKernelGGL(input_u8_nhwc8_kernel, dim3(grid_for(npix / 4 + 1)), dim3(256), 0, s, x, y, npix, f);
   }
   return (int)hipGetLastError();
 }

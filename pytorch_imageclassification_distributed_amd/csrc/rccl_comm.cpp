@@ -178,7 +178,7 @@ int rccl_group(bool start) {
 // 0 = healthy, else the communicator's asynchronous error code (a dead peer, a network failure)
 int rccl_async_error(int64_t h) {
   ncclComm_t c = comm_of(h);
-  if (!c) return -1;
+  if (!c) return 0;  // closed or unknown handle: nothing left that could fail (teardown is not a fault)
   ncclResult_t e = ncclSuccess;
   const ncclResult_t r = g_api.async_error(c, &e);
   if (r != ncclSuccess) return fail(r);

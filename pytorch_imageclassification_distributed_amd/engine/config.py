@@ -61,6 +61,10 @@ def build_parser() -> argparse.ArgumentParser:
                    help="every N train steps (and at each epoch end) check that all ranks hold bitwise-equal BN "
                         "running statistics and that no SyncBN peer exchange timed out (0: epoch end only)")
     p.add_argument("--bucket-mb", type=float, default=32.0)
+    p.add_argument("--tail-bucket-mb", type=float, default=4.0,
+                   help="cut the last gradient bucket (the last gradients of backward: stem + first stage) into "
+                        "pieces of at most this many MiB, so only the final piece's all-reduce sits after backward "
+                        "(0: one bucket)")
     p.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--comm-backend", default="pg", choices=["pg", "rccl"],
                    help="gradient buckets: torch.distributed's ProcessGroupNCCL (pg) or our C++ RCCL communicator "

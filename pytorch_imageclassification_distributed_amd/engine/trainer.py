@@ -188,7 +188,8 @@ class Trainer:
                     backend = "pg"
                 self.comm_backend = backend
                 self.reducer = GradReducer(model, bucket_cap_mb=a.bucket_mb, comm_dtype=comm, comm=backend,
-                                           timeout_s=60.0 * getattr(a, "timeout_min", 10.0))
+                                           timeout_s=60.0 * getattr(a, "timeout_min", 10.0),
+                                           tail_bucket_mb=getattr(a, "tail_bucket_mb", 4.0))
                 self.arena = self.reducer.arena
             elif self.hip:
                 params = [p for p in model.parameters() if p.requires_grad]

@@ -127,6 +127,12 @@ XA_COUNT = [0]  # BN backwards handed to their producer conv (tests / diagnostic
 XA_MAX_REP = int(os.environ.get("IMGCLS_XA_MAX_REP", "2"))
 XA_NARROW_OFF = os.environ.get("IMGCLS_XA_NARROW_OFF", "0") == "1"
 XF_MAX_REP = int(os.environ.get("IMGCLS_XF_MAX_REP", "2"))
+# XA with the dY written once by the data gradient (its first column tile stores the dY it formed in LDS):
+# the weight gradient then reads dY plainly instead of re-forming it from dz and y in every column tile
+# (the fused wgrads ran VALU-bound at 10-20 % MFMA busy).  Same bytes (one dY write on the
+# compute stream against one fewer tensor read on the side stream), no replicated transform.
+XA_OUT = os.environ.get("IMGCLS_XA_OUT", "0") == "1"
+XA_OUT_COUNT = [0]
 
 
 def _rep(taps: int, other: int) -> int:
@@ -153,6 +159,12 @@ class XaLink:
         out = (self.y, self.coef)
         self.dz = self.y = self.coef = None
         return out
+
+
+def _xa_out_ok(g) -> bool:
+    """Every dY element passes through the data gradient's A operand exactly once in a tile of the first
+    column: a 1x1 conv without padding (stride 1, or the single non-empty phase of stride 2)."""
+    return g.kh == 1 and g.kw == 1 and g.pt == 0 and g.pl == 0 and g.Cx == g.Ci
 
 
 def xa_eligible(x, conv) -> bool:
@@ -266,7 +278,13 @@ class ConvFn(torch.autograd.Function):
                 dx, dw_fused = conv_fused_bwd_raw(dy, x, w, g, xa, addend=addend, link=link)
             else:
                 dw_fused = None
-                dx = conv_dgrad_raw(dy, w, g, addend=addend, link=link, xa=xa)
+                if xa is not None and XA_OUT and ctx.needs_input_grad[1] and _xa_out_ok(g):
+                    xo = torch.empty_like(dy)
+                    dx = conv_dgrad_raw(dy, w, g, addend=addend, link=link, xa=xa, xa_out=xo)
+                    dy, xa = xo, None  # the weight gradient reads the materialised dY
+                    XA_OUT_COUNT[0] += 1
+                else:
+                    dx = conv_dgrad_raw(dy, w, g, addend=addend, link=link, xa=xa)
             if link is not None:
                 link.done = True
                 if link.group is not None:
@@ -321,7 +339,9 @@ def input_from_u8(u8, spec, mean, std):
     (Inception transform_input) folded into ``u * a + b``, written as bf16 either in the 16-channel
     space-to-depth stem layout (``spec[0]``, ResNet) or NHWC padded to 8 channels.  Replaces
     normalize_u8 (fp32 NCHW) + prepare_input / prepare_input_s2d (a second pass over that fp32 tensor).
-    The result carries a marker so prepare_input / the stem pass it through unchanged."""
+    The result carries a marker so prepare_input / the stem pass it through unchanged.  Odd image sizes
+    take the NHWC8 form even for an s2d stem (the stem then runs as a plain 7x7 implicit GEMM), and the
+    NHWC8 kernel handles any pixel count (299 x 299 maps, partial last batches)."""
     s2d, sc, sh = spec
     n, h, w, _ = u8.shape
     a = [1.0 / (255.0 * std[c]) for c in range(3)]
@@ -329,7 +349,7 @@ def input_from_u8(u8, spec, mean, std):
     if sc is not None:
         a = [a[c] * sc[c] for c in range(3)]
         b = [b[c] * sc[c] + sh[c] for c in range(3)]
-    if s2d:
+    if s2d and h % 2 == 0 and w % 2 == 0:
         y = _empty_cl(n, 16, h // 2, w // 2, u8.device)
         C.input_u8(u8, y, a, b, 1)
         y._imgcls_s2d = (h, w)
@@ -914,7 +934,7 @@ _OWNED = (
     'BNActFn', 'BNActPoolFn', 'BwdLink', 'ConvBiasFn', 'ConvFn', 'DW_LINK', 'DenseConvFn', 'DwConvFn',
     'FUSE_XA', 'FUSE_XF', 'GradSlot', 'PEER_BN_MAX_C', 'POOL_CONV_SWAP', 'RELU_MASK', 'STEM_DIRECT',
     'STEM_POOL_FUSE', 'STEM_S2D', 'SYNCBN_EARLY_COUNT', 'StemS2dFn', 'XA_COUNT', 'XA_MAX_REP', 'XA_NARROW_OFF',
-    'XF_COUNT', 'XF_MAX_REP', 'XaLink', 'XfHold', 'XfMaterializeFn', '_S2D_INDEX', '_as_pixel_rows',
+    'XF_COUNT', 'XF_MAX_REP', 'XA_OUT', 'XA_OUT_COUNT', '_xa_out_ok', 'XaLink', 'XfHold', 'XfMaterializeFn', '_S2D_INDEX', '_as_pixel_rows',
     '_bn_bwd_k', '_bn_coef', '_dense_geom', '_rep', '_s2d_geom', '_s2d_index', '_syncbn_bwd_start', 'conv',
     'conv_bn_act', 'conv_bn_act_pool', 'dense_conv_eligible', 'input_from_u8', 'materialize_deferred',
     'pool_conv_bn_act', 'stem_s2d_conv', 'stem_s2d_eligible', 'xa_eligible', 'xf_eligible',

@@ -151,15 +151,19 @@ def load_tuning(path: str) -> int:
         except (ValueError, SyntaxError, TypeError):
             continue
         fp8 = bool(k[10]) if len(k) > 10 else False
+        # a family switched off by its flag is not served from the db either, and the deep kernel's
+        # diagnostic variants (var & 6: wrong results by design) and untuned ones (var & 256) never are
         if v[2] >= PW_BASE:
-            ok = not fp8 and v[2] - PW_BASE < len(conv_pw_cfgs()) and len(v) == 3
+            ok = PW_CONV and not fp8 and v[2] - PW_BASE < len(conv_pw_cfgs()) and len(v) == 3
         elif v[2] >= DEEP_BASE:
-            ok = not fp8 and v[2] - DEEP_BASE < len(conv_deep_cfgs()) and len(v) == 3
+            ok = (DEEP_CONV and not fp8 and v[2] - DEEP_BASE < len(conv_deep_cfgs()) and len(v) == 3
+                  and not conv_deep_cfgs()[v[2] - DEEP_BASE][4] & (6 | 256))
         elif v[2] >= HALO_BASE:
-            ok = not fp8 and v[2] - HALO_BASE < len(conv_halo_cfgs()) and len(v) == 3
+            ok = HALO_CONV and not fp8 and v[2] - HALO_BASE < len(conv_halo_cfgs()) and len(v) == 3
+        elif v[2] >= DIRECT_BASE:
+            ok = DIRECT_CONV and v[2] - DIRECT_BASE in DIRECT_CFGS and len(v) == 3
         else:
-            ok = (v[2] - DIRECT_BASE in DIRECT_CFGS if v[2] >= DIRECT_BASE else
-                  v[2] < (nfp8 if fp8 else ncfg)) and len(v) == 3
+            ok = v[2] < (nfp8 if fp8 else ncfg) and len(v) == 3
         if ok and k not in _STAGES_TUNED:
             _STAGES_TUNED[k] = v
             n += 1
@@ -168,7 +172,7 @@ def load_tuning(path: str) -> int:
             k, v = ast.literal_eval(ks), tuple(int(x) for x in v)
         except (ValueError, SyntaxError, TypeError):
             continue
-        if len(v) == 2 and 1 <= v[1] <= 15 and v[0] > 0 and k not in _WGRAD_TUNED:
+        if len(v) == 2 and 1 <= v[1] <= 15 and v[0] > 0 and k not in _WGRAD_TUNED and (WGRAD_DEEP or v[1] < 13):
             _WGRAD_TUNED[k] = v
             n += 1
     return n
@@ -187,7 +191,7 @@ def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(
     BN backward's elementwise map on its operand loads (1x1 stride-1 geometry; ``XaLink``).
     ``xf`` = (coef, act): A holds a BN's input y and the kernel applies act(bn(y)) on its operand loads
     (``XfHold``)."""
-    xa3 = (xa[0], xa[1], None) if xa is not None else (None, None, None)
+    xa3 = (xa[0], xa[1], xa[2] if len(xa) > 2 else None) if xa is not None else (None, None, None)
     xf2 = (xf[0], xf[1]) if xf is not None else (None, 0)
     fused = xa is not None or xf is not None
     if DIRECT_FORCE is not None and not fused and \
@@ -554,13 +558,15 @@ def conv_fused_bwd_raw(dz, x, w_param, g: ConvGeom, xa, addend=None, link=None):
     return dx, dw
 
 
-def conv_dgrad_raw(dy, w_param, g: ConvGeom, addend=None, link=None, xa=None):
+def conv_dgrad_raw(dy, w_param, g: ConvGeom, addend=None, link=None, xa=None, xa_out=None):
     """dX = conv_transpose(dY, W) [+ addend], one MFMA GEMM per sub-pixel phase.
 
     With ``link`` (the producer BN of the conv input) the epilogue instead emits
     dz = act'(z) * dX and the producer's BN-backward partial sums (fused reduce).
     With ``xa`` = (y, coef) ``dy`` is the consuming BN's pre-elementwise gradient dz and the kernel
-    forms dY = coef0*dz + coef1*y + coef2 on its A-operand loads (1x1 convs, ``XaLink``)."""
+    forms dY = coef0*dz + coef1*y + coef2 on its A-operand loads (1x1 convs, ``XaLink``); with ``xa_out``
+    (a tensor shaped like dy) the first column tile also stores that dY, so the weight gradient can read it
+    plainly (``XA_OUT``)."""
     dev = dy.device
     bwd = (None, None, None, None, 0, 1)
     mask = None
@@ -577,7 +583,8 @@ def conv_dgrad_raw(dy, w_param, g: ConvGeom, addend=None, link=None, xa=None):
         geo = (g.N * gh * gw, g.Ci, len(tb) * g.Co, g.Co, gh, gw, g.OH, g.OW, 1, g.T * g.Co, g.H, g.W, g.sh,
                ph, pw, g.Ci, 0)
         _conv_gemm(dy, wt, dx, None, None, geo, dh, dw, tb, ws(dev).zero, addend, bwd,
-                   xa=xa if len(tb) else None, mask=mask)
+                   xa=(xa if xa_out is None else (xa[0], xa[1], xa_out)) if (xa is not None and len(tb)) else None,
+                   mask=mask)
     return dx
 
 

@@ -229,8 +229,9 @@ def check_syncbn_consistency(module, group=None, where: str = "") -> None:
     payloads in rank order (peer path) or receives the same all-reduce result (RCCL).  A transport fault - a
     stale or torn slot - shows up here as a mismatch, and the run stops instead of training on diverged
     statistics.  One flat pass: the running buffers are concatenated once and reduced to a position-weighted
-    checksum pair (a swapped or shifted buffer changes it too), then one 4-value all-reduce.  Non-finite
-    running statistics (a diverged run) are reported as such, not as a transport fault."""
+    checksum pair (a swapped or shifted buffer changes it too), then one 6-value all-reduce.  Non-finite
+    running statistics on every rank (a diverged run) are reported as divergence; on some ranks only, as the
+    transport mismatch they are."""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return
     bufs = [b for n, b in module.named_buffers() if "running_" in n]
@@ -241,11 +242,16 @@ def check_syncbn_consistency(module, group=None, where: str = "") -> None:
     s = torch.stack([flat.sum(), (flat * w).sum()])
     fin = torch.isfinite(s).all()
     s = torch.where(fin, s, torch.zeros_like(s))
-    both = torch.cat([s, -s, (~fin).double().reshape(1)])
+    nf = (~fin).double().reshape(1)
+    both = torch.cat([s, -s, nf, -nf])  # MAX of x and of -x: the max and the min over ranks in one reduce
     dist.all_reduce(both, op=dist.ReduceOp.MAX, group=group)
-    if both[4].item() > 0:
-        raise SyncBNMismatchError(f"SyncBN running statistics are not finite on some rank{' (' + where + ')' if where else ''}"
+    any_nf, all_nf = both[4].item() > 0, -both[5].item() > 0
+    if all_nf:
+        raise SyncBNMismatchError(f"SyncBN running statistics are not finite on every rank{' (' + where + ')' if where else ''}"
                                   ": the run diverged (not a transport fault)")
+    if any_nf:  # identical inputs on every rank cannot leave only some of them non-finite: a stale / torn slot
+        raise SyncBNMismatchError(f"SyncBN running statistics are not finite on some ranks only{' (' + where + ')' if where else ''}"
+                                  ": the ranks' statistics differ (transport fault)")
     if not torch.equal(both[:2], -both[2:4]):
         raise SyncBNMismatchError(f"SyncBN running statistics differ between ranks{' (' + where + ')' if where else ''}:"
                                   f" checksum max {both[:2].tolist()} vs min {(-both[2:4]).tolist()}")

@@ -95,7 +95,8 @@ class RcclComm:
             raise RuntimeError(f"RCCL communicator error {e}: {self.C.rccl_last_error()}")
 
     def async_error(self) -> int:
-        return int(self.C.rccl_async_error(self.handle)) if getattr(self, "handle", 0) else 0
+        h = getattr(self, "handle", 0)  # read once: close() may run between a check and the call
+        return int(self.C.rccl_async_error(h)) if h else 0
 
     def close(self, abort: bool = False) -> None:
         if getattr(self, "handle", 0):
@@ -106,8 +107,15 @@ class RcclComm:
 
 
 def close_all(abort: bool = False) -> None:
+    """Stop every live watchdog first (a watchdog polling a communicator that is being destroyed would
+    read a teardown as a fault and exit non-zero), then close every communicator."""
+    for w in list(_WATCHDOGS):
+        w.stop()
     for c in list(_LIVE):
         c.close(abort)
+
+
+_WATCHDOGS: "list[CommWatchdog]" = []  # running watchdogs (close_all stops them before any communicator goes)
 
 
 class CommWatchdog:
@@ -130,6 +138,7 @@ class CommWatchdog:
         self._stop = threading.Event()
         self.fired = None
         self._t = threading.Thread(target=self._run, name="imgcls-comm-watchdog", daemon=True)
+        _WATCHDOGS.append(self)
         self._t.start()
 
     def arm(self, done) -> None:
@@ -157,7 +166,7 @@ class CommWatchdog:
     def _run(self) -> None:
         while not self._stop.wait(self.interval):
             msg = self.check_once()
-            if msg is not None:
+            if msg is not None and not self._stop.is_set():  # stopped meanwhile: an orderly teardown
                 self.fired = msg
                 try:
                     self.abort()
@@ -167,7 +176,10 @@ class CommWatchdog:
 
     def stop(self) -> None:
         self._stop.set()
-        self._t.join(timeout=5)
+        if self._t is not threading.current_thread():
+            self._t.join(timeout=5)
+        if self in _WATCHDOGS:
+            _WATCHDOGS.remove(self)
 
 
 def rccl_version() -> int:

@@ -26,6 +26,10 @@ MI355X design:
   ~153 GB/s; RCCL's ring/tree algorithms saturate them from a few MiB, and
   fewer, larger buckets mean fewer ~10-20 us collective launches.  The first
   bucket is kept small (1 MiB) so communication starts early in backward.
+* the LAST bucket is cut into pieces of at most ``tail_bucket_mb`` (4 MiB): its gradients (ResNet's layer1
+  and stem, ~28 MiB) are the last ones backward produces, so a whole-bucket collective could only start
+  after the weight-gradient side stream drained and would sit entirely after backward; pieces launch as
+  their own gradients land, and only the final few MiB stay exposed (``ms_comm_wait`` in bench.py's line).
 * optional bf16 gradient transport (``comm_dtype=torch.bfloat16``) halves the
   xGMI bytes.
 * ``comm="rccl"``: the buckets go through our own C++ RCCL communicator
@@ -77,7 +81,7 @@ class GradReducer:
     def __init__(self, module: nn.Module, group=None, bucket_cap_mb: float = 32.0,
                  first_bucket_mb: float = 1.0, broadcast: bool = True,
                  rebuild_buckets: bool = True, comm_dtype: torch.dtype | None = None, comm: str = "pg",
-                 force_collectives: bool = False, timeout_s: float = 600.0):
+                 force_collectives: bool = False, timeout_s: float = 600.0, tail_bucket_mb: float = 4.0):
         self.module = module
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -85,6 +89,7 @@ class GradReducer:
         self.index = {id(p): i for i, p in enumerate(self.params)}
         self.bucket_cap = int(bucket_cap_mb * 2**20) // 4
         self.first_cap = int(first_bucket_mb * 2**20) // 4
+        self.tail_cap = int(tail_bucket_mb * 2**20) // 4 if tail_bucket_mb > 0 else 0
         self.comm_dtype = comm_dtype
         self._rebuild_pending = rebuild_buckets and self.world > 1
         self._ready_order: list[int] = []
@@ -141,12 +146,28 @@ class GradReducer:
             cur.append(i)
         if cur:
             buckets.append((cur_start, self.arena.flat.numel(), cur))
+        if self.tail_cap and len(buckets) > 1 and buckets[-1][1] - buckets[-1][0] > self.tail_cap:
+            buckets = buckets[:-1] + self._split(buckets[-1], offsets)
         self.buckets = buckets
         self.bucket_of = [0] * len(self.params)
         for b, (_s, _e, idx) in enumerate(buckets):
             for i in idx:
                 self.bucket_of[i] = b
         self._reset_counts()
+
+    def _split(self, bucket, offsets) -> list:
+        """Cut the last bucket into pieces of at most ``tail_cap`` elements on parameter boundaries (a single
+        larger parameter keeps a piece of its own), in the same ready order."""
+        start, end, idx = bucket
+        out, cur, cur_start = [], [], start
+        for i in idx:
+            off = offsets[i]
+            if cur and off - cur_start + self.params[i].numel() > self.tail_cap:
+                out.append((cur_start, off, cur))
+                cur, cur_start = [], off
+            cur.append(i)
+        out.append((cur_start, end, cur))
+        return out
 
     @property
     def flat(self) -> torch.Tensor:

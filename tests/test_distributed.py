@@ -86,6 +86,29 @@ def test_grad_reducer_matches_single_process():
     _run(_w_ddp)
 
 
+def test_resnet50_bucket_plan_bounds_the_tail():
+    """The ResNet-50 bucket plan (VERDICT r4 next #5a): 1 MiB first bucket, <= 32 MiB buckets, and the last
+    bucket - layer1 + stem, the gradients backward produces last, ~28 MiB as one bucket - cut into <= 4 MiB
+    pieces, so only the final piece's all-reduce is left after the weight-gradient side stream drains."""
+    from pytorch_imageclassification_distributed_amd.models import Classifier
+    from pytorch_imageclassification_distributed_amd.parallel import GradReducer
+    m = Classifier("resnet50", 7)
+    whole = GradReducer(m, bucket_cap_mb=32.0, tail_bucket_mb=0)
+    cut = GradReducer(m, bucket_cap_mb=32.0, tail_bucket_mb=4.0)
+    a, b = whole.bucket_sizes_mb(), cut.bucket_sizes_mb()
+    assert a[0] <= 1.0 and all(v <= 32.0 for v in a) and a[-1] > 20.0  # the unbounded tail bucket
+    assert b[:len(a) - 1] == a[:-1]  # only the last bucket changes
+    tail = b[len(a) - 1:]
+    assert len(tail) >= 6 and all(v <= 4.0 for v in tail) and abs(sum(tail) - a[-1]) < 1e-6
+    # contiguous cover of the flat buffer, in ready order; the stem conv's gradient is in the very last piece
+    assert cut.buckets[0][0] == 0 and cut.buckets[-1][1] == cut.flat.numel()
+    assert all(x[1] == y[0] for x, y in zip(cut.buckets, cut.buckets[1:]))
+    stem = cut.index[id(m.encoder.conv1.weight)]
+    assert cut.bucket_of[stem] == len(cut.buckets) - 1
+    for r in (whole, cut):
+        r.remove_hooks()
+
+
 # ---------------------------------------------------------------------------
 def _w_syncbn(rank, world, port):
     _setup(rank, world, port)
@@ -328,6 +351,23 @@ def test_bench_gpus_flag_launches_the_ranks():
     assert out["steps"] == 2 and out["value"] > 0 and "not a benchmark" in out["metric"]
 
 
+def test_bench_eight_rank_rehearsal():
+    """The driver's N = 8 launch shape, rehearsed on the CPU over gloo: ``bench.py --gpus 8`` starts 8 ranks,
+    reports n_gpus 8 / dp8 / global batch 8 x per-GPU, the time of the slowest rank (its index and every
+    rank's ms/step are in the line) and SyncBN on (reference semantics at N > 1); ``--data host`` is
+    rehearsed as ``--data device`` (the host loader is GPU-only)."""
+    rc, out, err = _bench(["--gpus", "8", "--device", "cpu", "--model", "resnet18", "--image-size", "32",
+                           "--batch", "2", "--steps", "2", "--warmup", "1", "--data", "host"], timeout=600)
+    assert rc == 0, err[-3000:]
+    assert out["n_gpus"] == 8 and out["config"]["parallelism"] == "dp8" and out["config"]["global_batch"] == 16
+    assert out["config"]["sync_bn"] is True and "not a benchmark" in out["metric"]
+    ranks = out["rank_ms_per_step"]
+    assert len(ranks) == 8 and 0 <= out["slowest_rank"] < 8
+    assert ranks[out["slowest_rank"]] == max(ranks)
+    assert abs(out["ms_per_step"] - max(ranks)) <= 0.01 * max(ranks) + 0.01  # the reported time is the max
+    assert "rehearsing with --data device" in err
+
+
 def test_bench_refuses_a_world_size_mismatch():
     """A single rank asked for ``--gpus 2`` under a launcher-provided WORLD_SIZE=1 exits non-zero without a
     (mislabelled) JSON line."""
@@ -434,6 +474,23 @@ def test_comm_watchdog_ends_a_hung_collective():
     assert "aborted" in r.stdout and "not reached" not in r.stdout and "have not completed" in r.stderr
 
 
+def test_close_all_stops_watchdogs_before_teardown():
+    """parallel.dist.destroy() -> rccl.close_all() stops every live watchdog before any communicator closes, so a
+    poll that sees the closed communicator (formerly -1 from the native side) never ends a clean run non-zero."""
+    import time
+
+    from pytorch_imageclassification_distributed_amd.parallel import rccl as R
+    err, calls = [0], []
+    wd = R.CommWatchdog(lambda: err[0], lambda: calls.append("abort"), timeout=60, interval=0.01,
+                        on_fatal=lambda m: calls.append(m))
+    assert wd in R._WATCHDOGS
+    R.close_all()
+    assert wd not in R._WATCHDOGS and not wd._t.is_alive()
+    err[0] = -1
+    time.sleep(0.1)
+    assert calls == [] and wd.fired is None
+
+
 def test_grad_reducer_wires_the_watchdog(monkeypatch):
     """GradReducer(comm='rccl') arms the watchdog with one completion event per step and check() raises on
     an async error (a stub communicator stands in for RcclComm: RCCL needs GPUs)."""
@@ -484,13 +541,16 @@ def _w_syncbn_guard(rank, world, port):
     if rank == 1:
         m[1].running_mean[2] -= 1e-6
         m[0].running_var[1] = float("nan")
-    with pytest.raises(SyncBNMismatchError, match="not finite"):
-        check_syncbn_consistency(m)
+    with pytest.raises(SyncBNMismatchError, match="some ranks only.*transport fault"):
+        check_syncbn_consistency(m)  # one rank non-finite: the statistics differ (a stale / torn slot)
+    m[0].running_var[1] = float("nan")
+    with pytest.raises(SyncBNMismatchError, match="every rank.*diverged"):
+        check_syncbn_consistency(m)  # every rank non-finite: divergence
 
 
 def test_syncbn_guard_flat_checksum_and_nonfinite():
     """The SyncBN guard (one flat checksum + one all-reduce): a one-ulp difference on one rank is a mismatch;
-    a NaN running statistic is reported as divergence, consistently on every rank, not as a transport fault."""
+    a NaN running statistic on every rank is divergence; on one rank only, a transport mismatch."""
     _run(_w_syncbn_guard)
 
 

@@ -74,8 +74,11 @@ def _unit_worker(rank, world, port):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_peer_allreduce_exact(world):
+    """Exact rank-ordered sums, both buffer parities (sync and side-stream calls alternate), 64-call bursts;
+    world 8 is the driver's node size (8 processes sharing this one GPU: the flag / parity protocol and the
+    bounded spin at the world size they will first meet)."""
     mp.spawn(_unit_worker, args=(world, _port()), nprocs=world, join=True)
 
 

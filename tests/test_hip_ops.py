@@ -1190,7 +1190,7 @@ def test_se_gate_fused_bn_backward(n, c, hw):
 # ---------------------------------------------------------------------------------------------------------
 # BN-backward elementwise fused into the producer 1x1 conv's dgrad / wgrad (ops/hip.py XaLink, csrc XA)
 # ---------------------------------------------------------------------------------------------------------
-def _xa_block(hip, n, cin, hw, cmid, stride, act, use_res, xa_on, cfg=None, wstages=None, k=1):
+def _xa_block(hip, n, cin, hw, cmid, stride, act, use_res, xa_on, cfg=None, wstages=None, k=1, xa_out=False):
     """x -> kxk conv (stride) -> BN -> act [+ res] -> 1x1 conv -> BN: the first BN's backward is linked to
     the second conv's dgrad (dz arrives fused), then handed to the first conv (XA).  Returns outputs and
     gradients, and how many BN backwards took the fused path."""
@@ -1207,8 +1207,9 @@ def _xa_block(hip, n, cin, hw, cmid, stride, act, use_res, xa_on, cfg=None, wsta
     x = bf(torch.randn(n, cin, hw, hw, device=DEV)).to(torch.bfloat16).contiguous(memory_format=CL)
     oh = (hw + 2 * (k // 2) - k) // stride + 1
     res = bf(torch.randn(n, cmid, oh, oh, device=DEV)).to(torch.bfloat16).contiguous(memory_format=CL)
-    keep = hip.FUSE_XA, hip.CONV_FORCE_CFG, hip.WGRAD_STAGES, hip.XA_MAX_REP
+    keep = hip.FUSE_XA, hip.CONV_FORCE_CFG, hip.WGRAD_STAGES, hip.XA_MAX_REP, hip.XA_OUT
     hip.FUSE_XA, hip.XA_MAX_REP = xa_on, 10 ** 6  # every eligible geometry, whatever the cost gate says
+    hip.XA_OUT = xa_out
     if cfg is not None:
         hip.CONV_FORCE_CFG = (0, 0, cfg)
     if wstages is not None:
@@ -1226,7 +1227,7 @@ def _xa_block(hip, n, cin, hw, cmid, stride, act, use_res, xa_on, cfg=None, wsta
                  c2.weight.grad.float()] + ([rb.grad.float()] if use_res else [])
         return out.float(), grads, hip.XA_COUNT[0] - n0
     finally:
-        hip.FUSE_XA, hip.CONV_FORCE_CFG, hip.WGRAD_STAGES, hip.XA_MAX_REP = keep
+        hip.FUSE_XA, hip.CONV_FORCE_CFG, hip.WGRAD_STAGES, hip.XA_MAX_REP, hip.XA_OUT = keep
 
 
 @pytest.mark.parametrize("case", [
@@ -1247,6 +1248,27 @@ def test_bn_backward_fused_into_producer_conv(case):
     o0, g0, k0 = _xa_block(hip, n, cin, hw, cmid, stride, act, use_res, False, k=k)
     o1, g1, k1 = _xa_block(hip, n, cin, hw, cmid, stride, act, use_res, True, k=k)
     assert k0 == 0 and k1 >= 1, (k0, k1)
+    assert torch.equal(o0, o1)
+    for a_, b_ in zip(g1, g0):
+        assert rel_err(a_, b_) < 2e-2, rel_err(a_, b_)
+        assert mean_err(a_, b_) < 5e-3, mean_err(a_, b_)
+
+
+@pytest.mark.parametrize("case", [
+    (4, 64, 28, 256, 1, "relu", True),     # bn3-like: wide output, residual + ReLU
+    (4, 256, 28, 64, 1, "relu", False),    # bn1-like: narrow output, 4 dgrad column tiles (only tile 0 stores)
+    (4, 128, 28, 128, 2, None, False),     # stride 2: dY stored from the single non-empty phase
+    (2, 512, 7, 512, 1, "relu", True),     # partial row tiles
+    (3, 64, 15, 192, 1, "silu", False),    # odd pixel count
+])
+def test_bn_backward_fused_dy_written_once(case):
+    """XA_OUT: the data gradient stores the dY it forms (first column tile) and the weight gradient reads it
+    plainly - same outputs and gradients as the in-kernel transform in both GEMMs and as the unfused path."""
+    hip = _hip()
+    n0 = hip.XA_OUT_COUNT[0]
+    o0, g0, _ = _xa_block(hip, *case, xa_on=False)
+    o1, g1, k1 = _xa_block(hip, *case, xa_on=True, xa_out=True)
+    assert k1 >= 1 and hip.XA_OUT_COUNT[0] > n0
     assert torch.equal(o0, o1)
     for a_, b_ in zip(g1, g0):
         assert rel_err(a_, b_) < 2e-2, rel_err(a_, b_)
@@ -1469,8 +1491,9 @@ def test_bn_statistics_large_mean(path):
     # output: ~1e-5 either way, which is that rounding, not the summation)
 
 
+@pytest.mark.parametrize("shape", [(3, 38, 22), (1, 299, 299), (5, 37, 21)])
 @pytest.mark.parametrize("s2d,affine", [(False, None), (False, "inception"), (True, None)])
-def test_input_u8_one_pass(s2d, affine):
+def test_input_u8_one_pass(s2d, affine, shape):
     """input_from_u8 (one kernel: uint8 NHWC -> bf16 model input) against the reference normalisation
     (data/folder.py normalize = reference dp/loader.py:86-91) in fp32, then the model's affine (Inception
     transform_input) and the layout the old two-pass path produced (prepare_input / prepare_input_s2d)."""
@@ -1480,7 +1503,7 @@ def test_input_u8_one_pass(s2d, affine):
     from pytorch_imageclassification_distributed_amd.models.inception import Inception3
     hip = _hip()
     torch.manual_seed(0)
-    n, h, w = 3, 38, 22
+    n, h, w = shape  # odd pixel counts (Inception's 299 x 299, partial batches) and odd sizes for the s2d stem
     u8 = torch.randint(0, 256, (n, h, w, 3), dtype=torch.uint8)
     ref = torch.from_numpy(np.stack([normalize(u8[i].numpy().astype(np.float32)) for i in range(n)]))  # NHWC fp32
     ref = ref.permute(0, 3, 1, 2).contiguous()  # NCHW
@@ -1489,7 +1512,7 @@ def test_input_u8_one_pass(s2d, affine):
         sc, sh = Inception3.TRANSFORM_SCALE, Inception3.TRANSFORM_SHIFT
         ref = ref * torch.tensor(sc).view(1, 3, 1, 1) + torch.tensor(sh).view(1, 3, 1, 1)
     y = hip.input_from_u8(u8.to(DEV), (s2d, sc, sh), IMAGENET_MEAN, IMAGENET_STD)
-    if s2d:
+    if s2d and h % 2 == 0 and w % 2 == 0:
         assert y._imgcls_s2d == (h, w) and tuple(y.shape) == (n, 16, h // 2, w // 2)
         want = torch.empty_like(y)
         hip.C.prepare_input_s2d(ref.to(DEV), want, n, h, w)

@@ -75,3 +75,25 @@ def test_round_trip_every_kernel_family(hip, tmp_path):
     hip._STAGES_TUNED.clear()
     assert hip.load_tuning(path) == len(cfgs)
     assert sorted(hip._STAGES_TUNED.values()) == sorted(cfgs)
+
+
+def test_diagnostic_and_disabled_families_rejected(hip, tmp_path, monkeypatch):
+    """A stale or hand-edited db cannot select the deep kernel's diagnostic variants (var & 6: wrong results
+    by design) or its untuned 32x32 form (var & 256), and a family switched off by its flag (IMGCLS_DEEP=0,
+    IMGCLS_PW=0, ...) is not served from the db either - the same filters the tuner applies."""
+    base = ((1024, 64, 64, 64, 8, 8, 8, 8, 1, 64, 8, 8, 1, 0, 0, 64, 0), 64, (0,), (0,), False, False, False,
+            False, False, 0, False, True)
+    deep = hip.conv_deep_cfgs()
+    bad = [i for i, c in enumerate(deep) if c[4] & (6 | 256)]
+    good = [i for i, c in enumerate(deep) if not c[4] & (6 | 256)]
+    assert bad and good
+    db = {"conv": [[repr(base[:1] + (16 * (j + 1),) + base[2:]), [0, 0, hip.DEEP_BASE + i]]
+                   for j, i in enumerate(bad + good[:1])], "wgrad": []}
+    path = tmp_path / "db.json"
+    path.write_text(json.dumps(db))
+    assert hip.load_tuning(str(path)) == 1
+    assert list(hip._STAGES_TUNED.values()) == [(0, 0, hip.DEEP_BASE + good[0])]
+    hip._STAGES_TUNED.clear()
+    from pytorch_imageclassification_distributed_amd.ops._hip import gemm
+    monkeypatch.setattr(gemm, "DEEP_CONV", False)
+    assert hip.load_tuning(str(path)) == 0
