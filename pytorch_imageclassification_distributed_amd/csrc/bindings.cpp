@@ -119,12 +119,12 @@ int peer_free(void*);
 int peer_ipc_handle(void*, char*);
 int peer_ipc_open(const char*, void**);
 int peer_ipc_close(void*);
-int peer_allreduce_f64_launch(const double*, double*, int, const unsigned long long*, int, int, unsigned long long,
+int peer_allreduce_f64_launch(const double*, double*, int, const unsigned long long*, int, int, unsigned long long*,
                               unsigned long long, int*, hipStream_t);
 int peer_bn_max_channels();
 int peer_bn_launch(bool, float*, int, int, double, const float*, const float*, float*, float*, long long*, float, float,
                    float*, float*, float*, double*, const float*, const unsigned long long*, int, int,
-                   unsigned long long, unsigned long long, int*, hipStream_t);
+                   unsigned long long*, unsigned long long, int*, hipStream_t);
 
 namespace {
 
@@ -796,6 +796,9 @@ class PeerComm {
     check(peer_alloc(&buf_), "peer_alloc");
     check((int)hipMalloc((void**)&err_, sizeof(int)), "peer err word");
     check((int)hipMemset(err_, 0, sizeof(int)), "peer err word");
+    // [0] call sequence number, [1] low word: the launch's block ticket (peer.hip call_seq / call_done)
+    check((int)hipMalloc((void**)&ctl_, 2 * sizeof(unsigned long long)), "peer seq word");
+    check((int)hipMemset(ctl_, 0, 2 * sizeof(unsigned long long)), "peer seq word");
     int dev = 0;
     check((int)hipGetDevice(&dev), "hipGetDevice");
     check((int)hipDeviceGetAttribute(&khz_, hipDeviceAttributeWallClockRate, dev), "wall clock rate");
@@ -835,7 +838,7 @@ class PeerComm {
     for (int q = 0; q < world_; ++q) TORCH_CHECK(bases_[q] != 0ull, "PeerComm: peers not opened");
     ++seq_;
     check(peer_allreduce_f64_launch(ptr<double>(in), ptr<double>(out), (int)in.numel(), bases_.data(), rank_, world_,
-                                    seq_, timeout_ticks_, err_, cur()),
+                                    ctl_, timeout_ticks_, err_, cur()),
           "peer_allreduce_f64");
   }
 
@@ -872,10 +875,19 @@ class PeerComm {
       if (p) { peer_ipc_close(p); p = nullptr; }
     if (buf_) { peer_free(buf_); buf_ = nullptr; }
     if (err_) { hipFree(err_); err_ = nullptr; }
+    if (ctl_) { hipFree(ctl_); ctl_ = nullptr; }
     for (auto& b : bases_) b = 0ull;
   }
 
+  // calls launched by this host (eager or captured; a replayed graph advances only the device counter)
   unsigned long long seq() const { return seq_; }
+
+  // the device call counter (syncs): eager calls + graph replays
+  unsigned long long device_seq() {
+    unsigned long long v = 0;
+    check((int)hipMemcpy(&v, ctl_, sizeof(v), hipMemcpyDeviceToHost), "peer seq read");
+    return v;
+  }
 
  private:
   void launch_bn(bool fwd, Tensor& part, int G, int C, double count, const float* gamma, const float* beta,
@@ -885,7 +897,7 @@ class PeerComm {
     for (int q = 0; q < world_; ++q) TORCH_CHECK(bases_[q] != 0ull, "PeerComm: peers not opened");
     ++seq_;
     check(peer_bn_launch(fwd, ptr<float>(part), G, C, count, gamma, beta, rmean, rvar, nbt, momentum, eps, out, dgamma,
-                         dbeta, count_io, shift, bases_.data(), rank_, world_, seq_, timeout_ticks_, err_, cur()),
+                         dbeta, count_io, shift, bases_.data(), rank_, world_, ctl_, timeout_ticks_, err_, cur()),
           "peer_bn");
   }
 
@@ -893,6 +905,7 @@ class PeerComm {
   int khz_ = 0;
   void* buf_ = nullptr;
   int* err_ = nullptr;
+  unsigned long long* ctl_ = nullptr;
   unsigned long long seq_ = 0, timeout_ticks_ = 0;
   std::vector<unsigned long long> bases_;
   std::vector<void*> mapped_;
@@ -902,7 +915,8 @@ class PeerComm {
 
 void register_loader(pybind11::module& m);  // loader.cpp: native image-folder loader
 void bn_set_reduce_blocks(int n, int chb);
-void bn_set_unroll(int v);  // bn.hip: target blocks / channel lanes of the row reductions
+void bn_set_unroll(int v);
+void bn_set_stream(int grid, long nt_mb);  // bn.hip: grid cap / non-temporal threshold of the streaming passes  // bn.hip: target blocks / channel lanes of the row reductions
 
 static void rccl_check(int r, const char* what) {
   TORCH_CHECK(r == 0, what, ": ", rccl_last_error(), " (code ", r, ")");
@@ -1024,6 +1038,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_set_reduce_blocks", &bn_set_reduce_blocks, pybind11::arg("n"), pybind11::arg("chb") = 0);
   m.def("bn_act_maxpool", &bn_act_maxpool);
   m.def("bn_set_unroll", [](bool v) { bn_set_unroll(v ? 1 : 0); });
+  m.def("bn_set_stream", [](int grid, long nt_mb) { bn_set_stream(grid, nt_mb); });
   m.def("stem_conv", &stem_conv, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"), pybind11::arg("part"),
         pybind11::arg("G"), pybind11::arg("N"), pybind11::arg("H"), pybind11::arg("W"),
         pybind11::arg("shift") = pybind11::none());
@@ -1126,7 +1141,8 @@ PYBIND11_MODULE(_C, m) {
       .def("error", &PeerComm::error)
       .def("set_timeout", &PeerComm::set_timeout)
       .def("close", &PeerComm::close)
-      .def_property_readonly("seq", &PeerComm::seq);
+      .def_property_readonly("seq", &PeerComm::seq)
+      .def("device_seq", &PeerComm::device_seq);
   m.attr("PEER_MAX_ELEMS") = peer_max_elems();
   m.attr("PEER_MAX_WORLD") = peer_max_world();
   m.attr("PEER_BN_MAX_C") = peer_bn_max_channels();

@@ -245,6 +245,30 @@ __global__ void bn_apply_kernel(const bf16_t* __restrict__ y, const float* __res
 // sits behind a runtime select (which makes hipcc branch around and wait for each load).
 constexpr int BN_U = 4;
 
+// 16-B row loads / stores of the streaming elementwise passes, optionally non-temporal: streams of
+// tensors far larger than the 256 MB Infinity Cache gain from the hint (scripts/probes/stream_bw.hip,
+// profiles/r5b_stream_bw.txt: block-contiguous walk, 4 blocks per CU, nt: 6.24 TB/s read-1-write-1 and
+// 6.07 read-2-write-1, against 5.3-5.4 at 8192 blocks without it)
+typedef unsigned int bn_u32x4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+DEVI uint4 ldrow(const bf16_t* p) {
+  if constexpr (NT) {
+    const bn_u32x4 v = __builtin_nontemporal_load((const bn_u32x4*)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+  } else {
+    return *(const uint4*)p;
+  }
+}
+template <bool NT>
+DEVI void strow(bf16_t* p, const uint4& v) {
+  if constexpr (NT) {
+    const bn_u32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, (bn_u32x4*)p);
+  } else {
+    *(uint4*)p = v;
+  }
+}
+
 // Rows of a channel-fixed elementwise pass (the grid's thread count is a multiple of C/8, grid_chan): when
 // 256 % (C/8) == 0 each block streams its own contiguous run of rows (256 / (C/8) rows per step), otherwise
 // the grid-wide stride.  The grid-wide stride had every wave's U loads land in U regions tens of MB apart;
@@ -274,7 +298,7 @@ DEVI RowWalk row_walk(long rows, int cch, int contiguous) {
   return w;
 }
 
-template <bool RES>
+template <bool RES, bool NT = false>
 __global__ void bn_apply_u_kernel(const bf16_t* __restrict__ y, const float* __restrict__ coef,
                                   const bf16_t* __restrict__ res, bf16_t* __restrict__ out, long rows, int C,
                                   int ldo, int c_off, int act, uint8_t* __restrict__ mask, int walk) {
@@ -296,8 +320,8 @@ __global__ void bn_apply_u_kernel(const bf16_t* __restrict__ y, const float* __r
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long r = row + u * rstride < rend ? row + u * rstride : row;
-      yv[u] = *(const uint4*)(y + r * C + c0);
-      if constexpr (RES) rv[u] = *(const uint4*)(res + r * C + c0);
+      yv[u] = ldrow<NT>(y + r * C + c0);
+      if constexpr (RES) rv[u] = ldrow<NT>(res + r * C + c0);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -314,7 +338,7 @@ __global__ void bn_apply_u_kernel(const bf16_t* __restrict__ y, const float* __r
         mk |= (z > 0.f ? 1u : 0u) << k;
         v[k] = apply_act(z, act);
       }
-      *(uint4*)(out + r * ldo + c_off + c0) = pack8(v);
+      strow<NT>(out + r * ldo + c_off + c0, pack8(v));
       // ReLU mask for the backward (residual BNs): bit k of byte r * C/8 + c0/8 = channel c0 + k positive
       if (mask) mask[r * (C >> 3) + (c0 >> 3)] = (uint8_t)mk;
     }
@@ -346,8 +370,8 @@ __global__ void bn_apply_mx_kernel(const bf16_t* __restrict__ y, const float* __
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
       const long r = row + u * rstride < rows ? row + u * rstride : row;
-      yv[u] = *(const uint4*)(y + r * C + c0);
-      if constexpr (RES) rv[u] = *(const uint4*)(res + r * C + c0);
+      yv[u] = ldrow<false>(y + r * C + c0);
+      if constexpr (RES) rv[u] = ldrow<false>(res + r * C + c0);
     }
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
@@ -722,7 +746,7 @@ __global__ void bn_bwd_elemt_kernel(const bf16_t* __restrict__ g, const bf16_t* 
 
 // MODE 0: dz given (dz_in); 1: g with the activation recomputed (no residual); 2: same with a residual;
 // 3: g is already dz (no activation).  U rows in flight as bn_apply_u_kernel.
-template <int MODE>
+template <int MODE, bool NT = false>
 __global__ void bn_bwd_elemt_u_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ y,
                                       const float* __restrict__ coef, const float* __restrict__ kk,
                                       const bf16_t* __restrict__ res, const bf16_t* __restrict__ dz_in,
@@ -746,10 +770,10 @@ __global__ void bn_bwd_elemt_u_kernel(const bf16_t* __restrict__ g, const bf16_t
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
       const long r = row + u * rstride < rend ? row + u * rstride : row;
-      yr[u] = *(const uint4*)(y + r * C + c0);
-      if constexpr (MODE == 0) gr[u] = *(const uint4*)(dz_in + r * C + c0);
-      else gr[u] = *(const uint4*)(g + r * ldg + c0);
-      if constexpr (MODE == 2) rr[u] = *(const uint4*)(res + r * C + c0);
+      yr[u] = ldrow<NT>(y + r * C + c0);
+      if constexpr (MODE == 0) gr[u] = ldrow<NT>(dz_in + r * C + c0);
+      else gr[u] = ldrow<NT>(g + r * ldg + c0);
+      if constexpr (MODE == 2) rr[u] = ldrow<NT>(res + r * C + c0);
     }
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
@@ -773,7 +797,7 @@ __global__ void bn_bwd_elemt_u_kernel(const bf16_t* __restrict__ g, const bf16_t
         const float xhat = (yv[k] - mu[k]) * is[k];
         gv[k] = sc[k] * (gv[k] - k1[k] - xhat * k2[k]);
       }
-      *(uint4*)(dy + r * C + c0) = pack8(gv);
+      strow<NT>(dy + r * C + c0, pack8(gv));
     }
   }
 }
@@ -834,6 +858,22 @@ int grid_chan(long rows, int C) {
   const int b = grid_for(rows * cch, 256, 8192);
   return (b + m - 1) / m * m;
 }
+
+// Streaming elementwise passes (bn_apply_u / bn_bwd_elemt_u with the block-contiguous walk): grid capped at
+// g_bn_grid blocks (4 per CU: each block streams one long contiguous run; 8192 blocks measured 5.3 TB/s
+// against 6.0-6.2 at 1024, profiles/r5b_stream_bw.txt) and non-temporal accesses on tensors of at least
+// g_bn_nt_mb MiB (IMGCLS_BN_NT_MB; 0 = never, < 0 = always)
+int g_bn_grid = getenv("IMGCLS_BN_GRID") ? atoi(getenv("IMGCLS_BN_GRID")) : 1024;
+long g_bn_nt_mb = getenv("IMGCLS_BN_NT_MB") ? atol(getenv("IMGCLS_BN_NT_MB")) : 256;
+
+int grid_stream(long rows, int C) {
+  const int cch = C / 8;
+  const int b = grid_chan(rows, C);
+  if (g_bn_grid <= 0 || !g_bn_walk || cch <= 0 || 256 % cch) return b;  // grid-stride walk: keep grid_chan's
+  return b < g_bn_grid ? b : g_bn_grid;
+}
+
+bool use_nt(long rows, int C) { return g_bn_nt_mb < 0 || (g_bn_nt_mb > 0 && rows * (long)C * 2 >= (g_bn_nt_mb << 20)); }
 
 }  // namespace
 
@@ -898,10 +938,18 @@ int bn_apply_launch(const bf16_t* y, const float* coef, const bf16_t* res, bf16_
     return 0;
   }
   if (g_bn_unroll || mask) {
-    if (res) hipLaunchKernelGGL(bn_apply_u_kernel<true>, dim3(grid_chan(rows, C)), dim3(256), 0, s, y, coef, res, out,
-                                rows, C, ldo, c_off, act, mask, g_bn_walk);
-    else hipLaunchKernelGGL(bn_apply_u_kernel<false>, dim3(grid_chan(rows, C)), dim3(256), 0, s, y, coef, res, out,
-                            rows, C, ldo, c_off, act, mask, g_bn_walk);
+    const dim3 gr(grid_stream(rows, C));
+    if (use_nt(rows, C)) {
+      if (res) hipLaunchKernelGGL((bn_apply_u_kernel<true, true>), gr, dim3(256), 0, s, y, coef, res, out, rows, C, ldo,
+                                  c_off, act, mask, g_bn_walk);
+      else hipLaunchKernelGGL((bn_apply_u_kernel<false, true>), gr, dim3(256), 0, s, y, coef, res, out, rows, C, ldo,
+                              c_off, act, mask, g_bn_walk);
+    } else {
+      if (res) hipLaunchKernelGGL((bn_apply_u_kernel<true, false>), gr, dim3(256), 0, s, y, coef, res, out, rows, C,
+                                  ldo, c_off, act, mask, g_bn_walk);
+      else hipLaunchKernelGGL((bn_apply_u_kernel<false, false>), gr, dim3(256), 0, s, y, coef, res, out, rows, C, ldo,
+                              c_off, act, mask, g_bn_walk);
+    }
   } else {
     hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_chan(rows, C)), dim3(256), 0, s, y, coef, res, out,
                        rows, C, ldo, c_off, act);
@@ -947,15 +995,19 @@ int bn_bwd_elemt_launch(const bf16_t* g, const bf16_t* y, const float* coef, con
                         int ldg, hipStream_t s) {
   const int lg = ldg > 0 ? ldg : C;
   if (g_bn_unroll) {
-    const dim3 gr(grid_chan(rows, C));
-    if (dz_in) hipLaunchKernelGGL(bn_bwd_elemt_u_kernel<0>, gr, dim3(256), 0, s, g, y, coef, k, res, dz_in, dy, rows, C, act, lg,
-                                       g_bn_walk);
-    else if (act == ACT_NONE) hipLaunchKernelGGL(bn_bwd_elemt_u_kernel<3>, gr, dim3(256), 0, s, g, y, coef, k, res, dz_in, dy, rows, C, act, lg,
-                                       g_bn_walk);
-    else if (res) hipLaunchKernelGGL(bn_bwd_elemt_u_kernel<2>, gr, dim3(256), 0, s, g, y, coef, k, res, dz_in, dy, rows, C, act, lg,
-                                       g_bn_walk);
-    else hipLaunchKernelGGL(bn_bwd_elemt_u_kernel<1>, gr, dim3(256), 0, s, g, y, coef, k, res, dz_in, dy, rows, C, act, lg,
-                                       g_bn_walk);
+    const dim3 gr(grid_stream(rows, C));
+#define BWD_ELEMT(M, NT_)                                                                                       \
+  hipLaunchKernelGGL((bn_bwd_elemt_u_kernel<M, NT_>), gr, dim3(256), 0, s, g, y, coef, k, res, dz_in, dy, rows, C, \
+                     act, lg, g_bn_walk)
+    const int mode = dz_in ? 0 : act == ACT_NONE ? 3 : res ? 2 : 1;
+    if (use_nt(rows, C)) {
+      if (mode == 0) BWD_ELEMT(0, true); else if (mode == 3) BWD_ELEMT(3, true);
+      else if (mode == 2) BWD_ELEMT(2, true); else BWD_ELEMT(1, true);
+    } else {
+      if (mode == 0) BWD_ELEMT(0, false); else if (mode == 3) BWD_ELEMT(3, false);
+      else if (mode == 2) BWD_ELEMT(2, false); else BWD_ELEMT(1, false);
+    }
+#undef BWD_ELEMT
   } else {
     hipLaunchKernelGGL(bn_bwd_elemt_kernel, dim3(grid_chan(rows, C)), dim3(256), 0, s, g, y, coef, k,
                        res, dz_in, dy, rows, C, act, lg);
@@ -996,3 +1048,9 @@ void bn_set_reduce_blocks(int n, int chb) {
 }
 
 void bn_set_unroll(int v) { g_bn_unroll = v; }
+
+// streaming elementwise passes: grid cap (<= 0: grid_chan's) and non-temporal threshold in MiB (0 never, < 0 always)
+void bn_set_stream(int grid, long nt_mb) {
+  g_bn_grid = grid;
+  g_bn_nt_mb = nt_mb;
+}

@@ -69,10 +69,29 @@ DEVI void acquire_after_poll() {
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 }
 
+// Call sequence numbers live on the device (ctl[0]), so a captured HIP graph replays a SyncBN step with
+// fresh numbers: every block reads seq = ctl[0] + 1 when it starts; after its wait, each block draws a
+// ticket (ctl[1]) and the last one of the launch stores ctl[0] = seq and re-arms the ticket.  Every block
+// reads the counter before it draws its ticket, so no block of this call can see the new value; the next
+// call is a later launch on the same stream and sees it.  (Vector atomics only.)
+DEVI unsigned long long call_seq(unsigned long long* ctl) {
+  return __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1ull;
+}
+
+DEVI void call_done(unsigned long long* ctl, unsigned long long seq) {
+  unsigned int* ticket = (unsigned int*)(ctl + 1);
+  const unsigned int k = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if (k == gridDim.x - 1) {
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(ctl, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 __global__ __launch_bounds__(kThreads) void peer_allreduce_f64_kernel(
     const double* in, double* out, int n, PeerTable tab, int rank, int world,
-    unsigned long long seq, unsigned long long timeout_ticks, int* __restrict__ err) {
+    unsigned long long* ctl, unsigned long long timeout_ticks, int* __restrict__ err) {
   const int g = blockIdx.x;
+  const unsigned long long seq = call_seq(ctl);
   const int par = (int)(seq & 1ull);
   const int beg = g * kChunk;
   const int cnt = min(kChunk, n - beg);
@@ -115,6 +134,7 @@ __global__ __launch_bounds__(kThreads) void peer_allreduce_f64_kernel(
     acquire_after_poll();
   }
   __syncthreads();
+  if (t == 0) call_done(ctl, seq);
 
   // 3) rank-ordered sum of the W payloads (system-scope loads of the local, uncached buffer)
   const unsigned long long* slots = (const unsigned long long*)(tab.base[rank] + kFlagBytes) +
@@ -163,9 +183,10 @@ struct PeerBnArgs {
 
 template <bool FWD>
 __global__ __launch_bounds__(256) void peer_bn_kernel(PeerBnArgs a, PeerTable tab, int rank, int world,
-                                                      unsigned long long seq, unsigned long long timeout_ticks,
+                                                      unsigned long long* ctl, unsigned long long timeout_ticks,
                                                       int* __restrict__ err) {
   const int g = blockIdx.x, t = threadIdx.x;
+  const unsigned long long seq = call_seq(ctl);
   const int par = (int)(seq & 1ull);
   const int C = a.C, c = g * kBnCB + t;
   // 1) local column sums of the partial rows (re-zeroed)
@@ -212,6 +233,7 @@ __global__ __launch_bounds__(256) void peer_bn_kernel(PeerBnArgs a, PeerTable ta
     acquire_after_poll();
   }
   __syncthreads();
+  if (t == 0) call_done(ctl, seq);
   // 4) rank-ordered sums, then the layer's coefficients for this block's channels
   const unsigned long long* slots = (const unsigned long long*)(tab.base[rank] + kFlagBytes) +
                                     (size_t)par * kMaxWorld * kSlotDoubles + (size_t)g * kBnStride;
@@ -286,7 +308,7 @@ int peer_ipc_open(const char* in64, void** p) {
 int peer_ipc_close(void* p) { return (int)hipIpcCloseMemHandle(p); }
 
 int peer_allreduce_f64_launch(const double* in, double* out, int n, const unsigned long long* bases, int rank,
-                              int world, unsigned long long seq, unsigned long long timeout_ticks, int* err,
+                              int world, unsigned long long* ctl, unsigned long long timeout_ticks, int* err,
                               hipStream_t st) {
   if (n <= 0) return 0;
   if (world < 1 || world > kMaxWorld || rank < 0 || rank >= world || n > (int)kSlotDoubles) return (int)hipErrorInvalidValue;
@@ -294,7 +316,7 @@ int peer_allreduce_f64_launch(const double* in, double* out, int n, const unsign
   for (int i = 0; i < kMaxWorld; ++i) tab.base[i] = i < world ? bases[i] : 0ull;
   const int blocks = (n + kChunk - 1) / kChunk;
   hipLaunchKernelGGL(peer_allreduce_f64_kernel, dim3(blocks), dim3(kThreads), 0, st, in, out, n, tab, rank, world,
-                     seq, timeout_ticks, err);
+                     ctl, timeout_ticks, err);
   return (int)hipGetLastError();
 }
 
@@ -303,7 +325,7 @@ int peer_bn_max_channels() { return kBnCB * kBnMaxBlocks; }
 int peer_bn_launch(bool fwd, float* part, int G, int C, double count, const float* gamma, const float* beta,
                    float* rmean, float* rvar, long long* nbt, float momentum, float eps, float* out, float* dgamma,
                    float* dbeta, double* count_io, const float* shift, const unsigned long long* bases, int rank,
-                   int world, unsigned long long seq, unsigned long long timeout_ticks, int* err, hipStream_t st) {
+                   int world, unsigned long long* ctl, unsigned long long timeout_ticks, int* err, hipStream_t st) {
   if (C <= 0) return 0;
   if (world < 1 || world > kMaxWorld || rank < 0 || rank >= world || C > kBnCB * kBnMaxBlocks || G < 1)
     return (int)hipErrorInvalidValue;
@@ -313,10 +335,10 @@ int peer_bn_launch(bool fwd, float* part, int G, int C, double count, const floa
                      shift};
   const int blocks = (C + kBnCB - 1) / kBnCB;
   if (fwd)
-    hipLaunchKernelGGL(peer_bn_kernel<true>, dim3(blocks), dim3(256), 0, st, a, tab, rank, world, seq, timeout_ticks,
+    hipLaunchKernelGGL(peer_bn_kernel<true>, dim3(blocks), dim3(256), 0, st, a, tab, rank, world, ctl, timeout_ticks,
                        err);
   else
-    hipLaunchKernelGGL(peer_bn_kernel<false>, dim3(blocks), dim3(256), 0, st, a, tab, rank, world, seq, timeout_ticks,
+    hipLaunchKernelGGL(peer_bn_kernel<false>, dim3(blocks), dim3(256), 0, st, a, tab, rank, world, ctl, timeout_ticks,
                        err);
   return (int)hipGetLastError();
 }

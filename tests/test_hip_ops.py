@@ -1542,3 +1542,56 @@ def test_input_u8_resnet_forward_matches_fp32_input():
         a = m(hip.input_from_u8(u8, spec, IMAGENET_MEAN, IMAGENET_STD)).float()
         b = m(x32).float()
     assert rel_err(a, b) < 2e-2
+
+
+@pytest.mark.parametrize("rows,c", [(4099, 256), (1000, 2048), (777, 64), (301, 1152)])
+def test_bn_streaming_passes_every_grid_and_nt(rows, c):
+    """bn_apply (+residual +ReLU mask, and plain) and bn_bwd_elemt (all four modes) under every streaming setting
+    (grid capped at 64 / 1024 / grid_chan's, non-temporal never / always) against fp32 torch: the grid and the
+    cache hint change the walk and the access form, never a value - all settings are bitwise identical."""
+    hip = _hip()
+    torch.manual_seed(5)
+    y = bf(torch.randn(rows, c, device=DEV) * 2).to(torch.bfloat16)
+    res = bf(torch.randn(rows, c, device=DEV)).to(torch.bfloat16)
+    g = bf(torch.randn(rows, c, device=DEV)).to(torch.bfloat16)
+    coef = torch.cat([torch.rand(c, device=DEV) + 0.5, torch.randn(c, device=DEV),
+                      torch.randn(c, device=DEV) * 0.1, torch.rand(c, device=DEV) + 0.5])
+    kk = torch.randn(2 * c, device=DEV) * 0.1
+    sc, sh, mu, iv = coef.view(4, c)
+    yf, rf, gf = y.float(), res.float(), g.float()
+    z_res = yf * sc + sh + rf
+    want_apply_res = torch.relu(z_res)
+    want_apply = torch.relu(yf * sc + sh)
+    xhat = (yf - mu) * iv
+    k1, k2 = kk.view(2, c)
+
+    def elemt(gz):
+        return sc * (gz - k1 - xhat * k2)
+    want_bwd = {0: elemt(gf), 1: elemt(gf * (yf * sc + sh > 0)), 2: elemt(gf * (z_res > 0)), 3: elemt(gf)}
+    outs = []
+    try:
+        for grid, nt in ((1024, 256), (0, 0), (1024, -1), (64, -1), (64, 0)):
+            hip.C.bn_set_stream(grid, nt)
+            o1 = torch.empty_like(y)
+            mask = torch.zeros(rows * c // 8, dtype=torch.uint8, device=DEV)
+            hip.C.bn_apply(y, coef, res, o1, rows, c, c, 0, 1, None, None, mask=mask)
+            o2 = torch.empty_like(y)
+            hip.C.bn_apply(y, coef, None, o2, rows, c, c, 0, 1, None, None)
+            bw = {}
+            for mode in range(4):
+                d = torch.empty_like(y)
+                hip.C.bn_bwd_elemt(None if mode == 0 else g, y, coef, kk, res if mode == 2 else None,
+                                   g if mode == 0 else None, d, rows, c, 0 if mode == 3 else 1, 0)
+                bw[mode] = d
+            torch.cuda.synchronize()
+            assert rel_err(o1.float(), want_apply_res) < 1e-2 and rel_err(o2.float(), want_apply) < 1e-2
+            bits = torch.stack([(mask >> k) & 1 for k in range(8)], 1).view(rows, c).bool()
+            assert torch.equal(bits, z_res.view(rows, c) > 0) or (bits != (z_res > 0)).float().mean() < 1e-4
+            for mode in range(4):
+                assert rel_err(bw[mode].float(), want_bwd[mode]) < 1e-2, (grid, nt, mode)
+            outs.append([o1, o2, mask] + [bw[m] for m in range(4)])
+    finally:
+        hip.C.bn_set_stream(1024, 256)
+    for o in outs[1:]:
+        for a_, b_ in zip(o, outs[0]):
+            assert torch.equal(a_, b_)
