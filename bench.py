@@ -68,7 +68,8 @@ def parse():
                    "does not list are still timed")
     p.add_argument("--tune-save", default="", help="write the kernel choices of this run to this file")
     p.add_argument("--graph", default="auto", choices=["on", "off", "auto"],
-                   help="replay the whole training step as one captured HIP graph (single process); auto = on "
+                   help="replay the whole training step as one captured HIP graph (at N > 1: forward + backward, "
+                        "then one flat gradient all-reduce and Adam); auto = on "
                         "at per-GPU batch <= 64 (host-bound steps, train.py --hip-graph auto)")
     p.add_argument("--dtype", default="bf16", choices=["bf16"],
                    help="compute dtype (bf16).  MX-FP8 is not a benchmark configuration: forward-only fp8 "
@@ -201,7 +202,9 @@ def main():
                                      steps=a.warmup + a.steps, ring=2, seed=1234 + ctx.rank)
         batches = list(iter(data))
 
-    use_graph = a.compute == "hip" and ctx.world_size == 1 and (
+    # at N > 1 the replay holds forward + backward (+ the SyncBN peer exchanges); the gradient all-reduce and
+    # Adam follow each replay (Trainer.capture_step)
+    use_graph = a.compute == "hip" and tr.graph_capable() and (
         a.graph == "on" or (a.graph == "auto" and a.batch <= GRAPH_AUTO_MAX_BATCH))
 
     def step(i):
@@ -224,7 +227,8 @@ def main():
     if not torch.isfinite(last).item():
         raise FloatingPointError(f"non-finite loss in warmup: {last.item()}")
     comm_t = None
-    if ctx.device.type == "cuda" and (a.comm_timing == "on" or (a.comm_timing == "auto" and ctx.world_size > 1)):
+    if ctx.device.type == "cuda" and not use_graph and (
+            a.comm_timing == "on" or (a.comm_timing == "auto" and ctx.world_size > 1)):
         from pytorch_imageclassification_distributed_amd.parallel import comm_timer
         comm_t = comm_timer.install()
     barrier(ctx)
@@ -273,6 +277,8 @@ def main():
             metric = "CPU REHEARSAL of the multi-rank path (gloo, fp32, not a benchmark): " + metric
         if os.environ.get("IMGCLS_DIAG_SKIP_WGRAD", "0") == "1":  # a diagnostic, never a benchmark number
             metric, base = "DIAGNOSTIC (weight gradients skipped, invalid as a benchmark): " + metric, None
+        if os.environ.get("IMGCLS_DIAG_SKIP_GRAD_COMM", "0") == "1" and ctx.world_size > 1:
+            metric, base = "DIAGNOSTIC (gradient all-reduce skipped, invalid as a benchmark): " + metric, None
         print(json.dumps({
             "metric": metric, "value": round(value, 2), "unit": "images/sec",
             "n_gpus": ctx.world_size, "steps": a.steps, "warmup": a.warmup,

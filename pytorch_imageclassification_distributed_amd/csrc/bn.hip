@@ -298,11 +298,15 @@ DEVI RowWalk row_walk(long rows, int cch, int contiguous) {
   return w;
 }
 
-template <bool RES, bool NT = false>
-__global__ void bn_apply_u_kernel(const bf16_t* __restrict__ y, const float* __restrict__ coef,
+// ACT is a template constant: with a runtime activation code hipcc compiled every element's SiLU branch
+// into the unrolled loop, and the register pressure spilled the in-flight loads to scratch behind
+// vmcnt(0) waits (5.0 TB/s where the same walk streams at 6+)
+template <bool RES, bool NT, int ACT>
+__global__ __launch_bounds__(256) void bn_apply_u_kernel(const bf16_t* __restrict__ y, const float* __restrict__ coef,
                                   const bf16_t* __restrict__ res, bf16_t* __restrict__ out, long rows, int C,
-                                  int ldo, int c_off, int act, uint8_t* __restrict__ mask, int walk) {
-  constexpr int U = 2 * BN_U;  // 8 rows in flight measured best with the block-contiguous walk
+                                  int ldo, int c_off, int act_unused, uint8_t* __restrict__ mask, int walk) {
+  constexpr int U = RES ? BN_U : 2 * BN_U;  // 8 loads in flight per lane (4 rows with a residual: the VGPRs of
+                                             // 8 rows x 2 loads cost a wave per SIMD)
   const int cch = C >> 3;
   if (cch == 0) return;
   const RowWalk w = row_walk(rows, cch, walk);
@@ -336,7 +340,7 @@ __global__ void bn_apply_u_kernel(const bf16_t* __restrict__ y, const float* __r
         float z = v[k] * sc[k] + sh[k];
         if constexpr (RES) z += rr[k];
         mk |= (z > 0.f ? 1u : 0u) << k;
-        v[k] = apply_act(z, act);
+        v[k] = apply_act(z, ACT);
       }
       strow<NT>(out + r * ldo + c_off + c0, pack8(v));
       // ReLU mask for the backward (residual BNs): bit k of byte r * C/8 + c0/8 = channel c0 + k positive
@@ -573,6 +577,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_u_kernel(
     const bf16_t* __restrict__ res, bf16_t* __restrict__ dz_out, long rows, int C, int act,
     long rows_per_block, float* __restrict__ part, int G, int ldg, int CHB) {
   constexpr bool RES = FL & 1, ACT = FL & 2, DZ = FL & 4;
+  constexpr int ACTC = (FL & 8) ? ACT_SILU : ACT_RELU;  // (bit 3: SiLU) the activation as a constant
   __shared__ float red[2][256][9];
   const int cch = C >> 3;
   const int RP = 256 / CHB;
@@ -614,7 +619,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_u_kernel(
           if constexpr (ACT) {
             float z = yv[k] * sc[k] + sh[k];
             if constexpr (RES) z += rv[k];
-            dz = act_grad(z, gv[k], act);
+            dz = act_grad(z, gv[k], ACTC);
           }
           gv[k] = dz;
           s[k] += dz;
@@ -746,11 +751,11 @@ __global__ void bn_bwd_elemt_kernel(const bf16_t* __restrict__ g, const bf16_t* 
 
 // MODE 0: dz given (dz_in); 1: g with the activation recomputed (no residual); 2: same with a residual;
 // 3: g is already dz (no activation).  U rows in flight as bn_apply_u_kernel.
-template <int MODE, bool NT = false>
-__global__ void bn_bwd_elemt_u_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ y,
+template <int MODE, bool NT, int ACT>
+__global__ __launch_bounds__(256) void bn_bwd_elemt_u_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ y,
                                       const float* __restrict__ coef, const float* __restrict__ kk,
                                       const bf16_t* __restrict__ res, const bf16_t* __restrict__ dz_in,
-                                      bf16_t* __restrict__ dy, long rows, int C, int act, int ldg, int walk) {
+                                      bf16_t* __restrict__ dy, long rows, int C, int act_unused, int ldg, int walk) {
   const int cch = C >> 3;
   if (cch == 0) return;
   const RowWalk w = row_walk(rows, cch, walk);
@@ -789,7 +794,7 @@ __global__ void bn_bwd_elemt_u_kernel(const bf16_t* __restrict__ g, const bf16_t
         for (int k = 0; k < 8; ++k) {
           float z = yv[k] * sc[k] + sh[k];
           if constexpr (MODE == 2) z += rv[k];
-          gv[k] = act_grad(z, gv[k], act);
+          gv[k] = act_grad(z, gv[k], ACT);
         }
       }
 #pragma unroll
@@ -939,17 +944,20 @@ int bn_apply_launch(const bf16_t* y, const float* coef, const bf16_t* res, bf16_
   }
   if (g_bn_unroll || mask) {
     const dim3 gr(grid_stream(rows, C));
-    if (use_nt(rows, C)) {
-      if (res) hipLaunchKernelGGL((bn_apply_u_kernel<true, true>), gr, dim3(256), 0, s, y, coef, res, out, rows, C, ldo,
-                                  c_off, act, mask, g_bn_walk);
-      else hipLaunchKernelGGL((bn_apply_u_kernel<false, true>), gr, dim3(256), 0, s, y, coef, res, out, rows, C, ldo,
-                              c_off, act, mask, g_bn_walk);
-    } else {
-      if (res) hipLaunchKernelGGL((bn_apply_u_kernel<true, false>), gr, dim3(256), 0, s, y, coef, res, out, rows, C,
-                                  ldo, c_off, act, mask, g_bn_walk);
-      else hipLaunchKernelGGL((bn_apply_u_kernel<false, false>), gr, dim3(256), 0, s, y, coef, res, out, rows, C, ldo,
-                              c_off, act, mask, g_bn_walk);
-    }
+#define APPLY(R, N, A)                                                                                          \
+  hipLaunchKernelGGL((bn_apply_u_kernel<R, N, A>), gr, dim3(256), 0, s, y, coef, res, out, rows, C, ldo, c_off, act, \
+                     mask, g_bn_walk)
+#define APPLY_ACT(R, N)                                    \
+  do {                                                     \
+    if (act == ACT_RELU) APPLY(R, N, ACT_RELU);            \
+    else if (act == ACT_SILU) APPLY(R, N, ACT_SILU);       \
+    else APPLY(R, N, ACT_NONE);                            \
+  } while (0)
+    const bool nt = use_nt(rows, C);
+    if (res) { if (nt) APPLY_ACT(true, true); else APPLY_ACT(true, false); }
+    else { if (nt) APPLY_ACT(false, true); else APPLY_ACT(false, false); }
+#undef APPLY_ACT
+#undef APPLY
   } else {
     hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_chan(rows, C)), dim3(256), 0, s, y, coef, res, out,
                        rows, C, ldo, c_off, act);
@@ -969,14 +977,14 @@ int bn_bwd_reduce_launch(const bf16_t* g, const bf16_t* y, const float* coef, co
     return 0;
   }
   const bool a = act != ACT_NONE;
-  const int fl = (res && a ? 1 : 0) | (a ? 2 : 0) | (dz_out ? 4 : 0);
+  const int fl = (res && a ? 1 : 0) | (a ? 2 : 0) | (dz_out ? 4 : 0) | (act == ACT_SILU ? 8 : 0);
 #define BWDRED(F)                                                                                        \
   case F:                                                                                               \
     hipLaunchKernelGGL(bn_bwd_reduce_u_kernel<F>, rg.grid, dim3(256), 0, s, g, y, coef, res, dz_out, rows, C, \
                        act, rg.rpb, part, G, ld, rg.chb);                                               \
     break;
   switch (fl) {
-    BWDRED(0) BWDRED(2) BWDRED(3) BWDRED(4) BWDRED(6) BWDRED(7)
+    BWDRED(0) BWDRED(2) BWDRED(3) BWDRED(4) BWDRED(6) BWDRED(7) BWDRED(10) BWDRED(11) BWDRED(14) BWDRED(15)
     default: return 2;
   }
 #undef BWDRED
@@ -996,17 +1004,22 @@ int bn_bwd_elemt_launch(const bf16_t* g, const bf16_t* y, const float* coef, con
   const int lg = ldg > 0 ? ldg : C;
   if (g_bn_unroll) {
     const dim3 gr(grid_stream(rows, C));
-#define BWD_ELEMT(M, NT_)                                                                                       \
-  hipLaunchKernelGGL((bn_bwd_elemt_u_kernel<M, NT_>), gr, dim3(256), 0, s, g, y, coef, k, res, dz_in, dy, rows, C, \
+#define BWD_ELEMT(M, NT_, A)                                                                                       \
+  hipLaunchKernelGGL((bn_bwd_elemt_u_kernel<M, NT_, A>), gr, dim3(256), 0, s, g, y, coef, k, res, dz_in, dy, rows, C, \
                      act, lg, g_bn_walk)
+#define BWD_ACT(M, NT_)                                                             \
+  do {                                                                              \
+    if (act == ACT_SILU) BWD_ELEMT(M, NT_, ACT_SILU); else BWD_ELEMT(M, NT_, ACT_RELU); \
+  } while (0)
     const int mode = dz_in ? 0 : act == ACT_NONE ? 3 : res ? 2 : 1;
     if (use_nt(rows, C)) {
-      if (mode == 0) BWD_ELEMT(0, true); else if (mode == 3) BWD_ELEMT(3, true);
-      else if (mode == 2) BWD_ELEMT(2, true); else BWD_ELEMT(1, true);
+      if (mode == 0) BWD_ELEMT(0, true, ACT_NONE); else if (mode == 3) BWD_ELEMT(3, true, ACT_NONE);
+      else if (mode == 2) BWD_ACT(2, true); else BWD_ACT(1, true);
     } else {
-      if (mode == 0) BWD_ELEMT(0, false); else if (mode == 3) BWD_ELEMT(3, false);
-      else if (mode == 2) BWD_ELEMT(2, false); else BWD_ELEMT(1, false);
+      if (mode == 0) BWD_ELEMT(0, false, ACT_NONE); else if (mode == 3) BWD_ELEMT(3, false, ACT_NONE);
+      else if (mode == 2) BWD_ACT(2, false); else BWD_ACT(1, false);
     }
+#undef BWD_ACT
 #undef BWD_ELEMT
   } else {
     hipLaunchKernelGGL(bn_bwd_elemt_kernel, dim3(grid_chan(rows, C)), dim3(256), 0, s, g, y, coef, k,

@@ -69,8 +69,11 @@ DEVI float wave_max(float v) {
   return v;
 }
 
-DEVI float silu_f(float x) { return x / (1.f + __expf(-x)); }
-DEVI float sigmoid_f(float x) { return 1.f / (1.f + __expf(-x)); }
+// v_exp + v_rcp (1 ulp) instead of an IEEE division: the division's scale / fma / fixup sequence made every
+// kernel with a runtime activation carry ~15 extra VALU per element and pushed the streaming BN passes and
+// several conv epilogues into scratch spills (results are rounded to bf16 either way)
+DEVI float sigmoid_f(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+DEVI float silu_f(float x) { return x * sigmoid_f(x); }
 
 // activation codes shared by host and device
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_SILU = 2 };

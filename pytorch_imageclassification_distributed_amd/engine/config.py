@@ -94,8 +94,9 @@ def build_parser() -> argparse.ArgumentParser:
                    help="bitwise-reproducible GPU kernels (no split-K / cross-block fp32 atomics; slower)")
     p.add_argument("--timeout-min", type=float, default=10.0, help="process-group timeout (minutes)")
     p.add_argument("--hip-graph", nargs="?", const="on", default="auto", choices=["on", "off", "auto"],
-                   help="single GPU: capture the whole training step once and replay it as one HIP graph "
-                        "(host-bound steps); a batch of another shape runs eagerly.  auto = on at per-GPU "
+                   help="capture the whole training step once and replay it as one HIP graph (host-bound steps; "
+                        "at N > 1 forward + backward with the SyncBN peer exchanges, then one flat gradient "
+                        "all-reduce and Adam); a batch of another shape runs eagerly.  auto = on at per-GPU "
                         f"batch <= {GRAPH_AUTO_MAX_BATCH} (Inception-v3 @299: b4 466 vs 164 img/s eager, b32 "
                         "2943 vs 1978; at b128 eager wins, profiles/r6_bench_host_data_and_inception_small_batch.jsonl)")
     return p
@@ -106,7 +107,7 @@ def hip_graph_enabled(args, world_size: int) -> bool:
     mode = getattr(args, "hip_graph", "off")
     if mode is True:
         mode = "on"
-    if mode in (False, None, "off") or world_size != 1:
+    if mode in (False, None, "off"):
         return False
     return mode == "on" or args.batchsize <= GRAPH_AUTO_MAX_BATCH
 

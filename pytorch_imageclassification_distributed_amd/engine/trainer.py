@@ -298,9 +298,16 @@ class Trainer:
         kernel shape is tuned (the tuner never runs under capture).  Single process (world 1): the
         graph carries no collectives.  Inputs are copied into static buffers on every replay; the
         learning rate is a kernel argument of the captured Adam launch, so a scheduler change
-        re-captures (``graph_step`` checks)."""
-        if not self.hip or self.ctx.world_size != 1:
-            raise RuntimeError("capture_step: HIP path on a single process only")
+        re-captures (``graph_step`` checks).
+
+        At N > 1 the graph holds forward + loss + backward, SyncBN exchanges included: the one-shot peer
+        kernels take their call numbers from a device counter (``csrc/peer.hip``), so every replay
+        exchanges fresh statistics.  The gradient collectives cannot sit in the graph (the reducer's hooks do
+        not run on replay), so after each replay one flat all-reduce of the gradient arena and the fused
+        Adam run eagerly (``graph_step``): ~1000 host dispatches become a replay plus three."""
+        if not self.graph_capable():
+            raise RuntimeError("capture_step: needs the HIP path and, at N > 1, SyncBN off or on the peer "
+                               "transport (no process-group collective inside the step) and no buffer broadcast")
         self._g_x = images.detach().clone()
         for attr in ("_imgcls_s2d", "_imgcls_prepared"):  # loader-converted input (input_from_u8) stays marked
             if hasattr(images, attr):
@@ -308,12 +315,28 @@ class Trainer:
         self._g_y = labels.detach().clone()
         self._g_lrs = tuple(g["lr"] for g in self.optimizer.param_groups)
         st = self.step_stream if self.step_stream is not None else torch.cuda.Stream(device=self.dev)
+        split = self.ctx.world_size > 1
         torch.cuda.synchronize(self.dev)
         g = torch.cuda.CUDAGraph()
+        if split:
+            self.reducer.deferred = True
         with torch.cuda.graph(g, stream=st):
-            self._g_loss = self._train_step(self._g_x, self._g_y)
+            self._g_loss = self._train_step(self._g_x, self._g_y, update=not split)
+        if split:  # replays run no hooks; an eager step in between (another batch shape) reduces as usual
+            self.reducer.deferred = False
+            self.reducer.reset_after_capture()
         torch.cuda.synchronize(self.dev)
-        self._graph, self._g_stream = g, st
+        self._graph, self._g_stream, self._g_split = g, st, split
+
+    def graph_capable(self) -> bool:
+        """Whole-step replay works: HIP path, and at N > 1 nothing inside the step that talks to the
+        process group (SyncBN over the peer kernels or off, no per-step buffer broadcast)."""
+        if not self.hip:
+            return False
+        if self.ctx.world_size == 1:
+            return True
+        return (self.reducer is not None and not getattr(self.args, "broadcast_buffers", False)
+                and (not self.args.sync_bn or self.syncbn_peer))
 
     def graph_step(self, images, labels):
         """Replay the captured step on new inputs (same shapes); returns the step's loss tensor, valid
@@ -329,6 +352,8 @@ class Trainer:
             self._g_x.copy_(images, non_blocking=True)
             self._g_y.copy_(labels, non_blocking=True)
             self._graph.replay()
+            if self._g_split:  # N > 1: the gradients of the replayed backward, summed once, then Adam
+                self.optimizer.step(grad_scale=self.reducer.flat_all_reduce())
         caller.wait_stream(st)
         images.record_stream(st)
         labels.record_stream(st)
@@ -340,7 +365,7 @@ class Trainer:
         counted per process, so a resumed run warms up too), then capture once - on a full batch of the
         loader's batch size, never on an epoch's short last batch - and replay; a batch of another shape
         runs eagerly."""
-        use = hip_graph_enabled(self.args, self.ctx.world_size) and self.hip and not self._prof
+        use = hip_graph_enabled(self.args, self.ctx.world_size) and self.graph_capable() and not self._prof
         if use:
             if self._graph is not None:
                 if self._g_x.shape == images.shape and self._g_y.shape == labels.shape:
@@ -350,10 +375,12 @@ class Trainer:
         self._eager_steps += 1
         return self.train_step(images, labels)
 
-    def _train_step(self, images, labels):
+    def _train_step(self, images, labels, update: bool = True):
+        """One step; ``update=False`` stops after backward (the N > 1 graph capture: the gradient reduce and
+        Adam run after each replay)."""
         rf = torch.profiler.record_function
         timer = self.timer
-        ct = comm_timer._TIMER if self.dev.type == "cuda" else None
+        ct = comm_timer._TIMER if (self.dev.type == "cuda" and not torch.cuda.is_current_stream_capturing()) else None
         if ct is not None:
             ct.begin()
         if self.reducer is not None and getattr(self.args, "broadcast_buffers", False):
@@ -370,6 +397,8 @@ class Trainer:
                 from ..ops import hip as _hip
                 _hip.join_side_streams()  # (normally already done by the engine callback)
         timer.mark("backward")
+        if not update:
+            return loss.detach()
         with rf("imgcls::comm_wait"):
             scale = self.reducer.finish() if self.reducer is not None else 1.0
         timer.mark("comm_wait")

@@ -41,6 +41,7 @@ MI355X design:
 from __future__ import annotations
 
 import contextlib
+import os
 
 import torch
 import torch.distributed as dist
@@ -97,8 +98,17 @@ class GradReducer:
         self.arena: GradArena | None = None
         # force_collectives (tests): run the bucket collectives even in a world of one
         self._collect = self.world > 1 or force_collectives
+        # diagnostic only (never a benchmark: bench.py relabels its line): no gradient collective at all, to time
+        # a multi-rank step without its gradient all-reduce (ranks sharing one GPU over gloo, where that
+        # all-reduce is a host copy that swamps everything else)
+        if os.environ.get("IMGCLS_DIAG_SKIP_GRAD_COMM", "0") == "1":
+            self._collect = False
         self.rccl = None
         self.watchdog = None
+        # deferred (whole-step HIP-graph replay at N > 1): backward only fills the arena; no collective is
+        # issued from a hook (a gloo / process-group call cannot sit inside a captured graph), and
+        # ``flat_all_reduce`` sums the whole arena once after the replay
+        self.deferred = False
         if comm == "rccl" and self._collect:
             from .rccl import CommWatchdog, RcclComm
             dev = next(iter(self.params)).device
@@ -204,7 +214,7 @@ class GradReducer:
 
     def _launch(self, b: int) -> None:
         self.launched[b] = True
-        if not self._collect:
+        if not self._collect or self.deferred:
             return
         s, e, _ = self.buckets[b]
         t = self.flat[s:e]
@@ -281,6 +291,24 @@ class GradReducer:
                 order = box[0]
             self._build(order)
             self._ready_order = []
+        return 1.0 / self.world
+
+    def reset_after_capture(self) -> None:
+        """Forget the hook bookkeeping of a captured backward (the replays do not run the hooks)."""
+        for p in self.params:  # the slots stay the gradients' storage (the captured kernels write there)
+            p.grad = self.arena.view(self.index[id(p)])
+        self._reset_counts()
+
+    @torch.no_grad()
+    def flat_all_reduce(self) -> float:
+        """After a replayed backward (``deferred``): one all-reduce of the whole gradient arena on the current
+        stream, in place of the per-bucket collectives.  Returns the mean factor for the optimizer."""
+        if self._collect:
+            if self.rccl is not None:
+                self.rccl.all_reduce_(self.flat)
+                self.rccl.join()
+            else:
+                dist.all_reduce(self.flat, group=self.group)
         return 1.0 / self.world
 
     def average_(self) -> None:

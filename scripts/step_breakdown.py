@@ -31,3 +31,36 @@ for r in step:
 print(f"step span {span / 1e6:.3f} ms, kernel busy {busy / 1e6:.3f} ms, launches {len(step)}")
 for k, (t, n) in sorted(agg.items(), key=lambda kv: -kv[1][0]):
     print(f"{t / 1e6:8.3f} ms {n:5d}x  {k}")
+
+# per stream (queue): union of busy intervals, time it runs alone, and its top kernels - the compute stream's
+# busy union is the critical chain; side-stream time that overlaps it is concurrency, not step time
+qkey = next((k for k in ("Stream_Id", "Queue_Id") if step and k in step[0]), None)
+if qkey is not None:
+    def union(iv):
+        iv = sorted(iv)
+        tot, cs, ce = 0, None, None
+        for s, e in iv:
+            if cs is None or s > ce:
+                if cs is not None:
+                    tot += ce - cs
+                cs, ce = s, e
+            else:
+                ce = max(ce, e)
+        return tot + (ce - cs if cs is not None else 0)
+    byq = collections.defaultdict(list)
+    for r in step:
+        byq[r[qkey]].append(r)
+    allu = union([(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in step])
+    print(f"\nper {qkey}: busy union of all streams {allu / 1e6:.3f} ms")
+    for q, rs in sorted(byq.items(), key=lambda kv: -len(kv[1])):
+        iv = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rs]
+        others = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in step if r[qkey] != q]
+        alone = allu - union(others)
+        print(f"  {qkey} {q}: {len(rs)} launches, busy union {union(iv) / 1e6:.3f} ms, alone {alone / 1e6:.3f} ms")
+        qa = collections.defaultdict(lambda: [0, 0])
+        for r in rs:
+            name = re.sub(r"\((?!\)).*", "", r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", ""))[:64]
+            qa[name][0] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            qa[name][1] += 1
+        for k, (t, n) in sorted(qa.items(), key=lambda kv: -kv[1][0])[:12]:
+            print(f"    {t / 1e6:8.3f} ms {n:5d}x  {k}")

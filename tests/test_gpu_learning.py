@@ -25,7 +25,7 @@ def _data(n, size, seed):
     return x, lab
 
 
-def _run(model, size, compute, dtype, steps, batch, lr, train, val):
+def _run(model, size, compute, dtype, steps, batch, lr, train, val, det=False):
     from pytorch_imageclassification_distributed_amd.engine import Trainer, build_parser
     from pytorch_imageclassification_distributed_amd.ops import functional as Fx
     from pytorch_imageclassification_distributed_amd.parallel import init_distributed
@@ -38,7 +38,7 @@ def _run(model, size, compute, dtype, steps, batch, lr, train, val):
     args = ["--synthetic", "--model", model, "--image-size", str(size), "--batchsize", str(batch),
             "--num-classes", str(NC), "--num-workers", "0", "--synthetic-train-size", "8",
             "--synthetic-val-size", "8", "--no-sync-bn", "--lr", str(lr), "--seed", "5",
-            "--compute", compute, "--dtype", dtype]
+            "--compute", compute, "--dtype", dtype] + (["--deterministic"] if det else [])
     try:
         tr = Trainer(build_parser().parse_args(args), ctx)
         # no stochastic regularisation: dropout / drop-connect draw from different RNG streams on the two
@@ -80,6 +80,10 @@ def _run(model, size, compute, dtype, steps, batch, lr, train, val):
     finally:
         Fx.set_backend("auto")
         torch.backends.cudnn.enabled = keep_cudnn
+        if det:
+            from pytorch_imageclassification_distributed_amd.ops import hip
+            hip.set_deterministic(False)
+            torch.backends.cudnn.deterministic = False
 
 
 @pytest.mark.parametrize("model,size,steps,batch,lr", [
@@ -93,7 +97,12 @@ def _run(model, size, compute, dtype, steps, batch, lr, train, val):
 def test_hip_bf16_learns_like_torch_fp32(model, size, steps, batch, lr):
     train = _data(max(steps * batch // 3, 4 * batch), size, seed=11)
     val = _data(256, size, seed=12)
-    lh, acc_h = _run(model, size, "hip", "bf16", steps, batch, lr, train, val)
+    # the HIP side runs deterministically (--deterministic: one contribution per fp32 atomic address), so it is
+    # reproducible bit for bit and the bands below measure only bf16-vs-fp32 rounding, not run-to-run noise
+    lh, acc_h = _run(model, size, "hip", "bf16", steps, batch, lr, train, val, det=True)
+    if model == "resnet18":
+        lh2, acc_h2 = _run(model, size, "hip", "bf16", steps, batch, lr, train, val, det=True)
+        assert torch.equal(lh, lh2) and acc_h == acc_h2, "deterministic HIP training is not reproducible"
     lt, acc_t = _run(model, size, "torch", "fp32", steps, batch, lr, train, val)
     w = max(steps // 5, 5)
     head_h, tail_h = lh[:w].mean().item(), lh[-w:].mean().item()
@@ -110,9 +119,12 @@ def test_hip_bf16_learns_like_torch_fp32(model, size, steps, batch, lr):
     # the two curves agree: windowed means within 0.3 absolute (or 50 %) over the whole run (two differently
     # rounded runs of a random-init network drift apart step by step; measured worst gaps 0.154 resnet18,
     # 0.263 resnet50 in its last window, r6b)
+    gaps = []
     for k in range(0, steps - w + 1, w):
         a, b = lh[k:k + w].mean().item(), lt[k:k + w].mean().item()
-        assert abs(a - b) < max(0.3, 0.5 * b), (k, a, b, msg)
+        gaps.append(round(abs(a - b), 3))
+        assert abs(a - b) < max(0.25, 0.4 * b), (k, a, b, msg)
+    print(f"{model}: windowed |hip - fp32| gaps {gaps}")
     # validation accuracy of a 100-step run swings with the eval-mode BN statistics (measured 0.43-0.82 on
     # one model): the HIP path must not be clearly worse than the reference; being better is not a failure
     assert acc_h > acc_t - 0.25, msg

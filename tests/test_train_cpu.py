@@ -144,14 +144,15 @@ def test_step_throttle_bounds_steps_in_flight(monkeypatch):
 
 
 def test_hip_graph_auto_mode():
-    """--hip-graph on / off / auto: auto replays the step as a graph only for a single process at a per-GPU
-    batch of at most GRAPH_AUTO_MAX_BATCH (where replay measured faster than eager dispatch); the bare flag
+    """--hip-graph on / off / auto: auto replays the step as a graph at a per-GPU batch of at most
+    GRAPH_AUTO_MAX_BATCH (where replay measured faster than eager dispatch), at any world size (N > 1: the
+    Trainer also needs the peer SyncBN transport or SyncBN off, ``Trainer.graph_capable``); the bare flag
     still means on."""
     from pytorch_imageclassification_distributed_amd.engine.config import (GRAPH_AUTO_MAX_BATCH, build_parser,
                                                                            hip_graph_enabled)
     p = build_parser()
     a = p.parse_args(["--batchsize", "4"])
-    assert a.hip_graph == "auto" and hip_graph_enabled(a, 1) and not hip_graph_enabled(a, 2)
+    assert a.hip_graph == "auto" and hip_graph_enabled(a, 1) and hip_graph_enabled(a, 2)
     a = p.parse_args(["--batchsize", str(GRAPH_AUTO_MAX_BATCH + 1)])
     assert not hip_graph_enabled(a, 1)
     a = p.parse_args(["--batchsize", "512", "--hip-graph"])
