@@ -20,7 +20,7 @@ for d in sys.argv[1:]:
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        if not any(t in k for t in ("glds_kernel", "direct_conv", "direct64", "deep_kernel", "Cijk", "conv_pw", "wgrad")):
+        if not any(t in k for t in ("glds_kernel", "direct_conv", "direct64", "deep_kernel", "Cijk", "conv_pw", "wgrad", "fused_bwd", "bn_apply", "bn_bwd", "stem")):
             continue
         kn = k.replace("void (anonymous namespace)::", "").split("(")[0]
         acc[kn][r["Counter_Name"]].append(float(r["Counter_Value"]))
