@@ -1625,6 +1625,208 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_fused_bwd_kernel(const C
       }
 }
 
+// Version 2 of the fused XA backward for CO >= 128 (ResNet-50 layer1 conv3 / downsample: 64 -> 256), round 5.
+// The round-4 kernel streamed dz / y at ~3.4 TB/s with ONE k-step of loads in flight: y came by register loads, and
+// beside LDS-DMAs hipcc waits vmcnt(0) for any VGPR-destination load (cdna_hip_programming.md 5 item 4(b)), so its
+// 3-deep ring drained every step anyway; each wave DMA'd its own copy of every k-step's coefficients; and the
+// tile epilogue was the runtime dispatcher over 18 epilogue bodies, whose register pressure spilled to scratch
+// (~120 B per lane).  Here:
+//   * y arrives by LDS-DMA into its own image of the stage (same per-lane offsets as dz), so every load of the
+//     k-loop is an LDS-DMA and the counted waits keep TWO k-steps in flight across each barrier (3-deep ring);
+//   * the [3][CO] coefficients are staged once per block (they depend on the channel only);
+//   * the epilogue body is a template constant (MODE, chosen on the host by the same rule as epi_mode), and it
+//     stages through the X buffer of the tile it finishes - free from that tile's last k-step until the X load of
+//     the tile two ahead, which is issued NKC - 1 >= 1 steps later - so the ring and both X slots fit 160 KB.
+template <int CO, int MODE>
+__global__ __launch_bounds__(512, 1) void conv_fused_bwd2_kernel(const ConvParams p, const FusedW f) {
+  constexpr int WM = 4, WN = 2, DEPTH = 3;
+  constexpr int TM = 128, BNc = 64, NW = WM * WN;
+  constexpr int WTM = TM / WM, WTN = BNc / WN;
+  constexpr int RM = WTM / 16, RN = WTN / 16;
+  constexpr int AL = TM / 8 / NW, BL = BNc / 8 / NW;
+  constexpr int QM = 64 / WM / 16, QN = 64 / WN / 16;
+  static_assert(AL >= 1 && BL >= 1 && QM >= 1 && QN >= 1, "fused backward mapping");
+  constexpr int A_BYTES = TM * BK * 2, B_BYTES = BNc * BK * 2;
+  constexpr int STAGE = 2 * A_BYTES + B_BYTES;  // dz, y, W^T rows
+  constexpr int NKC = CO / BK;
+  constexpr int EPI = TM * (BNc + 8) * 2 > NW * 2 * BNc * 4 ? TM * (BNc + 8) * 2 : NW * 2 * BNc * 4;
+  constexpr int XSLOT = TM * 128 > EPI ? TM * 128 : EPI;  // an X tile, later the epilogue of its tile
+  constexpr int COEF = 3 * CO * 4;
+  constexpr int RING = DEPTH * STAGE, XOFF = RING, COFF = XOFF + 2 * XSLOT, MAIN = COFF + COEF;
+  static_assert(CO % BK == 0 && NKC >= 2 && CO <= 256 && MAIN <= 160 * 1024, "fused backward v2: CO in {128, 192, 256}");
+  __shared__ __attribute__((aligned(16))) char smem[MAIN];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int lrow = lane >> 3, pch = lane & 7;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int g4 = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
+  const int CA = p.CA;  // == CO
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.A, 2 * p.a_elems);
+  const __amdgpu_buffer_rsrc_t rsZ = make_rsrc(p.xa_y, 2 * p.a_elems);
+  const __amdgpu_buffer_rsrc_t rsB = make_rsrc(p.B, 2 * p.b_elems);
+  const __amdgpu_buffer_rsrc_t rsX = make_rsrc(f.X, 2L * p.M * BNc);
+  float* const s_coef = (float*)(smem + COFF);
+  for (int t = tid; t < 3 * CO; t += 512) s_coef[t] = p.xa_coef[(t / CO) * CA + (t % CO)];
+  unsigned b_row[BL];
+#pragma unroll
+  for (int i = 0; i < BL; ++i) {
+    const int row = wid * (BNc / NW) + i * 8 + lrow;
+    b_row[i] = 2u * (unsigned)(row * p.ldb + (pch ^ ((row >> 1) & 7)) * 8);
+  }
+  auto a_addr = [](int r, int c) { return r * 128 + ((((c >> 3) ^ ((r >> 1) & 7))) << 4) + (c & 7) * 2; };
+
+  f32x4 accw[NKC][QM][QN];
+#pragma unroll
+  for (int c = 0; c < NKC; ++c)
+#pragma unroll
+    for (int i = 0; i < QM; ++i)
+#pragma unroll
+      for (int j = 0; j < QN; ++j) accw[c][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int ntiles = (p.M + TM - 1) / TM;
+  const int my_tiles = blockIdx.x < ntiles ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int nsteps = my_tiles * NKC;
+  __syncthreads();  // coefficients staged
+
+  // LDS-DMA instructions per wave of step s (all loads of the k-loop are LDS-DMAs, so vmcnt counts them)
+  auto nloads = [&](int s) { return s < nsteps ? 2 * AL + BL + ((s % NKC) == 0 ? AL : 0) : 0; };
+  auto issue = [&](int s) __attribute__((always_inline)) {
+    const int t = s / NKC, kc = s - t * NKC;
+    const int m0 = ((int)blockIdx.x + t * (int)gridDim.x) * TM;
+    char* sa = smem + (s % DEPTH) * STAGE;
+    if (kc == 0) {
+      char* sx = smem + XOFF + (t & 1) * XSLOT;
+#pragma unroll
+      for (int i = 0; i < AL; ++i) {
+        const int row = wid * (TM / NW) + i * 8 + lrow;
+        const int m = m0 + row;
+        const unsigned off = m < p.M ? 2u * (unsigned)(m * BNc + (pch ^ ((row >> 1) & 7)) * 8) : OOB;
+        blds16(rsX, off, sx + (wid * (TM / NW) + i * 8) * 128);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      const int row = wid * (TM / NW) + i * 8 + lrow;
+      const int m = m0 + row;
+      const unsigned va = m < p.M ? 2u * (unsigned)(m * CA + kc * BK + (pch ^ ((row >> 1) & 7)) * 8) : OOB;
+      blds16(rsA, va, sa + (wid * (TM / NW) + i * 8) * 128);
+      blds16(rsZ, va, sa + A_BYTES + (wid * (TM / NW) + i * 8) * 128);
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i)
+      blds16(rsB, b_row[i] + 2u * (unsigned)(kc * BK), sa + 2 * A_BYTES + (wid * (BNc / NW) + i * 8) * 128);
+  };
+
+  f32x4 acc[RM][RN];
+  if (nsteps > 0) issue(0);
+  if (nsteps > 1) issue(1);
+  for (int s = 0; s < nsteps; ++s) {
+    const int t = s / NKC, kc = s - t * NKC;
+    const int tile = (int)blockIdx.x + t * (int)gridDim.x, m0 = tile * TM;
+    char* sa = smem + (s % DEPTH) * STAGE;
+    const char* sb = sa + 2 * A_BYTES;
+    char* sx = smem + XOFF + (t & 1) * XSLOT;
+    // step s landed; step s + 1's loads stay in flight (a tile's epilogue stores sit behind them: over-waits once)
+    if (nloads(s + 1) == 2 * AL + BL + AL) wait_vmcnt<2 * AL + BL + AL>();
+    else if (nloads(s + 1) == 2 * AL + BL) wait_vmcnt<2 * AL + BL>();
+    else wait_vmcnt<0>();
+    // this wave's dz pieces -> dY in place (y from the stage's second image); rows past M stay zero
+#pragma unroll
+    for (int gg = 0; gg < 2; ++gg) {
+      const int ch = (pch ^ (((gg * 4 + (lrow >> 1)) & 7))) * 8;
+      const float* kc0 = s_coef + kc * BK + ch;
+      float c0[8], c1[8], c2[8];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        *(f32x4*)(c0 + 4 * h) = *(const f32x4*)(kc0 + 4 * h);
+        *(f32x4*)(c1 + 4 * h) = *(const f32x4*)(kc0 + CO + 4 * h);
+        *(f32x4*)(c2 + 4 * h) = *(const f32x4*)(kc0 + 2 * CO + 4 * h);
+      }
+#pragma unroll
+      for (int i = gg; i < AL; i += 2) {
+        if (m0 + wid * (TM / NW) + i * 8 + lrow >= p.M) continue;
+        uint4* dst = (uint4*)(sa + (wid * (TM / NW) + i * 8) * 128 + lane * 16);
+        const uint4 yv = *(const uint4*)(sa + A_BYTES + (wid * (TM / NW) + i * 8) * 128 + lane * 16);
+        float d[8], y[8];
+        unpack8(*dst, d);
+        unpack8(yv, y);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) d[k] = fmaf(c0[k], d[k], fmaf(c1[k], y[k], c2[k]));
+        *dst = pack8(d);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // step s published; all waves are done with step s - 1's slot, which step s + 2 reuses
+    __builtin_amdgcn_s_barrier();
+    if (s + 2 < nsteps) issue(s + 2);
+    if (kc == 0) {
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[RM], bfg[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i) af[i] = *(const bf16x8*)(sa + swz(wm * WTM + i * 16 + fr, 4 * kk + fq));
+#pragma unroll
+      for (int j = 0; j < RN; ++j) bfg[j] = *(const bf16x8*)(sb + swz(wn * WTN + j * 16 + fr, 4 * kk + fq));
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[j], af[i], acc[i][j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int kk = 0; kk < TM / 32; ++kk) {
+      const int r0 = kk * 32 + 4 * g4 + tq, r1 = r0 + 16;
+      bf16x8 ad[QM], bx[QN];
+#pragma unroll
+      for (int i = 0; i < QM; ++i) {
+        const int c = wm * 16 * QM + i * 16 + tp * 4;
+        const bf16x4 lo = tr_read(sa + a_addr(r0, c)), hi = tr_read(sa + a_addr(r1, c));
+        ad[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int j = 0; j < QN; ++j) {
+        const int c = wn * 16 * QN + j * 16 + tp * 4;
+        const bf16x4 lo = tr_read(sx + a_addr(r0, c)), hi = tr_read(sx + a_addr(r1, c));
+        bx[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int c = 0; c < NKC; ++c) {
+        if (c != kc) continue;
+#pragma unroll
+        for (int i = 0; i < QM; ++i)
+#pragma unroll
+          for (int j = 0; j < QN; ++j)
+            accw[c][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx[j], ad[i], accw[c][i][j], 0, 0, 0);
+      }
+    }
+    if (kc == NKC - 1) {
+      // the tile's X slot turns into its epilogue tile: every wave has read X (its wgrad fragments) first
+      __builtin_amdgcn_s_barrier();
+      if constexpr (MODE >= 0)
+        conv_epi<TM, BNc, WM, WN, (MODE < 0 ? 0 : MODE), 1>(p, acc, sx, tid, lane, wid, wm, wn, m0, 0, tile);
+      else
+        conv_epilogue_dispatch<TM, BNc, WM, WN, 1>(p, acc, sx, tid, lane, wid, wm, wn, m0, 0, tile, p.GH * p.GW);
+    }
+  }
+  float* slab = f.ws + (long)blockIdx.x * CO * BNc;
+#pragma unroll
+  for (int c = 0; c < NKC; ++c)
+#pragma unroll
+    for (int i = 0; i < QM; ++i)
+#pragma unroll
+      for (int j = 0; j < QN; ++j) {
+        const int co = c * 64 + wm * 16 * QM + i * 16 + fr, ci = wn * 16 * QN + j * 16 + fq * 4;
+        *(f32x4*)(slab + (long)co * BNc + ci) = accw[c][i][j];
+      }
+}
+
 // The same fusion for 64 output channels and CI = 128 / 256 input channels (ResNet layer1 conv1: 256 -> 64):
 // K = 64 is one k-step, so a tile's dY (dz + y -> dY in LDS, double-buffered by tile) is formed once and the
 // data gradient's CI columns are walked in 64-column chunks; each (tile, chunk) step streams its weight rows
@@ -1817,10 +2019,46 @@ static int launch_fused_bwd_n(const ConvParams& p, const FusedW& f, float* dW, i
 // the 2-deep ring stays the default; IMGCLS_FUSED_DEPTH=3 selects the other
 static const int g_fused_depth = getenv("IMGCLS_FUSED_DEPTH") ? atoi(getenv("IMGCLS_FUSED_DEPTH")) : 2;
 
+// version 2 (conv_fused_bwd2_kernel) for CO >= 128 unless IMGCLS_FUSED_V2=0
+static const int g_fused_v2 = getenv("IMGCLS_FUSED_V2") ? atoi(getenv("IMGCLS_FUSED_V2")) : 1;
+
+// the epilogue body epi_mode() picks on the device, on the host
+static int host_epi_mode(const ConvParams& p) {
+  if (p.bias != nullptr) return EP_GENERIC;
+  const bool direct = (p.so == 1 && p.oh0 == 0 && p.ow0 == 0 && p.GH == p.OH && p.GW == p.OW);
+  int m = direct ? EP_DIRECT : 0;
+  if (p.stats != nullptr) {
+    if (p.addend != nullptr || p.bwd_y != nullptr) return EP_GENERIC;
+    return m | EP_STATS;
+  }
+  if (p.addend != nullptr) m |= EP_ADD;
+  if (p.bwd_y != nullptr) {
+    if (p.bwd_act != ACT_RELU) return EP_GENERIC;
+    m |= EP_BWD | EP_RELU | (p.bwd_mask != nullptr ? EP_MASK : p.bwd_res != nullptr ? EP_RES : 0);
+  }
+  return m;
+}
+
+template <int CO>
+static void launch_fused_bwd2(const ConvParams& p, const FusedW& f, int blocks, hipStream_t stream) {
+#define FB2(M_) hipLaunchKernelGGL((conv_fused_bwd2_kernel<CO, M_>), dim3(blocks), dim3(512), 0, stream, p, f)
+  switch (host_epi_mode(p)) {
+    case EP_BWD | EP_RELU | EP_DIRECT: FB2(EP_BWD | EP_RELU | EP_DIRECT); break;
+    case EP_BWD | EP_RELU | EP_MASK | EP_DIRECT: FB2(EP_BWD | EP_RELU | EP_MASK | EP_DIRECT); break;
+    case EP_BWD | EP_RELU | EP_ADD | EP_DIRECT: FB2(EP_BWD | EP_RELU | EP_ADD | EP_DIRECT); break;
+    case EP_ADD | EP_DIRECT: FB2(EP_ADD | EP_DIRECT); break;
+    case EP_DIRECT: FB2(EP_DIRECT); break;
+    default: FB2(-1); break;  // any other feature set: the runtime dispatcher
+  }
+#undef FB2
+}
+
 template <int CO>
 static int launch_fused_bwd(const ConvParams& p, const FusedW& f, float* dW, int blocks, hipStream_t stream) {
   if constexpr (CO >= 128) {
-    if (g_fused_depth == 3)
+    if (g_fused_v2)
+      launch_fused_bwd2<CO>(p, f, blocks, stream);
+    else if (g_fused_depth == 3)
       hipLaunchKernelGGL((conv_fused_bwd_kernel<CO, 4, 2, 3>), dim3(blocks), dim3(512), 0, stream, p, f);
     else
       hipLaunchKernelGGL((conv_fused_bwd_kernel<CO, 4, 2>), dim3(blocks), dim3(512), 0, stream, p, f);

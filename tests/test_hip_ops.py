@@ -1239,6 +1239,11 @@ def _xa_block(hip, n, cin, hw, cmid, stride, act, use_res, xa_on, cfg=None, wsta
     (3, 64, 15, 192, 1, "silu", False, 1),   # odd pixel count, SiLU
     (4, 64, 14, 64, 1, "relu", False, 3),    # bn2-like: 3x3 dgrad, padded taps masked
     (4, 128, 15, 128, 2, "relu", False, 3),  # 3x3 stride 2: sub-pixel phases, odd input
+    # 64 input channels: the one-pass fused dgrad + wgrad kernel (conv_fused_bwd2 for 128 / 192 / 256 outputs) on
+    # maps large enough that every persistent block walks several tiles (X slots alternate, epilogues in them)
+    (8, 64, 112, 128, 1, "relu", False, 1),
+    (8, 64, 112, 192, 1, "relu", True, 1),
+    (6, 64, 113, 256, 1, None, True, 1),
 ])
 def test_bn_backward_fused_into_producer_conv(case):
     """dgrad / wgrad with the fused BN-backward operand map against the unfused path (bn_bwd_elemt + plain
