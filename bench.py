@@ -44,7 +44,7 @@ def parse():
     p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=10)
     # 1024 per GPU (44 GiB of the 288 GB HBM3E): +4-5 % img/s over 512 on one GPU (fuller last waves on the
-    # 14x14 / 7x7 layers, per-step fixed costs amortised; profiles/r4g_b1024_tuning_runs.txt) and half the
+    # 14x14 / 7x7 layers, per-step fixed costs amortised; profiles/history/r4g_b1024_tuning_runs.txt) and half the
     # share of per-step SyncBN / all-reduce latency at N>1; the reference stack is measured at the same
     # batch (benchmarks/reference_stack.json)
     p.add_argument("--batch", type=int, default=1024, help="per-GPU batch")

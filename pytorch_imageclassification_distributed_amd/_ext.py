@@ -28,5 +28,15 @@ def load():
             from . import build as _build
             _build.build()
         import torch  # noqa: F401  (libtorch symbols must be loaded first)
+        alt = os.environ.get("IMGCLS_EXT", "")
+        if alt:  # same-box A/B of a compile-time variant (build.py --out NAME -DFLAG=...): load that file as _C
+            import importlib.util
+            import sys
+            path = alt if os.path.isabs(alt) else os.path.join(here, alt)
+            spec = importlib.util.spec_from_file_location(__package__ + "._C", path)
+            _C = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(_C)
+            sys.modules[__package__ + "._C"] = _C
+            return _C
         _C = importlib.import_module(__package__ + "._C")
         return _C

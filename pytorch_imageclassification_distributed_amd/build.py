@@ -82,14 +82,20 @@ def _check_loadable(path: str) -> None:
         raise RuntimeError(f"linked module does not load:\n{r.stderr[-2000:]}")
 
 
-def build(verbose: bool = False, jobs: int | None = None) -> str:
+def build(verbose: bool = False, jobs: int | None = None, defines: dict | None = None, out: str | None = None) -> str:
+    """Compile and link the extension.  ``defines`` {source basename: [-D...]} adds compile-time switches to
+    those kernel sources only and ``out`` names another library in the package directory: a variant build
+    for a same-box A/B (loaded with IMGCLS_EXT=<name>, _ext.py)."""
+    OUT = os.path.join(PKG, out) if out else globals()["OUT"]
     os.makedirs(BUILD, exist_ok=True)
     cflags, ldflags = _torch_flags()
     kernels = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     binds = sorted(glob.glob(os.path.join(CSRC, "*.cpp")))
     jobs = jobs or min(8, os.cpu_count() or 4)
+    defines = defines or {}
     with cf.ThreadPoolExecutor(jobs) as ex:
-        futs = [ex.submit(_compile, k, KERNEL_FLAGS, verbose) for k in kernels]
+        futs = [ex.submit(_compile, k, KERNEL_FLAGS + defines.get(os.path.basename(k), []), verbose)
+                for k in kernels]
         futs += [ex.submit(_compile, b, cflags, verbose) for b in binds]
         objs = [f.result() for f in futs]
     key = hashlib.sha1(" ".join(objs).encode()).hexdigest()[:16]
@@ -110,4 +116,12 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
 
 
 if __name__ == "__main__":
-    print(build(verbose="-v" in sys.argv))
+    # python build.py [-v] [--out NAME.so SOURCE.hip:-DFLAG=V ...]  (variant build for an A/B)
+    args = [a for a in sys.argv[1:] if a != "-v"]
+    out, defs = None, {}
+    if args and args[0] == "--out":
+        out = args[1]
+        for spec in args[2:]:
+            src, flag = spec.split(":", 1)
+            defs.setdefault(src, []).append(flag)
+    print(build(verbose="-v" in sys.argv, defines=defs, out=out))

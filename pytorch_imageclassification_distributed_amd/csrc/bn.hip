@@ -247,7 +247,7 @@ constexpr int BN_U = 4;
 
 // 16-B row loads / stores of the streaming elementwise passes, optionally non-temporal: streams of
 // tensors far larger than the 256 MB Infinity Cache gain from the hint (scripts/probes/stream_bw.hip,
-// profiles/r5b_stream_bw.txt: block-contiguous walk, 4 blocks per CU, nt: 6.24 TB/s read-1-write-1 and
+// profiles/r12b_stream_bw.txt: block-contiguous walk, 4 blocks per CU, nt: 6.24 TB/s read-1-write-1 and
 // 6.07 read-2-write-1, against 5.3-5.4 at 8192 blocks without it)
 typedef unsigned int bn_u32x4 __attribute__((ext_vector_type(4)));
 template <bool NT>
@@ -702,7 +702,7 @@ __global__ void bn_bwd_k_kernel(const double* __restrict__ sums, const double* _
 
 // channel-fixed mapping as bn_apply_kernel: five (six with an activation) per-channel coefficient
 // vectors per thread instead of per 16-byte vector - at C >= 512 those loads were the bound
-// (3.5-4.6 TB/s against 4.7-6 TB/s at C <= 256, profiles/r1c_bn_elementwise_bandwidth_b512.txt)
+// (3.5-4.6 TB/s against 4.7-6 TB/s at C <= 256, profiles/history/r1c_bn_elementwise_bandwidth_b512.txt)
 __global__ void bn_bwd_elemt_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ y,
                                     const float* __restrict__ coef, const float* __restrict__ kk,
                                     const bf16_t* __restrict__ res, const bf16_t* __restrict__ dz_in,
@@ -814,7 +814,7 @@ static int g_reduce_blocks = getenv("IMGCLS_BN_REDUCE_BLOCKS") ? atoi(getenv("IM
 // (C/8 itself below 8; 32 when none divides), so a block ends in 2 x 64 .. 2 x 256 partial-row atomics
 // whatever C is.  With all C/8 chunks in one block (the former layout) a C = 2048 layer issued 4096
 // atomics per block and the reduce ran atomic-bound at 1.2 TB/s: 123 -> 42 us at batch 256
-// (profiles/r1d_bn_reduce_chunk_sweep_b256.txt); a divisor keeps every lane of every slice busy.
+// (profiles/history/r1d_bn_reduce_chunk_sweep_b256.txt); a divisor keeps every lane of every slice busy.
 static int g_reduce_chb = 0;
 
 int auto_chb(int cch) {
@@ -866,7 +866,7 @@ int grid_chan(long rows, int C) {
 
 // Streaming elementwise passes (bn_apply_u / bn_bwd_elemt_u with the block-contiguous walk): grid capped at
 // g_bn_grid blocks (4 per CU: each block streams one long contiguous run; 8192 blocks measured 5.3 TB/s
-// against 6.0-6.2 at 1024, profiles/r5b_stream_bw.txt) and non-temporal accesses on tensors of at least
+// against 6.0-6.2 at 1024, profiles/r12b_stream_bw.txt) and non-temporal accesses on tensors of at least
 // g_bn_nt_mb MiB (IMGCLS_BN_NT_MB; 0 = never, < 0 = always)
 int g_bn_grid = getenv("IMGCLS_BN_GRID") ? atoi(getenv("IMGCLS_BN_GRID")) : 1024;
 long g_bn_nt_mb = getenv("IMGCLS_BN_NT_MB") ? atol(getenv("IMGCLS_BN_NT_MB")) : 256;

@@ -352,6 +352,15 @@ DEVI void conv_epi(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16]
 
 // UR: rows of operands in flight per thread - 2 where the launch bound leaves >= 200 VGPRs, else 1 (two
 // rows of four 16-B operands plus the BN-backward coefficients cost ~150 VGPRs)
+//
+// epi_ur(OCC): the UR of a GEMM kernel sized for OCC waves per SIMD.  With 256 VGPRs per lane (OCC <= 2: the
+// 256 x 256 8-wave tiles) the accumulators are dead by the time the epilogue streams the tile out, so it keeps
+// IMGCLS_EPI_UR_WIDE rows in flight.  4 spilled 140 B per lane in the 256 x 256 kernels (the 18-body dispatch
+// keeps the accumulators' registers allocated), so the default stays 2 (no scratch in any 256 x 256 kernel).
+#ifndef IMGCLS_EPI_UR_WIDE
+#define IMGCLS_EPI_UR_WIDE 2
+#endif
+constexpr int epi_ur(int occ) { return 512 / occ >= 256 ? IMGCLS_EPI_UR_WIDE : 512 / occ >= 200 ? 2 : 1; }
 template <int TM, int BN, int WM, int WN, int UR, bool STAGED = false>
 DEVI void conv_epilogue_dispatch(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16], char* smem, int tid,
                                  int lane, int wid, int wm, int wn, int m0, int n0, int bm, int ghw) {
@@ -414,7 +423,7 @@ struct GldsCfg {
                                   4 * (TM / 8 / NW) + 2 * (BN / 8 / NW) + 48;
   static constexpr int OCC_REG = 512 / EST_VGPR < 1 ? 1 : 512 / EST_VGPR;
   // PR & 2 (lean): one fragment buffer instead of two, register budget of 4 waves per SIMD - more
-  // co-resident blocks to cover the 1-stage ring's load round trip (profiles/r5e_conv_pmc_b1024.txt)
+  // co-resident blocks to cover the 1-stage ring's load round trip (profiles/history/r5e_conv_pmc_b1024.txt)
   static constexpr int OCC = (PR & 2) ? (OCC_LDS < 4 ? OCC_LDS : 4) : (OCC_LDS < OCC_REG ? OCC_LDS : OCC_REG);
 };
 

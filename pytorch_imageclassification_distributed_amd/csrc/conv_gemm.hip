@@ -522,7 +522,7 @@ void conv_gemm_glds_kernel(const ConvParams p) {
     }
   }
   __syncthreads();
-  conv_epilogue_dispatch<TM, BN, WM, WN, (512 / Cfg::OCC >= 200 ? 2 : 1)>(p, acc, smem, tid, lane, wid, wm, wn, m0, n0, bm, ghw);
+  conv_epilogue_dispatch<TM, BN, WM, WN, epi_ur(Cfg::OCC)>(p, acc, smem, tid, lane, wid, wm, wn, m0, n0, bm, ghw);
 }
 
 // ---------------------------------------------------------------------------
@@ -2152,10 +2152,10 @@ static const ConvCfg g_cfgs[] = {
     // pieces per MFMA than 128 x 128 without the half-empty 256 x 256 tile (appended: find-db indices stay)
     CFG(256, 128, 4, 2, 1), CFG(256, 128, 4, 2, 2), CFGP(256, 128, 4, 2, 2),
     // 1-stage 128 x 128 on 8 waves (64 x 32 per wave): 4 waves per SIMD instead of the 4-wave tile's 3, more
-    // loads in flight per CU for the same LDS-DMA bytes per block (profiles/r5e_conv_pmc_b1024.txt)
+    // loads in flight per CU for the same LDS-DMA bytes per block (profiles/history/r5e_conv_pmc_b1024.txt)
     CFG(128, 128, 4, 2, 1), CFG(128, 128, 2, 4, 1), CFGL(128, 128, 2, 2, 1),
     // (measured and dropped: 256 x 128 / 128 x 256 tiles with a 3-deep ring, 1028-1029 TF at 4096^3 /
-    // 8192^3 against 1245 / 1151 for 256 x 256 with 2 stages - profiles/r2r_gemm_ref_3stage.txt)
+    // 8192^3 against 1245 / 1151 for 256 x 256 with 2 stages - profiles/history/r2r_gemm_ref_3stage.txt)
 };
 #undef CFG
 #undef CFGP

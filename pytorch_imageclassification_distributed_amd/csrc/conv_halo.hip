@@ -3,7 +3,7 @@
 //
 // The LDS-DMA implicit GEMM (conv_gemm.hip) gathers its A operand once per tap: a 3x3 conv moves every
 // input element from L2 to LDS nine times per output-channel tile, and the counters put its MFMAs at
-// 39-46 % busy, parked on those loads (profiles/r5e_conv_pmc_b1024.txt).  Here a block's TM output pixels
+// 39-46 % busy, parked on those loads (profiles/history/r5e_conv_pmc_b1024.txt).  Here a block's TM output pixels
 // are consecutive in the flattened (image, row, column) order, so for a tap (dh, dw) their input pixels
 // are the SAME consecutive run shifted by dh * W + dw.  One 64-channel patch of TM + 2W + 2 input rows
 // therefore serves all taps of that channel chunk: the k loop runs (chunk outer, tap inner), the patch is
@@ -202,7 +202,7 @@ void conv_halo_kernel(const ConvParams p) {
     if (++ct == T) { ct = 0; ++cc; }
   }
   __syncthreads();
-  conv_epilogue_dispatch<TM, BN, WM, WN, (512 / Cfg::OCC >= 200 ? 2 : 1)>(p, acc, smem, tid, lane, wid, wm, wn, m0, n0,
+  conv_epilogue_dispatch<TM, BN, WM, WN, epi_ur(Cfg::OCC)>(p, acc, smem, tid, lane, wid, wm, wn, m0, n0,
                                                                           bm, p.GH * p.GW);
 }
 

@@ -4,7 +4,7 @@
 // input xs [N, H2, W2, 16] (ops/hip.py, "space-to-depth stem").  As an implicit GEMM every output
 // pixel re-gathers its 4x4x16 input window (K = 256), so the input is fetched 16x over from L2 and a
 // 128-pixel tile moves 64 KB of im2col rows into LDS for 16 KB of output: the GEMM form ran at
-// 1.8 TB/s, far from both the MFMA and the HBM roofline (profiles/r1d_stem_conv_b512.txt).
+// 1.8 TB/s, far from both the MFMA and the HBM roofline (profiles/history/r1d_stem_conv_b512.txt).
 //
 // Here a persistent block keeps the whole weight (64 x 256 bf16) in LDS and walks 8 x 16-pixel output
 // tiles; each tile stages only its (8+3) x (16+3)-pixel input patch (halo included) in LDS, double
@@ -19,7 +19,7 @@
 // across all of the block's tiles; one partial row per block at the end (atomic add into row
 // block % G, as the GEMM epilogue does).
 //
-// Measured at batch 512 (profiles/r1d_stem_conv_b512.txt): 623 us (GEMM form + statistics) -> 339 us.
+// Measured at batch 512 (profiles/history/r1d_stem_conv_b512.txt): 623 us (GEMM form + statistics) -> 339 us.
 // The kernel is bound by its 822 MB of output stores: without them it runs in 81 us, without its
 // MFMAs in the full time; staging the output through LDS for 16-byte stores gained 6 %.
 #include "common.h"

@@ -98,7 +98,7 @@ def build_parser() -> argparse.ArgumentParser:
                         "at N > 1 forward + backward with the SyncBN peer exchanges, then one flat gradient "
                         "all-reduce and Adam); a batch of another shape runs eagerly.  auto = on at per-GPU "
                         f"batch <= {GRAPH_AUTO_MAX_BATCH} (Inception-v3 @299: b4 466 vs 164 img/s eager, b32 "
-                        "2943 vs 1978; at b128 eager wins, profiles/r6_bench_host_data_and_inception_small_batch.jsonl)")
+                        "2943 vs 1978; at b128 eager wins, profiles/history/r6_bench_host_data_and_inception_small_batch.jsonl)")
     return p
 
 

@@ -49,7 +49,7 @@ from .optim import FusedAdam, MultiStepLR
 
 # training steps the host may have enqueued ahead of the GPU (Trainer._throttle; 0 = unbounded).  Unset: 2, or
 # 4 when a step's peak allocation is under SMALL_STEP_FRACTION of the device (the host-bound small-memory
-# steps gain from the deeper queue - Inception-v3 b256 8323 -> 8400 img/s, profiles/r7d_* - and their cache
+# steps gain from the deeper queue - Inception-v3 b256 8323 -> 8400 img/s, profiles/history/r7d_* - and their cache
 # stays small; ResNet-50 b1024 at 44 GiB keeps 2)
 MAX_INFLIGHT_STEPS = int(os.environ.get("IMGCLS_MAX_INFLIGHT_STEPS", "-1"))
 SMALL_STEP_FRACTION = 0.1

@@ -138,7 +138,7 @@ XF_MAX_REP = int(os.environ.get("IMGCLS_XF_MAX_REP", "2"))
 # the weight gradient then reads dY plainly instead of re-forming it from dz and y in every column tile
 # (the fused wgrads ran VALU-bound at 10-20 % MFMA busy).  Same bytes (one dY write on the
 # compute stream against one fewer tensor read on the side stream), no replicated transform.
-# ResNet-50 b1024, same box, 2 rounds each: 13904 / 13942 img/s without, 14240 / 14221 with (profiles/r5b_xa_out_ab.txt)
+# ResNet-50 b1024, same box, 2 rounds each: 13904 / 13942 img/s without, 14240 / 14221 with (profiles/r12b_xa_out_ab.txt)
 XA_OUT = os.environ.get("IMGCLS_XA_OUT", "1") == "1"
 XA_OUT_COUNT = [0]
 
@@ -193,7 +193,7 @@ def xa_eligible(x, conv) -> bool:
 # feeds one conv hands that conv its input y and its [scale | shift] instead of writing act(bn(y)); the
 # conv's forward and weight-gradient kernels form act(scale * y + shift) on their operand loads, padded taps
 # kept at zero.  The activated tensor is never written or re-read (VERDICT round 2, item 1 "forward").
-# Off by default: measured on ResNet-50 b1024 (profiles/r5f_fusion_ab.txt) it does not pay - the bn_apply passes
+# Off by default: measured on ResNet-50 b1024 (profiles/history/r5f_fusion_ab.txt) it does not pay - the bn_apply passes
 # it removes are small (the non-residual ones were 3.5 ms of the 77 ms step) and a 3x3 consumer re-applies the
 # map once per tap
 FUSE_XF = os.environ.get("IMGCLS_BN_XF", "0") == "1"

@@ -251,7 +251,7 @@ def conv_cfgs():
 _HALO_CFGS = None
 HALO_CONV = os.environ.get("IMGCLS_HALO", "1") == "1"  # halo-patch 3x3 kernels as tuner candidates
 # entries the tuner times: only the 256 x 256 tile beat the LDS-DMA implicit GEMM on a ResNet-50 b1024 shape
-# (512-channel 7x7: 266 vs 279 us); the others lost 1.3-2x (profiles/r6b_halo_probe_b1024.txt)
+# (512-channel 7x7: 266 vs 279 us); the others lost 1.3-2x (profiles/history/r6b_halo_probe_b1024.txt)
 HALO_TUNE = tuple(int(v) for v in os.environ.get("IMGCLS_HALO_TUNE", "6").split(",") if v)
 HALO_FORCE = None  # tests: force a halo variant on every eligible launch
 HALO_COUNT = [0]   # halo-kernel launches (tests)
@@ -517,7 +517,7 @@ def _conv_forward_fp8(x, w_param, g: ConvGeom, stats, bias, out, c_off, shift=No
 FUSED_XA_BWD = os.environ.get("IMGCLS_FUSED_BWD", "1") == "1"
 FUSED_XA_BWD_COUNT = [0]  # fused dgrad + wgrad launches (tests / diagnostics)
 # the 64-output form (layer1 conv1: dgrad columns walked in 64-channel chunks) measured slower than the separate
-# launches (ResNet-50 b1024 13344-13358 vs 13589-13626 img/s with only the 64-input form, profiles/r7n_*): off
+# launches (ResNet-50 b1024 13344-13358 vs 13589-13626 img/s with only the 64-input form, profiles/history/r7n_*): off
 FUSED_XA_BWD_N = os.environ.get("IMGCLS_FUSED_BWD_N", "0") == "1"
 _CU_COUNT: dict = {}
 
@@ -717,7 +717,7 @@ def _wgrad_config(dy, x, g: ConvGeom, m, ntot, xa=None, xf=None):
             if g.Co >= 256:
                 cands += [(cand, 12) for cand in blocks if cand <= 1024]
         # (64 / 128 x 256 four-wave tiles, reading the narrow layers' dY half as often, were 5-70 % slower
-        # on every ResNet-50 shape: profiles/r4d_wgrad_wide_tiles_probe.txt)
+        # on every ResNet-50 shape: profiles/history/r4d_wgrad_wide_tiles_probe.txt)
     if fx or ff:
         cands = [(cand, st) for cand, st in cands if _wgrad_has(st, fx, ff)]
     for cand, st in cands:

@@ -29,7 +29,7 @@ from .gemm import ConvGeom, _wgrad_plan
 WGRAD_STREAM = os.environ.get("IMGCLS_WGRAD_STREAM", "1") == "1"
 # inside a HIP-graph capture the weight gradients stay on the capturing stream: a two-stream capture
 # (event fork / join edges) replays 2x slower than the single-stream one on this ROCm runtime
-# (Inception-v3 b128: 3303 vs 6523 img/s, profiles/r3g_hip_graph_modes.txt); IMGCLS_GRAPH_SIDE=1 forks
+# (Inception-v3 b128: 3303 vs 6523 img/s, profiles/history/r3g_hip_graph_modes.txt); IMGCLS_GRAPH_SIDE=1 forks
 GRAPH_SIDE = os.environ.get("IMGCLS_GRAPH_SIDE", "0") == "1"
 _SIDE: dict = {}  # device index -> _SideStream
 
@@ -126,7 +126,7 @@ def conv_wgrad_raw(dy, x, w_param, g: ConvGeom, xa=None, xf=None):
     if dw is not None:
         # padded input channels = the network's input layer, the last weight gradient of backward: on the
         # compute stream (idle by then) it runs beside the side stream's backlog instead of behind it - the
-        # ResNet-50 b1024 stem wgrad is ~0.7 ms of the step tail (profiles/r5e_conv_roofline_b1024.txt)
+        # ResNet-50 b1024 stem wgrad is ~0.7 ms of the step tail (profiles/history/r5e_conv_roofline_b1024.txt)
         if STEM_WGRAD_SIDE:
             def launch():
                 _gemm._wgrad_launch(dy, x, full, g, m, ntot, kps, splits, stages)

@@ -1,6 +1,6 @@
 """Per-candidate weight-gradient timings (split target x kernel variant) for the narrow-Cout ResNet-50
 layers at batch 512, from the tuner's own timing loop (ops/hip.py _wgrad_config -> WGRAD_TUNE_LOG).
-Variants (at the time of profiles/r4d_wgrad_wide_tiles_probe.txt): 1 / 2 = 64|128 x 128 tile, 1- / 2-stage
+Variants (at the time of profiles/history/r4d_wgrad_wide_tiles_probe.txt): 1 / 2 = 64|128 x 128 tile, 1- / 2-stage
 ring, 3 = 8-wave in-block pixel split,
 8 = 4-deep ring of 32-pixel stages, 10 / 11 = 64 x 256, 12 / 13 = 128 x 256."""
 import sys

@@ -26,7 +26,7 @@ def _worker(rank, world, port, out_dir, name="resnet18", damp=True, det=False, d
     # Fixed kernel choices (shape heuristic, one weight-gradient plan) in every process: ResNet-50 train-mode
     # gradients at random init are chaotic - 0.1 % fp32 weight noise alone drops some BN-bias gradient
     # cosines to 0.14-0.28 on the CPU fp32 path (scripts/cpu_weight_noise.py,
-    # profiles/r2_cpu_weight_noise_resnet50.txt) - so per-process timed tuner picks (two ranks contending
+    # profiles/history/r2_cpu_weight_noise_resnet50.txt) - so per-process timed tuner picks (two ranks contending
     # for one GPU time the candidates differently) made the comparison flaky (scripts/tune_random_choices.py).
     os.environ.update(IMGCLS_CONV_STAGES="0", IMGCLS_WGRAD_BLOCKS="512", IMGCLS_WGRAD_STAGES="2",
                       IMGCLS_DIRECT_CONV="1" if direct else "0")

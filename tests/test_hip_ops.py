@@ -1253,7 +1253,9 @@ def test_bn_backward_fused_into_producer_conv(case):
     o0, g0, k0 = _xa_block(hip, n, cin, hw, cmid, stride, act, use_res, False, k=k)
     o1, g1, k1 = _xa_block(hip, n, cin, hw, cmid, stride, act, use_res, True, k=k)
     assert k0 == 0 and k1 >= 1, (k0, k1)
-    assert torch.equal(o0, o1)
+    # (the forward is the same code both times; on maps of many blocks its BN statistics are summed by fp32
+    # atomics in arrival order, so the two forwards agree to rounding, not bitwise)
+    assert rel_err(o1, o0) < 1e-2 and mean_err(o1, o0) < 1e-3
     for a_, b_ in zip(g1, g0):
         assert rel_err(a_, b_) < 2e-2, rel_err(a_, b_)
         assert mean_err(a_, b_) < 5e-3, mean_err(a_, b_)
