@@ -30,11 +30,11 @@ def load():
         import torch  # noqa: F401  (libtorch symbols must be loaded first)
         alt = os.environ.get("IMGCLS_EXT", "")
         if alt:  # same-box A/B of a compile-time variant (build.py --out NAME -DFLAG=...): load that file as _C
-            import importlib.util
+            import importlib.util as _ilu
             import sys
             path = alt if os.path.isabs(alt) else os.path.join(here, alt)
-            spec = importlib.util.spec_from_file_location(__package__ + "._C", path)
-            _C = importlib.util.module_from_spec(spec)
+            spec = _ilu.spec_from_file_location(__package__ + "._C", path)
+            _C = _ilu.module_from_spec(spec)
             spec.loader.exec_module(_C)
             sys.modules[__package__ + "._C"] = _C
             return _C
