@@ -349,6 +349,96 @@ __global__ __launch_bounds__(256) void bn_apply_u_kernel(const bf16_t* __restric
   }
 }
 
+// Flat streaming form (round 5): one 16-B vector per thread, one 256-vector tile per block, ceil(vectors / 256)
+// blocks - the whole grid sweeps memory in address order.  On random data (scripts/probes/stream_bw.hip,
+// profiles/r12e_stream_bw_random.txt) that pattern streams 6.16 TB/s read-1-write-1 and 5.91 read-2-write-1; the
+// block-contiguous walk above reached 5.0-5.3 there (its 6+ TB/s in r12b came from constant-filled buffers).
+// Coefficients are per-thread cache hits (a C-float table).
+struct FlatIdx {
+  int shift;  // log2(C / 8) when C / 8 is a power of two, else -1
+  int cch;
+};
+DEVI void flat_pos(long i, const FlatIdx& f, long& row, int& c0) {
+  if (f.shift >= 0) {
+    row = i >> f.shift;
+    c0 = (int)(i & (f.cch - 1)) * 8;
+  } else {
+    row = i / f.cch;
+    c0 = (int)(i - row * f.cch) * 8;
+  }
+}
+
+template <bool RES, bool NT, int ACT>
+__global__ __launch_bounds__(256) void bn_apply_flat_kernel(const bf16_t* __restrict__ y, const float* __restrict__ coef,
+                                                            const bf16_t* __restrict__ res, bf16_t* __restrict__ out,
+                                                            long nvec, FlatIdx fi, int C, int ldo, int c_off,
+                                                            uint8_t* __restrict__ mask) {
+  const long i = blockIdx.x * 256L + threadIdx.x;
+  if (i >= nvec) return;
+  long row;
+  int c0;
+  flat_pos(i, fi, row, c0);
+  const uint4 yv = ldrow<NT>(y + row * C + c0);
+  uint4 rv;
+  if constexpr (RES) rv = ldrow<NT>(res + row * C + c0);
+  float sc[8], sh[8], v[8], rr[8];
+  load8f(coef + c0, sc);
+  load8f(coef + C + c0, sh);
+  unpack8(yv, v);
+  if constexpr (RES) unpack8(rv, rr);
+  unsigned mk = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float z = v[k] * sc[k] + sh[k];
+    if constexpr (RES) z += rr[k];
+    mk |= (z > 0.f ? 1u : 0u) << k;
+    v[k] = apply_act(z, ACT);
+  }
+  strow<NT>(out + row * ldo + c_off + c0, pack8(v));
+  if (mask) mask[i] = (uint8_t)mk;  // byte i = row * C/8 + c0/8
+}
+
+template <int MODE, bool NT, int ACT>
+__global__ __launch_bounds__(256) void bn_bwd_elemt_flat_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ y,
+                                                                 const float* __restrict__ coef, const float* __restrict__ kk,
+                                                                 const bf16_t* __restrict__ res, const bf16_t* __restrict__ dz_in,
+                                                                 bf16_t* __restrict__ dy, long nvec, FlatIdx fi, int C, int ldg) {
+  const long i = blockIdx.x * 256L + threadIdx.x;
+  if (i >= nvec) return;
+  long row;
+  int c0;
+  flat_pos(i, fi, row, c0);
+  const uint4 yr = ldrow<NT>(y + row * C + c0);
+  const uint4 gr = MODE == 0 ? ldrow<NT>(dz_in + row * C + c0) : ldrow<NT>(g + row * ldg + c0);
+  uint4 rr;
+  if constexpr (MODE == 2) rr = ldrow<NT>(res + row * C + c0);
+  float sc[8], mu[8], is[8], k1[8], k2[8], gv[8], yv[8];
+  load8f(coef + c0, sc);
+  load8f(coef + 2 * C + c0, mu);
+  load8f(coef + 3 * C + c0, is);
+  load8f(kk + c0, k1);
+  load8f(kk + C + c0, k2);
+  unpack8(yr, yv);
+  unpack8(gr, gv);
+  if constexpr (MODE == 1 || MODE == 2) {
+    float sh[8], rv[8];
+    load8f(coef + C + c0, sh);
+    if constexpr (MODE == 2) unpack8(rr, rv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float z = yv[k] * sc[k] + sh[k];
+      if constexpr (MODE == 2) z += rv[k];
+      gv[k] = act_grad(z, gv[k], ACT);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float xhat = (yv[k] - mu[k]) * is[k];
+    gv[k] = sc[k] * (gv[k] - k1[k] - xhat * k2[k]);
+  }
+  strow<NT>(dy + row * C + c0, pack8(gv));
+}
+
 // apply + MX-FP8 copy of the output for the fp8 forward convolution that consumes it (no separate
 // quantisation pass): the 4 lanes of a 32-channel block are consecutive lanes (C % 32 == 0), the
 // grid stride is a multiple of 4, so the block max is two xor-shuffles away.
@@ -854,7 +944,18 @@ int grid_for(long work, int per_block = 256, int cap = 4096) {
 int g_bn_unroll = 1;  // U-row elementwise kernels (bn_set_unroll; A/B and tests)
 // row walk of the U-row apply / backward-elementwise kernels: 1 = block-contiguous runs (row_walk), 0 = the
 // grid-wide stride (IMGCLS_BN_WALK=0, same-box A/B)
-int g_bn_walk = getenv("IMGCLS_BN_WALK") ? atoi(getenv("IMGCLS_BN_WALK")) : 1;
+// 2 = the flat one-vector-per-thread form (bn_apply_flat / bn_bwd_elemt_flat, the default since round 5)
+int g_bn_walk = getenv("IMGCLS_BN_WALK") ? atoi(getenv("IMGCLS_BN_WALK")) : 2;
+
+FlatIdx flat_idx(int C) {
+  const int cch = C / 8;
+  int sh = -1;
+  if ((cch & (cch - 1)) == 0) {
+    sh = 0;
+    while ((1 << sh) < cch) ++sh;
+  }
+  return FlatIdx{sh, cch};
+}
 
 int grid_chan(long rows, int C) {
   const int cch = C / 8;
@@ -874,7 +975,7 @@ long g_bn_nt_mb = getenv("IMGCLS_BN_NT_MB") ? atol(getenv("IMGCLS_BN_NT_MB")) : 
 int grid_stream(long rows, int C) {
   const int cch = C / 8;
   const int b = grid_chan(rows, C);
-  if (g_bn_grid <= 0 || !g_bn_walk || cch <= 0 || 256 % cch) return b;  // grid-stride walk: keep grid_chan's
+  if (g_bn_grid <= 0 || cch <= 0 || (g_bn_walk == 1 && 256 % cch)) return b;  // cap the U kernels' grid
   return b < g_bn_grid ? b : g_bn_grid;
 }
 
@@ -942,7 +1043,24 @@ int bn_apply_launch(const bf16_t* y, const float* coef, const bf16_t* res, bf16_
     HIP_CHECK_LAUNCH();
     return 0;
   }
-  if (g_bn_unroll || mask) {
+  if (g_bn_walk == 2 && (g_bn_unroll || mask)) {
+    const long nvec = rows * (long)(C / 8);
+    const dim3 gf((unsigned)((nvec + 255) / 256));
+    const FlatIdx fi = flat_idx(C);
+#define FAPPLY(R, N, A) \
+  hipLaunchKernelGGL((bn_apply_flat_kernel<R, N, A>), gf, dim3(256), 0, s, y, coef, res, out, nvec, fi, C, ldo, c_off, mask)
+#define FAPPLY_ACT(R, N)                                  \
+  do {                                                    \
+    if (act == ACT_RELU) FAPPLY(R, N, ACT_RELU);          \
+    else if (act == ACT_SILU) FAPPLY(R, N, ACT_SILU);     \
+    else FAPPLY(R, N, ACT_NONE);                          \
+  } while (0)
+    const bool nt = use_nt(rows, C);
+    if (res) { if (nt) FAPPLY_ACT(true, true); else FAPPLY_ACT(true, false); }
+    else { if (nt) FAPPLY_ACT(false, true); else FAPPLY_ACT(false, false); }
+#undef FAPPLY_ACT
+#undef FAPPLY
+  } else if (g_bn_unroll || mask) {
     const dim3 gr(grid_stream(rows, C));
 #define APPLY(R, N, A)                                                                                          \
   hipLaunchKernelGGL((bn_apply_u_kernel<R, N, A>), gr, dim3(256), 0, s, y, coef, res, out, rows, C, ldo, c_off, act, \
@@ -1002,7 +1120,28 @@ int bn_bwd_elemt_launch(const bf16_t* g, const bf16_t* y, const float* coef, con
                         const bf16_t* res, const bf16_t* dz_in, bf16_t* dy, long rows, int C, int act,
                         int ldg, hipStream_t s) {
   const int lg = ldg > 0 ? ldg : C;
-  if (g_bn_unroll) {
+  if (g_bn_unroll && g_bn_walk == 2) {
+    const long nvec = rows * (long)(C / 8);
+    const dim3 gf((unsigned)((nvec + 255) / 256));
+    const FlatIdx fi = flat_idx(C);
+#define FBWD(M, NT_, A)                                                                                          \
+  hipLaunchKernelGGL((bn_bwd_elemt_flat_kernel<M, NT_, A>), gf, dim3(256), 0, s, g, y, coef, k, res, dz_in, dy, nvec, \
+                     fi, C, lg)
+#define FBWD_ACT(M, NT_)                                                         \
+  do {                                                                           \
+    if (act == ACT_SILU) FBWD(M, NT_, ACT_SILU); else FBWD(M, NT_, ACT_RELU);    \
+  } while (0)
+    const int mode = dz_in ? 0 : act == ACT_NONE ? 3 : res ? 2 : 1;
+    if (use_nt(rows, C)) {
+      if (mode == 0) FBWD(0, true, ACT_NONE); else if (mode == 3) FBWD(3, true, ACT_NONE);
+      else if (mode == 2) FBWD_ACT(2, true); else FBWD_ACT(1, true);
+    } else {
+      if (mode == 0) FBWD(0, false, ACT_NONE); else if (mode == 3) FBWD(3, false, ACT_NONE);
+      else if (mode == 2) FBWD_ACT(2, false); else FBWD_ACT(1, false);
+    }
+#undef FBWD_ACT
+#undef FBWD
+  } else if (g_bn_unroll) {
     const dim3 gr(grid_stream(rows, C));
 #define BWD_ELEMT(M, NT_, A)                                                                                       \
   hipLaunchKernelGGL((bn_bwd_elemt_u_kernel<M, NT_, A>), gr, dim3(256), 0, s, g, y, coef, k, res, dz_in, dy, rows, C, \
@@ -1063,7 +1202,8 @@ void bn_set_reduce_blocks(int n, int chb) {
 void bn_set_unroll(int v) { g_bn_unroll = v; }
 
 // streaming elementwise passes: grid cap (<= 0: grid_chan's) and non-temporal threshold in MiB (0 never, < 0 always)
-void bn_set_stream(int grid, long nt_mb) {
+void bn_set_stream(int grid, long nt_mb, int walk) {
   g_bn_grid = grid;
   g_bn_nt_mb = nt_mb;
+  if (walk >= 0) g_bn_walk = walk;
 }

@@ -1554,8 +1554,9 @@ def test_input_u8_resnet_forward_matches_fp32_input():
 @pytest.mark.parametrize("rows,c", [(4099, 256), (1000, 2048), (777, 64), (301, 1152)])
 def test_bn_streaming_passes_every_grid_and_nt(rows, c):
     """bn_apply (+residual +ReLU mask, and plain) and bn_bwd_elemt (all four modes) under every streaming setting
-    (grid capped at 64 / 1024 / grid_chan's, non-temporal never / always) against fp32 torch: the grid and the
-    cache hint change the walk and the access form, never a value - all settings are bitwise identical."""
+    (flat one-vector-per-thread form; U-row kernels with the block-contiguous or grid-stride walk, grid capped at
+    64 / 1024 / grid_chan's; non-temporal never / always) against fp32 torch: the walk, grid and cache hint change
+    the access pattern, never a value - all settings are bitwise identical."""
     hip = _hip()
     torch.manual_seed(5)
     y = bf(torch.randn(rows, c, device=DEV) * 2).to(torch.bfloat16)
@@ -1577,8 +1578,9 @@ def test_bn_streaming_passes_every_grid_and_nt(rows, c):
     want_bwd = {0: elemt(gf), 1: elemt(gf * (yf * sc + sh > 0)), 2: elemt(gf * (z_res > 0)), 3: elemt(gf)}
     outs = []
     try:
-        for grid, nt in ((1024, 256), (0, 0), (1024, -1), (64, -1), (64, 0)):
-            hip.C.bn_set_stream(grid, nt)
+        for grid, nt, walk in ((1024, 256, 2), (1024, -1, 2), (1024, 256, 1), (0, 0, 1), (1024, -1, 1), (64, -1, 1),
+                               (64, 0, 0)):
+            hip.C.bn_set_stream(grid, nt, walk)
             o1 = torch.empty_like(y)
             mask = torch.zeros(rows * c // 8, dtype=torch.uint8, device=DEV)
             hip.C.bn_apply(y, coef, res, o1, rows, c, c, 0, 1, None, None, mask=mask)
@@ -1595,10 +1597,10 @@ def test_bn_streaming_passes_every_grid_and_nt(rows, c):
             bits = torch.stack([(mask >> k) & 1 for k in range(8)], 1).view(rows, c).bool()
             assert torch.equal(bits, z_res.view(rows, c) > 0) or (bits != (z_res > 0)).float().mean() < 1e-4
             for mode in range(4):
-                assert rel_err(bw[mode].float(), want_bwd[mode]) < 1e-2, (grid, nt, mode)
+                assert rel_err(bw[mode].float(), want_bwd[mode]) < 1e-2, (grid, nt, walk, mode)
             outs.append([o1, o2, mask] + [bw[m] for m in range(4)])
     finally:
-        hip.C.bn_set_stream(1024, 256)
+        hip.C.bn_set_stream(1024, 256, 2)
     for o in outs[1:]:
         for a_, b_ in zip(o, outs[0]):
             assert torch.equal(a_, b_)
