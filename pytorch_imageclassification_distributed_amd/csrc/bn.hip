@@ -355,13 +355,18 @@ __global__ __launch_bounds__(256) void bn_apply_u_kernel(const bf16_t* __restric
 // block-contiguous walk above reached 5.0-5.3 there (its 6+ TB/s in r12b came from constant-filled buffers).
 // Coefficients are per-thread cache hits (a C-float table).
 struct FlatIdx {
-  int shift;  // log2(C / 8) when C / 8 is a power of two, else -1
+  int shift;  // log2(C / 8) when C / 8 is a power of two; -1: 32-bit multiply-shift division; -2: 64-bit division
   int cch;
+  FastDiv fd;
 };
 DEVI void flat_pos(long i, const FlatIdx& f, long& row, int& c0) {
   if (f.shift >= 0) {
     row = i >> f.shift;
     c0 = (int)(i & (f.cch - 1)) * 8;
+  } else if (f.shift == -1) {  // the software 64-bit division cost EfficientNet's C = 144 / 240 / 672 / 1152 passes 3 %
+    const uint32_t q = fdiv((uint32_t)i, f.fd);
+    row = q;
+    c0 = (int)((uint32_t)i - q * (uint32_t)f.cch) * 8;
   } else {
     row = i / f.cch;
     c0 = (int)(i - row * f.cch) * 8;
@@ -947,14 +952,20 @@ int g_bn_unroll = 1;  // U-row elementwise kernels (bn_set_unroll; A/B and tests
 // 2 = the flat one-vector-per-thread form (bn_apply_flat / bn_bwd_elemt_flat, the default since round 5)
 int g_bn_walk = getenv("IMGCLS_BN_WALK") ? atoi(getenv("IMGCLS_BN_WALK")) : 2;
 
-FlatIdx flat_idx(int C) {
+// the backward elementwise pass reads five coefficient vectors per 16-B vector (six with the activation): in the
+// flat form those per-thread cache hits cost more than the sweep order gains (EfficientNet-B0 b1024: 13.1 vs
+// 12.1 ms of bn_bwd_elemt per step, profiles/r12g_bn_walk_per_kernel.txt), so it keeps the U-row walk unless
+// IMGCLS_BN_WALK_BWD says otherwise
+int g_bn_walk_bwd = getenv("IMGCLS_BN_WALK_BWD") ? atoi(getenv("IMGCLS_BN_WALK_BWD")) : 1;
+
+FlatIdx flat_idx(long nvec, int C) {
   const int cch = C / 8;
-  int sh = -1;
-  if ((cch & (cch - 1)) == 0) {
+  int sh = nvec < (1l << 32) ? -1 : -2;
+  if (cch > 0 && (cch & (cch - 1)) == 0) {
     sh = 0;
     while ((1 << sh) < cch) ++sh;
   }
-  return FlatIdx{sh, cch};
+  return FlatIdx{sh, cch, make_fastdiv((uint32_t)(cch > 0 ? cch : 1))};
 }
 
 int grid_chan(long rows, int C) {
@@ -965,17 +976,17 @@ int grid_chan(long rows, int C) {
   return (b + m - 1) / m * m;
 }
 
-// Streaming elementwise passes (bn_apply_u / bn_bwd_elemt_u with the block-contiguous walk): grid capped at
-// g_bn_grid blocks (4 per CU: each block streams one long contiguous run; 8192 blocks measured 5.3 TB/s
-// against 6.0-6.2 at 1024, profiles/r12b_stream_bw.txt) and non-temporal accesses on tensors of at least
-// g_bn_nt_mb MiB (IMGCLS_BN_NT_MB; 0 = never, < 0 = always)
+// Streaming elementwise passes.  The U-row kernels (walk 0 / 1) cap their grid at g_bn_grid blocks (4 per CU,
+// IMGCLS_BN_GRID).  All forms use non-temporal accesses on tensors of at least g_bn_nt_mb MiB (IMGCLS_BN_NT_MB;
+// 0 = never, < 0 = always, the default: with the flat walk always-nt measured +0.2 % ResNet-50, +0.4 %
+// Inception-v3, +0.6 % EfficientNet-B0 over a 256 MiB threshold, profiles/r12f_bn_flat_walk_ab.txt)
 int g_bn_grid = getenv("IMGCLS_BN_GRID") ? atoi(getenv("IMGCLS_BN_GRID")) : 1024;
-long g_bn_nt_mb = getenv("IMGCLS_BN_NT_MB") ? atol(getenv("IMGCLS_BN_NT_MB")) : 256;
+long g_bn_nt_mb = getenv("IMGCLS_BN_NT_MB") ? atol(getenv("IMGCLS_BN_NT_MB")) : -1;
 
-int grid_stream(long rows, int C) {
+int grid_stream(long rows, int C, int walk) {
   const int cch = C / 8;
   const int b = grid_chan(rows, C);
-  if (g_bn_grid <= 0 || cch <= 0 || (g_bn_walk == 1 && 256 % cch)) return b;  // cap the U kernels' grid
+  if (g_bn_grid <= 0 || cch <= 0 || (walk == 1 && 256 % cch)) return b;  // cap the U kernels' grid
   return b < g_bn_grid ? b : g_bn_grid;
 }
 
@@ -1046,7 +1057,7 @@ int bn_apply_launch(const bf16_t* y, const float* coef, const bf16_t* res, bf16_
   if (g_bn_walk == 2 && (g_bn_unroll || mask)) {
     const long nvec = rows * (long)(C / 8);
     const dim3 gf((unsigned)((nvec + 255) / 256));
-    const FlatIdx fi = flat_idx(C);
+    const FlatIdx fi = flat_idx(nvec, C);
 #define FAPPLY(R, N, A) \
   hipLaunchKernelGGL((bn_apply_flat_kernel<R, N, A>), gf, dim3(256), 0, s, y, coef, res, out, nvec, fi, C, ldo, c_off, mask)
 #define FAPPLY_ACT(R, N)                                  \
@@ -1061,7 +1072,7 @@ int bn_apply_launch(const bf16_t* y, const float* coef, const bf16_t* res, bf16_
 #undef FAPPLY_ACT
 #undef FAPPLY
   } else if (g_bn_unroll || mask) {
-    const dim3 gr(grid_stream(rows, C));
+    const dim3 gr(grid_stream(rows, C, g_bn_walk));
 #define APPLY(R, N, A)                                                                                          \
   hipLaunchKernelGGL((bn_apply_u_kernel<R, N, A>), gr, dim3(256), 0, s, y, coef, res, out, rows, C, ldo, c_off, act, \
                      mask, g_bn_walk)
@@ -1120,10 +1131,11 @@ int bn_bwd_elemt_launch(const bf16_t* g, const bf16_t* y, const float* coef, con
                         const bf16_t* res, const bf16_t* dz_in, bf16_t* dy, long rows, int C, int act,
                         int ldg, hipStream_t s) {
   const int lg = ldg > 0 ? ldg : C;
-  if (g_bn_unroll && g_bn_walk == 2) {
+  const int walk = g_bn_walk == 2 ? g_bn_walk_bwd : g_bn_walk;
+  if (g_bn_unroll && walk == 2) {
     const long nvec = rows * (long)(C / 8);
     const dim3 gf((unsigned)((nvec + 255) / 256));
-    const FlatIdx fi = flat_idx(C);
+    const FlatIdx fi = flat_idx(nvec, C);
 #define FBWD(M, NT_, A)                                                                                          \
   hipLaunchKernelGGL((bn_bwd_elemt_flat_kernel<M, NT_, A>), gf, dim3(256), 0, s, g, y, coef, k, res, dz_in, dy, nvec, \
                      fi, C, lg)
@@ -1142,10 +1154,10 @@ int bn_bwd_elemt_launch(const bf16_t* g, const bf16_t* y, const float* coef, con
 #undef FBWD_ACT
 #undef FBWD
   } else if (g_bn_unroll) {
-    const dim3 gr(grid_stream(rows, C));
+    const dim3 gr(grid_stream(rows, C, walk));
 #define BWD_ELEMT(M, NT_, A)                                                                                       \
   hipLaunchKernelGGL((bn_bwd_elemt_u_kernel<M, NT_, A>), gr, dim3(256), 0, s, g, y, coef, k, res, dz_in, dy, rows, C, \
-                     act, lg, g_bn_walk)
+                     act, lg, walk)
 #define BWD_ACT(M, NT_)                                                             \
   do {                                                                              \
     if (act == ACT_SILU) BWD_ELEMT(M, NT_, ACT_SILU); else BWD_ELEMT(M, NT_, ACT_RELU); \
@@ -1202,8 +1214,9 @@ void bn_set_reduce_blocks(int n, int chb) {
 void bn_set_unroll(int v) { g_bn_unroll = v; }
 
 // streaming elementwise passes: grid cap (<= 0: grid_chan's) and non-temporal threshold in MiB (0 never, < 0 always)
-void bn_set_stream(int grid, long nt_mb, int walk) {
+void bn_set_stream(int grid, long nt_mb, int walk, int walk_bwd) {
   g_bn_grid = grid;
   g_bn_nt_mb = nt_mb;
   if (walk >= 0) g_bn_walk = walk;
+  if (walk_bwd >= 0) g_bn_walk_bwd = walk_bwd;
 }
