@@ -373,75 +373,101 @@ DEVI void flat_pos(long i, const FlatIdx& f, long& row, int& c0) {
   }
 }
 
-template <bool RES, bool NT, int ACT>
+// U > 1: each thread also takes the vectors 256, 512, .. further on (a block owns 256 * U consecutive vectors),
+// which share its channel chunk when C / 8 divides 256 - one coefficient load per U vectors
+template <bool RES, bool NT, int ACT, int U>
 __global__ __launch_bounds__(256) void bn_apply_flat_kernel(const bf16_t* __restrict__ y, const float* __restrict__ coef,
                                                             const bf16_t* __restrict__ res, bf16_t* __restrict__ out,
                                                             long nvec, FlatIdx fi, int C, int ldo, int c_off,
                                                             uint8_t* __restrict__ mask) {
-  const long i = blockIdx.x * 256L + threadIdx.x;
-  if (i >= nvec) return;
+  const long i0 = blockIdx.x * (256L * U) + threadIdx.x;
+  if (i0 >= nvec) return;
   long row;
   int c0;
-  flat_pos(i, fi, row, c0);
-  const uint4 yv = ldrow<NT>(y + row * C + c0);
-  uint4 rv;
-  if constexpr (RES) rv = ldrow<NT>(res + row * C + c0);
-  float sc[8], sh[8], v[8], rr[8];
+  flat_pos(i0, fi, row, c0);
+  const long rstep = U > 1 ? (256 >> fi.shift) : 0;  // rows between vector i and i + 256 (C / 8 divides 256)
+  uint4 yv[U], rv[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long r = i0 + u * 256L < nvec ? row + u * rstep : row;
+    yv[u] = ldrow<NT>(y + r * C + c0);
+    if constexpr (RES) rv[u] = ldrow<NT>(res + r * C + c0);
+  }
+  float sc[8], sh[8];
   load8f(coef + c0, sc);
   load8f(coef + C + c0, sh);
-  unpack8(yv, v);
-  if constexpr (RES) unpack8(rv, rr);
-  unsigned mk = 0;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    float z = v[k] * sc[k] + sh[k];
-    if constexpr (RES) z += rr[k];
-    mk |= (z > 0.f ? 1u : 0u) << k;
-    v[k] = apply_act(z, ACT);
+  for (int u = 0; u < U; ++u) {
+    if (i0 + u * 256L >= nvec) break;
+    const long r = row + u * rstep;
+    float v[8], rr[8];
+    unpack8(yv[u], v);
+    if constexpr (RES) unpack8(rv[u], rr);
+    unsigned mk = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float z = v[k] * sc[k] + sh[k];
+      if constexpr (RES) z += rr[k];
+      mk |= (z > 0.f ? 1u : 0u) << k;
+      v[k] = apply_act(z, ACT);
+    }
+    strow<NT>(out + r * ldo + c_off + c0, pack8(v));
+    if (mask) mask[i0 + u * 256L] = (uint8_t)mk;  // byte i = row * C/8 + c0/8
   }
-  strow<NT>(out + row * ldo + c_off + c0, pack8(v));
-  if (mask) mask[i] = (uint8_t)mk;  // byte i = row * C/8 + c0/8
 }
 
-template <int MODE, bool NT, int ACT>
+// U vectors per thread as bn_apply_flat_kernel (the launcher takes U > 1 only when C / 8 divides 256, so the
+// five or six coefficient vectors are loaded once per U data vectors)
+template <int MODE, bool NT, int ACT, int U>
 __global__ __launch_bounds__(256) void bn_bwd_elemt_flat_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ y,
                                                                  const float* __restrict__ coef, const float* __restrict__ kk,
                                                                  const bf16_t* __restrict__ res, const bf16_t* __restrict__ dz_in,
                                                                  bf16_t* __restrict__ dy, long nvec, FlatIdx fi, int C, int ldg) {
-  const long i = blockIdx.x * 256L + threadIdx.x;
-  if (i >= nvec) return;
+  const long i0 = blockIdx.x * (256L * U) + threadIdx.x;
+  if (i0 >= nvec) return;
   long row;
   int c0;
-  flat_pos(i, fi, row, c0);
-  const uint4 yr = ldrow<NT>(y + row * C + c0);
-  const uint4 gr = MODE == 0 ? ldrow<NT>(dz_in + row * C + c0) : ldrow<NT>(g + row * ldg + c0);
-  uint4 rr;
-  if constexpr (MODE == 2) rr = ldrow<NT>(res + row * C + c0);
-  float sc[8], mu[8], is[8], k1[8], k2[8], gv[8], yv[8];
+  flat_pos(i0, fi, row, c0);
+  const long rstep = U > 1 ? (256 >> fi.shift) : 0;
+  uint4 yr[U], gr[U], rr[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long r = i0 + u * 256L < nvec ? row + u * rstep : row;
+    yr[u] = ldrow<NT>(y + r * C + c0);
+    gr[u] = MODE == 0 ? ldrow<NT>(dz_in + r * C + c0) : ldrow<NT>(g + r * ldg + c0);
+    if constexpr (MODE == 2) rr[u] = ldrow<NT>(res + r * C + c0);
+  }
+  float sc[8], sh[8], mu[8], is[8], k1[8], k2[8];
   load8f(coef + c0, sc);
   load8f(coef + 2 * C + c0, mu);
   load8f(coef + 3 * C + c0, is);
   load8f(kk + c0, k1);
   load8f(kk + C + c0, k2);
-  unpack8(yr, yv);
-  unpack8(gr, gv);
-  if constexpr (MODE == 1 || MODE == 2) {
-    float sh[8], rv[8];
-    load8f(coef + C + c0, sh);
-    if constexpr (MODE == 2) unpack8(rr, rv);
+  if constexpr (MODE == 1 || MODE == 2) load8f(coef + C + c0, sh);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (i0 + u * 256L >= nvec) break;
+    const long r = row + u * rstep;
+    float gv[8], yv[8];
+    unpack8(yr[u], yv);
+    unpack8(gr[u], gv);
+    if constexpr (MODE == 1 || MODE == 2) {
+      float rv[8];
+      if constexpr (MODE == 2) unpack8(rr[u], rv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float z = yv[k] * sc[k] + sh[k];
+        if constexpr (MODE == 2) z += rv[k];
+        gv[k] = act_grad(z, gv[k], ACT);
+      }
+    }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      float z = yv[k] * sc[k] + sh[k];
-      if constexpr (MODE == 2) z += rv[k];
-      gv[k] = act_grad(z, gv[k], ACT);
+      const float xhat = (yv[k] - mu[k]) * is[k];
+      gv[k] = sc[k] * (gv[k] - k1[k] - xhat * k2[k]);
     }
+    strow<NT>(dy + r * C + c0, pack8(gv));
   }
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const float xhat = (yv[k] - mu[k]) * is[k];
-    gv[k] = sc[k] * (gv[k] - k1[k] - xhat * k2[k]);
-  }
-  strow<NT>(dy + row * C + c0, pack8(gv));
 }
 
 // apply + MX-FP8 copy of the output for the fp8 forward convolution that consumes it (no separate
@@ -952,11 +978,16 @@ int g_bn_unroll = 1;  // U-row elementwise kernels (bn_set_unroll; A/B and tests
 // 2 = the flat one-vector-per-thread form (bn_apply_flat / bn_bwd_elemt_flat, the default since round 5)
 int g_bn_walk = getenv("IMGCLS_BN_WALK") ? atoi(getenv("IMGCLS_BN_WALK")) : 2;
 
-// the backward elementwise pass reads five coefficient vectors per 16-B vector (six with the activation): in the
-// flat form those per-thread cache hits cost more than the sweep order gains (EfficientNet-B0 b1024: 13.1 vs
-// 12.1 ms of bn_bwd_elemt per step, profiles/r12g_bn_walk_per_kernel.txt), so it keeps the U-row walk unless
-// IMGCLS_BN_WALK_BWD says otherwise
-int g_bn_walk_bwd = getenv("IMGCLS_BN_WALK_BWD") ? atoi(getenv("IMGCLS_BN_WALK_BWD")) : 1;
+// the backward elementwise pass reads five coefficient vectors per 16-B vector (six with the activation): one
+// vector per thread, those per-thread cache hits cost more than the sweep order gains (EfficientNet-B0 b1024:
+// 13.1 vs 12.1 ms of bn_bwd_elemt per step, profiles/r12g_bn_walk_per_kernel.txt).  So walk 2 is the flat form
+// with g_bn_flat_u_bwd vectors per thread when C / 8 divides 256 (one coefficient load per 4 vectors; +0.25 %
+// ResNet-50, +0.3 % EfficientNet-B0, profiles/r12i_bn_bwd_flat_u_ab.txt) and the U-row kernel otherwise
+int g_bn_walk_bwd = getenv("IMGCLS_BN_WALK_BWD") ? atoi(getenv("IMGCLS_BN_WALK_BWD")) : 2;
+int g_bn_flat_u_bwd = getenv("IMGCLS_BN_FLAT_U_BWD") ? atoi(getenv("IMGCLS_BN_FLAT_U_BWD")) : 4;
+
+// vectors per thread of the flat apply when C / 8 divides 256 (IMGCLS_BN_FLAT_U: 1, 2 or 4)
+int g_bn_flat_u = getenv("IMGCLS_BN_FLAT_U") ? atoi(getenv("IMGCLS_BN_FLAT_U")) : 1;
 
 FlatIdx flat_idx(long nvec, int C) {
   const int cch = C / 8;
@@ -1056,10 +1087,18 @@ int bn_apply_launch(const bf16_t* y, const float* coef, const bf16_t* res, bf16_
   }
   if (g_bn_walk == 2 && (g_bn_unroll || mask)) {
     const long nvec = rows * (long)(C / 8);
-    const dim3 gf((unsigned)((nvec + 255) / 256));
+    const int cch = C / 8;
+    const int fu = (cch > 0 && 256 % cch == 0) ? g_bn_flat_u : 1;
+    const dim3 gf((unsigned)((nvec + 256L * fu - 1) / (256L * fu)));
     const FlatIdx fi = flat_idx(nvec, C);
-#define FAPPLY(R, N, A) \
-  hipLaunchKernelGGL((bn_apply_flat_kernel<R, N, A>), gf, dim3(256), 0, s, y, coef, res, out, nvec, fi, C, ldo, c_off, mask)
+#define FAPPLY_U(R, N, A, U_) \
+  hipLaunchKernelGGL((bn_apply_flat_kernel<R, N, A, U_>), gf, dim3(256), 0, s, y, coef, res, out, nvec, fi, C, ldo, c_off, mask)
+#define FAPPLY(R, N, A)                  \
+  do {                                   \
+    if (fu == 4) FAPPLY_U(R, N, A, 4);   \
+    else if (fu == 2) FAPPLY_U(R, N, A, 2); \
+    else FAPPLY_U(R, N, A, 1);           \
+  } while (0)
 #define FAPPLY_ACT(R, N)                                  \
   do {                                                    \
     if (act == ACT_RELU) FAPPLY(R, N, ACT_RELU);          \
@@ -1071,6 +1110,7 @@ int bn_apply_launch(const bf16_t* y, const float* coef, const bf16_t* res, bf16_
     else { if (nt) FAPPLY_ACT(false, true); else FAPPLY_ACT(false, false); }
 #undef FAPPLY_ACT
 #undef FAPPLY
+#undef FAPPLY_U
   } else if (g_bn_unroll || mask) {
     const dim3 gr(grid_stream(rows, C, g_bn_walk));
 #define APPLY(R, N, A)                                                                                          \
@@ -1131,14 +1171,27 @@ int bn_bwd_elemt_launch(const bf16_t* g, const bf16_t* y, const float* coef, con
                         const bf16_t* res, const bf16_t* dz_in, bf16_t* dy, long rows, int C, int act,
                         int ldg, hipStream_t s) {
   const int lg = ldg > 0 ? ldg : C;
-  const int walk = g_bn_walk == 2 ? g_bn_walk_bwd : g_bn_walk;
-  if (g_bn_unroll && walk == 2) {
+  // walk 2: the flat form with U vectors per thread when C / 8 divides 256 (one coefficient load per U
+  // vectors); other channel counts keep the U-row kernel (per-vector coefficient loads cost more than the
+  // sweep order gains, EfficientNet-B0: profiles/r12g_bn_walk_per_kernel.txt).  3 = flat for every C.
+  int walk = g_bn_walk == 2 ? g_bn_walk_bwd : g_bn_walk;
+  const int cch = C / 8;
+  const bool div256 = cch > 0 && 256 % cch == 0;
+  if (walk == 2 && !div256) walk = 1;
+  if (g_bn_unroll && walk >= 2) {
     const long nvec = rows * (long)(C / 8);
-    const dim3 gf((unsigned)((nvec + 255) / 256));
+    const int fu = div256 ? g_bn_flat_u_bwd : 1;
+    const dim3 gf((unsigned)((nvec + 256L * fu - 1) / (256L * fu)));
     const FlatIdx fi = flat_idx(nvec, C);
-#define FBWD(M, NT_, A)                                                                                          \
-  hipLaunchKernelGGL((bn_bwd_elemt_flat_kernel<M, NT_, A>), gf, dim3(256), 0, s, g, y, coef, k, res, dz_in, dy, nvec, \
-                     fi, C, lg)
+#define FBWD_U(M, NT_, A, U_)                                                                                         \
+  hipLaunchKernelGGL((bn_bwd_elemt_flat_kernel<M, NT_, A, U_>), gf, dim3(256), 0, s, g, y, coef, k, res, dz_in, dy, \
+                     nvec, fi, C, lg)
+#define FBWD(M, NT_, A)                       \
+  do {                                        \
+    if (fu == 4) FBWD_U(M, NT_, A, 4);        \
+    else if (fu == 2) FBWD_U(M, NT_, A, 2);   \
+    else FBWD_U(M, NT_, A, 1);                \
+  } while (0)
 #define FBWD_ACT(M, NT_)                                                         \
   do {                                                                           \
     if (act == ACT_SILU) FBWD(M, NT_, ACT_SILU); else FBWD(M, NT_, ACT_RELU);    \
@@ -1153,6 +1206,7 @@ int bn_bwd_elemt_launch(const bf16_t* g, const bf16_t* y, const float* coef, con
     }
 #undef FBWD_ACT
 #undef FBWD
+#undef FBWD_U
   } else if (g_bn_unroll) {
     const dim3 gr(grid_stream(rows, C, walk));
 #define BWD_ELEMT(M, NT_, A)                                                                                       \
@@ -1214,7 +1268,9 @@ void bn_set_reduce_blocks(int n, int chb) {
 void bn_set_unroll(int v) { g_bn_unroll = v; }
 
 // streaming elementwise passes: grid cap (<= 0: grid_chan's) and non-temporal threshold in MiB (0 never, < 0 always)
-void bn_set_stream(int grid, long nt_mb, int walk, int walk_bwd) {
+void bn_set_stream(int grid, long nt_mb, int walk, int walk_bwd, int flat_u, int flat_u_bwd) {
+  if (flat_u > 0) g_bn_flat_u = flat_u;
+  if (flat_u_bwd > 0) g_bn_flat_u_bwd = flat_u_bwd;
   g_bn_grid = grid;
   g_bn_nt_mb = nt_mb;
   if (walk >= 0) g_bn_walk = walk;

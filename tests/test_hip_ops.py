@@ -1578,9 +1578,11 @@ def test_bn_streaming_passes_every_grid_and_nt(rows, c):
     want_bwd = {0: elemt(gf), 1: elemt(gf * (yf * sc + sh > 0)), 2: elemt(gf * (z_res > 0)), 3: elemt(gf)}
     outs = []
     try:
-        for grid, nt, walk, wb in ((1024, -1, 2, 1), (1024, 256, 2, 2), (1024, -1, 2, 2), (1024, 256, 1, 1),
-                                   (0, 0, 1, 1), (1024, -1, 1, 1), (64, -1, 1, 1), (64, 0, 0, 0)):
-            hip.C.bn_set_stream(grid, nt, walk, wb)
+        for grid, nt, walk, wb, fu in ((1024, -1, 2, 1, 1), (1024, -1, 2, 1, 2), (1024, 0, 2, 1, 4),
+                                       (1024, 256, 2, 2, 1), (1024, -1, 2, 2, 2), (1024, -1, 2, 2, 4),
+                                       (1024, -1, 2, 3, 1), (1024, -1, 2, 3, 4), (1024, 256, 1, 1, 1),
+                                       (0, 0, 1, 1, 1), (1024, -1, 1, 1, 1), (64, -1, 1, 1, 1), (64, 0, 0, 0, 1)):
+            hip.C.bn_set_stream(grid, nt, walk, wb, fu, fu)
             o1 = torch.empty_like(y)
             mask = torch.zeros(rows * c // 8, dtype=torch.uint8, device=DEV)
             hip.C.bn_apply(y, coef, res, o1, rows, c, c, 0, 1, None, None, mask=mask)
@@ -1597,10 +1599,10 @@ def test_bn_streaming_passes_every_grid_and_nt(rows, c):
             bits = torch.stack([(mask >> k) & 1 for k in range(8)], 1).view(rows, c).bool()
             assert torch.equal(bits, z_res.view(rows, c) > 0) or (bits != (z_res > 0)).float().mean() < 1e-4
             for mode in range(4):
-                assert rel_err(bw[mode].float(), want_bwd[mode]) < 1e-2, (grid, nt, walk, wb, mode)
+                assert rel_err(bw[mode].float(), want_bwd[mode]) < 1e-2, (grid, nt, walk, wb, fu, mode)
             outs.append([o1, o2, mask] + [bw[m] for m in range(4)])
     finally:
-        hip.C.bn_set_stream(1024, -1, 2, 1)  # the defaults
+        hip.C.bn_set_stream(1024, -1, 2, 2, 1, 4)  # the defaults
     for o in outs[1:]:
         for a_, b_ in zip(o, outs[0]):
             assert torch.equal(a_, b_)
