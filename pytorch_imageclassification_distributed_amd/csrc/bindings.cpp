@@ -916,7 +916,7 @@ class PeerComm {
 void register_loader(pybind11::module& m);  // loader.cpp: native image-folder loader
 void bn_set_reduce_blocks(int n, int chb);
 void bn_set_unroll(int v);
-void bn_set_stream(int grid, long nt_mb, int walk, int walk_bwd, int flat_u, int flat_u_bwd);  // bn.hip: grid cap / non-temporal threshold / row walk of the streaming passes
+void bn_set_stream(int grid, long nt_mb, int walk, int walk_bwd, int flat_u, int flat_u_bwd, int red_walk);  // bn.hip: grid cap / non-temporal threshold / row walk of the streaming passes
 
 static void rccl_check(int r, const char* what) {
   TORCH_CHECK(r == 0, what, ": ", rccl_last_error(), " (code ", r, ")");
@@ -1039,11 +1039,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_act_maxpool", &bn_act_maxpool);
   m.def("bn_set_unroll", [](bool v) { bn_set_unroll(v ? 1 : 0); });
   m.def("bn_set_stream",
-        [](int grid, long nt_mb, int walk, int walk_bwd, int flat_u, int flat_u_bwd) {
-          bn_set_stream(grid, nt_mb, walk, walk_bwd, flat_u, flat_u_bwd);
+        [](int grid, long nt_mb, int walk, int walk_bwd, int flat_u, int flat_u_bwd, int red_walk) {
+          bn_set_stream(grid, nt_mb, walk, walk_bwd, flat_u, flat_u_bwd, red_walk);
         },
         py::arg("grid"), py::arg("nt_mb"), py::arg("walk") = -1, py::arg("walk_bwd") = -1, py::arg("flat_u") = 0,
-        py::arg("flat_u_bwd") = 0);
+        py::arg("flat_u_bwd") = 0, py::arg("red_walk") = -1);
   m.def("stem_conv", &stem_conv, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"), pybind11::arg("part"),
         pybind11::arg("G"), pybind11::arg("N"), pybind11::arg("H"), pybind11::arg("W"),
         pybind11::arg("shift") = pybind11::none());

@@ -692,7 +692,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
 // FL bit 0 = residual in the activation input, bit 1 = activation, bit 2 = dz written out.  The
 // generic kernel above issues one row of g / y loads per iteration behind the runtime res / act /
 // dz_out branches (3.4 TB/s on the 822 MB stem activation against 5.2 for bn_bwd_elemt).
-template <int FL>
+template <int FL, bool NT>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_u_kernel(
     const bf16_t* __restrict__ g, const bf16_t* __restrict__ y, const float* __restrict__ coef,
     const bf16_t* __restrict__ res, bf16_t* __restrict__ dz_out, long rows, int C, int act,
@@ -716,20 +716,24 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_u_kernel(
     load8f(coef + C + c0, sh);
     load8f(coef + 2 * C + c0, mu);
     load8f(coef + 3 * C + c0, is);
-    const long rbeg = blockIdx.x * rows_per_block;
-    const long rend = rbeg + rows_per_block < rows ? rbeg + rows_per_block : rows;
-    for (long row = rbeg + lr; row < rend; row += BN_U * RP) {
+    // rows_per_block <= 0: grid-stride walk (all blocks sweep the tensor together, non-temporal loads:
+    // 5.7-5.8 TB/s in the random-data probe against 5.0-5.2 for a block's own contiguous run)
+    const bool gs = rows_per_block <= 0;
+    const long rbeg = gs ? (long)blockIdx.x * RP : blockIdx.x * rows_per_block;
+    const long rend = gs ? rows : (rbeg + rows_per_block < rows ? rbeg + rows_per_block : rows);
+    const long rstep = gs ? (long)RP * gridDim.x : RP;
+    for (long row = rbeg + lr; row < rend; row += BN_U * rstep) {
       uint4 gr[BN_U], yr[BN_U], rr[BN_U];
 #pragma unroll
       for (int u = 0; u < BN_U; ++u) {
-        const long r = row + u * RP < rend ? row + u * RP : row;  // clamped rows load, never count
-        gr[u] = *(const uint4*)(g + r * ldg + c0);
-        yr[u] = *(const uint4*)(y + r * C + c0);
-        if constexpr (RES) rr[u] = *(const uint4*)(res + r * C + c0);
+        const long r = row + u * rstep < rend ? row + u * rstep : row;  // clamped rows load, never count
+        gr[u] = ldrow<NT>(g + r * ldg + c0);
+        yr[u] = ldrow<NT>(y + r * C + c0);
+        if constexpr (RES) rr[u] = ldrow<NT>(res + r * C + c0);
       }
 #pragma unroll
       for (int u = 0; u < BN_U; ++u) {
-        if (row + u * RP >= rend) break;
+        if (row + u * rstep >= rend) break;
         float gv[8], yv[8], rv[8];
         unpack8(gr[u], gv);
         unpack8(yr[u], yv);
@@ -746,7 +750,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_u_kernel(
           s[k] += dz;
           q[k] += dz * (yv[k] - mu[k]) * is[k];
         }
-        if constexpr (DZ) *(uint4*)(dz_out + (row + u * RP) * C + c0) = pack8(gv);
+        if constexpr (DZ) strow<NT>(dz_out + (row + u * rstep) * C + c0, pack8(gv));
       }
     }
   }
@@ -771,6 +775,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_u_kernel(
 }
 
 // ---- standalone statistics pass (outputs not produced by the GEMM epilogue) --
+template <bool NT>
 __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict__ y, long rows, int C,
                                                        long rows_per_block, float* __restrict__ part, int G,
                                                        int CHB, const float* __restrict__ shift) {
@@ -784,17 +789,29 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict_
 #pragma unroll
   for (int k = 0; k < 8; ++k) { s[k] = 0.f; q[k] = 0.f; }
   if (lr < RP && chunk < cch) {
-    const long rbeg = blockIdx.x * rows_per_block;
-    const long rend = rbeg + rows_per_block < rows ? rbeg + rows_per_block : rows;
+    // rows_per_block <= 0: the grid-stride walk of bn_bwd_reduce_u_kernel (BN_U rows of loads in flight)
+    const bool gs = rows_per_block <= 0;
+    const long rbeg = gs ? (long)blockIdx.x * RP : blockIdx.x * rows_per_block;
+    const long rend = gs ? rows : (rbeg + rows_per_block < rows ? rbeg + rows_per_block : rows);
+    const long rstep = gs ? (long)RP * gridDim.x : RP;
     float K[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) K[k] = shift ? shift[chunk * 8 + k] : 0.f;
-#pragma unroll 4
-    for (long row = rbeg + lr; row < rend; row += RP) {
-      float v[8];
-      unpack8(*(const uint4*)(y + row * C + chunk * 8), v);
+    for (long row = rbeg + lr; row < rend; row += BN_U * rstep) {
+      uint4 yr[BN_U];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) { const float d = v[k] - K[k]; s[k] += d; q[k] += d * d; }
+      for (int u = 0; u < BN_U; ++u) {
+        const long r = row + u * rstep < rend ? row + u * rstep : row;
+        yr[u] = ldrow<NT>(y + r * C + chunk * 8);
+      }
+#pragma unroll
+      for (int u = 0; u < BN_U; ++u) {
+        if (row + u * rstep >= rend) break;
+        float v[8];
+        unpack8(yr[u], v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { const float d = v[k] - K[k]; s[k] += d; q[k] += d * d; }
+      }
     }
   }
 #pragma unroll
@@ -986,6 +1003,10 @@ int g_bn_walk = getenv("IMGCLS_BN_WALK") ? atoi(getenv("IMGCLS_BN_WALK")) : 2;
 int g_bn_walk_bwd = getenv("IMGCLS_BN_WALK_BWD") ? atoi(getenv("IMGCLS_BN_WALK_BWD")) : 2;
 int g_bn_flat_u_bwd = getenv("IMGCLS_BN_FLAT_U_BWD") ? atoi(getenv("IMGCLS_BN_FLAT_U_BWD")) : 4;
 
+// walk of the backward reduce (bn_bwd_reduce_u): 1 = grid-stride over g_bn_grid blocks, 0 = a block's own
+// contiguous run of rows (reduce_grid)
+int g_bn_red_walk = getenv("IMGCLS_BN_RED_WALK") ? atoi(getenv("IMGCLS_BN_RED_WALK")) : 1;
+
 // vectors per thread of the flat apply when C / 8 divides 256 (IMGCLS_BN_FLAT_U: 1, 2 or 4)
 int g_bn_flat_u = getenv("IMGCLS_BN_FLAT_U") ? atoi(getenv("IMGCLS_BN_FLAT_U")) : 1;
 
@@ -1019,6 +1040,22 @@ int grid_stream(long rows, int C, int walk) {
   const int b = grid_chan(rows, C);
   if (g_bn_grid <= 0 || cch <= 0 || (walk == 1 && 256 % cch)) return b;  // cap the U kernels' grid
   return b < g_bn_grid ? b : g_bn_grid;
+}
+
+// the row reductions' grid under g_bn_red_walk: 1 = grid-stride walk over g_bn_grid blocks in all (the
+// streaming passes' cap), rows_per_block 0 marks it; 0 = reduce_grid's block-contiguous runs
+RedGrid red_walk_grid(const RedGrid& rg, long rows) {
+  if (g_bn_red_walk != 1) return rg;
+  RedGrid w = rg;
+  const unsigned slices = rg.grid.y;
+  long rb = (g_bn_grid > 0 ? g_bn_grid : 1024) / (long)slices;
+  const long rp = 256 / rg.chb;
+  const long need = (rows + rp - 1) / rp;
+  if (rb > need) rb = need;
+  if (rb < 1) rb = 1;
+  w.grid = dim3((unsigned)rb, slices);
+  w.rpb = 0;
+  return w;
 }
 
 bool use_nt(long rows, int C) { return g_bn_nt_mb < 0 || (g_bn_nt_mb > 0 && rows * (long)C * 2 >= (g_bn_nt_mb << 20)); }
@@ -1147,10 +1184,16 @@ int bn_bwd_reduce_launch(const bf16_t* g, const bf16_t* y, const float* coef, co
   }
   const bool a = act != ACT_NONE;
   const int fl = (res && a ? 1 : 0) | (a ? 2 : 0) | (dz_out ? 4 : 0) | (act == ACT_SILU ? 8 : 0);
-#define BWDRED(F)                                                                                        \
-  case F:                                                                                               \
-    hipLaunchKernelGGL(bn_bwd_reduce_u_kernel<F>, rg.grid, dim3(256), 0, s, g, y, coef, res, dz_out, rows, C, \
-                       act, rg.rpb, part, G, ld, rg.chb);                                               \
+  const bool nt = use_nt(rows, C);
+  const RedGrid rgw = red_walk_grid(rg, rows);
+#define BWDRED(F)                                                                                             \
+  case F:                                                                                                    \
+    if (nt)                                                                                                  \
+      hipLaunchKernelGGL((bn_bwd_reduce_u_kernel<F, true>), rgw.grid, dim3(256), 0, s, g, y, coef, res, dz_out, \
+                         rows, C, act, rgw.rpb, part, G, ld, rgw.chb);                                       \
+    else                                                                                                     \
+      hipLaunchKernelGGL((bn_bwd_reduce_u_kernel<F, false>), rgw.grid, dim3(256), 0, s, g, y, coef, res,       \
+                         dz_out, rows, C, act, rgw.rpb, part, G, ld, rgw.chb);                               \
     break;
   switch (fl) {
     BWDRED(0) BWDRED(2) BWDRED(3) BWDRED(4) BWDRED(6) BWDRED(7) BWDRED(10) BWDRED(11) BWDRED(14) BWDRED(15)
@@ -1236,7 +1279,11 @@ int bn_bwd_elemt_launch(const bf16_t* g, const bf16_t* y, const float* coef, con
 
 int bn_stats_launch(const bf16_t* y, long rows, int C, float* part, int G, const float* shift, hipStream_t s) {
   const RedGrid rg = reduce_grid(rows, C);
-  hipLaunchKernelGGL(bn_stats_kernel, rg.grid, dim3(256), 0, s, y, rows, C, rg.rpb, part, G, rg.chb, shift);
+  const RedGrid rw = red_walk_grid(rg, rows);
+  if (use_nt(rows, C))
+    hipLaunchKernelGGL(bn_stats_kernel<true>, rw.grid, dim3(256), 0, s, y, rows, C, rw.rpb, part, G, rw.chb, shift);
+  else
+    hipLaunchKernelGGL(bn_stats_kernel<false>, rw.grid, dim3(256), 0, s, y, rows, C, rw.rpb, part, G, rw.chb, shift);
   HIP_CHECK_LAUNCH();
   return 0;
 }
@@ -1268,7 +1315,8 @@ void bn_set_reduce_blocks(int n, int chb) {
 void bn_set_unroll(int v) { g_bn_unroll = v; }
 
 // streaming elementwise passes: grid cap (<= 0: grid_chan's) and non-temporal threshold in MiB (0 never, < 0 always)
-void bn_set_stream(int grid, long nt_mb, int walk, int walk_bwd, int flat_u, int flat_u_bwd) {
+void bn_set_stream(int grid, long nt_mb, int walk, int walk_bwd, int flat_u, int flat_u_bwd, int red_walk) {
+  if (red_walk >= 0) g_bn_red_walk = red_walk;
   if (flat_u > 0) g_bn_flat_u = flat_u;
   if (flat_u_bwd > 0) g_bn_flat_u_bwd = flat_u_bwd;
   g_bn_grid = grid;

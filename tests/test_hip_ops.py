@@ -1256,9 +1256,12 @@ def test_bn_backward_fused_into_producer_conv(case):
     # (the forward is the same code both times; on maps of many blocks its BN statistics are summed by fp32
     # atomics in arrival order, so the two forwards agree to rounding, not bitwise)
     assert rel_err(o1, o0) < 1e-2 and mean_err(o1, o0) < 1e-3
+    # the gradients inherit that forward rounding: on the 64-channel maps of 50 K+ pixels the BN-parameter
+    # gradients (sums over every pixel of a bf16 dz) measured mean errors of 3-5.5e-3 from run to run
+    mtol = 1e-2 if n * hw * hw > 50000 else 5e-3
     for a_, b_ in zip(g1, g0):
         assert rel_err(a_, b_) < 2e-2, rel_err(a_, b_)
-        assert mean_err(a_, b_) < 5e-3, mean_err(a_, b_)
+        assert mean_err(a_, b_) < mtol, mean_err(a_, b_)
 
 
 @pytest.mark.parametrize("case", [
@@ -1551,6 +1554,51 @@ def test_input_u8_resnet_forward_matches_fp32_input():
     assert rel_err(a, b) < 2e-2
 
 
+@pytest.mark.parametrize("rows,c", [(4099, 256), (1000, 2048), (777, 64), (301, 1152), (20000, 128)])
+def test_bn_backward_reduce_walks(rows, c):
+    """bn_bwd_reduce (plain, ReLU, residual + ReLU with dz written) and bn_stats under the grid-stride walk
+    (default) and the block-contiguous walk, with and without non-temporal loads: partial sums against fp64
+    torch, dz bitwise."""
+    hip = _hip()
+    torch.manual_seed(6)
+    y = (torch.randn(rows, c, device=DEV) * 2).to(torch.bfloat16)
+    res = torch.randn(rows, c, device=DEV).to(torch.bfloat16)
+    g = torch.randn(rows, c, device=DEV).to(torch.bfloat16)
+    coef = torch.cat([torch.rand(c, device=DEV) + 0.5, torch.randn(c, device=DEV),
+                      torch.randn(c, device=DEV) * 0.1, torch.rand(c, device=DEV) + 0.5])
+    sc, sh, mu, iv = coef.view(4, c).double()
+    yd, rd, gd = y.double(), res.double(), g.double()
+    grp = 16
+    dz_ref = None
+    try:
+        for red_walk, nt in ((1, -1), (0, -1), (1, 0), (0, 0)):
+            hip.C.bn_set_stream(1024, nt, -1, -1, 0, 0, red_walk)
+            for act, use_res in ((0, False), (1, False), (1, True)):
+                part = torch.zeros(grp * 2 * c, dtype=torch.float32, device=DEV)
+                dz = torch.empty_like(y) if use_res else None
+                hip.C.bn_bwd_reduce(g, y, coef, res if use_res else None, dz, rows, c, act, part, grp)
+                torch.cuda.synchronize()
+                z = yd * sc + sh + (rd if use_res else 0)
+                dzw = gd * (z > 0) if act else gd
+                want = torch.stack([dzw.sum(0), (dzw * (yd - mu) * iv).sum(0)])
+                got = part.view(grp, 2, c).double().sum(0)
+                assert rel_err(got.float(), want.float()) < 1e-3, (red_walk, nt, act, use_res)
+                if use_res:
+                    if dz_ref is None:
+                        dz_ref = dz
+                    assert torch.equal(dz, dz_ref)
+            # forward statistics pass (sums of y - shift and their squares) under the same walk
+            part = torch.zeros(grp * 2 * c, dtype=torch.float32, device=DEV)
+            shift = torch.randn(c, device=DEV) * 0.1
+            hip.C.bn_stats(y, rows, c, part, grp, shift)
+            torch.cuda.synchronize()
+            d = yd - shift.double()
+            want = torch.stack([d.sum(0), (d * d).sum(0)])
+            assert rel_err(part.view(grp, 2, c).double().sum(0).float(), want.float()) < 1e-3, (red_walk, nt)
+    finally:
+        hip.C.bn_set_stream(1024, -1, 2, 2, 1, 4, 1)  # the defaults
+
+
 @pytest.mark.parametrize("rows,c", [(4099, 256), (1000, 2048), (777, 64), (301, 1152)])
 def test_bn_streaming_passes_every_grid_and_nt(rows, c):
     """bn_apply (+residual +ReLU mask, and plain) and bn_bwd_elemt (all four modes) under every streaming setting
@@ -1602,7 +1650,7 @@ def test_bn_streaming_passes_every_grid_and_nt(rows, c):
                 assert rel_err(bw[mode].float(), want_bwd[mode]) < 1e-2, (grid, nt, walk, wb, fu, mode)
             outs.append([o1, o2, mask] + [bw[m] for m in range(4)])
     finally:
-        hip.C.bn_set_stream(1024, -1, 2, 2, 1, 4)  # the defaults
+        hip.C.bn_set_stream(1024, -1, 2, 2, 1, 4, 1)  # the defaults
     for o in outs[1:]:
         for a_, b_ in zip(o, outs[0]):
             assert torch.equal(a_, b_)
