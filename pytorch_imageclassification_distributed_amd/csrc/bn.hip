@@ -245,29 +245,7 @@ __global__ void bn_apply_kernel(const bf16_t* __restrict__ y, const float* __res
 // sits behind a runtime select (which makes hipcc branch around and wait for each load).
 constexpr int BN_U = 4;
 
-// 16-B row loads / stores of the streaming elementwise passes, optionally non-temporal: streams of
-// tensors far larger than the 256 MB Infinity Cache gain from the hint (scripts/probes/stream_bw.hip,
-// profiles/r12b_stream_bw.txt: block-contiguous walk, 4 blocks per CU, nt: 6.24 TB/s read-1-write-1 and
-// 6.07 read-2-write-1, against 5.3-5.4 at 8192 blocks without it)
-typedef unsigned int bn_u32x4 __attribute__((ext_vector_type(4)));
-template <bool NT>
-DEVI uint4 ldrow(const bf16_t* p) {
-  if constexpr (NT) {
-    const bn_u32x4 v = __builtin_nontemporal_load((const bn_u32x4*)p);
-    return make_uint4(v.x, v.y, v.z, v.w);
-  } else {
-    return *(const uint4*)p;
-  }
-}
-template <bool NT>
-DEVI void strow(bf16_t* p, const uint4& v) {
-  if constexpr (NT) {
-    const bn_u32x4 w = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(w, (bn_u32x4*)p);
-  } else {
-    *(uint4*)p = v;
-  }
-}
+// (ldrow / strow: common.h)
 
 // Rows of a channel-fixed elementwise pass (the grid's thread count is a multiple of C/8, grid_chan): when
 // 256 % (C/8) == 0 each block streams its own contiguous run of rows (256 / (C/8) rows per step), otherwise

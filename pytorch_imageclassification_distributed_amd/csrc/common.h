@@ -150,9 +150,35 @@ DEVI void pix_decode(long i, int cch, int X, int Y, const PixIdx& fd, int& c0, i
   }
 }
 
+// 16-B row loads / stores of the streaming passes, optionally non-temporal: streams of tensors far larger
+// than the 256 MB Infinity Cache gain from the hint (scripts/probes/stream_bw.hip,
+// profiles/r12e_stream_bw_random.txt)
+typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
+template <bool NT>
+DEVI uint4 ldrow(const bf16_t* p) {
+  if constexpr (NT) {
+    const u32x4_nt v = __builtin_nontemporal_load((const u32x4_nt*)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+  } else {
+    return *(const uint4*)p;
+  }
+}
+template <bool NT>
+DEVI void strow(bf16_t* p, const uint4& v) {
+  if constexpr (NT) {
+    const u32x4_nt w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, (u32x4_nt*)p);
+  } else {
+    *(uint4*)p = v;
+  }
+}
+
 // out[n][c] (+)= scale * sum_{p in split} a[n][p][c] (* b[n][p][c] when PROD), NHWC bf16 inputs, fp32 out.
 // block = CHB channel-chunk lanes (8 channels each) x RP pixel lanes, LDS tree over RP; grid =
 // (N, channel slices, pixel splits); splits > 1 accumulate with one atomic per channel per block.
+// SR_U pixel rows of loads in flight per lane, non-temporal (the reduced tensors are streamed once): the
+// dependent one-row-per-iteration form read 2.5 TB/s (profiles/r13f_eff_byte_roofline.txt)
+constexpr int SR_U = 4;
 template <bool PROD>
 __global__ __launch_bounds__(256) void spatial_reduce_kernel(const bf16_t* __restrict__ a,
                                                              const bf16_t* __restrict__ b, float* __restrict__ out,
@@ -169,18 +195,28 @@ __global__ __launch_bounds__(256) void spatial_reduce_kernel(const bf16_t* __res
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (lr < RP && chunk < cch) {
     const long base = (long)n * HW * C + chunk * 8;
-#pragma unroll 4
-    for (int p = p0 + lr; p < p1; p += RP) {
-      float va[8];
-      unpack8(*(const uint4*)(a + base + (long)p * C), va);
-      if (PROD) {
-        float vb[8];
-        unpack8(*(const uint4*)(b + base + (long)p * C), vb);
+    for (int p = p0 + lr; p < p1; p += SR_U * RP) {
+      uint4 ra[SR_U], rb[SR_U];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] += va[k] * vb[k];
-      } else {
+      for (int u = 0; u < SR_U; ++u) {
+        const int r = p + u * RP < p1 ? p + u * RP : p;
+        ra[u] = ldrow<true>(a + base + (long)r * C);
+        if (PROD) rb[u] = ldrow<true>(b + base + (long)r * C);
+      }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] += va[k];
+      for (int u = 0; u < SR_U; ++u) {
+        if (p + u * RP >= p1) break;
+        float va[8];
+        unpack8(ra[u], va);
+        if (PROD) {
+          float vb[8];
+          unpack8(rb[u], vb);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[k] += va[k] * vb[k];
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[k] += va[k];
+        }
       }
     }
   }

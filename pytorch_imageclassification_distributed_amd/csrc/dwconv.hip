@@ -644,6 +644,83 @@ __global__ __launch_bounds__(256) void se_dx_link_kernel(const bf16_t* __restric
   link_flush(L, C, s8, q8);
 }
 
+// se_dx_link over per-image blocks (grid N x channel slices, block = CHB chunk lanes x RP pixel lanes as
+// spatial_reduce_kernel): every lane's image and channel chunk are fixed, so the gate s, dp / HW and the BN
+// coefficients are loaded once, 4 pixel rows of dy / y loads stay in flight, the activation is a template
+// constant, and a block stores its image's partial sums as row n of the link (plain stores: one writer per
+// row slice).  The grid-stride form above kept 4 rows x (s, dp) tables in registers (192 VGPRs, 2 waves per
+// SIMD) and read 2.9 TB/s.
+template <int ACT>
+__global__ __launch_bounds__(256) void se_dx_link_n_kernel(const bf16_t* __restrict__ dy, const float* __restrict__ s,
+                                                           const float* __restrict__ dp, bf16_t* __restrict__ dx,
+                                                           int HW, int C, DwLink L) {
+  constexpr int U = 4;
+  __shared__ float red[256][17];
+  const int cch = C >> 3;
+  const int CHB = cch < 64 ? cch : 64;
+  const int RP = 256 / CHB;
+  const int tid = threadIdx.x, lc = tid % CHB, lr = tid / CHB;
+  const int chunk = blockIdx.y * CHB + lc;
+  const int n = blockIdx.x;
+  float s8[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (lr < RP && chunk < cch) {
+    const int c0 = chunk * 8;
+    float sv[8], pv[8], sc[8], sh[8], mu[8], is[8];
+    const float inv = 1.f / HW;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      *(float4*)(sv + 4 * h) = *(const float4*)(s + (long)n * C + c0 + 4 * h);
+      *(float4*)(pv + 4 * h) = *(const float4*)(dp + (long)n * C + c0 + 4 * h);
+      *(float4*)(sc + 4 * h) = *(const float4*)(L.coef + c0 + 4 * h);
+      *(float4*)(sh + 4 * h) = *(const float4*)(L.coef + C + c0 + 4 * h);
+      *(float4*)(mu + 4 * h) = *(const float4*)(L.coef + 2 * C + c0 + 4 * h);
+      *(float4*)(is + 4 * h) = *(const float4*)(L.coef + 3 * C + c0 + 4 * h);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) pv[k] *= inv;
+    const long base = (long)n * HW * C + c0;
+    for (int p = lr; p < HW; p += U * RP) {
+      uint4 dr[U], yr[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int r = p + u * RP < HW ? p + u * RP : p;
+        dr[u] = ldrow<true>(dy + base + (long)r * C);
+        yr[u] = ldrow<true>(L.y + base + (long)r * C);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (p + u * RP >= HW) break;
+        float v[8], yv[8];
+        unpack8(dr[u], v);
+        unpack8(yr[u], yv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float g = v[k] * sv[k] + pv[k];
+          const float dz = ACT == ACT_NONE ? g : act_grad(yv[k] * sc[k] + sh[k], g, ACT);
+          v[k] = dz;
+          s8[k] += dz;
+          q8[k] += dz * (yv[k] - mu[k]) * is[k];
+        }
+        strow<true>(dx + base + (long)(p + u * RP) * C, pack8(v));
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { red[tid][k] = s8[k]; red[tid][8 + k] = q8[k]; }
+  __syncthreads();
+  if (lr == 0 && chunk < cch) {
+    for (int r = 1; r < RP; ++r)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        if (k < 8) s8[k] += red[tid + r * CHB][k];
+        else q8[k - 8] += red[tid + r * CHB][k];
+      }
+    float* dst = L.part + (size_t)n * 2 * C + chunk * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { dst[k] = s8[k]; dst[C + k] = q8[k]; }
+  }
+}
+
 // fp32 activations for the SE MLP: 0 = silu, 1 = sigmoid
 __global__ void act32_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, long n, int kind) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
@@ -674,6 +751,9 @@ __global__ void act32_bwd_kernel(const float* __restrict__ x, const float* __res
 // row-strip kernels on (default) or off (the per-pixel kernels; A/B and tests)
 static int g_dw_rs = 1;
 void dw_set_rowstrip(int v) { g_dw_rs = v; }
+// linked se_dx: 1 = per-image blocks (se_dx_link_n_kernel, default), 0 = the grid-stride kernel (A/B)
+static int g_se_dx_n = getenv("IMGCLS_SE_DX_N") ? atoi(getenv("IMGCLS_SE_DX_N")) : 1;
+void se_set_dx_n(int v) { g_se_dx_n = v; }
 
 static bool rs_ok(int kh, int kw, int sh, int sw) {
   return g_dw_rs && kh == kw && (kh == 3 || kh == 5) && sh == sw && (sh == 1 || sh == 2);
@@ -856,9 +936,12 @@ int se_ds_launch(const bf16_t* dy, const bf16_t* x, float* ds, int N, int HW, in
   return spatial_reduce_launch<true>(dy, x, ds, N, HW, C, 1.f, s);
 }
 
-// blocks of a linked se_dx launch (<= ~1024; a multiple of C/8 / gcd(C/8, 256) so lanes keep one channel
-// chunk): the caller gives the link that many partial rows and every block stores its own row
+
+// partial rows of a linked se_dx launch: one per image (per-image kernel) or one per block of the grid-stride
+// kernel (<= ~1024; a multiple of C/8 / gcd(C/8, 256) so lanes keep one channel chunk); every row is stored
+// by its writers with plain stores
 int se_dx_link_blocks(int N, int HW, int C) {
+  if (g_se_dx_n) return N;
   const int cch = C / 8;
   if (cch <= 0) return 1;
   int gcd = cch, m = 256;
@@ -871,6 +954,17 @@ int se_dx_link_blocks(int N, int HW, int C) {
 int se_dx_launch(const bf16_t* dy, const float* sc, const float* dp, bf16_t* dx, int N, int HW, int C,
                  const bf16_t* ly, const float* lcoef, float* lpart, int lG, int lact, hipStream_t s) {
   if ((long)N * HW * (C / 8) <= 0) return 0;
+  if (ly != nullptr && g_se_dx_n) {
+    if (lG < N) return 2;  // one partial row per image
+    const int cch = C / 8, CHB = cch < 64 ? cch : 64;
+    const dim3 grid(N, (cch + CHB - 1) / CHB);
+    const DwLink L{ly, lcoef, lpart, lG, lact};
+    if (lact == ACT_SILU) hipLaunchKernelGGL(se_dx_link_n_kernel<ACT_SILU>, grid, dim3(256), 0, s, dy, sc, dp, dx, HW, C, L);
+    else if (lact == ACT_RELU) hipLaunchKernelGGL(se_dx_link_n_kernel<ACT_RELU>, grid, dim3(256), 0, s, dy, sc, dp, dx, HW, C, L);
+    else hipLaunchKernelGGL(se_dx_link_n_kernel<ACT_NONE>, grid, dim3(256), 0, s, dy, sc, dp, dx, HW, C, L);
+    HIP_CHECK_LAUNCH();
+    return 0;
+  }
   if (ly != nullptr) {
     if ((long)N * HW >= (1L << 31)) return 2;
     const int b = se_dx_link_blocks(N, HW, C);

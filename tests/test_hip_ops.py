@@ -1149,11 +1149,21 @@ def test_se_gate_fused_grads(n, c, nsq, hw, fused):
         assert rel_err(mine.reshape(ref.shape), ref) < 2e-2
 
 
-@pytest.mark.parametrize("n,c,hw", [(4, 96, 14), (3, 1152, 7), (2, 2064, 5)])
-def test_se_gate_fused_bn_backward(n, c, hw):
-    """BN -> SiLU -> SE gate (exclusive consumer): se_dx emits dz and the BN's backward partial sums (BwdLink);
-    gradients of the input and of every parameter match fp32 autograd."""
+@pytest.mark.parametrize("per_image", [True, False])
+@pytest.mark.parametrize("n,c,hw", [(4, 96, 14), (3, 1152, 7), (2, 2064, 5), (2, 40, 57)])
+def test_se_gate_fused_bn_backward(n, c, hw, per_image):
+    """BN -> SiLU -> SE gate (exclusive consumer): se_dx emits dz and the BN's backward partial sums (BwdLink),
+    with the per-image kernel (default) and the grid-stride one; gradients of the input and of every parameter
+    match fp32 autograd."""
     hip = _hip()
+    hip.C.se_set_dx_n(per_image)
+    try:
+        _se_gate_fused_case(hip, n, c, hw)
+    finally:
+        hip.C.se_set_dx_n(True)
+
+
+def _se_gate_fused_case(hip, n, c, hw):
     torch.manual_seed(c)
     nsq = max(1, c // 24)
     conv = nn.Conv2d(c, c, 1, bias=False).to(DEV).to(memory_format=CL)
