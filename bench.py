@@ -89,13 +89,19 @@ def parse():
     return p.parse_args()
 
 
-def load_baseline(n_gpus: int, batch: int):
-    """Reference-stack images/sec measured on MI355X at the same per-GPU batch and GPU count."""
+def load_baseline(n_gpus: int, batch: int, model: str = "resnet50", image_size: int = 224):
+    """Reference-stack images/sec measured on MI355X for the same model, image size, per-GPU batch and GPU
+    count (``images_per_sec`` holds ResNet-50 @224, the headline; ``models`` the others); None if not
+    measured."""
     path = os.path.join(HERE, "benchmarks", "reference_stack.json")
     try:
         with open(path) as f:
             ref = json.load(f)
-        v = ref.get("images_per_sec", {}).get(str(batch), {}).get(str(n_gpus))
+        if model == "resnet50" and image_size == 224:
+            table = ref.get("images_per_sec", {})
+        else:
+            table = ref.get("models", {}).get(f"{model}@{image_size}", {})
+        v = table.get(str(batch), {}).get(str(n_gpus))
         return float(v) if v else None
     except (OSError, ValueError, AttributeError):
         return None
@@ -270,7 +276,8 @@ def main():
     if ctx.rank == 0:
         imgs = a.batch * ctx.world_size * a.steps
         value = imgs / dt
-        base = load_baseline(ctx.world_size, a.batch) if a.dtype == "bf16" and a.device == "cuda" else None
+        base = (load_baseline(ctx.world_size, a.batch, a.model, a.image_size)
+                if a.dtype == "bf16" and a.device == "cuda" else None)
         metric = METRIC if (a.model, a.image_size, a.dtype, a.device) == ("resnet50", 224, "bf16", "cuda") else \
             f"images/sec (whole node) {a.model} {a.image_size}x{a.image_size} {a.dtype} MI355X"
         if a.device == "cpu":
