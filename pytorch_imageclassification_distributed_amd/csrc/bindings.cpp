@@ -98,6 +98,7 @@ int dw_wgrad_launch(const bf16_t*, const bf16_t*, float*, int, int, int, int, in
 long dw_wgrad_partial_rows(int, int, int, int, int, int, int);
 void dw_set_rowstrip(int);
 void se_set_dx_n(int);
+void dw_set_wkr(int);
 void set_deterministic(int);
 void set_force_div64(int);
 int se_scale_launch(const bf16_t*, const float*, bf16_t*, int, int, int, hipStream_t);
@@ -1122,6 +1123,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("dw_wgrad", &dw_wgrad);
   m.def("dw_set_rowstrip", [](bool v) { dw_set_rowstrip(v ? 1 : 0); });
   m.def("se_set_dx_n", [](bool v) { se_set_dx_n(v ? 1 : 0); });
+  m.def("dw_set_wkr", [](int v) { dw_set_wkr(v); });
   m.def("se_scale", &se_scale);
   m.def("se_ds", &se_ds);
   m.def("se_dx", &se_dx, pybind11::arg("dy"), pybind11::arg("s"), pybind11::arg("dp"), pybind11::arg("dx"),

@@ -417,7 +417,7 @@ __global__ __launch_bounds__(256) void dw_wgrad_rs_kernel(const bf16_t* __restri
 #pragma unroll
         for (int q = 0; q < KR; ++q) {
           const int ih = oh * S - g.pt + r0 + q;
-          if ((unsigned)ih >= (unsigned)g.H) continue;
+          if (r0 + q >= K || (unsigned)ih >= (unsigned)g.H) continue;  // (KR need not divide K)
           const bf16_t* xr = x + (((long)n * g.H + ih) * g.W) * g.C + c0;
           uint4 xraw[NJ];
 #pragma unroll
@@ -442,6 +442,7 @@ __global__ __launch_bounds__(256) void dw_wgrad_rs_kernel(const bf16_t* __restri
     // share the reduction instead of the CHB row-0 lanes walking RP rows each
 #pragma unroll
     for (int q = 0; q < KR; ++q) {
+      if (r0 + q >= K) break;  // block-uniform
 #pragma unroll
       for (int c = 0; c < K; ++c)
 #pragma unroll
@@ -715,9 +716,14 @@ __global__ __launch_bounds__(256) void se_dx_link_n_kernel(const bf16_t* __restr
         if (k < 8) s8[k] += red[tid + r * CHB][k];
         else q8[k - 8] += red[tid + r * CHB][k];
       }
-    float* dst = L.part + (size_t)n * 2 * C + chunk * 8;
+    float* dst = L.part + (size_t)(n % L.G) * 2 * C + chunk * 8;
+    if (L.G >= (int)gridDim.x) {  // a row per image: plain stores
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { dst[k] = s8[k]; dst[C + k] = q8[k]; }
+      for (int k = 0; k < 8; ++k) { dst[k] = s8[k]; dst[C + k] = q8[k]; }
+    } else {  // images share rows (the finalizing reduce then reads G rows, not one per image)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { atomicAdd(dst + k, s8[k]); atomicAdd(dst + C + k, q8[k]); }
+    }
   }
 }
 
@@ -882,9 +888,13 @@ static long dw_wgrad_ppb(long npix, int T, long* pblocks_out) {
 // row-strip weight gradient: R = 4 outputs per strip, one kernel row per blockIdx.y
 constexpr int DW_WR = 4;
 
+// kernel rows per pass of the 5x5 row-strip weight gradient (IMGCLS_DW_WKR: 1 or 3)
+static int g_dw_wkr = getenv("IMGCLS_DW_WKR") ? atoi(getenv("IMGCLS_DW_WKR")) : 3;
+void dw_set_wkr(int v) { g_dw_wkr = v; }
+
 static long dw_wgrad_rs_ipb(int N, int OH, int OW, int K, long* pblocks_out) {
   const long items = (long)N * OH * ((OW + DW_WR - 1) / DW_WR);
-  long pblocks = K == 3 ? 1024 : 2048 / K;  // blocks per pass; K = 3 runs one pass, K = 5 five
+  long pblocks = K == 3 ? 1024 : (g_dw_wkr == 3 ? 1024 : 2048 / K);  // blocks per pass (K = 5: 2 or 5 passes)
   long ipb = (items + pblocks - 1) / pblocks;
   if (ipb < 16) ipb = 16;
   *pblocks_out = (items + ipb - 1) / ipb;
@@ -906,11 +916,14 @@ int dw_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* /*dw*/, int N, int
     long pblocks;
     const long ipb = dw_wgrad_rs_ipb(N, OH, OW, kh, &pblocks);
     const int OWB = (OW + DW_WR - 1) / DW_WR;
-    // K = 3: all kernel rows in one pass (one dY read); K = 5: one kernel row per blockIdx.y
-    const dim3 g3((unsigned)pblocks, 1), g5((unsigned)pblocks, 5);
+    // K = 3: all kernel rows in one pass (one dY read); K = 5: g_dw_wkr kernel rows per blockIdx.y pass
+    // (3: two passes read dY and x twice; 1: five passes, accumulators bounded to 5 x 8 per lane)
+    const dim3 g3((unsigned)pblocks, 1), g5((unsigned)pblocks, 5), g5b((unsigned)pblocks, 2);
     if (kh == 3 && sh == 1) hipLaunchKernelGGL((dw_wgrad_rs_kernel<3, 1, DW_WR, 3>), g3, dim3(256), 0, s, dy, x, part, g, OWB, ipb);
+    else if (kh == 5 && sh == 1 && g_dw_wkr == 3) hipLaunchKernelGGL((dw_wgrad_rs_kernel<5, 1, DW_WR, 3>), g5b, dim3(256), 0, s, dy, x, part, g, OWB, ipb);
     else if (kh == 5 && sh == 1) hipLaunchKernelGGL((dw_wgrad_rs_kernel<5, 1, DW_WR, 1>), g5, dim3(256), 0, s, dy, x, part, g, OWB, ipb);
     else if (kh == 3) hipLaunchKernelGGL((dw_wgrad_rs_kernel<3, 2, DW_WR, 3>), g3, dim3(256), 0, s, dy, x, part, g, OWB, ipb);
+    else if (g_dw_wkr == 3) hipLaunchKernelGGL((dw_wgrad_rs_kernel<5, 2, DW_WR, 3>), g5b, dim3(256), 0, s, dy, x, part, g, OWB, ipb);
     else hipLaunchKernelGGL((dw_wgrad_rs_kernel<5, 2, DW_WR, 1>), g5, dim3(256), 0, s, dy, x, part, g, OWB, ipb);
     HIP_CHECK_LAUNCH();
     return 0;
@@ -941,7 +954,8 @@ int se_ds_launch(const bf16_t* dy, const bf16_t* x, float* ds, int N, int HW, in
 // kernel (<= ~1024; a multiple of C/8 / gcd(C/8, 256) so lanes keep one channel chunk); every row is stored
 // by its writers with plain stores
 int se_dx_link_blocks(int N, int HW, int C) {
-  if (g_se_dx_n) return N;
+  // per-image kernel: 64 rows shared by the images (atomics), one per image in deterministic mode
+  if (g_se_dx_n) return g_imgcls_det ? N : (N < 64 ? N : 64);
   const int cch = C / 8;
   if (cch <= 0) return 1;
   int gcd = cch, m = 256;
@@ -955,7 +969,7 @@ int se_dx_launch(const bf16_t* dy, const float* sc, const float* dp, bf16_t* dx,
                  const bf16_t* ly, const float* lcoef, float* lpart, int lG, int lact, hipStream_t s) {
   if ((long)N * HW * (C / 8) <= 0) return 0;
   if (ly != nullptr && g_se_dx_n) {
-    if (lG < N) return 2;  // one partial row per image
+    if (lG < 1) return 2;
     const int cch = C / 8, CHB = cch < 64 ? cch : 64;
     const dim3 grid(N, (cch + CHB - 1) / CHB);
     const DwLink L{ly, lcoef, lpart, lG, lact};

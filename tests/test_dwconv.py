@@ -34,9 +34,11 @@ def rel(a, b):
     return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
 
 
-@pytest.mark.parametrize("rowstrip", [True, False])
+@pytest.mark.parametrize("rowstrip,wkr", [(True, 3), (True, 1), (False, 3)])
 @pytest.mark.parametrize("case", CASES)
-def test_depthwise_fwd_dgrad_wgrad(case, rowstrip):
+def test_depthwise_fwd_dgrad_wgrad(case, rowstrip, wkr):
+    """Depthwise forward / data gradient / weight gradient against fp32 torch: row-strip kernels (5x5 weight
+    gradient with 3 or 1 kernel rows per pass) and the per-pixel kernels."""
     from pytorch_imageclassification_distributed_amd.ops import hip
     C_ = hip.C
     n, c, h, w, k, s, pt, pb, pl, pr = case
@@ -56,6 +58,7 @@ def test_depthwise_fwd_dgrad_wgrad(case, rowstrip):
     dyb = dy.to(torch.bfloat16).contiguous(memory_format=CL)
     wtt = wt.view(c, k * k).t().contiguous().to(torch.bfloat16)  # [taps][C]
     C_.dw_set_rowstrip(rowstrip)
+    C_.dw_set_wkr(wkr)
     try:
         y = torch.empty(n, c, oh, ow, device=DEV, dtype=torch.bfloat16, memory_format=CL)
         C_.dw_fwd(xb, wtt, y, None, n, h, w, c, oh, ow, k, k, s, s, pt, pl)
@@ -66,6 +69,7 @@ def test_depthwise_fwd_dgrad_wgrad(case, rowstrip):
         torch.cuda.synchronize()
     finally:
         C_.dw_set_rowstrip(True)
+        C_.dw_set_wkr(3)
     assert rel(y, yr) < 1e-2, ("fwd", rel(y, yr))
     assert rel(dx, xr.grad) < 1e-2, ("dgrad", rel(dx, xr.grad))
     assert rel(dw, wr.grad) < 1e-4, ("wgrad", rel(dw, wr.grad))
