@@ -40,7 +40,7 @@ int bn_finalize_launch(const double*, const double*, double, const float*, const
                        long long*, float, float, int, float*, const float*, hipStream_t);
 int bn_eval_coef_launch(const float*, const float*, const float*, const float*, float, int, float*, hipStream_t);
 int bn_apply_launch(const bf16_t*, const float*, const bf16_t*, bf16_t*, long, int, int, int, int, uint8_t*, uint8_t*,
-                    uint8_t*, hipStream_t);
+                    uint8_t* /* mask */, const float* /* res_coef: the residual is a deferred BN's input */, hipStream_t);
 int bn_bwd_reduce_launch(const bf16_t*, const bf16_t*, const float*, const bf16_t*, bf16_t*, long, int, int,
                          float*, int, int, hipStream_t);
 int bn_bwd_k_launch(const double*, const double*, double, int, float*, hipStream_t);
@@ -383,7 +383,7 @@ void bn_eval_coef(OT gamma, OT beta, Tensor rmean, Tensor rvar, double eps, int 
 }
 
 void bn_apply(Tensor y, Tensor coef, OT res, Tensor out, long rows, int C, int ldo, int c_off, int act, OT q,
-              OT qs, OT mask) {
+              OT qs, OT mask, OT res_coef) {
   req(y, BF, "y"); req(out, BF, "out"); req(coef, F32, "coef");
   TORCH_CHECK(C % 8 == 0, "bn_apply: C % 8");
   uint8_t* qp = nullptr;
@@ -402,8 +402,15 @@ void bn_apply(Tensor y, Tensor coef, OT res, Tensor out, long rows, int C, int l
                 "bn_apply: mask needs uint8 [rows*C/8], a residual, ReLU and a dense bf16 output");
     mp = mask->data_ptr<uint8_t>();
   }
+  const float* rc = nullptr;
+  if (res_coef.has_value() && res_coef->defined()) {  // the residual is a deferred BN's input: res_coef = its coef
+    req(*res_coef, F32, "res_coef");
+    TORCH_CHECK(res.has_value() && res->defined() && res_coef->numel() >= 2 * C,
+                "bn_apply: res_coef needs a residual and [>= 2][C] coefficients");
+    rc = res_coef->data_ptr<float>();
+  }
   check(bn_apply_launch(ptr<bf16_t>(y), ptr<float>(coef), optr<bf16_t>(res), ptr<bf16_t>(out), rows, C, ldo, c_off,
-                        act, qp, qsp, mp, cur()),
+                        act, qp, qsp, mp, rc, cur()),
         "bn_apply");
 }
 
@@ -1008,7 +1015,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_apply", &bn_apply, pybind11::arg("y"), pybind11::arg("coef"), pybind11::arg("res"), pybind11::arg("out"),
         pybind11::arg("rows"), pybind11::arg("C"), pybind11::arg("ldo"), pybind11::arg("c_off"), pybind11::arg("act"),
         pybind11::arg("q") = pybind11::none(), pybind11::arg("qs") = pybind11::none(),
-        pybind11::arg("mask") = pybind11::none());
+        pybind11::arg("mask") = pybind11::none(), pybind11::arg("res_coef") = pybind11::none());
   m.def("bn_bwd_reduce", &bn_bwd_reduce, pybind11::arg("g"), pybind11::arg("y"), pybind11::arg("coef"), pybind11::arg("res"),
         pybind11::arg("dz_out"), pybind11::arg("rows"), pybind11::arg("C"), pybind11::arg("act"), pybind11::arg("part"), pybind11::arg("G"),
         pybind11::arg("ldg") = 0);

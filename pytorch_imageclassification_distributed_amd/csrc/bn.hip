@@ -353,11 +353,13 @@ DEVI void flat_pos(long i, const FlatIdx& f, long& row, int& c0) {
 
 // U > 1: each thread also takes the vectors 256, 512, .. further on (a block owns 256 * U consecutive vectors),
 // which share its channel chunk when C / 8 divides 256 - one coefficient load per U vectors
-template <bool RES, bool NT, int ACT, int U>
+// RB: the residual is itself a BN input (a deferred downsample BN, ops/_hip/convbn.py): it enters as
+// coef2[0] * res + coef2[1] instead of res, so that BN's own apply pass is never run
+template <bool RES, bool NT, int ACT, int U, bool RB = false>
 __global__ __launch_bounds__(256) void bn_apply_flat_kernel(const bf16_t* __restrict__ y, const float* __restrict__ coef,
                                                             const bf16_t* __restrict__ res, bf16_t* __restrict__ out,
                                                             long nvec, FlatIdx fi, int C, int ldo, int c_off,
-                                                            uint8_t* __restrict__ mask) {
+                                                            uint8_t* __restrict__ mask, const float* __restrict__ coef2) {
   const long i0 = blockIdx.x * (256L * U) + threadIdx.x;
   if (i0 >= nvec) return;
   long row;
@@ -371,9 +373,13 @@ __global__ __launch_bounds__(256) void bn_apply_flat_kernel(const bf16_t* __rest
     yv[u] = ldrow<NT>(y + r * C + c0);
     if constexpr (RES) rv[u] = ldrow<NT>(res + r * C + c0);
   }
-  float sc[8], sh[8];
+  float sc[8], sh[8], sc2[8], sh2[8];
   load8f(coef + c0, sc);
   load8f(coef + C + c0, sh);
+  if constexpr (RB) {
+    load8f(coef2 + c0, sc2);
+    load8f(coef2 + C + c0, sh2);
+  }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     if (i0 + u * 256L >= nvec) break;
@@ -381,6 +387,12 @@ __global__ __launch_bounds__(256) void bn_apply_flat_kernel(const bf16_t* __rest
     float v[8], rr[8];
     unpack8(yv[u], v);
     if constexpr (RES) unpack8(rv[u], rr);
+    if constexpr (RB) {  // rounded to bf16 as the downsample BN's own apply would have stored it: the output
+                         // and the ReLU mask are bitwise those of the materialized residual
+#pragma unroll
+      for (int k = 0; k < 8; ++k) rr[k] = rr[k] * sc2[k] + sh2[k];
+      unpack8(pack8(rr), rr);
+    }
     unsigned mk = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -1089,8 +1101,23 @@ int bn_eval_coef_launch(const float* gamma, const float* beta, const float* rmea
 }
 
 int bn_apply_launch(const bf16_t* y, const float* coef, const bf16_t* res, bf16_t* out, long rows, int C,
-                    int ldo, int c_off, int act, uint8_t* q, uint8_t* qs, uint8_t* mask, hipStream_t s) {
+                    int ldo, int c_off, int act, uint8_t* q, uint8_t* qs, uint8_t* mask, const float* coef2,
+                    hipStream_t s) {
   if (mask && (!res || act != ACT_RELU || ldo != C || c_off)) return 2;
+  if (coef2) {  // residual = a BN input with its coefficients: the flat kernel only
+    if (!res || q || act != ACT_RELU || !(g_bn_walk == 2 && (g_bn_unroll || mask))) return 2;
+    const long nvec = rows * (long)(C / 8);
+    const dim3 gf((unsigned)((nvec + 255) / 256));
+    const FlatIdx fi = flat_idx(nvec, C);
+    if (use_nt(rows, C))
+      hipLaunchKernelGGL((bn_apply_flat_kernel<true, true, ACT_RELU, 1, true>), gf, dim3(256), 0, s, y, coef, res, out,
+                         nvec, fi, C, ldo, c_off, mask, coef2);
+    else
+      hipLaunchKernelGGL((bn_apply_flat_kernel<true, false, ACT_RELU, 1, true>), gf, dim3(256), 0, s, y, coef, res, out,
+                         nvec, fi, C, ldo, c_off, mask, coef2);
+    HIP_CHECK_LAUNCH();
+    return 0;
+  }
   if (q) {
     if (C % 32 || ldo != C || c_off) return 2;
     if (res) hipLaunchKernelGGL(bn_apply_mx_kernel<true>, dim3(grid_chan(rows, C)), dim3(256), 0, s, y, coef, res, out, q,
@@ -1106,8 +1133,9 @@ int bn_apply_launch(const bf16_t* y, const float* coef, const bf16_t* res, bf16_
     const int fu = (cch > 0 && 256 % cch == 0) ? g_bn_flat_u : 1;
     const dim3 gf((unsigned)((nvec + 256L * fu - 1) / (256L * fu)));
     const FlatIdx fi = flat_idx(nvec, C);
-#define FAPPLY_U(R, N, A, U_) \
-  hipLaunchKernelGGL((bn_apply_flat_kernel<R, N, A, U_>), gf, dim3(256), 0, s, y, coef, res, out, nvec, fi, C, ldo, c_off, mask)
+#define FAPPLY_U(R, N, A, U_)                                                                                  \
+  hipLaunchKernelGGL((bn_apply_flat_kernel<R, N, A, U_>), gf, dim3(256), 0, s, y, coef, res, out, nvec, fi, C, ldo, \
+                     c_off, mask, nullptr)
 #define FAPPLY(R, N, A)                  \
   do {                                   \
     if (fu == 4) FAPPLY_U(R, N, A, 4);   \

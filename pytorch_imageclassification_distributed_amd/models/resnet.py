@@ -40,7 +40,7 @@ class BasicBlock(nn.Module):
     def forward(self, x):
         slot = Fx.grad_slot(x)  # x feeds conv1 and the identity/downsample branch
         if self.downsample is not None:
-            identity = Fx.conv_bn_act(x, self.downsample[0], self.downsample[1], None, x_slot=slot)
+            identity = Fx.conv_bn_act(x, self.downsample[0], self.downsample[1], None, x_slot=slot, defer_res=True)
         else:
             identity = x
         out = Fx.conv_bn_act(x, self.conv1, self.bn1, "relu", x_slot=slot, defer_act=True)
@@ -67,7 +67,7 @@ class Bottleneck(nn.Module):
     def forward(self, x):
         slot = Fx.grad_slot(x)  # x feeds conv1 and the identity/downsample branch
         if self.downsample is not None:
-            identity = Fx.conv_bn_act(x, self.downsample[0], self.downsample[1], None, x_slot=slot)
+            identity = Fx.conv_bn_act(x, self.downsample[0], self.downsample[1], None, x_slot=slot, defer_res=True)
         else:
             identity = x
         # bn1 / bn2 outputs feed only the next conv: the HIP path fuses their apply into that conv's loads

@@ -570,12 +570,26 @@ RELU_MASK = os.environ.get("IMGCLS_RELU_MASK", "1") == "1"
 class BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, y, gamma, beta, res, bn, act, stats_ready, res_slot=None, link=None, cat=None, xa=None,
-                shift=None, defer=None):
+                shift=None, defer=None, res_hold=None):
         dev = y.device
         n, c, h, w = y.shape
         rows = n * h * w
         a = ACT[act]
         coef, group, count_t = _bn_coef(y, gamma, beta, bn, stats_ready, shift)
+        # res_hold: the residual is a deferred BN output (it holds that BN's input); this apply forms it
+        res_coef = None
+        if res_hold is not None:
+            if res_hold.act != 0:
+                raise RuntimeError("deferred residual BN: identity activation only")
+            if cat is not None or defer is not None or a != 1 or _shadows.FP8_FWD or not RELU_MASK:
+                # any other form materializes the residual first (what the deferred BN would have written); the
+                # fused form needs the ReLU mask, which the backward consumers read instead of the residual
+                r = _empty_cl(n, c, h, w, dev)
+                C.bn_apply(res, res_hold.coef, None, r, rows, c, c, 0, 0)
+                res, res_hold = r, None
+            else:
+                res_coef = res_hold.coef
+                RES_DEFER_COUNT[0] += 1
         if defer is not None:
             # deferred (XfHold): the consuming conv applies act(bn(y)) itself; the output stands for
             # act(bn(y)) but holds y (autograd returns a view of the input)
@@ -604,7 +618,7 @@ class BNActFn(torch.autograd.Function):
             # reads instead of re-reading the residual (1/16 of its bytes, RELU_MASK)
             mask = (torch.empty(rows * c // 8, dtype=torch.uint8, device=dev)
                     if RELU_MASK and res is not None and a == 1 and bn.training and link is not None else None)
-            C.bn_apply(y, coef, res, out, rows, c, c, 0, a, mask=mask)
+            C.bn_apply(y, coef, res, out, rows, c, c, 0, a, mask=mask, res_coef=res_coef)
             if link is not None:
                 link.mask = mask
         ctx.act, ctx.group, ctx.rows, ctx.c = a, group, rows, c
@@ -613,11 +627,14 @@ class BNActFn(torch.autograd.Function):
         ctx.res_slot = res_slot
         ctx.link = None
         if link is not None and bn.training:  # (grad mode is always off inside forward)
+            # (a deferred residual holds the downsample BN's input: the consuming conv's epilogue reads the mask
+            # instead, and consumers that cannot take a residual still see one and decline the link)
             link.y, link.coef, link.res, link.act = y, coef, res, a
             link.group, link.params, link.c, link.rows = group, (gamma, beta), c, rows
             link.count_t = count_t
             ctx.link = link
         ctx.has_res = res is not None
+        ctx.res_coef = res_coef
         ctx.params = (gamma, beta)
         ctx.xa = xa if bn.training else None
         ctx.save_for_backward(y, coef, res if res is not None else y)
@@ -627,6 +644,12 @@ class BNActFn(torch.autograd.Function):
     def backward(ctx, gout):  # (with ``defer`` too: gout is the gradient w.r.t. act(bn(y)))
         y, coef, res = ctx.saved_tensors
         res = res if ctx.has_res else None
+        if res is not None and ctx.res_coef is not None and not (ctx.link is not None and ctx.link.done):
+            # the activation is recomputed from z = bn(y) + residual below: form the deferred residual
+            n_, c_, h_, w_ = res.shape
+            r = _empty_cl(n_, c_, h_, w_, res.device)
+            C.bn_apply(res, ctx.res_coef, None, r, n_ * h_ * w_, c_, c_, 0, 0)
+            res = r
         dev = y.device
         c, rows = ctx.c, ctx.rows
         ldg = channel_slice_stride(gout)  # a concat's gradient arrives as a channel slice: read in place
@@ -684,7 +707,7 @@ class BNActFn(torch.autograd.Function):
         dres = dz if ctx.has_res else None
         if dres is not None and ctx.res_slot is not None:
             dres = ctx.res_slot.deliver(dres)
-        return dy, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None
+        return dy, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None
 
 
 class BNActPoolFn(torch.autograd.Function):
@@ -837,8 +860,16 @@ def pool_conv_bn_act(x, conv, bn, act, prepool, x_slot=None, out=None, out_plan=
     return BNActFn.apply(yp, bn.weight, bn.bias, None, bn, act, False, None, None, out, None, stat_shift(bn))
 
 
+# A ResNet downsample BN (no activation) whose output is only the residual of its block's last BN is not
+# applied at all: it hands that BN its input y and coefficients (XfHold), and the residual BN's apply forms
+# sc3 * y3 + sh3 + (sc_ds * y_ds + sh_ds) itself - one read + one write of the downsample output fewer per
+# stage (the four bn_apply passes were 1.04 ms of the ResNet-50 b1024 step, profiles/r13a_step_breakdown.txt)
+RES_DEFER = os.environ.get("IMGCLS_RES_DEFER", "1") == "1"
+RES_DEFER_COUNT = [0]  # residual BNs that applied a deferred downsample BN (tests / diagnostics)
+
+
 def conv_bn_act(x, conv, bn, act, residual, x_slot=None, res_slot=None, exclusive_input=False, out=None,
-                defer_act=False):
+                defer_act=False, defer_res=False):
     """``exclusive_input``: this conv is the only consumer of ``x`` (lets its dgrad fuse the BN-backward
     reduce of x's producer); a slot-paired consumer qualifies automatically.  ``out`` = (ConcatBuffer,
     branch index): the result is written into that branch's channel slice of the concat output.
@@ -857,6 +888,7 @@ def conv_bn_act(x, conv, bn, act, residual, x_slot=None, res_slot=None, exclusiv
             out._imgcls_link = link
         return out
     x = _cl(x)
+    res_hold = getattr(residual, "_imgcls_xf", None) if residual is not None else None
     if residual is not None:
         residual = _cl(residual)
     ensure_channels_last_weight(conv)
@@ -884,10 +916,11 @@ def conv_bn_act(x, conv, bn, act, residual, x_slot=None, res_slot=None, exclusiv
     if conv.bias is not None:
         raise NotImplementedError("conv bias before BatchNorm")
     link = BwdLink() if (_common.FUSE_BN_BWD and bn.training and torch.is_grad_enabled()) else None
-    hold = XfHold() if (defer_act and FUSE_XF and bn.training and torch.is_grad_enabled() and residual is None
-                        and out is None and ACT[act] <= 1 and not _shadows.FP8_FWD) else None
+    hold = XfHold() if (((defer_act and FUSE_XF and ACT[act] <= 1) or (defer_res and RES_DEFER and ACT[act] == 0))
+                        and bn.training and torch.is_grad_enabled() and residual is None
+                        and out is None and not _shadows.FP8_FWD) else None
     res_out = BNActFn.apply(y, bn.weight, bn.bias, residual, bn, act, ready, res_slot, link, out,
-                            xa if not depthwise and not dense else None, shift, hold)
+                            xa if not depthwise and not dense else None, shift, hold, res_hold)
     if link is not None:
         res_out._imgcls_link = link
     if hold is not None:
@@ -941,7 +974,8 @@ DW_LINK = os.environ.get("IMGCLS_DW_LINK", "0") == "1"
 # names this part owns (ops/hip.py re-exports them)
 _OWNED = (
     'BNActFn', 'BNActPoolFn', 'BwdLink', 'ConvBiasFn', 'ConvFn', 'DW_LINK', 'DenseConvFn', 'DwConvFn',
-    'FUSE_XA', 'FUSE_XF', 'GradSlot', 'PEER_BN_MAX_C', 'POOL_CONV_SWAP', 'RELU_MASK', 'STEM_DIRECT',
+    'FUSE_XA', 'FUSE_XF', 'GradSlot', 'PEER_BN_MAX_C', 'POOL_CONV_SWAP', 'RELU_MASK', 'RES_DEFER', 'RES_DEFER_COUNT',
+    'STEM_DIRECT',
     'STEM_POOL_FUSE', 'STEM_S2D', 'SYNCBN_EARLY_COUNT', 'StemS2dFn', 'XA_COUNT', 'XA_MAX_REP', 'XA_NARROW_OFF',
     'XF_COUNT', 'XF_MAX_REP', 'XA_OUT', 'XA_OUT_COUNT', '_xa_out_ok', 'XaLink', 'XfHold', 'XfMaterializeFn', '_S2D_INDEX', '_as_pixel_rows',
     '_bn_bwd_k', '_bn_coef', '_dense_geom', '_rep', '_s2d_geom', '_s2d_index', '_syncbn_bwd_start', 'conv',

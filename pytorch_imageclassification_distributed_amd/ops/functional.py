@@ -112,7 +112,7 @@ def grad_slot(x, n: int = 2):
 
 
 def conv_bn_act(x, conv, bn, act="relu", residual=None, x_slot=None, res_slot=None, exclusive_input=False,
-                out=None, pool=None, prepool=None, defer_act=False):
+                out=None, pool=None, prepool=None, defer_act=False, defer_res=False):
     """act(bn(conv(x)) [+ residual]).
 
     Reference equivalents: torchvision ``BasicConv2d`` (conv -> BN -> ReLU),
@@ -125,6 +125,8 @@ def conv_bn_act(x, conv, bn, act="relu", residual=None, x_slot=None, res_slot=No
     output - both are linear, so conv1x1(avgpool(x)) == avgpool(conv1x1(x)).
     ``defer_act``: the caller feeds the result only to the next ``conv_bn_act`` (as its exclusive input);
     the HIP path may then skip writing act(bn(y)) and let that conv apply the BN on its operand loads.
+    ``defer_res``: the result (no activation) is used only as the ``residual`` of one later ``conv_bn_act``
+    (a ResNet downsample branch); the HIP path then skips writing bn(y) and that BN applies it on its loads.
     """
     if prepool is not None:
         if residual is not None or pool is not None:
@@ -143,7 +145,7 @@ def conv_bn_act(x, conv, bn, act="relu", residual=None, x_slot=None, res_slot=No
     if use_hip(x):
         hout = (out[0].hip(), out[1]) if (out is not None and _hip().CONCAT_INPLACE) else None
         return _hip().conv_bn_act(x, conv, bn, act, residual, x_slot, res_slot, exclusive_input, hout,
-                                  defer_act=defer_act)
+                                  defer_act=defer_act, defer_res=defer_res)
     y = _torch_bn(_torch_conv(x, conv), bn)
     if residual is not None:
         y = y + residual

@@ -390,3 +390,49 @@ def test_fused_xa_backward_matches_separate(n_blocks, hw):
     assert err(gx1, gx0) < 1e-2, err(gx1, gx0)
     for n in gp0:
         assert err(gp1[n], gp0[n]) < 1e-2, (n, err(gp1[n], gp0[n]))
+
+
+@pytest.mark.parametrize("kind", ["basic_ds", "bottle_ds", "chain"])
+@pytest.mark.parametrize("fused", [True, False])
+def test_deferred_downsample_bn(kind, fused):
+    """The downsample BN's apply folded into the residual BN's (ops/_hip/convbn.py RES_DEFER: the residual
+    apply forms sc3 * y3 + sh3 + bf16(sc_ds * y_ds + sh_ds)): input and parameter gradients and running
+    statistics equal the materialized residual's, with the fused BN backward on (the consumer reads the ReLU
+    mask) and off (the residual BN's backward re-forms the residual).  The output also matches in eval mode
+    (not deferred)."""
+    import torch.nn as nn
+    from pytorch_imageclassification_distributed_amd.models.resnet import BasicBlock, Bottleneck, _conv1x1
+    from pytorch_imageclassification_distributed_amd.ops import hip
+    torch.manual_seed(1)
+    if kind == "basic_ds":
+        blk, cin = BasicBlock(64, 128, 2, nn.Sequential(_conv1x1(64, 128, 2), nn.BatchNorm2d(128))), 64
+    elif kind == "bottle_ds":
+        blk, cin = Bottleneck(256, 128, 2, nn.Sequential(_conv1x1(256, 512, 2), nn.BatchNorm2d(512))), 256
+    else:
+        blk = nn.Sequential(Bottleneck(256, 128, 2, nn.Sequential(_conv1x1(256, 512, 2), nn.BatchNorm2d(512))),
+                            Bottleneck(512, 128))
+        cin = 256
+    blk = blk.to(DEV).to(memory_format=torch.channels_last)
+    ref = copy.deepcopy(blk)
+    x = torch.randn(4, cin, 16, 16, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    keep = hip.RES_DEFER
+    try:
+        hip.RES_DEFER = False
+        gx0, gp0 = _grads(ref, x, fused)
+        hip.RES_DEFER = True
+        n0 = hip.RES_DEFER_COUNT[0]
+        gx1, gp1 = _grads(blk, x, fused)
+        assert hip.RES_DEFER_COUNT[0] > n0, "the downsample BN was not deferred"
+    finally:
+        hip.RES_DEFER = keep
+    err = lambda a, b: ((a - b).abs().max() / b.abs().max().clamp(min=1e-6)).item()  # noqa: E731
+    assert err(gx1, gx0) < 1e-2, err(gx1, gx0)
+    for n in gp0:
+        assert err(gp1[n], gp0[n]) < 1e-2, (n, err(gp1[n], gp0[n]))
+    for (n, b0), b1 in zip(ref.named_buffers(), blk.buffers()):
+        if b0.is_floating_point():
+            assert torch.allclose(b1, b0, rtol=1e-3, atol=1e-4), n
+    blk.eval()
+    ref.eval()
+    with torch.no_grad():
+        assert err(blk(x).float(), ref(x).float()) < 1e-2
