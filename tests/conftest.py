@@ -13,6 +13,23 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running test")
 
 
+@pytest.fixture(autouse=True, scope="session")
+def _reference_convs_without_miopen():
+    """fp32 reference convolutions on ATen's own kernels (im2col + rocBLAS, native depthwise), not MIOpen.
+
+    On a fresh box MIOpen compiles its kernels at first use; twice in round 5 (gpurun_out r13o / r13x, the
+    fp32 backward of a 144 -> 24 1x1 conv in test_conv_pw_configs[case2-10]) and once before (r6b, the
+    EfficientNet-B0 reference in test_gpu_learning) that compile failed ("EvaluateInvokers ... Error setting
+    device", "Empty code object path") and the GPU was left faulted for every later test.  The references'
+    numerics do not depend on which library runs their convs.  IMGCLS_TEST_MIOPEN=1 keeps MIOpen."""
+    import torch
+    keep = torch.backends.cudnn.enabled
+    if os.environ.get("IMGCLS_TEST_MIOPEN", "0") != "1":
+        torch.backends.cudnn.enabled = False
+    yield
+    torch.backends.cudnn.enabled = keep
+
+
 def pytest_collection_modifyitems(config, items):
     import torch
     if torch.cuda.is_available():

@@ -259,6 +259,7 @@ def test_conv_pw_configs(case, cfg):
     assert torch.allclose(bn.running_var, bn_r.running_var, rtol=1e-2, atol=1e-3)
     g = bf(torch.randn_like(ref))
     out.backward(g.to(torch.bfloat16).contiguous(memory_format=CL))
+    torch.cuda.synchronize()  # a fault in this backward's kernels is reported here, not inside the reference's
     ref.backward(g)
     assert rel_err(xb.grad, xr.grad) < 3e-2
     assert rel_err(conv.weight.grad, conv_r.weight.grad) < 3e-2
