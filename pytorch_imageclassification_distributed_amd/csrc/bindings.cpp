@@ -173,7 +173,8 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
                std::vector<int> dh, std::vector<int> dw, std::vector<int> tb, int stats_groups, Tensor zero,
                OT addend, OT bwd_y, OT bwd_res, OT bwd_coef, OT bwd_part, int bwd_act, int bwd_groups,
                int stages, int tile_n, int cfg, OT a_sc, OT b_sc, OT xa_y, OT xa_coef, OT xa_out, OT stats_shift,
-               OT xf_coef, int xf_act, OT bwd_mask, OT fw_x, OT fw_ws, OT fw_dw, int fw_blocks) {
+               OT xf_coef, int xf_act, OT bwd_mask, OT fw_x, OT fw_ws, OT fw_dw, int fw_blocks, OT bwd_y2,
+               OT bwd_coef2, OT bwd_part2) {
   const bool fp8 = a_sc.has_value() && a_sc->defined();
   TORCH_CHECK(A.scalar_type() == (fp8 ? at::kFloat8_e4m3fn : BF) && B.scalar_type() == A.scalar_type(),
               "conv_gemm: A and B must both be bf16, or both float8_e4m3fn with scales");
@@ -236,6 +237,18 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
                   "conv_gemm: bwd_mask needs uint8 [C.numel()/8], ReLU and a dense output");
       p.bwd_mask = bwd_mask->data_ptr<uint8_t>();
     }
+  }
+  p.bwd_y2 = optr<bf16_t>(bwd_y2);
+  p.bwd_coef2 = optr<float>(bwd_coef2);
+  p.bwd_part2 = optr<float>(bwd_part2);
+  if (p.bwd_y2) {
+    // the deferred downsample BN's partial sums beside the residual BN's: the mask epilogue only
+    const bool direct = p.so == 1 && p.oh0 == 0 && p.ow0 == 0 && p.GH == p.OH && p.GW == p.OW;
+    TORCH_CHECK(direct && p.bwd_y && p.bwd_mask && !p.stats && !p.bias && !fp8 && bwd_y2->scalar_type() == BF &&
+                    bwd_y2->numel() == C.numel() && p.bwd_coef2 && bwd_coef2->numel() >= 4LL * Ncols && p.bwd_part2 &&
+                    bwd_part2->numel() >= 2LL * p.bwd_groups * Ncols && bwd_part->numel() >= 2LL * p.bwd_groups * Ncols,
+                "conv_gemm: bwd_y2 needs the masked fused BN backward of a direct (stride-1) data gradient, y2 matching C, [4][Ncols] coefficients and "
+                "[groups][2][Ncols] partial buffers");
   }
   if (p.addend) TORCH_CHECK(addend->numel() == C.numel() && addend->scalar_type() == BF, "conv_gemm: addend must match C");
   p.xa_y = optr<bf16_t>(xa_y);
@@ -983,7 +996,7 @@ static void rccl_bind(pybind11::module_& m) {
 PYBIND11_MODULE(_C, m) {
   rccl_bind(m);
   m.doc() = "gfx950 (MI355X) HIP kernels for pytorch_imageclassification_distributed_amd";
-  m.def("conv_gemm", &conv_gemm);
+  m.def("conv_gemm", &conv_gemm, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("C"), pybind11::arg("stats"), pybind11::arg("bias"), pybind11::arg("M"), pybind11::arg("Ncols"), pybind11::arg("K"), pybind11::arg("CA"), pybind11::arg("GH"), pybind11::arg("GW"), pybind11::arg("IH"), pybind11::arg("IW"), pybind11::arg("sA"), pybind11::arg("ldb"), pybind11::arg("OH"), pybind11::arg("OW"), pybind11::arg("so"), pybind11::arg("oh0"), pybind11::arg("ow0"), pybind11::arg("ldc"), pybind11::arg("c_off"), pybind11::arg("dh"), pybind11::arg("dw"), pybind11::arg("tb"), pybind11::arg("stats_groups"), pybind11::arg("zero"), pybind11::arg("addend"), pybind11::arg("bwd_y"), pybind11::arg("bwd_res"), pybind11::arg("bwd_coef"), pybind11::arg("bwd_part"), pybind11::arg("bwd_act"), pybind11::arg("bwd_groups"), pybind11::arg("stages"), pybind11::arg("tile_n"), pybind11::arg("cfg"), pybind11::arg("a_sc"), pybind11::arg("b_sc"), pybind11::arg("xa_y"), pybind11::arg("xa_coef"), pybind11::arg("xa_out"), pybind11::arg("stats_shift"), pybind11::arg("xf_coef"), pybind11::arg("xf_act"), pybind11::arg("bwd_mask"), pybind11::arg("fw_x"), pybind11::arg("fw_ws"), pybind11::arg("fw_dw"), pybind11::arg("fw_blocks"), pybind11::arg("bwd_y2") = pybind11::none(), pybind11::arg("bwd_coef2") = pybind11::none(), pybind11::arg("bwd_part2") = pybind11::none());
   m.def("conv_wgrad", &conv_wgrad, pybind11::arg("dY"), pybind11::arg("X"), pybind11::arg("dW"), pybind11::arg("M"),
         pybind11::arg("Cout"), pybind11::arg("Cin"), pybind11::arg("Ntot"), pybind11::arg("OH"), pybind11::arg("OW"),
         pybind11::arg("IH"), pybind11::arg("IW"), pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("pt"),

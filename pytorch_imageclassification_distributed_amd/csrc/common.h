@@ -42,6 +42,12 @@ DEVI void unpack8(const uint4& v, float* f) {
   f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
 }
 
+// element k (a compile-time constant after unrolling) of 8 bf16 held in a uint4, as unpack8 orders them
+DEVI float bf16_lane(const uint4& v, int k) {
+  const unsigned w = k < 2 ? v.x : k < 4 ? v.y : k < 6 ? v.z : v.w;
+  return __uint_as_float((k & 1) ? (w & 0xffff0000u) : (w << 16));
+}
+
 DEVI uint4 pack8(const float* f) {
   uint4 v;
   v.x = pack2(f[0], f[1]); v.y = pack2(f[2], f[3]);

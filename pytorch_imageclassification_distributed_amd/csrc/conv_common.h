@@ -172,7 +172,7 @@ DEVI void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN 
 // the store), coefficients arrive as 16-B vectors.
 // ---------------------------------------------------------------------------
 enum : int { EP_STATS = 1, EP_ADD = 2, EP_BWD = 4, EP_RES = 8, EP_DIRECT = 16, EP_RELU = 32, EP_MASK = 64,
-             EP_GENERIC = -1 };
+             EP_Y2 = 128, EP_GENERIC = -1 };
 
 DEVI int epi_mode(const ConvParams& p) {
   if (p.bias != nullptr) return EP_GENERIC;
@@ -186,6 +186,7 @@ DEVI int epi_mode(const ConvParams& p) {
   if (p.bwd_y != nullptr) {
     if (p.bwd_act != ACT_RELU) return EP_GENERIC;
     m |= EP_BWD | EP_RELU | (p.bwd_mask != nullptr ? EP_MASK : p.bwd_res != nullptr ? EP_RES : 0);
+    if (p.bwd_y2 != nullptr) m |= EP_Y2;  // (host-checked: with the mask, direct pixel map only)
   }
   return m;
 }
@@ -194,7 +195,8 @@ template <int TM, int BN, int WM, int WN, int MODE, int UR, bool STAGED = false>
 DEVI void conv_epi(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16], char* smem, int tid,
                    int lane, int wid, int wm, int wn, int m0, int n0, int bm) {
   constexpr bool STATS = MODE & EP_STATS, ADD = MODE & EP_ADD, BWD = MODE & EP_BWD, RES = MODE & EP_RES;
-  constexpr bool DIRECT = MODE & EP_DIRECT, RELU = MODE & EP_RELU, MASK = MODE & EP_MASK;
+  constexpr bool DIRECT = MODE & EP_DIRECT, RELU = MODE & EP_RELU, MASK = MODE & EP_MASK, Y2 = MODE & EP_Y2;
+  static_assert(!Y2 || MASK, "the second BN's partial sums ride on the mask epilogue only");
   constexpr int NTH = 64 * WM * WN;
   constexpr int WTM = TM / WM, WTN = BN / WN;
   constexpr int RM = WTM / 16, RN = WTN / 16;
@@ -222,9 +224,11 @@ DEVI void conv_epi(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16]
   const int col = n0 + sch * 8;
   const bool col_ok = col < p.Ncols;
   const int col_l = col_ok ? col : 0;
-  float s8[8], q8[8], k8[8];
+  float s8[8], q8[8], k8[8], r8[Y2 ? 8 : 1];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { s8[k] = 0.f; q8[k] = 0.f; k8[k] = 0.f; }
+#pragma unroll
+  for (int k = 0; k < (Y2 ? 8 : 1); ++k) r8[k] = 0.f;
   if constexpr (STATS) {
     if (p.stats_shift != nullptr) {  // pivot of the statistics (the BN's running mean)
       const f32x4 a = *(const f32x4*)(p.stats_shift + col_l), b = *(const f32x4*)(p.stats_shift + col_l + 4);
@@ -249,7 +253,7 @@ DEVI void conv_epi(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16]
   const int ghw = p.GH * p.GW;
 #pragma unroll 1
   for (int it0 = 0; it0 < IT; it0 += U) {  // not unrolled: the scheduler would hoist every row's loads
-    uint4 v[U], ad[U], yv[U], rv[U];
+    uint4 v[U], ad[U], yv[U], rv[U], y2v[Y2 ? U : 1];
     unsigned mk[U];
     long pix[U];
     bool ok[U];
@@ -271,6 +275,7 @@ DEVI void conv_epi(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16]
       if constexpr (BWD) yv[u] = *(const uint4*)(p.bwd_y + pix[u] * p.ldc + col_l);
       if constexpr (RES) rv[u] = *(const uint4*)(p.bwd_res + pix[u] * p.ldc + col_l);
       if constexpr (MASK) mk[u] = p.bwd_mask[pix[u] * (p.ldc >> 3) + (col_l >> 3)];
+      if constexpr (Y2) y2v[u] = *(const uint4*)(p.bwd_y2 + pix[u] * p.ldc + col_l);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -302,6 +307,8 @@ DEVI void conv_epi(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16]
           if (ok[u]) {
             s8[k] += dz;
             q8[k] += dz * (yf[k] - bmu[k]) * bis[k];
+            // (raw sum dz * y2: centred per block at the atomic below, no second coefficient set held)
+            if constexpr (Y2) r8[k] += dz * bf16_lane(y2v[u], k);
           }
         }
         v[u] = pack8(f);
@@ -324,28 +331,37 @@ DEVI void conv_epi(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16]
       for (int k = 0; k < 8; ++k) {
         s8[k] += __shfl_xor(s8[k], o, 64);
         q8[k] += __shfl_xor(q8[k], o, 64);
+        if constexpr (Y2) r8[k] += __shfl_xor(r8[k], o, 64);
       }
     }
+    constexpr int NS = Y2 ? 3 : 2;  // partial rows per wave
     __syncthreads();  // tile reads done; reuse LDS for the cross-wave reduction
-    float* red = (float*)smem;  // [waves][2][BN]
+    float* red = (float*)smem;  // [waves][NS][BN]
     if (lane < CPR) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        red[(wid * 2 + 0) * BN + sch * 8 + k] = s8[k];
-        red[(wid * 2 + 1) * BN + sch * 8 + k] = q8[k];
+        red[(wid * NS + 0) * BN + sch * 8 + k] = s8[k];
+        red[(wid * NS + 1) * BN + sch * 8 + k] = q8[k];
+        if constexpr (Y2) red[(wid * NS + 2) * BN + sch * 8 + k] = r8[k];
       }
     }
     __syncthreads();
     if (tid < BN && n0 + tid < p.Ncols) {
-      float s = 0.f, q = 0.f;
+      float s = 0.f, q = 0.f, r = 0.f;
 #pragma unroll
       for (int w = 0; w < WM * WN; ++w) {
-        s += red[(w * 2 + 0) * BN + tid];
-        q += red[(w * 2 + 1) * BN + tid];
+        s += red[(w * NS + 0) * BN + tid];
+        q += red[(w * NS + 1) * BN + tid];
+        if constexpr (Y2) r += red[(w * NS + 2) * BN + tid];
       }
-      float* dst = stat_dst + (size_t)(bm % stat_groups) * 2 * p.Ncols + n0 + tid;
-      atomicAdd(dst, s);
-      atomicAdd(dst + p.Ncols, q);
+      const size_t off = (size_t)(bm % stat_groups) * 2 * p.Ncols + n0 + tid;
+      atomicAdd(stat_dst + off, s);
+      atomicAdd(stat_dst + off + p.Ncols, q);
+      if constexpr (Y2) {
+        const int ch = n0 + tid;
+        atomicAdd(p.bwd_part2 + off, s);
+        atomicAdd(p.bwd_part2 + off + p.Ncols, (r - p.bwd_coef2[2 * p.Ncols + ch] * s) * p.bwd_coef2[3 * p.Ncols + ch]);
+      }
     }
   }
 }
@@ -377,6 +393,10 @@ DEVI void conv_epilogue_dispatch(const ConvParams& p, f32x4 (&acc)[TM / WM / 16]
     EPI_CASE(EP_BWD | EP_RELU | EP_RES | EP_ADD | EP_DIRECT)
     EPI_CASE(EP_BWD | EP_RELU | EP_MASK | EP_DIRECT)
     EPI_CASE(EP_BWD | EP_RELU | EP_MASK | EP_ADD | EP_DIRECT)
+    // (second-BN partials: direct pixel map only - with the remapped bodies too, every conv kernel measured
+    // ~960 B of scratch)
+    EPI_CASE(EP_BWD | EP_RELU | EP_MASK | EP_Y2 | EP_DIRECT)
+    EPI_CASE(EP_BWD | EP_RELU | EP_MASK | EP_Y2 | EP_ADD | EP_DIRECT)
     // stride-2 data gradients (sub-pixel phases, remapped pixels)
     EPI_CASE(EP_ADD)
     EPI_CASE(EP_BWD | EP_RELU)

@@ -44,6 +44,12 @@ struct ConvParams {
   const uint8_t* bwd_mask;
   const float* bwd_coef;
   float* bwd_part;
+  // optional, with bwd_mask only: a second BN whose output is the residual of this one (a deferred
+  // downsample BN) receives the same dz - its (sum dz, sum dz*xhat2) go into bwd_part2 rows, xhat2 from
+  // bwd_y2 and bwd_coef2 = [scale|shift|mean|invstd] of that BN
+  const bf16_t* bwd_y2;
+  const float* bwd_coef2;
+  float* bwd_part2;
   int bwd_act, bwd_groups;
   int stages;  // LDS-DMA ring depth: 1 (high occupancy), 2 or 3; 0 = k-step heuristic
   // MX-FP8 forward (A, B are e4m3 bytes; CA % 128 == 0): E8M0 scales, one per 32 channels -

@@ -2035,6 +2035,7 @@ static int host_epi_mode(const ConvParams& p) {
   if (p.bwd_y != nullptr) {
     if (p.bwd_act != ACT_RELU) return EP_GENERIC;
     m |= EP_BWD | EP_RELU | (p.bwd_mask != nullptr ? EP_MASK : p.bwd_res != nullptr ? EP_RES : 0);
+    if (p.bwd_y2 != nullptr) m |= EP_Y2;
   }
   return m;
 }

@@ -106,10 +106,11 @@ class BwdLink:
     the producer's BN-backward reduce (``done`` tells the producer its gradient arrives as dz)."""
 
     __slots__ = ("y", "coef", "res", "mask", "act", "part", "done", "group", "params", "pending", "c", "rows",
-                 "groups", "count_t")
+                 "groups", "count_t", "ds")
 
     def __init__(self):
         self.y = self.coef = self.res = self.mask = self.part = None
+        self.ds = None  # the deferred downsample BN's link when this BN's residual is its output (gemm.DS_FUSE)
         self.act = 0
         self.done = False
         self.group = self.params = self.pending = None  # SyncBN: early backward all-reduce
@@ -206,11 +207,12 @@ class XfHold:
     tensor holds y (the BN input), so only a conv taking the map (``ConvFn``) or ``XfMaterializeFn`` may
     read it."""
 
-    __slots__ = ("coef", "act")
+    __slots__ = ("coef", "act", "link")
 
     def __init__(self):
         self.coef = None
         self.act = 0
+        self.link = None  # a deferred residual: the deferred BN's backward link
 
 
 def xf_eligible(x, conv) -> bool:
@@ -299,6 +301,9 @@ class ConvFn(torch.autograd.Function):
                     # SyncBN: start the producer BN's backward all-reduce now, so its latency overlaps
                     # this conv's weight gradient instead of sitting between two dependent kernels
                     _syncbn_bwd_start(link)
+                ds = link.ds
+                if ds is not None and ds.done and ds.group is not None:
+                    _syncbn_bwd_start(ds)  # (the deferred downsample BN's partials came from the same epilogue)
             if slot is not None:
                 dx = slot.deliver(dx, fused=addend is not None)
         else:
@@ -632,6 +637,8 @@ class BNActFn(torch.autograd.Function):
             link.y, link.coef, link.res, link.act = y, coef, res, a
             link.group, link.params, link.c, link.rows = group, (gamma, beta), c, rows
             link.count_t = count_t
+            # a deferred downsample residual: the epilogue that produces this BN's dz also takes that BN's partials
+            link.ds = res_hold.link if (res_coef is not None and res_slot is None) else None
             ctx.link = link
         ctx.has_res = res is not None
         ctx.res_coef = res_coef
@@ -667,6 +674,7 @@ class BNActFn(torch.autograd.Function):
             _common.FUSED_BWD_COUNT[0] += 1
             pending = link.pending
             link.y = link.coef = link.res = link.mask = link.part = link.pending = link.params = link.count_t = None
+            link.ds = None
             if ldg:
                 xa = None
         else:
@@ -924,6 +932,8 @@ def conv_bn_act(x, conv, bn, act, residual, x_slot=None, res_slot=None, exclusiv
     if link is not None:
         res_out._imgcls_link = link
     if hold is not None:
+        if defer_res:
+            hold.link = link
         res_out._imgcls_xf = hold
     return res_out
 

@@ -182,7 +182,7 @@ TUNE_LOG: list = []  # (M, Ncols, K, {cfg: ms}) per tuned geometry (benchmarks/c
 
 
 def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(None, None, None, None, 0, 1),
-               groups=G_STATS, scales=(None, None), xa=None, shift=None, xf=None, mask=None):
+               groups=G_STATS, scales=(None, None), xa=None, shift=None, xf=None, mask=None, y2=None):
     """One implicit-GEMM launch.  The kernel configuration - LDS-DMA ring depth (1 = high occupancy,
     2 / 3 = pipelined) x output-channel tile (64 / 128 / 256: more tiles balance 256 CUs better on
     small layers) x pixel tile (128 rows on 4 waves, or 256 rows on 8 waves) - is chosen once per
@@ -190,11 +190,13 @@ def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(
     ``xa`` = (y, coef [3][CA]): A holds a BN's pre-elementwise gradient dz and the kernel applies the
     BN backward's elementwise map on its operand loads (1x1 stride-1 geometry; ``XaLink``).
     ``xf`` = (coef, act): A holds a BN's input y and the kernel applies act(bn(y)) on its operand loads
-    (``XfHold``)."""
+    (``XfHold``).  ``y2`` = (y2, coef2, part2) with the masked BN-backward epilogue: the partial sums of a second
+    BN that receives the same dz (a deferred downsample BN, ``BwdLink.ds``)."""
+    y2k = dict(bwd_y2=y2[0], bwd_coef2=y2[1], bwd_part2=y2[2]) if y2 is not None else {}
     xa3 = (xa[0], xa[1], xa[2] if len(xa) > 2 else None) if xa is not None else (None, None, None)
     xf2 = (xf[0], xf[1]) if xf is not None else (None, 0)
     fused = xa is not None or xf is not None
-    if DIRECT_FORCE is not None and not fused and \
+    if DIRECT_FORCE is not None and not fused and y2 is None and \
             _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales) is not None and \
             _direct_variant_ok(DIRECT_FORCE, _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales)):
         cfg = (0, 0, DIRECT_BASE + DIRECT_FORCE)  # (tests) every eligible launch on this direct variant
@@ -216,11 +218,12 @@ def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(
     else:
         key = (tuple(geo), out.shape[1], tuple(dh), tuple(dw), stats is not None, bias is not None,
                addend is not None, bwd[0] is not None, bwd[1] is not None, bwd[4], scales[0] is not None,
-               DIRECT_CONV) + ((True,) if xa is not None else ()) + (("xf",) if xf is not None else ())
+               DIRECT_CONV) + ((True,) if xa is not None else ()) + (("xf",) if xf is not None else ()) + \
+            (("y2",) if y2 is not None else ())
         cfg = _STAGES_TUNED.get(key)
         if cfg is None:
             cfg = (0, 0, -1) if torch.cuda.is_current_stream_capturing() else _tune_conv(
-                A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups, scales, xa, xf, mask)
+                A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups, scales, xa, xf, mask, y2)
             if cfg[0] or cfg[2] >= 0:
                 _STAGES_TUNED[key] = cfg
     if cfg[2] >= PW_BASE:
@@ -230,11 +233,13 @@ def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(
     elif cfg[2] >= HALO_BASE:
         HALO_COUNT[0] += 1
     elif cfg[2] >= DIRECT_BASE:
+        if y2 is not None:
+            raise RuntimeError("conv_gemm: the direct kernel has no second-BN partial sums")
         _direct_launch(A, B, out, stats, groups, _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales),
                        cfg[2] - DIRECT_BASE, bwd, shift)
         return
     C.conv_gemm(A, B, out, stats, bias, *geo, dh, dw, tb, groups, zero, addend, *bwd, *cfg, *scales, *xa3, shift,
-                *xf2, mask, None, None, None, 0)
+                *xf2, mask, None, None, None, 0, **y2k)
 
 
 _CFGS = None
@@ -425,8 +430,9 @@ def _direct_launch(A, B, out, stats, groups, dg, variant, bwd, shift=None):
 
 
 def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups, scales=(None, None), xa=None,
-               xf=None, mask=None):
+               xf=None, mask=None, y2=None):
     scratch = torch.empty_like(out)
+    y2k = dict(bwd_y2=y2[0], bwd_coef2=y2[1], bwd_part2=torch.zeros_like(y2[2])) if y2 is not None else {}
     sst = torch.zeros_like(stats) if stats is not None else None
     bwd = tuple(bwd)
     if bwd[3] is not None:
@@ -438,7 +444,7 @@ def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, group
     times = {}
     for cfg in cands:
         times[cfg] = _time_ms(lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, groups, zero,
-                                                  addend, *bwd, *cfg, *scales, *xa3, None, *xf2, mask, None, None, None, 0))
+                                                  addend, *bwd, *cfg, *scales, *xa3, None, *xf2, mask, None, None, None, 0, **y2k))
     if HALO_CONV and not fused and scales[0] is None:
         for v, (tm, bn, _wm, _wn, _bst, pmax) in enumerate(conv_halo_cfgs()):
             if v not in HALO_TUNE or not _halo_ok(geo, dh, dw, tm, pmax) or (bn > 64 and bn >= 2 * geo[1]) or \
@@ -446,7 +452,7 @@ def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, group
                 continue
             cfg = (0, 0, HALO_BASE + v)
             times[cfg] = _time_ms(lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, groups, zero,
-                                                      addend, *bwd, *cfg, *scales, *xa3, None, *xf2, mask, None, None, None, 0))
+                                                      addend, *bwd, *cfg, *scales, *xa3, None, *xf2, mask, None, None, None, 0, **y2k))
     if DEEP_CONV and not fused and scales[0] is None and _deep_ok(geo, dh, dw):
         for v, (tm, bn, _wm, _wn, var) in enumerate(conv_deep_cfgs()):
             # var & 256 (32x32x16 MFMA blocks) is measured but not tuned: 5-10% slower than the same schedule on
@@ -455,7 +461,7 @@ def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, group
                 continue
             cfg = (0, 0, DEEP_BASE + v)
             times[cfg] = _time_ms(lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, groups, zero,
-                                                      addend, *bwd, *cfg, *scales, *xa3, None, *xf2, mask, None, None, None, 0))
+                                                      addend, *bwd, *cfg, *scales, *xa3, None, *xf2, mask, None, None, None, 0, **y2k))
     if PW_CONV and not fused and scales[0] is None and bias is None and addend is None and bwd[0] is None and \
             bwd[1] is None and mask is None and _pw_ok(geo, dh, dw, tb):
         for v in range(len(conv_pw_cfgs())):
@@ -463,8 +469,8 @@ def _tune_conv(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, group
                 cfg = (0, 0, PW_BASE + v)
                 times[cfg] = _time_ms(lambda: C.conv_gemm(A, B, scratch, sst, bias, *geo, dh, dw, tb, groups, zero,
                                                           addend, *bwd, *cfg, *scales, *xa3, None, *xf2, mask, None,
-                                                          None, None, 0))
-    dg = _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales) if not fused else None
+                                                          None, None, 0, **y2k))
+    dg = _direct_geom(geo, dh, dw, tb, out, bias, addend, bwd, scales) if not fused and y2 is None else None
     if dg is not None:
         for v in DIRECT_CFGS:
             if _direct_variant_ok(v, dg):
@@ -530,17 +536,42 @@ def fused_bwd_eligible(g: ConvGeom, xa) -> bool:
     return (g.Ci == 64 and g.Co % 64 == 0 and g.Co <= 256) or (FUSED_XA_BWD_N and g.Co == 64 and g.Ci in (128, 256))
 
 
+# The deferred downsample BN of a ResNet stage (``BwdLink.ds``: its output is only the residual of this BN) receives
+# the same masked gradient dz as the residual BN: the data-gradient epilogue that produces dz also accumulates its
+# (sum dz, sum dz * xhat_ds) - one read of y_ds there instead of a separate reduce pass over dz and y_ds.
+DS_FUSE = os.environ.get("IMGCLS_DS_FUSE", "1") == "1"
+DS_FUSE_COUNT = [0]
+
+
+def _ds_partials(link, c, grp, dev, g):
+    """(y_ds, coef_ds, part_ds) for the epilogue, or None (no deferred downsample BN on this link, no mask, or a
+    data gradient whose pixels are remapped: the kernels carry the second partials on the direct map only)."""
+    ds = getattr(link, "ds", None)
+    if not DS_FUSE or ds is None or link.mask is None or ds.y is None or ds.done or ds.coef is None:
+        return None
+    if not (g.sh == 1 and g.sw == 1 and g.OH == g.H and g.OW == g.W):
+        return None
+    if ds.y.shape != link.y.shape or not ds.y.is_contiguous(memory_format=torch.channels_last):
+        return None
+    ds.part = ws(dev).take_part(c, grp)
+    ds.groups = grp
+    DS_FUSE_COUNT[0] += 1
+    return ds.y, ds.coef, ds.part
+
+
 def conv_fused_bwd_raw(dz, x, w_param, g: ConvGeom, xa, addend=None, link=None):
     """dX (as ``conv_dgrad_raw`` with ``xa``) and dW (into the parameter's arena slot or a fresh gradient
     buffer) of a ``fused_bwd_eligible`` conv from one launch; returns (dx, dw)."""
     dev = dz.device
     bwd = (None, None, None, None, 0, 1)
     mask = None
+    y2 = None
     if link is not None:
         grp = stat_groups(g.N * g.H * g.W)
         link.part = ws(dev).take_part(g.Ci, grp)
         bwd = (link.y, link.res, link.coef, link.part, link.act, grp)
         mask = link.mask
+        y2 = _ds_partials(link, g.Ci, grp, dev, g)
     wt = weight_bf16_t(w_param, g.Co, g.T, g.Ci)
     dx = _empty_cl(g.N, g.Ci, g.H, g.W, dev)
     dw = arena_slot(w_param)
@@ -553,7 +584,10 @@ def conv_fused_bwd_raw(dz, x, w_param, g: ConvGeom, xa, addend=None, link=None):
     m = g.N * g.H * g.W
     geo = (m, g.Ci, g.Co, g.Co, g.H, g.W, g.OH, g.OW, 1, g.Co, g.H, g.W, 1, 0, 0, g.Ci, 0)
     C.conv_gemm(dz, wt, dx, None, None, *geo, [0], [0], [0], G_STATS, ws(dev).zero, addend, *bwd, 0, 0, -1, None, None,
-                xa[0], xa[1], None, None, None, 0, mask, x, wsp, dw.view(-1), blocks)
+                xa[0], xa[1], None, None, None, 0, mask, x, wsp, dw.view(-1), blocks,
+                **(dict(bwd_y2=y2[0], bwd_coef2=y2[1], bwd_part2=y2[2]) if y2 is not None else {}))
+    if y2 is not None:
+        link.ds.done = True
     FUSED_XA_BWD_COUNT[0] += 1
     return dx, dw
 
@@ -570,11 +604,13 @@ def conv_dgrad_raw(dy, w_param, g: ConvGeom, addend=None, link=None, xa=None, xa
     dev = dy.device
     bwd = (None, None, None, None, 0, 1)
     mask = None
+    y2 = None
     if link is not None:
         grp = stat_groups(g.N * g.H * g.W)
         link.part = ws(dev).take_part(g.Ci, grp)
         bwd = (link.y, link.res, link.coef, link.part, link.act, grp)
         mask = link.mask
+        y2 = _ds_partials(link, g.Ci, grp, dev, g)
     wt = weight_bf16_t(w_param, g.Co, g.T, g.Ci)
     dx = _empty_cl(g.N, g.Ci, g.H, g.W, dev)
     for ph, pw, gh, gw, dh, dw, tb in _dgrad_phases(g):
@@ -584,7 +620,9 @@ def conv_dgrad_raw(dy, w_param, g: ConvGeom, addend=None, link=None, xa=None, xa
                ph, pw, g.Ci, 0)
         _conv_gemm(dy, wt, dx, None, None, geo, dh, dw, tb, ws(dev).zero, addend, bwd,
                    xa=(xa if xa_out is None else (xa[0], xa[1], xa_out)) if (xa is not None and len(tb)) else None,
-                   mask=mask)
+                   mask=mask, y2=y2)
+    if y2 is not None:
+        link.ds.done = True
     return dx
 
 
@@ -742,5 +780,5 @@ _OWNED = (
     '_fwd_taps', '_halo_ok', '_time_ms', '_tune_conv', '_weight_for_input', '_wgrad_config', '_wgrad_has',
     '_wgrad_launch', '_wgrad_plan', '_wgrad_split', '_wgrad_tiles', '_wgrad_ws', 'conv_cfgs', 'conv_deep_cfgs',
     'conv_dgrad_raw', 'conv_forward_raw', 'conv_fp8_cfgs', 'conv_fused_bwd_raw', 'conv_geom', 'conv_halo_cfgs',
-    'fp8_eligible', 'fused_bwd_eligible', 'load_tuning', 'save_tuning',
+    'fp8_eligible', 'fused_bwd_eligible', 'load_tuning', 'save_tuning', 'DS_FUSE', 'DS_FUSE_COUNT', '_ds_partials',
 )

@@ -72,7 +72,9 @@ def test_block_slots(kind):
     before = hip.FUSED_BWD_COUNT[0]
     gx1, gp1 = _grads(blk, x, True)
     fused = hip.FUSED_BWD_COUNT[0] - before
-    expect = {"basic_id": 1, "basic_ds": 1, "bottle_id": 2, "bottle_ds": 2, "chain": 5}[kind]
+    # chain: + the first block's deferred downsample BN, whose partial sums ride in the same epilogue as its BN3's
+    chain = 6 if (hip.RES_DEFER and hip.DS_FUSE and hip.RELU_MASK) else 5
+    expect = {"basic_id": 1, "basic_ds": 1, "bottle_id": 2, "bottle_ds": 2, "chain": chain}[kind]
     assert fused == expect, (kind, fused)
     err = lambda a, b: ((a - b).abs().max() / b.abs().max().clamp(min=1e-6)).item()  # noqa: E731
     assert err(gx1, gx0) < 2e-2, err(gx1, gx0)
@@ -399,7 +401,8 @@ def test_deferred_downsample_bn(kind, fused):
     apply forms sc3 * y3 + sh3 + bf16(sc_ds * y_ds + sh_ds)): input and parameter gradients and running
     statistics equal the materialized residual's, with the fused BN backward on (the consumer reads the ReLU
     mask) and off (the residual BN's backward re-forms the residual).  The output also matches in eval mode
-    (not deferred)."""
+    (not deferred).  In the chain the next block's conv1 data-gradient epilogue also accumulates the downsample
+    BN's backward partial sums (``BwdLink.ds``)."""
     import torch.nn as nn
     from pytorch_imageclassification_distributed_amd.models.resnet import BasicBlock, Bottleneck, _conv1x1
     from pytorch_imageclassification_distributed_amd.ops import hip
@@ -420,9 +423,13 @@ def test_deferred_downsample_bn(kind, fused):
         hip.RES_DEFER = False
         gx0, gp0 = _grads(ref, x, fused)
         hip.RES_DEFER = True
-        n0 = hip.RES_DEFER_COUNT[0]
+        n0, d0 = hip.RES_DEFER_COUNT[0], hip.DS_FUSE_COUNT[0]
         gx1, gp1 = _grads(blk, x, fused)
         assert hip.RES_DEFER_COUNT[0] > n0, "the downsample BN was not deferred"
+        if kind == "chain" and fused and hip.DS_FUSE:
+            # the second block's conv1 data gradient produced the first block's dz: it took the downsample BN's
+            # partial sums too (gemm.DS_FUSE)
+            assert hip.DS_FUSE_COUNT[0] > d0, "the downsample BN's partial sums did not ride in the epilogue"
     finally:
         hip.RES_DEFER = keep
     err = lambda a, b: ((a - b).abs().max() / b.abs().max().clamp(min=1e-6)).item()  # noqa: E731
