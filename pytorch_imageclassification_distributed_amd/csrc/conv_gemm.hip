@@ -2213,6 +2213,8 @@ int conv_gemm_launch(const ConvParams& p, hipStream_t stream) {
   }
   if (p.cfg >= CONV_HALO_BASE) return conv_halo_launch(p.cfg - CONV_HALO_BASE, p, stream);
   const int gm = cdiv(p.M, BM);
+  // the untuned variant-1 kernel (conv_gemm_kernel) runs the generic epilogue, which has no second-BN partials
+  if (p.bwd_y2 && p.cfg < 0 && !p.xa_y && !p.xf_coef && g_variant == 1) return 5;
   if (p.a_sc) {
     if (p.CA % 128 || p.K % 128 || !p.b_sc) return 3;
     if (p.cfg >= 0) {
