@@ -259,6 +259,10 @@ def main():
         from pytorch_imageclassification_distributed_amd.ops import hip
         print(f"[bench] saved {hip.save_tuning(a.tune_save)} kernel choices to {a.tune_save}", file=sys.stderr)
     extra = {}
+    if ctx.device.type == "cuda":
+        # allocator steady state: every device malloc / free in the timed steps is a device sync
+        extra["timed_device_malloc"] = m1["device_malloc"] - m0["device_malloc"]
+        extra["timed_device_free"] = m1["device_free"] - m0["device_free"]
     if comm_t is not None:
         from pytorch_imageclassification_distributed_amd.parallel import comm_timer
         comm_timer.uninstall()

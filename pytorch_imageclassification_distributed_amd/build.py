@@ -94,8 +94,9 @@ def build(verbose: bool = False, jobs: int | None = None, defines: dict | None =
     jobs = jobs or min(8, os.cpu_count() or 4)
     defines = defines or {}
     with cf.ThreadPoolExecutor(jobs) as ex:
-        futs = [ex.submit(_compile, k, KERNEL_FLAGS + defines.get(os.path.basename(k), []), verbose)
-                for k in kernels]
+        # a define keyed "*" applies to every kernel source (the bounds-checked build: '*:-DIMGCLS_BOUNDS_CHECK')
+        futs = [ex.submit(_compile, k, KERNEL_FLAGS + defines.get("*", []) + defines.get(os.path.basename(k), []),
+                          verbose) for k in kernels]
         futs += [ex.submit(_compile, b, cflags, verbose) for b in binds]
         objs = [f.result() for f in futs]
     key = hashlib.sha1(" ".join(objs).encode()).hexdigest()[:16]

@@ -7,11 +7,13 @@
 #include <c10/hip/HIPCachingAllocator.h>
 #include <c10/hip/HIPStream.h>
 
+#include <cstring>
 #include <optional>
 #include <unordered_map>
 #include <vector>
 
 #include "conv_gemm.h"
+#include "extents.h"
 
 extern int g_imgcls_det;  // misc.hip: deterministic mode
 
@@ -168,6 +170,26 @@ T* optr(const OT& t) { return t.has_value() && t->defined() ? reinterpret_cast<T
 constexpr auto BF = at::kBFloat16;
 constexpr auto F32 = at::kFloat;
 
+
+// [64] uint32 violation record per device for the bounds-checked build (csrc/common.h IMGCLS_INB)
+static unsigned* oob_record() {
+  static std::unordered_map<int, Tensor> rec;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  auto it = rec.find(dev);
+  if (it == rec.end())
+    it = rec.emplace(dev, torch::zeros({64}, torch::dtype(torch::kInt32).device(torch::kCUDA, dev))).first;
+  return reinterpret_cast<unsigned*>(it->second.data_ptr());
+}
+
+static std::vector<int64_t> bounds_violations() {
+  Tensor t = torch::from_blob(oob_record(), {64}, torch::dtype(torch::kInt32).device(torch::kCUDA)).clone().cpu();
+  (void)hipMemsetAsync(oob_record(), 0, 64 * sizeof(unsigned), cur());
+  std::vector<int64_t> out(64);
+  for (int i = 0; i < 64; ++i) out[i] = (int64_t)(uint32_t)t.data_ptr<int32_t>()[i];
+  return out;
+}
+
 void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols, int K, int CA, int GH, int GW,
                int IH, int IW, int sA, int ldb, int OH, int OW, int so, int oh0, int ow0, int ldc, int c_off,
                std::vector<int> dh, std::vector<int> dw, std::vector<int> tb, int stats_groups, Tensor zero,
@@ -188,6 +210,8 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
   ConvParams p{};
   p.A = ptr<bf16_t>(A); p.B = ptr<bf16_t>(B); p.C = ptr<bf16_t>(C);
   p.a_elems = A.numel(); p.b_elems = B.numel();
+  p.c_elems = C.numel();
+  p.oob = oob_record();
   p.fd_ghw = make_fastdiv((uint32_t)(GH * GW)); p.fd_gw = make_fastdiv((uint32_t)GW);
   TORCH_CHECK((long long)M < (1LL << 31), "conv_gemm: M must fit 32 bits");
   TORCH_CHECK(2LL * IH * IW * CA < (1LL << 31) && 2LL * B.numel() < (1LL << 31),
@@ -236,6 +260,7 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
                       bwd_mask->numel() * 8 >= C.numel() && bwd_act == 1 && ldc == Ncols,
                   "conv_gemm: bwd_mask needs uint8 [C.numel()/8], ReLU and a dense output");
       p.bwd_mask = bwd_mask->data_ptr<uint8_t>();
+      p.mask_bytes = bwd_mask->numel();
     }
   }
   p.bwd_y2 = optr<bf16_t>(bwd_y2);
@@ -268,6 +293,22 @@ void conv_gemm(Tensor A, Tensor B, Tensor C, OT stats, OT bias, int M, int Ncols
                 "conv_gemm: the fused BN-apply A operand needs bf16, [2][CA] coefficients, CA % 64 == 0, no bias, "
                 "identity or ReLU");
     TORCH_CHECK(cfg < 0 || conv_cfg_has_xa(cfg), "conv_gemm: configuration has no fused BN-apply variant");
+  }
+  {  // every raw-pointer access of every kernel family within its tensor (csrc/extents.h)
+    ConvExtentArgs e{};
+    e.M = M; e.Ncols = Ncols; e.K = K; e.CA = CA; e.GH = GH; e.GW = GW; e.IH = IH; e.IW = IW; e.sA = sA;
+    e.ldb = ldb; e.OH = OH; e.OW = OW; e.so = so; e.oh0 = oh0; e.ow0 = ow0; e.ldc = ldc; e.c_off = c_off;
+    e.ntaps = (long long)dh.size();
+    e.a_numel = A.numel(); e.b_numel = B.numel(); e.c_numel = C.numel();
+    e.max_tb = 0;
+    for (int t : tb) e.max_tb = t > e.max_tb ? t : e.max_tb;
+    e.stats_numel = p.stats ? stats->numel() : -1; e.stats_groups = p.stats_groups;
+    e.part_numel = p.bwd_part ? bwd_part->numel() : -1; e.part_groups = p.bwd_groups;
+    e.coef_numel = p.bwd_coef ? bwd_coef->numel() : -1;
+    e.mask_numel = p.bwd_mask ? bwd_mask->numel() : -1;
+    e.bias_numel = p.bias ? bias->numel() : -1;
+    const char* err = conv_gemm_extent_error(e);
+    TORCH_CHECK(err == nullptr, "conv_gemm: launch out of bounds: ", err ? err : "");
   }
   if (fw_x.has_value() && fw_x->defined()) {
     // fused XA 1x1 backward: this data-gradient launch also produces the weight gradient (fw_dw += ...)
@@ -302,6 +343,8 @@ void conv_wgrad(Tensor dY, Tensor X, Tensor dW, int M, int Cout, int Cin, int Nt
   p.stride_h = sh; p.stride_w = sw; p.pad_t = pt; p.pad_l = pl; p.dil_h = dh; p.dil_w = dwd; p.KW = KW;
   p.k_per_split = k_per_split;
   p.zero = ptr<bf16_t>(zero);
+  p.dw_elems = dW.numel();
+  p.oob = oob_record();
   TORCH_CHECK(stages >= 0 && stages <= 15, "conv_wgrad: stages must be 0..15");
   TORCH_CHECK((stages != 5 && stages != 6) || Cout <= 32, "conv_wgrad: stages 5 / 6 (32-row tile) need Cout <= 32");
   TORCH_CHECK((stages != 4 && stages != 7 && stages != 9) || Cout >= 256, "conv_wgrad: the 256x256 tile needs Cout >= 256");
@@ -312,6 +355,7 @@ void conv_wgrad(Tensor dY, Tensor X, Tensor dW, int M, int Cout, int Cin, int Nt
                     dW.is_non_overlapping_and_dense() && dW.numel() == (long long)Cout * Ntot && Ntot % 8 == 0,
                 "conv_wgrad: workspace must be fp32 [>= splits*Cout*Ntot] with a contiguous dW");
     p.ws = ws->data_ptr<float>();
+    p.ws_elems = ws->numel();
   }
   p.xa_y = optr<bf16_t>(xa_y);
   p.xa_coef = optr<float>(xa_coef);
@@ -326,6 +370,16 @@ void conv_wgrad(Tensor dY, Tensor X, Tensor dW, int M, int Cout, int Cin, int Nt
     TORCH_CHECK(xf_coef->numel() >= 2LL * Cin && (xf_act == 0 || xf_act == 1),
                 "conv_wgrad: the fused BN-apply X needs [2][Cin] coefficients and identity / ReLU");
     TORCH_CHECK(conv_wgrad_has_xf(stages), "conv_wgrad: this ring / tile variant has no fused BN-apply form");
+  }
+  {  // (csrc/extents.h)
+    WgradExtentArgs e{};
+    e.M = M; e.Cout = Cout; e.Cin = Cin; e.Ntot = Ntot; e.OH = OH; e.OW = OW; e.IH = IH; e.IW = IW; e.KW = KW;
+    e.k_per_split = k_per_split; e.splits = splits > 0 ? splits : 1;
+    e.dy_numel = dY.numel(); e.x_numel = X.numel(); e.dw_numel = dW.numel();
+    e.ws_numel = p.ws ? ws->numel() : -1;
+    e.tile_rows = 32; e.tile_cols = 64;  // the smallest tile of any variant: the largest grid
+    const char* err = conv_wgrad_extent_error(e);
+    TORCH_CHECK(err == nullptr, "conv_wgrad: launch out of bounds: ", err ? err : "");
   }
   if (side == 0) {
     check(conv_wgrad_launch(p, splits, cur()), "conv_wgrad");
@@ -938,6 +992,7 @@ class PeerComm {
 void register_loader(pybind11::module& m);  // loader.cpp: native image-folder loader
 void bn_set_reduce_blocks(int n, int chb);
 void bn_set_unroll(int v);
+bool bn_res_coef_ok(bool mask);
 void bn_set_stream(int grid, long nt_mb, int walk, int walk_bwd, int flat_u, int flat_u_bwd, int red_walk);  // bn.hip: grid cap / non-temporal threshold / row walk of the streaming passes
 
 static void rccl_check(int r, const char* what) {
@@ -1060,6 +1115,27 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_set_reduce_blocks", &bn_set_reduce_blocks, pybind11::arg("n"), pybind11::arg("chb") = 0);
   m.def("bn_act_maxpool", &bn_act_maxpool);
   m.def("bn_set_unroll", [](bool v) { bn_set_unroll(v ? 1 : 0); });
+  m.def("bn_res_coef_ok", &bn_res_coef_ok);
+  m.def("conv_bounds_checked", &conv_bounds_checked);
+  m.def("bounds_violations", &bounds_violations);  // and clears the record
+  // csrc/extents.h on the CPU (tests/test_extents.py): the checks every conv launch passes, from integers only.
+  // Fields in struct order; returns "" when in bounds, else the violated bound.
+  m.def("conv_extent_check", [](std::vector<long long> v) -> std::string {
+    TORCH_CHECK(v.size() == sizeof(ConvExtentArgs) / sizeof(long long), "conv_extent_check: ",
+                sizeof(ConvExtentArgs) / sizeof(long long), " fields");
+    ConvExtentArgs a;
+    std::memcpy(&a, v.data(), sizeof(a));
+    const char* e = conv_gemm_extent_error(a);
+    return e ? e : "";
+  });
+  m.def("wgrad_extent_check", [](std::vector<long long> v) -> std::string {
+    TORCH_CHECK(v.size() == sizeof(WgradExtentArgs) / sizeof(long long), "wgrad_extent_check: ",
+                sizeof(WgradExtentArgs) / sizeof(long long), " fields");
+    WgradExtentArgs a;
+    std::memcpy(&a, v.data(), sizeof(a));
+    const char* e = conv_wgrad_extent_error(a);
+    return e ? e : "";
+  });
   m.def("bn_set_stream",
         [](int grid, long nt_mb, int walk, int walk_bwd, int flat_u, int flat_u_bwd, int red_walk) {
           bn_set_stream(grid, nt_mb, walk, walk_bwd, flat_u, flat_u_bwd, red_walk);

@@ -1319,6 +1319,9 @@ void bn_set_reduce_blocks(int n, int chb) {
 }
 
 void bn_set_unroll(int v) { g_bn_unroll = v; }
+// bn_apply's residual-with-coefficients form (coef2: a deferred BN's input as the residual) exists on the flat
+// walk only, with the U-row kernels or a ReLU mask: the caller materialises the residual otherwise
+bool bn_res_coef_ok(bool mask) { return g_bn_walk == 2 && (g_bn_unroll || mask); }
 
 // streaming elementwise passes: grid cap (<= 0: grid_chan's) and non-temporal threshold in MiB (0 never, < 0 always)
 void bn_set_stream(int grid, long nt_mb, int walk, int walk_bwd, int flat_u, int flat_u_bwd, int red_walk) {

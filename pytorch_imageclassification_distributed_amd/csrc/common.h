@@ -18,12 +18,30 @@ extern int g_imgcls_div64;
 
 
 
+// Bounds-checked debug build (python build.py --out _C_bounds.so '*:-DIMGCLS_BOUNDS_CHECK', loaded with
+// IMGCLS_EXT=_C_bounds.so): every access wrapped in IMGCLS_INB whose element range ends past its tensor's extent
+// sets bit `site` in the launch's 64-word violation record (one word per lane: vector atomics) and is SKIPPED, so
+// an out-of-bounds launch is named (bounds_violations()) instead of faulting the GPU.  Release builds: `true`.
+#ifdef IMGCLS_BOUNDS_CHECK
+#define IMGCLS_INB(oob, end, lim, site) imgcls_inb((oob), (long long)(end), (long long)(lim), (site))
+#else
+#define IMGCLS_INB(oob, end, lim, site) true
+#endif
+
 typedef uint16_t bf16_t;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 #define DEVI __device__ __forceinline__
+
+#ifdef IMGCLS_BOUNDS_CHECK
+DEVI bool imgcls_inb(unsigned* oob, long long end, long long lim, unsigned site) {
+  if (end <= lim) return true;
+  if (oob != nullptr) atomicOr(oob + (threadIdx.x & 63), 1u << site);
+  return false;
+}
+#endif
 
 DEVI float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 

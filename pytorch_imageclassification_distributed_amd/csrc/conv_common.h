@@ -91,7 +91,8 @@ DEVI void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN 
       if (p.addend != nullptr) {
         float f[8], a[8];
         unpack8(v, f);
-        unpack8(*(const uint4*)(p.addend + pix * p.ldc + p.c_off + col), a);
+        if (IMGCLS_INB(p.oob, pix * p.ldc + p.c_off + col + 8, p.c_elems, 2))
+          unpack8(*(const uint4*)(p.addend + pix * p.ldc + p.c_off + col), a);
 #pragma unroll
         for (int k = 0; k < 8; ++k) f[k] += a[k];
         v = pack8(f);
@@ -99,9 +100,11 @@ DEVI void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN 
       if (bwd) {
         float gv[8], yv[8], rv[8];
         unpack8(v, gv);
-        unpack8(*(const uint4*)(p.bwd_y + pix * p.ldc + col), yv);
-        const unsigned mk = p.bwd_mask ? (unsigned)p.bwd_mask[pix * (p.ldc >> 3) + (col >> 3)] : 0u;
-        if (p.bwd_res && !p.bwd_mask) unpack8(*(const uint4*)(p.bwd_res + pix * p.ldc + col), rv);
+        if (IMGCLS_INB(p.oob, pix * p.ldc + col + 8, p.c_elems, 3)) unpack8(*(const uint4*)(p.bwd_y + pix * p.ldc + col), yv);
+        const unsigned mk = p.bwd_mask && IMGCLS_INB(p.oob, pix * (p.ldc >> 3) + (col >> 3) + 1, p.mask_bytes, 4)
+                                ? (unsigned)p.bwd_mask[pix * (p.ldc >> 3) + (col >> 3)] : 0u;
+        if (p.bwd_res && !p.bwd_mask && IMGCLS_INB(p.oob, pix * p.ldc + col + 8, p.c_elems, 5))
+          unpack8(*(const uint4*)(p.bwd_res + pix * p.ldc + col), rv);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           float dz = gv[k];
@@ -118,7 +121,7 @@ DEVI void conv_epilogue(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN 
         }
         v = pack8(gv);
       }
-      *(uint4*)(p.C + pix * p.ldc + p.c_off + col) = v;
+      if (IMGCLS_INB(p.oob, pix * p.ldc + p.c_off + col + 8, p.c_elems, 1)) *(uint4*)(p.C + pix * p.ldc + p.c_off + col) = v;
       if (p.stats != nullptr) {
         float f[8];
         unpack8(v, f);
@@ -237,7 +240,7 @@ DEVI void conv_epi(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16]
     }
   }
   __syncthreads();
-  float bsc[8], bsh[8], bmu[8], bis[8];
+  float bsc[8], bsh[8], bmu[8], bis[8], bmu2[Y2 ? 8 : 1];
   if constexpr (BWD) {
     const int C = p.Ncols;
 #pragma unroll
@@ -248,6 +251,11 @@ DEVI void conv_epi(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16]
       const f32x4 d = *(const f32x4*)(p.bwd_coef + 3 * C + col_l + 4 * h);
 #pragma unroll
       for (int k = 0; k < 4; ++k) { bsc[4 * h + k] = a[k]; bsh[4 * h + k] = b[k]; bmu[4 * h + k] = c[k]; bis[4 * h + k] = d[k]; }
+      if constexpr (Y2) {
+        const f32x4 e = *(const f32x4*)(p.bwd_coef2 + 2 * C + col_l + 4 * h);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) bmu2[4 * h + k] = e[k];
+      }
     }
   }
   const int ghw = p.GH * p.GW;
@@ -271,11 +279,14 @@ DEVI void conv_epi(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16]
         pix[u] = ((long)n * p.OH + gh * p.so + p.oh0) * p.OW + gw * p.so + p.ow0;
       }
       v[u] = *(const uint4*)(ct + row * CST + sch * 8);
-      if constexpr (ADD) ad[u] = *(const uint4*)(p.addend + pix[u] * p.ldc + p.c_off + col_l);
-      if constexpr (BWD) yv[u] = *(const uint4*)(p.bwd_y + pix[u] * p.ldc + col_l);
-      if constexpr (RES) rv[u] = *(const uint4*)(p.bwd_res + pix[u] * p.ldc + col_l);
-      if constexpr (MASK) mk[u] = p.bwd_mask[pix[u] * (p.ldc >> 3) + (col_l >> 3)];
-      if constexpr (Y2) y2v[u] = *(const uint4*)(p.bwd_y2 + pix[u] * p.ldc + col_l);
+      const bool inb = IMGCLS_INB(p.oob, pix[u] * p.ldc + p.c_off + col_l + 8, p.c_elems, 6);
+      if constexpr (ADD) ad[u] = inb ? *(const uint4*)(p.addend + pix[u] * p.ldc + p.c_off + col_l) : uint4{};
+      if constexpr (BWD) yv[u] = inb ? *(const uint4*)(p.bwd_y + pix[u] * p.ldc + col_l) : uint4{};
+      if constexpr (RES) rv[u] = inb ? *(const uint4*)(p.bwd_res + pix[u] * p.ldc + col_l) : uint4{};
+      if constexpr (MASK)
+        mk[u] = IMGCLS_INB(p.oob, pix[u] * (p.ldc >> 3) + (col_l >> 3) + 1, p.mask_bytes, 10)
+                    ? p.bwd_mask[pix[u] * (p.ldc >> 3) + (col_l >> 3)] : 0u;
+      if constexpr (Y2) y2v[u] = inb ? *(const uint4*)(p.bwd_y2 + pix[u] * p.ldc + col_l) : uint4{};
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -307,13 +318,15 @@ DEVI void conv_epi(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16]
           if (ok[u]) {
             s8[k] += dz;
             q8[k] += dz * (yf[k] - bmu[k]) * bis[k];
-            // (raw sum dz * y2: centred per block at the atomic below, no second coefficient set held)
-            if constexpr (Y2) r8[k] += dz * bf16_lane(y2v[u], k);
+            // second BN: centred per element like the first (a large |mean2| / std2 would cancel in a
+            // per-block centring); its invstd2 is a per-channel constant, applied to the block sum below
+            if constexpr (Y2) r8[k] += dz * (bf16_lane(y2v[u], k) - bmu2[k]);
           }
         }
         v[u] = pack8(f);
       }
-      if (ok[u]) *(uint4*)(p.C + pix[u] * p.ldc + p.c_off + col) = v[u];
+      if (ok[u] && IMGCLS_INB(p.oob, pix[u] * p.ldc + p.c_off + col + 8, p.c_elems, 7))
+        *(uint4*)(p.C + pix[u] * p.ldc + p.c_off + col) = v[u];
       if constexpr (STATS) {
         if (ok[u]) {
 #pragma unroll
@@ -360,7 +373,7 @@ DEVI void conv_epi(const ConvParams& p, f32x4 (&acc)[TM / WM / 16][BN / WN / 16]
       if constexpr (Y2) {
         const int ch = n0 + tid;
         atomicAdd(p.bwd_part2 + off, s);
-        atomicAdd(p.bwd_part2 + off + p.Ncols, (r - p.bwd_coef2[2 * p.Ncols + ch] * s) * p.bwd_coef2[3 * p.Ncols + ch]);
+        atomicAdd(p.bwd_part2 + off + p.Ncols, r * p.bwd_coef2[3 * p.Ncols + ch]);
       }
     }
   }

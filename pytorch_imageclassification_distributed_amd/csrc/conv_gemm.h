@@ -74,6 +74,8 @@ struct ConvParams {
   int xf_act;
   int tile_n;  // output-channel tile: 64 or 128; 0 = 64 iff Ncols <= 64 (heuristic / fp8 path)
   int cfg;     // index into the tuned configuration table (conv_cfg_info; MX-FP8: conv_fp8_cfg_info), -1 = stages/tile_n
+  long long c_elems, mask_bytes;  // C (= addend / bwd_y / bwd_res / y2) and ReLU-mask extents (bounds-checked build)
+  unsigned* oob;                  // [64] violation record of the bounds-checked build (IMGCLS_INB), else unused
   int tap_dh[CONV_MAX_TAPS];
   int tap_dw[CONV_MAX_TAPS];
   int tap_b[CONV_MAX_TAPS];
@@ -102,13 +104,17 @@ struct WgradParams {
   // are issued (overlapping them) instead of between the wait and the barrier of stage kt (set by the launcher)
   int xa_pipe;
   int xa_tab;  // floats per 8-channel chunk of the XA coefficient table in LDS: 12 (conflict-free) or 8 (packed)
+  long long dw_elems, ws_elems;  // dW / split-workspace extents (bounds-checked build)
+  unsigned* oob;                 // [64] violation record of the bounds-checked build, else unused
 };
 
 int conv_gemm_launch(const ConvParams& p, hipStream_t stream);
+bool conv_bounds_checked();  // the library was built with IMGCLS_BOUNDS_CHECK (common.h IMGCLS_INB)
 void conv_set_variant(int v);  // 0 = auto, 1 = register-staged, 2 = LDS-DMA 2-stage, 3 = LDS-DMA 3-stage
 void conv_set_single_stage(int nk);  // GEMMs with K <= nk*64 use the 1-stage (high-occupancy) ring
 int conv_num_cfgs();
 int conv_num_fp8_cfgs();
+int conv_fp8_launch(const ConvParams& p, hipStream_t stream);  // conv_fp8.hip: the MX-FP8 forward (p.a_sc set)
 void conv_fp8_cfg_info(int i, int* out5);
 void conv_cfg_info(int i, int* out5);  // {tile rows, tile channels, waves M, waves N, ring depth}
 bool conv_cfg_has_xa(int i);           // configuration i has fused BN-backward / BN-apply A-operand variants

@@ -98,7 +98,7 @@ __global__ __launch_bounds__(256) void conv_pw_kernel(const ConvParams p, int nc
           uint2 pk;
           pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
           pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-          *(uint2*)(dst + co) = pk;
+          if (IMGCLS_INB(p.oob, pix * p.ldc + p.c_off + co + 4, p.c_elems, 15)) *(uint2*)(dst + co) = pk;
         }
       }
     }

@@ -270,7 +270,8 @@ __global__ __launch_bounds__(256, 1) void wgrad_deep_kernel(const WgradParams p)
       for (int e = tid * 4; e < WTM * TN; e += NTH * 4) {
         const int row = e / TN, c = e - row * TN;
         const int co = co0 + r0 + row, col = j0 + c;
-        if (co < p.Cout && col < p.Ntot)
+        if (co < p.Cout && col < p.Ntot &&
+            IMGCLS_INB(p.oob, (long)split * p.Cout * p.Ntot + (long)co * p.Ntot + col + 4, p.ws_elems, 16))
           *(f32x4*)(slab + (long)co * p.Ntot + col) = *(const f32x4*)(st + row * LDT + c);
       }
     } else {
@@ -278,7 +279,8 @@ __global__ __launch_bounds__(256, 1) void wgrad_deep_kernel(const WgradParams p)
       for (int e = tid; e < WTM * TN; e += NTH) {
         const int row = e / TN, c = e - row * TN;
         const int co = co0 + r0 + row, col = j0 + c;
-        if (co < p.Cout && col < p.Ntot) atomicAdd(p.dW + (long)co * p.Ntot + col, st[row * LDT + c]);
+        if (co < p.Cout && col < p.Ntot && IMGCLS_INB(p.oob, (long)co * p.Ntot + col + 1, p.dw_elems, 17))
+          atomicAdd(p.dW + (long)co * p.Ntot + col, st[row * LDT + c]);
       }
     }
   }

@@ -53,6 +53,14 @@ from .optim import FusedAdam, MultiStepLR
 # stays small; ResNet-50 b1024 at 44 GiB keeps 2)
 MAX_INFLIGHT_STEPS = int(os.environ.get("IMGCLS_MAX_INFLIGHT_STEPS", "-1"))
 SMALL_STEP_FRACTION = 0.1
+# Allocator steady state: once the tuning steps are over, the caching allocator gets a spare cached segment of
+# this fraction of the step's peak allocation (large pool) plus SMALL_SPARE_MB of small-pool blocks.  With two
+# steps in flight and record_stream'ed side-stream tensors, the blocks a step needs free up at slightly different
+# points of every step, and an unlucky interleaving used to map a new segment (hipMalloc, a device sync) inside
+# otherwise steady training: Inception-v3 b128 29-49 per 20 steps, EfficientNet-B3 35, ResNet-50 b1024 1.  The
+# spare is split for such requests instead (no max_split_size is set) and coalesces back when they are freed.
+ALLOC_SPARE_FRACTION = float(os.environ.get("IMGCLS_ALLOC_SPARE", "0.25"))
+SMALL_SPARE_MB = 64
 
 
 def _is_inception(name: str) -> bool:
@@ -212,6 +220,7 @@ class Trainer:
         self.log = JsonlLogger(getattr(a, "metrics_file", None), self.ctx.is_main)
         self._prof = None
         self._graph = None  # captured whole-step HIP graph (``capture_step``)
+        self._g_coll = False  # the captured step carries the gradient collectives (native RCCL communicator)
         self._eager_steps = 0  # eager training steps run by this process (graph capture waits for 2)
         self._steps_enqueued = 0
         self._auto_inflight = None  # MAX_INFLIGHT_STEPS unset: chosen from the steady-state peak allocation
@@ -289,6 +298,23 @@ class Trainer:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.dev))
             self._inflight.append(ev)
+        if self._steps_enqueued == 3:  # (after the in-flight decision, which reads this step's peak)
+            self._reserve_allocator_spare()
+
+    def _reserve_allocator_spare(self) -> None:
+        """Leave a spare cached segment in the caching allocator (ALLOC_SPARE_FRACTION of the peak allocation;
+        never more than a quarter of the free device memory): allocate it, free it, keep it cached."""
+        if self.dev.type != "cuda" or ALLOC_SPARE_FRACTION <= 0:
+            return
+        free, _total = torch.cuda.mem_get_info(self.dev)
+        peak = torch.cuda.max_memory_allocated(self.dev)
+        big = min(int(ALLOC_SPARE_FRACTION * peak), free // 4) // (2 << 20) * (2 << 20)
+        keep = []
+        if big >= (32 << 20):
+            keep.append(torch.empty(big, dtype=torch.uint8, device=self.dev))
+        keep += [torch.empty(1 << 20, dtype=torch.uint8, device=self.dev) for _ in range(SMALL_SPARE_MB)]
+        del keep  # back to the cache: reserved, not returned to the device
+        torch.cuda.reset_peak_memory_stats(self.dev)  # the spare is not the step's peak
 
     # ------------------------------------------------------------------ HIP graph
     def capture_step(self, images, labels) -> None:
@@ -302,9 +328,13 @@ class Trainer:
 
         At N > 1 the graph holds forward + loss + backward, SyncBN exchanges included: the one-shot peer
         kernels take their call numbers from a device counter (``csrc/peer.hip``), so every replay
-        exchanges fresh statistics.  The gradient collectives cannot sit in the graph (the reducer's hooks do
-        not run on replay), so after each replay one flat all-reduce of the gradient arena and the fused
-        Adam run eagerly (``graph_step``): ~1000 host dispatches become a replay plus three."""
+        exchanges fresh statistics.  With the native RCCL communicator (``--comm-backend rccl``) the bucket
+        collectives are captured as well: the hooks run once, at capture, and enqueue each bucket's all-reduce
+        on the comm stream, which forks from the capture stream at that point and joins back before the
+        captured Adam, so on replay the collectives overlap the rest of backward exactly as in an eager step.
+        ProcessGroupNCCL's collectives cannot sit in a graph, so on that backend the capture defers them (the
+        hooks only fill the arena) and after each replay one flat all-reduce of the gradient arena and the
+        fused Adam run eagerly (``graph_step``): ~1000 host dispatches become a replay plus three."""
         if not self.graph_capable():
             raise RuntimeError("capture_step: needs the HIP path and, at N > 1, SyncBN off or on the peer "
                                "transport (no process-group collective inside the step) and no buffer broadcast")
@@ -315,7 +345,10 @@ class Trainer:
         self._g_y = labels.detach().clone()
         self._g_lrs = tuple(g["lr"] for g in self.optimizer.param_groups)
         st = self.step_stream if self.step_stream is not None else torch.cuda.Stream(device=self.dev)
-        split = self.ctx.world_size > 1
+        # in-graph collectives (native RCCL communicator): the bucket all-reduces are captured on the comm
+        # stream's fork and overlap the rest of the captured backward; Adam is captured too
+        self._g_coll = self.reducer is not None and self.reducer.graph_collectives
+        split = self.ctx.world_size > 1 and not self._g_coll
         torch.cuda.synchronize(self.dev)
         g = torch.cuda.CUDAGraph()
         if split:
@@ -324,6 +357,7 @@ class Trainer:
             self._g_loss = self._train_step(self._g_x, self._g_y, update=not split)
         if split:  # replays run no hooks; an eager step in between (another batch shape) reduces as usual
             self.reducer.deferred = False
+        if self.reducer is not None:
             self.reducer.reset_after_capture()
         torch.cuda.synchronize(self.dev)
         self._graph, self._g_stream, self._g_split = g, st, split
@@ -341,7 +375,10 @@ class Trainer:
     def graph_step(self, images, labels):
         """Replay the captured step on new inputs (same shapes); returns the step's loss tensor, valid
         until the next replay is enqueued."""
-        if self._graph is None or tuple(g["lr"] for g in self.optimizer.param_groups) != self._g_lrs:
+        # the learning rate is baked into a captured Adam launch; at N > 1 with deferred collectives Adam runs
+        # eagerly after the replay and reads the current lr, so a schedule change needs no re-capture there
+        if self._graph is None or (not self._g_split and
+                                   tuple(g["lr"] for g in self.optimizer.param_groups) != self._g_lrs):
             self._graph = None
             self.capture_step(images, labels)
         self._throttle()
@@ -354,6 +391,8 @@ class Trainer:
             self._graph.replay()
             if self._g_split:  # N > 1: the gradients of the replayed backward, summed once, then Adam
                 self.optimizer.step(grad_scale=self.reducer.flat_all_reduce())
+            elif self._g_coll:  # the replay carried the collectives: give them a deadline
+                self.reducer.arm_watchdog(st)
         caller.wait_stream(st)
         images.record_stream(st)
         labels.record_stream(st)

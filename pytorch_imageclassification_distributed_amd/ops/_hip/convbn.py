@@ -586,9 +586,12 @@ class BNActFn(torch.autograd.Function):
         if res_hold is not None:
             if res_hold.act != 0:
                 raise RuntimeError("deferred residual BN: identity activation only")
-            if cat is not None or defer is not None or a != 1 or _shadows.FP8_FWD or not RELU_MASK:
+            will_mask = bn.training and link is not None  # (the mask condition of the plain apply below)
+            if (cat is not None or defer is not None or a != 1 or _shadows.FP8_FWD or not RELU_MASK
+                    or not C.bn_res_coef_ok(will_mask)):
                 # any other form materializes the residual first (what the deferred BN would have written); the
-                # fused form needs the ReLU mask, which the backward consumers read instead of the residual
+                # fused form needs the ReLU mask, which the backward consumers read instead of the residual, and
+                # the flat apply walk (bn_res_coef_ok: the A/B knobs IMGCLS_BN_WALK / unroll can turn it off)
                 r = _empty_cl(n, c, h, w, dev)
                 C.bn_apply(res, res_hold.coef, None, r, rows, c, c, 0, 0)
                 res, res_hold = r, None

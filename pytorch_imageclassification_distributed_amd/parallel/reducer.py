@@ -50,6 +50,11 @@ import torch.nn as nn
 from ..ops.grad_arena import GradArena
 from . import comm_timer
 
+# 1: with the native communicator, a captured whole-step HIP graph carries the bucket collectives themselves
+# (forked onto the comm stream inside the graph, overlapping the rest of the captured backward); 0: the
+# capture defers them and one flat all-reduce runs after every replay
+GRAPH_COLLECTIVES = os.environ.get("IMGCLS_GRAPH_COLLECTIVES", "1") == "1"
+
 
 def _comm_stream(dev):
     """The HIP path's side stream for a bucket all-reduce (ops.hip.comm_stream), else None."""
@@ -266,9 +271,8 @@ class GradReducer:
                 self._launch(b)
         if self.rccl is not None and self.works:
             self.rccl.join()  # the compute stream waits for every bucket's collective
-            done = torch.cuda.Event()
-            done.record(self.rccl.stream)
-            self.watchdog.arm(done)  # a step whose collectives never finish ends the process (CommWatchdog)
+            if not torch.cuda.is_current_stream_capturing():  # a captured step is armed after each replay
+                self.arm_watchdog(self.rccl.stream)
         for work, dst, comp in self.works:
             if work is not None:
                 work.wait()
@@ -299,16 +303,38 @@ class GradReducer:
             p.grad = self.arena.view(self.index[id(p)])
         self._reset_counts()
 
+    @property
+    def graph_collectives(self) -> bool:
+        """The bucket collectives can sit inside a captured whole-step graph: they go through our own RCCL
+        communicator, enqueued on its comm stream (a forked branch of the capture that joins back before the
+        optimizer), with no Work object and no host wait.  ProcessGroupNCCL's Work / watchdog bookkeeping is
+        not capture-safe, so the process-group path stays ``deferred`` (``flat_all_reduce`` after replay)."""
+        return self.rccl is not None and self._collect and GRAPH_COLLECTIVES
+
+    def arm_watchdog(self, stream) -> None:
+        """Register "every collective enqueued so far on ``stream`` has finished" with the CommWatchdog: a step
+        whose collectives never complete ends the process instead of hanging (native communicator only)."""
+        if self.watchdog is not None:
+            done = torch.cuda.Event()
+            done.record(stream)
+            self.watchdog.arm(done)
+
     @torch.no_grad()
     def flat_all_reduce(self) -> float:
         """After a replayed backward (``deferred``): one all-reduce of the whole gradient arena on the current
-        stream, in place of the per-bucket collectives.  Returns the mean factor for the optimizer."""
+        stream, in place of the per-bucket collectives, in the same transport dtype as the bucketed path
+        (``comm_dtype``: bf16 casts, reduces and copies back).  Returns the mean factor for the optimizer."""
         if self._collect:
+            t = self.flat
+            c = t.to(self.comm_dtype) if self.comm_dtype not in (None, torch.float32) else t
             if self.rccl is not None:
-                self.rccl.all_reduce_(self.flat)
+                self.rccl.all_reduce_(c)
                 self.rccl.join()
+                self.arm_watchdog(self.rccl.stream)
             else:
-                dist.all_reduce(self.flat, group=self.group)
+                dist.all_reduce(c, group=self.group)
+            if c is not t:
+                t.copy_(c)
         return 1.0 / self.world
 
     def average_(self) -> None:

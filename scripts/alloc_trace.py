@@ -1,0 +1,77 @@
+"""Which allocations map new device memory (hipMalloc, a device sync each) inside steady-state training steps.
+
+    python scripts/alloc_trace.py [--model inceptionv3 --image-size 299 --batch 128] [--warmup 8] [--steps 10]
+
+Runs the bench's training step (synthetic on-device data, find-db choices) ``warmup`` times, then records the
+caching allocator's history (``torch.cuda.memory._record_memory_history``) over ``steps`` more steps and prints
+every ``segment_alloc`` event of the recorded window with its size, stream and the innermost Python frames of
+the allocation that caused it, grouped by call site.  Used to chase VERDICT r5 weak #4 (device mallocs inside the
+timed region).
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import os
+import sys
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, HERE)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="inceptionv3")
+    ap.add_argument("--image-size", type=int, default=299)
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=10)
+    a = ap.parse_args()
+    import torch
+
+    from pytorch_imageclassification_distributed_amd.data import DeviceSyntheticLoader
+    from pytorch_imageclassification_distributed_amd.engine import Trainer, build_parser
+    from pytorch_imageclassification_distributed_amd.ops import hip
+    from pytorch_imageclassification_distributed_amd.parallel import init_distributed
+
+    ctx = init_distributed(device="cuda")
+    targs = build_parser().parse_args([
+        "--synthetic", "--model", a.model, "--image-size", str(a.image_size), "--batchsize", str(a.batch),
+        "--num-classes", "7", "--num-workers", "0", "--synthetic-train-size", "8", "--synthetic-val-size", "8",
+        "--no-sync-bn", "--lr", "1e-4"])
+    tr = Trainer(targs, ctx)
+    tr.net.train()
+    hip.load_tuning(os.path.join(HERE, "tuning", "mi355x_find_db.json"))
+    data = list(iter(DeviceSyntheticLoader(a.batch, 7, a.image_size, ctx.device, steps=2, ring=2, seed=1)))
+    for i in range(a.warmup):
+        tr.train_step(data[i % 2]["image"], data[i % 2]["label"])
+    torch.cuda.synchronize()
+    s0 = torch.cuda.memory_stats()
+    torch.cuda.memory._record_memory_history(max_entries=200000, stacks="python")
+    for i in range(a.steps):
+        tr.train_step(data[i % 2]["image"], data[i % 2]["label"])
+    torch.cuda.synchronize()
+    snap = torch.cuda.memory._snapshot()
+    torch.cuda.memory._record_memory_history(enabled=None)
+    s1 = torch.cuda.memory_stats()
+    print(f"{a.model} b{a.batch}: {s1['num_device_alloc'] - s0['num_device_alloc']} device mallocs, "
+          f"{s1['num_device_free'] - s0['num_device_free']} frees in {a.steps} steps after {a.warmup} warmup; "
+          f"reserved {torch.cuda.memory_reserved() / 2**30:.1f} GiB, allocated now {torch.cuda.memory_allocated() / 2**30:.1f} GiB")
+    sites = collections.Counter()
+    sizes = collections.defaultdict(list)
+    for dev_trace in snap["device_traces"]:
+        for e in dev_trace:
+            if e["action"] != "segment_alloc":
+                continue
+            fr = [f for f in e.get("frames", []) if f.get("filename", "").find("pytorch_imageclassification") >= 0 or
+                  f.get("filename", "").endswith("bench.py")]
+            site = " <- ".join(f"{os.path.basename(f['filename'])}:{f['line']}:{f['name']}" for f in fr[:4]) or "(no python frame)"
+            sites[(site, e.get("stream", 0))] += 1
+            sizes[(site, e.get("stream", 0))].append(e["size"])
+    for (site, stream), n in sites.most_common(30):
+        sz = sizes[(site, stream)]
+        print(f"{n:4d} x  {min(sz) / 2**20:9.2f}..{max(sz) / 2**20:9.2f} MiB  stream {stream}  {site}")
+
+
+if __name__ == "__main__":
+    main()

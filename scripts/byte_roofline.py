@@ -2,7 +2,12 @@
 
     rocprofv3 --pmc FETCH_SIZE -d <dir_fetch> -o p --output-format csv -- python3 bench.py ...
     rocprofv3 --pmc WRITE_SIZE -d <dir_write> -o p --output-format csv -- python3 bench.py ...
-    python scripts/byte_roofline.py <dir_fetch> <dir_write> [peak_tbps=6.0] [peak_tf=2300]
+    python scripts/byte_roofline.py <dir_fetch> <dir_write> [peak_tbps=6.0] [fetch_scale=2.0]
+
+``fetch_scale`` multiplies FETCH_SIZE: on gfx950 the counter reports half the bytes of 16-B-per-lane streaming
+reads, global loads and LDS-DMA alike (MI355X_MICROARCH.md §HBM; calibrated on known byte counts by
+scripts/probes/fetch_calib.hip, profiles/r15c_fetch_calibration.txt), which is how every kernel here reads its
+tensors.  Round-5 byte rooflines (r13a, r13f) used the raw counter: their read bytes are half the real ones.
 
 The step is the span between the last two ``adam_kernel`` dispatches of each pass (counter runs serialise
 the kernels, so each dispatch's time is its own, without the side-stream overlap of a real step).  Bytes
@@ -44,6 +49,7 @@ def _step(path):
 def main():
     fetch, write = _step(sys.argv[1]), _step(sys.argv[2])
     peak_bw = float(sys.argv[3]) if len(sys.argv) > 3 else 6.0
+    fscale = float(sys.argv[4]) if len(sys.argv) > 4 else 2.0
     if len(fetch) != len(write):
         raise SystemExit("the two passes ran different kernel sequences")
     # the per-shape tuner may pick another tile for a shape the find-db does not list: pair dispatches by
@@ -56,7 +62,7 @@ def main():
     for f, w in zip(fetch, write):
         k = _short(f["Kernel_Name"])
         us = (int(f["End_Timestamp"]) - int(f["Start_Timestamp"])) / 1e3
-        nb = (float(f["Counter_Value"]) + float(w["Counter_Value"])) * 1024.0
+        nb = (fscale * float(f["Counter_Value"]) + float(w["Counter_Value"])) * 1024.0
         per[k][0] += us
         per[k][1] += nb
         per[k][2] += 1
@@ -70,6 +76,7 @@ def main():
         cls[c][2] += n
     tot_us = sum(v[0] for v in per.values())
     tot_b = sum(v[1] for v in per.values())
+    print(f"(FETCH_SIZE x {fscale:g}: gfx950 counts half the bytes of 16-B streaming reads)")
     print(f"one step, kernels serialised: {tot_us / 1e3:.2f} ms, {tot_b / 1e9:.2f} GB HBM traffic "
           f"({tot_b / tot_us / 1e6:.2f} TB/s mean); roofline at {peak_bw:.1f} TB/s = {tot_b / peak_bw / 1e9:.2f} ms")
     print(f"{'class':28s} {'ms':>7s} {'GB':>7s} {'TB/s':>5s} {'roof_ms':>7s} {'x_roof':>6s} {'launch':>6s}")

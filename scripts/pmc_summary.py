@@ -22,7 +22,7 @@ for d in sys.argv[1:]:
         k = r["Kernel_Name"]
         if not any(t in k for t in ("glds_kernel", "direct_conv", "direct64", "deep_kernel", "Cijk", "conv_pw", "wgrad", "fused_bwd", "bn_apply", "bn_bwd", "stem")):
             continue
-        kn = k.replace("void (anonymous namespace)::", "").split("(")[0]
+        kn = k.replace("void ", "", 1).replace("(anonymous namespace)::", "").split("(")[0]
         acc[kn][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for kn, cs in acc.items():
         runs[(tag, kn)].update({c: sum(v) / len(v) for c, v in cs.items()})

@@ -1,0 +1,81 @@
+"""Gradient collectives inside a captured whole-step HIP graph.
+
+With the native RCCL communicator (``GradReducer(comm="rccl")``) ``Trainer.capture_step`` captures the bucket
+all-reduces on the comm stream's fork of the capture, and the fused Adam behind their join.  One GPU hosts a
+world of one; ``force_collectives`` makes the reducer issue every bucket collective anyway (a sum over one rank
+is the identity), so replay must equal eager training bitwise in deterministic mode, while the graph really
+carries RCCL nodes.  The multi-GPU run is the driver's; reference: /root/reference/train.py:128 (DDP), README:6.
+"""
+import time
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _trainer(collectives: bool):
+    from pytorch_imageclassification_distributed_amd.engine import Trainer, build_parser
+    from pytorch_imageclassification_distributed_amd.parallel import GradReducer, init_distributed
+    ctx = init_distributed(device="cuda")
+    args = ["--synthetic", "--model", "resnet18", "--image-size", "64", "--batchsize", "8", "--num-classes", "7",
+            "--num-workers", "0", "--synthetic-train-size", "8", "--synthetic-val-size", "8", "--no-sync-bn",
+            "--lr", "1e-3", "--seed", "3", "--deterministic"]
+    tr = Trainer(build_parser().parse_args(args), ctx)
+    if collectives:
+        tr.arena.detach_params()
+        tr.reducer = GradReducer(tr.model, comm="rccl", force_collectives=True, broadcast=False,
+                                 bucket_cap_mb=4.0, tail_bucket_mb=1.0)
+        tr.arena = tr.reducer.arena
+    tr.net.train()
+    return tr
+
+
+def test_graph_with_rccl_collectives_matches_eager():
+    from pytorch_imageclassification_distributed_amd.data import DeviceSyntheticLoader
+    from pytorch_imageclassification_distributed_amd.ops import hip
+    data = list(iter(DeviceSyntheticLoader(8, 7, 64, torch.device("cuda"), steps=6, ring=2, seed=4)))
+    try:
+        eager = _trainer(True)
+        le = [float(eager.train_step(d["image"], d["label"])) for d in data]
+        pe = [t.detach().clone() for t in list(eager.model.parameters()) + list(eager.model.buffers())]
+        eager.reducer.close()
+        del eager
+        graph = _trainer(True)
+        assert len(graph.reducer.buckets) > 1 and graph.reducer.graph_collectives
+        lg = [float(graph.train_step(d["image"], d["label"]) if i < 2 else graph.graph_step(d["image"], d["label"]))
+              for i, d in enumerate(data)]
+        pg = [t.detach() for t in list(graph.model.parameters()) + list(graph.model.buffers())]
+        assert graph._graph is not None and graph._g_coll and not graph._g_split
+        # every replay armed the watchdog with its completion event, and they all completed
+        assert graph.reducer.watchdog.check_once() is None
+        graph.reducer.close()
+    finally:
+        hip.set_deterministic(False)
+    assert le == lg
+    assert all(torch.equal(a, b) for a, b in zip(pe, pg))
+
+
+def test_graph_collective_fork_replay_cost():
+    """Replay time of the captured step with the bucket collectives forked onto the comm stream vs without
+    collectives (printed; the forked capture must not fall off a cliff the way a forked weight-gradient stream
+    did on this runtime: DESIGN.md, whole-step graph replay)."""
+    from pytorch_imageclassification_distributed_amd.data import DeviceSyntheticLoader
+    data = list(iter(DeviceSyntheticLoader(8, 7, 64, torch.device("cuda"), steps=2, ring=2, seed=4)))
+    ms = {}
+    for coll in (False, True):
+        tr = _trainer(coll)
+        for i in range(3):
+            tr.train_step(data[i % 2]["image"], data[i % 2]["label"])
+        for i in range(5):
+            tr.graph_step(data[i % 2]["image"], data[i % 2]["label"])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(30):
+            tr.graph_step(data[i % 2]["image"], data[i % 2]["label"])
+        torch.cuda.synchronize()
+        ms[coll] = (time.perf_counter() - t0) / 30 * 1e3
+        if tr.reducer is not None:
+            tr.reducer.close()
+    print(f"replay ms/step: no collectives {ms[False]:.3f}, in-graph RCCL buckets {ms[True]:.3f}")
+    assert ms[True] < 2.0 * ms[False] + 1.0

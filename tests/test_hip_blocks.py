@@ -394,7 +394,7 @@ def test_fused_xa_backward_matches_separate(n_blocks, hw):
         assert err(gp1[n], gp0[n]) < 1e-2, (n, err(gp1[n], gp0[n]))
 
 
-@pytest.mark.parametrize("kind", ["basic_ds", "bottle_ds", "chain"])
+@pytest.mark.parametrize("kind", ["basic_ds", "bottle_ds", "chain", "chain_bigmean"])
 @pytest.mark.parametrize("fused", [True, False])
 def test_deferred_downsample_bn(kind, fused):
     """The downsample BN's apply folded into the residual BN's (ops/_hip/convbn.py RES_DEFER: the residual
@@ -415,9 +415,16 @@ def test_deferred_downsample_bn(kind, fused):
         blk = nn.Sequential(Bottleneck(256, 128, 2, nn.Sequential(_conv1x1(256, 512, 2), nn.BatchNorm2d(512))),
                             Bottleneck(512, 128))
         cin = 256
+    shift = 0.0
+    if kind == "chain_bigmean":
+        # the downsample conv's output channels with |mean| / std ~ 30: the second-BN partial sums of the fused
+        # epilogue (sum dz * (y_ds - mean_ds)) must not cancel (centred per element, not per block)
+        with torch.no_grad():
+            blk[0].downsample[0].weight.add_(0.05)
+        shift = 3.0
     blk = blk.to(DEV).to(memory_format=torch.channels_last)
     ref = copy.deepcopy(blk)
-    x = torch.randn(4, cin, 16, 16, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x = (torch.randn(4, cin, 16, 16, device=DEV) + shift).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     keep = hip.RES_DEFER
     try:
         hip.RES_DEFER = False
@@ -425,8 +432,11 @@ def test_deferred_downsample_bn(kind, fused):
         hip.RES_DEFER = True
         n0, d0 = hip.RES_DEFER_COUNT[0], hip.DS_FUSE_COUNT[0]
         gx1, gp1 = _grads(blk, x, fused)
-        assert hip.RES_DEFER_COUNT[0] > n0, "the downsample BN was not deferred"
-        if kind == "chain" and fused and hip.DS_FUSE:
+        # (IMGCLS_BN_WALK / unroll A/B knobs can leave bn_apply without its residual-coefficient form: the
+        # residual is then materialised, and the results below must still match)
+        if hip.C.bn_res_coef_ok(True):
+            assert hip.RES_DEFER_COUNT[0] > n0, "the downsample BN was not deferred"
+        if kind.startswith("chain") and fused and hip.DS_FUSE:
             # the second block's conv1 data gradient produced the first block's dz: it took the downsample BN's
             # partial sums too (gemm.DS_FUSE)
             assert hip.DS_FUSE_COUNT[0] > d0, "the downsample BN's partial sums did not ride in the epilogue"
