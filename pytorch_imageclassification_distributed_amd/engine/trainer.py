@@ -53,14 +53,6 @@ from .optim import FusedAdam, MultiStepLR
 # stays small; ResNet-50 b1024 at 44 GiB keeps 2)
 MAX_INFLIGHT_STEPS = int(os.environ.get("IMGCLS_MAX_INFLIGHT_STEPS", "-1"))
 SMALL_STEP_FRACTION = 0.1
-# Allocator steady state: once the tuning steps are over, the caching allocator gets a spare cached segment of
-# this fraction of the step's peak allocation (large pool) plus SMALL_SPARE_MB of small-pool blocks.  With two
-# steps in flight and record_stream'ed side-stream tensors, the blocks a step needs free up at slightly different
-# points of every step, and an unlucky interleaving used to map a new segment (hipMalloc, a device sync) inside
-# otherwise steady training: Inception-v3 b128 29-49 per 20 steps, EfficientNet-B3 35, ResNet-50 b1024 1.  The
-# spare is split for such requests instead (no max_split_size is set) and coalesces back when they are freed.
-ALLOC_SPARE_FRACTION = float(os.environ.get("IMGCLS_ALLOC_SPARE", "0.25"))
-SMALL_SPARE_MB = 64
 
 
 def _is_inception(name: str) -> bool:
@@ -298,23 +290,6 @@ class Trainer:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.dev))
             self._inflight.append(ev)
-        if self._steps_enqueued == 3:  # (after the in-flight decision, which reads this step's peak)
-            self._reserve_allocator_spare()
-
-    def _reserve_allocator_spare(self) -> None:
-        """Leave a spare cached segment in the caching allocator (ALLOC_SPARE_FRACTION of the peak allocation;
-        never more than a quarter of the free device memory): allocate it, free it, keep it cached."""
-        if self.dev.type != "cuda" or ALLOC_SPARE_FRACTION <= 0:
-            return
-        free, _total = torch.cuda.mem_get_info(self.dev)
-        peak = torch.cuda.max_memory_allocated(self.dev)
-        big = min(int(ALLOC_SPARE_FRACTION * peak), free // 4) // (2 << 20) * (2 << 20)
-        keep = []
-        if big >= (32 << 20):
-            keep.append(torch.empty(big, dtype=torch.uint8, device=self.dev))
-        keep += [torch.empty(1 << 20, dtype=torch.uint8, device=self.dev) for _ in range(SMALL_SPARE_MB)]
-        del keep  # back to the cache: reserved, not returned to the device
-        torch.cuda.reset_peak_memory_stats(self.dev)  # the spare is not the step's peak
 
     # ------------------------------------------------------------------ HIP graph
     def capture_step(self, images, labels) -> None:

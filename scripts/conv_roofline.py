@@ -43,15 +43,47 @@ def _timed(kind, fn, flop, nbytes, desc):
     return r
 
 
+def _kernel_label(geo, out, stats, bias, addend, bwd, dh, dw, kw):
+    """The kernel the tuner picked for this launch (the same key as gemm._conv_gemm builds)."""
+    from pytorch_imageclassification_distributed_amd.ops._hip import gemm as G
+    xa, xf, y2 = kw.get("xa"), kw.get("xf"), kw.get("y2")
+    key = (tuple(geo), out.shape[1], tuple(dh), tuple(dw), stats is not None, bias is not None,
+           addend is not None, bwd[0] is not None, bwd[1] is not None, bwd[4], False,
+           G.DIRECT_CONV) + ((True,) if xa is not None else ()) + (("xf",) if xf is not None else ()) + \
+        (("y2",) if y2 is not None else ())
+    cfg = G._STAGES_TUNED.get(key)
+    if cfg is None:
+        return "?"
+    c = cfg[2]
+    tag = "+xa" if xa is not None else "+xf" if xf is not None else ""
+    if c >= G.PW_BASE:
+        return f"pw{c - G.PW_BASE}{tag}"
+    if c >= G.DEEP_BASE:
+        t = G.conv_deep_cfgs()[c - G.DEEP_BASE]
+        return f"deep{t[0]}x{t[1]}v{t[4]}{tag}"
+    if c >= G.HALO_BASE:
+        return f"halo{c - G.HALO_BASE}{tag}"
+    if c >= G.DIRECT_BASE:
+        return f"direct{c - G.DIRECT_BASE}{tag}"
+    if c >= 0:
+        t = G.conv_cfgs()[c]
+        return f"glds{t[0]}x{t[1]}/{t[2]}x{t[3]}/s{t[4]}{tag}"
+    return f"auto{tag}"
+
+
 def gemm(A, B_, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(None,) * 4 + (0, 1), **kw):
     m, n, k = geo[0], geo[1], geo[2]
     xa = kw.get("xa")
     kind = "dgrad" if (bwd[0] is not None or addend is not None or xa is not None or geo[12] > 1 or geo[13]
                        or geo[14]) else "fwd"
     nb = 2 * (A.numel() + B_.numel() + m * n) + (2 * m * n if addend is not None else 0) + \
-        (4 * m * n if bwd[0] is not None else 0) + (2 * A.numel() if xa is not None else 0)
-    return _timed(kind, lambda: _orig_gemm(A, B_, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, **kw),
-                  2.0 * m * n * k, nb, f"M={m} N={n} K={k} CA={geo[3]}")
+        (4 * m * n if bwd[0] is not None else 0) + (2 * A.numel() if xa is not None else 0) + \
+        (2 * A.numel() if (xa is not None and len(xa) > 2 and xa[2] is not None) else 0)  # XA_OUT writes dY
+    r = _timed(kind, lambda: _orig_gemm(A, B_, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, **kw),
+               2.0 * m * n * k, nb, f"M={m} N={n} K={k} CA={geo[3]}")
+    if ON[0]:
+        REC[-1] = REC[-1][:2] + REC[-1][2:] + (_kernel_label(geo, out, stats, bias, addend, bwd, dh, dw, kw),)
+    return r
 
 
 def wgrad(dy, x, out, g, m, ntot, kps, splits, stages=2, side=None, **kw):
@@ -87,9 +119,9 @@ torch.cuda.synchronize()
 
 tot = collections.defaultdict(lambda: [0.0, 0.0])
 rows = []
-for kind, desc, us, flop, nb in REC:
+for kind, desc, us, flop, nb, *lab in REC:
     roof = max(flop / (PEAK_TF * 1e12), nb / (PEAK_BW * 1e12)) * 1e6
-    rows.append((us - roof, kind, desc, us, roof, flop / us / 1e6, nb / us / 1e6))
+    rows.append((us - roof, kind, desc + (f"  [{lab[0]}]" if lab else ""), us, roof, flop / us / 1e6, nb / us / 1e6))
     tot[kind][0] += us
     tot[kind][1] += roof
 print(f"batch {B}: {len(REC)} conv GEMM launches; roofline at {PEAK_TF:.0f} TF/s, {PEAK_BW:.1f} TB/s")

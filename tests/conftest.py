@@ -17,11 +17,15 @@ def pytest_configure(config):
 def _reference_convs_without_miopen():
     """fp32 reference convolutions on ATen's own kernels (im2col + rocBLAS, native depthwise), not MIOpen.
 
-    On a fresh box MIOpen compiles its kernels at first use; twice in round 5 (gpurun_out r13o / r13x, the
-    fp32 backward of a 144 -> 24 1x1 conv in test_conv_pw_configs[case2-10]) and once before (r6b, the
-    EfficientNet-B0 reference in test_gpu_learning) that compile failed ("EvaluateInvokers ... Error setting
-    device", "Empty code object path") and the GPU was left faulted for every later test.  The references'
-    numerics do not depend on which library runs their convs.  IMGCLS_TEST_MIOPEN=1 keeps MIOpen."""
+    On a fresh box MIOpen compiles its kernels at first use.  Three times (gpurun_out r13o, r13x, and r15d on the
+    bounds-checked library) that build failed for the fp32 NCHW backward of the 144 -> 24 1x1 conv in
+    test_conv_pw_configs[case2-10] ("EvaluateInvokers ... Error setting device", "Empty code object path",
+    miopenStatusInternalError) and the context was faulted (illegal address) from then on; once before (r6b) the
+    EfficientNet-B0 reference in test_gpu_learning.  In r15d the test synchronised right after our HIP backward and
+    that synchronisation succeeded: every kernel of ours had completed without a fault, and the bounds record of every
+    earlier test - including case2-0 .. case2-9, whose backward launches are the same - was empty
+    (profiles/r15d_gpu_suite_miopen_fault.txt).  The fault follows MIOpen's failed build.  The references' numerics
+    do not depend on which library runs their convs.  IMGCLS_TEST_MIOPEN=1 keeps MIOpen."""
     import torch
     keep = torch.backends.cudnn.enabled
     if os.environ.get("IMGCLS_TEST_MIOPEN", "0") != "1":
