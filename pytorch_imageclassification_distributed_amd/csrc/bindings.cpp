@@ -55,7 +55,8 @@ int stem_s2d_conv_launch(const bf16_t*, const bf16_t*, bf16_t*, float*, int, int
 int maxpool_fwd_launch(const bf16_t*, bf16_t*, uint8_t*, int, int, int, int, int, int, int, int, int, int, int,
                        int, hipStream_t);
 int maxpool_bwd_launch(const bf16_t*, const uint8_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int,
-                       int, int, hipStream_t);
+                       int, int, hipStream_t, const bf16_t* y_out = nullptr);
+bool maxpool_bwd_relu_ok(int N, int H, int W, int C, int kh, int kw, int sh, int sw, int ph, int pw);
 int avgpool_fwd_launch(const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int, int, int,
                        hipStream_t);
 int avgpool_bwd_launch(const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int, int, int,
@@ -88,8 +89,10 @@ int add_launch(const bf16_t*, const bf16_t*, bf16_t*, long, hipStream_t);
 int dropout_launch(const float*, float*, uint8_t*, long, float, const long long*, hipStream_t);
 int dropout_bwd_launch(const float*, const uint8_t*, float*, long, float, hipStream_t);
 int scale_rows_launch(const bf16_t*, const float*, bf16_t*, long, long, hipStream_t);
-int dw_fwd_launch(const bf16_t*, const bf16_t*, bf16_t*, float*, int, int, int, int, int, int, int, int, int,
-                  int, int, int, hipStream_t);
+int dw_fwd_launch(const bf16_t*, const bf16_t*, bf16_t*, float*, int, const float*, int, int, int, int, int, int, int, int,
+                  int, int, int, int, hipStream_t);
+bool dw_fwd_stats_ok(int N, int C, int OH, int OW, int kh, int kw, int sh, int sw);
+int dw_set_stats_min_px(int v);
 int dw_dgrad_launch(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int, int,
                     int, const bf16_t*, const float*, float*, int, int, hipStream_t);
 bool dw_dgrad_link_ok(int, int, int, int, int, int);
@@ -591,10 +594,14 @@ void maxpool_fwd(Tensor x, Tensor y, OT idx, int N, int H, int W, int C, int OH,
         "maxpool_fwd");
 }
 
+// relu_out (optional): the pooled output of maxpool(relu(.)); dx then receives the ReLU-masked gradient
 void maxpool_bwd(Tensor dy, Tensor idx, Tensor dx, int N, int H, int W, int C, int OH, int OW, int kh, int kw,
-                 int sh, int sw, int ph, int pw) {
+                 int sh, int sw, int ph, int pw, OT relu_out) {
+  const bf16_t* yo = optr<bf16_t>(relu_out);
+  TORCH_CHECK(!yo || (relu_out->numel() == dy.numel() && relu_out->scalar_type() == BF),
+              "maxpool_bwd: relu_out must be the pooled output (like dy)");
   check(maxpool_bwd_launch(ptr<bf16_t>(dy), ptr<uint8_t>(idx), ptr<bf16_t>(dx), N, H, W, C, OH, OW, kh, kw, sh, sw,
-                           ph, pw, cur()),
+                           ph, pw, cur(), yo),
         "maxpool_bwd");
 }
 
@@ -767,12 +774,22 @@ void scale_rows(Tensor x, Tensor scale, Tensor y, long per_sample) {
         "scale_rows");
 }
 
+// stats / G / shift (optional): the consumer BN's batch statistics rows [G][2][C] about the pivot shift [C]
 void dw_fwd(Tensor x, Tensor w, Tensor y, OT stats, int N, int H, int W, int C, int OH, int OW, int kh, int kw,
-            int sh, int sw, int pt, int pl) {
+            int sh, int sw, int pt, int pl, int G, OT shift) {
   req(x, BF, "x"); req(w, BF, "w"); req(y, BF, "y");
   TORCH_CHECK(C % 8 == 0, "dwconv: C % 8");
-  check(dw_fwd_launch(ptr<bf16_t>(x), ptr<bf16_t>(w), ptr<bf16_t>(y), optr<float>(stats), N, H, W, C, OH, OW, kh,
-                      kw, sh, sw, pt, pl, cur()),
+  TORCH_CHECK(x.numel() == (long long)N * H * W * C && y.numel() == (long long)N * OH * OW * C &&
+                  w.numel() == (long long)kh * kw * C,
+              "dw_fwd: tensor sizes do not match the geometry");
+  float* st = optr<float>(stats);
+  if (st) {
+    req(*stats, F32, "stats");
+    TORCH_CHECK(G > 0 && stats->numel() >= 2LL * G * C, "dw_fwd: statistics rows [G][2][C]");
+    TORCH_CHECK(!shift.has_value() || !shift->defined() || shift->numel() >= C, "dw_fwd: shift [C]");
+  }
+  check(dw_fwd_launch(ptr<bf16_t>(x), ptr<bf16_t>(w), ptr<bf16_t>(y), st, G, st ? optr<float>(shift) : nullptr, N, H,
+                      W, C, OH, OW, kh, kw, sh, sw, pt, pl, cur()),
         "dw_fwd");
 }
 
@@ -1091,7 +1108,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd_elemt", &bn_bwd_elemt, pybind11::arg("g"), pybind11::arg("y"), pybind11::arg("coef"), pybind11::arg("k"), pybind11::arg("res"),
         pybind11::arg("dz_in"), pybind11::arg("dy"), pybind11::arg("rows"), pybind11::arg("C"), pybind11::arg("act"), pybind11::arg("ldg") = 0);
   m.def("maxpool_fwd", &maxpool_fwd);
-  m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("maxpool_bwd", &maxpool_bwd, pybind11::arg("dy"), pybind11::arg("idx"), pybind11::arg("dx"), pybind11::arg("N"),
+        pybind11::arg("H"), pybind11::arg("W"), pybind11::arg("C"), pybind11::arg("OH"), pybind11::arg("OW"),
+        pybind11::arg("kh"), pybind11::arg("kw"), pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("ph"),
+        pybind11::arg("pw"), pybind11::arg("relu_out") = pybind11::none());
+  m.def("maxpool_bwd_relu_ok", &maxpool_bwd_relu_ok);
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("gap_fwd", &gap_fwd);
@@ -1207,7 +1228,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("dropout", &dropout);
   m.def("dropout_bwd", &dropout_bwd);
   m.def("scale_rows", &scale_rows);
-  m.def("dw_fwd", &dw_fwd);
+  m.def("dw_fwd", &dw_fwd, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"), pybind11::arg("stats"),
+        pybind11::arg("N"), pybind11::arg("H"), pybind11::arg("W"), pybind11::arg("C"), pybind11::arg("OH"),
+        pybind11::arg("OW"), pybind11::arg("kh"), pybind11::arg("kw"), pybind11::arg("sh"), pybind11::arg("sw"),
+        pybind11::arg("pt"), pybind11::arg("pl"), pybind11::arg("G") = 0, pybind11::arg("shift") = pybind11::none());
+  m.def("dw_fwd_stats_ok", &dw_fwd_stats_ok);
+  m.def("dw_set_stats_min_px", &dw_set_stats_min_px);
   m.def("dw_dgrad", &dw_dgrad, pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("dx"), pybind11::arg("N"),
         pybind11::arg("H"), pybind11::arg("W"), pybind11::arg("C"), pybind11::arg("OH"), pybind11::arg("OW"),
         pybind11::arg("kh"), pybind11::arg("kw"), pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("pt"),

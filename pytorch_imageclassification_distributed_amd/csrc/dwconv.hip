@@ -230,16 +230,28 @@ DEVI void link_flush(const DwLink& L, int C, const float* s8, const float* q8) {
 
 // y[n][oh][ow0 + o] for o < R.  FLIP: correlate with the 180-degree rotated filter (the stride-1 data
 // gradient is this kernel on dY with padding K-1-p).
-template <int K, int S, int R, bool FLIP, bool LINK = false>
+// EPI 1 (LINK): the stride-1 data gradient with the producer BN's fused backward reduce (above).  EPI 2 (STATS):
+// the forward with the consumer BN's batch statistics in its epilogue, as the GEMM convs do (conv_common.h): the
+// lane's channel chunk is fixed, so it sums (y - K) and (y - K)^2 of the stored bf16 outputs about the BN's pivot
+// K (L.coef: the running mean, or null) in registers and flushes them like the link sums - the BN's separate
+// statistics pass over y (bn_stats, 6.4 GB of an EfficientNet-B0 b1024 step) disappears.
+template <int K, int S, int R, bool FLIP, int EPI = 0>
 __global__ __launch_bounds__(256) void dw_fwd_rs_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                         bf16_t* __restrict__ y, DwGeom g, PixIdx fd, int OWB,
                                                         DwLink L) {
+  constexpr bool LINK = EPI == 1, STATS = EPI == 2;
   constexpr int NJ = (R - 1) * S + K;
   const int cch = g.C >> 3;
   const long total = (long)g.N * g.OH * OWB * cch;
   float s8[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   LinkCoef lk;
   if constexpr (LINK) link_coef(L, g.C, lk);
+  float piv[STATS ? 8 : 1];
+  if constexpr (STATS) {
+    const int c0 = (int)(((long)blockIdx.x * blockDim.x + threadIdx.x) % cch) * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) piv[k] = L.coef != nullptr ? L.coef[c0 + k] : 0.f;
+  }
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     int c0, owb, oh, n;
     pix_decode(i, cch, OWB, g.OH, fd, c0, owb, oh, n);
@@ -285,10 +297,17 @@ __global__ __launch_bounds__(256) void dw_fwd_rs_kernel(const bf16_t* __restrict
     for (int o = 0; o < R; ++o)
       if (ow0 + o < g.OW) {
         if constexpr (LINK) link_dz(L, lk, pix0 + o, g.C, c0, acc[o], s8, q8);
-        *(uint4*)(yo + (long)o * g.C) = pack8(acc[o]);
+        const uint4 v = pack8(acc[o]);
+        *(uint4*)(yo + (long)o * g.C) = v;
+        if constexpr (STATS) {
+          float f[8];
+          unpack8(v, f);  // statistics of the stored (bf16) output
+#pragma unroll
+          for (int k = 0; k < 8; ++k) { const float d = f[k] - piv[k]; s8[k] += d; q8[k] += d * d; }
+        }
       }
   }
-  if constexpr (LINK) link_flush(L, g.C, s8, q8);
+  if constexpr (LINK || STATS) link_flush(L, g.C, s8, q8);
 }
 
 // Stride-2 data gradient in phase form: a lane owns 8 channels of the 2R input pixels w0 .. w0+2R-1 of
@@ -767,40 +786,69 @@ static bool rs_ok(int kh, int kw, int sh, int sw) {
 
 // blocks for a LINK launch: at most 2048 (one 16-value atomic flush per chunk and block), a multiple of
 // cch / gcd(cch, 256) so the grid stride is a multiple of cch (every lane keeps one channel chunk)
-static int link_grid(long total, int cch) {
-  const int b = grid_for(total, 2048);
+static int link_grid(long total, int cch, int cap = 2048) {
+  const int b = grid_for(total, cap);
   int gcd = cch, m = 256;
   while (m) { const int t = gcd % m; gcd = m; m = t; }
   const int unit = cch / gcd;
   return ((b + unit - 1) / unit) * unit;
 }
 
-template <int K, int S, int R, bool FLIP, bool LINK>
+// the statistics flush costs 2 x C atomics per block: the link grid's cap (2048) measured best (EfficientNet-B0
+// b1024 +0.6 % vs 8192 -0.6 %, profiles/r15j_dw_stats_ab.txt), and layers with few output pixels per block keep
+// the BN's own statistics pass (EfficientNet-B3 b128, 7 pixels per block at 10 x 10 x 1392: -3 % fused)
+static int g_dw_stats_cap = getenv("IMGCLS_DW_STATS_GRID") ? atoi(getenv("IMGCLS_DW_STATS_GRID")) : 2048;
+static int g_dw_stats_min_px = getenv("IMGCLS_DW_STATS_MIN_PX") ? atoi(getenv("IMGCLS_DW_STATS_MIN_PX")) : 64;
+
+template <int K, int S, int R, bool FLIP, int EPI>
 static void launch_fwd_rs(const bf16_t* x, const bf16_t* w, bf16_t* y, const DwGeom& g, const DwLink& L,
                           hipStream_t s) {
   const int OWB = (g.OW + R - 1) / R;
   const long total = (long)g.N * g.OH * OWB * (g.C / 8);
-  const int grid = LINK ? link_grid(total, g.C / 8) : grid_for(total);
-  hipLaunchKernelGGL((dw_fwd_rs_kernel<K, S, R, FLIP, LINK>), dim3(grid), dim3(256), 0, s, x, w, y, g,
+  // (the statistics flush is 16 atomics per channel chunk and block: the forward affords the plain grid's cap)
+  const int grid = EPI == 1 ? link_grid(total, g.C / 8) : EPI == 2 ? link_grid(total, g.C / 8, g_dw_stats_cap)
+                                                                    : grid_for(total);
+  hipLaunchKernelGGL((dw_fwd_rs_kernel<K, S, R, FLIP, EPI>), dim3(grid), dim3(256), 0, s, x, w, y, g,
                      make_pixidx(total, g.C / 8, OWB, g.OH), OWB, L);
 }
 
-// forward (FLIP = false) or stride-1 data gradient (FLIP = true, g = the dY -> dX geometry)
-template <bool FLIP, bool LINK = false>
+// forward (FLIP = false) or stride-1 data gradient (FLIP = true, g = the dY -> dX geometry); EPI as the kernel
+template <bool FLIP, int EPI = 0>
 static void fwd_rs(const bf16_t* x, const bf16_t* w, bf16_t* y, const DwGeom& g, hipStream_t s,
                    const DwLink& L = DwLink{nullptr, nullptr, nullptr, 1, 0}) {
-  if (g.kh == 3 && g.sh == 1) launch_fwd_rs<3, 1, 8, FLIP, LINK>(x, w, y, g, L, s);
-  else if (g.kh == 5 && g.sh == 1) launch_fwd_rs<5, 1, 8, FLIP, LINK>(x, w, y, g, L, s);
-  else if (g.kh == 3) launch_fwd_rs<3, 2, 4, FLIP, LINK>(x, w, y, g, L, s);
-  else launch_fwd_rs<5, 2, 4, FLIP, LINK>(x, w, y, g, L, s);
+  if (g.kh == 3 && g.sh == 1) launch_fwd_rs<3, 1, 8, FLIP, EPI>(x, w, y, g, L, s);
+  else if (g.kh == 5 && g.sh == 1) launch_fwd_rs<5, 1, 8, FLIP, EPI>(x, w, y, g, L, s);
+  else if (g.kh == 3) launch_fwd_rs<3, 2, 4, FLIP, EPI>(x, w, y, g, L, s);
+  else launch_fwd_rs<5, 2, 4, FLIP, EPI>(x, w, y, g, L, s);
 }
 
-int dw_fwd_launch(const bf16_t* x, const bf16_t* w, bf16_t* y, float* /*stats*/, int N, int H, int W, int C, int OH,
-                  int OW, int kh, int kw, int sh, int sw, int pt, int pl, hipStream_t s) {
+int dw_set_stats_min_px(int v) {  // (tests: 0 fuses every row-strip geometry); returns the previous value
+  const int old = g_dw_stats_min_px;
+  g_dw_stats_min_px = v;
+  return old;
+}
+
+// the forward produces the consumer BN's statistics: row-strip kernels, and enough output pixels per block that
+// the flush's atomics cost less than the statistics pass they replace
+bool dw_fwd_stats_ok(int N, int C, int OH, int OW, int kh, int kw, int sh, int sw) {
+  if (!rs_ok(kh, kw, sh, sw) || C % 8) return false;
+  const int R = sh == 1 ? 8 : 4;
+  const long total = (long)N * OH * ((OW + R - 1) / R) * (C / 8);
+  const long px = (long)N * OH * OW;
+  return px >= (long)g_dw_stats_min_px * link_grid(total, C / 8, g_dw_stats_cap);
+}
+
+
+// stats (optional): [G][2][C] rows receiving the batch statistics of y about the pivot shift (row-strip geometries
+// only: 3x3 / 5x5, stride 1 / 2; 4 = not handled, the caller runs the BN's own statistics pass)
+int dw_fwd_launch(const bf16_t* x, const bf16_t* w, bf16_t* y, float* stats, int G, const float* shift, int N, int H,
+                  int W, int C, int OH, int OW, int kh, int kw, int sh, int sw, int pt, int pl, hipStream_t s) {
   DwGeom g{N, H, W, C, OH, OW, kh, kw, sh, sw, pt, pl};
   if ((long)N * OH * OW * (C / 8) <= 0) return 0;
+  if (stats != nullptr && !rs_ok(kh, kw, sh, sw)) return 4;
   if (rs_ok(kh, kw, sh, sw)) {
-    fwd_rs<false>(x, w, y, g, s);
+    if (stats != nullptr) fwd_rs<false, 2>(x, w, y, g, s, DwLink{nullptr, shift, stats, G > 0 ? G : 1, 0});
+    else fwd_rs<false>(x, w, y, g, s);
     HIP_CHECK_LAUNCH();
     return 0;
   }
@@ -829,7 +877,7 @@ static void dgrad_rs(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const DwGeom
   if (g.sh == 1) {
     // dX = dY correlated with the rotated filter, padding K-1-p (right/bottom padding follows from the sizes)
     const DwGeom gt{g.N, g.OH, g.OW, g.C, g.H, g.W, g.kh, g.kw, 1, 1, g.kh - 1 - g.pt, g.kw - 1 - g.pl};
-    fwd_rs<true, LINK>(dy, w, dx, gt, s, L);
+    fwd_rs<true, LINK ? 1 : 0>(dy, w, dx, gt, s, L);
   } else if (g.kh == 3) {
     if (g.pl & 1) launch_dgrad_s2<3, 4, 1, LINK>(dy, w, dx, g, L, s);
     else launch_dgrad_s2<3, 4, 0, LINK>(dy, w, dx, g, L, s);

@@ -149,9 +149,13 @@ struct QuadDiv {
   FastDiv cch, MW, MH;
 };
 
+// RELU (a stem: maxpool(relu(bn(y)))): dx is the BN's dz = relu'(z) * dx - the max candidate's pooled value
+// relu(z) is positive exactly where z is, so the pooled output y_out itself gives the mask (read at the same
+// offsets as dy); the BN backward then runs with the identity activation and never recomputes it
+template <bool RELU>
 __global__ void maxpool_bwd_quad_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx,
                                         bf16_t* __restrict__ dx, PoolGeom g, QuadDiv fd, int MH, int MW,
-                                        uint32_t total) {
+                                        uint32_t total, const bf16_t* __restrict__ y_out) {
   const int cch = g.C >> 3;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     const uint32_t q = fdiv(i, fd.cch);
@@ -170,6 +174,19 @@ __global__ void maxpool_bwd_quad_kernel(const bf16_t* __restrict__ dy, const uin
         const long o = (((long)n * g.OH + ohc) * g.OW + owc) * g.C + c0;
         v[a * 2 + b] = *(const uint4*)(dy + o);
         pk[a * 2 + b] = *(const uint2*)(idx + o);
+        if constexpr (RELU) {
+          // zero the gradient of every channel whose pooled output is 0 (relu'(z) = 0 at its max candidate)
+          const uint4 yo = *(const uint4*)(y_out + o);
+          uint4& d = v[a * 2 + b];
+          const unsigned w[4] = {yo.x, yo.y, yo.z, yo.w};
+          unsigned* dd = &d.x;
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            const unsigned lo = (w[h] & 0xffffu) != 0u && !(w[h] & 0x8000u) ? 0x0000ffffu : 0u;
+            const unsigned hi = (w[h] >> 16) != 0u && !(w[h] & 0x80000000u) ? 0xffff0000u : 0u;
+            dd[h] &= lo | hi;
+          }
+        }
       }
     }
 #pragma unroll
@@ -291,18 +308,29 @@ int maxpool_fwd_launch(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, i
   return 0;
 }
 
+static bool quad_ok(long qtotal, int C, int kh, int kw, int sh, int sw, int ph, int pw) {
+  return sh == 2 && sw == 2 && kh <= 3 && kw <= 3 && ph <= 1 && pw <= 1 && qtotal < (1L << 31) && C >= 8 &&
+         !g_imgcls_div64;
+}
+
+// y_out (optional): the pooled output of maxpool(relu(.)) - dx receives the ReLU-masked gradient (quad kernel
+// geometries only: 2 = not handled, the caller keeps the activation in the BN backward)
 int maxpool_bwd_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W, int C, int OH,
-                       int OW, int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t s) {
+                       int OW, int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t s, const bf16_t* y_out) {
   PoolGeom g{N, H, W, C, OH, OW, kh, kw, sh, sw, ph, pw};
   const long total = (long)N * H * W * (C / 8);
   const int MH = (H + ph + 1) / 2, MW = (W + pw + 1) / 2;
   const long qtotal = (long)N * MH * MW * (C / 8);
   if (total <= 0) return 0;
-  if (sh == 2 && sw == 2 && kh <= 3 && kw <= 3 && ph <= 1 && pw <= 1 && qtotal < (1L << 31) && C >= 8 &&
-      !g_imgcls_div64) {
+  if (y_out != nullptr && !quad_ok(qtotal, C, kh, kw, sh, sw, ph, pw)) return 2;
+  if (quad_ok(qtotal, C, kh, kw, sh, sw, ph, pw)) {
     const QuadDiv fd{make_fastdiv(C / 8), make_fastdiv(MW), make_fastdiv(MH)};
-    hipLaunchKernelGGL(maxpool_bwd_quad_kernel, dim3(grid_for(qtotal)), dim3(256), 0, s, dy, idx, dx, g, fd, MH, MW,
-                       (uint32_t)qtotal);
+    if (y_out != nullptr)
+      hipLaunchKernelGGL(maxpool_bwd_quad_kernel<true>, dim3(grid_for(qtotal)), dim3(256), 0, s, dy, idx, dx, g, fd,
+                         MH, MW, (uint32_t)qtotal, y_out);
+    else
+      hipLaunchKernelGGL(maxpool_bwd_quad_kernel<false>, dim3(grid_for(qtotal)), dim3(256), 0, s, dy, idx, dx, g, fd,
+                         MH, MW, (uint32_t)qtotal, nullptr);
   } else if ((kh - 1) / sh <= 1 && (kw - 1) / sw <= 1 && total < (1L << 31) && !g_imgcls_div64) {
     const PoolDiv fd{make_fastdiv(C / 8), make_fastdiv(W), make_fastdiv(H), make_fastdiv(sh), make_fastdiv(sw)};
     hipLaunchKernelGGL(maxpool_bwd2x2_kernel, dim3(grid_for(total)), dim3(256), 0, s, dy, idx, dx, g, fd,
@@ -312,6 +340,11 @@ int maxpool_bwd_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, 
   }
   HIP_CHECK_LAUNCH();
   return 0;
+}
+
+bool maxpool_bwd_relu_ok(int N, int H, int W, int C, int kh, int kw, int sh, int sw, int ph, int pw) {
+  const long qtotal = (long)N * ((H + ph + 1) / 2) * ((W + pw + 1) / 2) * (C / 8);
+  return quad_ok(qtotal, C, kh, kw, sh, sw, ph, pw);
 }
 
 int avgpool_fwd_launch(const bf16_t* x, bf16_t* y, int N, int H, int W, int C, int OH, int OW, int kh, int kw,

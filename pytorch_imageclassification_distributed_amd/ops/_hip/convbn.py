@@ -403,7 +403,7 @@ class StemS2dFn(torch.autograd.Function):
     """The ResNet stem conv on the space-to-depth input (the image itself needs no gradient)."""
 
     @staticmethod
-    def forward(ctx, x, w, conv, want_stats, shift=None, s2d_hw=None):
+    def forward(ctx, x, w, conv, want_stats, shift=None, s2d_hw=None, xa=None):
         co = w.shape[0]
         if s2d_hw is not None:  # the loader converted the batch already (input_from_u8)
             n, (h, wd), xs = x.shape[0], s2d_hw, x
@@ -423,6 +423,7 @@ class StemS2dFn(torch.autograd.Function):
         else:
             y = conv_forward_raw(xs, None, g, stats=stats, wb=wq.view(-1), shift=shift if want_stats else None)
         ctx.g = g
+        ctx.xa = xa
         ctx.save_for_backward(xs, w)
         return y
 
@@ -430,11 +431,13 @@ class StemS2dFn(torch.autograd.Function):
     def backward(ctx, dy):
         xs, w = ctx.saved_tensors
         g = ctx.g
+        # STEM_XA: the pooled BN's backward handed over dz and its map; the weight gradient forms dY on its loads
+        xa = ctx.xa.take(dy) if ctx.xa is not None else None
         dy = _cl(dy)
         dw = None
         if ctx.needs_input_grad[1]:
             m, ntot = g.N * g.OH * g.OW, g.T * g.Cx
-            kps, splits, stages = _wgrad_plan(g, dy, xs, m, ntot)
+            kps, splits, stages = _wgrad_plan(g, dy, xs, m, ntot, xa=xa)
             full = torch.zeros(g.Co * ntot, dtype=torch.float32, device=dy.device)
             idx = _s2d_index(dy.device)
             slot = arena_slot(w)
@@ -442,21 +445,42 @@ class StemS2dFn(torch.autograd.Function):
 
             # the last weight gradient of backward: on the compute stream (idle by then) it runs beside the
             # side stream's backlog instead of behind it (conv_wgrad_raw, padded-channel path)
-            _gemm._wgrad_launch(dy, xs, full, g, m, ntot, kps, splits, stages)
+            _gemm._wgrad_launch(dy, xs, full, g, m, ntot, kps, splits, stages, xa=xa)
             dw.permute(0, 2, 3, 1).reshape(g.Co, 147).copy_(full.view(g.Co, ntot)[:, idx])
-        return None, dw, None, None, None, None
+        return None, dw, None, None, None, None, None
 
 
 # ---------------------------------------------------------------------------
 # depthwise convolution (EfficientNet)
 # ---------------------------------------------------------------------------
+# The depthwise forward also produces the consumer BN's batch statistics (csrc/dwconv.hip dw_fwd_rs_kernel EPI 2),
+# as the GEMM convs' epilogues do: the BN's separate statistics pass over y disappears (IMGCLS_DW_STATS=0: keep it)
+DW_STATS = os.environ.get("IMGCLS_DW_STATS", "1") == "1"
+DW_STATS_COUNT = [0]  # depthwise launches that produced their BN's statistics (tests / diagnostics)
+
+
+def dw_stats_eligible(x, conv) -> bool:
+    # (deterministic mode keeps the BN's own statistics pass: its rows take one contribution each)
+    if not DW_STATS or _common.DETERMINISTIC:
+        return False
+    g = conv_geom(x, conv)
+    return C.dw_fwd_stats_ok(g.N, g.Co, g.OH, g.OW, g.kh, g.kw, g.sh, g.sw)
+
+
 class DwConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, conv, fuse_bwd=False):
+    def forward(ctx, x, w, conv, fuse_bwd=False, want_stats=False, shift=None):
         g = conv_geom(x, conv)
         wt = weight_bf16_t(w, g.Co, g.T, 1)
         y = _empty_cl(g.N, g.Co, g.OH, g.OW, x.device)
-        C.dw_fwd(x, wt, y, None, g.N, g.H, g.W, g.Co, g.OH, g.OW, g.kh, g.kw, g.sh, g.sw, g.pt, g.pl)
+        if want_stats:
+            grp = stat_groups(g.N * g.OH * g.OW)  # the rows the BN reduces (_bn_coef)
+            stats = ws(x.device).stats_buf(g.Co, grp)
+            C.dw_fwd(x, wt, y, stats, g.N, g.H, g.W, g.Co, g.OH, g.OW, g.kh, g.kw, g.sh, g.sw, g.pt, g.pl,
+                     G=grp, shift=shift)
+            DW_STATS_COUNT[0] += 1
+        else:
+            C.dw_fwd(x, wt, y, None, g.N, g.H, g.W, g.Co, g.OH, g.OW, g.kh, g.kw, g.sh, g.sw, g.pt, g.pl)
         ctx.g = g
         # producer BN of x (this conv its only consumer): its backward reduce rides in the dgrad kernel
         link = getattr(x, "_imgcls_link", None) if fuse_bwd else None
@@ -491,7 +515,7 @@ class DwConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             dw = grad_buffer(w, zero=False)  # dw_wgrad overwrites it (ordered column sum of partial rows)
             C.dw_wgrad(dy, x, dw, g.N, g.H, g.W, g.Co, g.OH, g.OW, g.kh, g.kw, g.sh, g.sw, g.pt, g.pl)
-        return dx, dw, None, None
+        return dx, dw, None, None, None, None
 
 
 # ---------------------------------------------------------------------------
@@ -728,7 +752,7 @@ class BNActPoolFn(torch.autograd.Function):
     gathering the pooled gradient inside both BN-backward passes measured slower (docs/DESIGN.md)."""
 
     @staticmethod
-    def forward(ctx, y, gamma, beta, bn, act, stats_ready, pool, shift=None):
+    def forward(ctx, y, gamma, beta, bn, act, stats_ready, pool, shift=None, xa=None):
         dev = y.device
         n, c, h, w = y.shape
         (kh, kw), (sh, sw), (ph, pw) = pool
@@ -743,28 +767,46 @@ class BNActPoolFn(torch.autograd.Function):
         ctx.act, ctx.group, ctx.count_t, ctx.geo = a, group, count_t, geo
         ctx.training = bn.training
         ctx.params = (gamma, beta)
-        ctx.save_for_backward(y, coef, idx)
+        # STEM_XA: the ReLU mask comes from the pooled output in the pool backward, and the producer conv's
+        # weight gradient forms dY itself (XaLink) - no bn_bwd_elemt pass, no dY tensor
+        ctx.xa = xa if (xa is not None and bn.training and a == ACT["relu"] and
+                        C.maxpool_bwd_relu_ok(n, h, w, c, *geo[4:])) else None
+        ctx.save_for_backward(y, coef, idx, out if ctx.xa is not None else y)
         return out
 
     @staticmethod
     def backward(ctx, gout):
-        y, coef, idx = ctx.saved_tensors
+        y, coef, idx, out = ctx.saved_tensors
         dev = y.device
         n, c, h, w = y.shape
         rows = n * h * w
         _, _, oh, ow, kh, kw, sh, sw, ph, pw = ctx.geo
+        xa = ctx.xa
         g = _empty_cl(n, c, h, w, dev)
-        C.maxpool_bwd(_cl(gout), idx, g, n, h, w, c, oh, ow, kh, kw, sh, sw, ph, pw)
+        C.maxpool_bwd(_cl(gout), idx, g, n, h, w, c, oh, ow, kh, kw, sh, sw, ph, pw,
+                      relu_out=out if xa is not None else None)
+        act = 0 if xa is not None else ctx.act  # (g is already dz: masked by the pooled output)
         grp = stat_groups(rows)
         part = ws(dev).stats_buf(c, grp)
-        C.bn_bwd_reduce(g, y, coef, None, None, rows, c, ctx.act, part, grp)
-        k, dgamma, dbeta = _bn_bwd_k(part, grp, c, rows, ctx.training, ctx.group, ctx.count_t, ctx.params, dev)
+        C.bn_bwd_reduce(g, y, coef, None, None, rows, c, act, part, grp)
+        xac = torch.empty(3 * c, dtype=torch.float32, device=dev) if xa is not None else None
+        k, dgamma, dbeta = _bn_bwd_k(part, grp, c, rows, ctx.training, ctx.group, ctx.count_t, ctx.params, dev,
+                                     coef=coef, xa=xac)
+        if xa is not None:
+            xa.dz, xa.y, xa.coef = g, y, xac
+            STEM_XA_COUNT[0] += 1
+            return g, dgamma, dbeta, None, None, None, None, None, None
         dy = torch.empty_like(y, memory_format=CL)
-        C.bn_bwd_elemt(g, y, coef, k, None, None, dy, rows, c, ctx.act)
-        return dy, dgamma, dbeta, None, None, None, None, None
+        C.bn_bwd_elemt(g, y, coef, k, None, None, dy, rows, c, act)
+        return dy, dgamma, dbeta, None, None, None, None, None, None
 
 
 STEM_POOL_FUSE = os.environ.get("IMGCLS_STEM_POOL_FUSE", "1") == "1"
+# The ResNet stem's BN backward hands its dz and elementwise map to the stem conv's weight gradient (XA), which is
+# the only consumer of the stem's dY: the bn_bwd_elemt pass over the 112 x 112 x 64 activation and its dY tensor
+# disappear from the tail of every step (IMGCLS_STEM_XA=0: keep them)
+STEM_XA = os.environ.get("IMGCLS_STEM_XA", "1") == "1"
+STEM_XA_COUNT = [0]
 
 
 def conv_bn_act_pool(x, conv, bn, act, pool, exclusive_input=False):
@@ -777,11 +819,12 @@ def conv_bn_act_pool(x, conv, bn, act, pool, exclusive_input=False):
     ensure_channels_last_weight(conv)
     shift = stat_shift(bn)
     if stem_s2d_eligible(x, conv) and not x.requires_grad:
-        y = StemS2dFn.apply(x, conv.weight, conv, bn.training, shift, getattr(x, "_imgcls_s2d", None))
-    else:
-        if conv.groups != 1 or conv.bias is not None:
-            raise NotImplementedError("conv_bn_act_pool: grouped conv / conv bias")
-        y = ConvFn.apply(_cl(x), conv.weight, conv, bn.training, None, exclusive_input and _common.FUSE_BN_BWD, None, shift)
+        xa = XaLink() if (STEM_XA and bn.training and torch.is_grad_enabled() and conv.weight.requires_grad) else None
+        y = StemS2dFn.apply(x, conv.weight, conv, bn.training, shift, getattr(x, "_imgcls_s2d", None), xa)
+        return BNActPoolFn.apply(y, bn.weight, bn.bias, bn, act, bn.training, (k, s, p), shift, xa)
+    if conv.groups != 1 or conv.bias is not None:
+        raise NotImplementedError("conv_bn_act_pool: grouped conv / conv bias")
+    y = ConvFn.apply(_cl(x), conv.weight, conv, bn.training, None, exclusive_input and _common.FUSE_BN_BWD, None, shift)
     return BNActPoolFn.apply(y, bn.weight, bn.bias, bn, act, bn.training, (k, s, p), shift)
 
 
@@ -909,8 +952,9 @@ def conv_bn_act(x, conv, bn, act, residual, x_slot=None, res_slot=None, exclusiv
     if depthwise:
         if not (conv.groups == conv.in_channels == conv.out_channels):
             raise NotImplementedError("grouped (non-depthwise) convolution")
-        y = DwConvFn.apply(x, conv.weight, conv, exclusive_input and _common.FUSE_BN_BWD and DW_LINK)
-        ready = False
+        ready = bn.training and dw_stats_eligible(x, conv)
+        y = DwConvFn.apply(x, conv.weight, conv, exclusive_input and _common.FUSE_BN_BWD and DW_LINK, ready,
+                           shift if ready else None)
     elif dense_conv_eligible(x, conv) and x.shape[2] * x.shape[3] > 1:
         dense = True
         y = DenseConvFn.apply(x, conv.weight, conv, bn.training, shift)
@@ -986,10 +1030,11 @@ DW_LINK = os.environ.get("IMGCLS_DW_LINK", "0") == "1"
 
 # names this part owns (ops/hip.py re-exports them)
 _OWNED = (
-    'BNActFn', 'BNActPoolFn', 'BwdLink', 'ConvBiasFn', 'ConvFn', 'DW_LINK', 'DenseConvFn', 'DwConvFn',
+    'BNActFn', 'BNActPoolFn', 'BwdLink', 'ConvBiasFn', 'ConvFn', 'DW_LINK', 'DW_STATS', 'DW_STATS_COUNT',
+    'DenseConvFn', 'DwConvFn', 'dw_stats_eligible',
     'FUSE_XA', 'FUSE_XF', 'GradSlot', 'PEER_BN_MAX_C', 'POOL_CONV_SWAP', 'RELU_MASK', 'RES_DEFER', 'RES_DEFER_COUNT',
     'STEM_DIRECT',
-    'STEM_POOL_FUSE', 'STEM_S2D', 'SYNCBN_EARLY_COUNT', 'StemS2dFn', 'XA_COUNT', 'XA_MAX_REP', 'XA_NARROW_OFF',
+    'STEM_POOL_FUSE', 'STEM_S2D', 'STEM_XA', 'STEM_XA_COUNT', 'SYNCBN_EARLY_COUNT', 'StemS2dFn', 'XA_COUNT', 'XA_MAX_REP', 'XA_NARROW_OFF',
     'XF_COUNT', 'XF_MAX_REP', 'XA_OUT', 'XA_OUT_COUNT', '_xa_out_ok', 'XaLink', 'XfHold', 'XfMaterializeFn', '_S2D_INDEX', '_as_pixel_rows',
     '_bn_bwd_k', '_bn_coef', '_dense_geom', '_rep', '_s2d_geom', '_s2d_index', '_syncbn_bwd_start', 'conv',
     'conv_bn_act', 'conv_bn_act_pool', 'dense_conv_eligible', 'input_from_u8', 'materialize_deferred',

@@ -2,6 +2,8 @@
 groups=C on the same bf16-rounded operands): forward, data gradient, weight gradient, for the row-strip
 kernels (K 3/5, stride 1/2) and the per-pixel kernels they replace, over odd sizes, widths below one
 strip, asymmetric (TF "same") and symmetric padding with both parities of the left pad."""
+import copy
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -128,3 +130,59 @@ def test_depthwise_fused_bn_backward(k, s, hw, c):
     for i, r in enumerate(refs):
         assert rel(grads[True][i], r) < 3e-2, (i, rel(grads[True][i], r))
         assert rel(grads[True][i], grads[False][i]) < 3e-2, (i, rel(grads[True][i], grads[False][i]))
+
+
+@pytest.mark.parametrize("k,s,hw,c", [(3, 1, 14, 96), (5, 2, 15, 40), (3, 2, 16, 144), (5, 1, 7, 672)])
+def test_depthwise_forward_bn_statistics(k, s, hw, c):
+    """depthwise -> BN (train) -> SiLU with the BN's batch statistics produced by the depthwise forward
+    (ops/_hip/convbn.py DW_STATS, csrc/dwconv.hip EPI 2) against the BN's own statistics pass and fp32 torch:
+    output, running mean / var (about a non-zero pivot, with a large channel mean), and the backward."""
+    import torch.nn as nn
+    from pytorch_imageclassification_distributed_amd.ops import hip
+    from pytorch_imageclassification_distributed_amd.ops.functional import conv_padding
+    torch.manual_seed(k * 10 + c)
+    dw = nn.Conv2d(c, c, k, s, 0, groups=c, bias=False).to(DEV).to(memory_format=CL)
+    dw.tf_same = True
+    bn = nn.BatchNorm2d(c, eps=1e-3).to(DEV)
+    with torch.no_grad():
+        dw.weight.copy_(bf(dw.weight.abs() + 0.05))  # positive taps: channel means of ~10 std from the +3 input
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+        bn.running_mean.uniform_(-0.2, 0.2)  # the statistics pivot
+    x = bf(torch.randn(4, c, hw, hw, device=DEV) + 3.0)
+    g = bf(torch.randn(4, c, (hw + s - 1) // s, (hw + s - 1) // s, device=DEV))
+    res = {}
+    keep = hip.DW_STATS
+    keep_px = hip.C.dw_set_stats_min_px(0)  # fuse every geometry here (the trainer gates on pixels per block)
+    try:
+        for fused in (True, False):
+            hip.DW_STATS = fused
+            b = copy.deepcopy(bn)
+            xb = x.to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
+            before = hip.DW_STATS_COUNT[0]
+            out = hip.conv_bn_act(xb, dw, b, "silu", None)
+            assert (hip.DW_STATS_COUNT[0] > before) == fused
+            out.backward(g.to(torch.bfloat16).contiguous(memory_format=CL))
+            torch.cuda.synchronize()
+            res[fused] = (out.float(), b.running_mean.clone(), b.running_var.clone(), xb.grad.float(),
+                          [p_.grad.float().clone() for p_ in b.parameters()])
+            dw.weight.grad = None
+    finally:
+        hip.DW_STATS = keep
+        hip.C.dw_set_stats_min_px(keep_px)
+    br = copy.deepcopy(bn)
+    xr = x.clone().requires_grad_(True)
+    pt, pb, pl, pr = conv_padding(dw, hw, hw)
+    z = F.conv2d(F.pad(xr, (pl, pr, pt, pb)), dw.weight.detach(), None, s, 0, 1, c)
+    z = z + (bf(z) - z).detach()  # the stored output is bf16
+    ref = F.silu(br(z))
+    ref.backward(g)
+    for fused in (True, False):
+        o, rm, rv, gx, gp = res[fused]
+        assert rel(o, ref) < 2e-2, (fused, rel(o, ref))
+        assert torch.allclose(rm, br.running_mean, rtol=1e-3, atol=1e-3), fused
+        assert torch.allclose(rv, br.running_var, rtol=1e-2, atol=1e-3), fused
+        assert rel(gx, xr.grad) < 3e-2, (fused, rel(gx, xr.grad))
+        for a, r in zip(gp, br.parameters()):
+            assert rel(a, r.grad) < 3e-2, fused
+    assert rel(res[True][0], res[False][0]) < 1e-2

@@ -712,11 +712,24 @@ def test_depthwise_bn_silu():
     (2, 32, 35, 64, (3, 1, 1), (3, 2, 0)),    # Inception Conv2d_2b -> maxpool (odd size, no padding)
     (1, 16, 17, 48, (3, 1, 0), (3, 2, 1)),
 ])
-def test_conv_bn_act_pool(case):
+@pytest.mark.parametrize("stem_xa", [True, False])
+def test_conv_bn_act_pool(case, stem_xa):
     """Stem fusion: max_pool2d(relu(bn(conv(x)))) - forward, running stats and every gradient, against
-    the fp32 reference and (tightly) against the unfused HIP composition conv_bn_act -> max_pool2d."""
+    the fp32 reference and (tightly) against the unfused HIP composition conv_bn_act -> max_pool2d.  With
+    STEM_XA (ResNet stem) the pool backward masks by the pooled output and the stem conv's weight gradient
+    forms dY itself from the BN's dz and map (no bn_bwd_elemt pass)."""
     import copy
     hip = _hip()
+    keep_xa = hip.STEM_XA
+    hip.STEM_XA = stem_xa
+    try:
+        _conv_bn_act_pool_case(hip, case, stem_xa)
+    finally:
+        hip.STEM_XA = keep_xa
+
+
+def _conv_bn_act_pool_case(hip, case, stem_xa):
+    import copy
     n, cin, h, co, (k, s, p), pool = case
     torch.manual_seed(7)
     conv = nn.Conv2d(cin, co, k, s, p, bias=False).to(DEV).to(memory_format=CL)
@@ -737,6 +750,7 @@ def test_conv_bn_act_pool(case):
         return x if stem else x.to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
 
     xb, xu = inp(), inp()
+    n_xa = hip.STEM_XA_COUNT[0]
     out = hip.conv_bn_act_pool(xb, conv, bn, "relu", pool)
     unf = hip.max_pool2d(hip.conv_bn_act(xu, conv_u, bn_u, "relu", None), *pool)
     xr = x.clone().requires_grad_(not stem)
@@ -754,6 +768,7 @@ def test_conv_bn_act_pool(case):
     g = bf(torch.randn_like(ref))
     gb = g.to(torch.bfloat16).contiguous(memory_format=CL)
     out.backward(gb)
+    assert (hip.STEM_XA_COUNT[0] > n_xa) == (stem and stem_xa)
     unf.backward(gb)
     ref.backward(g)
     # the fused gather matches the unfused maxpool_bwd -> BN backward (which rounds the full-resolution
@@ -812,8 +827,9 @@ def test_div64_fallback_paths(which):
         elif which == "se":
             test_se_gate_and_misc()
         elif which == "stem_pool":
-            test_conv_bn_act_pool((2, 3, 64, 64, (7, 2, 3), (3, 2, 1)))
-            test_conv_bn_act_pool((2, 32, 35, 64, (3, 1, 1), (3, 2, 0)))
+            # (the ReLU-masked pool backward of STEM_XA is a quad-kernel form, which the forced decode turns off)
+            test_conv_bn_act_pool((2, 3, 64, 64, (7, 2, 3), (3, 2, 1)), False)
+            test_conv_bn_act_pool((2, 32, 35, 64, (3, 1, 1), (3, 2, 0)), False)
         else:
             test_gap_head_ce()
     finally:
