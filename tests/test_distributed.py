@@ -395,6 +395,27 @@ def test_bench_eight_rank_rehearsal():
     assert "rehearsing with --data device" in err
 
 
+def test_scale_sweep_script_rehearsal(tmp_path):
+    """scripts/scale_sweep.sh (the 8-GPU node's sweep: N x SyncBN x bucket MiB x transport dtype x gradient
+    backend) runs end to end as a CPU rehearsal: 2 gloo ranks, one bucket size, both transport dtypes; one
+    JSON line per run, tagged with its sweep point."""
+    import json
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "sweep.jsonl"
+    env = dict(os.environ, NS="2", SYNCBN="on", BUCKETS="8", COMMS="fp32 bf16", BACKENDS="pg", REF="0",
+               BACKEND="gloo", BATCH="2", STEPS="1", WARMUP="1", MODEL="resnet18", IMAGE_SIZE="32",
+               EXTRA="--device cpu", OUT=str(out), TIMEOUT="600", GRAFT_REPO_ROOT=root)
+    r = subprocess.run(["bash", os.path.join(root, "scripts", "scale_sweep.sh")], env=env, capture_output=True,
+                       text=True, timeout=900)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+    rows = [json.loads(line) for line in out.read_text().splitlines()]
+    assert [row["tag"] for row in rows] == ["resnet18_n2_sbon_b8_fp32_pg", "resnet18_n2_sbon_b8_bf16_pg"]
+    for row in rows:
+        run = row["run"]
+        assert run["n_gpus"] == 2 and run["config"]["sync_bn"] is True and run["value"] > 0
+
+
 def test_bench_refuses_a_world_size_mismatch():
     """A single rank asked for ``--gpus 2`` under a launcher-provided WORLD_SIZE=1 exits non-zero without a
     (mislabelled) JSON line."""
