@@ -4,6 +4,7 @@
 // pointers to the launchers in the .hip files.  No allocation happens here:
 // outputs are allocated by the Python op layer through the caching allocator.
 #include <torch/extension.h>
+#include <hip/hip_runtime_api.h>
 #include <c10/hip/HIPCachingAllocator.h>
 #include <c10/hip/HIPStream.h>
 
@@ -55,8 +56,10 @@ int stem_s2d_conv_launch(const bf16_t*, const bf16_t*, bf16_t*, float*, int, int
 int maxpool_fwd_launch(const bf16_t*, bf16_t*, uint8_t*, int, int, int, int, int, int, int, int, int, int, int,
                        int, hipStream_t);
 int maxpool_bwd_launch(const bf16_t*, const uint8_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int,
-                       int, int, hipStream_t, const bf16_t* y_out = nullptr);
+                       int, int, hipStream_t, const bf16_t* y_out, const bf16_t* bn_y, const float* bn_coef, float* part,
+                       int G);
 bool maxpool_bwd_relu_ok(int N, int H, int W, int C, int kh, int kw, int sh, int sw, int ph, int pw);
+bool maxpool_bwd_reduce_ok(int N, int H, int W, int C, int kh, int kw, int sh, int sw, int ph, int pw);
 int avgpool_fwd_launch(const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int, int, int,
                        hipStream_t);
 int avgpool_bwd_launch(const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int, int, int,
@@ -594,14 +597,24 @@ void maxpool_fwd(Tensor x, Tensor y, OT idx, int N, int H, int W, int C, int OH,
         "maxpool_fwd");
 }
 
-// relu_out (optional): the pooled output of maxpool(relu(.)); dx then receives the ReLU-masked gradient
+// relu_out (optional): the pooled output of maxpool(relu(.)); dx then receives the ReLU-masked gradient.
+// bn_y / bn_coef / part / G (optional, with relu_out): also that BN's backward partial rows (sum dz, sum dz*xhat)
 void maxpool_bwd(Tensor dy, Tensor idx, Tensor dx, int N, int H, int W, int C, int OH, int OW, int kh, int kw,
-                 int sh, int sw, int ph, int pw, OT relu_out) {
+                 int sh, int sw, int ph, int pw, OT relu_out, OT bn_y, OT bn_coef, OT part, int G) {
   const bf16_t* yo = optr<bf16_t>(relu_out);
   TORCH_CHECK(!yo || (relu_out->numel() == dy.numel() && relu_out->scalar_type() == BF),
               "maxpool_bwd: relu_out must be the pooled output (like dy)");
+  TORCH_CHECK(dx.numel() == (long)N * H * W * C && dy.numel() == (long)N * OH * OW * C, "maxpool_bwd: sizes");
+  float* pt = optr<float>(part);
+  if (pt) {
+    TORCH_CHECK(bn_y.has_value() && bn_y->numel() == dx.numel() && bn_y->scalar_type() == BF,
+                "maxpool_bwd: bn_y must be the BN input (like dx)");
+    TORCH_CHECK(bn_coef.has_value() && bn_coef->numel() >= 4L * C && G >= 1 && part->numel() >= 2L * C * G,
+                "maxpool_bwd: bn_coef [4][C] and part [G][2][C]");
+  }
   check(maxpool_bwd_launch(ptr<bf16_t>(dy), ptr<uint8_t>(idx), ptr<bf16_t>(dx), N, H, W, C, OH, OW, kh, kw, sh, sw,
-                           ph, pw, cur(), yo),
+                           ph, pw, cur(), yo, pt ? optr<bf16_t>(bn_y) : nullptr, pt ? optr<float>(bn_coef) : nullptr,
+                           pt, G),
         "maxpool_bwd");
 }
 
@@ -1111,8 +1124,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("maxpool_bwd", &maxpool_bwd, pybind11::arg("dy"), pybind11::arg("idx"), pybind11::arg("dx"), pybind11::arg("N"),
         pybind11::arg("H"), pybind11::arg("W"), pybind11::arg("C"), pybind11::arg("OH"), pybind11::arg("OW"),
         pybind11::arg("kh"), pybind11::arg("kw"), pybind11::arg("sh"), pybind11::arg("sw"), pybind11::arg("ph"),
-        pybind11::arg("pw"), pybind11::arg("relu_out") = pybind11::none());
+        pybind11::arg("pw"), pybind11::arg("relu_out") = pybind11::none(), pybind11::arg("bn_y") = pybind11::none(),
+        pybind11::arg("bn_coef") = pybind11::none(), pybind11::arg("part") = pybind11::none(), pybind11::arg("G") = 0);
   m.def("maxpool_bwd_relu_ok", &maxpool_bwd_relu_ok);
+  m.def("maxpool_bwd_reduce_ok", &maxpool_bwd_reduce_ok);
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("gap_fwd", &gap_fwd);
@@ -1137,6 +1152,17 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_act_maxpool", &bn_act_maxpool);
   m.def("bn_set_unroll", [](bool v) { bn_set_unroll(v ? 1 : 0); });
   m.def("bn_res_coef_ok", &bn_res_coef_ok);
+  // a stream whose kernels may only occupy the CUs set in ``mask`` (32 per word; ops/_hip/streams.py
+  // IMGCLS_WGRAD_CU_FRAC: the weight-gradient side stream on a subset, the compute stream keeps the rest)
+  m.def("cu_mask_stream", [](int device, std::vector<uint32_t> mask) -> uintptr_t {
+    int prev = 0;
+    TORCH_CHECK(hipGetDevice(&prev) == hipSuccess && hipSetDevice(device) == hipSuccess, "cu_mask_stream: device");
+    hipStream_t s = nullptr;
+    hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data());
+    (void)hipSetDevice(prev);
+    TORCH_CHECK(e == hipSuccess, "hipExtStreamCreateWithCUMask: ", hipGetErrorString(e));
+    return (uintptr_t)s;
+  });
   m.def("conv_bounds_checked", &conv_bounds_checked);
   m.def("bounds_violations", &bounds_violations);  // and clears the record
   // csrc/extents.h on the CPU (tests/test_extents.py): the checks every conv launch passes, from integers only.

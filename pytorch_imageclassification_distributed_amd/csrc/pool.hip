@@ -152,11 +152,34 @@ struct QuadDiv {
 // RELU (a stem: maxpool(relu(bn(y)))): dx is the BN's dz = relu'(z) * dx - the max candidate's pooled value
 // relu(z) is positive exactly where z is, so the pooled output y_out itself gives the mask (read at the same
 // offsets as dy); the BN backward then runs with the identity activation and never recomputes it
-template <bool RELU>
-__global__ void maxpool_bwd_quad_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx,
-                                        bf16_t* __restrict__ dx, PoolGeom g, QuadDiv fd, int MH, int MW,
-                                        uint32_t total, const bf16_t* __restrict__ y_out) {
+// RED (with RELU): also the BN-backward reduce of that dz - per channel sum dz and sum dz * (y - mean) * invstd,
+// y the BN input at the same pixels, into the rotating partial rows part[(block % G)][2][C] that bn_reduce_bwd
+// finalizes (bn_bwd_reduce_u_kernel's layout and sums; the separate pass re-read all of dz).  Needs 256 % (C / 8)
+// == 0: a lane's channel chunk is then fixed across its grid-stride iterations.
+struct QuadRed {
+  const bf16_t* y;
+  const float* coef;
+  float* part;
+  int G;
+};
+
+template <bool RELU, bool RED>
+__global__ __launch_bounds__(256) void maxpool_bwd_quad_kernel(const bf16_t* __restrict__ dy,
+                                                               const uint8_t* __restrict__ idx,
+                                                               bf16_t* __restrict__ dx, PoolGeom g, QuadDiv fd, int MH,
+                                                               int MW, uint32_t total, const bf16_t* __restrict__ y_out,
+                                                               QuadRed rd) {
   const int cch = g.C >> 3;
+  float rs[8], rq[8], mu[8], is[8];
+  if constexpr (RED) {
+    const int cr = (int)((blockIdx.x * blockDim.x + threadIdx.x) % (uint32_t)cch) * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      rs[k] = rq[k] = 0.f;
+      mu[k] = rd.coef[2 * g.C + cr + k];
+      is[k] = rd.coef[3 * g.C + cr + k];
+    }
+  }
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     const uint32_t q = fdiv(i, fd.cch);
     const int c0 = (int)(i - q * cch) * 8;
@@ -214,7 +237,38 @@ __global__ void maxpool_bwd_quad_kernel(const bf16_t* __restrict__ dy, const uin
             }
           }
         }
-        *(uint4*)(dx + (((long)n * g.H + h) * g.W + w) * g.C + c0) = pack8(acc);
+        const long off = (((long)n * g.H + h) * g.W + w) * g.C + c0;
+        *(uint4*)(dx + off) = pack8(acc);
+        if constexpr (RED) {
+          float yv[8], dz[8];
+          unpack8(*(const uint4*)(rd.y + off), yv);
+          unpack8(pack8(acc), dz);  // the bf16 dz the separate reduce pass would have read back
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            rs[k] += dz[k];
+            rq[k] += dz[k] * (yv[k] - mu[k]) * is[k];
+          }
+        }
+      }
+    }
+  }
+  if constexpr (RED) {
+    __shared__ float red[2][256][9];
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { red[0][tid][k] = rs[k]; red[1][tid][k] = rq[k]; }
+    __syncthreads();
+    if (tid < cch) {  // lanes tid, tid + cch, ... hold the same channel chunk
+      for (int r = tid + cch; r < 256; r += cch) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { rs[k] += red[0][r][k]; rq[k] += red[1][r][k]; }
+      }
+      const int cr = (int)((blockIdx.x * blockDim.x + tid) % (uint32_t)cch) * 8;
+      float* dst = rd.part + (size_t)(blockIdx.x % rd.G) * 2 * g.C + cr;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        atomicAdd(dst + k, rs[k]);
+        atomicAdd(dst + g.C + k, rq[k]);
       }
     }
   }
@@ -313,24 +367,37 @@ static bool quad_ok(long qtotal, int C, int kh, int kw, int sh, int sw, int ph, 
          !g_imgcls_div64;
 }
 
+static bool quad_red_ok(long qtotal, int C, int kh, int kw, int sh, int sw, int ph, int pw) {
+  return quad_ok(qtotal, C, kh, kw, sh, sw, ph, pw) && C % 8 == 0 && 256 % (C / 8) == 0;
+}
+
 // y_out (optional): the pooled output of maxpool(relu(.)) - dx receives the ReLU-masked gradient (quad kernel
-// geometries only: 2 = not handled, the caller keeps the activation in the BN backward)
+// geometries only: 2 = not handled, the caller keeps the activation in the BN backward).  bn_y / bn_coef / part
+// (optional, with y_out): also that BN's backward partial sums (3 = not handled on this geometry)
 int maxpool_bwd_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W, int C, int OH,
-                       int OW, int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t s, const bf16_t* y_out) {
+                       int OW, int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t s, const bf16_t* y_out,
+                       const bf16_t* bn_y, const float* bn_coef, float* part, int G) {
   PoolGeom g{N, H, W, C, OH, OW, kh, kw, sh, sw, ph, pw};
   const long total = (long)N * H * W * (C / 8);
   const int MH = (H + ph + 1) / 2, MW = (W + pw + 1) / 2;
   const long qtotal = (long)N * MH * MW * (C / 8);
   if (total <= 0) return 0;
   if (y_out != nullptr && !quad_ok(qtotal, C, kh, kw, sh, sw, ph, pw)) return 2;
+  if (part != nullptr && (y_out == nullptr || bn_y == nullptr || bn_coef == nullptr || G < 1 ||
+                          !quad_red_ok(qtotal, C, kh, kw, sh, sw, ph, pw)))
+    return 3;
   if (quad_ok(qtotal, C, kh, kw, sh, sw, ph, pw)) {
     const QuadDiv fd{make_fastdiv(C / 8), make_fastdiv(MW), make_fastdiv(MH)};
-    if (y_out != nullptr)
-      hipLaunchKernelGGL(maxpool_bwd_quad_kernel<true>, dim3(grid_for(qtotal)), dim3(256), 0, s, dy, idx, dx, g, fd,
-                         MH, MW, (uint32_t)qtotal, y_out);
+    const QuadRed rd{bn_y, bn_coef, part, G};
+    if (part != nullptr)
+      hipLaunchKernelGGL((maxpool_bwd_quad_kernel<true, true>), dim3(grid_for(qtotal)), dim3(256), 0, s, dy, idx, dx,
+                         g, fd, MH, MW, (uint32_t)qtotal, y_out, rd);
+    else if (y_out != nullptr)
+      hipLaunchKernelGGL((maxpool_bwd_quad_kernel<true, false>), dim3(grid_for(qtotal)), dim3(256), 0, s, dy, idx, dx,
+                         g, fd, MH, MW, (uint32_t)qtotal, y_out, rd);
     else
-      hipLaunchKernelGGL(maxpool_bwd_quad_kernel<false>, dim3(grid_for(qtotal)), dim3(256), 0, s, dy, idx, dx, g, fd,
-                         MH, MW, (uint32_t)qtotal, nullptr);
+      hipLaunchKernelGGL((maxpool_bwd_quad_kernel<false, false>), dim3(grid_for(qtotal)), dim3(256), 0, s, dy, idx,
+                         dx, g, fd, MH, MW, (uint32_t)qtotal, nullptr, rd);
   } else if ((kh - 1) / sh <= 1 && (kw - 1) / sw <= 1 && total < (1L << 31) && !g_imgcls_div64) {
     const PoolDiv fd{make_fastdiv(C / 8), make_fastdiv(W), make_fastdiv(H), make_fastdiv(sh), make_fastdiv(sw)};
     hipLaunchKernelGGL(maxpool_bwd2x2_kernel, dim3(grid_for(total)), dim3(256), 0, s, dy, idx, dx, g, fd,
@@ -345,6 +412,11 @@ int maxpool_bwd_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, 
 bool maxpool_bwd_relu_ok(int N, int H, int W, int C, int kh, int kw, int sh, int sw, int ph, int pw) {
   const long qtotal = (long)N * ((H + ph + 1) / 2) * ((W + pw + 1) / 2) * (C / 8);
   return quad_ok(qtotal, C, kh, kw, sh, sw, ph, pw);
+}
+
+bool maxpool_bwd_reduce_ok(int N, int H, int W, int C, int kh, int kw, int sh, int sw, int ph, int pw) {
+  const long qtotal = (long)N * ((H + ph + 1) / 2) * ((W + pw + 1) / 2) * (C / 8);
+  return quad_red_ok(qtotal, C, kh, kw, sh, sw, ph, pw);
 }
 
 int avgpool_fwd_launch(const bf16_t* x, bf16_t* y, int N, int H, int W, int C, int OH, int OW, int kh, int kw,

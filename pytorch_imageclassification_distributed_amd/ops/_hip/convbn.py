@@ -783,12 +783,18 @@ class BNActPoolFn(torch.autograd.Function):
         _, _, oh, ow, kh, kw, sh, sw, ph, pw = ctx.geo
         xa = ctx.xa
         g = _empty_cl(n, c, h, w, dev)
-        C.maxpool_bwd(_cl(gout), idx, g, n, h, w, c, oh, ow, kh, kw, sh, sw, ph, pw,
-                      relu_out=out if xa is not None else None)
-        act = 0 if xa is not None else ctx.act  # (g is already dz: masked by the pooled output)
         grp = stat_groups(rows)
         part = ws(dev).stats_buf(c, grp)
-        C.bn_bwd_reduce(g, y, coef, None, None, rows, c, act, part, grp)
+        # POOL_BN_REDUCE: the pool backward also takes the BN-backward partial sums of the dz it writes
+        red = xa is not None and POOL_BN_REDUCE and C.maxpool_bwd_reduce_ok(n, h, w, c, kh, kw, sh, sw, ph, pw)
+        C.maxpool_bwd(_cl(gout), idx, g, n, h, w, c, oh, ow, kh, kw, sh, sw, ph, pw,
+                      relu_out=out if xa is not None else None,
+                      **(dict(bn_y=y, bn_coef=coef, part=part, G=grp) if red else {}))
+        act = 0 if xa is not None else ctx.act  # (g is already dz: masked by the pooled output)
+        if red:
+            POOL_BN_REDUCE_COUNT[0] += 1
+        else:
+            C.bn_bwd_reduce(g, y, coef, None, None, rows, c, act, part, grp)
         xac = torch.empty(3 * c, dtype=torch.float32, device=dev) if xa is not None else None
         k, dgamma, dbeta = _bn_bwd_k(part, grp, c, rows, ctx.training, ctx.group, ctx.count_t, ctx.params, dev,
                                      coef=coef, xa=xac)
@@ -807,6 +813,10 @@ STEM_POOL_FUSE = os.environ.get("IMGCLS_STEM_POOL_FUSE", "1") == "1"
 # disappear from the tail of every step (IMGCLS_STEM_XA=0: keep them)
 STEM_XA = os.environ.get("IMGCLS_STEM_XA", "1") == "1"
 STEM_XA_COUNT = [0]
+# with STEM_XA the stem's max-pool backward also accumulates the BN-backward partial sums of the dz it writes (one
+# read of y there instead of a separate reduce pass re-reading dz and y; IMGCLS_POOL_BN_REDUCE=0: the separate pass)
+POOL_BN_REDUCE = os.environ.get("IMGCLS_POOL_BN_REDUCE", "1") == "1"
+POOL_BN_REDUCE_COUNT = [0]
 
 
 def conv_bn_act_pool(x, conv, bn, act, pool, exclusive_input=False):
@@ -1034,7 +1044,7 @@ _OWNED = (
     'DenseConvFn', 'DwConvFn', 'dw_stats_eligible',
     'FUSE_XA', 'FUSE_XF', 'GradSlot', 'PEER_BN_MAX_C', 'POOL_CONV_SWAP', 'RELU_MASK', 'RES_DEFER', 'RES_DEFER_COUNT',
     'STEM_DIRECT',
-    'STEM_POOL_FUSE', 'STEM_S2D', 'STEM_XA', 'STEM_XA_COUNT', 'SYNCBN_EARLY_COUNT', 'StemS2dFn', 'XA_COUNT', 'XA_MAX_REP', 'XA_NARROW_OFF',
+    'POOL_BN_REDUCE', 'POOL_BN_REDUCE_COUNT', 'STEM_POOL_FUSE', 'STEM_S2D', 'STEM_XA', 'STEM_XA_COUNT', 'SYNCBN_EARLY_COUNT', 'StemS2dFn', 'XA_COUNT', 'XA_MAX_REP', 'XA_NARROW_OFF',
     'XF_COUNT', 'XF_MAX_REP', 'XA_OUT', 'XA_OUT_COUNT', '_xa_out_ok', 'XaLink', 'XfHold', 'XfMaterializeFn', '_S2D_INDEX', '_as_pixel_rows',
     '_bn_bwd_k', '_bn_coef', '_dense_geom', '_rep', '_s2d_geom', '_s2d_index', '_syncbn_bwd_start', 'conv',
     'conv_bn_act', 'conv_bn_act_pool', 'dense_conv_eligible', 'input_from_u8', 'materialize_deferred',

@@ -32,13 +32,33 @@ WGRAD_STREAM = os.environ.get("IMGCLS_WGRAD_STREAM", "1") == "1"
 # (Inception-v3 b128: 3303 vs 6523 img/s, profiles/history/r3g_hip_graph_modes.txt); IMGCLS_GRAPH_SIDE=1 forks
 GRAPH_SIDE = os.environ.get("IMGCLS_GRAPH_SIDE", "0") == "1"
 _SIDE: dict = {}  # device index -> _SideStream
+# < 1: the side stream's kernels may occupy only this fraction of the CUs (a CU-masked HIP stream, k of every 8
+# CUs of each XCD whichever way the driver numbers them), so a long weight-gradient wave cannot hold CUs the
+# compute stream's next launch needs; 1 (default): all CUs, the compute stream wins only by queue priority
+WGRAD_CU_FRAC = float(os.environ.get("IMGCLS_WGRAD_CU_FRAC", "1"))
+
+
+def cu_mask_words(n_cu: int, frac: float) -> list:
+    """32-bit CU mask words enabling round(8 * frac) of every 8 CUs: CU i is on when (i // 8 + i) % 8 < k, which
+    keeps k of 8 per XCD for XCD-major (i // 32) and XCD-interleaved (i % 8) numbering alike."""
+    k = max(1, min(8, round(8 * frac)))
+    words = [0] * (-(-n_cu // 32))
+    for i in range(n_cu):
+        if (i // 8 + i) % 8 < k:
+            words[i // 32] |= 1 << (i % 32)
+    return words
 
 
 class _SideStream:
     __slots__ = ("stream", "joins", "handle", "ws")
 
     def __init__(self, dev):
-        self.stream = torch.cuda.Stream(device=dev)
+        if WGRAD_CU_FRAC < 1:
+            n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+            ptr = C.cu_mask_stream(dev.index, cu_mask_words(n_cu, WGRAD_CU_FRAC))
+            self.stream = torch.cuda.ExternalStream(ptr, device=dev)
+        else:
+            self.stream = torch.cuda.Stream(device=dev)
         self.joins = set()  # compute streams that must wait for this stream when backward ends
         self.handle = self.stream.cuda_stream  # raw hipStream_t for launchers that fork to it themselves
         self.ws = None  # split-K workspace of the wgrad launches on this stream
@@ -144,6 +164,6 @@ def conv_wgrad_raw(dy, x, w_param, g: ConvGeom, xa=None, xf=None):
 
 # names this part owns (ops/hip.py re-exports them)
 _OWNED = (
-    'GRAPH_SIDE', 'STEM_WGRAD_SIDE', 'WGRAD_STREAM', '_SIDE', '_SideStream', '_on_side', 'comm_stream',
-    'conv_wgrad_raw', 'join_side_streams', 'side_stream',
+    'GRAPH_SIDE', 'STEM_WGRAD_SIDE', 'WGRAD_CU_FRAC', 'WGRAD_STREAM', '_SIDE', '_SideStream', '_on_side',
+    'comm_stream', 'conv_wgrad_raw', 'cu_mask_words', 'join_side_streams', 'side_stream',
 )

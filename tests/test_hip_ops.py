@@ -750,7 +750,7 @@ def _conv_bn_act_pool_case(hip, case, stem_xa):
         return x if stem else x.to(torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
 
     xb, xu = inp(), inp()
-    n_xa = hip.STEM_XA_COUNT[0]
+    n_xa, n_red = hip.STEM_XA_COUNT[0], hip.POOL_BN_REDUCE_COUNT[0]
     out = hip.conv_bn_act_pool(xb, conv, bn, "relu", pool)
     unf = hip.max_pool2d(hip.conv_bn_act(xu, conv_u, bn_u, "relu", None), *pool)
     xr = x.clone().requires_grad_(not stem)
@@ -769,6 +769,8 @@ def _conv_bn_act_pool_case(hip, case, stem_xa):
     gb = g.to(torch.bfloat16).contiguous(memory_format=CL)
     out.backward(gb)
     assert (hip.STEM_XA_COUNT[0] > n_xa) == (stem and stem_xa)
+    # (the pool backward also took the BN-backward partial sums: no separate reduce pass)
+    assert (hip.POOL_BN_REDUCE_COUNT[0] > n_red) == (stem and stem_xa and hip.POOL_BN_REDUCE)
     unf.backward(gb)
     ref.backward(g)
     # the fused gather matches the unfused maxpool_bwd -> BN backward (which rounds the full-resolution
