@@ -647,6 +647,12 @@ WGRAD_STAGES = int(os.environ.get("IMGCLS_WGRAD_STAGES", "0"))  # 0 = tuned with
 
 
 WGRAD_WS = os.environ.get("IMGCLS_WGRAD_WS", "1") == "1"  # split-K partials: workspace slabs + reduce (0: atomics)
+# ... except for layers of at most this many output pixels (N * OH * OW): there the split-K partials go straight into
+# the zeroed gradient slot by fp32 atomics, which saves the reduce launch - the whole cost of a tiny layer's split
+# (Inception-v3 b4 graph replay: ~75 wgrad_reduce launches of ~5 us in an 8.4 ms step).  Same box: Inception-v3 b4
+# +3.7 % at this threshold; b32, b128 and ResNet-50 b64 unchanged; all-atomic weight gradients lose 3.5 % at b128 and
+# an 8192-pixel threshold 2.2 % (its 8 x 8 layers), profiles/r15o_*, r15p_*
+WGRAD_ATOMIC_PIX = int(os.environ.get("IMGCLS_WGRAD_ATOMIC_PIX", "6144"))
 _WGRAD_WS: dict = {}  # (device index, stream id) -> fp32 workspace, grown on demand
 
 
@@ -673,7 +679,7 @@ def _wgrad_launch(dy, x, out, g: ConvGeom, m, ntot, kps, splits, stages=2, side=
     if SKIP_WGRAD:
         return
     wsp = None
-    if WGRAD_WS and splits > 1 and ntot % 8 == 0:
+    if WGRAD_WS and splits > 1 and ntot % 8 == 0 and m > WGRAD_ATOMIC_PIX:
         n = splits * g.Co * ntot
         if side is None:
             wsp = _wgrad_ws(dy.device, n)
@@ -774,7 +780,7 @@ _OWNED = (
     'DEEP_FORCE', 'DIRECT_BASE', 'PW_BASE', 'PW_CONV', 'PW_COUNT', 'PW_FORCE', '_PW_CFGS', 'DIRECT_CFGS', 'DIRECT_CONV', 'DIRECT_DGRAD', 'DIRECT_FORCE', 'FUSED_XA_BWD',
     'FUSED_XA_BWD_COUNT', 'FUSED_XA_BWD_N', 'HALO_BASE', 'HALO_CONV', 'HALO_COUNT', 'HALO_FORCE', 'HALO_TUNE',
     'SKIP_WGRAD', 'TUNE_LOG', 'WGRAD_CANDIDATES', 'WGRAD_DEEP', 'WGRAD_MIN_K', 'WGRAD_NARROW_TILES', 'WGRAD_STAGES',
-    'WGRAD_TARGET_BLOCKS', 'WGRAD_TUNE_LOG', 'WGRAD_WS', '_CFGS', '_CU_COUNT', '_DEEP_CFGS', '_FP8_CFGS',
+    'WGRAD_ATOMIC_PIX', 'WGRAD_TARGET_BLOCKS', 'WGRAD_TUNE_LOG', 'WGRAD_WS', '_CFGS', '_CU_COUNT', '_DEEP_CFGS', '_FP8_CFGS',
     '_HALO_CFGS', '_ORDER_IDX', '_STAGES_TUNED', '_WGRAD_TUNED', '_WGRAD_WS', '_conv_candidates',
     '_conv_forward_fp8', '_conv_gemm', '_deep_ok', '_dgrad_phases', '_direct_geom', '_direct_launch', '_direct_variant_ok', '_pw_ok', 'conv_pw_cfgs',
     '_fwd_taps', '_halo_ok', '_time_ms', '_tune_conv', '_weight_for_input', '_wgrad_config', '_wgrad_has',
