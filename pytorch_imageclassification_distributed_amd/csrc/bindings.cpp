@@ -35,6 +35,8 @@ int rccl_comm_close(int64_t, bool);
 
 // ---- launcher prototypes (defined in *.hip) ----
 int bn_partials_launch(float*, int, int, double*, float*, float*, double, hipStream_t);
+int bn_fin_apply_launch(const bf16_t*, bf16_t*, float*, int, int, long, double, const float*, const float*, float*, float*,
+                        long long*, float, float, float*, const float*, int, int, int, unsigned*, hipStream_t);
 int bn_reduce_finalize_launch(float*, int, int, double, const float*, const float*, float*, float*, long long*, float,
                               float, float*, const float*, hipStream_t);
 int bn_reduce_bwd_launch(float*, int, int, double, float*, float*, float*, const float*, float*, hipStream_t);
@@ -430,6 +432,26 @@ void bn_reduce_finalize(Tensor part, int G, int C, double count, OT gamma, OT be
                                   optr<float>(rmean), optr<float>(rvar), optr<long long>(nbt), (float)momentum,
                                   (float)eps, ptr<float>(coef), optr<float>(shift), cur()),
         "bn_reduce_finalize");
+}
+
+// training BN forward of a small tensor in one launch: partial-row reduce + finalize (coef, running statistics,
+// re-zeroed rows) + apply into out[:, c_off : c_off + C] (row stride ldo); ctr: >= ceil(C / 64) zeroed int32
+void bn_fin_apply(Tensor y, Tensor part, int G, double count, OT gamma, OT beta, OT rmean, OT rvar, OT nbt,
+                  double momentum, double eps, Tensor coef, OT shift, Tensor out, long rows, int C, int ldo, int c_off,
+                  int act, Tensor ctr) {
+  req(part, F32, "part"); req(coef, F32, "coef");
+  TORCH_CHECK(y.scalar_type() == BF && out.scalar_type() == BF && ctr.scalar_type() == torch::kInt32,
+              "bn_fin_apply: dtypes");
+  TORCH_CHECK(part.numel() >= (int64_t)G * 2 * C && coef.numel() >= 4 * C && y.numel() == rows * C &&
+                  out.numel() >= rows * ldo && ldo >= c_off + C && ctr.numel() >= (C + 63) / 64,
+              "bn_fin_apply: buffer sizes");
+  for (const OT* t : {&gamma, &beta, &rmean, &rvar, &shift})
+    TORCH_CHECK(!t->has_value() || !(*t)->defined() || (*t)->numel() >= C, "bn_fin_apply: per-channel sizes");
+  check(bn_fin_apply_launch(ptr<bf16_t>(y), ptr<bf16_t>(out), ptr<float>(part), G, C, rows, count, optr<float>(gamma),
+                            optr<float>(beta), optr<float>(rmean), optr<float>(rvar), optr<long long>(nbt),
+                            (float)momentum, (float)eps, ptr<float>(coef), optr<float>(shift), ldo, c_off, act,
+                            reinterpret_cast<unsigned*>(ctr.data_ptr()), cur()),
+        "bn_fin_apply");
 }
 
 void bn_reduce_bwd(Tensor part, int G, int C, double count, OT dgamma, OT dbeta, Tensor k, OT coef, OT xa) {
@@ -1152,6 +1174,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_act_maxpool", &bn_act_maxpool);
   m.def("bn_set_unroll", [](bool v) { bn_set_unroll(v ? 1 : 0); });
   m.def("bn_res_coef_ok", &bn_res_coef_ok);
+  m.def("bn_fin_apply", &bn_fin_apply);
   // a stream whose kernels may only occupy the CUs set in ``mask`` (32 per word; ops/_hip/streams.py
   // IMGCLS_WGRAD_CU_FRAC: the weight-gradient side stream on a subset, the compute stream keeps the rest)
   m.def("cu_mask_stream", [](int device, std::vector<uint32_t> mask) -> uintptr_t {

@@ -152,6 +152,109 @@ __global__ __launch_bounds__(256) void bn_reduce_bwd_kernel(float* part, int G, 
   if (xa) bn_xa_coef_one(coef, C, c, s / count, q / count, xa);
 }
 
+// ---- small-tensor training forward: finalize folded into the apply (IMGCLS_BN_FIN) ----------------------------
+// Below a few MB per tensor a BN's bn_reduce_finalize launch costs as much as its apply (~5 us each: 96 of them in
+// the 8.4 ms Inception-v3 b4 graph replay).  Here grid.y walks 64-channel chunks and grid.x row blocks; every
+// block reduces its chunk's G partial rows (32 KB at G = 64, from L2), forms scale / shift and applies them to its
+// rows.  The partial rows and the pivot (`shift` is the running mean the producer summed about) are still being
+// read by the chunk's other blocks, so the running-stat update and the re-zeroing of the rows fall to the chunk's
+// LAST block: each block counts itself in `ctr[chunk]` after its reads; the block that completes the count updates
+// the chunk's running statistics, zeroes its partial columns and resets the counter for the next launch.  No
+// block ever waits for another.
+struct BnFinApplyArgs {
+  const bf16_t* y; bf16_t* out; float* part; int G, C; long rows; double count;
+  const float* gamma; const float* beta; float* rmean; float* rvar; long long* nbt;
+  float momentum, eps; float* coef; const float* shift;
+  int ldo, c_off;
+  unsigned* ctr;
+};
+
+template <int ACT>
+__global__ __launch_bounds__(256) void bn_fin_apply_kernel(BnFinApplyArgs a) {
+  __shared__ double red[2][4][64];
+  __shared__ float scs[64], shs[64];
+  __shared__ double mus[64], vars[64];
+  __shared__ unsigned last;
+  const int lc = threadIdx.x & 63, lg = threadIdx.x >> 6;
+  const int C = a.C;
+  const int c = blockIdx.y * 64 + lc;
+  double s = 0.0, q = 0.0;
+  if (c < C) {
+#pragma unroll 4
+    for (int g = lg; g < a.G; g += 4) {
+      const float* r = a.part + (size_t)g * 2 * C;
+      s += (double)r[c];
+      q += (double)r[C + c];
+    }
+  }
+  red[0][lg][lc] = s;
+  red[1][lg][lc] = q;
+  __syncthreads();
+  if (lg == 0) {
+    float sc = 0.f, sh = 0.f;
+    double mean = 0.0, var = 0.0;
+    if (c < C) {
+      s = red[0][0][lc] + red[0][1][lc] + red[0][2][lc] + red[0][3][lc];
+      q = red[1][0][lc] + red[1][1][lc] + red[1][2][lc] + red[1][3][lc];
+      shifted_moments(s, q, a.count, a.shift ? (double)a.shift[c] : 0.0, mean, var);
+      const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
+      const float g = a.gamma ? a.gamma[c] : 1.f, b = a.beta ? a.beta[c] : 0.f;
+      sc = g * invstd;
+      sh = b - (float)mean * sc;
+      if (blockIdx.x == 0) {
+        a.coef[c] = sc;
+        a.coef[C + c] = sh;
+        a.coef[2 * C + c] = (float)mean;
+        a.coef[3 * C + c] = invstd;
+      }
+    }
+    scs[lc] = sc;
+    shs[lc] = sh;
+    mus[lc] = mean;
+    vars[lc] = var;
+  }
+  // every read of this block (partials, pivot) has returned: its values were consumed above.  No fence: a
+  // device-scope release here is an L2 writeback on this chip (it cost 3-7 % of the step), and nothing this block
+  // wrote needs to be seen by the chunk's last block - the rows it zeroes are visible to the next kernel anyway
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(a.ctr + blockIdx.y, 1u) == gridDim.x - 1 ? 1u : 0u;
+  __syncthreads();
+  if (last) {  // the chunk's other blocks have all read the rows and the pivot
+    if (lg == 0 && c < C && a.rmean) {
+      const double n = a.count, var = vars[lc];
+      const double unb = n > 1.0 ? var * n / (n - 1.0) : var;
+      a.rmean[c] = (1.f - a.momentum) * a.rmean[c] + a.momentum * (float)mus[lc];
+      a.rvar[c] = (1.f - a.momentum) * a.rvar[c] + a.momentum * (float)unb;
+    }
+    if (blockIdx.y == 0 && threadIdx.x == 0 && a.nbt) *a.nbt += 1;
+    if (c < C) {
+      for (int g = lg; g < a.G; g += 4) {
+        float* r = a.part + (size_t)g * 2 * C;
+        r[c] = 0.f;
+        r[C + c] = 0.f;
+      }
+    }
+    if (threadIdx.x == 0) a.ctr[blockIdx.y] = 0u;
+  }
+  // apply: a lane owns 8 channels of the chunk, the block 32 rows per step
+  const int v = threadIdx.x & 7, rl = threadIdx.x >> 3;
+  const int c0 = blockIdx.y * 64 + v * 8;
+  if (c0 >= C) return;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    sc[k] = scs[v * 8 + k];
+    sh[k] = shs[v * 8 + k];
+  }
+  for (long row = (long)blockIdx.x * 32 + rl; row < a.rows; row += (long)gridDim.x * 32) {
+    float x[8];
+    unpack8(*(const uint4*)(a.y + row * C + c0), x);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = apply_act(x[k] * sc[k] + sh[k], ACT);
+    *(uint4*)(a.out + row * a.ldo + a.c_off + c0) = pack8(x);
+  }
+}
+
 // the fused form from k (SyncBN paths, where k comes from the exchange)
 __global__ void bn_xa_coef_kernel(const float* __restrict__ coef, const float* __restrict__ k, int C,
                                   float* __restrict__ xa) {
@@ -1065,6 +1168,32 @@ int bn_reduce_finalize_launch(float* part, int G, int C, double count, const flo
                               const float* shift, hipStream_t s) {
   BnFinalizeArgs a{part, G, C, count, gamma, beta, rmean, rvar, nbt, momentum, eps, coef, shift};
   hipLaunchKernelGGL(bn_reduce_finalize_kernel, dim3(cdiv(C, 64)), dim3(256), 0, s, a);
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+// row blocks per 64-channel chunk (each reads the chunk's partial rows once, then grid-strides over the rows)
+static int g_fin_blocks = getenv("IMGCLS_BN_FIN_BLOCKS") ? atoi(getenv("IMGCLS_BN_FIN_BLOCKS")) : 256;
+
+// BnFinApplyArgs: ctr = at least cdiv(C, 64) zeroed counters (left zeroed); C % 8 == 0, act 0 / 1 / 2
+int bn_fin_apply_launch(const bf16_t* y, bf16_t* out, float* part, int G, int C, long rows, double count,
+                        const float* gamma, const float* beta, float* rmean, float* rvar, long long* nbt,
+                        float momentum, float eps, float* coef, const float* shift, int ldo, int c_off, int act,
+                        unsigned* ctr, hipStream_t s) {
+  if (C % 8 || rows <= 0 || G < 1 || ldo < c_off + C) return 2;
+  const BnFinApplyArgs a{y, out, part, G, C, rows, count, gamma, beta, rmean, rvar, nbt, momentum, eps, coef, shift,
+                         ldo, c_off, ctr};
+  long bx = (rows + 127) / 128;
+  bx = bx > g_fin_blocks ? g_fin_blocks : bx;
+  const dim3 grid((unsigned)bx, (unsigned)cdiv(C, 64));
+  if (act == ACT_RELU)
+    hipLaunchKernelGGL((bn_fin_apply_kernel<ACT_RELU>), grid, dim3(256), 0, s, a);
+  else if (act == ACT_SILU)
+    hipLaunchKernelGGL((bn_fin_apply_kernel<ACT_SILU>), grid, dim3(256), 0, s, a);
+  else if (act == ACT_NONE)
+    hipLaunchKernelGGL((bn_fin_apply_kernel<ACT_NONE>), grid, dim3(256), 0, s, a);
+  else
+    return 2;
   HIP_CHECK_LAUNCH();
   return 0;
 }

@@ -74,6 +74,7 @@ class _Workspace:
         self.stats = torch.zeros(0, dtype=torch.float32, device=dev)
         self.zero = torch.zeros(64, dtype=BF16, device=dev)  # zero page for padded LDS-DMA chunks
         self.parts: list = []  # zeroed partial-stat buffers for fused BN-backward reduces
+        self.fin_ctr = torch.zeros(64, dtype=torch.int32, device=dev)  # bn_fin_apply's per-chunk block counters
 
     def take_part(self, c: int, groups: int = G_STATS) -> torch.Tensor:
         """A zeroed partial-sum buffer for a fused BN-backward reduce; handed back by ``give_part``

@@ -591,6 +591,13 @@ def _bn_bwd_k(part, grp, c, rows, training, group, count_t, params, dev, coef=No
     return k, dgamma, dbeta
 
 
+# Training BN of a small tensor (<= IMGCLS_BN_FIN_MAX elements): the partial-row reduce and finalize run inside the
+# apply kernel (csrc/bn.hip bn_fin_apply_kernel) - one launch instead of two, which is what a BN costs at the
+# reference's Inception-v3 b4 launch (graph replay, ~5 us per kernel)
+BN_FIN = os.environ.get("IMGCLS_BN_FIN", "1") == "1"
+BN_FIN_MAX = int(os.environ.get("IMGCLS_BN_FIN_MAX", str(1 << 21)))
+BN_FIN_COUNT = [0]
+
 # The residual BN's ReLU mask (1 bit per element, written by bn_apply) replaces the consumer dgrad epilogue's
 # re-read of the residual when it recomputes z = bn(y) + res > 0: ~11 GB less per ResNet-50 b1024 step.
 RELU_MASK = os.environ.get("IMGCLS_RELU_MASK", "1") == "1"
@@ -604,7 +611,31 @@ class BNActFn(torch.autograd.Function):
         n, c, h, w = y.shape
         rows = n * h * w
         a = ACT[act]
-        coef, group, count_t = _bn_coef(y, gamma, beta, bn, stats_ready, shift)
+        fin = (BN_FIN and bn.training and res is None and res_hold is None and defer is None and a <= 2
+               and c % 8 == 0 and c <= 64 * 64 and rows * c <= BN_FIN_MAX and not _shadows.FP8_FWD
+               and not _common.DETERMINISTIC and _sync_group(bn) is None)
+        if fin:
+            # small tensor: the finalize rides in the apply (one launch instead of two)
+            coef, group, count_t = torch.empty(4 * c, dtype=torch.float32, device=dev), None, None
+            grp = stat_groups(rows)
+            part = ws(dev).stats_buf(c, grp)
+            if not stats_ready:
+                C.bn_stats(y, rows, c, part, grp, shift=shift)
+            mom = bn.momentum if bn.momentum is not None else 0.1
+            track = bn.track_running_stats and bn.running_mean is not None
+            rs = (bn.running_mean, bn.running_var, bn.num_batches_tracked) if track else (None, None, None)
+            if cat is not None:
+                cbuf, idx = cat
+                dst, ldo, off = cbuf.ensure(n, h, w, dev), cbuf.total, cbuf.offs[idx]
+                out = cbuf.part(idx, c)
+            else:
+                out = dst = _empty_cl(n, c, h, w, dev)
+                ldo, off = c, 0
+            C.bn_fin_apply(y, part, grp, float(rows), gamma, beta, *rs, mom, bn.eps, coef, shift, dst, rows, c, ldo,
+                           off, a, ws(dev).fin_ctr)
+            BN_FIN_COUNT[0] += 1
+        else:
+            coef, group, count_t = _bn_coef(y, gamma, beta, bn, stats_ready, shift)
         # res_hold: the residual is a deferred BN output (it holds that BN's input); this apply forms it
         res_coef = None
         if res_hold is not None:
@@ -622,7 +653,9 @@ class BNActFn(torch.autograd.Function):
             else:
                 res_coef = res_hold.coef
                 RES_DEFER_COUNT[0] += 1
-        if defer is not None:
+        if fin:
+            pass  # (applied above)
+        elif defer is not None:
             # deferred (XfHold): the consuming conv applies act(bn(y)) itself; the output stands for
             # act(bn(y)) but holds y (autograd returns a view of the input)
             if res is not None or cat is not None or a > 1:
@@ -1040,7 +1073,7 @@ DW_LINK = os.environ.get("IMGCLS_DW_LINK", "0") == "1"
 
 # names this part owns (ops/hip.py re-exports them)
 _OWNED = (
-    'BNActFn', 'BNActPoolFn', 'BwdLink', 'ConvBiasFn', 'ConvFn', 'DW_LINK', 'DW_STATS', 'DW_STATS_COUNT',
+    'BNActFn', 'BNActPoolFn', 'BN_FIN', 'BN_FIN_COUNT', 'BN_FIN_MAX', 'BwdLink', 'ConvBiasFn', 'ConvFn', 'DW_LINK', 'DW_STATS', 'DW_STATS_COUNT',
     'DenseConvFn', 'DwConvFn', 'dw_stats_eligible',
     'FUSE_XA', 'FUSE_XF', 'GradSlot', 'PEER_BN_MAX_C', 'POOL_CONV_SWAP', 'RELU_MASK', 'RES_DEFER', 'RES_DEFER_COUNT',
     'STEM_DIRECT',

@@ -1,0 +1,7 @@
+set -o pipefail
+# BN finalize folded into the apply for small tensors (IMGCLS_BN_FIN), without the device-scope fences: numerics, A/B
+cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out; export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_hip_blocks.py -x -q --timeout 120 --timeout-method thread -k "bn_fin or block_slots" > gpurun_out/r15q_pytest.log 2>&1 || { tail -30 gpurun_out/r15q_pytest.log; exit 1; }
+tail -1 gpurun_out/r15q_pytest.log
+TAG=r15q2_b4 ROUNDS=2 ARGS="--model inceptionv3 --image-size 299 --batch 4 --steps 50 --warmup 10" bash scripts/ab_env.sh "IMGCLS_BN_FIN=0" "-" || exit 1
+TAG=r15q2_b32 ROUNDS=2 ARGS="--model inceptionv3 --image-size 299 --batch 32 --steps 30 --warmup 8" bash scripts/ab_env.sh "IMGCLS_BN_FIN=0" "-" || exit 1

@@ -453,3 +453,65 @@ def test_deferred_downsample_bn(kind, fused):
     ref.eval()
     with torch.no_grad():
         assert err(blk(x).float(), ref(x).float()) < 1e-2
+
+
+def _bn_fin_run(hip, fn, x, mods, fin):
+    """One forward + backward with IMGCLS_BN_FIN set to ``fin``: (output, input grad, param grads, buffers, fused
+    BN count).  Buffers are restored first (running stats are the statistics pivot)."""
+    keep = hip.BN_FIN
+    hip.BN_FIN = fin
+    try:
+        for m in mods:
+            m._imgcls_same_state = getattr(m, "_imgcls_same_state", None) or _SameState(m)
+            m._imgcls_same_state()
+            for p in m.parameters():
+                p.grad = None
+        n0 = hip.BN_FIN_COUNT[0]
+        xx = x.clone().requires_grad_(True)
+        out = fn(xx)
+        (out.float() * torch.linspace(-1, 1, out.numel(), device=DEV).view_as(out)).sum().backward()
+        torch.cuda.synchronize()
+        grads = [p.grad.float().clone() for m in mods for p in m.parameters()]
+        bufs = [b.detach().clone() for m in mods for b in m.buffers()]
+        return out.float(), xx.grad.float(), grads, bufs, hip.BN_FIN_COUNT[0] - n0
+    finally:
+        hip.BN_FIN = keep
+
+
+@pytest.mark.parametrize("kind", ["inception_a", "silu_136", "none_80"])
+def test_bn_fin_apply_matches_two_launch_path(kind):
+    """BN_FIN (the training BN's partial-row reduce and finalize inside its apply kernel, csrc/bn.hip
+    bn_fin_apply_kernel) against the finalize + apply launches: outputs (incl. concat slices), running statistics,
+    batch counters and every gradient.  Two fused runs in a row must agree: the kernel's last block per channel
+    chunk re-zeroes the partial rows and resets its counter, or the second run would double-count."""
+    import torch.nn as nn
+    from pytorch_imageclassification_distributed_amd.models.inception import InceptionA
+    from pytorch_imageclassification_distributed_amd.ops import hip
+    CL = torch.channels_last
+    torch.manual_seed(0)
+    if kind == "inception_a":  # 64 / 48 / 96 / 32-channel BNs writing concat slices, 35 x 35 -> 11 x 11 here
+        blk = InceptionA(192, 32).to(DEV).to(memory_format=CL).train()
+        mods, fn = [blk], blk
+        x = torch.randn(2, 192, 11, 11, device=DEV).to(torch.bfloat16).contiguous(memory_format=CL)
+    else:
+        c, act = (136, "silu") if kind == "silu_136" else (80, None)  # a partial 64-channel chunk
+        conv = nn.Conv2d(32, c, 1, bias=False).to(DEV).to(memory_format=CL)
+        bn = nn.BatchNorm2d(c).to(DEV)
+        with torch.no_grad():
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.5, 0.5)
+            bn.running_mean.uniform_(-0.2, 0.2)
+        mods = [conv, bn]
+        fn = lambda t: hip.conv_bn_act(t, conv, bn, act, None)  # noqa: E731
+        x = torch.randn(3, 32, 13, 13, device=DEV).to(torch.bfloat16).contiguous(memory_format=CL)
+    ref = _bn_fin_run(hip, fn, x, mods, False)
+    f1 = _bn_fin_run(hip, fn, x, mods, True)
+    f2 = _bn_fin_run(hip, fn, x, mods, True)
+    assert ref[4] == 0 and f1[4] > 0 and f1[4] == f2[4]
+    for r in (f1, f2):
+        assert (r[0] - ref[0]).abs().max().item() <= 1e-2 * ref[0].abs().max().item()
+        assert (r[1] - ref[1]).abs().max().item() <= 1e-2 * ref[1].abs().max().item() + 1e-6
+        for a_, b_ in zip(r[2], ref[2]):
+            assert (a_ - b_).abs().max().item() <= 1e-2 * b_.abs().max().item() + 1e-6
+        for a_, b_ in zip(r[3], ref[3]):
+            assert torch.allclose(a_.float(), b_.float(), rtol=1e-5, atol=1e-6)
