@@ -212,6 +212,14 @@ __global__ __launch_bounds__(256) void maxpool_bwd_quad_kernel(const bf16_t* __r
         }
       }
     }
+    uint4 yq[4];
+    if constexpr (RED) {  // the BN input at the quad's pixels, in flight with the dy / argmax loads above
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int h = min(max(2 * mh - g.ph + (j >> 1), 0), g.H - 1), w = min(max(2 * mw - g.pw + (j & 1), 0), g.W - 1);
+        yq[j] = *(const uint4*)(rd.y + (((long)n * g.H + h) * g.W + w) * g.C + c0);
+      }
+    }
 #pragma unroll
     for (int dh = 0; dh < 2; ++dh) {
       const int h = 2 * mh - g.ph + dh;
@@ -241,7 +249,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_quad_kernel(const bf16_t* __r
         *(uint4*)(dx + off) = pack8(acc);
         if constexpr (RED) {
           float yv[8], dz[8];
-          unpack8(*(const uint4*)(rd.y + off), yv);
+          unpack8(yq[dh * 2 + dw], yv);
           unpack8(pack8(acc), dz);  // the bf16 dz the separate reduce pass would have read back
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
