@@ -35,6 +35,8 @@ int rccl_comm_close(int64_t, bool);
 
 // ---- launcher prototypes (defined in *.hip) ----
 int bn_partials_launch(float*, int, int, double*, float*, float*, double, hipStream_t);
+int bn_fin_bwd_launch(float*, int, int, long, double, float*, float*, const bf16_t*, const bf16_t*, const float*,
+                      const bf16_t*, const bf16_t*, bf16_t*, int, int, unsigned*, hipStream_t);
 int bn_fin_apply_launch(const bf16_t*, bf16_t*, float*, int, int, long, double, const float*, const float*, float*, float*,
                         long long*, float, float, float*, const float*, int, int, int, unsigned*, hipStream_t);
 int bn_reduce_finalize_launch(float*, int, int, double, const float*, const float*, float*, float*, long long*, float,
@@ -452,6 +454,31 @@ void bn_fin_apply(Tensor y, Tensor part, int G, double count, OT gamma, OT beta,
                             (float)momentum, (float)eps, ptr<float>(coef), optr<float>(shift), ldo, c_off, act,
                             reinterpret_cast<unsigned*>(ctr.data_ptr()), cur()),
         "bn_fin_apply");
+}
+
+// training BN backward of a small tensor in one launch: partial-row reduce (dgamma, dbeta; rows re-zeroed) +
+// bn_bwd_elemt (g / dz_in / res / act / ldg as there); ctr: >= ceil(C / 64) zeroed int32
+void bn_fin_bwd(Tensor part, int G, double count, OT dgamma, OT dbeta, OT g, Tensor y, Tensor coef, OT res, OT dz_in,
+                Tensor dy, long rows, int C, int act, int ldg, Tensor ctr) {
+  req(part, F32, "part"); req(coef, F32, "coef");
+  TORCH_CHECK(y.scalar_type() == BF && dy.scalar_type() == BF && ctr.scalar_type() == torch::kInt32,
+              "bn_fin_bwd: dtypes");
+  TORCH_CHECK(part.numel() >= (int64_t)G * 2 * C && coef.numel() >= 4 * C && y.numel() == rows * C &&
+                  dy.numel() == rows * C && ctr.numel() >= (C + 63) / 64,
+              "bn_fin_bwd: buffer sizes");
+  const int lg = ldg > 0 ? ldg : C;
+  // (g may be a channel slice of a concat gradient, row stride ldg: check the storage it indexes)
+  TORCH_CHECK(!g.has_value() || !g->defined() ||
+                  (int64_t)(g->storage().nbytes() / 2) - g->storage_offset() >= (rows - 1) * lg + C,
+              "bn_fin_bwd: g size");
+  for (const OT* t : {&res, &dz_in})
+    TORCH_CHECK(!t->has_value() || !(*t)->defined() || (*t)->numel() == rows * C, "bn_fin_bwd: res / dz_in size");
+  for (const OT* t : {&dgamma, &dbeta})
+    TORCH_CHECK(!t->has_value() || !(*t)->defined() || (*t)->numel() >= C, "bn_fin_bwd: dgamma / dbeta size");
+  check(bn_fin_bwd_launch(ptr<float>(part), G, C, rows, count, optr<float>(dgamma), optr<float>(dbeta),
+                          optr<bf16_t>(g), ptr<bf16_t>(y), ptr<float>(coef), optr<bf16_t>(res), optr<bf16_t>(dz_in),
+                          ptr<bf16_t>(dy), act, ldg, reinterpret_cast<unsigned*>(ctr.data_ptr()), cur()),
+        "bn_fin_bwd");
 }
 
 void bn_reduce_bwd(Tensor part, int G, int C, double count, OT dgamma, OT dbeta, Tensor k, OT coef, OT xa) {
@@ -1175,6 +1202,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_set_unroll", [](bool v) { bn_set_unroll(v ? 1 : 0); });
   m.def("bn_res_coef_ok", &bn_res_coef_ok);
   m.def("bn_fin_apply", &bn_fin_apply);
+  m.def("bn_fin_bwd", &bn_fin_bwd);
   // a stream whose kernels may only occupy the CUs set in ``mask`` (32 per word; ops/_hip/streams.py
   // IMGCLS_WGRAD_CU_FRAC: the weight-gradient side stream on a subset, the compute stream keeps the rest)
   m.def("cu_mask_stream", [](int device, std::vector<uint32_t> mask) -> uintptr_t {

@@ -255,6 +255,107 @@ __global__ __launch_bounds__(256) void bn_fin_apply_kernel(BnFinApplyArgs a) {
   }
 }
 
+// The backward counterpart (IMGCLS_BN_FIN): bn_reduce_bwd folded into bn_bwd_elemt for small tensors.  Blocks
+// reduce their chunk's partial rows (sum dz, sum dz * xhat), blocks with blockIdx.x == 0 write dbeta / dgamma, the
+// chunk's last block re-zeroes the rows and resets its counter (as bn_fin_apply_kernel), and every block forms
+// dy = scale * (dz - k1 - xhat * k2) on its rows.  MODE as bn_bwd_elemt_u_kernel: 0 dz given, 1 g with the
+// activation recomputed, 2 the same with a residual, 3 g is already dz.
+struct BnFinBwdArgs {
+  float* part; int G, C; long rows; double count;
+  float* dgamma; float* dbeta;
+  const bf16_t* g; const bf16_t* y; const float* coef; const bf16_t* res; const bf16_t* dz_in; bf16_t* dy;
+  int ldg;
+  unsigned* ctr;
+};
+
+template <int MODE, int ACT>
+__global__ __launch_bounds__(256) void bn_fin_bwd_kernel(BnFinBwdArgs a) {
+  __shared__ double red[2][4][64];
+  __shared__ float k1s[64], k2s[64];
+  __shared__ unsigned last;
+  const int lc = threadIdx.x & 63, lg = threadIdx.x >> 6;
+  const int C = a.C;
+  const int c = blockIdx.y * 64 + lc;
+  double s = 0.0, q = 0.0;
+  if (c < C) {
+#pragma unroll 4
+    for (int g = lg; g < a.G; g += 4) {
+      const float* r = a.part + (size_t)g * 2 * C;
+      s += (double)r[c];
+      q += (double)r[C + c];
+    }
+  }
+  red[0][lg][lc] = s;
+  red[1][lg][lc] = q;
+  __syncthreads();
+  if (lg == 0) {
+    float k1 = 0.f, k2 = 0.f;
+    if (c < C) {
+      s = red[0][0][lc] + red[0][1][lc] + red[0][2][lc] + red[0][3][lc];
+      q = red[1][0][lc] + red[1][1][lc] + red[1][2][lc] + red[1][3][lc];
+      k1 = (float)(s / a.count);
+      k2 = (float)(q / a.count);
+      if (blockIdx.x == 0) {
+        if (a.dbeta) a.dbeta[c] = (float)s;
+        if (a.dgamma) a.dgamma[c] = (float)q;
+      }
+    }
+    k1s[lc] = k1;
+    k2s[lc] = k2;
+  }
+  __syncthreads();  // (no fence: see bn_fin_apply_kernel)
+  if (threadIdx.x == 0) last = atomicAdd(a.ctr + blockIdx.y, 1u) == gridDim.x - 1 ? 1u : 0u;
+  __syncthreads();
+  if (last) {
+    if (c < C) {
+      for (int g = lg; g < a.G; g += 4) {
+        float* r = a.part + (size_t)g * 2 * C;
+        r[c] = 0.f;
+        r[C + c] = 0.f;
+      }
+    }
+    if (threadIdx.x == 0) a.ctr[blockIdx.y] = 0u;
+  }
+  const int v = threadIdx.x & 7, rl = threadIdx.x >> 3;
+  const int c0 = blockIdx.y * 64 + v * 8;
+  if (c0 >= C) return;
+  float sc[8], sh[8], mu[8], is[8], k1[8], k2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    sc[k] = a.coef[c0 + k];
+    sh[k] = a.coef[C + c0 + k];
+    mu[k] = a.coef[2 * C + c0 + k];
+    is[k] = a.coef[3 * C + c0 + k];
+    k1[k] = k1s[v * 8 + k];
+    k2[k] = k2s[v * 8 + k];
+  }
+  for (long row = (long)blockIdx.x * 32 + rl; row < a.rows; row += (long)gridDim.x * 32) {
+    float gv[8], yv[8];
+    unpack8(*(const uint4*)(a.y + row * C + c0), yv);
+    if constexpr (MODE == 0) {
+      unpack8(*(const uint4*)(a.dz_in + row * C + c0), gv);
+    } else {
+      unpack8(*(const uint4*)(a.g + row * a.ldg + c0), gv);
+      if constexpr (MODE == 1 || MODE == 2) {
+        float rv[8];
+        if constexpr (MODE == 2) unpack8(*(const uint4*)(a.res + row * C + c0), rv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float z = yv[k] * sc[k] + sh[k];
+          if constexpr (MODE == 2) z += rv[k];
+          gv[k] = act_grad(z, gv[k], ACT);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float xhat = (yv[k] - mu[k]) * is[k];
+      gv[k] = sc[k] * (gv[k] - k1[k] - xhat * k2[k]);
+    }
+    *(uint4*)(a.dy + row * C + c0) = pack8(gv);
+  }
+}
+
 // the fused form from k (SyncBN paths, where k comes from the exchange)
 __global__ void bn_xa_coef_kernel(const float* __restrict__ coef, const float* __restrict__ k, int C,
                                   float* __restrict__ xa) {
@@ -1194,6 +1295,26 @@ int bn_fin_apply_launch(const bf16_t* y, bf16_t* out, float* part, int G, int C,
     hipLaunchKernelGGL((bn_fin_apply_kernel<ACT_NONE>), grid, dim3(256), 0, s, a);
   else
     return 2;
+  HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+int bn_fin_bwd_launch(float* part, int G, int C, long rows, double count, float* dgamma, float* dbeta,
+                      const bf16_t* g, const bf16_t* y, const float* coef, const bf16_t* res, const bf16_t* dz_in,
+                      bf16_t* dy, int act, int ldg, unsigned* ctr, hipStream_t s) {
+  if (C % 8 || rows <= 0 || G < 1) return 2;
+  const int mode = dz_in ? 0 : act == ACT_NONE ? 3 : res ? 2 : 1;
+  if (mode != 0 && !g) return 2;
+  const BnFinBwdArgs a{part, G, C, rows, count, dgamma, dbeta, g, y, coef, res, dz_in, dy, ldg > 0 ? ldg : C, ctr};
+  long bx = (rows + 127) / 128;
+  bx = bx > g_fin_blocks ? g_fin_blocks : bx;
+  const dim3 grid((unsigned)bx, (unsigned)cdiv(C, 64));
+#define FINB(M, A) hipLaunchKernelGGL((bn_fin_bwd_kernel<M, A>), grid, dim3(256), 0, s, a)
+  if (mode == 0) FINB(0, ACT_NONE);
+  else if (mode == 3) FINB(3, ACT_NONE);
+  else if (mode == 1) { if (act == ACT_SILU) FINB(1, ACT_SILU); else FINB(1, ACT_RELU); }
+  else { if (act == ACT_SILU) FINB(2, ACT_SILU); else FINB(2, ACT_RELU); }
+#undef FINB
   HIP_CHECK_LAUNCH();
   return 0;
 }

@@ -597,6 +597,11 @@ def _bn_bwd_k(part, grp, c, rows, training, group, count_t, params, dev, coef=No
 BN_FIN = os.environ.get("IMGCLS_BN_FIN", "1") == "1"
 BN_FIN_MAX = int(os.environ.get("IMGCLS_BN_FIN_MAX", str(1 << 21)))
 BN_FIN_COUNT = [0]
+# the backward counterpart (bn_reduce_bwd inside bn_bwd_elemt, csrc/bn.hip bn_fin_bwd_kernel): measured no better
+# than the two launches (Inception-v3 b4 491 vs 493-495 img/s with the forward form alone, b128 -1.5 %;
+# profiles/r15v_bn_fin_bwd_ab.txt), so off by default
+BN_FIN_BWD = os.environ.get("IMGCLS_BN_FIN_BWD", "0") == "1"
+BN_FIN_BWD_COUNT = [0]  # BN backwards whose reduce rode in the elementwise pass
 
 # The residual BN's ReLU mask (1 bit per element, written by bn_apply) replaces the consumer dgrad epilogue's
 # re-read of the residual when it recomputes z = bn(y) + res > 0: ~11 GB less per ResNet-50 b1024 step.
@@ -749,7 +754,16 @@ class BNActFn(torch.autograd.Function):
                 dz = None
             C.bn_bwd_reduce(g, y, coef, res, dz if dz is not g else None, rows, c, ctx.act, part, grp, ldg)
         xac = torch.empty(3 * c, dtype=torch.float32, device=dev) if xa is not None else None
-        if pending is not None:  # SyncBN all-reduce launched early by the consuming conv's backward
+        fin = (BN_FIN_BWD and xa is None and pending is None and ctx.training and ctx.group is None and c % 8 == 0
+               and rows * c <= BN_FIN_MAX and not _common.DETERMINISTIC)
+        if fin:  # small tensor: the partial-row reduce rides in the elementwise pass (one launch instead of two)
+            dgamma = grad_buffer(ctx.params[0], zero=False)
+            dbeta = grad_buffer(ctx.params[1], zero=False)
+            dy = torch.empty_like(y, memory_format=CL)
+            C.bn_fin_bwd(part, grp, float(rows), dgamma, dbeta, None if dz is not None else g, y, coef, res, dz, dy,
+                         rows, c, ctx.act, 0 if dz is not None else ldg, ws(dev).fin_ctr)
+            BN_FIN_BWD_COUNT[0] += 1
+        elif pending is not None:  # SyncBN all-reduce launched early by the consuming conv's backward
             sums, work, dgamma, dbeta, k = pending
             if work is not None:  # (None: ran on this stream, inside a graph capture)
                 work.wait()
@@ -768,7 +782,7 @@ class BNActFn(torch.autograd.Function):
             xa.dz, xa.y, xa.coef = dz, y, xac
             XA_COUNT[0] += 1
             dy = dz
-        else:
+        elif not fin:
             dy = torch.empty_like(y, memory_format=CL)
             C.bn_bwd_elemt(None if dz is not None else g, y, coef, k, res, dz, dy, rows, c, ctx.act,
                            0 if dz is not None else ldg)
@@ -1073,7 +1087,7 @@ DW_LINK = os.environ.get("IMGCLS_DW_LINK", "0") == "1"
 
 # names this part owns (ops/hip.py re-exports them)
 _OWNED = (
-    'BNActFn', 'BNActPoolFn', 'BN_FIN', 'BN_FIN_COUNT', 'BN_FIN_MAX', 'BwdLink', 'ConvBiasFn', 'ConvFn', 'DW_LINK', 'DW_STATS', 'DW_STATS_COUNT',
+    'BNActFn', 'BNActPoolFn', 'BN_FIN', 'BN_FIN_BWD', 'BN_FIN_BWD_COUNT', 'BN_FIN_COUNT', 'BN_FIN_MAX', 'BwdLink', 'ConvBiasFn', 'ConvFn', 'DW_LINK', 'DW_STATS', 'DW_STATS_COUNT',
     'DenseConvFn', 'DwConvFn', 'dw_stats_eligible',
     'FUSE_XA', 'FUSE_XF', 'GradSlot', 'PEER_BN_MAX_C', 'POOL_CONV_SWAP', 'RELU_MASK', 'RES_DEFER', 'RES_DEFER_COUNT',
     'STEM_DIRECT',

@@ -458,30 +458,32 @@ def test_deferred_downsample_bn(kind, fused):
 def _bn_fin_run(hip, fn, x, mods, fin):
     """One forward + backward with IMGCLS_BN_FIN set to ``fin``: (output, input grad, param grads, buffers, fused
     BN count).  Buffers are restored first (running stats are the statistics pivot)."""
-    keep = hip.BN_FIN
-    hip.BN_FIN = fin
+    keep, keep_bwd = hip.BN_FIN, hip.BN_FIN_BWD
+    hip.BN_FIN = hip.BN_FIN_BWD = fin
     try:
         for m in mods:
             m._imgcls_same_state = getattr(m, "_imgcls_same_state", None) or _SameState(m)
             m._imgcls_same_state()
             for p in m.parameters():
                 p.grad = None
-        n0 = hip.BN_FIN_COUNT[0]
+        n0 = hip.BN_FIN_COUNT[0] + 1000 * hip.BN_FIN_BWD_COUNT[0]
         xx = x.clone().requires_grad_(True)
         out = fn(xx)
         (out.float() * torch.linspace(-1, 1, out.numel(), device=DEV).view_as(out)).sum().backward()
         torch.cuda.synchronize()
         grads = [p.grad.float().clone() for m in mods for p in m.parameters()]
         bufs = [b.detach().clone() for m in mods for b in m.buffers()]
-        return out.float(), xx.grad.float(), grads, bufs, hip.BN_FIN_COUNT[0] - n0
+        return (out.float(), xx.grad.float(), grads, bufs,
+                hip.BN_FIN_COUNT[0] + 1000 * hip.BN_FIN_BWD_COUNT[0] - n0)
     finally:
-        hip.BN_FIN = keep
+        hip.BN_FIN, hip.BN_FIN_BWD = keep, keep_bwd
 
 
 @pytest.mark.parametrize("kind", ["inception_a", "silu_136", "none_80"])
 def test_bn_fin_apply_matches_two_launch_path(kind):
     """BN_FIN (the training BN's partial-row reduce and finalize inside its apply kernel, csrc/bn.hip
-    bn_fin_apply_kernel) against the finalize + apply launches: outputs (incl. concat slices), running statistics,
+    bn_fin_apply_kernel, and the backward reduce inside the elementwise pass, bn_fin_bwd_kernel) against the
+    separate launches: outputs (incl. concat slices), running statistics,
     batch counters and every gradient.  Two fused runs in a row must agree: the kernel's last block per channel
     chunk re-zeroes the partial rows and resets its counter, or the second run would double-count."""
     import torch.nn as nn
@@ -507,7 +509,7 @@ def test_bn_fin_apply_matches_two_launch_path(kind):
     ref = _bn_fin_run(hip, fn, x, mods, False)
     f1 = _bn_fin_run(hip, fn, x, mods, True)
     f2 = _bn_fin_run(hip, fn, x, mods, True)
-    assert ref[4] == 0 and f1[4] > 0 and f1[4] == f2[4]
+    assert ref[4] == 0 and f1[4] % 1000 > 0 and f1[4] >= 1000 and f1[4] == f2[4]  # forward and backward fused
     for r in (f1, f2):
         assert (r[0] - ref[0]).abs().max().item() <= 1e-2 * ref[0].abs().max().item()
         assert (r[1] - ref[1]).abs().max().item() <= 1e-2 * ref[1].abs().max().item() + 1e-6
