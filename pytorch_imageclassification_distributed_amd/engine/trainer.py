@@ -48,9 +48,11 @@ from .config import hip_graph_enabled, parse_class_weights
 from .optim import FusedAdam, MultiStepLR
 
 # training steps the host may have enqueued ahead of the GPU (Trainer._throttle; 0 = unbounded).  Unset: 2, or
-# 4 when a step's peak allocation is under SMALL_STEP_FRACTION of the device (the host-bound small-memory
-# steps gain from the deeper queue - Inception-v3 b256 8323 -> 8400 img/s, profiles/history/r7d_* - and their cache
-# stays small; ResNet-50 b1024 at 44 GiB keeps 2)
+# 3 when a step's peak allocation is under SMALL_STEP_FRACTION of the device (host-bound small-memory steps; round
+# 4 measured Inception-v3 b256 8323 -> 8400 img/s with 4, profiles/history/r7d_*).  Round 6 re-measured 2 / 3 / 4 on
+# the current build: throughput equal within noise, but with 4 the caching allocator kept mapping blocks in the
+# timed region (ResNet-101 b256: 118 hipMallocs in 20 steps, EfficientNet-B0 b256: 23) while 3 left 0 there
+# (profiles/r15x_inflight_alloc_ab.txt).  ResNet-50 b1024 at 44 GiB keeps 2.
 MAX_INFLIGHT_STEPS = int(os.environ.get("IMGCLS_MAX_INFLIGHT_STEPS", "-1"))
 SMALL_STEP_FRACTION = 0.1
 
@@ -281,7 +283,7 @@ class Trainer:
                 return 2
             total = torch.cuda.get_device_properties(self.dev).total_memory
             small = torch.cuda.max_memory_allocated(self.dev) < SMALL_STEP_FRACTION * total
-            self._auto_inflight = 4 if small else 2
+            self._auto_inflight = 3 if small else 2
         return self._auto_inflight
 
     def _step_enqueued(self) -> None:

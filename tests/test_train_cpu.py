@@ -136,11 +136,11 @@ def test_step_throttle_bounds_steps_in_flight(monkeypatch):
     monkeypatch.setattr(tm, "MAX_INFLIGHT_STEPS", 0)  # 0: unbounded, never waits
     tm.Trainer._throttle(fake)
     assert waited == [0, 1, 2]
-    # unset (-1): 2 while the first steps tune, then the memory-based choice (4 for a small step)
+    # unset (-1): 2 while the first steps tune, then the memory-based choice (3 for a small step)
     monkeypatch.setattr(tm, "MAX_INFLIGHT_STEPS", -1)
     assert tm.Trainer._inflight_limit(fake) == 2
-    fake._steps_enqueued, fake._auto_inflight = 5, 4
-    assert tm.Trainer._inflight_limit(fake) == 4
+    fake._steps_enqueued, fake._auto_inflight = 5, 3
+    assert tm.Trainer._inflight_limit(fake) == 3
 
 
 def test_hip_graph_auto_mode():
