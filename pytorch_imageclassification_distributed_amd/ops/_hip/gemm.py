@@ -651,7 +651,7 @@ WGRAD_WS = os.environ.get("IMGCLS_WGRAD_WS", "1") == "1"  # split-K partials: wo
 # the zeroed gradient slot by fp32 atomics, which saves the reduce launch - the whole cost of a tiny layer's split
 # (Inception-v3 b4 graph replay: ~75 wgrad_reduce launches of ~5 us in an 8.4 ms step).  Same box: Inception-v3 b4
 # +3.7 % at this threshold; b32, b128 and ResNet-50 b64 unchanged; all-atomic weight gradients lose 3.5 % at b128 and
-# an 8192-pixel threshold 2.2 % (its 8 x 8 layers), profiles/r15o_*, r15p_*
+# an 8192-pixel threshold 2.2 % (its 8 x 8 layers), profiles/r15p_wgrad_atomic_small_layers_ab.txt
 WGRAD_ATOMIC_PIX = int(os.environ.get("IMGCLS_WGRAD_ATOMIC_PIX", "6144"))
 _WGRAD_WS: dict = {}  # (device index, stream id) -> fp32 workspace, grown on demand
 
