@@ -355,7 +355,7 @@ void conv_wgrad(Tensor dY, Tensor X, Tensor dW, int M, int Cout, int Cin, int Nt
   p.zero = ptr<bf16_t>(zero);
   p.dw_elems = dW.numel();
   p.oob = oob_record();
-  TORCH_CHECK(stages >= 0 && stages <= 15, "conv_wgrad: stages must be 0..15");
+  TORCH_CHECK(stages >= 0 && stages <= 16, "conv_wgrad: stages must be 0..16");
   TORCH_CHECK((stages != 5 && stages != 6) || Cout <= 32, "conv_wgrad: stages 5 / 6 (32-row tile) need Cout <= 32");
   TORCH_CHECK((stages != 4 && stages != 7 && stages != 9) || Cout >= 256, "conv_wgrad: the 256x256 tile needs Cout >= 256");
   p.stages = stages;

@@ -2052,13 +2052,13 @@ static bool launch_wg(const WgradParams& p, int splits, hipStream_t stream) {
 // variants with a fused BN-backward form: all but the 256 x 256 tile with a 2-deep 64-pixel ring (its
 // register y pieces spill at 2 waves per SIMD; LDS y would not fit) and the 4-deep 256 x 256 ring (LDS)
 bool conv_wgrad_has_xa(int stages) {
-  return stages >= 1 && stages <= 12 && stages != 4 && stages != 7 && stages != 12;
+  return (stages >= 1 && stages <= 12 && stages != 4 && stages != 7 && stages != 12) || stages == 16;
 }
 // the fused BN-apply X form needs no register operand: every LDS-DMA variant has it
-bool conv_wgrad_has_xf(int stages) { return stages >= 1 && stages <= 12; }
+bool conv_wgrad_has_xf(int stages) { return (stages >= 1 && stages <= 12) || stages == 16; }
 
 int conv_wgrad_tile_n(int stages) {
-  return (stages == 4 || stages == 7 || stages == 9) ? 256 : stages >= 10 ? 64 : WBN;
+  return (stages == 4 || stages == 7 || stages == 9 || stages == 16) ? 256 : stages >= 10 ? 64 : WBN;
 }
 
 // the bounds-checked debug build (common.h IMGCLS_INB) is this translation unit compiled with IMGCLS_BOUNDS_CHECK
@@ -2073,7 +2073,7 @@ bool conv_bounds_checked() {
 int conv_wgrad_launch(const WgradParams& p_in, int splits, hipStream_t stream) {
   if (p_in.M <= 0) return 0;
   if (p_in.xa_y && (g_wvariant == 1 || !conv_wgrad_has_xa(p_in.stages))) return 4;
-  if (p_in.stages >= 13) {
+  if (p_in.stages >= 13 && p_in.stages <= 15) {  // (16: the 64 x 256 LDS-DMA tile below)
     if (p_in.xf_coef) return 4;
     WgradParams p = p_in;
     if (splits <= 1) p.ws = nullptr;
@@ -2096,7 +2096,12 @@ int conv_wgrad_launch(const WgradParams& p_in, int splits, hipStream_t stream) {
   // stages: 1 | 2 (4 waves, 64/128 x 128 tile), 3 = 2-stage ring with the in-block 2-way pixel split
   // (8 waves), 4 = 256 x 256 tile on 8 waves (2-stage ring, one block per CU; Cout >= 256 only),
   // 5 / 6 = 32 x 128 tile with a 1 / 2-stage ring (Cout <= 32 only)
-  if (dma && p.stages >= 10 && p.stages <= 12) {
+  if (dma && p.stages == 16) {
+    // 64 x 256 on 4 waves (Cout <= 64, Ntot >= 256: the s2d stem, 256 = 16 taps x 16 channels): one column tile,
+    // so an XA weight gradient forms each dY element once instead of once per 128-column tile
+    if (p.Cout > 64) return 2;
+    ok = launch_wg<64, 256, 1, 4, 1, 2>(p, splits, stream);
+  } else if (dma && p.stages >= 10 && p.stages <= 12) {
     // 64-column tiles for Ntot <= 64 (ResNet layer1 conv3: Cin 64), where a 128-column tile is half empty:
     // 10 / 11 = 64|128 x 64 on 4 waves with a 1- / 2-stage ring, 12 = 256 x 64 on 8 waves (Cout >= 256)
     if (p.stages == 12) {

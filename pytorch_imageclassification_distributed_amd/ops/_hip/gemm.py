@@ -698,6 +698,8 @@ def _wgrad_tiles(co, ntot, stages):
     stages 5 / 6, 64-column tiles for stages 10 / 11 (64|128 rows) and 12 (256 rows), else 64|128 x 128."""
     if stages in (4, 7, 9, 13):
         return (-(-co // 256)) * (-(-ntot // 256))
+    if stages == 16:  # 64 x 256 on 4 waves (Cout <= 64)
+        return (-(-co // 64)) * (-(-ntot // 256))
     if stages in (14, 15):  # prefetch-depth-2 kernel (csrc/wgrad_deep.hip): 128 x 256 / 256 x 128
         return (-(-co // (128 if stages == 14 else 256))) * (-(-ntot // (256 if stages == 14 else 128)))
     if stages >= 10:
@@ -756,6 +758,8 @@ def _wgrad_config(dy, x, g: ConvGeom, m, ntot, xa=None, xf=None):
                 cands += [(cand, 15) for cand in (256, 512, 768, 1024)]
         if g.Co <= 32:  # 32-row tiles: a 64-row tile would be half empty
             cands += [(cand, st) for st in (5, 6) for cand in blocks]
+        if g.Co <= 64 and ntot >= 256:  # 64 x 256: one column tile where an XA / XF form re-forms per tile
+            cands += [(cand, 16) for cand in blocks]
         if ntot <= 64 and WGRAD_NARROW_TILES:  # 64-column tiles: a 128-column tile is half empty (layer1 conv3)
             cands += [(cand, st) for st in (10, 11) for cand in blocks]
             if g.Co >= 256:

@@ -96,12 +96,14 @@ def _launches(conv, shape, batch):
             part_numel=2 * G_STATS * g.Ci, part_groups=G_STATS, coef_numel=4 * g.Ci, mask_numel=dx_n // 8)))
     wg = []
     ntot = g.T * g.Cx
-    for stages in range(1, 16):
+    for stages in range(1, 17):
+        if stages == 16 and g.Co > 64:
+            continue
         tiles = G._wgrad_tiles(g.Co, ntot, stages)
         for target in G.WGRAD_CANDIDATES:
             kps, splits = G._wgrad_split(M, tiles, target)
             tr = 256 if stages in (4, 7, 9, 12, 13, 15) else 32 if stages in (5, 6) else 64 if g.Co <= 64 else 128
-            tc = 256 if stages in (4, 7, 9, 13, 14) else 64 if stages in (10, 11, 12) else 128
+            tc = 256 if stages in (4, 7, 9, 13, 14, 16) else 64 if stages in (10, 11, 12) else 128
             wg.append((f"wgrad st{stages} t{target}", dict(
                 M=M, Cout=g.Co, Cin=g.Cx, Ntot=ntot, OH=g.OH, OW=g.OW, IH=g.H, IW=g.W, KW=g.kw, k_per_split=kps,
                 splits=splits, dy_numel=y_n, x_numel=x_n, dw_numel=g.Co * ntot,

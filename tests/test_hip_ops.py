@@ -98,7 +98,8 @@ N_FP8_CFG = _table_len("conv_fp8_cfgs", 8)
 def _wgrad_stage_ok(case, stages):
     # stages 4 / 7 / 9 = 256x256 8-wave tile (Cout >= 256), 5/6 = 32-row tile (Cout <= 32), 8 = any,
     # 10 / 11 = 64-column tiles (any), 12 = 256 x 64 (Cout >= 256)
-    return not ((stages in (4, 7, 9, 12) and case[4] < 256) or (stages in (5, 6) and case[4] > 32))
+    return not ((stages in (4, 7, 9, 12) and case[4] < 256) or (stages in (5, 6) and case[4] > 32)
+                or (stages == 16 and case[4] > 64))
 
 
 @pytest.mark.parametrize("cfg", range(N_CFG))
@@ -283,7 +284,7 @@ def test_conv_bn_act_halo(act, use_res, cfg):
 
 @pytest.mark.parametrize("case,stages", [
     (c, st) for c in [CONV_CASES[i] for i in (0, 1, 3, 4, 5, 6, 7, 8, 12, 13, 14, 15)]
-    for st in (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
+    for st in (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16)
     if _wgrad_stage_ok(c, st)])
 def test_conv_wgrad_ring_variants(case, stages):
     """Weight-gradient kernel variants: 1-stage (occupancy), 2-stage ring, the 8-wave in-block
@@ -726,6 +727,17 @@ def test_conv_bn_act_pool(case, stem_xa):
         _conv_bn_act_pool_case(hip, case, stem_xa)
     finally:
         hip.STEM_XA = keep_xa
+
+
+def test_stem_xa_wgrad_64x256():
+    """The s2d stem's XA weight gradient on the 64 x 256 tile (stages 16: Cout 64 x Ntot 256 in one column tile)."""
+    hip = _hip()
+    keep = hip.STEM_XA, hip.WGRAD_STAGES
+    hip.STEM_XA, hip.WGRAD_STAGES = True, 16
+    try:
+        _conv_bn_act_pool_case(hip, (2, 3, 64, 64, (7, 2, 3), (3, 2, 1)), True)
+    finally:
+        hip.STEM_XA, hip.WGRAD_STAGES = keep
 
 
 def _conv_bn_act_pool_case(hip, case, stem_xa):
