@@ -161,6 +161,8 @@ __global__ __launch_bounds__(256) void bn_reduce_bwd_kernel(float* part, int G, 
 // LAST block: each block counts itself in `ctr[chunk]` after its reads; the block that completes the count updates
 // the chunk's running statistics, zeroes its partial columns and resets the counter for the next launch.  No
 // block ever waits for another.
+constexpr int BN_FIN_U = 4;
+
 struct BnFinApplyArgs {
   const bf16_t* y; bf16_t* out; float* part; int G, C; long rows; double count;
   const float* gamma; const float* beta; float* rmean; float* rvar; long long* nbt;
@@ -246,12 +248,26 @@ __global__ __launch_bounds__(256) void bn_fin_apply_kernel(BnFinApplyArgs a) {
     sc[k] = scs[v * 8 + k];
     sh[k] = shs[v * 8 + k];
   }
-  for (long row = (long)blockIdx.x * 32 + rl; row < a.rows; row += (long)gridDim.x * 32) {
-    float x[8];
-    unpack8(*(const uint4*)(a.y + row * C + c0), x);
+  // BN_U rows of loads in flight per lane before any is used (one dependent load per iteration capped the
+  // larger tensors' bandwidth)
+  const long step = (long)gridDim.x * 32;
+  for (long row = (long)blockIdx.x * 32 + rl; row < a.rows; row += BN_FIN_U * step) {
+    uint4 yv[BN_FIN_U];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) x[k] = apply_act(x[k] * sc[k] + sh[k], ACT);
-    *(uint4*)(a.out + row * a.ldo + a.c_off + c0) = pack8(x);
+    for (int u = 0; u < BN_FIN_U; ++u) {
+      const long r = row + u * step < a.rows ? row + u * step : row;
+      yv[u] = *(const uint4*)(a.y + r * C + c0);
+    }
+#pragma unroll
+    for (int u = 0; u < BN_FIN_U; ++u) {
+      const long r = row + u * step;
+      if (r >= a.rows) break;
+      float x[8];
+      unpack8(yv[u], x);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) x[k] = apply_act(x[k] * sc[k] + sh[k], ACT);
+      *(uint4*)(a.out + r * a.ldo + a.c_off + c0) = pack8(x);
+    }
   }
 }
 
