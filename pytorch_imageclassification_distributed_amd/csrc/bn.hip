@@ -345,16 +345,28 @@ __global__ __launch_bounds__(256) void bn_fin_bwd_kernel(BnFinBwdArgs a) {
     k1[k] = k1s[v * 8 + k];
     k2[k] = k2s[v * 8 + k];
   }
-  for (long row = (long)blockIdx.x * 32 + rl; row < a.rows; row += (long)gridDim.x * 32) {
+  const long step = (long)gridDim.x * 32;
+  for (long row0 = (long)blockIdx.x * 32 + rl; row0 < a.rows; row0 += 2 * step) {
+    // two rows of loads in flight per lane before either is used
+    uint4 yl[2], gl[2], rl2[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const long r = row0 + u * step < a.rows ? row0 + u * step : row0;
+      yl[u] = *(const uint4*)(a.y + r * C + c0);
+      gl[u] = MODE == 0 ? *(const uint4*)(a.dz_in + r * C + c0) : *(const uint4*)(a.g + r * a.ldg + c0);
+      if constexpr (MODE == 2) rl2[u] = *(const uint4*)(a.res + r * C + c0);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+    const long row = row0 + u * step;
+    if (row >= a.rows) break;
     float gv[8], yv[8];
-    unpack8(*(const uint4*)(a.y + row * C + c0), yv);
-    if constexpr (MODE == 0) {
-      unpack8(*(const uint4*)(a.dz_in + row * C + c0), gv);
-    } else {
-      unpack8(*(const uint4*)(a.g + row * a.ldg + c0), gv);
+    unpack8(yl[u], yv);
+    unpack8(gl[u], gv);
+    if constexpr (MODE != 0) {
       if constexpr (MODE == 1 || MODE == 2) {
         float rv[8];
-        if constexpr (MODE == 2) unpack8(*(const uint4*)(a.res + row * C + c0), rv);
+        if constexpr (MODE == 2) unpack8(rl2[u], rv);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           float z = yv[k] * sc[k] + sh[k];
@@ -369,6 +381,7 @@ __global__ __launch_bounds__(256) void bn_fin_bwd_kernel(BnFinBwdArgs a) {
       gv[k] = sc[k] * (gv[k] - k1[k] - xhat * k2[k]);
     }
     *(uint4*)(a.dy + row * C + c0) = pack8(gv);
+    }
   }
 }
 

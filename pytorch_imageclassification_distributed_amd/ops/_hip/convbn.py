@@ -597,10 +597,10 @@ def _bn_bwd_k(part, grp, c, rows, training, group, count_t, params, dev, coef=No
 BN_FIN = os.environ.get("IMGCLS_BN_FIN", "1") == "1"
 BN_FIN_MAX = int(os.environ.get("IMGCLS_BN_FIN_MAX", str(1 << 21)))
 BN_FIN_COUNT = [0]
-# the backward counterpart (bn_reduce_bwd inside bn_bwd_elemt, csrc/bn.hip bn_fin_bwd_kernel): measured no better
-# than the two launches (Inception-v3 b4 491 vs 493-495 img/s with the forward form alone, b128 -1.5 %;
-# profiles/r15v_bn_fin_bwd_ab.txt), so off by default
-BN_FIN_BWD = os.environ.get("IMGCLS_BN_FIN_BWD", "0") == "1"
+# the backward counterpart (bn_reduce_bwd inside bn_bwd_elemt, csrc/bn.hip bn_fin_bwd_kernel).  Its first form (one
+# dependent row load per iteration) measured no better than the two launches (profiles/r15v_bn_fin_bwd_ab.txt); with
+# two rows of loads in flight per lane: Inception-v3 b4 +1 %, b32 +1 %, ResNet-50 b64 unchanged (profiles/r16a_*)
+BN_FIN_BWD = os.environ.get("IMGCLS_BN_FIN_BWD", "1") == "1"
 BN_FIN_BWD_COUNT = [0]  # BN backwards whose reduce rode in the elementwise pass
 
 # The residual BN's ReLU mask (1 bit per element, written by bn_apply) replaces the consumer dgrad epilogue's
