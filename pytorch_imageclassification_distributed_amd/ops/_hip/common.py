@@ -26,7 +26,8 @@ DETERMINISTIC = os.environ.get("IMGCLS_DETERMINISTIC", "0") == "1"
 
 def set_deterministic(flag: bool = True) -> None:
     """Bitwise-reproducible mode: every fp32 atomic site gets one contribution per address - BN partial
-    rows >= producing blocks, no split-K (wgrad, head GEMMs), ordered column sums.  Slower."""
+    rows >= producing blocks, no split-K (wgrad, head GEMMs), ordered column sums - and conv kernel choices
+    come from the find-db or the shape heuristic, never from timing, so separate processes agree too.  Slower."""
     global DETERMINISTIC
     DETERMINISTIC = bool(flag)
     C.set_deterministic(DETERMINISTIC)

@@ -222,7 +222,9 @@ def _conv_gemm(A, B, out, stats, bias, geo, dh, dw, tb, zero, addend=None, bwd=(
             (("y2",) if y2 is not None else ())
         cfg = _STAGES_TUNED.get(key)
         if cfg is None:
-            cfg = (0, 0, -1) if torch.cuda.is_current_stream_capturing() else _tune_conv(
+            # (deterministic mode: a find-db entry or the shape heuristic, never a timing - timed picks differ
+            # between processes, and different kernels round differently)
+            cfg = (0, 0, -1) if (torch.cuda.is_current_stream_capturing() or _common.DETERMINISTIC) else _tune_conv(
                 A, B, out, stats, bias, geo, dh, dw, tb, zero, addend, bwd, groups, scales, xa, xf, mask, y2)
             if cfg[0] or cfg[2] >= 0:
                 _STAGES_TUNED[key] = cfg
