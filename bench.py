@@ -71,9 +71,10 @@ def parse():
                    help="replay the whole training step as one captured HIP graph (at N > 1: forward + backward, "
                         "then one flat gradient all-reduce and Adam); auto = on "
                         "at per-GPU batch <= 64 (host-bound steps, train.py --hip-graph auto)")
-    p.add_argument("--dtype", default="bf16", choices=["bf16"],
-                   help="compute dtype (bf16).  MX-FP8 is not a benchmark configuration: forward-only fp8 "
-                        "measured no speed-up over bf16 (README, BASELINE.md config 5)")
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
+                   help="compute dtype: bf16 (the headline), or fp8 = the experimental MX-FP8 forward convolutions "
+                        "(e4m3 operands with block scales, bf16 backward; BASELINE.json config 5).  fp8 measured no "
+                        "speed-up over bf16 (README, BASELINE.md), and its JSON line says what ran")
     p.add_argument("--data", default="device", choices=["device", "host"],
                    help="device: batches generated once in HBM (the step alone); host: pinned uint8 host batches "
                         "copied by hipMemcpyAsync on a copy stream and normalised on the GPU inside the timed loop "
@@ -295,7 +296,8 @@ def main():
             "n_gpus": ctx.world_size, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": round(value / base, 4) if base else None,
-            "dtype": a.dtype if a.device == "cuda" else "fp32 (cpu rehearsal, not a benchmark)",
+            "dtype": (("fp8 (MX-FP8 e4m3 forward convolutions, bf16 backward and BN)" if a.dtype == "fp8" else a.dtype)
+                      if a.device == "cuda" else "fp32 (cpu rehearsal, not a benchmark)"),
             "data": ("synthetic (on-device random images, random-init weights)" if a.data == "device" else
                      "synthetic (pinned uint8 host batches, H2D copy + normalisation in the timed loop, "
                      "random-init weights)"),
