@@ -131,3 +131,23 @@ def test_hip_bf16_learns_like_torch_fp32(model, size, steps, batch, lr):
     # that swing: Inception-v3 landed at 0.43 against the reference's 0.78 with its loss curve inside the band,
     # r16e - the bound is the swing's width, and the chance-level check above stays)
     assert acc_h > acc_t - 0.4, msg
+
+
+def test_hip_fp8_forward_learns_like_torch_fp32():
+    """BASELINE config 5's compute mode (``--dtype fp8``: MX-FP8 e4m3 forward convolutions with block scales, bf16
+    backward) learns like the fp32 reference stack: ResNet-18 at 64 px, the band of the bf16 test above."""
+    steps, batch, size = 150, 64, 64
+    train = _data(max(steps * batch // 3, 4 * batch), size, seed=11)
+    val = _data(256, size, seed=12)
+    lh, acc_h = _run("resnet18", size, "hip", "fp8", steps, batch, 1e-3, train, val, det=True)
+    lt, acc_t = _run("resnet18", size, "torch", "fp32", steps, batch, 1e-3, train, val)
+    w = steps // 5
+    head_h, tail_h = lh[:w].mean().item(), lh[-w:].mean().item()
+    msg = f"resnet18 fp8: hip loss {head_h:.3f} -> {tail_h:.3f} acc {acc_h:.2f}; torch fp32 acc {acc_t:.2f}"
+    print(msg)
+    assert torch.isfinite(lh).all(), msg
+    assert tail_h < 0.65 * head_h and acc_h > 0.35, msg
+    for k in range(0, steps - w + 1, w):
+        a, b = lh[k:k + w].mean().item(), lt[k:k + w].mean().item()
+        assert abs(a - b) < max(0.25, 0.4 * b), (k, a, b, msg)
+    assert acc_h > acc_t - 0.4, msg
