@@ -231,6 +231,11 @@ def main():
     t_host = time.perf_counter() - t_host
     _sync(ctx.device)
     print(f"[bench] rank {ctx.rank}: host enqueue {t_host * 1e3:.1f} ms/step", file=sys.stderr, flush=True)
+    if a.compute == "hip" and ctx.device.type == "cuda":
+        from pytorch_imageclassification_distributed_amd.ops import hip as _h
+        # shapes the find-db did not cover were timed during warmup: their picks can differ between processes
+        print(f"[bench] rank {ctx.rank}: timed at run time (not in the find-db): {len(_h.TUNE_LOG)} conv, "
+              f"{len(_h.WGRAD_TUNE_LOG)} weight-gradient shapes", file=sys.stderr, flush=True)
     if not torch.isfinite(last).item():
         raise FloatingPointError(f"non-finite loss in warmup: {last.item()}")
     comm_t = None
