@@ -36,9 +36,11 @@ int rccl_comm_close(int64_t, bool);
 // ---- launcher prototypes (defined in *.hip) ----
 int bn_partials_launch(float*, int, int, double*, float*, float*, double, hipStream_t);
 int bn_fin_bwd_launch(float*, int, int, long, double, float*, float*, const bf16_t*, const bf16_t*, const float*,
-                      const bf16_t*, const bf16_t*, bf16_t*, int, int, unsigned*, hipStream_t);
+                      const bf16_t*, const bf16_t*, bf16_t*, int, int, unsigned*, hipStream_t, int /* ldy */,
+                      int /* ldd */);
 int bn_fin_apply_launch(const bf16_t*, bf16_t*, float*, int, int, long, double, const float*, const float*, float*, float*,
-                        long long*, float, float, float*, const float*, int, int, int, unsigned*, hipStream_t);
+                        long long*, float, float, float*, const float*, int, int, int, unsigned*, hipStream_t,
+                        int /* ldy */, int /* ldp */);
 int bn_reduce_finalize_launch(float*, int, int, double, const float*, const float*, float*, float*, long long*, float,
                               float, float*, const float*, hipStream_t);
 int bn_reduce_bwd_launch(float*, int, int, double, float*, float*, float*, const float*, float*, hipStream_t);
@@ -49,7 +51,7 @@ int bn_eval_coef_launch(const float*, const float*, const float*, const float*, 
 int bn_apply_launch(const bf16_t*, const float*, const bf16_t*, bf16_t*, long, int, int, int, int, uint8_t*, uint8_t*,
                     uint8_t* /* mask */, const float* /* res_coef: the residual is a deferred BN's input */, hipStream_t);
 int bn_bwd_reduce_launch(const bf16_t*, const bf16_t*, const float*, const bf16_t*, bf16_t*, long, int, int,
-                         float*, int, int, hipStream_t);
+                         float*, int, int, hipStream_t, int /* ldy */);
 int bn_bwd_k_launch(const double*, const double*, double, int, float*, hipStream_t);
 int bn_bwd_elemt_launch(const bf16_t*, const bf16_t*, const float*, const float*, const bf16_t*, const bf16_t*,
                         bf16_t*, long, int, int, int, hipStream_t);
@@ -436,35 +438,43 @@ void bn_reduce_finalize(Tensor part, int G, int C, double count, OT gamma, OT be
         "bn_reduce_finalize");
 }
 
+// elements from t's first element to the end of its storage (a channel slice indexes past its own numel)
+int64_t extent(const Tensor& t) { return (int64_t)(t.storage().nbytes() / t.element_size()) - t.storage_offset(); }
+
 // training BN forward of a small tensor in one launch: partial-row reduce + finalize (coef, running statistics,
 // re-zeroed rows) + apply into out[:, c_off : c_off + C] (row stride ldo); ctr: >= ceil(C / 64) zeroed int32
+// ldy / ldp (0 = C): row strides of y and of the partial rows - a channel slice of a wider GEMM output
 void bn_fin_apply(Tensor y, Tensor part, int G, double count, OT gamma, OT beta, OT rmean, OT rvar, OT nbt,
                   double momentum, double eps, Tensor coef, OT shift, Tensor out, long rows, int C, int ldo, int c_off,
-                  int act, Tensor ctr) {
+                  int act, Tensor ctr, int ldy, int ldp) {
   req(part, F32, "part"); req(coef, F32, "coef");
   TORCH_CHECK(y.scalar_type() == BF && out.scalar_type() == BF && ctr.scalar_type() == torch::kInt32,
               "bn_fin_apply: dtypes");
-  TORCH_CHECK(part.numel() >= (int64_t)G * 2 * C && coef.numel() >= 4 * C && y.numel() == rows * C &&
-                  out.numel() >= rows * ldo && ldo >= c_off + C && ctr.numel() >= (C + 63) / 64,
+  const int64_t ly = ldy > 0 ? ldy : C, lp = ldp > 0 ? ldp : C;
+  TORCH_CHECK(extent(part) >= ((int64_t)G * 2 - 1) * lp + C && coef.numel() >= 4 * C &&
+                  extent(y) >= (rows - 1) * ly + C && out.numel() >= rows * ldo && ldo >= c_off + C &&
+                  ctr.numel() >= (C + 63) / 64,
               "bn_fin_apply: buffer sizes");
   for (const OT* t : {&gamma, &beta, &rmean, &rvar, &shift})
     TORCH_CHECK(!t->has_value() || !(*t)->defined() || (*t)->numel() >= C, "bn_fin_apply: per-channel sizes");
   check(bn_fin_apply_launch(ptr<bf16_t>(y), ptr<bf16_t>(out), ptr<float>(part), G, C, rows, count, optr<float>(gamma),
                             optr<float>(beta), optr<float>(rmean), optr<float>(rvar), optr<long long>(nbt),
                             (float)momentum, (float)eps, ptr<float>(coef), optr<float>(shift), ldo, c_off, act,
-                            reinterpret_cast<unsigned*>(ctr.data_ptr()), cur()),
+                            reinterpret_cast<unsigned*>(ctr.data_ptr()), cur(), ldy, ldp),
         "bn_fin_apply");
 }
 
 // training BN backward of a small tensor in one launch: partial-row reduce (dgamma, dbeta; rows re-zeroed) +
 // bn_bwd_elemt (g / dz_in / res / act / ldg as there); ctr: >= ceil(C / 64) zeroed int32
+// ldy / ldd (0 = C): row strides of y and dy (channel slices of a wider GEMM's output and of its gradient)
 void bn_fin_bwd(Tensor part, int G, double count, OT dgamma, OT dbeta, OT g, Tensor y, Tensor coef, OT res, OT dz_in,
-                Tensor dy, long rows, int C, int act, int ldg, Tensor ctr) {
+                Tensor dy, long rows, int C, int act, int ldg, Tensor ctr, int ldy, int ldd) {
   req(part, F32, "part"); req(coef, F32, "coef");
   TORCH_CHECK(y.scalar_type() == BF && dy.scalar_type() == BF && ctr.scalar_type() == torch::kInt32,
               "bn_fin_bwd: dtypes");
-  TORCH_CHECK(part.numel() >= (int64_t)G * 2 * C && coef.numel() >= 4 * C && y.numel() == rows * C &&
-                  dy.numel() == rows * C && ctr.numel() >= (C + 63) / 64,
+  const int64_t ly = ldy > 0 ? ldy : C, ld = ldd > 0 ? ldd : C;
+  TORCH_CHECK(part.numel() >= (int64_t)G * 2 * C && coef.numel() >= 4 * C && extent(y) >= (rows - 1) * ly + C &&
+                  extent(dy) >= (rows - 1) * ld + C && ctr.numel() >= (C + 63) / 64,
               "bn_fin_bwd: buffer sizes");
   const int lg = ldg > 0 ? ldg : C;
   // (g may be a channel slice of a concat gradient, row stride ldg: check the storage it indexes)
@@ -477,7 +487,7 @@ void bn_fin_bwd(Tensor part, int G, double count, OT dgamma, OT dbeta, OT g, Ten
     TORCH_CHECK(!t->has_value() || !(*t)->defined() || (*t)->numel() >= C, "bn_fin_bwd: dgamma / dbeta size");
   check(bn_fin_bwd_launch(ptr<float>(part), G, C, rows, count, optr<float>(dgamma), optr<float>(dbeta),
                           optr<bf16_t>(g), ptr<bf16_t>(y), ptr<float>(coef), optr<bf16_t>(res), optr<bf16_t>(dz_in),
-                          ptr<bf16_t>(dy), act, ldg, reinterpret_cast<unsigned*>(ctr.data_ptr()), cur()),
+                          ptr<bf16_t>(dy), act, ldg, reinterpret_cast<unsigned*>(ctr.data_ptr()), cur(), ldy, ldd),
         "bn_fin_bwd");
 }
 
@@ -537,12 +547,15 @@ void bn_apply(Tensor y, Tensor coef, OT res, Tensor out, long rows, int C, int l
 }
 
 // ldg: row stride (elements) of g - a channel slice of a wider NHWC gradient (concat backward); 0 = C
+// ldy (0 = C): y's row stride (a channel slice of a wider GEMM output; reduce only, no res / dz_out)
 void bn_bwd_reduce(Tensor g, Tensor y, Tensor coef, OT res, OT dz_out, long rows, int C, int act, Tensor part,
-                   int G, int ldg) {
+                   int G, int ldg, int ldy) {
   req(g, BF, "g"); req(y, BF, "y");
   TORCH_CHECK(ldg == 0 || (ldg >= C && ldg % 8 == 0), "bn_bwd_reduce: bad ldg");
+  TORCH_CHECK(ldy == 0 || ldy == C || (ldy > C && ldy % 8 == 0 && extent(y) >= (rows - 1) * (int64_t)ldy + C),
+              "bn_bwd_reduce: bad ldy");
   check(bn_bwd_reduce_launch(ptr<bf16_t>(g), ptr<bf16_t>(y), ptr<float>(coef), optr<bf16_t>(res),
-                             optr<bf16_t>(dz_out), rows, C, act, ptr<float>(part), G, ldg, cur()),
+                             optr<bf16_t>(dz_out), rows, C, act, ptr<float>(part), G, ldg, cur(), ldy),
         "bn_bwd_reduce");
 }
 
@@ -1165,7 +1178,7 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("mask") = pybind11::none(), pybind11::arg("res_coef") = pybind11::none());
   m.def("bn_bwd_reduce", &bn_bwd_reduce, pybind11::arg("g"), pybind11::arg("y"), pybind11::arg("coef"), pybind11::arg("res"),
         pybind11::arg("dz_out"), pybind11::arg("rows"), pybind11::arg("C"), pybind11::arg("act"), pybind11::arg("part"), pybind11::arg("G"),
-        pybind11::arg("ldg") = 0);
+        pybind11::arg("ldg") = 0, pybind11::arg("ldy") = 0);
   m.def("bn_bwd_k", &bn_bwd_k);
   m.def("bn_bwd_elemt", &bn_bwd_elemt, pybind11::arg("g"), pybind11::arg("y"), pybind11::arg("coef"), pybind11::arg("k"), pybind11::arg("res"),
         pybind11::arg("dz_in"), pybind11::arg("dy"), pybind11::arg("rows"), pybind11::arg("C"), pybind11::arg("act"), pybind11::arg("ldg") = 0);
@@ -1201,8 +1214,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_act_maxpool", &bn_act_maxpool);
   m.def("bn_set_unroll", [](bool v) { bn_set_unroll(v ? 1 : 0); });
   m.def("bn_res_coef_ok", &bn_res_coef_ok);
-  m.def("bn_fin_apply", &bn_fin_apply);
-  m.def("bn_fin_bwd", &bn_fin_bwd);
+  m.def("bn_fin_apply", &bn_fin_apply, py::arg("y"), py::arg("part"), py::arg("G"), py::arg("count"), py::arg("gamma"),
+        py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("nbt"), py::arg("momentum"), py::arg("eps"),
+        py::arg("coef"), py::arg("shift"), py::arg("out"), py::arg("rows"), py::arg("C"), py::arg("ldo"),
+        py::arg("c_off"), py::arg("act"), py::arg("ctr"), py::arg("ldy") = 0, py::arg("ldp") = 0);
+  m.def("bn_fin_bwd", &bn_fin_bwd, py::arg("part"), py::arg("G"), py::arg("count"), py::arg("dgamma"), py::arg("dbeta"),
+        py::arg("g"), py::arg("y"), py::arg("coef"), py::arg("res"), py::arg("dz_in"), py::arg("dy"), py::arg("rows"),
+        py::arg("C"), py::arg("act"), py::arg("ldg"), py::arg("ctr"), py::arg("ldy") = 0, py::arg("ldd") = 0);
   // a stream whose kernels may only occupy the CUs set in ``mask`` (32 per word; ops/_hip/streams.py
   // IMGCLS_WGRAD_CU_FRAC: the weight-gradient side stream on a subset, the compute stream keeps the rest)
   m.def("cu_mask_stream", [](int device, std::vector<uint32_t> mask) -> uintptr_t {

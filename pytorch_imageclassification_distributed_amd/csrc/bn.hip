@@ -163,12 +163,15 @@ __global__ __launch_bounds__(256) void bn_reduce_bwd_kernel(float* part, int G, 
 // block ever waits for another.
 constexpr int BN_FIN_U = 4;
 
+// ldy / ldp: row strides of y and of the partial rows (C, or the width of a concatenated-sibling GEMM whose channel
+// slice this BN normalises: ops/_hip/convbn.py SiblingBNFn)
 struct BnFinApplyArgs {
   const bf16_t* y; bf16_t* out; float* part; int G, C; long rows; double count;
   const float* gamma; const float* beta; float* rmean; float* rvar; long long* nbt;
   float momentum, eps; float* coef; const float* shift;
   int ldo, c_off;
   unsigned* ctr;
+  int ldy, ldp;
 };
 
 template <int ACT>
@@ -184,9 +187,9 @@ __global__ __launch_bounds__(256) void bn_fin_apply_kernel(BnFinApplyArgs a) {
   if (c < C) {
 #pragma unroll 4
     for (int g = lg; g < a.G; g += 4) {
-      const float* r = a.part + (size_t)g * 2 * C;
+      const float* r = a.part + (size_t)g * 2 * a.ldp;
       s += (double)r[c];
-      q += (double)r[C + c];
+      q += (double)r[a.ldp + c];
     }
   }
   red[0][lg][lc] = s;
@@ -231,9 +234,9 @@ __global__ __launch_bounds__(256) void bn_fin_apply_kernel(BnFinApplyArgs a) {
     if (blockIdx.y == 0 && threadIdx.x == 0 && a.nbt) *a.nbt += 1;
     if (c < C) {
       for (int g = lg; g < a.G; g += 4) {
-        float* r = a.part + (size_t)g * 2 * C;
+        float* r = a.part + (size_t)g * 2 * a.ldp;
         r[c] = 0.f;
-        r[C + c] = 0.f;
+        r[a.ldp + c] = 0.f;
       }
     }
     if (threadIdx.x == 0) a.ctr[blockIdx.y] = 0u;
@@ -256,7 +259,7 @@ __global__ __launch_bounds__(256) void bn_fin_apply_kernel(BnFinApplyArgs a) {
 #pragma unroll
     for (int u = 0; u < BN_FIN_U; ++u) {
       const long r = row + u * step < a.rows ? row + u * step : row;
-      yv[u] = *(const uint4*)(a.y + r * C + c0);
+      yv[u] = *(const uint4*)(a.y + r * a.ldy + c0);
     }
 #pragma unroll
     for (int u = 0; u < BN_FIN_U; ++u) {
@@ -282,6 +285,7 @@ struct BnFinBwdArgs {
   const bf16_t* g; const bf16_t* y; const float* coef; const bf16_t* res; const bf16_t* dz_in; bf16_t* dy;
   int ldg;
   unsigned* ctr;
+  int ldy, ldd;  // row strides of y and dy (C, or a concatenated-sibling GEMM's width)
 };
 
 template <int MODE, int ACT>
@@ -352,7 +356,7 @@ __global__ __launch_bounds__(256) void bn_fin_bwd_kernel(BnFinBwdArgs a) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const long r = row0 + u * step < a.rows ? row0 + u * step : row0;
-      yl[u] = *(const uint4*)(a.y + r * C + c0);
+      yl[u] = *(const uint4*)(a.y + r * a.ldy + c0);
       gl[u] = MODE == 0 ? *(const uint4*)(a.dz_in + r * C + c0) : *(const uint4*)(a.g + r * a.ldg + c0);
       if constexpr (MODE == 2) rl2[u] = *(const uint4*)(a.res + r * C + c0);
     }
@@ -380,7 +384,7 @@ __global__ __launch_bounds__(256) void bn_fin_bwd_kernel(BnFinBwdArgs a) {
       const float xhat = (yv[k] - mu[k]) * is[k];
       gv[k] = sc[k] * (gv[k] - k1[k] - xhat * k2[k]);
     }
-    *(uint4*)(a.dy + row * C + c0) = pack8(gv);
+    *(uint4*)(a.dy + row * a.ldd + c0) = pack8(gv);
     }
   }
 }
@@ -848,7 +852,7 @@ __global__ void bn_act_maxpool32_kernel(const bf16_t* __restrict__ y, const floa
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     const bf16_t* __restrict__ g, const bf16_t* __restrict__ y, const float* __restrict__ coef,
     const bf16_t* __restrict__ res, bf16_t* __restrict__ dz_out, long rows, int C, int act,
-    long rows_per_block, float* __restrict__ part, int G, int ldg, int CHB) {
+    long rows_per_block, float* __restrict__ part, int G, int ldg, int CHB, int ldy) {
   __shared__ float red[2][256][9];
   const int cch = C >> 3;
   const int RP = 256 / CHB;
@@ -873,7 +877,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     for (long row = rbeg + lr; row < rend; row += RP) {
       float gv[8], yv[8], rv[8];
       unpack8(*(const uint4*)(g + row * ldg + c0), gv);
-      unpack8(*(const uint4*)(y + row * C + c0), yv);
+      unpack8(*(const uint4*)(y + row * ldy + c0), yv);
       if (res) unpack8(*(const uint4*)(res + row * C + c0), rv);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -919,7 +923,7 @@ template <int FL, bool NT>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_u_kernel(
     const bf16_t* __restrict__ g, const bf16_t* __restrict__ y, const float* __restrict__ coef,
     const bf16_t* __restrict__ res, bf16_t* __restrict__ dz_out, long rows, int C, int act,
-    long rows_per_block, float* __restrict__ part, int G, int ldg, int CHB) {
+    long rows_per_block, float* __restrict__ part, int G, int ldg, int CHB, int ldy) {
   constexpr bool RES = FL & 1, ACT = FL & 2, DZ = FL & 4;
   constexpr int ACTC = (FL & 8) ? ACT_SILU : ACT_RELU;  // (bit 3: SiLU) the activation as a constant
   __shared__ float red[2][256][9];
@@ -951,7 +955,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_u_kernel(
       for (int u = 0; u < BN_U; ++u) {
         const long r = row + u * rstep < rend ? row + u * rstep : row;  // clamped rows load, never count
         gr[u] = ldrow<NT>(g + r * ldg + c0);
-        yr[u] = ldrow<NT>(y + r * C + c0);
+        yr[u] = ldrow<NT>(y + r * ldy + c0);
         if constexpr (RES) rr[u] = ldrow<NT>(res + r * C + c0);
       }
 #pragma unroll
@@ -1309,10 +1313,12 @@ static int g_fin_blocks = getenv("IMGCLS_BN_FIN_BLOCKS") ? atoi(getenv("IMGCLS_B
 int bn_fin_apply_launch(const bf16_t* y, bf16_t* out, float* part, int G, int C, long rows, double count,
                         const float* gamma, const float* beta, float* rmean, float* rvar, long long* nbt,
                         float momentum, float eps, float* coef, const float* shift, int ldo, int c_off, int act,
-                        unsigned* ctr, hipStream_t s) {
-  if (C % 8 || rows <= 0 || G < 1 || ldo < c_off + C) return 2;
+                        unsigned* ctr, hipStream_t s, int ldy, int ldp) {
+  ldy = ldy > 0 ? ldy : C;
+  ldp = ldp > 0 ? ldp : C;
+  if (C % 8 || ldy % 8 || ldy < C || ldp < C || rows <= 0 || G < 1 || ldo < c_off + C) return 2;
   const BnFinApplyArgs a{y, out, part, G, C, rows, count, gamma, beta, rmean, rvar, nbt, momentum, eps, coef, shift,
-                         ldo, c_off, ctr};
+                         ldo, c_off, ctr, ldy, ldp};
   long bx = (rows + 127) / 128;
   bx = bx > g_fin_blocks ? g_fin_blocks : bx;
   const dim3 grid((unsigned)bx, (unsigned)cdiv(C, 64));
@@ -1330,11 +1336,15 @@ int bn_fin_apply_launch(const bf16_t* y, bf16_t* out, float* part, int G, int C,
 
 int bn_fin_bwd_launch(float* part, int G, int C, long rows, double count, float* dgamma, float* dbeta,
                       const bf16_t* g, const bf16_t* y, const float* coef, const bf16_t* res, const bf16_t* dz_in,
-                      bf16_t* dy, int act, int ldg, unsigned* ctr, hipStream_t s) {
-  if (C % 8 || rows <= 0 || G < 1) return 2;
+                      bf16_t* dy, int act, int ldg, unsigned* ctr, hipStream_t s, int ldy, int ldd) {
+  ldy = ldy > 0 ? ldy : C;
+  ldd = ldd > 0 ? ldd : C;
+  if (C % 8 || ldy % 8 || ldd % 8 || ldy < C || ldd < C || rows <= 0 || G < 1) return 2;
   const int mode = dz_in ? 0 : act == ACT_NONE ? 3 : res ? 2 : 1;
   if (mode != 0 && !g) return 2;
-  const BnFinBwdArgs a{part, G, C, rows, count, dgamma, dbeta, g, y, coef, res, dz_in, dy, ldg > 0 ? ldg : C, ctr};
+  if ((mode == 0 || mode == 2) && (ldy != C || ldd != C)) return 2;  // (dz_in / res rows are dense)
+  const BnFinBwdArgs a{part, G, C, rows, count, dgamma, dbeta, g, y, coef, res, dz_in, dy, ldg > 0 ? ldg : C, ctr,
+                       ldy, ldd};
   long bx = (rows + 127) / 128;
   bx = bx > g_fin_blocks ? g_fin_blocks : bx;
   const dim3 grid((unsigned)bx, (unsigned)cdiv(C, 64));
@@ -1458,12 +1468,15 @@ int bn_apply_launch(const bf16_t* y, const float* coef, const bf16_t* res, bf16_
 }
 
 int bn_bwd_reduce_launch(const bf16_t* g, const bf16_t* y, const float* coef, const bf16_t* res,
-                         bf16_t* dz_out, long rows, int C, int act, float* part, int G, int ldg, hipStream_t s) {
+                         bf16_t* dz_out, long rows, int C, int act, float* part, int G, int ldg, hipStream_t s,
+                         int ldy) {
   const RedGrid rg = reduce_grid(rows, C);
   const int ld = ldg > 0 ? ldg : C;
+  ldy = ldy > 0 ? ldy : C;
+  if (ldy != C && (res || dz_out || ldy % 8 || ldy < C)) return 2;  // (a strided y: reduce only)
   if (!g_bn_unroll) {
     hipLaunchKernelGGL(bn_bwd_reduce_kernel, rg.grid, dim3(256), 0, s, g, y, coef, res, dz_out, rows, C, act,
-                       rg.rpb, part, G, ld, rg.chb);
+                       rg.rpb, part, G, ld, rg.chb, ldy);
     HIP_CHECK_LAUNCH();
     return 0;
   }
@@ -1475,10 +1488,10 @@ int bn_bwd_reduce_launch(const bf16_t* g, const bf16_t* y, const float* coef, co
   case F:                                                                                                    \
     if (nt)                                                                                                  \
       hipLaunchKernelGGL((bn_bwd_reduce_u_kernel<F, true>), rgw.grid, dim3(256), 0, s, g, y, coef, res, dz_out, \
-                         rows, C, act, rgw.rpb, part, G, ld, rgw.chb);                                       \
+                         rows, C, act, rgw.rpb, part, G, ld, rgw.chb, ldy);                                  \
     else                                                                                                     \
       hipLaunchKernelGGL((bn_bwd_reduce_u_kernel<F, false>), rgw.grid, dim3(256), 0, s, g, y, coef, res,       \
-                         dz_out, rows, C, act, rgw.rpb, part, G, ld, rgw.chb);                               \
+                         dz_out, rows, C, act, rgw.rpb, part, G, ld, rgw.chb, ldy);                          \
     break;
   switch (fl) {
     BWDRED(0) BWDRED(2) BWDRED(3) BWDRED(4) BWDRED(6) BWDRED(7) BWDRED(10) BWDRED(11) BWDRED(14) BWDRED(15)

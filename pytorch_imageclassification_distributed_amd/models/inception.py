@@ -39,6 +39,11 @@ class BasicConv2d(nn.Module):
                               pool=pool, prepool=prepool, defer_act=defer)
 
 
+def _pairs(mods):
+    """(conv, bn) of BasicConv2d modules (the sibling 1x1 heads of an Inception block)."""
+    return [(m.conv, m.bn) for m in mods]
+
+
 class InceptionA(nn.Module):
     def __init__(self, cin, pool_features):
         super().__init__()
@@ -51,12 +56,18 @@ class InceptionA(nn.Module):
         self.branch_pool = BasicConv2d(cin, pool_features, kernel_size=1)
 
     def forward(self, x):
-        s = Fx.grad_slot(x, 4)  # x feeds three convs and the pool: summed inside their backward kernels
         cat = Fx.concat_buffer([64, 64, 96, self.branch_pool.conv.out_channels])  # branches write in place
-        b1 = self.branch1x1(x, slot=s, out=(cat, 0))
-        b5 = self.branch5x5_2(self.branch5x5_1(x, slot=s), True, out=(cat, 1))
-        b3 = self.branch3x3dbl_3(self.branch3x3dbl_2(self.branch3x3dbl_1(x, slot=s, defer=True), True), True,
-                                 out=(cat, 2))
+        heads = [self.branch1x1, self.branch5x5_1, self.branch3x3dbl_1]
+        if Fx.siblings_ok(x, _pairs(heads)):  # the three 1x1 heads as one GEMM (HIP path, small steps)
+            s = Fx.grad_slot(x, 2)
+            b1, t5, t3 = Fx.conv_bn_act_siblings(x, _pairs(heads), [(cat, 0), None, None], x_slot=s)
+        else:
+            s = Fx.grad_slot(x, 4)  # x feeds three convs and the pool: summed inside their backward kernels
+            b1 = self.branch1x1(x, slot=s, out=(cat, 0))
+            t5 = self.branch5x5_1(x, slot=s)
+            t3 = self.branch3x3dbl_1(x, slot=s, defer=True)
+        b5 = self.branch5x5_2(t5, True, out=(cat, 1))
+        b3 = self.branch3x3dbl_3(self.branch3x3dbl_2(t3, True), True, out=(cat, 2))
         bp = self.branch_pool(x, slot=s, prepool=(3, 1, 1), out=(cat, 3))
         return Fx.cat_channels([b1, b5, b3, bp], cat)
 
@@ -95,13 +106,18 @@ class InceptionC(nn.Module):
         self.branch_pool = BasicConv2d(cin, 192, kernel_size=1)
 
     def forward(self, x):
-        s = Fx.grad_slot(x, 4)
         cat = Fx.concat_buffer([192, 192, 192, 192])
-        b1 = self.branch1x1(x, slot=s, out=(cat, 0))
-        # chain-internal outputs are deferred (their consumer applies BN + ReLU; c7 = 160 materialises them)
-        b7 = self.branch7x7_1(x, slot=s, defer=True)
+        heads = [self.branch1x1, self.branch7x7_1, self.branch7x7dbl_1]
+        if Fx.siblings_ok(x, _pairs(heads)):  # the three 1x1 heads as one GEMM (HIP path, small steps)
+            s = Fx.grad_slot(x, 2)
+            b1, b7, bd = Fx.conv_bn_act_siblings(x, _pairs(heads), [(cat, 0), None, None], x_slot=s)
+        else:
+            s = Fx.grad_slot(x, 4)
+            b1 = self.branch1x1(x, slot=s, out=(cat, 0))
+            # chain-internal outputs are deferred (their consumer applies BN + ReLU; c7 = 160 materialises them)
+            b7 = self.branch7x7_1(x, slot=s, defer=True)
+            bd = self.branch7x7dbl_1(x, slot=s, defer=True)
         b7 = self.branch7x7_3(self.branch7x7_2(b7, True, defer=True), True, out=(cat, 1))
-        bd = self.branch7x7dbl_1(x, slot=s, defer=True)
         bd = self.branch7x7dbl_3(self.branch7x7dbl_2(bd, True, defer=True), True, defer=True)
         bd = self.branch7x7dbl_5(self.branch7x7dbl_4(bd, True, defer=True), True, out=(cat, 2))
         bp = self.branch_pool(x, slot=s, prepool=(3, 1, 1), out=(cat, 3))
@@ -142,13 +158,19 @@ class InceptionE(nn.Module):
         self.branch_pool = BasicConv2d(cin, 192, kernel_size=1)
 
     def forward(self, x):
-        s = Fx.grad_slot(x, 4)
         cat = Fx.concat_buffer([320, 384, 384, 384, 384, 192])
-        b1 = self.branch1x1(x, slot=s, out=(cat, 0))
-        b3 = self.branch3x3_1(x, slot=s)
+        heads = [self.branch1x1, self.branch3x3_1, self.branch3x3dbl_1]
+        if Fx.siblings_ok(x, _pairs(heads)):  # the three 1x1 heads as one GEMM (HIP path, small steps)
+            s = Fx.grad_slot(x, 2)
+            b1, b3, td = Fx.conv_bn_act_siblings(x, _pairs(heads), [(cat, 0), None, None], x_slot=s)
+        else:
+            s = Fx.grad_slot(x, 4)
+            b1 = self.branch1x1(x, slot=s, out=(cat, 0))
+            b3 = self.branch3x3_1(x, slot=s)
+            td = self.branch3x3dbl_1(x, slot=s, defer=True)
         s3 = Fx.grad_slot(b3)  # b3 and bd each feed exactly two convs: paired gradient slots
         b3a, b3b = self.branch3x3_2a(b3, slot=s3, out=(cat, 1)), self.branch3x3_2b(b3, slot=s3, out=(cat, 2))
-        bd = self.branch3x3dbl_2(self.branch3x3dbl_1(x, slot=s, defer=True), True)
+        bd = self.branch3x3dbl_2(td, True)
         sd = Fx.grad_slot(bd)
         bda, bdb = self.branch3x3dbl_3a(bd, slot=sd, out=(cat, 3)), self.branch3x3dbl_3b(bd, slot=sd, out=(cat, 4))
         bp = self.branch_pool(x, slot=s, prepool=(3, 1, 1), out=(cat, 5))

@@ -16,11 +16,11 @@ from ..grad_arena import arena_slot, grad_buffer
 from . import common as _common
 from . import shadows as _shadows
 from . import gemm as _gemm
-from .common import ACT, BF16, C, CL, _cl, _empty_cl, _sync_group, stat_groups, stat_shift, ws
+from .common import ACT, BF16, C, CL, SHIFT_STATS, _cl, _empty_cl, _sync_group, stat_groups, stat_shift, ws
 from .shadows import FP8, ensure_channels_last_weight, weight_bf16, weight_bf16_t
 from .gemm import (ConvGeom, _wgrad_plan, conv_dgrad_raw, conv_forward_raw, conv_fused_bwd_raw, conv_geom,
                    fused_bwd_eligible)
-from .streams import conv_wgrad_raw
+from .streams import _on_side, conv_wgrad_raw
 from .pool import AvgPoolFn, _pool_args, avg_pool2d, channel_slice_stride, max_pool2d
 
 
@@ -1042,6 +1042,181 @@ def conv_bn_act(x, conv, bn, act, residual, x_slot=None, res_slot=None, exclusiv
     return res_out
 
 
+# Sibling 1x1 convs sharing one input (Inception's branch heads: InceptionA 64 + 48 + 64, InceptionC 192 + c7 + c7,
+# InceptionE 320 + 384 + 448) as ONE implicit GEMM with their output channels concatenated: x is read once by the
+# forward and by the weight gradient, and the data gradient is one K = sum(Co) GEMM.  That replaces three gradient-slot
+# accumulations.  Each branch's BN then normalises its channel slice in place with the one-launch BN kernels (row
+# strides: csrc/bn.hip bn_fin_apply_kernel / bn_fin_bwd_kernel), writing its output where that branch wrote it
+# (a concat slice or its own tensor).  Per block and step this is 2 + 2 x 2 fewer GEMM launches, which is what a
+# step costs at the reference's Inception-v3 b4 launch.  The merged path gives up the per-branch fusions (XA,
+# consumer-epilogue BN reduces) and still wins at every batch measured: b4 +3.5 %, b32 +3.1 %, b256 +2-4 %, b512 +3.9 %
+# (profiles/r16q_*); IMGCLS_SIBLINGS_MAX caps the concatenated output's elements, IMGCLS_SIBLINGS=0 turns it off.
+SIBLINGS = os.environ.get("IMGCLS_SIBLINGS", "1") == "1"
+SIBLINGS_MAX = int(os.environ.get("IMGCLS_SIBLINGS_MAX", str(1 << 30)))
+SIBLINGS_COUNT = [0]
+
+
+def siblings_eligible(x, pairs) -> bool:
+    """Every (conv, bn) is a plain 1x1 stride-1 conv of ``x`` followed by a training BN without SyncBN, and the
+    concatenated output is small enough for the one-launch BN kernels."""
+    if (not SIBLINGS or _common.DETERMINISTIC or _shadows.FP8_FWD or not torch.is_grad_enabled() or x.dim() != 4
+            or x.shape[1] % 8 or getattr(x, "_imgcls_xf", None) is not None):
+        return False
+    co = 0
+    for conv, bn in pairs:
+        if not (bn.training and conv.groups == 1 and conv.bias is None and tuple(conv.kernel_size) == (1, 1)
+                and tuple(conv.stride) == (1, 1) and tuple(conv.padding) == (0, 0) and tuple(conv.dilation) == (1, 1)
+                and not getattr(conv, "tf_same", False) and conv.in_channels == x.shape[1]
+                and conv.out_channels % 8 == 0 and bn.num_features == conv.out_channels
+                and bn.track_running_stats and bn.running_mean is not None and _sync_group(bn) is None):
+            return False
+        co += conv.out_channels
+    n, _, h, w = x.shape
+    return co <= 64 * 64 and n * h * w * co <= SIBLINGS_MAX
+
+
+def _sibling_geom(x, convs) -> ConvGeom:
+    """The 1x1 geometry of the merged GEMM: the first sibling's, with the concatenated output channels."""
+    g0 = conv_geom(x, convs[0])
+    co = sum(c.out_channels for c in convs)
+    cache = convs[0].__dict__.setdefault("_imgcls_sib_geom", {})
+    g = cache.get((x.shape, co))
+    if g is None:
+        g = ConvGeom.__new__(ConvGeom)
+        for k in ConvGeom.__slots__:
+            setattr(g, k, getattr(g0, k))
+        g.Co = co
+        cache[(x.shape, co)] = g
+    return g
+
+
+class SiblingConvFn(torch.autograd.Function):
+    """y = x conv [W_0; W_1; ...] (1x1) with the BN statistics of every output channel in the GEMM epilogue."""
+
+    @staticmethod
+    def forward(ctx, x, slot, convs, shift, *weights):
+        g = _sibling_geom(x, convs)
+        wb = torch.cat([weight_bf16(w) for w in weights])  # [sum Co][Ci]
+        stats = ws(x.device).stats_buf(g.Co, stat_groups(g.N * g.OH * g.OW))
+        y = conv_forward_raw(x, None, g, stats=stats, wb=wb, shift=shift)
+        ctx.g, ctx.slot = g, slot
+        ctx.save_for_backward(x, *weights)
+        SIBLINGS_COUNT[0] += 1
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, *weights = ctx.saved_tensors
+        g = ctx.g
+        dy = _cl(dy)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            wt = torch.cat([weight_bf16_t(w, w.shape[0], 1, g.Ci).view(g.Ci, w.shape[0]) for w in weights], dim=1)
+            slot = ctx.slot
+            addend = slot.t if slot is not None else None  # (the other consumers' sum rides in as the addend)
+            dx = conv_dgrad_raw(dy, None, g, addend=addend, wt=wt.contiguous())
+            if slot is not None:
+                dx = slot.deliver(dx, fused=addend is not None)
+        dws = [None] * len(weights)
+        if any(ctx.needs_input_grad[4:]):
+            m, ntot = g.N * g.OH * g.OW, g.T * g.Cx
+            kps, splits, stages = _wgrad_plan(g, dy, x, m, ntot)
+            for i, w in enumerate(weights):
+                if ctx.needs_input_grad[4 + i]:
+                    dws[i] = grad_buffer(w, zero=False)
+
+            def launch():  # the merged weight gradient, then its split into the siblings' gradient slots
+                full = torch.zeros(g.Co * ntot, dtype=torch.float32, device=dy.device)  # (small splits add atomically)
+                _gemm._wgrad_launch(dy, x, full, g, m, ntot, kps, splits, stages)
+                off = 0
+                for w, d in zip(weights, dws):
+                    if d is not None:
+                        d.copy_(full[off:off + w.numel()].view(w.shape[0], w.shape[1], 1, 1))
+                    off += w.numel()
+            # on the weight-gradient side stream, as every other conv's (joined when backward ends)
+            _on_side(dy.device, launch, dy, x, *[d for d in dws if d is not None])
+        return (dx, None, None, None, *dws)
+
+
+class SiblingBNFn(torch.autograd.Function):
+    """act_i(bn_i(y[:, slice_i])) for every sibling: one launch per BN in each direction, reading its channel slice
+    of the merged GEMM output in place (row stride sum(Co)); outputs go to a concat slice or their own tensor."""
+
+    @staticmethod
+    def forward(ctx, y, bns, acts, outs, shifted, *params):
+        dev = y.device
+        n, ctot, h, w = y.shape
+        rows = n * h * w
+        grp = stat_groups(rows)
+        part = ws(dev).stats_buf(ctot, grp)
+        results, coefs, off = [], [], 0
+        for i, bn in enumerate(bns):
+            c = bn.num_features
+            coef = torch.empty(4 * c, dtype=torch.float32, device=dev)
+            mom = bn.momentum if bn.momentum is not None else 0.1
+            if outs[i] is not None:
+                cbuf, idx = outs[i]
+                dst, ldo, c_off = cbuf.ensure(n, h, w, dev), cbuf.total, cbuf.offs[idx]
+                out = cbuf.part(idx, c)
+            else:
+                out = dst = _empty_cl(n, c, h, w, dev)
+                ldo, c_off = c, 0
+            C.bn_fin_apply(y[:, off:off + c], part[off:], grp, float(rows), params[2 * i], params[2 * i + 1],
+                           bn.running_mean, bn.running_var, bn.num_batches_tracked, mom, bn.eps, coef,
+                           bn.running_mean if shifted else None, dst, rows, c, ldo, c_off, ACT[acts[i]],
+                           ws(dev).fin_ctr, ldy=ctot, ldp=ctot)
+            results.append(out)
+            coefs.append(coef)
+            off += c
+        ctx.bns, ctx.acts = bns, acts
+        ctx.params = params
+        ctx.save_for_backward(y, *coefs)
+        return tuple(results)
+
+    @staticmethod
+    def backward(ctx, *gouts):
+        y, *coefs = ctx.saved_tensors
+        dev = y.device
+        n, ctot, h, w = y.shape
+        rows = n * h * w
+        grp = stat_groups(rows)
+        dy = _empty_cl(n, ctot, h, w, dev)
+        grads, off = [], 0
+        for i, bn in enumerate(ctx.bns):
+            c = bn.num_features
+            gout = gouts[i]
+            if gout is None:
+                gout = torch.zeros((n, c, h, w), dtype=y.dtype, device=dev).contiguous(memory_format=CL)
+            ldg = channel_slice_stride(gout)  # a concat's gradient arrives as a channel slice: read in place
+            g = gout if ldg else _cl(gout)
+            a = ACT[ctx.acts[i]]
+            part = ws(dev).take_part(c, grp)
+            C.bn_bwd_reduce(g, y[:, off:off + c], coefs[i], None, None, rows, c, a, part, grp, ldg, ldy=ctot)
+            dgamma = grad_buffer(ctx.params[2 * i], zero=False)
+            dbeta = grad_buffer(ctx.params[2 * i + 1], zero=False)
+            C.bn_fin_bwd(part, grp, float(rows), dgamma, dbeta, g, y[:, off:off + c], coefs[i], None, None,
+                         dy[:, off:off + c], rows, c, a, ldg, ws(dev).fin_ctr, ldy=ctot, ldd=ctot)
+            ws(dev).give_part(part)
+            grads += [dgamma, dbeta]
+            off += c
+        return (dy, None, None, None, None, *grads)
+
+
+def conv_bn_act_siblings(x, pairs, outs, act="relu", x_slot=None):
+    """[act(bn_i(conv_i(x)))] for sibling 1x1 convs of one input (``siblings_eligible``), as one GEMM; ``outs[i]`` =
+    (ConcatBuffer, branch) or None; ``x_slot``: x's gradient slot (this call is ONE consumer of it)."""
+    x = _cl(x)
+    convs = [c for c, _ in pairs]
+    bns = [b for _, b in pairs]
+    for c in convs:
+        ensure_channels_last_weight(c)
+    shifts = [stat_shift(b) for b in bns]  # (each BN's statistics pivot; the GEMM epilogue sums about their concat)
+    shifted = all(t is not None for t in shifts)
+    y = SiblingConvFn.apply(x, x_slot, convs, torch.cat(shifts) if shifted else None, *[c.weight for c in convs])
+    params = [t for b in bns for t in (b.weight, b.bias)]
+    return list(SiblingBNFn.apply(y, bns, [act] * len(bns), list(outs), shifted, *params))
+
+
 class ConvBiasFn(torch.autograd.Function):
     """Plain convolution with optional bias (no BN)."""
 
@@ -1096,4 +1271,6 @@ _OWNED = (
     '_bn_bwd_k', '_bn_coef', '_dense_geom', '_rep', '_s2d_geom', '_s2d_index', '_syncbn_bwd_start', 'conv',
     'conv_bn_act', 'conv_bn_act_pool', 'dense_conv_eligible', 'input_from_u8', 'materialize_deferred',
     'pool_conv_bn_act', 'stem_s2d_conv', 'stem_s2d_eligible', 'xa_eligible', 'xf_eligible',
+    'SIBLINGS', 'SIBLINGS_COUNT', 'SIBLINGS_MAX', 'SiblingBNFn', 'SiblingConvFn', 'conv_bn_act_siblings',
+    'siblings_eligible',
 )

@@ -594,7 +594,7 @@ def conv_fused_bwd_raw(dz, x, w_param, g: ConvGeom, xa, addend=None, link=None):
     return dx, dw
 
 
-def conv_dgrad_raw(dy, w_param, g: ConvGeom, addend=None, link=None, xa=None, xa_out=None):
+def conv_dgrad_raw(dy, w_param, g: ConvGeom, addend=None, link=None, xa=None, xa_out=None, wt=None):
     """dX = conv_transpose(dY, W) [+ addend], one MFMA GEMM per sub-pixel phase.
 
     With ``link`` (the producer BN of the conv input) the epilogue instead emits
@@ -602,7 +602,8 @@ def conv_dgrad_raw(dy, w_param, g: ConvGeom, addend=None, link=None, xa=None, xa
     With ``xa`` = (y, coef) ``dy`` is the consuming BN's pre-elementwise gradient dz and the kernel
     forms dY = coef0*dz + coef1*y + coef2 on its A-operand loads (1x1 convs, ``XaLink``); with ``xa_out``
     (a tensor shaped like dy) the first column tile also stores that dY, so the weight gradient can read it
-    plainly (``XA_OUT``)."""
+    plainly (``XA_OUT``).  ``wt``: the [Ci][T][Co] bf16 operand itself (concatenated siblings), else
+    ``w_param``'s transposed shadow."""
     dev = dy.device
     bwd = (None, None, None, None, 0, 1)
     mask = None
@@ -613,7 +614,8 @@ def conv_dgrad_raw(dy, w_param, g: ConvGeom, addend=None, link=None, xa=None, xa
         bwd = (link.y, link.res, link.coef, link.part, link.act, grp)
         mask = link.mask
         y2 = _ds_partials(link, g.Ci, grp, dev, g)
-    wt = weight_bf16_t(w_param, g.Co, g.T, g.Ci)
+    if wt is None:
+        wt = weight_bf16_t(w_param, g.Co, g.T, g.Ci)
     dx = _empty_cl(g.N, g.Ci, g.H, g.W, dev)
     for ph, pw, gh, gw, dh, dw, tb in _dgrad_phases(g):
         if gh <= 0 or gw <= 0:

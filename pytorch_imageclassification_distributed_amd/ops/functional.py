@@ -152,6 +152,21 @@ def conv_bn_act(x, conv, bn, act="relu", residual=None, x_slot=None, res_slot=No
     return _act(y, act)
 
 
+def siblings_ok(x, pairs) -> bool:
+    """The HIP path can run these (conv, bn) pairs - 1x1 convs of the same ``x`` - as one GEMM
+    (``conv_bn_act_siblings``); the caller then gives ``x`` one gradient-slot consumer for all of them."""
+    return use_hip(x) and _hip().siblings_eligible(x, pairs)
+
+
+def conv_bn_act_siblings(x, pairs, outs, act="relu", x_slot=None):
+    """[act(bn(conv(x))) for (conv, bn) in pairs] as one concatenated-output GEMM (HIP path, ``siblings_ok``);
+    ``outs[i]`` = (ConcatPlan, branch) writes that result into the concat output in place."""
+    h = _hip()
+    hout = [(o[0].hip(), o[1]) if (o is not None and h.CONCAT_INPLACE) else None for o in outs]
+    res = h.conv_bn_act_siblings(x, pairs, hout, act, x_slot)
+    return res
+
+
 def conv(x, conv_mod):
     """Plain convolution (with optional bias), no normalisation."""
     if use_hip(x):

@@ -54,7 +54,7 @@ def wrap(owner, name, label):
 
 
 for cls in ("ConvFn", "BNActFn", "BNActPoolFn", "MaxPoolFn", "AvgPoolFn", "GapFn", "MlpFn", "CrossEntropyFn", "CatFn",
-            "DropoutFn", "DwConvFn", "SEFn", "AddFn"):
+            "DropoutFn", "DwConvFn", "SEFn", "AddFn", "SiblingConvFn", "SiblingBNFn"):
     c = getattr(hip, cls, None)
     if c is not None:
         wrap(c, "forward", f"{cls}.forward")
@@ -65,7 +65,7 @@ for fn in ("conv_forward_raw", "conv_dgrad_raw", "conv_wgrad_raw", "_conv_gemm",
     if hasattr(hip, fn):
         wrap(hip, fn, fn)
 for fn in ("conv_gemm", "conv_wgrad", "bn_apply", "bn_bwd_elemt", "bn_bwd_reduce", "bn_reduce_finalize",
-           "bn_reduce_bwd", "direct_conv"):
+           "bn_reduce_bwd", "direct_conv", "bn_fin_apply", "bn_fin_bwd"):
     if hasattr(hip.C, fn):
         wrap(hip.C, fn, "C." + fn)
 

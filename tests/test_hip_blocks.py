@@ -240,9 +240,13 @@ def test_inception_block_fusion(kind, expect):
                     "E": (inc.InceptionE(128), 128, 8)}[kind]
     blk = blk.to(DEV).to(memory_format=torch.channels_last)
     x = torch.randn(4, cin, hw, hw, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    gx0, gp0 = _grads(blk, x, False)
-    before = hip.FUSED_BWD_COUNT[0]
-    gx1, gp1 = _grads(blk, x, True)
+    keep_sib, hip.SIBLINGS = hip.SIBLINGS, False  # (the per-branch path: merged sibling heads take no consumer reduce)
+    try:
+        gx0, gp0 = _grads(blk, x, False)
+        before = hip.FUSED_BWD_COUNT[0]
+        gx1, gp1 = _grads(blk, x, True)
+    finally:
+        hip.SIBLINGS = keep_sib
     assert hip.FUSED_BWD_COUNT[0] - before == expect
     err = lambda a, b: ((a - b).abs().max() / b.abs().max().clamp(min=1e-6)).item()  # noqa: E731
     assert err(gx1, gx0) < 3e-2, err(gx1, gx0)
@@ -517,3 +521,50 @@ def test_bn_fin_apply_matches_two_launch_path(kind):
             assert (a_ - b_).abs().max().item() <= 1e-2 * b_.abs().max().item() + 1e-6
         for a_, b_ in zip(r[3], ref[3]):
             assert torch.allclose(a_.float(), b_.float(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("kind", ["A", "C", "E"])
+def test_inception_sibling_heads_merged(kind):
+    """The 1x1 heads of an Inception block as one concatenated-output GEMM with per-slice BN (ops/_hip/convbn.py
+    SiblingConvFn / SiblingBNFn) == the per-branch path: block output, input gradient, every parameter gradient,
+    the BN running statistics and batch counters."""
+    from pytorch_imageclassification_distributed_amd.models import inception as inc
+    from pytorch_imageclassification_distributed_amd.ops import hip
+    torch.manual_seed(0)
+    blk, cin, hw = {"A": (inc.InceptionA(192, 32), 192, 11), "C": (inc.InceptionC(256, 64), 256, 9),
+                    "E": (inc.InceptionE(256), 256, 5)}[kind]
+    blk = blk.to(DEV).to(memory_format=torch.channels_last).train()
+    with torch.no_grad():
+        for m in blk.modules():
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.weight.uniform_(0.5, 1.5)
+                m.bias.uniform_(-0.5, 0.5)
+                m.running_mean.uniform_(-0.2, 0.2)
+    x = torch.randn(4, cin, hw, hw, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    same = _SameState(blk)
+
+    def run(merged):
+        keep, hip.SIBLINGS = hip.SIBLINGS, merged
+        try:
+            same()
+            for p in blk.parameters():
+                p.grad = None
+            n0 = hip.SIBLINGS_COUNT[0]
+            xx = x.clone().requires_grad_(True)
+            out = blk(xx)
+            (out.float() * torch.linspace(-1, 1, out.numel(), device=DEV).view_as(out)).sum().backward()
+            torch.cuda.synchronize()
+            return (out.float(), xx.grad.float(), {n: p.grad.float().clone() for n, p in blk.named_parameters()},
+                    [b.detach().float().clone() for b in blk.buffers()], hip.SIBLINGS_COUNT[0] - n0)
+        finally:
+            hip.SIBLINGS = keep
+
+    ref, mrg = run(False), run(True)
+    assert ref[4] == 0 and mrg[4] == 1
+    err = lambda a, b: ((a - b).abs().max() / b.abs().max().clamp(min=1e-6)).item()  # noqa: E731
+    assert err(mrg[0], ref[0]) < 2e-2, err(mrg[0], ref[0])
+    assert err(mrg[1], ref[1]) < 3e-2, err(mrg[1], ref[1])
+    for n in ref[2]:
+        assert err(mrg[2][n], ref[2][n]) < 3e-2, (n, err(mrg[2][n], ref[2][n]))
+    for a, b in zip(mrg[3], ref[3]):
+        assert torch.allclose(a, b, rtol=1e-3, atol=1e-4)
