@@ -1438,8 +1438,9 @@ def test_resnet_bottleneck_defers_bn_apply():
     x = torch.randn(4, 256, 28, 28, device=DEV).to(torch.bfloat16).contiguous(memory_format=CL)
     res = []
     for on in (False, True):
-        keep = hip.FUSE_XF, hip.XF_MAX_REP
-        hip.FUSE_XF, hip.XF_MAX_REP = on, 10 ** 6
+        keep = hip.FUSE_XF, hip.XF_MAX_REP, hip.SIBLINGS
+        # (the per-branch heads: merged sibling heads (SIBLINGS) write their outputs instead of deferring them)
+        hip.FUSE_XF, hip.XF_MAX_REP, hip.SIBLINGS = on, 10 ** 6, False
         try:
             b = copy.deepcopy(blk)
             xb = x.clone().requires_grad_(True)
@@ -1483,7 +1484,7 @@ def test_inception_defers_chain_bn_apply(block, expect):
             wg = [m.weight.grad.float() for m in b.modules() if isinstance(m, nn.Conv2d)]
             res.append((out.float(), xb.grad.float(), wg, hip.XF_COUNT[0] - n0))
         finally:
-            hip.FUSE_XF, hip.XF_MAX_REP = keep
+            hip.FUSE_XF, hip.XF_MAX_REP, hip.SIBLINGS = keep
     assert res[0][3] == 0 and res[1][3] == expect, (res[0][3], res[1][3])
     assert rel_err(res[1][0], res[0][0]) < 2e-2
     assert rel_err(res[1][1], res[0][1]) < 3e-2, rel_err(res[1][1], res[0][1])
