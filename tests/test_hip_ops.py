@@ -1451,7 +1451,7 @@ def test_resnet_bottleneck_defers_bn_apply():
             res.append((out.float(), xb.grad.float(), b.conv2.weight.grad.float(), b.conv3.weight.grad.float(),
                         hip.XF_COUNT[0] - n0))
         finally:
-            hip.FUSE_XF, hip.XF_MAX_REP = keep
+            hip.FUSE_XF, hip.XF_MAX_REP, hip.SIBLINGS = keep
     assert res[0][-1] == 0 and res[1][-1] == 2, (res[0][-1], res[1][-1])
     for a_, b_ in zip(res[1][:-1], res[0][:-1]):
         assert rel_err(a_, b_) < 2e-2, rel_err(a_, b_)
@@ -1472,8 +1472,8 @@ def test_inception_defers_chain_bn_apply(block, expect):
     x = torch.randn(4, mk[1], mk[2], mk[2], device=DEV).to(torch.bfloat16).contiguous(memory_format=CL)
     res = []
     for on in (False, True):
-        keep = hip.FUSE_XF, hip.XF_MAX_REP
-        hip.FUSE_XF, hip.XF_MAX_REP = on, 10 ** 6
+        keep = hip.FUSE_XF, hip.XF_MAX_REP, hip.SIBLINGS
+        hip.FUSE_XF, hip.XF_MAX_REP, hip.SIBLINGS = on, 10 ** 6, False
         try:
             b = copy.deepcopy(blk)
             xb = x.clone().requires_grad_(True)
