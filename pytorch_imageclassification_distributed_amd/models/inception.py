@@ -135,10 +135,17 @@ class InceptionD(nn.Module):
         self.branch7x7x3_4 = BasicConv2d(192, 192, kernel_size=3, stride=2)
 
     def forward(self, x):
-        s = Fx.grad_slot(x, 3)
         cat = Fx.concat_buffer([320, 192, x.shape[1]])
-        b3 = self.branch3x3_2(self.branch3x3_1(x, slot=s, defer=True), True, out=(cat, 0))
-        b7 = self.branch7x7x3_2(self.branch7x7x3_1(x, slot=s, defer=True), True, defer=True)
+        heads = [self.branch3x3_1, self.branch7x7x3_1]
+        if Fx.siblings_ok(x, _pairs(heads)):  # the two 1x1 heads as one GEMM (HIP path)
+            s = Fx.grad_slot(x, 2)
+            t3, t7 = Fx.conv_bn_act_siblings(x, _pairs(heads), [None, None], x_slot=s)
+        else:
+            s = Fx.grad_slot(x, 3)
+            t3 = self.branch3x3_1(x, slot=s, defer=True)
+            t7 = self.branch7x7x3_1(x, slot=s, defer=True)
+        b3 = self.branch3x3_2(t3, True, out=(cat, 0))
+        b7 = self.branch7x7x3_2(t7, True, defer=True)
         b7 = self.branch7x7x3_4(self.branch7x7x3_3(b7, True, defer=True), True, out=(cat, 1))
         bp = Fx.max_pool2d(x, 3, 2, 0, slot=s)
         return Fx.cat_channels([b3, b7, bp], cat)

@@ -1271,6 +1271,6 @@ _OWNED = (
     '_bn_bwd_k', '_bn_coef', '_dense_geom', '_rep', '_s2d_geom', '_s2d_index', '_syncbn_bwd_start', 'conv',
     'conv_bn_act', 'conv_bn_act_pool', 'dense_conv_eligible', 'input_from_u8', 'materialize_deferred',
     'pool_conv_bn_act', 'stem_s2d_conv', 'stem_s2d_eligible', 'xa_eligible', 'xf_eligible',
-    'SIBLINGS', 'SIBLINGS_COUNT', 'SIBLINGS_MAX', 'SiblingBNFn', 'SiblingConvFn', 'conv_bn_act_siblings',
+    'SIBLINGS', 'SIBLINGS_COUNT', 'SIBLINGS_MAX', 'SiblingBNFn', 'SiblingConvFn', '_sibling_geom', 'conv_bn_act_siblings',
     'siblings_eligible',
 )

@@ -523,7 +523,7 @@ def test_bn_fin_apply_matches_two_launch_path(kind):
             assert torch.allclose(a_.float(), b_.float(), rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("kind", ["A", "C", "E"])
+@pytest.mark.parametrize("kind", ["A", "C", "D", "E"])
 def test_inception_sibling_heads_merged(kind):
     """The 1x1 heads of an Inception block as one concatenated-output GEMM with per-slice BN (ops/_hip/convbn.py
     SiblingConvFn / SiblingBNFn) == the per-branch path: block output, input gradient, every parameter gradient,
@@ -532,7 +532,7 @@ def test_inception_sibling_heads_merged(kind):
     from pytorch_imageclassification_distributed_amd.ops import hip
     torch.manual_seed(0)
     blk, cin, hw = {"A": (inc.InceptionA(192, 32), 192, 11), "C": (inc.InceptionC(256, 64), 256, 9),
-                    "E": (inc.InceptionE(256), 256, 5)}[kind]
+                    "D": (inc.InceptionD(256), 256, 9), "E": (inc.InceptionE(256), 256, 5)}[kind]
     blk = blk.to(DEV).to(memory_format=torch.channels_last).train()
     with torch.no_grad():
         for m in blk.modules():
