@@ -2,19 +2,26 @@
 over the base file's entries with the same key; the base's other entries are kept.
 
     python scripts/merge_find_db.py tuning/mi355x_find_db.json new1.json [new2.json ...]  (rewrites the first)
+    python scripts/merge_find_db.py --missing-only BASE new1.json ...  (add only keys the base lacks)
 """
 import json
 import sys
 
 
 def main():
-    base_path, news = sys.argv[1], sys.argv[2:]
+    args = sys.argv[1:]
+    missing_only = args[0] == "--missing-only"
+    if missing_only:
+        args = args[1:]
+    base_path, news = args[0], args[1:]
     base = json.load(open(base_path))
     for kind in ("conv", "wgrad"):
         merged = {}
+        have = {k for k, _ in base.get(kind, [])}
         for path in news:
             for k, v in json.load(open(path)).get(kind, []):
-                merged.setdefault(k, v)
+                if not (missing_only and k in have):
+                    merged.setdefault(k, v)
         n_new = len(merged)
         kept = 0
         for k, v in base.get(kind, []):
