@@ -183,9 +183,23 @@ __global__ __launch_bounds__(256) void bn_fin_apply_kernel(BnFinApplyArgs a) {
   const int lc = threadIdx.x & 63, lg = threadIdx.x >> 6;
   const int C = a.C;
   const int c = blockIdx.y * 64 + lc;
+  // the lane's first BN_FIN_U rows of y are loaded before the partial-row reduce, which they do not depend on: a
+  // block's reduce (G rows from L2) otherwise sat in front of every load it streams (1.9 TB/s on the Inception b128
+  // sibling BNs, profiles/r17a_inception_b128_byte_roofline.txt)
+  const int v = threadIdx.x & 7, rl = threadIdx.x >> 3;
+  const int c0 = blockIdx.y * 64 + v * 8;
+  const long step = (long)gridDim.x * 32, row0 = (long)blockIdx.x * 32 + rl;
+  uint4 yv[BN_FIN_U];
+  if (c0 < C) {
+#pragma unroll
+    for (int u = 0; u < BN_FIN_U; ++u) {
+      const long r = row0 + u * step < a.rows ? row0 + u * step : 0;  // (past the end: a valid row, never stored)
+      yv[u] = *(const uint4*)(a.y + r * a.ldy + c0);
+    }
+  }
   double s = 0.0, q = 0.0;
   if (c < C) {
-#pragma unroll 4
+#pragma unroll 16
     for (int g = lg; g < a.G; g += 4) {
       const float* r = a.part + (size_t)g * 2 * a.ldp;
       s += (double)r[c];
@@ -242,8 +256,6 @@ __global__ __launch_bounds__(256) void bn_fin_apply_kernel(BnFinApplyArgs a) {
     if (threadIdx.x == 0) a.ctr[blockIdx.y] = 0u;
   }
   // apply: a lane owns 8 channels of the chunk, the block 32 rows per step
-  const int v = threadIdx.x & 7, rl = threadIdx.x >> 3;
-  const int c0 = blockIdx.y * 64 + v * 8;
   if (c0 >= C) return;
   float sc[8], sh[8];
 #pragma unroll
@@ -253,13 +265,13 @@ __global__ __launch_bounds__(256) void bn_fin_apply_kernel(BnFinApplyArgs a) {
   }
   // BN_U rows of loads in flight per lane before any is used (one dependent load per iteration capped the
   // larger tensors' bandwidth)
-  const long step = (long)gridDim.x * 32;
-  for (long row = (long)blockIdx.x * 32 + rl; row < a.rows; row += BN_FIN_U * step) {
-    uint4 yv[BN_FIN_U];
+  for (long row = row0; row < a.rows; row += BN_FIN_U * step) {
+    if (row != row0) {
 #pragma unroll
-    for (int u = 0; u < BN_FIN_U; ++u) {
-      const long r = row + u * step < a.rows ? row + u * step : row;
-      yv[u] = *(const uint4*)(a.y + r * a.ldy + c0);
+      for (int u = 0; u < BN_FIN_U; ++u) {
+        const long r = row + u * step < a.rows ? row + u * step : row;
+        yv[u] = *(const uint4*)(a.y + r * a.ldy + c0);
+      }
     }
 #pragma unroll
     for (int u = 0; u < BN_FIN_U; ++u) {
@@ -296,9 +308,23 @@ __global__ __launch_bounds__(256) void bn_fin_bwd_kernel(BnFinBwdArgs a) {
   const int lc = threadIdx.x & 63, lg = threadIdx.x >> 6;
   const int C = a.C;
   const int c = blockIdx.y * 64 + lc;
+  // the lane's first two rows of y / g (/ dz_in / res) are loaded before the partial-row reduce (as the apply)
+  const int v = threadIdx.x & 7, rl = threadIdx.x >> 3;
+  const int c0 = blockIdx.y * 64 + v * 8;
+  const long step = (long)gridDim.x * 32, row0 = (long)blockIdx.x * 32 + rl;
+  uint4 yl[2], gl[2], rl2[2];
+  if (c0 < C) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const long r = row0 + u * step < a.rows ? row0 + u * step : 0;  // (past the end: a valid row, never stored)
+      yl[u] = *(const uint4*)(a.y + r * a.ldy + c0);
+      gl[u] = MODE == 0 ? *(const uint4*)(a.dz_in + r * C + c0) : *(const uint4*)(a.g + r * a.ldg + c0);
+      if constexpr (MODE == 2) rl2[u] = *(const uint4*)(a.res + r * C + c0);
+    }
+  }
   double s = 0.0, q = 0.0;
   if (c < C) {
-#pragma unroll 4
+#pragma unroll 16
     for (int g = lg; g < a.G; g += 4) {
       const float* r = a.part + (size_t)g * 2 * C;
       s += (double)r[c];
@@ -336,8 +362,6 @@ __global__ __launch_bounds__(256) void bn_fin_bwd_kernel(BnFinBwdArgs a) {
     }
     if (threadIdx.x == 0) a.ctr[blockIdx.y] = 0u;
   }
-  const int v = threadIdx.x & 7, rl = threadIdx.x >> 3;
-  const int c0 = blockIdx.y * 64 + v * 8;
   if (c0 >= C) return;
   float sc[8], sh[8], mu[8], is[8], k1[8], k2[8];
 #pragma unroll
@@ -349,20 +373,20 @@ __global__ __launch_bounds__(256) void bn_fin_bwd_kernel(BnFinBwdArgs a) {
     k1[k] = k1s[v * 8 + k];
     k2[k] = k2s[v * 8 + k];
   }
-  const long step = (long)gridDim.x * 32;
-  for (long row0 = (long)blockIdx.x * 32 + rl; row0 < a.rows; row0 += 2 * step) {
-    // two rows of loads in flight per lane before either is used
-    uint4 yl[2], gl[2], rl2[2];
+  for (long rowb = row0; rowb < a.rows; rowb += 2 * step) {
+    // two rows of loads in flight per lane before either is used (the first two were issued before the reduce)
+    if (rowb != row0) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const long r = row0 + u * step < a.rows ? row0 + u * step : row0;
-      yl[u] = *(const uint4*)(a.y + r * a.ldy + c0);
-      gl[u] = MODE == 0 ? *(const uint4*)(a.dz_in + r * C + c0) : *(const uint4*)(a.g + r * a.ldg + c0);
-      if constexpr (MODE == 2) rl2[u] = *(const uint4*)(a.res + r * C + c0);
+      for (int u = 0; u < 2; ++u) {
+        const long r = rowb + u * step < a.rows ? rowb + u * step : rowb;
+        yl[u] = *(const uint4*)(a.y + r * a.ldy + c0);
+        gl[u] = MODE == 0 ? *(const uint4*)(a.dz_in + r * C + c0) : *(const uint4*)(a.g + r * a.ldg + c0);
+        if constexpr (MODE == 2) rl2[u] = *(const uint4*)(a.res + r * C + c0);
+      }
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-    const long row = row0 + u * step;
+    const long row = rowb + u * step;
     if (row >= a.rows) break;
     float gv[8], yv[8];
     unpack8(yl[u], yv);
