@@ -71,6 +71,20 @@ def main():
     for (site, stream), n in sites.most_common(30):
         sz = sizes[(site, stream)]
         print(f"{n:4d} x  {min(sz) / 2**20:9.2f}..{max(sz) / 2**20:9.2f} MiB  stream {stream}  {site}")
+    from pytorch_imageclassification_distributed_amd.ops._hip.streams import side_stream
+    names = {torch.cuda.current_stream().cuda_stream: "caller", side_stream(ctx.device).handle: "wgrad side"}
+    if tr.step_stream is not None:
+        names[tr.step_stream.cuda_stream] = "step"
+    pools = collections.defaultdict(lambda: [0, 0, 0, 0])
+    for seg in snap["segments"]:
+        p = pools[seg["stream"]]
+        p[0] += 1
+        p[1] += seg["total_size"]
+        p[2] += seg["allocated_size"]
+        p[3] = max(p[3], max((b["size"] for b in seg["blocks"] if b["state"] == "inactive"), default=0))
+    for stream, (n, tot, used, big) in sorted(pools.items()):
+        print(f"pool stream {stream} ({names.get(stream, '?')}): {n} segments, {tot / 2**30:.2f} GiB mapped, "
+              f"{used / 2**30:.2f} GiB in use at the end, largest free block {big / 2**20:.0f} MiB")
 
 
 if __name__ == "__main__":
